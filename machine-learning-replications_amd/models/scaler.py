@@ -1,0 +1,49 @@
+"""StandardScaler (reference ``train_ensemble_public.py:44``; semantics sklearn
+``preprocessing/_data.py``: population variance, ``scale_ = sqrt(var_)`` with
+zero variance mapped to 1)."""
+from __future__ import annotations
+
+import torch
+
+from .base import Estimator, as_tensor
+
+
+class StandardScaler(Estimator):
+    _param_names = ("with_mean", "with_std", "copy")
+
+    def __init__(self, with_mean=True, with_std=True, copy=True):
+        self.with_mean = with_mean
+        self.with_std = with_std
+        self.copy = copy
+
+    def fit(self, X, sample_mask=None):
+        """Column moments in fp64 (K2 ``col_moments``); ``sample_mask`` selects rows."""
+        X = as_tensor(X)
+        if sample_mask is not None:
+            X = X[sample_mask]
+        n = X.shape[0]
+        mean = X.mean(0)
+        var = ((X - mean) ** 2).mean(0)
+        self._set(mean, var, n)
+        return self
+
+    def _set(self, mean, var, n):
+        self.n_features_in_ = int(mean.numel())
+        self.n_samples_seen_ = int(n)
+        self.mean_ = mean.to(torch.float64)
+        self.var_ = var.to(torch.float64)
+        scale = torch.sqrt(self.var_)
+        self.scale_ = torch.where(scale < 10 * torch.finfo(torch.float64).eps,
+                                  torch.ones_like(scale), scale)
+        return self
+
+    def transform(self, X):
+        X = as_tensor(X, device=self.mean_.device)
+        if self.with_mean:
+            X = X - self.mean_
+        if self.with_std:
+            X = X / self.scale_
+        return X
+
+    def fit_transform(self, X):
+        return self.fit(X).transform(X)

@@ -1,0 +1,60 @@
+"""Op entry points: validate, then route ``cuda`` tensors to the HIP extension and
+host tensors to :mod:`hfens.ops.reference`."""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from .packing import pack_forest, pack_svs
+
+__all__ = ["rbf_decision", "svc_proba1", "tree_raw", "expit", "pack_svs", "pack_forest"]
+
+
+def _c(t: torch.Tensor, dtype) -> torch.Tensor:
+    return t.to(dtype).contiguous()
+
+
+def rbf_decision(z, sv, coef, gamma: float, intercept: float, packed=None):
+    """libsvm RBF decision values; ``packed`` = cached :class:`PackedSV` for ``sv``/``coef``."""
+    if z.is_cuda:
+        from . import ext, stream_ptr
+        pk = packed if packed is not None else pack_svs(sv, coef, z.device)
+        z32 = _c(z, torch.float32)
+        n, F = z32.shape
+        if F != pk.F:
+            raise ValueError(f"rbf_decision: X has {F} features, model has {pk.F}")
+        out = torch.empty(n, dtype=torch.float32, device=z.device)
+        ext().rbf_decision(z32.data_ptr(), n, F, pk.svt.data_ptr(), pk.sn.data_ptr(), pk.coef.data_ptr(),
+                           pk.mp, float(gamma), float(intercept), out.data_ptr(), stream_ptr(z.device))
+        return out
+    return ref.rbf_decision(z, sv, coef, gamma, intercept)
+
+
+def svc_proba1(dec, A: float, B: float):
+    if dec.is_cuda:
+        from . import ext, stream_ptr
+        d32 = _c(dec, torch.float32)
+        out = torch.empty_like(d32)
+        ext().svc_proba1(d32.data_ptr(), out.data_ptr(), d32.numel(), float(A), float(B),
+                         stream_ptr(dec.device))
+        return out
+    return ref.svc_proba1(dec, A, B)
+
+
+def tree_raw(x, feature, threshold, left, right, value, init: float, lr: float, packed=None):
+    if x.is_cuda:
+        from . import ext, stream_ptr
+        pk = packed if packed is not None else pack_forest(feature, threshold, left, right, value, x.device)
+        x32 = _c(x, torch.float32)
+        n, F = x32.shape
+        if pk.max_feature >= F:
+            raise ValueError("tree_raw: a split feature index exceeds the input width")
+        out = torch.empty(n, dtype=torch.float32, device=x.device)
+        ext().forest_raw(x32.data_ptr(), n, F, pk.nodes.data_ptr(), pk.values.data_ptr(), pk.n_trees,
+                         pk.max_nodes, float(init), float(lr), out.data_ptr(), stream_ptr(x.device))
+        return out
+    return ref.tree_raw(x, feature, threshold, left, right, value, init, lr)
+
+
+def expit(x):
+    return torch.sigmoid(x)

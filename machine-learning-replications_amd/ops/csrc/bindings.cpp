@@ -1,0 +1,30 @@
+// pybind11 module _hfens_hip: thin host entry points for the gfx950 kernels.
+// Tensors cross the boundary as device pointers (torch.Tensor.data_ptr()) and the
+// current HIP stream; the Python wrappers in hfens/ops validate shapes/dtypes.
+#include <pybind11/pybind11.h>
+#include <cstdint>
+
+namespace hfens {
+// infer.hip
+void rbf_decision(uintptr_t Z, int n, int F, uintptr_t SVt, uintptr_t sn, uintptr_t coef, int mp,
+                  double gamma, double b, uintptr_t out, uintptr_t stream);
+void svc_proba1(uintptr_t dec, uintptr_t out, int n, double A, double B, uintptr_t stream);
+void forest_raw(uintptr_t X, int n, int F, uintptr_t nodes, uintptr_t values, int T, int K,
+                double init, double lr, uintptr_t out, uintptr_t stream);
+#define HFENS_DECLS
+#include "decls.inc"
+#undef HFENS_DECLS
+}  // namespace hfens
+
+namespace py = pybind11;
+
+PYBIND11_MODULE(_hfens_hip, m) {
+  m.doc() = "hfens gfx950 HIP kernels (MI355X / CDNA4)";
+  m.def("rbf_decision", &hfens::rbf_decision);
+  m.def("svc_proba1", &hfens::svc_proba1);
+  m.def("forest_raw", &hfens::forest_raw);
+#define HFENS_DEFS
+#include "decls.inc"
+#undef HFENS_DEFS
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,83 @@
+// Shared helpers for the hfens gfx950 (CDNA4) kernels.
+// Wave = 64 lanes everywhere; no CUDA shims, no dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace hfens {
+
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define HFENS_CHECK(expr)                                                                  \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                 \
+  } while (0)
+
+#define HFENS_REQUIRE(cond, msg)                                   \
+  do {                                                            \
+    if (!(cond)) throw std::invalid_argument(std::string(msg));   \
+  } while (0)
+
+inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline void launch_check() { HFENS_CHECK(hipGetLastError()); }
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// ---- wave reductions (64 lanes) ---------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// max of (value, index) with lowest-index tie-break
+__device__ __forceinline__ void wave_argmax(double& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o, kWave);
+    int oi = __shfl_xor(i, o, kWave);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+__device__ __forceinline__ void wave_argmin(double& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o, kWave);
+    int oi = __shfl_xor(i, o, kWave);
+    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+
+__device__ __forceinline__ float fast_exp(float x) {  // e^x via v_exp_f32 (2^x)
+  return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+}
+
+// XCD-aware bijective block remap (8 XCDs; blocks b and b+8 share an XCD under
+// round-robin dispatch).  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int nx = 8;
+  if (nblk < nx) return bid;
+  int q = nblk / nx, r = nblk % nx, x = bid % nx;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / nx;
+}
+
+}  // namespace hfens

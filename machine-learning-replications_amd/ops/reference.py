@@ -1,0 +1,111 @@
+"""Plain-PyTorch reference implementations of every device op.
+
+These define the semantics the gfx950 HIP kernels must reproduce and run the
+host (CPU) path.  They follow the algorithms the reference delegates to
+(libsvm / sklearn trees / liblinear), re-derived from the published math; see
+the per-function notes and SURVEY.md §2.2 (E2-E12).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+LOG2E = 1.4426950408889634
+
+
+# ----------------------------------------------------------------------------- SVC inference
+def rbf_decision(z: torch.Tensor, sv: torch.Tensor, coef: torch.Tensor, gamma: float,
+                 intercept: float, chunk: int = 65536) -> torch.Tensor:
+    """``dec_i = Σ_j coef_j · exp(-γ‖z_i − sv_j‖²) + intercept`` (libsvm ``svm_predict_values``,
+    RBF kernel ``k(x,y)=exp(-γ‖x−y‖²)``)."""
+    out = torch.empty(z.shape[0], dtype=z.dtype, device=z.device)
+    for s in range(0, z.shape[0], chunk):
+        zz = z[s:s + chunk]
+        d2 = ((zz[:, None, :] - sv[None, :, :]) ** 2).sum(-1)
+        out[s:s + chunk] = torch.exp(-gamma * d2) @ coef + intercept
+    return out
+
+
+def sigmoid_predict(dec: torch.Tensor, A: float, B: float) -> torch.Tensor:
+    """Platt ``1/(1+exp(A·f+B))`` evaluated in libsvm's overflow-safe form."""
+    fApB = dec * A + B
+    pos = torch.exp(-fApB.clamp(min=0)) / (1.0 + torch.exp(-fApB.clamp(min=0)))
+    neg = 1.0 / (1.0 + torch.exp(fApB.clamp(max=0)))
+    return torch.where(fApB >= 0, pos, neg)
+
+
+def couple2(r01: torch.Tensor, max_iter: int = 100) -> torch.Tensor:
+    """Two-class pairwise coupling (Wu, Lin & Weng 2004, method 2 — the iterative
+    solver libsvm's ``multiclass_probability`` runs even for k = 2), vectorised over
+    rows.  Input r01 = P(class 0 | {0,1}); returns p1 = P(class 1).  Stopping rule
+    ``max_t |(Qp)_t − pᵀQp| < 0.005/k``."""
+    r10 = 1.0 - r01
+    q00 = r10 * r10
+    q11 = r01 * r01
+    q01 = -r10 * r01
+    p0 = torch.full_like(r01, 0.5)
+    p1 = torch.full_like(r01, 0.5)
+    eps = 0.005 / 2
+    active = torch.ones_like(r01, dtype=torch.bool)
+    for _ in range(max_iter):
+        qp0 = q00 * p0 + q01 * p1
+        qp1 = q01 * p0 + q11 * p1
+        pqp = p0 * qp0 + p1 * qp1
+        err = torch.maximum((qp0 - pqp).abs(), (qp1 - pqp).abs())
+        active = active & ~(err < eps)
+        if not bool(active.any()):
+            break
+        # t = 0 update
+        d = (-qp0 + pqp) / q00
+        np0 = p0 + d
+        npqp = (pqp + d * (d * q00 + 2 * qp0)) / (1 + d) / (1 + d)
+        nqp0 = (qp0 + d * q00) / (1 + d)
+        nqp1 = (qp1 + d * q01) / (1 + d)
+        np0 = np0 / (1 + d)
+        np1 = p1 / (1 + d)
+        # t = 1 update
+        d = (-nqp1 + npqp) / q11
+        np1 = np1 + d
+        np0 = np0 / (1 + d)
+        np1 = np1 / (1 + d)
+        p0 = torch.where(active, np0, p0)
+        p1 = torch.where(active, np1, p1)
+    return p1
+
+
+def svc_proba1(dec: torch.Tensor, A: float, B: float) -> torch.Tensor:
+    """libsvm ``svm_predict_probability`` for two classes → P(class 1)."""
+    r01 = sigmoid_predict(dec, A, B).clamp(1e-7, 1 - 1e-7)
+    return couple2(r01)
+
+
+# ----------------------------------------------------------------------------- tree inference
+def tree_raw(x: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor, left: torch.Tensor,
+             right: torch.Tensor, value: torch.Tensor, init: float, lr: float) -> torch.Tensor:
+    """Sum of tree outputs ``init + lr·Σ_t value_t[leaf_t(x)]``.  Decision rule
+    ``float32(x[f]) <= threshold`` → left (sklearn compares the float32-cast input
+    against the float64 threshold).  Arrays are [T, K] node tables, leaves have
+    feature < 0."""
+    x32 = x.to(torch.float32).to(torch.float64)
+    n = x.shape[0]
+    T = feature.shape[0]
+    raw = torch.full((n,), float(init), dtype=torch.float64, device=x.device)
+    rows = torch.arange(n, device=x.device)
+    for t in range(T):
+        node = torch.zeros(n, dtype=torch.long, device=x.device)
+        while True:
+            f = feature[t, node]
+            leaf = f < 0
+            if bool(leaf.all()):
+                break
+            fv = x32[rows, f.clamp(min=0).long()]
+            go_left = fv <= threshold[t, node]
+            nxt = torch.where(go_left, left[t, node], right[t, node]).long()
+            node = torch.where(leaf, node, nxt)
+        raw += lr * value[t, node].to(torch.float64)
+    return raw
+
+
+def expit(x: torch.Tensor) -> torch.Tensor:
+    return torch.sigmoid(x)
