@@ -1,0 +1,381 @@
+"""Batched histogram GBDT training (binomial deviance) on device.
+
+B models — e.g. the 5 stacking OOF folds + the full refit, or several seeds —
+share one binned matrix and train in lock-step: every boosting stage is one
+``apply_prep`` launch, then per tree level one ``hist`` + one ``split`` (+ one
+``route`` above the last level) launch, each covering all B models.  Kernels:
+``ops/csrc/gbdt.hip``.  The same algorithm runs on host tensors through a
+plain-PyTorch mirror (``_HostKernels``) so CPU runs and kernel tests share
+semantics.
+
+Exactness notes (vs sklearn ``GradientBoostingClassifier``):
+* per-stage residual r = y − σ(raw), Newton leaf value Σr / Σp(1−p), raw += lr·value,
+  init raw = log-odds of the (weighted) class prior; node values/impurities and
+  ``train_score_`` (binomial deviance after each stage) as sklearn stores them.
+* histogram sums are fixed-point int64 (scale 2^shift): exact, deterministic and
+  identical for any data-parallel split of the rows.
+* split candidates/thresholds = sklearn's exact splitter when a feature has ≤256
+  distinct values; ties between features resolve to the lowest feature index
+  (sklearn: first in a random feature permutation).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .binning import BinMapper, fit_bins
+
+F32_EPS = float(np.finfo(np.float32).eps)
+
+
+def _qshift(n_total: int) -> int:
+    return 40 if n_total <= (1 << 22) else 32
+
+
+# ============================================================================ host mirror
+class _HostKernels:
+    """Plain-PyTorch mirror of gbdt.hip (same fixed-point semantics)."""
+
+    @staticmethod
+    def apply_prep(st, prev, t):
+        raw, w, y = st.raw, st.w, st.y
+        if prev is not None:
+            feat, blo, value = prev
+            nd = st.node
+            f = feat.gather(1, nd)
+            split = f >= 0
+            fb = st.bins[f.clamp(min=0).long(), torch.arange(st.n, device=raw.device)[None, :].expand_as(f)]
+            side = torch.where(fb.to(torch.int64) <= blo.gather(1, nd).to(torch.int64), 1, 2)
+            nd = torch.where(split, 2 * nd + side, nd)
+            p0 = torch.sigmoid(raw)
+            r0 = y[None] - p0
+            q = torch.round(w * r0 * r0 * st.qscale).to(torch.int64) * (w > 0)
+            st.r2[t - 1].scatter_add_(1, nd, q)
+            raw = raw + st.lr * value.gather(1, nd)
+            st.raw = raw
+            l1p = torch.where(raw > 0, raw + torch.log1p(torch.exp(-raw)), torch.log1p(torch.exp(raw)))
+            dq = torch.round(w * (-2.0) * (y[None] * raw - l1p) * st.dscale).to(torch.int64) * (w > 0)
+            st.dev[t - 1] += dq.sum(1)
+        p = torch.sigmoid(st.raw)
+        r = y[None] - p
+        st.g = (w * r).to(torch.float32)
+        st.h = (w * p * (1 - p)).to(torch.float32)
+        st.node = torch.zeros_like(st.node)
+        if t < st.T:
+            q = torch.round(w * r * r * st.qscale).to(torch.int64) * (w > 0)
+            st.r2[t][:, 0] += q.sum(1)
+
+    @staticmethod
+    def hist(st, node0, NL):
+        B, n, F = st.B, st.n, st.F
+        H = torch.zeros(B, NL, F, 256, 3, dtype=torch.int64, device=st.raw.device)
+        qs = st.qscale
+        qg = torch.round(st.g.double() * qs).to(torch.int64)
+        qh = torch.round(st.h.double() * qs).to(torch.int64)
+        qw = torch.round(st.w.double() * qs).to(torch.int64)
+        for b in range(B):
+            nd = st.node[b] - node0
+            ok = (nd >= 0) & (nd < NL) & (st.w[b] > 0)
+            rows = ok.nonzero().squeeze(1)
+            if rows.numel() == 0:
+                continue
+            base = nd[rows][:, None] * (F * 256) + torch.arange(F, device=rows.device)[None, :] * 256
+            idx = (base + st.bins[:, rows].t().to(torch.int64)).reshape(-1)
+            flat = H[b].view(-1, 3)
+            for s, q in enumerate((qg, qh, qw)):
+                flat[:, s].index_add_(0, idx, q[b, rows][:, None].expand(-1, F).reshape(-1))
+        return H
+
+    @staticmethod
+    def split(st, H, node0, NL, last, t):
+        inv = 1.0 / st.qscale
+        feat, blo, thr, value, stats = st.feat[t], st.blo[t], st.thr[t], st.value[t], st.stats[t]
+        r2 = st.r2[t]
+        nbins = st.bm.nbins.cpu()
+        lo_val, hi_val = st.bm.lo_val.cpu(), st.bm.hi_val.cpu()
+        Hc = H.cpu()
+        for b in range(st.B):
+            for j in range(NL):
+                hn = node0 + j
+                hb = Hc[b, j]
+                nb0 = int(nbins[0])
+                tg, th, tw = [int(hb[0, :nb0, s].sum()) for s in range(3)]
+                if tw <= 0:
+                    feat[b, hn] = -3
+                    continue
+                best = (-1.0, 1 << 30, 0)
+                if tw >= st.min_split_q:
+                    for f in range(st.F):
+                        nb = int(nbins[f])
+                        cw = torch.cumsum(hb[f, :nb, 2], 0)[:-1]
+                        cg = torch.cumsum(hb[f, :nb, 0], 0)[:-1]
+                        rw, rg = tw - cw, tg - cg
+                        ok = (cw.double() >= st.min_leaf_q) & (rw.double() >= st.min_leaf_q)
+                        if not bool(ok.any()):
+                            continue
+                        dlw, drw = cw.double(), rw.double()
+                        diff = drw * cg.double() - dlw * rg.double()
+                        gain = torch.where(ok, diff / dlw * diff / drw, torch.full_like(dlw, -1.0))
+                        k = int(torch.argmax(gain))
+                        gv = float(gain[k])
+                        if gv > best[0]:
+                            best = (gv, f, k)
+                stats[b, hn, 0], stats[b, hn, 1], stats[b, hn, 2] = tw, tg, th
+                dw, dg = tw * inv, tg * inv
+                imp = int(r2[b, hn]) * inv / dw - (dg / dw) ** 2
+                bg, bf, bbin = best
+                if not (bg >= 0 and bf < st.F and imp > 2.220446049250313e-16):
+                    feat[b, hn] = -2
+                    blo[b, hn] = 0
+                    thr[b, hn] = -2.0
+                    den = th * inv
+                    value[b, hn] = 0.0 if abs(den) < 1e-150 else dg / den
+                    continue
+                hf = hb[bf]
+                lg, lh, lw = [int(hf[:bbin + 1, s].sum()) for s in range(3)]
+                hi = bbin + 1
+                nbf = int(nbins[bf])
+                while hi < nbf - 1 and int(hf[hi, 2]) == 0:
+                    hi += 1
+                a, c = float(hi_val[bf, bbin]), float(lo_val[bf, hi])
+                tt = a / 2.0 + c / 2.0
+                if tt == c or math.isinf(tt):
+                    tt = a
+                feat[b, hn], blo[b, hn], thr[b, hn], value[b, hn] = bf, bbin, tt, dg / dw
+                L, R = 2 * hn + 1, 2 * hn + 2
+                stats[b, L, 0], stats[b, L, 1], stats[b, L, 2] = lw, lg, lh
+                stats[b, R, 0], stats[b, R, 1], stats[b, R, 2] = tw - lw, tg - lg, th - lh
+                if last:
+                    feat[b, L] = feat[b, R] = -2
+                    blo[b, L] = blo[b, R] = 0
+                    thr[b, L] = thr[b, R] = -2.0
+                    dl, dr = lh * inv, (th - lh) * inv
+                    value[b, L] = 0.0 if abs(dl) < 1e-150 else lg * inv / dl
+                    value[b, R] = 0.0 if abs(dr) < 1e-150 else (tg - lg) * inv / dr
+
+    @staticmethod
+    def route(st, node0, NL, t):
+        nd = st.node
+        f = st.feat[t].gather(1, nd)
+        inl = (nd >= node0) & (nd < node0 + NL) & (f >= 0)
+        fb = st.bins[f.clamp(min=0).long(), torch.arange(st.n, device=nd.device)[None, :].expand_as(f)]
+        child = 2 * nd + torch.where(fb.to(torch.int64) <= st.blo[t].gather(1, nd).to(torch.int64), 1, 2)
+        new = torch.where(inl, child, nd)
+        r = torch.where(st.w > 0, st.g.double() / st.w.clamp(min=1e-30), torch.zeros_like(st.raw))
+        q = torch.round(st.w * r * r * st.qscale).to(torch.int64) * ((st.w > 0) & inl)
+        st.r2[t].scatter_add_(1, new, q)
+        st.node = new
+
+
+# ============================================================================ state
+@dataclass
+class _State:
+    B: int
+    n: int
+    F: int
+    T: int
+    D: int
+    NN: int
+    lr: float
+    qscale: float
+    dscale: float
+    min_leaf_q: float
+    min_split_q: float
+    bm: BinMapper
+    bins: torch.Tensor
+    y: torch.Tensor
+    w: torch.Tensor
+    raw: torch.Tensor
+    g: torch.Tensor
+    h: torch.Tensor
+    node: torch.Tensor
+    feat: torch.Tensor
+    blo: torch.Tensor
+    thr: torch.Tensor
+    value: torch.Tensor
+    stats: torch.Tensor
+    r2: torch.Tensor
+    dev: torch.Tensor
+
+
+def _check_same(models, attrs):
+    for a in attrs:
+        vals = {repr(getattr(m, a)) for m in models}
+        if len(vals) != 1:
+            raise ValueError(f"batched GBDT fit needs identical '{a}' across models: {vals}")
+
+
+def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
+                   group=None, binned: Optional[tuple] = None):
+    """Fit ``len(models)`` GBDTs on row subsets ``masks[b]`` (bool [B, n]) of one matrix.
+
+    ``group``: torch.distributed process group when rows are sharded across ranks
+    (histograms / node sums / deviance are all-reduced; results are bit-identical
+    to the single-device fit).  ``binned``: optional precomputed ``(BinMapper, bins)``.
+    """
+    m0 = models[0]
+    _check_same(models, ("n_estimators", "learning_rate", "max_depth", "min_samples_leaf",
+                         "min_samples_split", "subsample", "max_bins", "loss", "criterion"))
+    if m0.loss not in ("deviance", "log_loss") or m0.criterion != "friedman_mse":
+        raise NotImplementedError("binomial deviance with friedman_mse only")
+    if m0.subsample != 1.0 or m0.max_features not in (None, "auto"):
+        raise NotImplementedError("subsample<1 / max_features are not supported by the batched fit")
+    dev = X.device
+    n, F = X.shape
+    B = len(models)
+    T, D = int(m0.n_estimators), int(m0.max_depth)
+    if not 1 <= D <= 5:
+        raise ValueError("max_depth must be in [1, 5]")
+    NN = 2 ** (D + 1) - 1
+    if masks is None:
+        masks = torch.ones(B, n, dtype=torch.bool, device=dev)
+    w = masks.to(device=dev, dtype=torch.float32).contiguous()
+    yv = y.to(device=dev, dtype=torch.float32).contiguous()
+    if binned is None:
+        bm = fit_bins(X, int(m0.max_bins), group)
+        bins = bm.transform(X).contiguous()
+    else:
+        bm, bins = binned
+    n_total = n
+    if group is not None:
+        from ..parallel import dist as pdist
+        n_total = pdist.all_reduce_int(n, group)
+    shift = _qshift(n_total)
+    qscale = float(2 ** shift)
+    dscale = float(2 ** 26)
+    # init = log-odds of the weighted class prior (DummyClassifier 'prior')
+    sw = w.double().sum(1)
+    sy = (w.double() * yv.double()[None]).sum(1)
+    if group is not None:
+        sw, sy = pdist.all_reduce_sum_f64([sw, sy], group)
+    p1 = (sy / sw).clamp(F32_EPS, 1 - F32_EPS)
+    raw0 = torch.log(p1 / (1 - p1))
+    st = _State(
+        B=B, n=n, F=F, T=T, D=D, NN=NN, lr=float(m0.learning_rate), qscale=qscale, dscale=dscale,
+        min_leaf_q=float(m0.min_samples_leaf) * qscale, min_split_q=float(m0.min_samples_split) * qscale,
+        bm=bm, bins=bins, y=yv, w=w, raw=raw0[:, None].expand(B, n).contiguous(),
+        g=torch.empty(B, n, dtype=torch.float32, device=dev), h=torch.empty(B, n, dtype=torch.float32, device=dev),
+        node=torch.zeros(B, n, dtype=torch.int64 if not X.is_cuda else torch.int32, device=dev),
+        feat=torch.full((T, B, NN), -3, dtype=torch.int32, device=dev),
+        blo=torch.zeros(T, B, NN, dtype=torch.int32, device=dev),
+        thr=torch.full((T, B, NN), -2.0, dtype=torch.float64, device=dev),
+        value=torch.zeros(T, B, NN, dtype=torch.float64, device=dev),
+        stats=torch.zeros(T, B, NN, 4, dtype=torch.int64, device=dev),
+        r2=torch.zeros(T, B, NN, dtype=torch.int64, device=dev),
+        dev=torch.zeros(T, B, dtype=torch.int64, device=dev))
+    if X.is_cuda:
+        _run_device(st, group)
+    else:
+        _run_host(st, group)
+    _finish(models, st, sw, p1, group)
+    return models
+
+
+def _run_host(st: _State, group):
+    K = _HostKernels
+    st.node = st.node.to(torch.int64)
+    for t in range(st.T + 1):
+        prev = None
+        if t > 0:
+            prev = (st.feat[t - 1].to(torch.int64), st.blo[t - 1].to(torch.int64), st.value[t - 1])
+        K.apply_prep(st, prev, t)
+        if t == st.T:
+            break
+        if group is not None:
+            _allreduce_r2(st, t, group)
+        for level in range(st.D):
+            node0, NL = 2 ** level - 1, 2 ** level
+            H = K.hist(st, node0, NL)
+            if group is not None:
+                from ..parallel import dist as pdist
+                pdist.all_reduce_sum_(H, group)
+            K.split(st, H, node0, NL, level == st.D - 1, t)
+            if level < st.D - 1:
+                K.route(st, node0, NL, t)
+                if group is not None:
+                    _allreduce_r2(st, t, group)
+
+
+def _allreduce_r2(st, t, group):
+    from ..parallel import dist as pdist
+    pdist.all_reduce_sum_(st.r2[t], group)
+
+
+def _run_device(st: _State, group):
+    from .. import ops
+    from ..ops import stream_ptr
+    E = ops.ext()
+    s = stream_ptr(st.raw.device)
+    max_nb = st.bm.max_nb
+    nb_ptr = st.bm.nbins.data_ptr()
+    H = torch.empty(st.B * (2 ** (st.D - 1)) * st.F * 256 * 3, dtype=torch.int64, device=st.raw.device)
+    scratch = torch.zeros(st.B, st.NN, dtype=torch.int64, device=st.raw.device)
+    for t in range(st.T + 1):
+        if t > 0:
+            pf, pb, pv = st.feat[t - 1], st.blo[t - 1], st.value[t - 1]
+            prev = (pf.data_ptr(), pb.data_ptr(), pv.data_ptr(), st.r2[t - 1].data_ptr(),
+                    st.dev[t - 1].data_ptr())
+        else:
+            prev = (0, 0, 0, 0, 0)
+        cur_r2 = st.r2[t] if t < st.T else scratch
+        E.gbdt_apply_prep(st.B, st.n, st.F, st.NN, st.bins.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
+                          st.raw.data_ptr(), st.g.data_ptr(), st.h.data_ptr(), st.node.data_ptr(),
+                          prev[0], prev[1], prev[2], prev[3], prev[4], cur_r2.data_ptr(), st.lr,
+                          st.qscale, st.dscale, s)
+        if t == st.T:
+            break
+        if group is not None:
+            _allreduce_r2(st, t, group)
+        for level in range(st.D):
+            node0, NL = 2 ** level - 1, 2 ** level
+            Hl = H[: st.B * NL * st.F * 768]
+            Hl.zero_()
+            E.gbdt_hist(st.B, st.n, st.F, st.bins.data_ptr(), nb_ptr, max_nb, st.g.data_ptr(),
+                        st.h.data_ptr(), st.w.data_ptr(), st.node.data_ptr(), node0, NL, Hl.data_ptr(),
+                        st.qscale, s)
+            if group is not None:
+                from ..parallel import dist as pdist
+                pdist.all_reduce_sum_(Hl, group)
+            E.gbdt_split(st.B, st.F, st.NN, Hl.data_ptr(), nb_ptr, st.bm.lo_val.data_ptr(),
+                         st.bm.hi_val.data_ptr(), node0, NL, int(level == st.D - 1), st.min_leaf_q,
+                         st.min_split_q, st.qscale, st.feat[t].data_ptr(), st.blo[t].data_ptr(),
+                         st.thr[t].data_ptr(), st.value[t].data_ptr(), st.stats[t].data_ptr(),
+                         st.r2[t].data_ptr(), s)
+            if level < st.D - 1:
+                E.gbdt_route(st.B, st.n, st.NN, st.bins.data_ptr(), st.g.data_ptr(), st.w.data_ptr(),
+                             st.node.data_ptr(), st.feat[t].data_ptr(), st.blo[t].data_ptr(),
+                             st.r2[t].data_ptr(), node0, NL, st.qscale, s)
+                if group is not None:
+                    _allreduce_r2(st, t, group)
+
+
+def _finish(models, st: _State, sw, p1, group):
+    if group is not None:
+        from ..parallel import dist as pdist
+        pdist.all_reduce_sum_(st.dev, group)
+    inv = 1.0 / st.qscale
+    stats = st.stats.double() * inv            # [T,B,NN,4]
+    r2 = st.r2.double() * inv
+    wsum = stats[..., 0]
+    mean = stats[..., 1] / wsum.clamp(min=1e-300)
+    imp = (r2 / wsum.clamp(min=1e-300) - mean * mean).clamp(min=0.0)
+    imp = torch.where(wsum > 0, imp, torch.zeros_like(imp))
+    train_score = (st.dev.double() / st.dscale) / sw[None, :]
+    heap_l = torch.arange(st.NN, device=st.feat.device) * 2 + 1
+    for b, m in enumerate(models):
+        feat = st.feat[:, b]
+        leaf = feat < 0
+        left = torch.where(leaf, torch.full_like(heap_l, -1), heap_l[None].expand(st.T, -1))
+        right = torch.where(leaf, torch.full_like(heap_l, -1), heap_l[None].expand(st.T, -1) + 1)
+        m.set_fitted(feature=torch.where(feat == -3, torch.full_like(feat, -2), feat),
+                     threshold=st.thr[:, b], left=left, right=right, value=st.value[:, b],
+                     impurity=imp[:, b], n_node_samples=torch.round(wsum[:, b]).to(torch.int64),
+                     weighted_n_node_samples=wsum[:, b], node_count=torch.full((st.T,), st.NN),
+                     class_prior=torch.stack([1 - p1[b], p1[b]]).double(), train_score=train_score[:, b],
+                     n_features=st.F, rng_state=None, device=st.feat.device)
+        m.tree_layout_ = "heap"
+        m._bin_mapper = st.bm

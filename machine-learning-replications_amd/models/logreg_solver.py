@@ -1,0 +1,186 @@
+"""Batched logistic-regression solvers.
+
+All B fits (CV folds / refit) advance together; each outer iteration is a few
+device GEMM/reduction ops over the rows plus one tiny subproblem launch:
+
+* L1 (liblinear ``solve_l1r_lr`` objective, intercept as an L1-penalised augmented
+  feature with ``intercept_scaling``): proximal Newton.  Quadratic model
+  (g, H = C·X̃ᵀDX̃) → L1-QP solved by the ``l1_qp_cd`` kernel (one wave per model, H in
+  LDS) → Armijo line search on 8 step sizes evaluated in one pass.
+* L2 (the lbfgs meta-learner's objective ½‖w‖² + C·Σ s·logloss, intercept not
+  penalised): damped Newton with a batched dense solve.
+
+Both converge to the unique optimum well below liblinear's / lbfgs's tolerance,
+so coefficients agree with sklearn to its own stopping accuracy.
+With ``group`` (rows sharded over ranks) the per-iteration g, H and line-search
+losses are all-reduced (F² + F + 8 doubles per model).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .base import balanced_class_weight
+
+
+def _check_same(models, attrs):
+    for a in attrs:
+        if len({repr(getattr(m, a)) for m in models}) != 1:
+            raise ValueError(f"batched logistic fit needs identical '{a}' across models")
+
+
+def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-13):
+    Hn, gn, wn = H.cpu().numpy(), g.cpu().numpy(), w.cpu().numpy()
+    pn = penal.cpu().numpy().astype(bool)
+    B, F1 = gn.shape
+    out = np.zeros_like(gn)
+    for b in range(B):
+        Hb, gb, wb = Hn[b], gn[b], wn[b]
+        d = np.zeros(F1)
+        Hd = np.zeros(F1)
+        for _ in range(max_sweeps):
+            mx = 0.0
+            for k in range(F1):
+                a = max(Hb[k, k], 1e-300)
+                lin = gb[k] + Hd[k] - a * d[k]
+                z0 = wb[k] - lin / a
+                lk = lam if pn[k] else 0.0
+                z = z0
+                if lk > 0:
+                    z = z0 - lk / a if z0 > lk / a else (z0 + lk / a if z0 < -lk / a else 0.0)
+                nd = z - wb[k]
+                step = nd - d[k]
+                if step != 0.0:
+                    Hd += Hb[:, k] * step
+                    d[k] = nd
+                    mx = max(mx, abs(step))
+            if mx <= tol:
+                break
+        out[b] = d
+    return torch.as_tensor(out, dtype=g.dtype, device=g.device)
+
+
+def _allreduce(ts, group):
+    if group is None:
+        return ts
+    from ..parallel import dist as pdist
+    return pdist.all_reduce_sum_f64(ts, group)
+
+
+def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
+                     group=None, max_outer: int = 100):
+    m0 = models[0]
+    _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
+    if m0.penalty not in ("l1", "l2"):
+        raise NotImplementedError("penalty must be 'l1' or 'l2'")
+    dev = X.device
+    X = X.to(torch.float64)
+    n, F = X.shape
+    B = len(models)
+    if masks is None:
+        masks = torch.ones(B, n, dtype=torch.bool, device=dev)
+    yv = y.to(device=dev, dtype=torch.float64)
+    ypm = 2.0 * yv - 1.0
+    if m0.fit_intercept:
+        Xa = torch.cat([X, torch.full((n, 1), float(m0.intercept_scaling), dtype=torch.float64, device=dev)], 1)
+    else:
+        Xa = X
+    F1 = Xa.shape[1]
+    # per-model sample weights: class weights computed on that model's training rows
+    mk = masks.to(torch.float64)
+    if m0.class_weight == "balanced":
+        cnt1 = (mk * yv[None]).sum(1)
+        cnt = torch.stack([mk.sum(1) - cnt1, cnt1], 1)
+        cnt, = _allreduce([cnt], group)
+        cw = cnt.sum(1, keepdim=True) / (2.0 * cnt)             # [B, 2]
+        s = mk * torch.where(yv[None] > 0.5, cw[:, 1:2], cw[:, 0:1])
+    else:
+        s = mk
+    C = float(m0.C)
+    l1 = m0.penalty == "l1"
+    penal = torch.ones(F1, dtype=torch.uint8, device=dev)
+    if not l1 and m0.fit_intercept:
+        penal[-1] = 0  # lbfgs path: intercept not penalised
+    pen_f = penal.to(torch.float64)
+    W = torch.zeros(B, F1, dtype=torch.float64, device=dev)
+    alphas = 0.5 ** torch.arange(8, dtype=torch.float64, device=dev)
+
+    def objective(Z, Wc):
+        # Z: [..., n, B] margins; returns [..., B]
+        data = C * (s.t() * torch.nn.functional.softplus(-ypm[:, None] * Z)).sum(-2)
+        if l1:
+            reg = (Wc.abs() * pen_f).sum(-1)
+        else:
+            reg = 0.5 * (Wc * Wc * pen_f).sum(-1)
+        return data, reg
+
+    n_iter = 0
+    Z = Xa @ W.t()                                                # [n, B]
+    g0norm = None
+    for it in range(max_outer):
+        n_iter = it + 1
+        M = ypm[:, None] * Z
+        sig = torch.sigmoid(M)
+        coef_g = s.t() * (sig - 1.0) * ypm[:, None]               # [n, B]
+        grad = C * (coef_g.t() @ Xa)                              # [B, F1]
+        D = s.t() * sig * (1.0 - sig)                             # [n, B]
+        H = C * torch.einsum("ni,nb,nj->bij", Xa, D, Xa)
+        data0 = C * (s.t() * torch.nn.functional.softplus(-M)).sum(0)
+        grad, H, data0 = _allreduce([grad, H, data0], group)
+        if l1:
+            # min-norm subgradient for the stopping rule
+            sub = torch.where(W != 0, grad + torch.sign(W),
+                              torch.sign(grad) * (grad.abs() - 1.0).clamp(min=0.0))
+            gn = sub.abs().sum(1)
+            if g0norm is None:
+                g0norm = gn.clamp(min=1e-300)
+            if bool((gn <= 1e-9 * g0norm).all()):
+                break
+            Hr = H + 1e-12 * torch.eye(F1, dtype=torch.float64, device=dev)
+            if X.is_cuda:
+                from .. import ops
+                E = ops.ext()
+                d = torch.empty_like(W)
+                E.l1_qp_cd(B, F1, Hr.contiguous().data_ptr(), grad.contiguous().data_ptr(),
+                           W.contiguous().data_ptr(), penal.data_ptr(), 1.0, 500, 1e-14,
+                           d.data_ptr(), ops.stream_ptr(dev))
+            else:
+                d = _host_l1_qp(Hr, grad, W, penal, 1.0)
+            delta = (grad * d).sum(1) + (W + d).abs().sum(1) - W.abs().sum(1)
+        else:
+            gfull = grad + W * pen_f
+            if g0norm is None:
+                g0norm = gfull.abs().sum(1).clamp(min=1e-300)
+            if bool((gfull.abs().sum(1) <= 1e-10 * g0norm).all()):
+                break
+            Hf = H + torch.diag_embed(pen_f.expand(B, -1))
+            d = -torch.linalg.solve(Hf, gfull.unsqueeze(-1)).squeeze(-1)
+            delta = (gfull * d).sum(1)
+        Xd = Xa @ d.t()                                           # [n, B]
+        Zc = Z[None] + alphas[:, None, None] * Xd[None]           # [8, n, B]
+        Wc = W[None] + alphas[:, None, None] * d[None]            # [8, B, F1]
+        dataK = C * (s.t()[None] * torch.nn.functional.softplus(-ypm[None, :, None] * Zc)).sum(1)
+        dataK, = _allreduce([dataK], group)
+        regK = (Wc.abs() * pen_f).sum(-1) if l1 else 0.5 * (Wc * Wc * pen_f).sum(-1)
+        reg0 = (W.abs() * pen_f).sum(-1) if l1 else 0.5 * (W * W * pen_f).sum(-1)
+        F0 = data0 + reg0
+        FK = dataK + regK                                         # [8, B]
+        ok = FK <= F0[None] + 1e-2 * alphas[:, None] * delta[None]
+        # largest admissible step (first True); none → smallest step if it decreases, else 0
+        first = torch.where(ok.any(0), ok.to(torch.int8).argmax(0), torch.full((B,), 7, device=dev))
+        a = alphas[first]
+        a = torch.where(ok.any(0) | (FK[7] < F0), a, torch.zeros_like(a))
+        if bool((a == 0).all()):
+            break
+        W = W + a[:, None] * d
+        Z = Z + a[None, :] * Xd
+        if bool(((a[:, None] * d).abs().max(1).values <= 1e-14 * (1 + W.abs().max(1).values)).all()):
+            break
+    scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
+    for b, m in enumerate(models):
+        coef = W[b, :F]
+        intercept = W[b, F] * scale if m0.fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
+        m.set_fitted(coef, intercept.reshape(1), [n_iter], F, device=dev)
+    return models

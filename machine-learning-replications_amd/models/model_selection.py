@@ -1,0 +1,49 @@
+"""Deterministic CV splitters with sklearn's fold assignment (so OOF meta-features
+and LassoCV paths follow the same rows as the reference run).
+
+* :func:`stratified_kfold_test_folds` — ``StratifiedKFold(n_splits, shuffle=False)``
+  (``StackingClassifier``'s ``cv=None`` on a classifier; reference
+  ``train_ensemble_public.py:48``): classes encoded by first appearance, the sorted
+  label vector dealt round-robin over folds, then each class's members assigned to
+  folds in row order.
+* :func:`kfold_test_folds` — ``KFold(n_splits)`` unshuffled (``LassoCV(cv=10)``,
+  reference ``train_ensemble_public.py:51``): contiguous blocks, the first
+  ``n % k`` folds one row larger.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+def stratified_kfold_test_folds(y, n_splits: int = 5) -> np.ndarray:
+    y = np.asarray(y.cpu() if isinstance(y, torch.Tensor) else y).ravel()
+    _, y_idx, y_inv = np.unique(y, return_index=True, return_inverse=True)
+    _, class_perm = np.unique(y_idx, return_inverse=True)
+    y_enc = class_perm[y_inv]
+    n_classes = len(y_idx)
+    counts = np.bincount(y_enc)
+    if np.all(n_splits > counts):
+        raise ValueError(f"n_splits={n_splits} cannot be greater than the number of members in each class")
+    y_order = np.sort(y_enc)
+    alloc = np.asarray([np.bincount(y_order[i::n_splits], minlength=n_classes) for i in range(n_splits)])
+    test_folds = np.empty(len(y), dtype=np.int64)
+    for k in range(n_classes):
+        test_folds[y_enc == k] = np.arange(n_splits).repeat(alloc[:, k])
+    return test_folds
+
+
+def kfold_test_folds(n: int, n_splits: int) -> np.ndarray:
+    sizes = np.full(n_splits, n // n_splits, dtype=np.int64)
+    sizes[: n % n_splits] += 1
+    return np.repeat(np.arange(n_splits), sizes)
+
+
+def fold_masks(test_folds, n_splits: int, device=None, with_full: bool = True) -> torch.Tensor:
+    """Training masks ``[n_splits (+1), n]``: fold k trains on rows not in test fold k;
+    the optional last row is the full refit."""
+    tf = torch.as_tensor(np.asarray(test_folds), device=device)
+    m = torch.stack([tf != k for k in range(n_splits)])
+    if with_full:
+        m = torch.cat([m, torch.ones(1, tf.numel(), dtype=torch.bool, device=device)])
+    return m

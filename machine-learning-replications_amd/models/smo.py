@@ -1,0 +1,421 @@
+"""Batched C-SVC training with libsvm semantics.
+
+``fit_svc_batch`` trains any number of RBF ``SVC(probability=True)`` fits at once.
+Each fit expands into libsvm's problems:
+
+* Platt CV (``svm_binary_svc_probability``): the class-grouped training set is
+  shuffled with libsvm's RNG (``std::mt19937`` seeded with sklearn's
+  ``RandomState(random_state).randint(INT_MAX)``, Lemire-bounded draws), split into
+  5 contiguous folds; each fold's training part is a sub-problem whose points are
+  re-grouped by sorted label (class 1 first) with per-class C;
+* the final solve on the class-grouped problem (class 0 = internal +1).
+
+All problems of all fits get their RBF Gram matrix from one batched MFMA launch
+(``gram_rbf_batch``) and are solved by one batched SMO launch (``smo_batch``, one
+workgroup per problem).  Held-out Platt decision values use the MFMA
+``rbf_decision`` kernel and the sigmoids are fitted by ``platt_batch``.  The host
+path mirrors every step in numpy (used on CPU and by the kernel tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+TAU = 1e-12
+INT_MAX = np.iinfo(np.int32).max
+
+
+# ----------------------------------------------------------------------------- libsvm RNG
+class _MTStream:
+    """Raw std::mt19937 output (numpy's legacy int seeding == init_genrand)."""
+
+    def __init__(self, seed: int):
+        self._bg = np.random.RandomState(seed & 0xFFFFFFFF)._bit_generator
+        self._buf = np.empty(0, dtype=np.uint64)
+        self._pos = 0
+
+    def next(self) -> int:
+        if self._pos >= self._buf.size:
+            self._buf = self._bg.random_raw(4096)
+            self._pos = 0
+        v = int(self._buf[self._pos])
+        self._pos += 1
+        return v
+
+
+def bounded_rand_int(mt: _MTStream, rng: int) -> int:
+    """sklearn newrand.h ``bounded_rand_int`` (tweaked Lemire)."""
+    x = mt.next()
+    m = x * rng
+    lo = m & 0xFFFFFFFF
+    if lo < rng:
+        t = (-rng) & 0xFFFFFFFF
+        if t >= rng:
+            t -= rng
+            if t >= rng:
+                t %= rng
+        while lo < t:
+            x = mt.next()
+            m = x * rng
+            lo = m & 0xFFFFFFFF
+    return m >> 32
+
+
+def libsvm_perm(l: int, seed: int) -> np.ndarray:
+    mt = _MTStream(seed)
+    perm = np.arange(l)
+    for i in range(l):
+        j = i + bounded_rand_int(mt, l - i)
+        perm[i], perm[j] = perm[j], perm[i]
+    return perm
+
+
+def sklearn_libsvm_seed(random_state) -> int:
+    """``check_random_state(random_state).randint(np.iinfo('i').max)`` (sklearn svm/_base.py)."""
+    if random_state is None:
+        rs = np.random.mtrand._rand
+    elif isinstance(random_state, (int, np.integer)):
+        rs = np.random.RandomState(int(random_state))
+    else:
+        rs = random_state
+    return int(rs.randint(INT_MAX))
+
+
+# ----------------------------------------------------------------------------- problems
+@dataclass
+class _Prob:
+    fit: int
+    fold: int             # -1 = final solve
+    rows: torch.Tensor    # indices into the fit's Z, in problem order
+    npos: int
+    Cp: float
+    Cn: float
+    gamma: float
+    held: Optional[torch.Tensor] = None   # Platt: held-out grouped positions
+    held_rows: Optional[torch.Tensor] = None
+
+
+def _expand(fit_id, Z, y, svc, device):
+    """libsvm problem list of one SVC fit."""
+    yb = (y > 0.5)
+    idx0 = torch.nonzero(~yb).squeeze(1)
+    idx1 = torch.nonzero(yb).squeeze(1)
+    grouped = torch.cat([idx0, idx1])
+    n0, l = int(idx0.numel()), int(grouped.numel())
+    gamma = svc.resolve_gamma(Z)
+    cw = svc.class_weights(y.to(torch.float64)).cpu()
+    C0, C1 = float(svc.C * cw[0]), float(svc.C * cw[1])
+    probs = []
+    platt = None
+    if svc.probability:
+        seed = sklearn_libsvm_seed(svc.random_state)
+        perm = torch.as_tensor(libsvm_perm(l, seed), device=grouped.device)
+        is_pos = torch.arange(l, device=grouped.device) < n0   # grouped position → class 0
+        for k in range(5):
+            b, e = k * l // 5, (k + 1) * l // 5
+            train = torch.cat([perm[:b], perm[e:]])
+            cls1 = train[~is_pos[train]]
+            cls0 = train[is_pos[train]]
+            held = perm[b:e]
+            if cls1.numel() == 0 or cls0.numel() == 0:
+                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, grouped[held]))
+                probs[-1].const = 1.0 if cls1.numel() == 0 else -1.0
+                continue
+            rows_pos = torch.cat([cls1, cls0])        # sub-problem order: label −1 (class 1) first
+            probs.append(_Prob(fit_id, k, grouped[rows_pos], int(cls1.numel()), C1, C0, gamma,
+                               held, grouped[held]))
+        platt = perm
+    probs.append(_Prob(fit_id, -1, grouped, n0, C0, C1, gamma))
+    return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
+
+
+# ----------------------------------------------------------------------------- host solver
+def _smo_host(K: np.ndarray, npos: int, Cp: float, Cn: float, eps: float, max_iter: int):
+    l = K.shape[0]
+    pos = np.arange(l) < npos
+    C = np.where(pos, Cp, Cn)
+    G = -np.ones(l)
+    alpha = np.zeros(l)
+    st = np.zeros(l, dtype=np.int8)
+    it = 0
+    for it in range(max_iter):
+        up = np.where(pos, st != 2, st != 0)
+        if not up.any():
+            break
+        v = np.where(up, np.where(pos, -G, G), -np.inf)
+        Gmax = v.max()
+        i = int(np.flatnonzero(v == Gmax)[-1])
+        yi = 1 if pos[i] else -1
+        Ki = K[i].astype(np.float64)
+        low = np.where(pos, st != 0, st != 2)
+        yG = np.where(pos, G, -G)
+        gmax2 = yG[low].max() if low.any() else -np.inf
+        gd = Gmax + yG
+        cand = low & (gd > 0)
+        quad = 2.0 - 2.0 * Ki
+        quad[quad <= 0] = TAU
+        nobj = np.where(cand, gd * gd / quad, -np.inf)
+        if not cand.any() or Gmax + gmax2 < eps:
+            break
+        best = nobj.max()
+        j = int(np.flatnonzero(nobj == best)[-1])
+        yj = 1 if pos[j] else -1
+        Ci, Cj = C[i], C[j]
+        Qij = yi * yj * float(K[i, j])
+        ai, aj = alpha[i], alpha[j]
+        Gi, Gj = G[i], G[j]
+        ai_old, aj_old = ai, aj
+        if yi != yj:
+            qc = 2.0 + 2.0 * Qij
+            qc = qc if qc > 0 else TAU
+            delta = (-Gi - Gj) / qc
+            diff = ai - aj
+            ai += delta
+            aj += delta
+            if diff > 0:
+                if aj < 0:
+                    aj, ai = 0.0, diff
+            else:
+                if ai < 0:
+                    ai, aj = 0.0, -diff
+            if diff > Ci - Cj:
+                if ai > Ci:
+                    ai, aj = Ci, Ci - diff
+            else:
+                if aj > Cj:
+                    aj, ai = Cj, Cj + diff
+        else:
+            qc = 2.0 - 2.0 * Qij
+            qc = qc if qc > 0 else TAU
+            delta = (Gi - Gj) / qc
+            s = ai + aj
+            ai -= delta
+            aj += delta
+            if s > Ci:
+                if ai > Ci:
+                    ai, aj = Ci, s - Ci
+            else:
+                if aj < 0:
+                    aj, ai = 0.0, s
+            if s > Cj:
+                if aj > Cj:
+                    aj, ai = Cj, s - Cj
+            else:
+                if ai < 0:
+                    ai, aj = 0.0, s
+        dai, daj = ai - ai_old, aj - aj_old
+        yv = np.where(pos, 1.0, -1.0)
+        G += yv * (yi * Ki * dai + yj * K[j].astype(np.float64) * daj)
+        alpha[i], alpha[j] = ai, aj
+        st[i] = 2 if ai >= Ci else (0 if ai <= 0 else 1)
+        st[j] = 2 if aj >= Cj else (0 if aj <= 0 else 1)
+    yG = np.where(pos, G, -G)
+    free = st == 1
+    if free.any():
+        rho = yG[free].sum() / free.sum()
+    else:
+        ubm = np.where(pos, st == 0, st == 2)
+        lbm = np.where(pos, st == 2, st == 0)
+        ub = yG[ubm].min() if ubm.any() else np.inf
+        lb = yG[lbm].max() if lbm.any() else -np.inf
+        rho = (ub + lb) / 2
+    return alpha, float(rho), it
+
+
+def _gram_host(Zp: np.ndarray, gamma: float) -> np.ndarray:
+    sq = (Zp * Zp).sum(1)
+    d2 = np.maximum(sq[:, None] + sq[None, :] - 2.0 * Zp @ Zp.T, 0.0)
+    K = np.exp(-gamma * d2).astype(np.float32)
+    np.fill_diagonal(K, 1.0)
+    return K
+
+
+def _sigmoid_train_host(dec, labels):
+    prior1 = float((labels > 0).sum())
+    prior0 = float(labels.size - prior1)
+    hiT, loT = (prior1 + 1.0) / (prior1 + 2.0), 1 / (prior0 + 2.0)
+    t = np.where(labels > 0, hiT, loT)
+    A, B = 0.0, np.log((prior0 + 1.0) / (prior1 + 1.0))
+
+    def f(a, b):
+        fApB = dec * a + b
+        return np.where(fApB >= 0, t * fApB + np.log1p(np.exp(-np.abs(fApB))),
+                        (t - 1) * fApB + np.log1p(np.exp(-np.abs(fApB)))).sum()
+    fval = f(A, B)
+    for _ in range(100):
+        fApB = dec * A + B
+        p = np.where(fApB >= 0, np.exp(-fApB) / (1 + np.exp(-fApB)), 1 / (1 + np.exp(fApB)))
+        q = 1 - p
+        d2 = p * q
+        h11 = (dec * dec * d2).sum() + 1e-12
+        h22 = d2.sum() + 1e-12
+        h21 = (dec * d2).sum()
+        d1 = t - p
+        g1, g2 = (dec * d1).sum(), d1.sum()
+        if abs(g1) < 1e-5 and abs(g2) < 1e-5:
+            break
+        det = h11 * h22 - h21 * h21
+        dA = -(h22 * g1 - h21 * g2) / det
+        dB = -(-h21 * g1 + h11 * g2) / det
+        gd = g1 * dA + g2 * dB
+        step = 1.0
+        while step >= 1e-10:
+            nA, nB = A + step * dA, B + step * dB
+            nf = f(nA, nB)
+            if nf < fval + 0.0001 * step * gd:
+                A, B, fval = nA, nB, nf
+                break
+            step /= 2.0
+        if step < 1e-10:
+            break
+    return A, B
+
+
+# ----------------------------------------------------------------------------- device helpers
+_GRAM_DT = np.dtype([("zoff", "<i8"), ("koff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("ngl2e", "<f4"),
+                     ("pad", "<i4")])
+_SMO_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
+                    ("pad", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
+_PLATT_DT = np.dtype([("off", "<i8"), ("l", "<i4"), ("pad", "<i4")])
+
+
+def _dev_struct(arr: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
+    from .. import ops
+    E = ops.ext()
+    s = ops.stream_ptr(device)
+    live = [p for p in probs if p.rows is not None]
+    F = Zs[0].shape[1]
+    zcat = torch.cat([Zs[p.fit][p.rows].to(torch.float32) for p in live]).contiguous()
+    g = np.zeros(len(live), _GRAM_DT)
+    sm = np.zeros(len(live), _SMO_DT)
+    zoff = koff = aoff = 0
+    for k, p in enumerate(live):
+        l = int(p.rows.numel())
+        ld = (l + 63) // 64 * 64
+        g[k] = (zoff, koff, l, ld, -p.gamma * 1.4426950408889634, 0)
+        sm[k] = (koff, aoff, l, ld, p.npos, 0, p.Cp, p.Cn)
+        zoff += l
+        koff += l * ld
+        aoff += l
+    max_l = max(int(p.rows.numel()) for p in live)
+    K = torch.empty(koff, dtype=torch.float32, device=device)
+    gdev = _dev_struct(g, device)
+    E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
+    alpha = torch.empty(aoff, dtype=torch.float64, device=device)
+    rho = torch.empty(len(live), dtype=torch.float64, device=device)
+    iters = torch.empty(len(live), dtype=torch.int32, device=device)
+    gap = torch.empty(len(live), dtype=torch.float64, device=device)
+    max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
+    sdev = _dev_struct(sm, device)
+    E.smo_batch(sdev.data_ptr(), len(live), max_l, K.data_ptr(), alpha.data_ptr(), eps, max_iter,
+                rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), s)
+    del K
+    out = {}
+    for k, p in enumerate(live):
+        a0 = int(sm[k]["aoff"])
+        out[id(p)] = (alpha[a0:a0 + int(sm[k]["l"])], rho[k], iters[k])
+    return out
+
+
+def _solve_host(probs: List[_Prob], Zs, eps, max_iter_cap=None):
+    out = {}
+    for p in probs:
+        if p.rows is None:
+            continue
+        Zp = Zs[p.fit][p.rows].double().cpu().numpy()
+        K = _gram_host(Zp, p.gamma)
+        l = K.shape[0]
+        mi = max(10_000_000, 100 * l) if max_iter_cap is None else max_iter_cap
+        a, r, it = _smo_host(K, p.npos, p.Cp, p.Cn, eps, mi)
+        out[id(p)] = (torch.as_tensor(a), torch.tensor(r, dtype=torch.float64), torch.tensor(it))
+    return out
+
+
+# ----------------------------------------------------------------------------- public
+def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None):
+    """Fit ``svcs[f]`` on (already scaled) ``Zs[f]`` with labels ``ys[f]`` ∈ {0,1}."""
+    from .. import ops
+    device = Zs[0].device
+    cuda = Zs[0].is_cuda
+    all_probs, meta = [], []
+    for f, (svc, Z, y) in enumerate(zip(svcs, Zs, ys)):
+        pr, mt = _expand(f, Z, y.to(device), svc, device)
+        all_probs += pr
+        meta.append(mt)
+    eps = float(svcs[0].tol)
+    sol = _solve_device(all_probs, Zs, device, eps, max_iter_cap) if cuda else _solve_host(all_probs, Zs, eps, max_iter_cap)
+    # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
+    AB = [None] * len(svcs)
+    decs, labs, pl = [], [], []
+    for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
+        if not svc.probability:
+            continue
+        l = mt["l"]
+        dec = torch.zeros(l, dtype=torch.float64, device=device)
+        for p in all_probs:
+            if p.fit != f or p.fold < 0:
+                continue
+            if p.rows is None:
+                dec[p.held] = p.const
+                continue
+            a, r, _ = sol[id(p)]
+            a = a.to(device)
+            yint = torch.where(torch.arange(a.numel(), device=device) < p.npos, 1.0, -1.0).to(torch.float64)
+            coef = yint * a
+            Zh = Z[p.held_rows]
+            if cuda:
+                d = ops.rbf_decision(Zh, Z[p.rows], coef, p.gamma, 0.0).to(torch.float64) - r.to(device)
+            else:
+                from ..ops import reference as ref
+                d = ref.rbf_decision(Zh.double(), Z[p.rows].double(), coef, p.gamma, 0.0) - r
+            dec[p.held] = -d    # × submodel label[0] (= −1)
+        lab = torch.where(torch.arange(l, device=device) < mt["n0"], 1.0, -1.0)
+        decs.append(dec)
+        labs.append(lab)
+        pl.append(f)
+    if pl:
+        if cuda:
+            E = ops.ext()
+            arr = np.zeros(len(pl), _PLATT_DT)
+            off = 0
+            for k, d in enumerate(decs):
+                arr[k] = (off, d.numel(), 0)
+                off += d.numel()
+            dcat = torch.cat(decs).contiguous()
+            lcat = torch.cat(labs).to(torch.float32).contiguous()
+            ABt = torch.empty(2 * len(pl), dtype=torch.float64, device=device)
+            pdev = _dev_struct(arr, device)
+            E.platt_batch(pdev.data_ptr(), len(pl), dcat.data_ptr(), lcat.data_ptr(), ABt.data_ptr(),
+                          ops.stream_ptr(device))
+            ABc = ABt.cpu().numpy()
+            for k, f in enumerate(pl):
+                AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
+        else:
+            for k, f in enumerate(pl):
+                AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
+    # ---- final models
+    for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
+        p = [q for q in all_probs if q.fit == f and q.fold < 0][0]
+        a, r, it = sol[id(p)]
+        a = a.to(device)
+        sv = a > 0
+        pos_idx = torch.nonzero(sv).squeeze(1)
+        yint = torch.where(pos_idx < mt["n0"], 1.0, -1.0).to(torch.float64)
+        coef = yint * a[pos_idx]
+        support = mt["grouped"][pos_idx]
+        n_sv0 = int((pos_idx < mt["n0"]).sum())
+        A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
+        svc.set_fitted(support=support, support_vectors=Z[support].to(torch.float64),
+                       n_support=[n_sv0, int(pos_idx.numel()) - n_sv0], dual_coef_libsvm=coef,
+                       rho=float(r), probA=A, probB=B, gamma=mt["gamma"],
+                       class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
+                       shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
+        svc.n_iter_ = int(it)
+    return svcs

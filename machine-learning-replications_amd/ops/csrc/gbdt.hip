@@ -1,0 +1,411 @@
+// Histogram GBDT training for binomial deviance (reference model
+// GradientBoostingClassifier(100 stumps), train_ensemble_public.py:45).
+//
+// B independent models (CV folds + full refit, or seeds) train together on one binned matrix;
+// model b sees rows with weight w[b][i] > 0.  Trees grow level-wise in heap layout (node k →
+// children 2k+1, 2k+2).  Per boosting stage:
+//   gbdt_apply_prep : route rows through the previous tree's last level, add lr·leaf value to
+//                     raw (f64), accumulate that tree's leaf Σw·r² (impurity) and the training
+//                     deviance, then compute this stage's residual g = w(y−p) and hessian
+//                     h = w·p(1−p) (f32) and reset every row to the root.
+//   gbdt_hist       : per (model, node, feature, bin) sums of (g, h, w) in FIXED POINT (int64,
+//                     scale 2^shift).  Integer sums are exact and order-independent, so the
+//                     histogram is bit-identical for any launch geometry, any atomics order and
+//                     any data-parallel sharding (RCCL all-reduce of int64 SUM is exact).
+//                     Low-cardinality features (≤ 8 bins, 80 % of the HF columns) accumulate in
+//                     registers over a whole row chunk and reduce once per chunk; others use an
+//                     LDS histogram with ds_add_u64 and one global flush per workgroup.
+//   gbdt_split      : per (model, node): prefix scan over bins, friedman_mse proxy
+//                     (w_r·S_l − w_l·S_r)²/(w_l·w_r), deterministic tie-break (lowest feature,
+//                     lowest bin), threshold = midpoint of the adjacent *non-empty* bins' values
+//                     (= sklearn's exact splitter on the model's own training rows), Newton leaf
+//                     values Σr/Σh for children of the last level.
+//   gbdt_route      : move rows of split nodes one level down, accumulating child Σw·r².
+#include "common.h"
+
+namespace hfens {
+
+struct GbdtShape {
+  int B, n, F, NN;  // models, rows, features, heap nodes per tree
+};
+
+__device__ __forceinline__ long long q_of(double v, double scale) {
+  return (long long)rint(v * scale);
+}
+
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// A: apply previous tree (one pending routing level + leaf values) and prepare this stage.
+// prev_* are the previous tree's tables [B][NN] (heap), or nullptr for the first stage.
+__global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
+    GbdtShape S, const unsigned char* __restrict__ bins, const float* __restrict__ y,
+    const float* __restrict__ w, double* __restrict__ raw, float* __restrict__ g,
+    float* __restrict__ h, int* __restrict__ node, const int* __restrict__ prev_feat,
+    const int* __restrict__ prev_blo, const double* __restrict__ prev_value,
+    long long* __restrict__ prev_r2 /*[B][NN] previous tree Σw r²*/, long long* __restrict__ dev_acc /*[B]*/,
+    long long* __restrict__ cur_r2 /*[B][NN] this tree (root slot)*/, double lr, double qscale,
+    double dscale) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  long long dev_q = 0, r2_q = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += gridDim.x * blockDim.x) {
+    const size_t bi = (size_t)b * S.n + i;
+    const float wi = w[bi];
+    double rw = raw[bi];
+    const double yi = y[i];
+    if (prev_feat != nullptr) {
+      int nd = node[bi];
+      const int f = prev_feat[b * S.NN + nd];
+      if (f >= 0) {  // pending split at the last level
+        const int side = bins[(size_t)f * S.n + i] <= prev_blo[b * S.NN + nd] ? 1 : 2;
+        nd = 2 * nd + side;
+      }
+      if (wi > 0.f) {
+        const double p0 = 1.0 / (1.0 + exp(-rw));
+        const double r0 = yi - p0;
+        atomicAdd((unsigned long long*)&prev_r2[(size_t)b * S.NN + nd],
+                  (unsigned long long)q_of(wi * r0 * r0, qscale));
+      }
+      rw += lr * prev_value[b * S.NN + nd];
+      raw[bi] = rw;
+    }
+    const double p = 1.0 / (1.0 + exp(-rw));
+    const double r = yi - p;
+    const float gi = (float)(wi * r);
+    const float hi = (float)(wi * p * (1.0 - p));
+    g[bi] = gi;
+    h[bi] = hi;
+    node[bi] = 0;
+    if (wi > 0.f) {
+      // binomial deviance term −2(y·raw − log(1+e^raw)) (sklearn BinomialDeviance), after the update
+      const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
+      dev_q += q_of(wi * (-2.0) * (yi * rw - l1p), dscale);
+      r2_q += q_of(wi * r * r, qscale);
+    }
+  }
+  dev_q = wave_sum_i64(dev_q);
+  r2_q = wave_sum_i64(r2_q);
+  if (lane == 0) {
+    if (prev_feat != nullptr) atomicAdd((unsigned long long*)&dev_acc[b], (unsigned long long)dev_q);
+    atomicAdd((unsigned long long*)&cur_r2[(size_t)b * S.NN], (unsigned long long)r2_q);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// B: histograms.  grid = (row chunks, F, B).  hist layout [B][NL][F][256][3] int64 where the
+// level's nodes are heap indices node0 .. node0+NL-1.
+template <int C>
+__device__ void hist_registers(const unsigned char* __restrict__ col, const float* __restrict__ g,
+                               const float* __restrict__ h, const float* __restrict__ w,
+                               const int* __restrict__ node, int node0, int r0, int r1,
+                               double qscale, long long* __restrict__ out /*[256][3]*/) {
+  long long ag[C], ah[C], aw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { ag[c] = 0; ah[c] = 0; aw[c] = 0; }
+  for (int i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    if (node[i] != node0) continue;
+    const float wi = w[i];
+    if (!(wi > 0.f)) continue;
+    const int bb = col[i];
+    const long long qg = q_of(g[i], qscale), qh = q_of(h[i], qscale), qw = q_of(wi, qscale);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const bool m = (bb == c);
+      ag[c] += m ? qg : 0;
+      ah[c] += m ? qh : 0;
+      aw[c] += m ? qw : 0;
+    }
+  }
+  __shared__ long long red[4][C * 3];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    long long a = wave_sum_i64(ag[c]), b2 = wave_sum_i64(ah[c]), c2 = wave_sum_i64(aw[c]);
+    if (lane == 0) { red[wave][3 * c] = a; red[wave][3 * c + 1] = b2; red[wave][3 * c + 2] = c2; }
+  }
+  __syncthreads();
+  if (threadIdx.x < C * 3) {
+    long long s = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += red[k][threadIdx.x];
+    if (s != 0) atomicAdd((unsigned long long*)&out[threadIdx.x], (unsigned long long)s);
+  }
+}
+
+__global__ __launch_bounds__(256) void gbdt_hist_kernel(
+    GbdtShape S, const unsigned char* __restrict__ bins, const int* __restrict__ nbins,
+    const float* __restrict__ g, const float* __restrict__ h, const float* __restrict__ w,
+    const int* __restrict__ node, int node0, int NL, int chunk, long long* __restrict__ hist,
+    double qscale) {
+  const int f = blockIdx.y;
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.x * chunk;
+  const int r1 = min(S.n, r0 + chunk);
+  const size_t boff = (size_t)b * S.n;
+  const unsigned char* col = bins + (size_t)f * S.n;
+  const int nb = nbins[f];
+  long long* hb = hist + (size_t)b * NL * S.F * 768;
+  if (NL == 1) {
+    long long* out = hb + (size_t)f * 768;
+    if (nb <= 2) return hist_registers<2>(col, g + boff, h + boff, w + boff, node + boff, node0, r0, r1, qscale, out);
+    if (nb <= 4) return hist_registers<4>(col, g + boff, h + boff, w + boff, node + boff, node0, r0, r1, qscale, out);
+    if (nb <= 8) return hist_registers<8>(col, g + boff, h + boff, w + boff, node + boff, node0, r0, r1, qscale, out);
+  }
+  // LDS path: NL ≤ 16 nodes × 256 bins × 3 stats × 8 B = up to 96 KiB
+  extern __shared__ __attribute__((aligned(16))) long long lh[];
+  const int tot = NL * nb * 3;
+  for (int k = threadIdx.x; k < tot; k += blockDim.x) lh[k] = 0;
+  __syncthreads();
+  for (int i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    const int nd = node[boff + i] - node0;
+    if (nd < 0 || nd >= NL) continue;
+    const float wi = w[boff + i];
+    if (!(wi > 0.f)) continue;
+    const int bb = col[i];
+    long long* cell = lh + ((size_t)nd * nb + bb) * 3;
+    atomicAdd((unsigned long long*)&cell[0], (unsigned long long)q_of(g[boff + i], qscale));
+    atomicAdd((unsigned long long*)&cell[1], (unsigned long long)q_of(h[boff + i], qscale));
+    atomicAdd((unsigned long long*)&cell[2], (unsigned long long)q_of(wi, qscale));
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < tot; k += blockDim.x) {
+    const long long v = lh[k];
+    if (v == 0) continue;
+    const int s = k % 3, bb = (k / 3) % nb, nd = k / (3 * nb);
+    atomicAdd((unsigned long long*)&hb[(((size_t)nd * S.F + f) * 256 + bb) * 3 + s],
+              (unsigned long long)v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// C: split finding.  grid = (NL, B), 256 threads (4 waves; wave ↔ features f ≡ wave mod 4).
+struct SplitOut {
+  int* feat;          // [B][NN]  split feature, -2 leaf
+  int* blo;           // [B][NN]  last bin going left
+  double* thr;        // [B][NN]
+  double* value;      // [B][NN]  node value (mean residual for internal, Newton for leaves)
+  long long* stats;   // [B][NN][4] Σw, Σr, Σh, (unused)   (fixed point)
+  const long long* r2;  // [B][NN] Σw r² (filled by apply_prep / route)
+};
+
+__device__ __forceinline__ void scan_feature(const long long* __restrict__ hf, int nb, int lane,
+                                             long long tw, long long tg, double min_leaf_q,
+                                             double& best_gain, int& best_bin) {
+  // lane owns bins 4·lane .. 4·lane+3; exclusive prefix across lanes via shuffles
+  long long pw[4], pg[4];
+  long long sw = 0, sg = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bb = 4 * lane + j;
+    const long long gw = bb < nb ? hf[bb * 3 + 2] : 0;
+    const long long gg = bb < nb ? hf[bb * 3 + 0] : 0;
+    sw += gw; sg += gg;
+    pw[j] = sw; pg[j] = sg;
+  }
+  long long xw = sw, xg = sg;  // inclusive scan of lane totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    long long tw2 = __shfl_up(xw, o, kWave), tg2 = __shfl_up(xg, o, kWave);
+    if (lane >= o) { xw += tw2; xg += tg2; }
+  }
+  const long long ew = xw - sw, eg = xg - sg;
+  best_gain = -1.0;
+  best_bin = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bb = 4 * lane + j;
+    if (bb >= nb - 1) continue;
+    const long long lw = ew + pw[j], lg = eg + pg[j];
+    const long long rw = tw - lw, rg = tg - lg;
+    if ((double)lw < min_leaf_q || (double)rw < min_leaf_q) continue;
+    const double dlw = (double)lw, drw = (double)rw;
+    const double diff = drw * (double)lg - dlw * (double)rg;
+    const double gain = diff / dlw * diff / drw;
+    if (gain > best_gain) { best_gain = gain; best_bin = bb; }
+  }
+  // wave argmax, lowest bin on ties
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double og = __shfl_xor(best_gain, o, kWave);
+    int ob = __shfl_xor(best_bin, o, kWave);
+    if (og > best_gain || (og == best_gain && ob < best_bin)) { best_gain = og; best_bin = ob; }
+  }
+}
+
+__global__ __launch_bounds__(256) void gbdt_split_kernel(
+    GbdtShape S, const long long* __restrict__ hist, const int* __restrict__ nbins,
+    const double* __restrict__ lo_val, const double* __restrict__ hi_val, int node0, int NL,
+    int last_level, double min_leaf_q, double min_split_q, double qscale, SplitOut o) {
+  const int nd = blockIdx.x;      // node within level
+  const int b = blockIdx.y;
+  const int hn = node0 + nd;      // heap index
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long* hb = hist + ((size_t)b * NL + nd) * S.F * 768;
+  long long* st = o.stats + ((size_t)b * S.NN + hn) * 4;
+  // node totals from feature 0's bins
+  __shared__ long long tot[3];
+  __shared__ double wg[4];
+  __shared__ int wf[4], wbin[4];
+  if (wave == 0) {
+    long long a = 0, c = 0, d = 0;
+    const int nb0 = nbins[0];
+    for (int bb = lane; bb < nb0; bb += 64) { a += hb[bb * 3]; c += hb[bb * 3 + 1]; d += hb[bb * 3 + 2]; }
+    a = wave_sum_i64(a); c = wave_sum_i64(c); d = wave_sum_i64(d);
+    if (lane == 0) { tot[0] = a; tot[1] = c; tot[2] = d; }
+  }
+  __syncthreads();
+  const long long tg = tot[0], th = tot[1], tw = tot[2];
+  if (tw <= 0) {  // unreachable / empty node
+    if (threadIdx.x == 0) { o.feat[b * S.NN + hn] = -3; }
+    return;
+  }
+  double bg = -1.0;
+  int bf = 0x7fffffff, bbin = 0;
+  if ((double)tw >= min_split_q) {
+    for (int f = wave; f < S.F; f += 4) {
+      double gg;
+      int gb;
+      scan_feature(hb + (size_t)f * 768, nbins[f], lane, tw, tg, min_leaf_q, gg, gb);
+      if (gg > bg) { bg = gg; bf = f; bbin = gb; }  // f ascending within a wave
+    }
+  }
+  if (lane == 0) { wg[wave] = bg; wf[wave] = bf; wbin[wave] = bbin; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  bg = wg[0]; bf = wf[0]; bbin = wbin[0];
+  for (int k = 1; k < 4; ++k)
+    if (wg[k] > bg || (wg[k] == bg && wf[k] < bf)) { bg = wg[k]; bf = wf[k]; bbin = wbin[k]; }
+  // node record
+  st[0] = tw; st[1] = tg; st[2] = th;
+  const double inv = 1.0 / qscale;
+  // impurity==0 ⇒ leaf (sklearn: impurity <= EPSILON); impurity from Σw r² (st[3], filled by prep/route)
+  const double dw = tw * inv, dg = tg * inv;
+  const double imp = o.r2[(size_t)b * S.NN + hn] * inv / dw - (dg / dw) * (dg / dw);
+  const bool can_split = bg >= 0.0 && bf < S.F && imp > 2.220446049250313e-16;
+  const int idx = b * S.NN + hn;
+  if (!can_split) {
+    o.feat[idx] = -2;
+    o.blo[idx] = 0;
+    o.thr[idx] = -2.0;
+    const double den = th * inv;
+    o.value[idx] = fabs(den) < 1e-150 ? 0.0 : dg / den;
+    return;
+  }
+  // children sums at the chosen bin; the following non-empty bin gives the threshold
+  const long long* hf = hb + (size_t)bf * 768;
+  long long lw = 0, lg = 0, lh = 0;
+  for (int bb = 0; bb <= bbin; ++bb) { lg += hf[bb * 3]; lh += hf[bb * 3 + 1]; lw += hf[bb * 3 + 2]; }
+  int hi = bbin + 1;
+  const int nbf = nbins[bf];
+  while (hi < nbf - 1 && hf[hi * 3 + 2] == 0) ++hi;
+  const double a = hi_val[bf * 256 + bbin], c = lo_val[bf * 256 + hi];
+  double t = a / 2.0 + c / 2.0;
+  if (t == c || isinf(t)) t = a;
+  o.feat[idx] = bf;
+  o.blo[idx] = bbin;
+  o.thr[idx] = t;
+  o.value[idx] = dg / dw;  // internal node value: weighted mean residual
+  const int L = 2 * hn + 1, R = 2 * hn + 2;
+  long long* sl = o.stats + ((size_t)b * S.NN + L) * 4;
+  long long* sr = o.stats + ((size_t)b * S.NN + R) * 4;
+  sl[0] = lw; sl[1] = lg; sl[2] = lh;
+  sr[0] = tw - lw; sr[1] = tg - lg; sr[2] = th - lh;
+  if (last_level) {  // children are leaves: Newton values, sklearn _update_terminal_regions
+    o.feat[b * S.NN + L] = -2; o.feat[b * S.NN + R] = -2;
+    o.blo[b * S.NN + L] = 0; o.blo[b * S.NN + R] = 0;
+    o.thr[b * S.NN + L] = -2.0; o.thr[b * S.NN + R] = -2.0;
+    const double dl = lh * inv, dr = (th - lh) * inv;
+    o.value[b * S.NN + L] = fabs(dl) < 1e-150 ? 0.0 : lg * inv / dl;
+    o.value[b * S.NN + R] = fabs(dr) < 1e-150 ? 0.0 : (tg - lg) * inv / dr;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// D: route rows of split nodes at the current level one level down (not the last level: that
+// routing is fused into the next stage's apply_prep).
+__global__ __launch_bounds__(256) void gbdt_route_kernel(
+    GbdtShape S, const unsigned char* __restrict__ bins, const float* __restrict__ g,
+    const float* __restrict__ w, int* __restrict__ node, const int* __restrict__ feat,
+    const int* __restrict__ blo, long long* __restrict__ r2, int node0, int NL, double qscale) {
+  const int b = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += gridDim.x * blockDim.x) {
+    const size_t bi = (size_t)b * S.n + i;
+    const int nd = node[bi];
+    if (nd < node0 || nd >= node0 + NL) continue;
+    const int f = feat[b * S.NN + nd];
+    if (f < 0) continue;
+    const int child = 2 * nd + (bins[(size_t)f * S.n + i] <= blo[b * S.NN + nd] ? 1 : 2);
+    node[bi] = child;
+    const float wi = w[bi];
+    if (wi > 0.f) {
+      const double r = (double)g[bi] / wi;
+      atomicAdd((unsigned long long*)&r2[(size_t)b * S.NN + child],
+                (unsigned long long)q_of(wi * r * r, qscale));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host entry points
+static int grid_rows(int n) {
+  int g = (n + 255) / 256;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+}
+
+void gbdt_apply_prep(int B, int n, int F, int NN, uintptr_t bins, uintptr_t y, uintptr_t w,
+                     uintptr_t raw, uintptr_t g, uintptr_t h, uintptr_t node, uintptr_t prev_feat,
+                     uintptr_t prev_blo, uintptr_t prev_value, uintptr_t prev_r2,
+                     uintptr_t dev_acc, uintptr_t cur_r2, double lr, double qscale, double dscale,
+                     uintptr_t stream) {
+  GbdtShape S{B, n, F, NN};
+  hipLaunchKernelGGL(gbdt_apply_prep_kernel, dim3(grid_rows(n), B), dim3(256), 0, as_stream(stream),
+                     S, (const unsigned char*)bins, (const float*)y, (const float*)w, (double*)raw,
+                     (float*)g, (float*)h, (int*)node, (const int*)prev_feat, (const int*)prev_blo,
+                     (const double*)prev_value, (long long*)prev_r2, (long long*)dev_acc,
+                     (long long*)cur_r2, lr, qscale, dscale);
+  launch_check();
+}
+
+void gbdt_hist(int B, int n, int F, uintptr_t bins, uintptr_t nbins, int max_nb, uintptr_t g,
+               uintptr_t h, uintptr_t w, uintptr_t node, int node0, int NL, uintptr_t hist,
+               double qscale, uintptr_t stream) {
+  HFENS_REQUIRE(NL >= 1 && NL <= 16, "gbdt_hist: at most 16 nodes per level on the LDS path");
+  GbdtShape S{B, n, F, 0};
+  const int chunk = n <= 16384 ? 1024 : 8192;
+  dim3 grid((n + chunk - 1) / chunk, F, B);
+  const size_t lds = (size_t)NL * max_nb * 3 * sizeof(long long);
+  HFENS_REQUIRE(lds <= 160 * 1024, "gbdt_hist: histogram does not fit LDS");
+  hipLaunchKernelGGL(gbdt_hist_kernel, grid, dim3(256), lds, as_stream(stream), S,
+                     (const unsigned char*)bins, (const int*)nbins, (const float*)g, (const float*)h,
+                     (const float*)w, (const int*)node, node0, NL, chunk, (long long*)hist, qscale);
+  launch_check();
+}
+
+void gbdt_split(int B, int F, int NN, uintptr_t hist, uintptr_t nbins, uintptr_t lo_val,
+                uintptr_t hi_val, int node0, int NL, int last_level, double min_leaf_q,
+                double min_split_q, double qscale, uintptr_t feat, uintptr_t blo, uintptr_t thr,
+                uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t stream) {
+  GbdtShape S{B, 0, F, NN};
+  SplitOut o{(int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
+             (const long long*)r2};
+  hipLaunchKernelGGL(gbdt_split_kernel, dim3(NL, B), dim3(256), 0, as_stream(stream), S,
+                     (const long long*)hist, (const int*)nbins, (const double*)lo_val,
+                     (const double*)hi_val, node0, NL, last_level, min_leaf_q, min_split_q, qscale, o);
+  launch_check();
+}
+
+void gbdt_route(int B, int n, int NN, uintptr_t bins, uintptr_t g, uintptr_t w, uintptr_t node,
+                uintptr_t feat, uintptr_t blo, uintptr_t r2, int node0, int NL, double qscale,
+                uintptr_t stream) {
+  GbdtShape S{B, n, 0, NN};
+  hipLaunchKernelGGL(gbdt_route_kernel, dim3(grid_rows(n), B), dim3(256), 0, as_stream(stream), S,
+                     (const unsigned char*)bins, (const float*)g, (const float*)w, (int*)node,
+                     (const int*)feat, (const int*)blo, (long long*)r2, node0, NL, qscale);
+  launch_check();
+}
+
+}  // namespace hfens

@@ -1,0 +1,157 @@
+// Small dense solvers for the linear models (SURVEY.md §2.3 K3 lasso_cd_path, K13 logreg_cd).
+//
+//  l1_qp_cd      : batched L1-regularised quadratic subproblem of proximal Newton (the
+//                  newGLMNET inner problem of liblinear's solve_l1r_lr):
+//                      min_d  gᵀd + ½ dᵀHd + λ‖w + d‖₁      (per model, dense H ≤ 64×64)
+//                  One 64-lane wave per model: H lives in LDS, lane j owns coordinate j's
+//                  (Hd)_j, cyclic coordinate descent with soft-thresholding.
+//  lasso_cd_path : batched Gram-form coordinate descent over a decreasing alpha grid
+//                  (sklearn enet_coordinate_descent_gram semantics: objective
+//                  ½‖y−Xw‖²/n + α‖w‖₁ with centred X, y; duality-gap stop), one wave per
+//                  problem (CV fold), warm-started along the path, recording the path.
+#include "common.h"
+
+namespace hfens {
+
+__global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __restrict__ H,
+                                                      const double* __restrict__ g,
+                                                      const double* __restrict__ w,
+                                                      const unsigned char* __restrict__ penal,
+                                                      double lam, int max_sweeps, double tol,
+                                                      double* __restrict__ d_out) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int b = blockIdx.x;
+  const int j = threadIdx.x;
+  double* Hs = sm;                 // [F1][F1]
+  const double* Hb = H + (size_t)b * F1 * F1;
+  for (int k = j; k < F1 * F1; k += 64) Hs[k] = Hb[k];
+  __syncthreads();
+  const double gj = j < F1 ? g[b * F1 + j] : 0.0;
+  const double wj = j < F1 ? w[b * F1 + j] : 0.0;
+  double Hd = 0.0;  // (H d)_j
+  double dj = 0.0;
+  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+    double maxstep = 0.0;
+    for (int k = 0; k < F1; ++k) {
+      // coordinate k: quantities owned by lane k
+      const double gk = __shfl(gj, k, kWave), wk = __shfl(wj, k, kWave);
+      const double Hdk = __shfl(Hd, k, kWave), dk = __shfl(dj, k, kWave);
+      const double hkk = Hs[k * F1 + k];
+      const double a = hkk > 1e-300 ? hkk : 1e-300;
+      // 1-D problem in z = w_k + d_k:  (gk + Hdk − hkk·dk)(z − wk) + ½hkk(z − wk)² + λ|z|
+      const double lin = gk + Hdk - a * dk;
+      const double z0 = wk - lin / a;  // unpenalised minimiser
+      const double lk = penal[k] ? lam : 0.0;
+      double z = z0;
+      if (lk > 0) z = z0 > lk / a ? z0 - lk / a : (z0 < -lk / a ? z0 + lk / a : 0.0);
+      const double nd = z - wk;
+      const double step = nd - dk;
+      if (step != 0.0) {
+        if (j < F1) Hd += Hs[j * F1 + k] * step;
+        if (j == k) dj = nd;
+        maxstep = fmax(maxstep, fabs(step));
+      }
+    }
+    if (maxstep <= tol) break;
+  }
+  if (j < F1) d_out[b * F1 + j] = dj;
+}
+
+void l1_qp_cd(int B, int F1, uintptr_t H, uintptr_t g, uintptr_t w, uintptr_t penal, double lam,
+              int max_sweeps, double tol, uintptr_t d_out, uintptr_t stream) {
+  HFENS_REQUIRE(F1 >= 1 && F1 <= 64, "l1_qp_cd: 1 <= F+1 <= 64");
+  const size_t lds = (size_t)F1 * F1 * sizeof(double);
+  hipLaunchKernelGGL(l1_qp_cd_kernel, dim3(B), dim3(64), lds, as_stream(stream), F1,
+                     (const double*)H, (const double*)g, (const double*)w,
+                     (const unsigned char*)penal, lam, max_sweeps, tol, (double*)d_out);
+  launch_check();
+}
+
+// ------------------------------------------------------------------------------------------
+// Lasso path, Gram form.  Per problem p: G = XᵀX (F×F), q = Xᵀy (F), n_p rows, yy = yᵀy.
+// Objective  (1/(2 n_p))‖y − Xw‖² + α‖w‖₁  ⇔ sklearn's enet with l1_ratio=1 (alpha scaled by n).
+// coefs out: [P][A][F]; gaps out [P][A]; iters [P][A].
+__global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const double* __restrict__ G,
+                                                           const double* __restrict__ q,
+                                                           const double* __restrict__ yy,
+                                                           const double* __restrict__ nrows,
+                                                           const double* __restrict__ alphas,
+                                                           int max_iter, double tol,
+                                                           double* __restrict__ coefs,
+                                                           double* __restrict__ gaps,
+                                                           int* __restrict__ iters) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int p = blockIdx.x;
+  const int j = threadIdx.x;
+  double* Gs = sm;  // [F][F]
+  const double* Gp = G + (size_t)p * F * F;
+  for (int k = j; k < F * F; k += 64) Gs[k] = Gp[k];
+  __syncthreads();
+  const double n = nrows[p];
+  const double qj = j < F ? q[p * F + j] : 0.0;
+  const double gjj = j < F ? Gs[j * F + j] : 0.0;
+  const double yyp = yy[p];
+  double wj = 0.0;   // coefficient owned by lane j
+  double Hw = 0.0;   // (G w)_j
+  // sklearn: tol *= ‖y‖² (Gram path) ; l1_reg = alpha·n
+  const double tol_s = tol * yyp;
+  for (int a = 0; a < A; ++a) {
+    const double l1 = alphas[p * A + a] * n;
+    int it = 0;
+    double gap = 0.0;
+    for (it = 0; it < max_iter; ++it) {
+      double w_max = 0.0, d_w_max = 0.0;
+      for (int k = 0; k < F; ++k) {
+        const double gkk = __shfl(gjj, k, kWave);
+        if (gkk == 0.0) continue;
+        const double wk = __shfl(wj, k, kWave), Hwk = __shfl(Hw, k, kWave), qk = __shfl(qj, k, kWave);
+        // tmp = q_k − (Gw)_k + G_kk w_k
+        const double tmp = qk - Hwk + gkk * wk;
+        double nw = fabs(tmp) > l1 ? copysign(fabs(tmp) - l1, tmp) / gkk : 0.0;
+        const double dw = nw - wk;
+        if (dw != 0.0) {
+          if (j < F) Hw += Gs[j * F + k] * dw;
+          if (j == k) wj = nw;
+        }
+        d_w_max = fmax(d_w_max, fabs(dw));
+        w_max = fmax(w_max, fabs(nw));
+      }
+      if (w_max == 0.0 || d_w_max / w_max < tol || it == max_iter - 1) {
+        // duality gap (sklearn enet_coordinate_descent_gram, l2_reg = 0)
+        const double wq = wave_sum(j < F ? wj * qj : 0.0);
+        const double wHw = wave_sum(j < F ? wj * Hw : 0.0);
+        const double l1n = wave_sum(j < F ? fabs(wj) : 0.0);
+        double dual_norm = j < F ? fabs(qj - Hw) : 0.0;  // |Xᵀ R|_∞ with R = y − Xw
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dual_norm = fmax(dual_norm, __shfl_xor(dual_norm, o, kWave));
+        const double R_norm2 = yyp - 2.0 * wq + wHw;
+        double const_ = 1.0;
+        double gp = R_norm2;
+        if (dual_norm > l1) {
+          const_ = l1 / dual_norm;
+          const double A_norm2 = R_norm2 * const_ * const_;
+          gp = 0.5 * (R_norm2 + A_norm2);
+        }
+        // q_dot_w = wq ; y_norm2 = yy
+        gap = gp + l1 * l1n - const_ * (yyp - wq);  // R·y = yy − wᵀq
+        if (gap < tol_s) break;
+      }
+    }
+    if (j < F) coefs[((size_t)p * A + a) * F + j] = wj;
+    if (j == 0) { gaps[p * A + a] = gap; iters[p * A + a] = it + 1; }
+  }
+}
+
+void lasso_cd_path(int P, int F, int A, uintptr_t G, uintptr_t q, uintptr_t yy, uintptr_t nrows,
+                   uintptr_t alphas, int max_iter, double tol, uintptr_t coefs, uintptr_t gaps,
+                   uintptr_t iters, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64, "lasso_cd_path: 1 <= F <= 64");
+  const size_t lds = (size_t)F * F * sizeof(double);
+  hipLaunchKernelGGL(lasso_cd_path_kernel, dim3(P), dim3(64), lds, as_stream(stream), F, A,
+                     (const double*)G, (const double*)q, (const double*)yy, (const double*)nrows,
+                     (const double*)alphas, max_iter, tol, (double*)coefs, (double*)gaps,
+                     (int*)iters);
+  launch_check();
+}
+
+}  // namespace hfens

@@ -1,0 +1,491 @@
+// SVM training kernels (SURVEY.md §2.3 K4 rbf_kernel_tile, K5 smo_step, K6 platt_fit).
+//
+// One stacking fit of the reference SVC is 36 dual QPs (6 SVC fits × (5 Platt CV folds + the
+// final solve)); they are independent, so they run as ONE batched launch with one workgroup
+// per problem.
+//
+//  gram_rbf_batch : K_p[a][b] = exp(-γ_p‖z_a − z_b‖²) for every problem p, rows in the
+//                   problem's own (libsvm class-grouped) order so SMO row reads are contiguous.
+//                   f32-input MFMA (v_mfma_f32_32x32x2_f32) for the dot products, 64×64 tile
+//                   per 256-thread workgroup, diagonal forced to exactly 1 (libsvm's QD).
+//  smo_batch      : libsvm Solver::Solve for C-SVC with second-order working-set selection
+//                   (WSS3, Fan-Chen-Lin 2005) and libsvm's tie rules (last index wins), no
+//                   shrinking.  1024 threads per problem; each thread keeps the gradient G (f64)
+//                   of its strided elements in registers (KMAX per thread); α lives in global
+//                   memory and only its owner thread touches it; two block arg-reductions and
+//                   two contiguous Gram-row reads per iteration.  Ends with calculate_rho.
+//  platt_batch    : sigmoid_train (Lin-Lin-Weng 2007 Newton + backtracking), one workgroup
+//                   per SVC fit.
+#include "common.h"
+
+namespace hfens {
+
+// ------------------------------------------------------------------------------------------
+// Gram matrices
+struct GramProb {
+  long long zoff;   // first row of this problem in Z (rows of F floats)
+  long long koff;   // offset of K_p in the output (floats)
+  int l;            // rows
+  int ld;           // leading dimension of K_p
+  float ngl2e;      // −γ·log2(e)
+  int pad;
+};
+
+template <int KS>
+__global__ __launch_bounds__(256) void gram_rbf_kernel(const float* __restrict__ Z, int F,
+                                                       const GramProb* __restrict__ probs,
+                                                       float* __restrict__ K) {
+  const GramProb P = probs[blockIdx.z];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  if (r0 >= P.l || c0 >= P.l) return;
+  __shared__ float As[64][2 * KS + 1];
+  __shared__ float Bs[64][2 * KS + 1];
+  __shared__ float na[64], nb[64];
+  const float* Zp = Z + P.zoff * F;
+  for (int e = threadIdx.x; e < 64 * 2 * KS; e += 256) {
+    const int r = e / (2 * KS), k = e % (2 * KS);
+    As[r][k] = (r0 + r < P.l && k < F) ? Zp[(size_t)(r0 + r) * F + k] : 0.f;
+    Bs[r][k] = (c0 + r < P.l && k < F) ? Zp[(size_t)(c0 + r) * F + k] : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int r = threadIdx.x & 63;
+    const float(*T)[2 * KS + 1] = threadIdx.x < 64 ? As : Bs;
+    float s = 0.f;
+    for (int k = 0; k < 2 * KS; ++k) s = fmaf(T[r][k], T[r][k], s);
+    (threadIdx.x < 64 ? na : nb)[r] = s;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  const int r32 = lane & 31, hi = lane >> 5;
+  f32x16 acc = {0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float a = As[wr + r32][2 * s + hi];
+    const float b = Bs[wc + r32][2 * s + hi];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+  }
+  float* Kp = K + P.koff;
+  const int col = c0 + wc + r32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ri = wr + (r & 3) + 8 * (r >> 2) + 4 * hi;
+    const int row = r0 + ri;
+    if (row < P.l && col < P.l) {
+      float d2 = fmaf(-2.f, acc[r], na[ri] + nb[wc + r32]);
+      d2 = fmaxf(d2, 0.f);
+      float v = __builtin_amdgcn_exp2f(P.ngl2e * d2);
+      if (row == col) v = 1.f;
+      Kp[(size_t)row * P.ld + col] = v;
+    }
+  }
+}
+
+void gram_rbf_batch(uintptr_t Z, int F, uintptr_t probs, int P, int max_l, uintptr_t K,
+                    uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64, "gram_rbf_batch: 1 <= F <= 64");
+  const int t = (max_l + 63) / 64;
+  dim3 grid(t, t, P);
+  const int ks = (F + 1) / 2;
+  auto zp = (const float*)Z;
+  auto pp = (const GramProb*)probs;
+  auto kp = (float*)K;
+  hipStream_t st = as_stream(stream);
+#define GRAM_CASE(KS_)                                                                   \
+  if (ks <= KS_) {                                                                       \
+    hipLaunchKernelGGL(gram_rbf_kernel<KS_>, grid, dim3(256), 0, st, zp, F, pp, kp);      \
+    launch_check();                                                                      \
+    return;                                                                              \
+  }
+  GRAM_CASE(4) GRAM_CASE(8) GRAM_CASE(12) GRAM_CASE(16) GRAM_CASE(24) GRAM_CASE(32)
+#undef GRAM_CASE
+}
+
+// ------------------------------------------------------------------------------------------
+// SMO
+struct SmoProb {
+  long long koff;   // K_p offset (floats)
+  long long aoff;   // alpha offset (doubles)
+  int l;            // problem size
+  int ld;           // K_p leading dimension
+  int npos;         // indices [0, npos) have y = +1, the rest y = −1
+  int pad;
+  double Cp, Cn;    // box constraints for y = +1 / y = −1
+};
+
+struct SmoOut {
+  double* rho;      // [P]
+  int* iters;       // [P]
+  double* gap;      // [P]  final Gmax + Gmax2
+};
+
+constexpr int kSmoThreads = 1024;
+constexpr int kSmoWaves = kSmoThreads / 64;
+constexpr double kTau = 1e-12;
+constexpr double kInf = 1.0e300;
+
+// block arg-max of v (ties → larger index); all threads receive the result
+__device__ __forceinline__ void block_argmax_last(double& v, int& idx, double* sv, int* si) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, kWave);
+    const int oi = __shfl_xor(idx, o, kWave);
+    if (ov > v || (ov == v && oi > idx)) { v = ov; idx = oi; }
+  }
+  if (lane == 0) { sv[wave] = v; si[wave] = idx; }
+  __syncthreads();
+  if (wave == 0) {
+    v = lane < kSmoWaves ? sv[lane] : -kInf;
+    idx = lane < kSmoWaves ? si[lane] : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o, kWave);
+      const int oi = __shfl_xor(idx, o, kWave);
+      if (ov > v || (ov == v && oi > idx)) { v = ov; idx = oi; }
+    }
+    if (lane == 0) { sv[kSmoWaves] = v; si[kSmoWaves] = idx; }
+  }
+  __syncthreads();
+  v = sv[kSmoWaves];
+  idx = si[kSmoWaves];
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restrict__ probs,
+                                                          const float* __restrict__ K,
+                                                          double* __restrict__ alpha_all,
+                                                          double eps, long long max_iter,
+                                                          SmoOut out) {
+  const SmoProb P = probs[blockIdx.x];
+  const float* Kp = K + P.koff;
+  double* alpha = alpha_all + P.aoff;
+  const int tid = threadIdx.x;
+  __shared__ double sv[kSmoWaves + 1];
+  __shared__ int si[kSmoWaves + 1];
+  __shared__ double sv2[kSmoWaves + 1];
+  __shared__ int si2[kSmoWaves + 1];
+  __shared__ double pub[4];  // alpha_i, alpha_j, Q_ij (K_ij), unused
+
+  double G[KMAX];
+  float Qi[KMAX];
+  // α status, 2 bits per element (0 lower, 1 free, 2 upper), packed to save VGPRs
+  constexpr int NST = (KMAX + 15) / 16;
+  unsigned int stp[NST];
+#pragma unroll
+  for (int q = 0; q < NST; ++q) stp[q] = 0u;
+#define ST_GET(k) ((stp[(k) >> 4] >> (((k) & 15) * 2)) & 3u)
+#define ST_SET(k, v) (stp[(k) >> 4] = (stp[(k) >> 4] & ~(3u << (((k) & 15) * 2))) | ((unsigned)(v) << (((k) & 15) * 2)))
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int t = tid + k * kSmoThreads;
+    G[k] = -1.0;  // p_i = −1 for C-SVC
+    Qi[k] = 0.f;
+    if (t < P.l) alpha[t] = 0.0;
+  }
+  long long iter = 0;
+  double last_gap = 0.0;
+  for (; iter < max_iter; ++iter) {
+    // ---- WSS step 1: i = argmax_{t ∈ I_up} −y_t G_t
+    double bv = -kInf;
+    int bi = -1;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int t = tid + k * kSmoThreads;
+      if (t < P.l) {
+        const bool pos = t < P.npos;
+        const bool up = pos ? ST_GET(k) != 2u : ST_GET(k) != 0u;
+        const double v = pos ? -G[k] : G[k];
+        if (up && (v > bv || (v == bv && t > bi))) { bv = v; bi = t; }
+      }
+    }
+    block_argmax_last(bv, bi, sv, si);
+    const double Gmax = bv;
+    const int i = bi;
+    if (i < 0) break;
+    const int yi = i < P.npos ? 1 : -1;
+    // ---- WSS step 2
+    const float* Ki = Kp + (size_t)i * P.ld;
+    double gmax2 = -kInf;
+    double best = -kInf;  // maximise −obj_diff ⇔ minimise obj_diff
+    int bj = -1;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int t = tid + k * kSmoThreads;
+      if (t < P.l) {
+        const float kij = Ki[t];
+        Qi[k] = kij;
+        const bool pos = t < P.npos;
+        const bool low = pos ? ST_GET(k) != 0u : ST_GET(k) != 2u;
+        if (low) {
+          const double yG = pos ? G[k] : -G[k];
+          if (yG > gmax2) gmax2 = yG;
+          const double grad_diff = Gmax + yG;
+          if (grad_diff > 0) {
+            double quad = 2.0 - 2.0 * (double)kij;
+            if (quad <= 0) quad = kTau;
+            const double nobj = (grad_diff * grad_diff) / quad;
+            if (nobj > best || (nobj == best && t > bj)) { best = nobj; bj = t; }
+          }
+        }
+      }
+    }
+    // Gmax2 (value only) and j together: reduce Gmax2 first through sv2/si2
+    {
+      double g2 = gmax2;
+      int dummy = 0;
+      block_argmax_last(g2, dummy, sv2, si2);
+      gmax2 = g2;
+    }
+    block_argmax_last(best, bj, sv, si);
+    const int j = bj;
+    last_gap = Gmax + gmax2;
+    if (Gmax + gmax2 < eps || j < 0) break;
+    // ---- publish α_i (owner of i) and α_j, K_ij, G_j (owner of j); G_i = −y_i·Gmax exactly
+    const int oi_t = i % kSmoThreads, oj_t = j % kSmoThreads;
+    if (tid == oi_t) pub[0] = alpha[i];
+    if (tid == oj_t) {
+      pub[1] = alpha[j];
+      const int kk = j / kSmoThreads;
+      float kij = 0.f;
+      double gj = 0.0;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k == kk) { kij = Qi[k]; gj = G[k]; }
+      pub[2] = kij;
+      pub[3] = gj;
+    }
+    __syncthreads();
+    const double ai_old = pub[0], aj_old = pub[1];
+    const double Kij = pub[2];
+    const int yj = j < P.npos ? 1 : -1;
+    const double Ci = yi > 0 ? P.Cp : P.Cn, Cj = yj > 0 ? P.Cp : P.Cn;
+    const double Qij = (double)(yi * yj) * Kij;
+    double ai = ai_old, aj = aj_old;
+    const double Gi = -(double)yi * Gmax;
+    const double Gj = pub[3];
+    if (yi != yj) {
+      double quad = 2.0 + 2.0 * Qij;
+      if (quad <= 0) quad = kTau;
+      const double delta = (-Gi - Gj) / quad;
+      const double diff = ai - aj;
+      ai += delta;
+      aj += delta;
+      if (diff > 0) {
+        if (aj < 0) { aj = 0; ai = diff; }
+      } else {
+        if (ai < 0) { ai = 0; aj = -diff; }
+      }
+      if (diff > Ci - Cj) {
+        if (ai > Ci) { ai = Ci; aj = Ci - diff; }
+      } else {
+        if (aj > Cj) { aj = Cj; ai = Cj + diff; }
+      }
+    } else {
+      double quad = 2.0 - 2.0 * Qij;
+      if (quad <= 0) quad = kTau;
+      const double delta = (Gi - Gj) / quad;
+      const double sum = ai + aj;
+      ai -= delta;
+      aj += delta;
+      if (sum > Ci) {
+        if (ai > Ci) { ai = Ci; aj = sum - Ci; }
+      } else {
+        if (aj < 0) { aj = 0; ai = sum; }
+      }
+      if (sum > Cj) {
+        if (aj > Cj) { aj = Cj; ai = sum - Cj; }
+      } else {
+        if (ai < 0) { ai = 0; aj = sum; }
+      }
+    }
+    const double dai = ai - ai_old, daj = aj - aj_old;
+    // ---- gradient update with rows i (registers) and j (read now)
+    const float* Kj = Kp + (size_t)j * P.ld;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int t = tid + k * kSmoThreads;
+      if (t < P.l) {
+        const double yt = t < P.npos ? 1.0 : -1.0;
+        const double kjt = Kj[t];
+        G[k] += yt * ((double)yi * (double)Qi[k] * dai + (double)yj * kjt * daj);
+      }
+    }
+    // owners update α and status
+    if (tid == oi_t) {
+      alpha[i] = ai;
+      const int kk = i / kSmoThreads;
+      const unsigned char s = ai >= Ci ? 2 : (ai <= 0 ? 0 : 1);
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k == kk) ST_SET(k, s);
+    }
+    if (tid == oj_t) {
+      alpha[j] = aj;
+      const int kk = j / kSmoThreads;
+      const unsigned char s = aj >= Cj ? 2 : (aj <= 0 ? 0 : 1);
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k == kk) ST_SET(k, s);
+    }
+    __syncthreads();  // pub[] reuse
+  }
+  // ---- calculate_rho
+  double ub = kInf, lb = -kInf, sum_free = 0.0;
+  int nfree = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int t = tid + k * kSmoThreads;
+    if (t < P.l) {
+      const bool pos = t < P.npos;
+      const double yG = pos ? G[k] : -G[k];
+      if (ST_GET(k) == 2u) {
+        if (!pos) ub = fmin(ub, yG); else lb = fmax(lb, yG);
+      } else if (ST_GET(k) == 0u) {
+        if (pos) ub = fmin(ub, yG); else lb = fmax(lb, yG);
+      } else {
+        ++nfree;
+        sum_free += yG;
+      }
+    }
+  }
+  {
+    int dummy = 0;
+    double nub = -ub;
+    block_argmax_last(nub, dummy, sv, si);
+    ub = -nub;
+    block_argmax_last(lb, dummy, sv2, si2);
+    // sums
+    const int lane = tid & 63, wave = tid >> 6;
+    double s = sum_free;
+    double c = (double)nfree;
+    s = wave_sum(s);
+    c = wave_sum(c);
+    __syncthreads();
+    if (lane == 0) { sv[wave] = s; sv2[wave] = c; }
+    __syncthreads();
+    if (tid == 0) {
+      double S = 0, Cc = 0;
+      for (int w = 0; w < kSmoWaves; ++w) { S += sv[w]; Cc += sv2[w]; }
+      const double r = Cc > 0 ? S / Cc : (ub + lb) / 2;
+      out.rho[blockIdx.x] = r;
+      out.iters[blockIdx.x] = (int)iter;
+      out.gap[blockIdx.x] = last_gap;
+    }
+  }
+#undef ST_GET
+#undef ST_SET
+}
+
+void smo_batch(uintptr_t probs, int P, int max_l, uintptr_t K, uintptr_t alpha, double eps,
+               long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t stream) {
+  SmoOut o{(double*)rho, (int*)iters, (double*)gap};
+  auto pp = (const SmoProb*)probs;
+  auto kp = (const float*)K;
+  auto ap = (double*)alpha;
+  hipStream_t st = as_stream(stream);
+#define SMO_CASE(KM)                                                                        \
+  if (max_l <= KM * kSmoThreads) {                                                          \
+    hipLaunchKernelGGL(smo_kernel<KM>, dim3(P), dim3(kSmoThreads), 0, st, pp, kp, ap, eps,  \
+                       max_iter, o);                                                        \
+    launch_check();                                                                         \
+    return;                                                                                 \
+  }
+  SMO_CASE(1) SMO_CASE(2) SMO_CASE(4) SMO_CASE(8) SMO_CASE(16) SMO_CASE(32)
+#undef SMO_CASE
+  throw std::invalid_argument("smo_batch: problem larger than 32768 points on the register path");
+}
+
+// ------------------------------------------------------------------------------------------
+// Platt scaling: sigmoid_train on decision values (one workgroup per fit).
+struct PlattProb {
+  long long off;  // offset into dec / labels
+  int l;
+  int pad;
+};
+
+__device__ double block_sum256(double v, double* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(256) void platt_kernel(const PlattProb* __restrict__ probs,
+                                                    const double* __restrict__ dec,
+                                                    const float* __restrict__ labels,
+                                                    double* __restrict__ AB) {
+  const PlattProb P = probs[blockIdx.x];
+  const double* d = dec + P.off;
+  const float* y = labels + P.off;
+  __shared__ double sh[4];
+  double p1 = 0, p0 = 0;
+  for (int i = threadIdx.x; i < P.l; i += 256) {
+    if (y[i] > 0) p1 += 1; else p0 += 1;
+  }
+  const double prior1 = block_sum256(p1, sh);
+  const double prior0 = block_sum256(p0, sh);
+  const int max_iter = 100;
+  const double min_step = 1e-10, sigma = 1e-12, eps = 1e-5;
+  const double hiT = (prior1 + 1.0) / (prior1 + 2.0), loT = 1 / (prior0 + 2.0);
+  double A = 0.0, B = log((prior0 + 1.0) / (prior1 + 1.0));
+  auto fobj = [&](double a, double b) {
+    double f = 0;
+    for (int i = threadIdx.x; i < P.l; i += 256) {
+      const double t = y[i] > 0 ? hiT : loT;
+      const double fApB = d[i] * a + b;
+      f += fApB >= 0 ? t * fApB + log(1 + exp(-fApB)) : (t - 1) * fApB + log(1 + exp(fApB));
+    }
+    return block_sum256(f, sh);
+  };
+  double fval = fobj(A, B);
+  for (int it = 0; it < max_iter; ++it) {
+    double h11 = 0, h22 = 0, h21 = 0, g1 = 0, g2 = 0;
+    for (int i = threadIdx.x; i < P.l; i += 256) {
+      const double t = y[i] > 0 ? hiT : loT;
+      const double fApB = d[i] * A + B;
+      double p, q;
+      if (fApB >= 0) { p = exp(-fApB) / (1.0 + exp(-fApB)); q = 1.0 / (1.0 + exp(-fApB)); }
+      else { p = 1.0 / (1.0 + exp(fApB)); q = exp(fApB) / (1.0 + exp(fApB)); }
+      const double d2 = p * q;
+      h11 += d[i] * d[i] * d2;
+      h22 += d2;
+      h21 += d[i] * d2;
+      const double d1 = t - p;
+      g1 += d[i] * d1;
+      g2 += d1;
+    }
+    h11 = block_sum256(h11, sh) + sigma;
+    h22 = block_sum256(h22, sh) + sigma;
+    h21 = block_sum256(h21, sh);
+    g1 = block_sum256(g1, sh);
+    g2 = block_sum256(g2, sh);
+    if (fabs(g1) < eps && fabs(g2) < eps) break;
+    const double det = h11 * h22 - h21 * h21;
+    const double dA = -(h22 * g1 - h21 * g2) / det;
+    const double dB = -(-h21 * g1 + h11 * g2) / det;
+    const double gd = g1 * dA + g2 * dB;
+    double step = 1;
+    while (step >= min_step) {
+      const double nA = A + step * dA, nB = B + step * dB;
+      const double nf = fobj(nA, nB);
+      if (nf < fval + 0.0001 * step * gd) { A = nA; B = nB; fval = nf; break; }
+      step = step / 2.0;
+    }
+    if (step < min_step) break;
+  }
+  if (threadIdx.x == 0) { AB[2 * blockIdx.x] = A; AB[2 * blockIdx.x + 1] = B; }
+}
+
+void platt_batch(uintptr_t probs, int P, uintptr_t dec, uintptr_t labels, uintptr_t AB,
+                 uintptr_t stream) {
+  hipLaunchKernelGGL(platt_kernel, dim3(P), dim3(256), 0, as_stream(stream),
+                     (const PlattProb*)probs, (const double*)dec, (const float*)labels,
+                     (double*)AB);
+  launch_check();
+}
+
+}  // namespace hfens
