@@ -1,0 +1,127 @@
+"""Headline benchmark: training rows/s (+ held-out AUROC) of the HF-progression
+stacking ensemble (BASELINE.json metric; BASELINE.md config 2 shape: synthetic
+Table-S1 cohort, 40 candidate features, 10,000 development rows per GPU).
+
+One *step* = the complete development fit of the reference pipeline
+(``train_ensemble_public.py:37-61``): KNN imputation of the development rows,
+LassoCV(10-fold, 100 alphas) + top-17 SelectFromModel, and the stacking fit —
+SVC (Platt, 36 SMO problems), GBC (100 stumps) and L1-LR, each as 5 OOF folds +
+refit, then the L2 meta-learner.  Nothing is skipped or cached inside the timed
+region.  The held-out AUROC (independent synthetic draw, imputed with the fitted
+imputer) is computed after timing.
+
+Multi-GPU (``torchrun --nproc-per-node N``): weak scaling — every rank owns
+``--rows`` development rows, the job trains ONE ensemble on all ``N·rows`` rows
+(KNN donors and LassoCV moments reduced over ranks, GBDT histograms / LR
+gradients all-reduced over RCCL, the 6 SVC fits task-parallel over ranks).
+``value`` = total development rows × steps ÷ slowest rank's time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--features F]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CPU_BASELINE_ROWS_PER_S = 305.0   # sklearn pipeline, 10k x 40, 8-vCPU Xeon
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=10000, help="development rows per GPU")
+    ap.add_argument("--features", type=int, default=40)
+    ap.add_argument("--seed", type=int, default=2020)
+    ap.add_argument("--timings", action="store_true", help="print a per-stage table to stderr")
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from hfens.parallel import dist as pdist
+    from hfens.io.synth import make_hf_cohort
+    from hfens.pipeline import develop
+    from hfens.utils.timing import StageTimer
+    from hfens.utils import metrics
+    from hfens import ops
+
+    group, rank, world = pdist.init_from_env()
+    if world != a.gpus:
+        if rank == 0:
+            print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", pdist.local_rank()) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+        ops.ext()  # the HIP extension must be there; no silent fallback
+    # weak scaling: each rank draws its own shard of one synthetic cohort
+    Xd, yd, names = make_hf_cohort(a.rows, a.features, seed=a.seed * 1000 + rank, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(a.rows, a.features, seed=a.seed * 1000 + 500 + rank, nan_frac=0.02)
+    Xd_t = torch.as_tensor(Xd, device=dev)
+    yd_t = torch.as_tensor(yd, device=dev)
+    Xs_t = torch.as_tensor(Xs, device=dev)
+    ys_t = torch.as_tensor(ys, device=dev)
+
+    def step(evaluate=False, timer=None):
+        return develop(Xd_t, yd_t, Xs_t, ys_t, names, device=dev, group=group, evaluate=evaluate,
+                       timer=timer or StageTimer(enabled=False))
+
+    def barrier():
+        if group is not None:
+            torch.distributed.barrier(group)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if group is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
+        elapsed = float(t)
+    n_total = res.n_train
+    # untimed: per-stage profile + held-out AUROC of a final fit
+    prof = StageTimer(enabled=True, device=dev if dev.type == "cuda" else None)
+    final = step(evaluate=True, timer=prof)
+    value = n_total * a.steps / elapsed
+    if rank == 0:
+        if a.timings:
+            print(prof.table(), file=sys.stderr)
+        out = {
+            "metric": "train_rows_per_sec",
+            "value": round(value, 2),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / CPU_BASELINE_ROWS_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (Table S1-shaped HCM cohort, 2% NaN, random-init models)",
+            "auroc": round(final.scores["auroc"], 4),
+            "average_precision": round(final.scores["average_precision"], 4),
+            "config": {"model": "HF-progression stack: KNN-impute + LassoCV top-17 + "
+                                "Stacking{Scaler+SVC(rbf,Platt), GBC(100 stumps), LR-L1} -> LR-L2",
+                       "global_batch": n_total, "seq_len": a.features, "rows_per_gpu": a.rows,
+                       "features": a.features, "parallelism": f"dp{world}",
+                       "stage_seconds": {k: round(v, 4) for k, v in prof.times.items()}},
+        }
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,94 @@
+"""Model development entry point (reference ``train_ensemble_public.py``).
+
+No-argument behaviour follows the reference: load ``develop_data.mat`` and
+``model_select_data.mat`` next to the script (``T:34-40``), print the selected
+feature names and count (``T:56-59``), fit the stack, print the held-out
+``classification_report`` at ``> 0.5`` (``T:62-64``) and draw ROC/PR with Wald
+bands (``T:66-90``; saved as PNGs instead of ``plt.show()``).  Those ``.mat``
+files are private, so when they are absent a Table-S1-shaped synthetic cohort is
+generated (``--rows``, ``--features``).  Extras: ``--device cuda``, ``--save-model``
+(writes the sklearn-0.23.2 ``.pkl`` layout that ``predict_hf.py`` reads),
+``--timings``; under ``torchrun`` the development rows are sharded over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="train the HF-progression stacking ensemble")
+    ap.add_argument("--data-dir", default=None, help="directory with develop_data.mat / model_select_data.mat")
+    ap.add_argument("--rows", type=int, default=713, help="synthetic rows per set (when no .mat files)")
+    ap.add_argument("--features", type=int, default=64, help="synthetic candidate features")
+    ap.add_argument("--seed", type=int, default=2020)
+    ap.add_argument("--device", default=None, help="cpu | cuda (default: cuda if available)")
+    ap.add_argument("--save-model", default=None, help="write a 0.23.2-layout hf_predict_model.pkl")
+    ap.add_argument("--plots", default=None, help="PNG prefix for ROC/PR plots")
+    ap.add_argument("--timings", action="store_true")
+    ap.add_argument("--json", default=None, help="append a JSON result line to this file")
+    a = ap.parse_args(argv)
+
+    import torch
+    from ..io.mat import load_data, names_list
+    from ..io.synth import make_dev_select
+    from ..pipeline import develop
+    from ..utils import metrics
+    from ..parallel import dist as pdist
+
+    group, rank, world = pdist.init_from_env()
+    device = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    if device == "cuda":
+        device = f"cuda:{pdist.local_rank()}"
+        torch.cuda.set_device(torch.device(device))
+    data_dir = a.data_dir or os.getcwd()
+    dev_path = os.path.join(data_dir, "develop_data.mat")
+    sel_path = os.path.join(data_dir, "model_select_data.mat")
+    if os.path.exists(dev_path) and os.path.exists(sel_path):
+        X_dev, y_dev, names = load_data(dev_path)
+        X_sel, y_sel, _ = load_data(sel_path)
+        names = names_list(names)
+        source = "mat"
+    else:
+        X_dev, y_dev, X_sel, y_sel, names = make_dev_select(a.rows, a.features, seed=a.seed)
+        source = "synthetic"
+        if rank == 0:
+            print(f"[hfens] {dev_path} not found: using a synthetic Table-S1 cohort "
+                  f"({a.rows} rows x {a.features} features per set)")
+    if group is not None:
+        X_dev, y_dev = pdist.shard_rows(X_dev, rank, world), pdist.shard_rows(y_dev, rank, world)
+        X_sel, y_sel = pdist.shard_rows(X_sel, rank, world), pdist.shard_rows(y_sel, rank, world)
+    res = develop(X_dev, y_dev, X_sel, y_sel, names, device=device, group=group)
+    if rank == 0:
+        print("Important Features")
+        print(np.array(res.selected_names, dtype=object))
+        print("number of features = ", len(res.selected_names))
+        print(res.report)
+        print(f"AUROC = {res.scores['auroc']:.4f}   AP = {res.scores['average_precision']:.4f}")
+        if a.timings:
+            print(res.timer.table())
+        if a.plots:
+            p_all = res.proba_sel if group is None else pdist.all_gather_rows(res.proba_sel[:, None], group)[:, 0]
+            y_all = torch.as_tensor(y_sel) if group is None else pdist.all_gather_rows(
+                torch.as_tensor(y_sel, device=p_all.device)[:, None], group)[:, 0]
+            print("plots:", metrics.save_plots(y_all, p_all, a.plots))
+        if a.save_model:
+            from ..io.checkpoint import save_checkpoint
+            model = res.model
+            model.to("cpu")
+            save_checkpoint(model, a.save_model)
+            print(f"saved {a.save_model}")
+        if a.json:
+            with open(a.json, "a") as f:
+                f.write(json.dumps({"source": source, "n_train": res.n_train, "scores": res.scores,
+                                    "timings": dict(res.timer.times), "world_size": world}) + "\n")
+    pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

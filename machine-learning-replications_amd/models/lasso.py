@@ -1,0 +1,190 @@
+"""LassoCV + SelectFromModel feature selection (reference
+``train_ensemble_public.py:51-55``: ``LassoCV(random_state=2020, cv=10)`` inside
+``SelectFromModel(threshold=-inf, max_features=17)``).
+
+Semantics (sklearn ``linear_model/_coordinate_descent.py``): a 100-alpha
+geometric grid from ``max|Xcᵀyc|/n`` down to ``1e-3×`` that, 10 unshuffled KFold
+folds, per fold a warm-started cyclic coordinate-descent path on the fold's
+centred Gram matrix with the duality-gap stop (``tol·‖y‖²``), test MSE per alpha,
+best alpha = argmin of the fold-mean MSE, refit on all rows at that alpha.
+All 10 paths (+ the refit) run in the ``lasso_cd_path`` kernel, one wave per
+fold; the Gram matrices come from one batched GEMM.  With a process group the
+per-fold Gram / Xᵀy / yᵀy / row counts are all-reduced (rows sharded).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .base import Estimator, as_tensor
+from .model_selection import kfold_test_folds
+
+
+def _cd_path_host(G, q, yy, n, alphas, max_iter, tol):
+    """numpy mirror of the lasso_cd_path kernel (one problem)."""
+    F = G.shape[0]
+    w = np.zeros(F)
+    H = np.zeros(F)
+    out = np.zeros((len(alphas), F))
+    tol_s = tol * yy
+    for a, alpha in enumerate(alphas):
+        l1 = alpha * n
+        for it in range(max_iter):
+            w_max = d_w_max = 0.0
+            for k in range(F):
+                gkk = G[k, k]
+                if gkk == 0.0:
+                    continue
+                tmp = q[k] - H[k] + gkk * w[k]
+                nw = np.sign(tmp) * (abs(tmp) - l1) / gkk if abs(tmp) > l1 else 0.0
+                dw = nw - w[k]
+                if dw != 0.0:
+                    H += G[:, k] * dw
+                    w[k] = nw
+                d_w_max = max(d_w_max, abs(dw))
+                w_max = max(w_max, abs(nw))
+            if w_max == 0.0 or d_w_max / w_max < tol or it == max_iter - 1:
+                wq = w @ q
+                dual = np.abs(q - H).max()
+                R2 = yy - 2 * wq + w @ H
+                const = 1.0
+                gp = R2
+                if dual > l1:
+                    const = l1 / dual
+                    gp = 0.5 * (R2 + R2 * const * const)
+                gap = gp + l1 * np.abs(w).sum() - const * (yy - wq)
+                if gap < tol_s:
+                    break
+        out[a] = w
+    return out
+
+
+class LassoCV(Estimator):
+    _param_names = ("eps", "n_alphas", "alphas", "fit_intercept", "max_iter", "tol", "cv", "random_state",
+                    "selection")
+
+    def __init__(self, eps=1e-3, n_alphas=100, alphas=None, fit_intercept=True, max_iter=1000, tol=1e-4,
+                 cv=None, random_state=None, selection="cyclic"):
+        self.eps = eps
+        self.n_alphas = n_alphas
+        self.alphas = alphas
+        self.fit_intercept = fit_intercept
+        self.max_iter = max_iter
+        self.tol = tol
+        self.cv = cv
+        self.random_state = random_state
+        self.selection = selection
+
+    def _solve(self, Gs, qs, yys, ns, alpha_grid):
+        """Run P coordinate-descent paths; Gs [P,F,F], qs [P,F], alpha_grid [P,A]."""
+        P, F = qs.shape
+        A = alpha_grid.shape[1]
+        if Gs.is_cuda and F <= 64:
+            from .. import ops
+            E = ops.ext()
+            coefs = torch.empty(P, A, F, dtype=torch.float64, device=Gs.device)
+            gaps = torch.empty(P, A, dtype=torch.float64, device=Gs.device)
+            iters = torch.empty(P, A, dtype=torch.int32, device=Gs.device)
+            E.lasso_cd_path(P, F, A, Gs.contiguous().data_ptr(), qs.contiguous().data_ptr(),
+                            yys.contiguous().data_ptr(), ns.contiguous().data_ptr(),
+                            alpha_grid.contiguous().data_ptr(), int(self.max_iter), float(self.tol),
+                            coefs.data_ptr(), gaps.data_ptr(), iters.data_ptr(), ops.stream_ptr(Gs.device))
+            return coefs
+        out = [torch.as_tensor(_cd_path_host(Gs[p].cpu().numpy(), qs[p].cpu().numpy(), float(yys[p]),
+                                             float(ns[p]), alpha_grid[p].cpu().numpy(), int(self.max_iter),
+                                             float(self.tol))) for p in range(P)]
+        return torch.stack(out).to(Gs.device)
+
+    def fit(self, X, y, group=None):
+        X = as_tensor(X)
+        y = as_tensor(y, device=X.device)
+        n, F = X.shape
+        dev = X.device
+        k = 5 if self.cv is None else int(self.cv)
+        if group is None:
+            tf = torch.as_tensor(kfold_test_folds(n, k), device=dev)
+        else:
+            from ..parallel import dist as pdist
+            tf = pdist.sharded_kfold_test_folds(n, k, group, dev)
+        # per-fold training moments (rows in fold f are excluded from problem f) + full data
+        masks = torch.stack([tf != f for f in range(k)] + [torch.ones(n, dtype=torch.bool, device=dev)])
+        mk = masks.to(torch.float64)                         # [P, n]
+        cnt = mk.sum(1)
+        sx = mk @ X
+        sy = mk @ y
+        Sxx = torch.einsum("pn,ni,nj->pij", mk, X, X)
+        Sxy = torch.einsum("pn,ni,n->pi", mk, X, y)
+        Syy = mk @ (y * y)
+        if group is not None:
+            from ..parallel import dist as pdist
+            cnt, sx, sy, Sxx, Sxy, Syy = pdist.all_reduce_sum_f64([cnt, sx, sy, Sxx, Sxy, Syy], group)
+        mx = sx / cnt[:, None]
+        my = sy / cnt
+        G = Sxx - cnt[:, None, None] * mx[:, :, None] * mx[:, None, :]
+        q = Sxy - cnt[:, None] * mx * my[:, None]
+        yy = Syy - cnt * my * my
+        # alpha grid on all rows (problem k = full data)
+        if self.alphas is None:
+            amax = float(q[k].abs().max()) / float(cnt[k])
+            if amax <= np.finfo(np.float64).resolution:
+                grid = torch.full((self.n_alphas,), np.finfo(np.float64).resolution, dtype=torch.float64)
+            else:
+                grid = torch.as_tensor(np.geomspace(amax, amax * self.eps, num=self.n_alphas))
+        else:
+            grid = torch.as_tensor(np.sort(np.asarray(self.alphas, dtype=np.float64))[::-1].copy())
+        grid = grid.to(dev)
+        coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+        # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
+        inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
+        # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
+        # already globally reduced, so no per-row pass and no [k, A, n] intermediate.
+        Txx, Tx, Txy = Sxx[k] - Sxx[:k], sx[k] - sx[:k], Sxy[k] - Sxy[:k]
+        Ty, Tyy, nt = sy[k] - sy[:k], Syy[k] - Syy[:k], cnt[k] - cnt[:k]
+        c = inter
+        se = (torch.einsum("paf,pfg,pag->pa", coefs, Txx, coefs)
+              + 2 * c * torch.einsum("pf,paf->pa", Tx, coefs) - 2 * torch.einsum("pf,paf->pa", Txy, coefs)
+              + nt[:, None] * c * c - 2 * c * Ty[:, None] + Tyy[:, None])
+        mse = se / nt[:, None]                                                          # [k, A]
+        mean_mse = mse.mean(0)
+        best = int(torch.argmin(mean_mse))
+        self.alpha_ = float(grid[best])
+        self.alphas_ = grid
+        self.mse_path_ = mse.t()
+        final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
+        w = final[0, 0]
+        self.coef_ = w
+        self.intercept_ = my[k] - mx[k] @ w
+        self.n_features_in_ = F
+        return self
+
+
+class SelectFromModel(Estimator):
+    """``SelectFromModel(estimator, threshold=-inf, max_features=k)``: keep the k
+    largest |coef| (stable order), in original column order."""
+    _param_names = ("estimator", "threshold", "max_features")
+
+    def __init__(self, estimator, threshold=None, max_features=None):
+        self.estimator = estimator
+        self.threshold = threshold
+        self.max_features = max_features
+
+    def fit(self, X, y, group=None):
+        self.estimator_ = self.estimator.fit(X, y, group=group)
+        scores = self.estimator_.coef_.abs().cpu().numpy()
+        F = scores.size
+        mask = np.ones(F, dtype=bool)
+        if self.threshold is not None and not (isinstance(self.threshold, float) and np.isneginf(self.threshold)):
+            thr = float(np.mean(scores)) if self.threshold == "mean" else float(self.threshold)
+            mask &= scores >= thr
+        if self.max_features is not None:
+            keep = np.zeros(F, dtype=bool)
+            keep[np.argsort(-scores, kind="mergesort")[: int(self.max_features)]] = True
+            mask &= keep
+        self.support_ = mask
+        return self
+
+    def get_support(self) -> np.ndarray:
+        return self.support_
+
+    def transform(self, X):
+        return X[:, torch.as_tensor(self.support_, device=X.device)]

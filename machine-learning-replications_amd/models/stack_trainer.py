@@ -1,0 +1,110 @@
+"""StackingClassifier.fit as batched device work (reference ``train_ensemble_public.py:61``;
+sklearn ``ensemble/_stacking.py`` semantics).
+
+Fit plan for the reference stack (3 base models × (5 OOF folds + full refit)):
+
+1. StratifiedKFold(5) test folds (sklearn assignment) → 6 training masks.
+2. svc pipeline: 6 StandardScaler fits (masked column moments) → 6 scaled training
+   matrices → ONE ``fit_svc_batch`` (36 SMO problems in one launch).
+3. gbc: ONE ``fit_gbdt_batch`` over the 6 masks (shared binned matrix).
+4. lg: ONE ``fit_logreg_batch`` over the 6 masks.
+5. OOF ``predict_proba[:, 1]`` of the 5 fold models on their test rows → meta features
+   (svc, gbc, lg order) → final LR(L2, balanced).
+
+With a process group: rows are sharded; GBDT / LR / scaler moments reduce across
+ranks, the 36 SVM problems are split across ranks (task parallel) and the OOF
+meta-features all-gathered (:mod:`hfens.parallel.stack`).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..utils.timing import StageTimer
+from .gbdt import GradientBoostingClassifier
+from .hist_gbdt import fit_gbdt_batch
+from .linear import LogisticRegression
+from .logreg_solver import fit_logreg_batch
+from .model_selection import fold_masks, stratified_kfold_test_folds
+from .scaler import StandardScaler
+from .smo import fit_svc_batch
+from .stacking import Pipeline
+from .svc import SVC
+
+N_FOLDS = 5
+
+
+def _kind(est):
+    if isinstance(est, Pipeline):
+        if not (isinstance(est.steps[0][1], StandardScaler) and isinstance(est.steps[-1][1], SVC)
+                and len(est.steps) == 2):
+            raise NotImplementedError("pipeline must be StandardScaler → SVC")
+        return "svc"
+    if isinstance(est, SVC):
+        return "svc_raw"
+    if isinstance(est, GradientBoostingClassifier):
+        return "gbc"
+    if isinstance(est, LogisticRegression):
+        return "lr"
+    raise NotImplementedError(f"unsupported base estimator {type(est).__name__}")
+
+
+def fit_base_batch(est, X, y, masks, group=None, timer=None):
+    """Fit ``masks.shape[0]`` clones of ``est`` on the masked row subsets; returns them."""
+    kind = _kind(est)
+    B = masks.shape[0]
+    clones = [est.clone() for _ in range(B)]
+    if kind in ("svc", "svc_raw"):
+        Zs, ys = [], []
+        for c, m in zip(clones, masks):
+            rows = torch.nonzero(m).squeeze(1)
+            Xm = X[rows]
+            if kind == "svc":
+                sc = c.steps[0][1]
+                sc.fit(Xm)
+                Zs.append(sc.transform(Xm))
+            else:
+                Zs.append(Xm)
+            ys.append(y[rows])
+        svcs = [c.steps[-1][1] if kind == "svc" else c for c in clones]
+        if group is None:
+            fit_svc_batch(svcs, Zs, ys)
+        else:
+            from ..parallel.stack import fit_svc_batch_distributed
+            fit_svc_batch_distributed(svcs, Zs, ys, group)
+    elif kind == "gbc":
+        fit_gbdt_batch(clones, X, y, masks, group=group)
+    else:
+        fit_logreg_batch(clones, X, y, masks, group=group)
+    return clones
+
+
+def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None):
+    timer = timer or StageTimer(enabled=False)
+    dev = X.device
+    n = X.shape[0]
+    if group is None:
+        folds = torch.as_tensor(stratified_kfold_test_folds(y.cpu().numpy(), N_FOLDS), device=dev)
+    else:
+        from ..parallel import dist as pdist
+        folds = pdist.sharded_stratified_folds(y, N_FOLDS, group)
+    masks = fold_masks(folds.cpu().numpy(), N_FOLDS, device=dev)        # [6, n]
+    full, oof = [], []
+    meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
+    for col, (name, est) in enumerate(clf.estimators):
+        with timer.stage(f"fit_{name}"):
+            fitted = fit_base_batch(est, X, y, masks, group=group)
+        with timer.stage(f"oof_{name}"):
+            for k in range(N_FOLDS):
+                test = folds == k
+                if bool(test.any()):
+                    meta[test, col] = fitted[k].predict_proba(X[test])[:, 1].to(torch.float64)
+        full.append(fitted[N_FOLDS])
+    with timer.stage("fit_meta"):
+        final = clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
+        fit_logreg_batch([final], meta, y.to(torch.float64), group=group)
+    clf.estimators_ = full
+    clf.final_estimator_ = final
+    clf.stack_method_ = ["predict_proba"] * len(full)
+    clf.classes_ = torch.tensor([0.0, 1.0], dtype=torch.float64)
+    clf.oof_meta_ = meta
+    return clf

@@ -27,9 +27,10 @@ __global__ __launch_bounds__(256) void rbf_decision_kernel(
   float* sn_l = lds + 2 * KS * mp;     // [mp]
   float* cf_l = sn_l + mp;             // [mp]
   const int tot = (2 * KS + 2) * mp;
+  // SVt holds only F rows (k-major): rows F .. 2·KS−1 of the LDS image are zero padding
   for (int i = threadIdx.x; i < tot; i += blockDim.x) {
     float v;
-    if (i < 2 * KS * mp) v = SVt[i];
+    if (i < 2 * KS * mp) v = (i / mp) < F ? SVt[i] : 0.f;
     else if (i < (2 * KS + 1) * mp) v = sn[i - 2 * KS * mp];
     else v = coef[i - (2 * KS + 1) * mp];
     lds[i] = v;

@@ -1,0 +1,42 @@
+"""Task-parallel SVC fits for the sharded stack (SURVEY.md §2.4 "ensemble parallel",
+call site R9).
+
+An SVM dual QP is not row-separable, so the six SVC fits of a stacking fit (5 OOF
+folds + refit, each = 6 SMO problems) are distributed over ranks instead:
+every fit's (scaled) training rows are all-gathered once, fit ``f`` is solved by
+rank ``f mod world`` with the batched SMO, and the fitted parameters are
+broadcast back so every rank holds the full model.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.smo import fit_svc_batch
+from . import dist as pdist
+
+
+def fit_svc_batch_distributed(svcs, Zs, ys, group):
+    world, rank = pdist.dist.get_world_size(group), pdist.dist.get_rank(group)
+    full_Z = [pdist.all_gather_rows(Z, group) for Z in Zs]
+    full_y = [pdist.all_gather_rows(y[:, None].to(torch.float64), group)[:, 0] for y in ys]
+    mine = [f for f in range(len(svcs)) if f % world == rank]
+    if mine:
+        fit_svc_batch([svcs[f] for f in mine], [full_Z[f] for f in mine], [full_y[f] for f in mine])
+    for f, svc in enumerate(svcs):
+        src = f % world
+        if rank == src:
+            ts = [svc.support_, svc.support_vectors_, svc._n_support, svc._dual_coef_[0],
+                  svc._intercept_, svc._probA, svc._probB, svc.class_weight_,
+                  torch.tensor([svc._gamma, float(svc.shape_fit_[0]), float(svc.shape_fit_[1])],
+                               dtype=torch.float64, device=svc.support_vectors_.device)]
+        else:
+            ts = None
+        got = pdist.broadcast_tensors(ts, src, group)
+        if rank != src:
+            sup, sv, ns, coef, ic, pa, pb, cw, misc = got
+            dev = Zs[f].device
+            svc.set_fitted(support=sup.to(dev), support_vectors=sv.to(dev), n_support=ns.to(dev),
+                           dual_coef_libsvm=coef.to(dev), rho=-float(ic[0]), probA=float(pa[0]),
+                           probB=float(pb[0]), gamma=float(misc[0]), class_weight=cw.to(dev),
+                           shape_fit=(int(misc[1]), int(misc[2])), n_features=sv.shape[1], device=dev)
+    return svcs

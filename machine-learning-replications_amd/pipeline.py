@@ -1,0 +1,85 @@
+"""End-to-end model development (reference ``train_ensemble_public.py:33-90``).
+
+``develop(X_dev, y_dev, X_sel, y_sel, names)``:
+KNN-impute (fit on dev, applied to both) → LassoCV/SelectFromModel top-17 →
+stacking fit on dev → held-out ``predict_proba`` → report / AUROC / AP (+ plots).
+Every step runs on the tensors' device; with ``group`` the dev rows are sharded
+across ranks (see :mod:`hfens.parallel`).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .config import EnsembleConfig, build_estimators, build_selector
+from .models.imputer import KNNImputer
+from .utils import metrics
+from .utils.timing import StageTimer
+
+
+@dataclass
+class DevelopResult:
+    model: object
+    selected: np.ndarray
+    selected_names: List[str]
+    proba_sel: torch.Tensor
+    report: str
+    scores: Dict[str, float]
+    timer: StageTimer
+    n_train: int = 0
+
+
+def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[EnsembleConfig] = None,
+            timer: Optional[StageTimer] = None, group=None, evaluate: bool = True) -> DevelopResult:
+    cfg = cfg or EnsembleConfig()
+    timer = timer or StageTimer(enabled=True, device=device if str(device).startswith("cuda") else None)
+    dev = torch.device(device)
+    X_dev = torch.as_tensor(np.asarray(X_dev) if not isinstance(X_dev, torch.Tensor) else X_dev,
+                            dtype=torch.float64).to(dev)
+    y_dev = torch.as_tensor(np.asarray(y_dev) if not isinstance(y_dev, torch.Tensor) else y_dev,
+                            dtype=torch.float64).to(dev)
+    X_sel = torch.as_tensor(np.asarray(X_sel) if not isinstance(X_sel, torch.Tensor) else X_sel,
+                            dtype=torch.float64).to(dev)
+    y_sel = torch.as_tensor(np.asarray(y_sel) if not isinstance(y_sel, torch.Tensor) else y_sel,
+                            dtype=torch.float64).to(dev)
+    with timer.stage("impute"):
+        if group is None:
+            imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(X_dev)
+        else:
+            from .parallel import dist as pdist
+            imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(pdist.all_gather_rows(X_dev, group))
+        X_dev = imputer.transform(X_dev)
+        X_sel = imputer.transform(X_sel)
+    with timer.stage("select"):
+        sfm = build_selector(cfg).fit(X_dev, y_dev, group=group)
+        mask = sfm.get_support()
+        mt = torch.as_tensor(mask, device=dev)
+        X_dev_optm = X_dev[:, mt]
+        X_sel_optm = X_sel[:, mt]
+        fn_new = [n for n, m in zip(names, mask) if m]
+    clf = build_estimators(cfg)
+    clf.fit(X_dev_optm, y_dev, timer=timer, group=group)
+    proba = None
+    report = ""
+    scores: Dict[str, float] = {}
+    if evaluate:
+        with timer.stage("predict_select"):
+            proba = clf.predict_proba(X_sel_optm)[:, 1]
+        yy = (proba > 0.5).to(torch.float64)
+        if group is not None:
+            from .parallel import dist as pdist
+            proba_all = pdist.all_gather_rows(proba[:, None], group)[:, 0]
+            ysel_all = pdist.all_gather_rows(y_sel[:, None], group)[:, 0]
+            yy_all = (proba_all > 0.5).to(torch.float64)
+        else:
+            proba_all, ysel_all, yy_all = proba, y_sel, yy
+        report = metrics.classification_report(ysel_all, yy_all)
+        scores = metrics.evaluate(ysel_all, proba_all)
+    n_train = X_dev.shape[0]
+    if group is not None:
+        from .parallel import dist as pdist
+        n_train = pdist.all_reduce_int(n_train, group)
+    return DevelopResult(clf, mask, fn_new, proba, report, scores, timer, n_train)

@@ -1,0 +1,67 @@
+"""End-to-end development flow vs the reference pipeline re-run with the installed
+scikit-learn (reference train_ensemble_public.py:37-64, plots omitted)."""
+import numpy as np
+import pytest
+import torch
+
+from hfens.io.synth import make_dev_select
+from hfens.pipeline import develop
+
+
+def _sklearn_reference(Xd, yd, Xs, ys):
+    from sklearn.ensemble import GradientBoostingClassifier, StackingClassifier
+    from sklearn.feature_selection import SelectFromModel
+    from sklearn.impute import KNNImputer
+    from sklearn.linear_model import LassoCV, LogisticRegression
+    from sklearn.pipeline import make_pipeline
+    from sklearn.preprocessing import StandardScaler
+    from sklearn.svm import SVC
+    from sklearn.metrics import roc_auc_score
+    np.random.seed(2020)
+    imp = KNNImputer(missing_values=np.nan, n_neighbors=1)
+    Xd = imp.fit_transform(Xd)
+    Xs = imp.transform(Xs)
+    est = [("svc", make_pipeline(StandardScaler(), SVC(class_weight="balanced", probability=True, random_state=2020))),
+           ("gbc", GradientBoostingClassifier(n_estimators=100, max_depth=1, random_state=2020)),
+           ("lg", LogisticRegression(class_weight="balanced", penalty="l1", solver="liblinear"))]
+    clf = StackingClassifier(estimators=est, final_estimator=LogisticRegression(class_weight="balanced"))
+    sfm = SelectFromModel(LassoCV(random_state=2020, cv=10), threshold=-np.inf, max_features=17).fit(Xd, yd)
+    m = sfm.get_support()
+    clf.fit(Xd[:, m], yd)
+    p = clf.predict_proba(Xs[:, m])[:, 1]
+    return m, p, roc_auc_score(ys, p)
+
+
+@pytest.mark.slow
+def test_develop_matches_sklearn_pipeline():
+    Xd, yd, Xs, ys, names = make_dev_select(713, 64, seed=2020)
+    res = develop(Xd, yd, Xs, ys, names, device="cpu")
+    m, p, auc = _sklearn_reference(Xd.copy(), yd, Xs.copy(), ys)
+    assert np.array_equal(res.selected, m)
+    ours = res.proba_sel.numpy()
+    # same selected features; stack probabilities agree to the solvers' tolerances
+    assert np.abs(ours - p).max() < 0.02
+    assert abs(res.scores["auroc"] - auc) < 0.005
+
+
+def test_classification_report_format():
+    from sklearn.metrics import classification_report as skr
+    from hfens.utils.metrics import classification_report
+    rng = np.random.default_rng(0)
+    y = (rng.random(300) < 0.2).astype(float)
+    p = rng.random(300) > 0.6
+    assert classification_report(torch.as_tensor(y), torch.as_tensor(p.astype(float))) == skr(y, p)
+
+
+def test_auc_ap_match_sklearn():
+    from sklearn.metrics import average_precision_score, roc_auc_score, roc_curve as skroc
+    from hfens.utils import metrics
+    rng = np.random.default_rng(1)
+    y = (rng.random(2000) < 0.25).astype(float)
+    s = np.round(rng.random(2000) + 0.3 * y, 2)  # ties
+    assert abs(metrics.roc_auc(torch.as_tensor(y), torch.as_tensor(s)) - roc_auc_score(y, s)) < 1e-12
+    assert abs(metrics.average_precision(torch.as_tensor(y), torch.as_tensor(s)) - average_precision_score(y, s)) < 1e-12
+    fpr, tpr, _ = metrics.roc_curve(torch.as_tensor(y), torch.as_tensor(s))
+    f2, t2, _ = skroc(y, s)
+    np.testing.assert_allclose(fpr.numpy(), f2)
+    np.testing.assert_allclose(tpr.numpy(), t2)
