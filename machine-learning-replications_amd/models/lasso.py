@@ -110,11 +110,10 @@ class LassoCV(Estimator):
         masks = torch.stack([tf != f for f in range(k)] + [torch.ones(n, dtype=torch.bool, device=dev)])
         mk = masks.to(torch.float64)                         # [P, n]
         cnt = mk.sum(1)
-        sx = mk @ X
         sy = mk @ y
-        Sxx = torch.einsum("pn,ni,nj->pij", mk, X, X)
-        Sxy = torch.einsum("pn,ni,n->pi", mk, X, y)
         Syy = mk @ (y * y)
+        from .. import ops
+        Sxx, sx, Sxy = ops.weighted_moments(X, mk, mk * y[None])   # one reduction kernel
         if group is not None:
             from ..parallel import dist as pdist
             cnt, sx, sy, Sxx, Sxy, Syy = pdist.all_reduce_sum_f64([cnt, sx, sy, Sxx, Sxy, Syy], group)

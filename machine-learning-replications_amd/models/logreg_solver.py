@@ -22,6 +22,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from .. import ops
 from .base import balanced_class_weight
 
 
@@ -124,9 +125,10 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
         M = ypm[:, None] * Z
         sig = torch.sigmoid(M)
         coef_g = s.t() * (sig - 1.0) * ypm[:, None]               # [n, B]
-        grad = C * (coef_g.t() @ Xa)                              # [B, F1]
         D = s.t() * sig * (1.0 - sig)                             # [n, B]
-        H = C * torch.einsum("ni,nb,nj->bij", Xa, D, Xa)
+        H, _, grad = ops.weighted_moments(Xa, D.t(), coef_g.t())   # X̃ᵀDX̃, X̃ᵀr in one kernel
+        H = C * H
+        grad = C * grad                                           # [B, F1]
         data0 = C * (s.t() * torch.nn.functional.softplus(-M)).sum(0)
         grad, H, data0 = _allreduce([grad, H, data0], group)
         if l1:
@@ -140,7 +142,6 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
                 break
             Hr = H + 1e-12 * torch.eye(F1, dtype=torch.float64, device=dev)
             if X.is_cuda:
-                from .. import ops
                 E = ops.ext()
                 d = torch.empty_like(W)
                 E.l1_qp_cd(B, F1, Hr.contiguous().data_ptr(), grad.contiguous().data_ptr(),

@@ -7,7 +7,7 @@ import torch
 from . import reference as ref
 from .packing import pack_forest, pack_svs
 
-__all__ = ["rbf_decision", "svc_proba1", "tree_raw", "expit", "pack_svs", "pack_forest"]
+__all__ = ["rbf_decision", "svc_proba1", "tree_raw", "expit", "pack_svs", "pack_forest", "weighted_moments"]
 
 
 def _c(t: torch.Tensor, dtype) -> torch.Tensor:
@@ -58,3 +58,31 @@ def tree_raw(x, feature, threshold, left, right, value, init: float, lr: float, 
 
 def expit(x):
     return torch.sigmoid(x)
+
+
+def weighted_moments(X, W, V=None):
+    """``G[p] = Σ_n W[p,n] x_n x_nᵀ``, ``a[p] = Σ_n W[p,n] x_n``, ``v[p] = Σ_n V[p,n] x_n`` (f64)."""
+    X = X.to(torch.float64).contiguous()
+    W = W.to(torch.float64).contiguous()
+    n, F = X.shape
+    P = W.shape[0]
+    if X.is_cuda:
+        from . import ext, stream_ptr
+        C = (n + 127) // 128
+        npairs = F * (F + 1) // 2
+        Gp = torch.empty(P, C, npairs, dtype=torch.float64, device=X.device)
+        ap = torch.empty(P, C, F, dtype=torch.float64, device=X.device)
+        vp = torch.empty(P, C, F, dtype=torch.float64, device=X.device)
+        Vc = V.to(torch.float64).contiguous() if V is not None else None
+        ext().weighted_moments(X.data_ptr(), n, F, W.data_ptr(), Vc.data_ptr() if Vc is not None else 0,
+                               P, Gp.data_ptr(), ap.data_ptr(), vp.data_ptr(), stream_ptr(X.device))
+        Gu = Gp.sum(1)
+        iu = torch.triu_indices(F, F, device=X.device)
+        G = torch.zeros(P, F, F, dtype=torch.float64, device=X.device)
+        G[:, iu[0], iu[1]] = Gu
+        G[:, iu[1], iu[0]] = Gu
+        return G, ap.sum(1), (vp.sum(1) if V is not None else None)
+    G = torch.einsum("pn,ni,nj->pij", W, X, X)
+    a = W @ X
+    v = V.to(torch.float64) @ X if V is not None else None
+    return G, a, v

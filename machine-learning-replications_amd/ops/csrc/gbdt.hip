@@ -53,6 +53,11 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63;
   long long dev_q = 0, r2_q = 0;
+  // per-node Σw r² of the previous tree: block-local LDS accumulation, one global atomic per
+  // (block, node) — a direct global atomic per row serialises on ~3 hot addresses per model
+  __shared__ long long nacc[64];
+  if (threadIdx.x < 64) nacc[threadIdx.x] = 0;
+  __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += gridDim.x * blockDim.x) {
     const size_t bi = (size_t)b * S.n + i;
     const float wi = w[bi];
@@ -68,8 +73,7 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
       if (wi > 0.f) {
         const double p0 = 1.0 / (1.0 + exp(-rw));
         const double r0 = yi - p0;
-        atomicAdd((unsigned long long*)&prev_r2[(size_t)b * S.NN + nd],
-                  (unsigned long long)q_of(wi * r0 * r0, qscale));
+        atomicAdd((unsigned long long*)&nacc[nd], (unsigned long long)q_of(wi * r0 * r0, qscale));
       }
       rw += lr * prev_value[b * S.NN + nd];
       raw[bi] = rw;
@@ -91,9 +95,13 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
   dev_q = wave_sum_i64(dev_q);
   r2_q = wave_sum_i64(r2_q);
   if (lane == 0) {
-    if (prev_feat != nullptr) atomicAdd((unsigned long long*)&dev_acc[b], (unsigned long long)dev_q);
-    atomicAdd((unsigned long long*)&cur_r2[(size_t)b * S.NN], (unsigned long long)r2_q);
+    if (prev_feat != nullptr && dev_q != 0) atomicAdd((unsigned long long*)&dev_acc[b], (unsigned long long)dev_q);
+    if (r2_q != 0) atomicAdd((unsigned long long*)&cur_r2[(size_t)b * S.NN], (unsigned long long)r2_q);
   }
+  __syncthreads();
+  if (prev_feat != nullptr && threadIdx.x < S.NN && nacc[threadIdx.x] != 0)
+    atomicAdd((unsigned long long*)&prev_r2[(size_t)b * S.NN + threadIdx.x],
+              (unsigned long long)nacc[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -332,6 +340,9 @@ __global__ __launch_bounds__(256) void gbdt_route_kernel(
     const float* __restrict__ w, int* __restrict__ node, const int* __restrict__ feat,
     const int* __restrict__ blo, long long* __restrict__ r2, int node0, int NL, double qscale) {
   const int b = blockIdx.y;
+  __shared__ long long nacc[64];
+  if (threadIdx.x < 64) nacc[threadIdx.x] = 0;
+  __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += gridDim.x * blockDim.x) {
     const size_t bi = (size_t)b * S.n + i;
     const int nd = node[bi];
@@ -343,10 +354,12 @@ __global__ __launch_bounds__(256) void gbdt_route_kernel(
     const float wi = w[bi];
     if (wi > 0.f) {
       const double r = (double)g[bi] / wi;
-      atomicAdd((unsigned long long*)&r2[(size_t)b * S.NN + child],
-                (unsigned long long)q_of(wi * r * r, qscale));
+      atomicAdd((unsigned long long*)&nacc[child], (unsigned long long)q_of(wi * r * r, qscale));
     }
   }
+  __syncthreads();
+  if (threadIdx.x < S.NN && nacc[threadIdx.x] != 0)
+    atomicAdd((unsigned long long*)&r2[(size_t)b * S.NN + threadIdx.x], (unsigned long long)nacc[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -6,7 +6,8 @@
 //                    (rows = SVs in the accumulator registers), the data rows the B operand
 //                    (columns = lanes), so the Σ over SVs is a register sum + one cross-half
 //                    shuffle and each lane ends owning one output row (coalesced store).
-//                    SVs (+ norms, coefs) are staged once per workgroup in LDS.
+//                    SVs (+ norms, coefs) stream through LDS in ≤96 KiB chunks (one chunk ⇒
+//                    staged once per workgroup).
 //  * svc_proba1    : libsvm Platt sigmoid + iterative 2-class pairwise coupling, in fp64.
 //  * forest_raw    : generic tree-ensemble walk (thresholds pre-rounded down to f32 so that
 //                    `x32 <= thr32` ≡ sklearn's `float(x32) <= thr64`).
@@ -16,88 +17,104 @@ namespace hfens {
 
 // ------------------------------------------------------------------------------------------
 // RBF decision (MFMA)
-// SVt : [2*KS][mp] (k-major), sn/coef : [mp], zero padded (coef 0 ⇒ no contribution).
+// SVt : [F'][mp] (k-major, F' >= F rows), sn/coef : [mp], zero padded (coef 0 ⇒ no contribution).
+// SVs stream through LDS in chunks of CH (multiple of 32); with one chunk they are staged once
+// per workgroup and stay resident across the grid-stride row loop.
 template <int KS>
 __global__ __launch_bounds__(256) void rbf_decision_kernel(
     const float* __restrict__ Z, int n, int F, const float* __restrict__ SVt,
-    const float* __restrict__ sn, const float* __restrict__ coef, int mp, float ngl2e,
+    const float* __restrict__ sn, const float* __restrict__ coef, int mp, int CH, float ngl2e,
     float intercept, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* sv_l = lds;                   // [2KS][mp]
-  float* sn_l = lds + 2 * KS * mp;     // [mp]
-  float* cf_l = sn_l + mp;             // [mp]
-  const int tot = (2 * KS + 2) * mp;
-  // SVt holds only F rows (k-major): rows F .. 2·KS−1 of the LDS image are zero padding
-  for (int i = threadIdx.x; i < tot; i += blockDim.x) {
-    float v;
-    if (i < 2 * KS * mp) v = (i / mp) < F ? SVt[i] : 0.f;
-    else if (i < (2 * KS + 1) * mp) v = sn[i - 2 * KS * mp];
-    else v = coef[i - (2 * KS + 1) * mp];
-    lds[i] = v;
-  }
-  __syncthreads();
-
+  float* sv_l = lds;                   // [2KS][CH]
+  float* sn_l = lds + 2 * KS * CH;     // [CH]
+  float* cf_l = sn_l + CH;             // [CH]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r32 = lane & 31;
   const int hi = lane >> 5;
   const int ntile = (n + 31) >> 5;
   const int wpb = blockDim.x >> 6;
-  for (int tile = blockIdx.x * wpb + wave; tile < ntile; tile += gridDim.x * wpb) {
+  const int nch = (mp + CH - 1) / CH;
+  int staged = -1;
+  for (int base = blockIdx.x * wpb; base < ntile; base += gridDim.x * wpb) {
+    const int tile = base + wave;
+    const bool valid = tile < ntile;
     const int row = tile * 32 + r32;
     float z[KS];
     float znp = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k = 2 * s + hi;
-      z[s] = (row < n && k < F) ? Z[(size_t)row * F + k] : 0.f;
+      z[s] = (valid && row < n && k < F) ? Z[(size_t)row * F + k] : 0.f;
       znp = fmaf(z[s], z[s], znp);
     }
     const float zn = znp + __shfl_xor(znp, 32, kWave);
     float part = 0.f;
-    for (int t = 0; t < mp; t += 32) {
-      f32x16 acc = {0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const float a = sv_l[(2 * s + hi) * mp + t + r32];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, z[s], acc, 0, 0, 0);
+    for (int c = 0; c < nch; ++c) {
+      const int c0 = c * CH;
+      const int cl = min(CH, mp - c0);
+      if (staged != c) {  // block-uniform
+        __syncthreads();
+        for (int i = threadIdx.x; i < (2 * KS + 2) * cl; i += blockDim.x) {
+          const int k = i / cl, j = i % cl;
+          float v;
+          if (k < 2 * KS) v = k < F ? SVt[(size_t)k * mp + c0 + j] : 0.f;
+          else if (k == 2 * KS) v = sn[c0 + j];
+          else v = coef[c0 + j];
+          (k < 2 * KS ? sv_l[k * CH + j] : (k == 2 * KS ? sn_l[j] : cf_l[j])) = v;
+        }
+        __syncthreads();
+        staged = c;
       }
-      // accumulator reg r ↔ SV t + (r&3) + 8*(r>>2) + 4*hi ; column (lane&31) ↔ data row
+      if (!valid) continue;
+      for (int t = 0; t < cl; t += 32) {
+        f32x16 acc = {0.f};
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int base = t + 8 * g + 4 * hi;
-        const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[base]);
-        const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[base]);
+        for (int s = 0; s < KS; ++s) {
+          const float a = sv_l[(2 * s + hi) * CH + t + r32];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, z[s], acc, 0, 0, 0);
+        }
+        // accumulator reg r ↔ SV t + (r&3) + 8*(r>>2) + 4*hi ; column (lane&31) ↔ data row
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float d2 = fmaf(-2.f, acc[4 * g + q], snv[q] + zn);
-          d2 = fmaxf(d2, 0.f);
-          part = fmaf(cfv[q], __builtin_amdgcn_exp2f(ngl2e * d2), part);
+        for (int g = 0; g < 4; ++g) {
+          const int b0 = t + 8 * g + 4 * hi;
+          const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[b0]);
+          const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[b0]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float d2 = fmaf(-2.f, acc[4 * g + q], snv[q] + zn);
+            d2 = fmaxf(d2, 0.f);
+            part = fmaf(cfv[q], __builtin_amdgcn_exp2f(ngl2e * d2), part);
+          }
         }
       }
     }
     part += __shfl_xor(part, 32, kWave);
-    if (hi == 0 && row < n) out[row] = part + intercept;
+    if (valid && hi == 0 && row < n) out[row] = part + intercept;
+    if (nch > 1) staged = -1;  // next row tile restarts at chunk 0
   }
 }
 
 template <int KS>
 static void launch_rbf(const float* Z, int n, int F, const float* SVt, const float* sn,
                        const float* coef, int mp, float gamma, float b, float* out, hipStream_t st) {
-  const size_t lds = (size_t)(2 * KS + 2) * mp * sizeof(float);
-  HFENS_REQUIRE(lds <= 160 * 1024, "rbf_decision: support vectors do not fit LDS (160 KiB)");
+  // chunk so that one chunk image stays ≤ 96 KiB of LDS
+  int CH = (96 * 1024 / (int)((2 * KS + 2) * sizeof(float))) / 32 * 32;
+  if (CH > mp) CH = mp;
+  const size_t lds = (size_t)(2 * KS + 2) * CH * sizeof(float);
   const int ntile = (n + 31) / 32;
   int grid = (ntile + 3) / 4;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(rbf_decision_kernel<KS>, dim3(grid), dim3(256), lds, st, Z, n, F, SVt, sn,
-                     coef, mp, -gamma * 1.4426950408889634f, b, out);
+                     coef, mp, CH, -gamma * 1.4426950408889634f, b, out);
   launch_check();
 }
 
 void rbf_decision(uintptr_t Z, int n, int F, uintptr_t SVt, uintptr_t sn, uintptr_t coef, int mp,
                   double gamma, double b, uintptr_t out, uintptr_t stream) {
-  HFENS_REQUIRE(mp % 32 == 0, "rbf_decision: padded SV count must be a multiple of 32");
+  HFENS_REQUIRE(mp % 32 == 0 && mp > 0, "rbf_decision: padded SV count must be a positive multiple of 32");
   HFENS_REQUIRE(F >= 1 && F <= 64, "rbf_decision: 1 <= F <= 64");
   const int ks = (F + 1) / 2;
   auto Zp = reinterpret_cast<const float*>(Z);

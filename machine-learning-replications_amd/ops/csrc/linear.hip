@@ -154,4 +154,65 @@ void lasso_cd_path(int P, int F, int A, uintptr_t G, uintptr_t q, uintptr_t yy, 
   launch_check();
 }
 
+// ------------------------------------------------------------------------------------------
+// Weighted moments  G_p = Σ_n W[p,n]·x_n x_nᵀ (upper triangle), a_p = Σ_n W[p,n]·x_n,
+// v_p = Σ_n V[p,n]·x_n  for P weight vectors over one row matrix X [n, F] (f64).
+// These are the Gram / Hessian / gradient reductions of LassoCV (per-fold moments) and of the
+// logistic solvers (X̃ᵀDX̃, X̃ᵀr) — tall-skinny (n ≫ F ≤ 64) so a library GEMM runs them on one
+// tile; here every (row chunk, p) is a workgroup writing a partial, summed in fixed chunk order
+// (deterministic).  Row chunks are staged in LDS; each thread owns a few (i ≤ j) pairs.
+constexpr int kMomRows = 128;
+
+__global__ __launch_bounds__(256) void weighted_moments_kernel(
+    const double* __restrict__ X, int n, int F, const double* __restrict__ W,
+    const double* __restrict__ V, int npairs, double* __restrict__ Gpart, double* __restrict__ apart,
+    double* __restrict__ vpart) {
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [kMomRows][F+1] + w + v
+  const int ld = F + 1;
+  double* ws = xs + kMomRows * ld;
+  double* vs = ws + kMomRows;
+  const int c = blockIdx.x, p = blockIdx.y, C = gridDim.x;
+  const int r0 = c * kMomRows;
+  const int nr = min(kMomRows, n - r0);
+  for (int e = threadIdx.x; e < nr * F; e += blockDim.x) {
+    const int r = e / F, f = e % F;
+    xs[r * ld + f] = X[(size_t)(r0 + r) * F + f];
+  }
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+    ws[r] = W[(size_t)p * n + r0 + r];
+    vs[r] = V != nullptr ? V[(size_t)p * n + r0 + r] : 0.0;
+  }
+  __syncthreads();
+  // pairs: k → (i, j) with i ≤ j, row-major over the upper triangle
+  for (int k = threadIdx.x; k < npairs; k += blockDim.x) {
+    int i = 0, rem = k;
+    while (rem >= F - i) { rem -= F - i; ++i; }
+    const int j = i + rem;
+    double acc = 0.0;
+    for (int r = 0; r < nr; ++r) acc = fma(ws[r] * xs[r * ld + i], xs[r * ld + j], acc);
+    Gpart[((size_t)p * C + c) * npairs + k] = acc;
+  }
+  for (int f = threadIdx.x; f < F; f += blockDim.x) {
+    double a = 0.0, v = 0.0;
+    for (int r = 0; r < nr; ++r) {
+      a = fma(ws[r], xs[r * ld + f], a);
+      v = fma(vs[r], xs[r * ld + f], v);
+    }
+    apart[((size_t)p * C + c) * F + f] = a;
+    vpart[((size_t)p * C + c) * F + f] = v;
+  }
+}
+
+void weighted_moments(uintptr_t X, int n, int F, uintptr_t W, uintptr_t V, int P, uintptr_t Gpart,
+                      uintptr_t apart, uintptr_t vpart, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 128, "weighted_moments: 1 <= F <= 128");
+  if (n == 0) return;
+  const int C = (n + kMomRows - 1) / kMomRows;
+  const size_t lds = ((size_t)kMomRows * (F + 1) + 2 * kMomRows) * sizeof(double);
+  hipLaunchKernelGGL(weighted_moments_kernel, dim3(C, P), dim3(256), lds, as_stream(stream),
+                     (const double*)X, n, F, (const double*)W, (const double*)V, F * (F + 1) / 2,
+                     (double*)Gpart, (double*)apart, (double*)vpart);
+  launch_check();
+}
+
 }  // namespace hfens

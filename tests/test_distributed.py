@@ -1,0 +1,151 @@
+"""Data-parallel paths on the CPU with gloo (world_size 2): sharded training must
+reproduce the single-process fit (GBDT bit-identically thanks to fixed-point
+histograms)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = globals()[fn_name](rank, world, dist.group.WORLD)
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn_name, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue as _q
+    out = None
+    while out is None:
+        try:
+            out = q.get(timeout=2)
+        except _q.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                for p in procs:
+                    p.kill()
+                raise RuntimeError(f"worker failed: {[p.exitcode for p in procs]}")
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def _data(n=1200, F=20, seed=3):
+    from hfens.io.synth import make_hf_cohort
+    X, y, names = make_hf_cohort(n, F, seed=seed, nan_frac=0.0)
+    return torch.as_tensor(X), torch.as_tensor(y), names
+
+
+def _gbdt(rank, world, group):
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    from hfens.parallel.dist import shard_rows
+    X, y, _ = _data()
+    masks = torch.ones(2, X.shape[0], dtype=torch.bool)
+    masks[0, ::4] = False
+    ms = [GradientBoostingClassifier(n_estimators=15, max_depth=2) for _ in range(2)]
+    fit_gbdt_batch(ms, shard_rows(X, rank, world), shard_rows(y, rank, world),
+                   shard_rows(masks.t(), rank, world).t().contiguous(), group=group)
+    return [(m.tree_feature_.clone(), m.tree_threshold_.clone(), m.tree_value_.clone(), m.train_score_.clone())
+            for m in ms]
+
+
+def _logreg(rank, world, group):
+    from hfens.models.linear import LogisticRegression
+    from hfens.models.logreg_solver import fit_logreg_batch
+    from hfens.parallel.dist import shard_rows
+    X, y, _ = _data()
+    m = LogisticRegression(penalty="l1", solver="liblinear", class_weight="balanced")
+    fit_logreg_batch([m], shard_rows(X, rank, world), shard_rows(y, rank, world), group=group)
+    return m.coef_.clone(), m.intercept_.clone()
+
+
+def _lasso(rank, world, group):
+    from hfens.models.lasso import LassoCV, SelectFromModel
+    from hfens.parallel.dist import shard_rows
+    X, y, _ = _data()
+    s = SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=8)
+    s.fit(shard_rows(X, rank, world), shard_rows(y, rank, world), group=group)
+    return s.estimator_.alpha_, s.estimator_.coef_.clone(), s.get_support().copy()
+
+
+def _develop(rank, world, group):
+    from hfens.io.synth import make_dev_select
+    from hfens.parallel.dist import shard_rows
+    from hfens.pipeline import develop
+    Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
+    r = develop(shard_rows(Xd, rank, world), shard_rows(yd, rank, world), shard_rows(Xs, rank, world),
+                shard_rows(ys, rank, world), names, device="cpu", group=group)
+    return r.selected.copy(), r.scores
+
+
+def test_gbdt_dp_bit_identical():
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    got = _run("_gbdt")
+    X, y, _ = _data()
+    masks = torch.ones(2, X.shape[0], dtype=torch.bool)
+    masks[0, ::4] = False
+    ms = [GradientBoostingClassifier(n_estimators=15, max_depth=2) for _ in range(2)]
+    fit_gbdt_batch(ms, X, y, masks)
+    for (f, t, v, ts), m in zip(got, ms):
+        assert torch.equal(f, m.tree_feature_)
+        assert torch.equal(t, m.tree_threshold_)
+        assert torch.equal(v, m.tree_value_)
+        assert torch.equal(ts, m.train_score_)
+
+
+def test_logreg_dp():
+    from hfens.models.linear import LogisticRegression
+    from hfens.models.logreg_solver import fit_logreg_batch
+    coef, ic = _run("_logreg")
+    X, y, _ = _data()
+    m = LogisticRegression(penalty="l1", solver="liblinear", class_weight="balanced")
+    fit_logreg_batch([m], X, y)
+    assert torch.allclose(coef, m.coef_, atol=1e-8)
+
+
+def test_lasso_dp():
+    from hfens.models.lasso import LassoCV, SelectFromModel
+    alpha, coef, sup = _run("_lasso")
+    X, y, _ = _data()
+    s = SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=8).fit(X, y)
+    assert abs(alpha - s.estimator_.alpha_) < 1e-15
+    assert np.array_equal(sup, s.get_support())
+    assert torch.allclose(coef, s.estimator_.coef_, atol=1e-10)
+
+
+@pytest.mark.slow
+def test_develop_dp_matches_single():
+    from hfens.io.synth import make_dev_select
+    from hfens.pipeline import develop
+    sel, scores = _run("_develop")
+    Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
+    r = develop(Xd, yd, Xs, ys, names, device="cpu")
+    assert np.array_equal(sel, r.selected)
+    assert abs(scores["auroc"] - r.scores["auroc"]) < 1e-3  # f64 reduction order differs per rank

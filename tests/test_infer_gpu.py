@@ -11,7 +11,7 @@ from hfens.cli.predict_hf import PATIENT_PARAMS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,m,F", [(1, 434, 17), (1000, 434, 17), (777, 100, 40), (64, 33, 3)])
+@pytest.mark.parametrize("n,m,F", [(1, 434, 17), (1000, 434, 17), (777, 100, 40), (64, 33, 3), (300, 5000, 17), (200, 3000, 40)])
 def test_rbf_decision(dev, n, m, F):
     g = torch.Generator().manual_seed(n + m + F)
     z = torch.randn(n, F, generator=g, dtype=torch.float64)
