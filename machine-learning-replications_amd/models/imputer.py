@@ -87,14 +87,14 @@ class KNNImputer(Estimator):
             k = torch.arange(s0, s0 + SLOTS, device=X.device)
             valid = k[None, :] < nmiss[:, None]
             slot = torch.where(valid, cols, torch.full_like(cols, -1)).to(torch.int32).contiguous()
-            bi = torch.empty_like(slot)
-            bd = torch.empty(slot.shape, dtype=torch.float32, device=X.device)
+            best = torch.empty(slot.shape, dtype=torch.int64, device=X.device)
             E.knn_donors(R32.data_ptr(), rm.data_ptr(), rows.numel(), D32.data_ptr(), dm.data_ptr(),
-                         D32.shape[0], F, slot.data_ptr(), bi.data_ptr(), bd.data_ptr(),
-                         ops.stream_ptr(X.device))
+                         D32.shape[0], F, slot.data_ptr(), best.data_ptr(), ops.stream_ptr(X.device))
+            # packed (d² float bits << 32 | donor); all-ones = no donor with a defined distance
+            donor = torch.where(best == -1, torch.full_like(best, -1), best & 0xFFFFFFFF)
             r_idx = rows[:, None].expand_as(slot)[valid]
             c_idx = slot[valid].long()
-            donor = bi[valid].long()
+            donor = donor[valid]
             vals = torch.where(donor >= 0, self._fit_X[donor.clamp(min=0), c_idx], self._col_mean[c_idx])
             X[r_idx, c_idx] = vals
 

@@ -32,7 +32,7 @@ def _check_same(models, attrs):
             raise ValueError(f"batched logistic fit needs identical '{a}' across models")
 
 
-def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-13):
+def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
     Hn, gn, wn = H.cpu().numpy(), g.cpu().numpy(), w.cpu().numpy()
     pn = penal.cpu().numpy().astype(bool)
     B, F1 = gn.shape
@@ -145,7 +145,7 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
                 E = ops.ext()
                 d = torch.empty_like(W)
                 E.l1_qp_cd(B, F1, Hr.contiguous().data_ptr(), grad.contiguous().data_ptr(),
-                           W.contiguous().data_ptr(), penal.data_ptr(), 1.0, 500, 1e-14,
+                           W.contiguous().data_ptr(), penal.data_ptr(), 1.0, 200, 1e-12,
                            d.data_ptr(), ops.stream_ptr(dev))
             else:
                 d = _host_l1_qp(Hr, grad, W, penal, 1.0)

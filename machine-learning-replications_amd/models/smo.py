@@ -280,6 +280,8 @@ _GRAM_DT = np.dtype([("zoff", "<i8"), ("koff", "<i8"), ("l", "<i4"), ("ld", "<i4
 _SMO_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
                     ("pad", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
 _PLATT_DT = np.dtype([("off", "<i8"), ("l", "<i4"), ("pad", "<i4")])
+_DEC_DT = np.dtype([("zoff", "<i8"), ("hoff", "<i8"), ("l", "<i4"), ("h", "<i4"), ("ngl2e", "<f4"),
+                    ("per", "<i4")])
 
 
 def _dev_struct(arr: np.ndarray, device) -> torch.Tensor:
@@ -321,6 +323,33 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
     for k, p in enumerate(live):
         a0 = int(sm[k]["aoff"])
         out[id(p)] = (alpha[a0:a0 + int(sm[k]["l"])], rho[k], iters[k])
+    # ---- Platt held-out decision values of every CV sub-model: one batched launch
+    platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
+    if platt:
+        sign = torch.empty(aoff, dtype=torch.float32, device=device)
+        for k, p in enumerate(live):
+            a0, l = int(sm[k]["aoff"]), int(sm[k]["l"])
+            sign[a0:a0 + p.npos] = 1.0
+            sign[a0 + p.npos:a0 + l] = -1.0
+        coef = (sign * alpha.to(torch.float32)).contiguous()
+        hcat = torch.cat([Zs[p.fit][p.held_rows].to(torch.float32) for _, p in platt]).contiguous()
+        per = 1024
+        S = (max_l + per - 1) // per
+        dt = np.zeros(len(platt), _DEC_DT)
+        hoff = 0
+        for i, (k, p) in enumerate(platt):
+            h = int(p.held_rows.numel())
+            dt[i] = (int(g[k]["zoff"]), hoff, int(g[k]["l"]), h, -p.gamma * 1.4426950408889634, per)
+            hoff += h
+        part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
+        ddev = _dev_struct(dt, device)
+        max_h = int(dt["h"].max())
+        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(platt),
+                        max_h, S, part.data_ptr(), s)
+        dec = part.to(torch.float64).sum(1)
+        for i, (k, p) in enumerate(platt):
+            h0, h = int(dt[i]["hoff"]), int(dt[i]["h"])
+            out[("dec", id(p))] = dec[h0:h0 + h] - rho[k]
     return out
 
 
@@ -371,7 +400,7 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
             coef = yint * a
             Zh = Z[p.held_rows]
             if cuda:
-                d = ops.rbf_decision(Zh, Z[p.rows], coef, p.gamma, 0.0).to(torch.float64) - r.to(device)
+                d = sol[("dec", id(p))]
             else:
                 from ..ops import reference as ref
                 d = ref.rbf_decision(Zh.double(), Z[p.rows].double(), coef, p.gamma, 0.0) - r

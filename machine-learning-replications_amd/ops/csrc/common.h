@@ -67,6 +67,18 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
   }
 }
 
+// Broadcast lane `l` (wave-uniform) of a value: v_readlane_b32 into an SGPR — far cheaper than
+// a ds_bpermute shuffle when every lane wants the same source lane.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 __device__ __forceinline__ float fast_exp(float x) {  // e^x via v_exp_f32 (2^x)
   return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
 }

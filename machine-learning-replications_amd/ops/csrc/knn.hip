@@ -2,74 +2,87 @@
 // KNNImputer(n_neighbors=1), train_ensemble_public.py:37-40; distance semantics of sklearn
 // nan_euclidean_distances: d² = F/|common| · Σ_{common present} (x−y)²).
 //
-// One thread owns one receiver row (values in LDS, its ≤ 8 missing-column slots and their running
-// (distance, donor) minima in registers).  Donor rows stream through LDS in tiles of 256 rows and
-// are read by every thread simultaneously (LDS broadcast).  Per (receiver, donor) pair the
+// grid = (receiver blocks of 256) × (donor splits).  One thread owns one receiver row (values in
+// registers, statically indexed up to FMAX features) and up to 8 missing-column slots.  Each
+// workgroup streams its donor range through LDS in 256-row tiles (row stride padded to 4 floats
+// so every lane reads the same 16-byte vector: broadcast ds_read_b128).  Per (receiver, donor) the
 // distance is the direct difference form Σ(x_r − x_d)² over zero-filled rows (no ‖x‖²+‖y‖²−2x·y
 // cancellation, so exact ties stay exact) minus the cross-missing corrections, which only loop
-// over the set bits of the two 64-bit missing masks.  Tie-break: lowest donor index.
+// over the set bits of the two 64-bit missing masks.  Results merge across donor splits with a
+// 64-bit atomicMin on (float bits of d², donor index): smallest distance, then lowest donor index
+// — deterministic regardless of split count or arrival order.
 #include "common.h"
+#include <type_traits>
 
 namespace hfens {
 
 constexpr int kKnnTile = 256;
 constexpr int kKnnSlots = 8;
 
+template <int FMAX>
 __global__ __launch_bounds__(256) void knn_donor_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
-    const int* __restrict__ slot_col /*[nr][kKnnSlots] column or −1*/, int* __restrict__ best_idx,
-    float* __restrict__ best_dist) {
+    int per_split, const int* __restrict__ slot_col /*[nr][kKnnSlots] column or −1*/,
+    unsigned long long* __restrict__ best /*[nr][kKnnSlots] packed (dist bits, idx)*/) {
+  constexpr int LD = (FMAX + 3) / 4 * 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int ld = F | 1;
-  float* rs = sm;                                  // [256][ld]  receiver rows
-  float* ds = sm + 256 * ld;                       // [256][ld]  donor tile
-  unsigned long long* dm = (unsigned long long*)(ds + 256 * ld + ((256 * ld) & 1));  // [256]
+  float* ds = sm;                                                        // [256][LD] donor tile
+  unsigned long long* dm = (unsigned long long*)(ds + kKnnTile * LD);    // [256]
   const int r = blockIdx.x * 256 + threadIdx.x;
-  for (int e = threadIdx.x; e < 256 * F; e += 256) {
-    const int rr = e / F, c = e % F;
-    const int gr = blockIdx.x * 256 + rr;
-    rs[rr * ld + c] = gr < nr ? R[(size_t)gr * F + c] : 0.f;
-  }
   const bool active = r < nr;
+  const int d_begin = blockIdx.y * per_split;
+  const int d_end = min(nd, d_begin + per_split);
+  float xr[LD];
+#pragma unroll
+  for (int f = 0; f < LD; ++f) xr[f] = (active && f < F) ? R[(size_t)r * F + f] : 0.f;
   const unsigned long long mr = active ? rmask[r] : 0ull;
   int col[kKnnSlots];
   float bd[kKnnSlots];
   int bi[kKnnSlots];
-  int nslot = 0;
+  bool any = false;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k) {
     col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
     bd[k] = INFINITY;
     bi[k] = -1;
-    if (col[k] >= 0) nslot = k + 1;
+    any |= col[k] >= 0;
   }
-  const float* xr = rs + threadIdx.x * ld;
-  for (int d0 = 0; d0 < nd; d0 += kKnnTile) {
+  unsigned long long need = 0ull;  // bitmask of this receiver's slot columns
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k)
+    if (col[k] >= 0) need |= 1ull << col[k];
+  const float* xrs = R + (size_t)(active ? r : 0) * F;  // rare correction path reads global
+  for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
     __syncthreads();
-    const int nt = min(kKnnTile, nd - d0);
-    for (int e = threadIdx.x; e < nt * F; e += 256) {
-      const int rr = e / F, c = e % F;
-      ds[rr * ld + c] = D[(size_t)(d0 + rr) * F + c];
+    const int nt = min(kKnnTile, d_end - d0);
+    for (int e = threadIdx.x; e < nt * LD; e += 256) {
+      const int rr = e / LD, c = e % LD;
+      ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
     }
     if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
     __syncthreads();
-    if (nslot == 0) continue;
+    if (!any) continue;
     for (int t = 0; t < nt; ++t) {
-      const float* xd = ds + t * ld;
       const unsigned long long md = dm[t];
-      // does this donor have any of the receiver's missing columns?  (cheap early-out)
-      bool useful = false;
+      if ((need & ~md) == 0ull) continue;  // donor lacks every column this receiver needs
+      const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
+      float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-      for (int k = 0; k < kKnnSlots; ++k)
-        if (col[k] >= 0 && !((md >> col[k]) & 1ull)) useful = true;
-      if (!useful) continue;
-      float s = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const float df = xr[f] - xd[f];
-        s = fmaf(df, df, s);
+      for (int q = 0; q < LD / 4; ++q) {
+        if (4 * q < F) {
+          const float4 v = xd4[q];
+          const float a = xr[4 * q] - v.x, b = xr[4 * q + 1] - v.y;
+          const float c = xr[4 * q + 2] - v.z, d = xr[4 * q + 3] - v.w;
+          s0 = fmaf(a, a, s0);
+          s1 = fmaf(b, b, s1);
+          s0 = fmaf(c, c, s0);
+          s1 = fmaf(d, d, s1);
+        }
       }
+      float s = s0 + s1;
       // remove terms where exactly one side is missing (the other side's x² was added)
+      const float* xd = ds + t * LD;
       unsigned long long only_r = mr & ~md, only_d = md & ~mr;
       while (only_r) {
         const int f = __builtin_ctzll(only_r);
@@ -79,7 +92,7 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
       while (only_d) {
         const int f = __builtin_ctzll(only_d);
         only_d &= only_d - 1;
-        s -= xr[f] * xr[f];
+        s -= xrs[f] * xrs[f];
       }
       const int present = F - __builtin_popcountll(mr | md);
       if (present <= 0) continue;  // undefined distance (sklearn: NaN, ignored)
@@ -94,24 +107,43 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
   if (active) {
 #pragma unroll
     for (int k = 0; k < kKnnSlots; ++k) {
-      best_idx[(size_t)r * kKnnSlots + k] = bi[k];
-      best_dist[(size_t)r * kKnnSlots + k] = bd[k];
+      if (bi[k] >= 0) {
+        const unsigned long long key =
+            ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned long long)(unsigned)bi[k];
+        atomicMin(&best[(size_t)r * kKnnSlots + k], key);
+      }
     }
   }
 }
 
 void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
-                uintptr_t slot_col, uintptr_t best_idx, uintptr_t best_dist, uintptr_t stream) {
+                uintptr_t slot_col, uintptr_t best, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_donors: 1 <= F <= 64 (64-bit missing masks)");
-  if (nr == 0) return;
-  const int ld = F | 1;
-  const size_t lds = (size_t)2 * 256 * ld * sizeof(float) + 16 + 256 * sizeof(unsigned long long);
-  HFENS_REQUIRE(lds <= 160 * 1024, "knn_donors: LDS budget");
-  hipLaunchKernelGGL(knn_donor_kernel, dim3((nr + 255) / 256), dim3(256), lds, as_stream(stream),
-                     (const float*)R, (const unsigned long long*)rmask, nr, (const float*)D,
-                     (const unsigned long long*)dmask, nd, F, (const int*)slot_col, (int*)best_idx,
-                     (float*)best_dist);
-  launch_check();
+  if (nr == 0 || nd == 0) return;
+  hipStream_t st = as_stream(stream);
+  HFENS_CHECK(hipMemsetAsync((void*)best, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned long long), st));
+  const int rb = (nr + 255) / 256;
+  int splits = 2048 / rb;
+  const int max_splits = (nd + kKnnTile - 1) / kKnnTile;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int per = (nd + splits - 1) / splits;
+  per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
+  splits = (nd + per - 1) / per;
+  auto go = [&](auto fm) {
+    constexpr int FM = decltype(fm)::value;
+    constexpr int LD = (FM + 3) / 4 * 4;
+    const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
+    hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
+                       (const unsigned long long*)rmask, nr, (const float*)D,
+                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
+                       (unsigned long long*)best);
+    launch_check();
+  };
+  if (F <= 16) go(std::integral_constant<int, 16>{});
+  else if (F <= 32) go(std::integral_constant<int, 32>{});
+  else if (F <= 48) go(std::integral_constant<int, 48>{});
+  else go(std::integral_constant<int, 64>{});
 }
 
 }  // namespace hfens

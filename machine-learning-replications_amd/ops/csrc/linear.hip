@@ -28,15 +28,16 @@ __global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __re
   __syncthreads();
   const double gj = j < F1 ? g[b * F1 + j] : 0.0;
   const double wj = j < F1 ? w[b * F1 + j] : 0.0;
+  const double hjj = j < F1 ? Hs[j * F1 + j] : 0.0;
   double Hd = 0.0;  // (H d)_j
   double dj = 0.0;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     double maxstep = 0.0;
     for (int k = 0; k < F1; ++k) {
       // coordinate k: quantities owned by lane k
-      const double gk = __shfl(gj, k, kWave), wk = __shfl(wj, k, kWave);
-      const double Hdk = __shfl(Hd, k, kWave), dk = __shfl(dj, k, kWave);
-      const double hkk = Hs[k * F1 + k];
+      const double gk = readlane_f64(gj, k), wk = readlane_f64(wj, k);
+      const double Hdk = readlane_f64(Hd, k), dk = readlane_f64(dj, k);
+      const double hkk = readlane_f64(hjj, k);
       const double a = hkk > 1e-300 ? hkk : 1e-300;
       // 1-D problem in z = w_k + d_k:  (gk + Hdk − hkk·dk)(z − wk) + ½hkk(z − wk)² + λ|z|
       const double lin = gk + Hdk - a * dk;
@@ -102,9 +103,9 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
     for (it = 0; it < max_iter; ++it) {
       double w_max = 0.0, d_w_max = 0.0;
       for (int k = 0; k < F; ++k) {
-        const double gkk = __shfl(gjj, k, kWave);
+        const double gkk = readlane_f64(gjj, k);
         if (gkk == 0.0) continue;
-        const double wk = __shfl(wj, k, kWave), Hwk = __shfl(Hw, k, kWave), qk = __shfl(qj, k, kWave);
+        const double wk = readlane_f64(wj, k), Hwk = readlane_f64(Hw, k), qk = readlane_f64(qj, k);
         // tmp = q_k − (Gw)_k + G_kk w_k
         const double tmp = qk - Hwk + gkk * wk;
         double nw = fabs(tmp) > l1 ? copysign(fabs(tmp) - l1, tmp) / gkk : 0.0;

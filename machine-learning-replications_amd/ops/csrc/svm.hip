@@ -398,6 +398,107 @@ void smo_batch(uintptr_t probs, int P, int max_l, uintptr_t K, uintptr_t alpha, 
 }
 
 // ------------------------------------------------------------------------------------------
+// Batched decision values of many sub-models on their held-out rows (the Platt CV step):
+//   part[row][s] = Σ_{t ∈ split s} coef_p[t]·exp(-γ_p‖h_row − z_t‖²)
+// for every problem p (SVs = the problem's training rows in zcat, coef = y·α, zero for non-SVs).
+// grid = (128-row held tiles, SV splits, problems); per split the SVs stream through LDS in
+// k-major chunks; f32-input MFMA as in rbf_decision.  Partials are summed on the host side in a
+// fixed order (deterministic).
+struct DecProb {
+  long long zoff;   // first SV row in zcat
+  long long hoff;   // first held row in hcat
+  int l;            // SVs
+  int h;            // held rows
+  float ngl2e;
+  int per;          // SVs per split (multiple of 32)
+};
+
+template <int KS>
+__global__ __launch_bounds__(256) void svm_dec_batch_kernel(const float* __restrict__ zcat,
+                                                            const float* __restrict__ coef,
+                                                            const float* __restrict__ hcat, int F,
+                                                            const DecProb* __restrict__ probs,
+                                                            int S, float* __restrict__ part) {
+  const DecProb P = probs[blockIdx.z];
+  const int row0 = blockIdx.x * 128;
+  const int s = blockIdx.y;
+  const int t_begin = s * P.per;
+  if (row0 >= P.h || t_begin >= P.l) return;
+  const int t_end = min(P.l, t_begin + P.per);
+  constexpr int CH = 256;
+  __shared__ __attribute__((aligned(16))) float sv_l[2 * KS][CH];
+  __shared__ __attribute__((aligned(16))) float sn_l[CH];
+  __shared__ __attribute__((aligned(16))) float cf_l[CH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r32 = lane & 31, hi = lane >> 5;
+  const int row = row0 + wave * 32 + r32;
+  float z[KS];
+  float znp = 0.f;
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    const int k = 2 * q + hi;
+    z[q] = (row < P.h && k < F) ? hcat[(size_t)(P.hoff + row) * F + k] : 0.f;
+    znp = fmaf(z[q], z[q], znp);
+  }
+  const float zn = znp + __shfl_xor(znp, 32, kWave);
+  float acc_part = 0.f;
+  for (int c0 = t_begin; c0 < t_end; c0 += CH) {
+    const int cl = min(CH, t_end - c0);
+    const int clp = (cl + 31) / 32 * 32;
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * KS * CH; e += 256) {
+      const int k = e / CH, j = e % CH;
+      sv_l[k][j] = (j < cl && k < F) ? zcat[(size_t)(P.zoff + c0 + j) * F + k] : 0.f;
+    }
+    for (int j = threadIdx.x; j < CH; j += 256) cf_l[j] = j < cl ? coef[P.zoff + c0 + j] : 0.f;
+    __syncthreads();
+    for (int j = threadIdx.x; j < CH; j += 256) {
+      float a = 0.f;
+      for (int k = 0; k < 2 * KS; ++k) a = fmaf(sv_l[k][j], sv_l[k][j], a);
+      sn_l[j] = a;
+    }
+    __syncthreads();
+    for (int t = 0; t < clp; t += 32) {
+      f32x16 acc = {0.f};
+#pragma unroll
+      for (int q = 0; q < KS; ++q)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sv_l[2 * q + hi][t + r32], z[q], acc, 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b0 = t + 8 * g + 4 * hi;
+        const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[b0]);
+        const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[b0]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d2 = fmaxf(fmaf(-2.f, acc[4 * g + q], snv[q] + zn), 0.f);
+          acc_part = fmaf(cfv[q], __builtin_amdgcn_exp2f(P.ngl2e * d2), acc_part);
+        }
+      }
+    }
+  }
+  acc_part += __shfl_xor(acc_part, 32, kWave);
+  if (hi == 0 && row < P.h) part[(size_t)(P.hoff + row) * S + s] = acc_part;
+}
+
+void svm_dec_batch(uintptr_t zcat, uintptr_t coef, uintptr_t hcat, int F, uintptr_t probs, int P,
+                   int max_h, int S, uintptr_t part, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64, "svm_dec_batch: 1 <= F <= 64");
+  dim3 grid((max_h + 127) / 128, S, P);
+  const int ks = (F + 1) / 2;
+  hipStream_t st = as_stream(stream);
+#define DEC_CASE(KS_)                                                                            \
+  if (ks <= KS_) {                                                                               \
+    hipLaunchKernelGGL(svm_dec_batch_kernel<KS_>, grid, dim3(256), 0, st, (const float*)zcat,    \
+                       (const float*)coef, (const float*)hcat, F, (const DecProb*)probs, S,      \
+                       (float*)part);                                                            \
+    launch_check();                                                                              \
+    return;                                                                                      \
+  }
+  DEC_CASE(4) DEC_CASE(8) DEC_CASE(12) DEC_CASE(16) DEC_CASE(24) DEC_CASE(32)
+#undef DEC_CASE
+}
+
+// ------------------------------------------------------------------------------------------
 // Platt scaling: sigmoid_train on decision values (one workgroup per fit).
 struct PlattProb {
   long long off;  // offset into dec / labels
