@@ -105,16 +105,18 @@ class KNNImputer(Estimator):
         F = X.shape[1]
         D = torch.where(mf, torch.zeros_like(fit), fit)
         pres_f = (~mf).to(torch.float64)
-        for s in range(0, rows.numel(), 2048):
-            rr = rows[s:s + 2048]
+        step = max(1, (1 << 24) // max(1, fit.shape[0] * F))
+        for s in range(0, rows.numel(), step):
+            rr = rows[s:s + step]
             R = X[rr]
             mr = torch.isnan(R)
             Rz = torch.where(mr, torch.zeros_like(R), R)
             pres_r = (~mr).to(torch.float64)
-            # Σ_common (x−y)² via the masked expansion
-            d2 = (Rz * Rz) @ pres_f.t() + pres_r @ (D * D).t() - 2.0 * Rz @ D.t()
-            common = pres_r @ pres_f.t()
-            dist = torch.where(common > 0, d2.clamp(min=0) * F / common.clamp(min=1),
+            # Σ_common (x−y)², direct differences in f64 (exact ties stay ties)
+            both = pres_r[:, None, :] * pres_f[None, :, :]
+            d2 = (both * (Rz[:, None, :] - D[None, :, :]) ** 2).sum(-1)
+            common = both.sum(-1)
+            dist = torch.where(common > 0, d2 * F / common.clamp(min=1),
                                torch.full_like(d2, float("inf")))
             for j, r in enumerate(rr.tolist()):
                 for c in torch.nonzero(mr[j]).squeeze(1).tolist():

@@ -65,6 +65,15 @@ def bounded_rand_int(mt: _MTStream, rng: int) -> int:
 
 
 def libsvm_perm(l: int, seed: int) -> np.ndarray:
+    from .. import ops
+    if ops.has_ext():  # native host loop (ops/csrc/host.hip)
+        out = np.empty(l, dtype=np.int64)
+        ops.ext().libsvm_perm(l, int(seed) & 0xFFFFFFFF, out.ctypes.data)
+        return out
+    return libsvm_perm_py(l, seed)
+
+
+def libsvm_perm_py(l: int, seed: int) -> np.ndarray:
     mt = _MTStream(seed)
     perm = np.arange(l)
     for i in range(l):

@@ -125,133 +125,139 @@ constexpr int kSmoWaves = kSmoThreads / 64;
 constexpr double kTau = 1e-12;
 constexpr double kInf = 1.0e300;
 
-// block arg-max of v (ties → larger index); all threads receive the result
-__device__ __forceinline__ void block_argmax_last(double& v, int& idx, double* sv, int* si) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ov = __shfl_xor(v, o, kWave);
-    const int oi = __shfl_xor(idx, o, kWave);
-    if (ov > v || (ov == v && oi > idx)) { v = ov; idx = oi; }
-  }
-  if (lane == 0) { sv[wave] = v; si[wave] = idx; }
-  __syncthreads();
-  if (wave == 0) {
-    v = lane < kSmoWaves ? sv[lane] : -kInf;
-    idx = lane < kSmoWaves ? si[lane] : -1;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(v, o, kWave);
-      const int oi = __shfl_xor(idx, o, kWave);
-      if (ov > v || (ov == v && oi > idx)) { v = ov; idx = oi; }
-    }
-    if (lane == 0) { sv[kSmoWaves] = v; si[kSmoWaves] = idx; }
-  }
-  __syncthreads();
-  v = sv[kSmoWaves];
-  idx = si[kSmoWaves];
+// Block reduction of (a, b, idx): a → max; (b, idx) → arg-max with ties to the larger index.
+// Used with a = −∞ when only the arg-max is wanted.  All threads receive the result.
+struct Red3 {
+  double a, b;
+  int idx;
+};
+
+__device__ __forceinline__ void red3_combine(Red3& x, double a, double b, int idx) {
+  x.a = fmax(x.a, a);
+  if (b > x.b || (b == x.b && idx > x.idx)) { x.b = b; x.idx = idx; }
 }
 
-template <int KMAX>
+__device__ __forceinline__ Red3 block_red3(Red3 v, Red3* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    red3_combine(v, __shfl_xor(v.a, o, kWave), __shfl_xor(v.b, o, kWave), __shfl_xor(v.idx, o, kWave));
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    Red3 w = lane < kSmoWaves ? sh[lane] : Red3{-kInf, -kInf, -1};
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1)  // kSmoWaves = 16 partials live in lanes 0..15
+      red3_combine(w, __shfl_xor(w.a, o, kWave), __shfl_xor(w.b, o, kWave), __shfl_xor(w.idx, o, kWave));
+    if (lane == 0) sh[kSmoWaves] = w;
+  }
+  __syncthreads();
+  return sh[kSmoWaves];
+}
+
+// Element ownership: thread `tid`, group g < K4, lane-of-vector e < 4 owns index
+// t = 4·(tid + g·kSmoThreads) + e, so every Gram-row read is one float4 per (thread, group).
+template <int K4>
 __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restrict__ probs,
                                                           const float* __restrict__ K,
                                                           double* __restrict__ alpha_all,
                                                           double eps, long long max_iter,
                                                           SmoOut out) {
+  // libsvm's arithmetic (x86-64, no FMA): keep a*b + c*d un-contracted so the gradient path
+  // follows the reference bit for bit given the same Gram entries
+#pragma clang fp contract(off)
+  constexpr int KM = 4 * K4;
+  static_assert(KM <= 64, "per-thread element masks are 64-bit");
   const SmoProb P = probs[blockIdx.x];
   const float* Kp = K + P.koff;
   double* alpha = alpha_all + P.aoff;
   const int tid = threadIdx.x;
-  __shared__ double sv[kSmoWaves + 1];
-  __shared__ int si[kSmoWaves + 1];
-  __shared__ double sv2[kSmoWaves + 1];
-  __shared__ int si2[kSmoWaves + 1];
-  __shared__ double pub[4];  // alpha_i, alpha_j, Q_ij (K_ij), unused
+  __shared__ Red3 sh[kSmoWaves + 1];
+  __shared__ double pub[4];
 
-  double G[KMAX];
-  float Qi[KMAX];
-  // α status, 2 bits per element (0 lower, 1 free, 2 upper), packed to save VGPRs
-  constexpr int NST = (KMAX + 15) / 16;
-  unsigned int stp[NST];
+  double G[KM];
+  float Qi[KM];
+  unsigned long long ypos = 0ull;   // y_t = +1
+  unsigned long long upm = 0ull;    // t ∈ I_up   (y=+1: α<C ; y=−1: α>0)
+  unsigned long long lowm = 0ull;   // t ∈ I_low  (y=+1: α>0 ; y=−1: α<C)
+  unsigned long long freem = 0ull;  // 0 < α < C
+  unsigned long long upperm = 0ull; // α = C
 #pragma unroll
-  for (int q = 0; q < NST; ++q) stp[q] = 0u;
-#define ST_GET(k) ((stp[(k) >> 4] >> (((k) & 15) * 2)) & 3u)
-#define ST_SET(k, v) (stp[(k) >> 4] = (stp[(k) >> 4] & ~(3u << (((k) & 15) * 2))) | ((unsigned)(v) << (((k) & 15) * 2)))
+  for (int g = 0; g < K4; ++g)
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    const int t = tid + k * kSmoThreads;
-    G[k] = -1.0;  // p_i = −1 for C-SVC
-    Qi[k] = 0.f;
-    if (t < P.l) alpha[t] = 0.0;
-  }
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * g + e;
+      const int t = 4 * (tid + g * kSmoThreads) + e;
+      G[k] = -1.0;  // p_i = −1 for C-SVC, α = 0
+      Qi[k] = 0.f;
+      if (t < P.l) {
+        alpha[t] = 0.0;
+        const bool pos = t < P.npos;
+        if (pos) { ypos |= 1ull << k; upm |= 1ull << k; }   // α = 0 is at the lower bound
+        else lowm |= 1ull << k;
+      }
+    }
+  // ---- WSS step 1 for the first iteration
+  Red3 r1{-kInf, -kInf, -1};
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+    if ((upm >> k) & 1ull) {
+      const int t = 4 * (tid + (k >> 2) * kSmoThreads) + (k & 3);
+      red3_combine(r1, -kInf, ((ypos >> k) & 1ull) ? -G[k] : G[k], t);
+    }
+  r1 = block_red3(r1, sh);
   long long iter = 0;
   double last_gap = 0.0;
   for (; iter < max_iter; ++iter) {
-    // ---- WSS step 1: i = argmax_{t ∈ I_up} −y_t G_t
-    double bv = -kInf;
-    int bi = -1;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int t = tid + k * kSmoThreads;
-      if (t < P.l) {
-        const bool pos = t < P.npos;
-        const bool up = pos ? ST_GET(k) != 2u : ST_GET(k) != 0u;
-        const double v = pos ? -G[k] : G[k];
-        if (up && (v > bv || (v == bv && t > bi))) { bv = v; bi = t; }
-      }
-    }
-    block_argmax_last(bv, bi, sv, si);
-    const double Gmax = bv;
-    const int i = bi;
+    const double Gmax = r1.b;
+    const int i = r1.idx;
     if (i < 0) break;
     const int yi = i < P.npos ? 1 : -1;
-    // ---- WSS step 2
-    const float* Ki = Kp + (size_t)i * P.ld;
-    double gmax2 = -kInf;
-    double best = -kInf;  // maximise −obj_diff ⇔ minimise obj_diff
+    // ---- WSS step 2 over row i (second order, libsvm's "last index wins" on ties).  Per thread
+    // the candidates compare by cross-multiplication (no divide); one divide per thread at the end.
+    const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)i * P.ld);
+    double gmax2 = -kInf, bnum = 0.0, bden = 1.0;
     int bj = -1;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int t = tid + k * kSmoThreads;
-      if (t < P.l) {
-        const float kij = Ki[t];
-        Qi[k] = kij;
-        const bool pos = t < P.npos;
-        const bool low = pos ? ST_GET(k) != 0u : ST_GET(k) != 2u;
-        if (low) {
-          const double yG = pos ? G[k] : -G[k];
-          if (yG > gmax2) gmax2 = yG;
-          const double grad_diff = Gmax + yG;
-          if (grad_diff > 0) {
-            double quad = 2.0 - 2.0 * (double)kij;
+    for (int g = 0; g < K4; ++g) {
+      const int t0 = 4 * (tid + g * kSmoThreads);
+      if (t0 < P.l) {
+        const float4 q = Ki4[tid + g * kSmoThreads];
+        Qi[4 * g] = q.x; Qi[4 * g + 1] = q.y; Qi[4 * g + 2] = q.z; Qi[4 * g + 3] = q.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * g + e;
+        if ((lowm >> k) & 1ull) {
+          const double yG = ((ypos >> k) & 1ull) ? G[k] : -G[k];
+          gmax2 = fmax(gmax2, yG);
+          const double gd = Gmax + yG;
+          if (gd > 0) {
+            double quad = 2.0 - 2.0 * (double)Qi[k];
             if (quad <= 0) quad = kTau;
-            const double nobj = (grad_diff * grad_diff) / quad;
-            if (nobj > best || (nobj == best && t > bj)) { best = nobj; bj = t; }
+            const double num = gd * gd;
+            // num/quad > bnum/bden  (ties → larger index = later k within the thread)
+            const double lhs = num * bden, rhs = bnum * quad;
+            if (bj < 0 || lhs >= rhs) { bnum = num; bden = quad; bj = t0 + e; }
           }
         }
       }
     }
-    // Gmax2 (value only) and j together: reduce Gmax2 first through sv2/si2
-    {
-      double g2 = gmax2;
-      int dummy = 0;
-      block_argmax_last(g2, dummy, sv2, si2);
-      gmax2 = g2;
-    }
-    block_argmax_last(best, bj, sv, si);
-    const int j = bj;
-    last_gap = Gmax + gmax2;
-    if (Gmax + gmax2 < eps || j < 0) break;
+    Red3 r2{gmax2, bj >= 0 ? bnum / bden : -kInf, bj};
+    r2 = block_red3(r2, sh);
+    const int j = r2.idx;
+    last_gap = Gmax + r2.a;
+    if (Gmax + r2.a < eps || j < 0) break;
     // ---- publish α_i (owner of i) and α_j, K_ij, G_j (owner of j); G_i = −y_i·Gmax exactly
-    const int oi_t = i % kSmoThreads, oj_t = j % kSmoThreads;
-    if (tid == oi_t) pub[0] = alpha[i];
-    if (tid == oj_t) {
+    const int oi = (i >> 2) % kSmoThreads, oj = (j >> 2) % kSmoThreads;
+    if (tid == oi) pub[0] = alpha[i];
+    if (tid == oj) {
       pub[1] = alpha[j];
-      const int kk = j / kSmoThreads;
+      const int kk = 4 * ((j >> 2) / kSmoThreads) + (j & 3);
       float kij = 0.f;
       double gj = 0.0;
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k)
+      for (int k = 0; k < KM; ++k)
         if (k == kk) { kij = Qi[k]; gj = G[k]; }
       pub[2] = kij;
       pub[3] = gj;
@@ -259,12 +265,12 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
     __syncthreads();
     const double ai_old = pub[0], aj_old = pub[1];
     const double Kij = pub[2];
+    const double Gj = pub[3];
     const int yj = j < P.npos ? 1 : -1;
     const double Ci = yi > 0 ? P.Cp : P.Cn, Cj = yj > 0 ? P.Cp : P.Cn;
     const double Qij = (double)(yi * yj) * Kij;
-    double ai = ai_old, aj = aj_old;
     const double Gi = -(double)yi * Gmax;
-    const double Gj = pub[3];
+    double ai = ai_old, aj = aj_old;
     if (yi != yj) {
       double quad = 2.0 + 2.0 * Qij;
       if (quad <= 0) quad = kTau;
@@ -300,82 +306,90 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
         if (ai < 0) { ai = 0; aj = sum; }
       }
     }
-    const double dai = ai - ai_old, daj = aj - aj_old;
-    // ---- gradient update with rows i (registers) and j (read now)
-    const float* Kj = Kp + (size_t)j * P.ld;
+    const double ci = (double)yi * (ai - ai_old), cj = (double)yj * (aj - aj_old);
+    // owners: store α and refresh the bound masks of i and j
+    if (tid == oi || tid == oj) {
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int t = tid + k * kSmoThreads;
-      if (t < P.l) {
-        const double yt = t < P.npos ? 1.0 : -1.0;
-        const double kjt = Kj[t];
-        G[k] += yt * ((double)yi * (double)Qi[k] * dai + (double)yj * kjt * daj);
+      for (int w = 0; w < 2; ++w) {
+        const int t = w == 0 ? i : j;
+        if ((w == 0 && tid != oi) || (w == 1 && tid != oj)) continue;
+        const double a = w == 0 ? ai : aj;
+        const double C = w == 0 ? Ci : Cj;
+        alpha[t] = a;
+        const int kk = 4 * ((t >> 2) / kSmoThreads) + (t & 3);
+        const unsigned long long bit = 1ull << kk;
+        const bool pos = (ypos & bit) != 0ull;
+        const bool atU = a >= C, atL = a <= 0;
+        freem = (!atU && !atL) ? (freem | bit) : (freem & ~bit);
+        upperm = atU ? (upperm | bit) : (upperm & ~bit);
+        const bool up = pos ? !atU : !atL;
+        const bool low = pos ? !atL : !atU;
+        upm = up ? (upm | bit) : (upm & ~bit);
+        lowm = low ? (lowm | bit) : (lowm & ~bit);
       }
     }
-    // owners update α and status
-    if (tid == oi_t) {
-      alpha[i] = ai;
-      const int kk = i / kSmoThreads;
-      const unsigned char s = ai >= Ci ? 2 : (ai <= 0 ? 0 : 1);
+    // ---- fused: gradient update with rows i (registers) and j, then next step-1 candidates
+    const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)j * P.ld);
+    r1 = Red3{-kInf, -kInf, -1};
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k)
-        if (k == kk) ST_SET(k, s);
-    }
-    if (tid == oj_t) {
-      alpha[j] = aj;
-      const int kk = j / kSmoThreads;
-      const unsigned char s = aj >= Cj ? 2 : (aj <= 0 ? 0 : 1);
+    for (int g = 0; g < K4; ++g) {
+      const int t0 = 4 * (tid + g * kSmoThreads);
+      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t0 < P.l) q = Kj4[tid + g * kSmoThreads];
+      const float qj[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k)
-        if (k == kk) ST_SET(k, s);
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * g + e;
+        const bool pos = (ypos >> k) & 1ull;
+        const double upd = (double)Qi[k] * ci + (double)qj[e] * cj;
+        G[k] += pos ? upd : -upd;
+        if ((upm >> k) & 1ull) red3_combine(r1, -kInf, pos ? -G[k] : G[k], t0 + e);
+      }
     }
-    __syncthreads();  // pub[] reuse
+    r1 = block_red3(r1, sh);
   }
   // ---- calculate_rho
-  double ub = kInf, lb = -kInf, sum_free = 0.0;
+  Red3 ru{-kInf, -kInf, -1};   // a = max(−ub)
+  Red3 rl{-kInf, -kInf, -1};   // a = max(lb)
+  double sum_free = 0.0;
   int nfree = 0;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    const int t = tid + k * kSmoThreads;
+  for (int k = 0; k < KM; ++k) {
+    const int t = 4 * (tid + (k >> 2) * kSmoThreads) + (k & 3);
     if (t < P.l) {
-      const bool pos = t < P.npos;
+      const bool pos = (ypos >> k) & 1ull;
       const double yG = pos ? G[k] : -G[k];
-      if (ST_GET(k) == 2u) {
-        if (!pos) ub = fmin(ub, yG); else lb = fmax(lb, yG);
-      } else if (ST_GET(k) == 0u) {
-        if (pos) ub = fmin(ub, yG); else lb = fmax(lb, yG);
-      } else {
+      if ((upperm >> k) & 1ull) {
+        if (!pos) ru.a = fmax(ru.a, -yG); else rl.a = fmax(rl.a, yG);
+      } else if ((freem >> k) & 1ull) {
         ++nfree;
         sum_free += yG;
+      } else {
+        if (pos) ru.a = fmax(ru.a, -yG); else rl.a = fmax(rl.a, yG);
       }
     }
   }
+  ru = block_red3(ru, sh);
+  rl = block_red3(rl, sh);
+  Red3 rs{-kInf, sum_free, nfree};
   {
-    int dummy = 0;
-    double nub = -ub;
-    block_argmax_last(nub, dummy, sv, si);
-    ub = -nub;
-    block_argmax_last(lb, dummy, sv2, si2);
-    // sums
+    // plain sums (not arg-max): reuse the shared buffer with a sum reduction
+    double s = wave_sum(sum_free);
+    double c = wave_sum((double)nfree);
     const int lane = tid & 63, wave = tid >> 6;
-    double s = sum_free;
-    double c = (double)nfree;
-    s = wave_sum(s);
-    c = wave_sum(c);
     __syncthreads();
-    if (lane == 0) { sv[wave] = s; sv2[wave] = c; }
+    if (lane == 0) { sh[wave].a = s; sh[wave].b = c; }
     __syncthreads();
     if (tid == 0) {
       double S = 0, Cc = 0;
-      for (int w = 0; w < kSmoWaves; ++w) { S += sv[w]; Cc += sv2[w]; }
-      const double r = Cc > 0 ? S / Cc : (ub + lb) / 2;
-      out.rho[blockIdx.x] = r;
+      for (int w = 0; w < kSmoWaves; ++w) { S += sh[w].a; Cc += sh[w].b; }
+      const double ub = -ru.a, lb = rl.a;
+      out.rho[blockIdx.x] = Cc > 0 ? S / Cc : (ub + lb) / 2;
       out.iters[blockIdx.x] = (int)iter;
       out.gap[blockIdx.x] = last_gap;
     }
   }
-#undef ST_GET
-#undef ST_SET
+  (void)rs;
 }
 
 void smo_batch(uintptr_t probs, int P, int max_l, uintptr_t K, uintptr_t alpha, double eps,
@@ -385,14 +399,14 @@ void smo_batch(uintptr_t probs, int P, int max_l, uintptr_t K, uintptr_t alpha, 
   auto kp = (const float*)K;
   auto ap = (double*)alpha;
   hipStream_t st = as_stream(stream);
-#define SMO_CASE(KM)                                                                        \
-  if (max_l <= KM * kSmoThreads) {                                                          \
-    hipLaunchKernelGGL(smo_kernel<KM>, dim3(P), dim3(kSmoThreads), 0, st, pp, kp, ap, eps,  \
+#define SMO_CASE(K4)                                                                        \
+  if (max_l <= 4 * K4 * kSmoThreads) {                                                      \
+    hipLaunchKernelGGL(smo_kernel<K4>, dim3(P), dim3(kSmoThreads), 0, st, pp, kp, ap, eps,  \
                        max_iter, o);                                                        \
     launch_check();                                                                         \
     return;                                                                                 \
   }
-  SMO_CASE(1) SMO_CASE(2) SMO_CASE(4) SMO_CASE(8) SMO_CASE(16) SMO_CASE(32)
+  SMO_CASE(1) SMO_CASE(2) SMO_CASE(3) SMO_CASE(4) SMO_CASE(6) SMO_CASE(8)
 #undef SMO_CASE
   throw std::invalid_argument("smo_batch: problem larger than 32768 points on the register path");
 }

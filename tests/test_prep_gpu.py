@@ -1,0 +1,52 @@
+"""Preprocessing kernels on the MI355X: KNN donor search and the LassoCV path vs host mirrors."""
+import numpy as np
+import pytest
+import torch
+
+from hfens.io.synth import make_hf_cohort
+from hfens.models.imputer import KNNImputer
+from hfens.models.lasso import LassoCV, SelectFromModel
+from hfens import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,F,nan", [(3000, 40, 0.02), (700, 64, 0.05), (500, 17, 0.3)])
+def test_knn_imputer_device_matches_host(dev, n, F, nan):
+    X, _, _ = make_hf_cohort(n, F, seed=n + F, nan_frac=nan)
+    Xt = torch.as_tensor(X)
+    host = KNNImputer(n_neighbors=1).fit(Xt).transform(Xt)
+    devo = KNNImputer(n_neighbors=1).fit(Xt.to(dev)).transform(Xt.to(dev)).cpu()
+    bad = (host - devo).abs() > 1e-9
+    # device distances are f32: only donors whose f64 distances differ by < f32 rounding can flip
+    assert int(bad.sum()) <= max(2, int(0.005 * np.isnan(X).sum()))
+
+
+def test_knn_matches_sklearn(dev):
+    from sklearn.impute import KNNImputer as SK
+    X, _, _ = make_hf_cohort(2000, 40, seed=9, nan_frac=0.02)
+    ours = KNNImputer(n_neighbors=1).fit(torch.as_tensor(X).to(dev)).transform(torch.as_tensor(X).to(dev)).cpu().numpy()
+    theirs = SK(n_neighbors=1).fit_transform(X)
+    assert (np.abs(ours - theirs) > 1e-9).sum() <= max(1, int(0.01 * np.isnan(X).sum()))
+
+
+def test_lasso_device_matches_host(dev):
+    X, y, _ = make_hf_cohort(4000, 40, seed=21, nan_frac=0.0)
+    Xt, yt = torch.as_tensor(X), torch.as_tensor(y)
+    h = SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=17).fit(Xt, yt)
+    d = SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=17).fit(Xt.to(dev), yt.to(dev))
+    assert abs(h.estimator_.alpha_ - d.estimator_.alpha_) < 1e-12
+    assert np.array_equal(h.get_support(), d.get_support())
+    assert torch.allclose(h.estimator_.coef_, d.estimator_.coef_.cpu(), atol=1e-9)
+
+
+def test_weighted_moments(dev):
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(5000, 41, generator=g, dtype=torch.float64)
+    W = torch.rand(7, 5000, generator=g, dtype=torch.float64)
+    V = torch.randn(7, 5000, generator=g, dtype=torch.float64)
+    G, a, v = ops.weighted_moments(X.to(dev), W.to(dev), V.to(dev))
+    Gr, ar, vr = ops.weighted_moments(X, W, V)
+    assert torch.allclose(G.cpu(), Gr, rtol=1e-12, atol=1e-9)
+    assert torch.allclose(a.cpu(), ar, rtol=1e-12, atol=1e-9)
+    assert torch.allclose(v.cpu(), vr, rtol=1e-12, atol=1e-9)
