@@ -43,7 +43,7 @@ def main(argv=None) -> int:
     group, rank, world = pdist.init_from_env()
     device = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     if device == "cuda":
-        device = f"cuda:{pdist.local_rank()}"
+        device = str(pdist.rank_device())
         torch.cuda.set_device(torch.device(device))
     data_dir = a.data_dir or os.getcwd()
     dev_path = os.path.join(data_dir, "develop_data.mat")

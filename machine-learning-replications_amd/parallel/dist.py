@@ -32,9 +32,9 @@ def init_from_env(backend: str = None):
         return None, 0, 1
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("HFENS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(local_rank())
+            torch.cuda.set_device(rank_device())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend)
     return dist.group.WORLD, dist.get_rank(), dist.get_world_size()
@@ -42,6 +42,15 @@ def init_from_env(backend: str = None):
 
 def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def rank_device() -> torch.device:
+    """This rank's GPU (one process per GPU).  With fewer visible GPUs than local ranks
+    (rehearsing several ranks on one card over gloo) ranks share devices round-robin."""
+    if not torch.cuda.is_available():
+        return torch.device("cpu")
+    n = torch.cuda.device_count()
+    return torch.device("cuda", local_rank() % max(1, n))
 
 
 def shutdown():
