@@ -20,6 +20,11 @@ fixed-size problem is the honest multi-GPU setting for this ensemble.
 ``value`` = development rows × steps ÷ slowest rank's time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--features F]
+
+``--config infer`` (BASELINE config 4): batched inference of the shipped checkpoint
+(``assets/hf_predict_model.pkl``) over 100M synthetic patient rows with the fused
+whole-stack HIP kernel; one step = one pass over all rows (device-resident, HIP-graph
+replay); the host-streaming (pinned H2D ∥ kernel ∥ D2H) rate is reported alongside.
 """
 from __future__ import annotations
 
@@ -44,7 +49,10 @@ def main():
     ap.add_argument("--features", type=int, default=40)
     ap.add_argument("--seed", type=int, default=2020)
     ap.add_argument("--timings", action="store_true", help="print a per-stage table to stderr")
+    ap.add_argument("--config", default="train", choices=["train", "infer"])
     a = ap.parse_args()
+    if a.config == "infer":
+        return bench_infer(a)
 
     import numpy as np
     import torch
@@ -126,6 +134,104 @@ def main():
                        "stage_seconds": {k: round(v, 4) for k, v in prof.times.items()}},
         }
         print(json.dumps(out), flush=True)
+    pdist.shutdown()
+
+
+CPU_BASELINE_INFER_ROWS_PER_S = 158e3   # BASELINE.md (B): numpy full-stack batched inference
+
+
+def synth_patients(n: int, device, seed: int = 0, chunk: int = 1 << 24):
+    """[n, 17] f32 patient rows in predict_hf.py's feature order (binary flags, NYHA 1-2,
+    FEV-like, count 0-4, age), generated on the device chunk by chunk."""
+    import torch
+    g = torch.Generator(device=device).manual_seed(seed)
+    X = torch.empty(n, 17, dtype=torch.float32, device=device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        blk = torch.randint(0, 2, (m, 17), generator=g, device=device).to(torch.float32)
+        blk[:, 6] += 1
+        blk[:, 13] = (18.6 + 4.4 * torch.randn(m, generator=g, device=device)).round()
+        blk[:, 15] = torch.randint(0, 5, (m,), generator=g, device=device).to(torch.float32)
+        blk[:, 16] = (63 + 5 * torch.randn(m, generator=g, device=device)).round()
+        X[s:e] = blk
+    return X
+
+
+def bench_infer(a):
+    import torch
+    from hfens.parallel import dist as pdist
+    from hfens.io.checkpoint import load_checkpoint
+    from hfens.infer import BatchedPredictor
+
+    group, rank, world = pdist.init_from_env()
+    dev = pdist.rank_device()
+    if dev.type != "cuda":
+        raise SystemExit("bench --config infer needs a GPU")
+    torch.cuda.set_device(dev)
+    rows = a.rows if a.rows != 10000 else 100_000_000
+    lo, hi = pdist.shard_bounds(rows, rank, world)
+    n = hi - lo
+    model = load_checkpoint(device=dev)
+    pred = BatchedPredictor(model, dev)
+    X = synth_patients(n, dev, seed=a.seed + rank)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def barrier():
+        if group is not None:
+            torch.distributed.barrier(group)
+        torch.cuda.synchronize(dev)
+
+    for _ in range(max(1, a.warmup)):
+        pred.predict_device(X, out)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pred.predict_device(X, out)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    # spot-check against the per-model path on a slice (untimed)
+    model.fused_inference = False
+    ref = model.predict_p1(X[:4096])
+    model.fused_inference = True
+    max_err = float((out[:4096].double() - ref.double()).abs().max())
+    # host streaming (untimed by the step clock, reported alongside)
+    Xh = X.cpu().pin_memory()
+    oh = torch.empty(n, dtype=torch.float32).pin_memory()
+    pred.predict_host(Xh, oh)
+    barrier()
+    t1 = time.perf_counter()
+    pred.predict_host(Xh, oh)
+    barrier()
+    t_stream = time.perf_counter() - t1
+    stream_ok = bool(torch.equal(oh[:65536], out[:65536].cpu()))
+    if group is not None:
+        t = torch.tensor([elapsed, t_stream], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
+        elapsed, t_stream = float(t[0]), float(t[1])
+    value = rows * a.steps / elapsed
+    if rank == 0:
+        out_line = {
+            "metric": "infer_rows_per_sec",
+            "value": round(value, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / CPU_BASELINE_INFER_ROWS_PER_S, 1),
+            "dtype": "fp32",
+            "data": "synthetic patient rows; shipped hf_predict_model.pkl weights",
+            "host_stream_rows_per_sec": round(rows / t_stream, 1),
+            "host_stream_matches": stream_ok,
+            "max_abs_err_vs_per_model_path": max_err,
+            "config": {"model": "hf_predict_model.pkl stack (SVC 434 SV + GBC 100 stumps + LR-L1 -> LR)",
+                       "global_batch": rows, "seq_len": 17, "parallelism": f"dp{world}",
+                       "kernel": "fused stack_infer, HIP-graph replay"},
+        }
+        print(json.dumps(out_line), flush=True)
     pdist.shutdown()
 
 

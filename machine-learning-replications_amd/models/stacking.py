@@ -16,6 +16,7 @@ from typing import List, Tuple
 
 import torch
 
+from .. import ops
 from .base import Estimator, as_tensor
 
 
@@ -89,7 +90,32 @@ class StackingClassifier(Estimator):
         dev = cols[0].device
         return torch.stack([c.to(dev, torch.float64) for c in cols], dim=1)
 
+    # fused single-kernel inference (ops.stack_infer) for the HF stack on the GPU
+    fused_inference = True
+
+    def _packed_stack(self, device):
+        key = (id(self.estimators_), id(self.final_estimator_), str(device))
+        cached = getattr(self, "_pstack", None)
+        if cached is None or cached[0] != key:
+            from ..ops.packing import pack_stack
+            cached = self._pstack = (key, pack_stack(self, device))
+        return cached[1]
+
+    def predict_p1(self, X) -> torch.Tensor:
+        """P(class 1) per row.  On the GPU, a fitted HF-shaped stack runs as ONE fused kernel
+        (scaler → SVC/Platt, trees, LR → meta LR; f32 output); otherwise per-model."""
+        X = as_tensor(X)
+        if X.is_cuda and self.fused_inference:
+            pk = self._packed_stack(X.device)
+            if pk is not None:
+                return ops.stack_infer(X, pk)
+        return self.final_estimator_.predict_proba(self.transform(X))[:, 1]
+
     def predict_proba(self, X) -> torch.Tensor:
+        X = as_tensor(X)
+        if X.is_cuda and self.fused_inference and self._packed_stack(X.device) is not None:
+            p1 = self.predict_p1(X).to(torch.float64)
+            return torch.stack([1 - p1, p1], dim=1)
         return self.final_estimator_.predict_proba(self.transform(X))
 
     def decision_function(self, X) -> torch.Tensor:

@@ -5,9 +5,10 @@ from __future__ import annotations
 import torch
 
 from . import reference as ref
-from .packing import pack_forest, pack_svs
+from .packing import pack_forest, pack_stack, pack_svs
 
-__all__ = ["rbf_decision", "svc_proba1", "tree_raw", "expit", "pack_svs", "pack_forest", "weighted_moments"]
+__all__ = ["rbf_decision", "svc_proba1", "tree_raw", "expit", "pack_svs", "pack_forest", "pack_stack",
+           "stack_infer", "weighted_moments"]
 
 
 def _c(t: torch.Tensor, dtype) -> torch.Tensor:
@@ -54,6 +55,37 @@ def tree_raw(x, feature, threshold, left, right, value, init: float, lr: float, 
                          pk.max_nodes, float(init), float(lr), out.data_ptr(), stream_ptr(x.device))
         return out
     return ref.tree_raw(x, feature, threshold, left, right, value, init, lr)
+
+
+def stack_infer(x, pk, out=None, grid: int = 0, stream=None):
+    """Fused P(class 1) of the whole HF stack (one kernel, one pass over ``x``).
+    ``x``: [n, F] f32 or f64; ``pk``: :class:`PackedStack` on ``x``'s device.  Returns f32 on
+    the GPU (written into ``out`` if given), f64 on the host."""
+    if x.is_cuda:
+        from . import ext, stream_ptr
+        if x.dtype not in (torch.float32, torch.float64):
+            x = x.to(torch.float32)
+        x = x.contiguous()
+        n, F = x.shape
+        if F != pk.F:
+            raise ValueError(f"stack_infer: X has {F} features, model has {pk.F}")
+        if out is None:
+            out = torch.empty(n, dtype=torch.float32, device=x.device)
+        elif out.dtype != torch.float32 or out.numel() < n or not out.is_contiguous():
+            raise ValueError("stack_infer: out must be a contiguous f32 buffer of >= n elements")
+        f, s, st = pk.forest, pk.sv, pk.stumps
+        ext().stack_infer(x.data_ptr(), int(x.dtype == torch.float64), n, F, s.mp, f.n_trees, f.max_nodes,
+                          -pk.gamma * 1.4426950408889634, pk.svc_b, pk.probA, pk.probB, pk.gb_init,
+                          pk.gb_lr, pk.lr_b, pk.meta_w[0], pk.meta_w[1], pk.meta_w[2], pk.meta_b,
+                          pk.mean.data_ptr(), pk.inv_scale.data_ptr(), s.svt.data_ptr(), s.sn.data_ptr(),
+                          s.coef.data_ptr(), f.nodes.data_ptr(), f.values.data_ptr(), pk.lr_w.data_ptr(),
+                          st.off.data_ptr() if st is not None else 0,
+                          st.pairs.data_ptr() if st is not None else 0,
+                          st.base if st is not None else 0.0,
+                          out.data_ptr(), int(grid),
+                          stream if stream is not None else stream_ptr(x.device))
+        return out[:n]
+    return ref.stack_infer(x, pk)
 
 
 def expit(x):

@@ -11,6 +11,8 @@ void rbf_decision(uintptr_t Z, int n, int F, uintptr_t SVt, uintptr_t sn, uintpt
 void svc_proba1(uintptr_t dec, uintptr_t out, int n, double A, double B, uintptr_t stream);
 void forest_raw(uintptr_t X, int n, int F, uintptr_t nodes, uintptr_t values, int T, int K,
                 double init, double lr, uintptr_t out, uintptr_t stream);
+// stack.hip
+long long stack_infer_lds(int F, int mp, int nodes_total);
 #define HFENS_DECLS
 #include "decls.inc"
 #undef HFENS_DECLS
@@ -23,6 +25,7 @@ PYBIND11_MODULE(_hfens_hip, m) {
   m.def("rbf_decision", &hfens::rbf_decision);
   m.def("svc_proba1", &hfens::svc_proba1);
   m.def("forest_raw", &hfens::forest_raw);
+  m.def("stack_infer_lds", &hfens::stack_infer_lds);
 #define HFENS_DEFS
 #include "decls.inc"
 #undef HFENS_DEFS

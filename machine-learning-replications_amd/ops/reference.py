@@ -109,3 +109,33 @@ def tree_raw(x: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor, le
 
 def expit(x: torch.Tensor) -> torch.Tensor:
     return torch.sigmoid(x)
+
+
+# ----------------------------------------------------------------------------- fused stack
+def stack_infer(x: torch.Tensor, pk) -> torch.Tensor:
+    """fp64 reference of the fused ``stack_infer`` kernel on a :class:`PackedStack` (host
+    tensors): scaler → RBF SVC (Platt + coupling) / trees / L1-LR → meta LR, P(class 1)."""
+    x = x.to(torch.float64)
+    F = pk.F
+    z = (x - pk.mean.to(torch.float64)) * pk.inv_scale.to(torch.float64)
+    sv = pk.sv.svt[:F].t().to(torch.float64)
+    dec = rbf_decision(z, sv, pk.sv.coef.to(torch.float64), pk.gamma, pk.svc_b)
+    p_svc = svc_proba1(dec, pk.probA, pk.probB)
+    if pk.stumps is not None:
+        st = pk.stumps
+        x32 = x.to(torch.float32).to(torch.float64)
+        raw = torch.full((x.shape[0],), st.base, dtype=torch.float64)
+        off = st.off.tolist()
+        for f in range(F):
+            for j in range(off[f], off[f + 1]):
+                t, d = float(st.pairs[j, 0]), float(st.pairs[j, 1])
+                raw += (x32[:, f] > t).to(torch.float64) * d
+    else:
+        nd = pk.forest.nodes.reshape(pk.forest.n_trees, pk.forest.max_nodes, 4)
+        thr = nd[..., 3].contiguous().view(torch.float32).to(torch.float64)
+        raw = tree_raw(x, nd[..., 0], thr, nd[..., 1], nd[..., 2],
+                       pk.forest.values.reshape(pk.forest.n_trees, -1), pk.gb_init, pk.gb_lr)
+    p_gbc = torch.sigmoid(raw)
+    p_lg = torch.sigmoid(x @ pk.lr_w.to(torch.float64) + pk.lr_b)
+    w0, w1, w2 = pk.meta_w
+    return torch.sigmoid(pk.meta_b + w0 * p_svc + w1 * p_gbc + w2 * p_lg)
