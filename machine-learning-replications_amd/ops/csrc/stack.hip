@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
       float v = 0.f;
       if (j < cl) {
         if (k < 2 * KS) v = k < F ? M.svt[(size_t)k * mp + c0 + j] : 0.f;
-        else if (k == 2 * KS) v = M.sn[c0 + j];
+        else if (k == 2 * KS) v = M.ngl2e * M.sn[c0 + j];
         else v = M.coef[c0 + j];
       }
       lds[i] = v;
@@ -175,7 +175,35 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
     }
     zna += __shfl_xor(zna, 32, kWave);
     znb += __shfl_xor(znb, 32, kWave);
+    // exponent of exp(−γ‖sv−z‖²) in base 2: (γ'·‖sv‖²) + (γ'·‖z‖²) + (−2γ')·(sv·z), γ' = −γ·log2 e;
+    // ‖sv‖² is staged pre-scaled.  No clamp at 0: a rounding-negative distance only turns
+    // exp2 into 1+ε, exactly like the double-precision kernel evaluation it mirrors.
+    const float zsa = M.ngl2e * zna, zsb = M.ngl2e * znb, k2 = -2.f * M.ngl2e;
     float pa = 0.f, pb = 0.f;
+    auto mma = [&](int t, f32x16& A, f32x16& B) {
+      A = f32x16{0.f};
+      B = f32x16{0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float sv = sv_l[(2 * s + hi) * CH + t + r32];
+        A = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, za[s], A, 0, 0, 0);
+        B = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, zb[s], B, 0, 0, 0);
+      }
+    };
+    // accumulator reg r ↔ SV t + (r&3) + 8(r>>2) + 4·hi ; column (lane&31) ↔ data row
+    auto epi = [&](int t, const f32x16& A, const f32x16& B) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b0 = t + 8 * g + 4 * hi;
+        const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[b0]);
+        const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[b0]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pa = fmaf(cfv[q], __builtin_amdgcn_exp2f(fmaf(k2, A[4 * g + q], snv[q] + zsa)), pa);
+          pb = fmaf(cfv[q], __builtin_amdgcn_exp2f(fmaf(k2, B[4 * g + q], snv[q] + zsb)), pb);
+        }
+      }
+    };
     for (int c = 0; c < nch; ++c) {
       if (nch > 1) {  // block-uniform: restage chunk c (chunk 0 is resident on entry)
         if (c > 0 || base != (long long)blockIdx.x * W) {
@@ -185,28 +213,12 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
         }
       }
       const int cl = min(CH, mp - c * CH);
+      // (a software-pipelined variant — MFMAs of tile t+32 issued before the epilogue of t —
+      // measured 9 % slower: +49 VGPRs cost a wave/SIMD of occupancy)
       for (int t = 0; t < cl; t += 32) {
-        f32x16 acc_a = {0.f}, acc_b = {0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const float sv = sv_l[(2 * s + hi) * CH + t + r32];
-          acc_a = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, za[s], acc_a, 0, 0, 0);
-          acc_b = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, zb[s], acc_b, 0, 0, 0);
-        }
-        // accumulator reg r ↔ SV t + (r&3) + 8(r>>2) + 4·hi ; column (lane&31) ↔ data row
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int b0 = t + 8 * g + 4 * hi;
-          const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[b0]);
-          const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[b0]);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float da = fmaxf(fmaf(-2.f, acc_a[4 * g + q], snv[q] + zna), 0.f);
-            const float db = fmaxf(fmaf(-2.f, acc_b[4 * g + q], snv[q] + znb), 0.f);
-            pa = fmaf(cfv[q], __builtin_amdgcn_exp2f(M.ngl2e * da), pa);
-            pb = fmaf(cfv[q], __builtin_amdgcn_exp2f(M.ngl2e * db), pb);
-          }
-        }
+        f32x16 A, B;
+        mma(t, A, B);
+        epi(t, A, B);
       }
     }
     pa += __shfl_xor(pa, 32, kWave);
@@ -320,17 +332,19 @@ static void stack_go(const TX* X, long long n, const StackModel& M, const StackP
   launch_check();
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
 // Pick the workgroup size that keeps the most waves resident per CU: one workgroup shares one
 // LDS copy of the SVs, so wider workgroups trade LDS for occupancy.  Only shapes that compile
 // without VGPR spills are candidates (KS ≤ 9: 8 or 12 waves; 12 waves fit 152 VGPRs at 3
-// waves/SIMD); HFENS_STACK_WAVES=8|12|16 forces a shape (tuning runs).
+// waves/SIMD — measured 4.9 G rows/s vs 4.7 for 8); HFENS_STACK_WAVES=8|12|16 forces a shape.
 template <int KS, typename TX>
 static void stack_pick(const TX* X, long long n, const StackModel& M, int grid, float* out,
                        hipStream_t st) {
-  static const int forced = [] {
-    const char* e = std::getenv("HFENS_STACK_WAVES");
-    return e ? std::atoi(e) : 0;
-  }();
+  static const int forced = env_int("HFENS_STACK_WAVES", 0);
   constexpr bool narrow = KS <= 9;
   const StackPlan p8 = stack_plan<KS, 8, TX>(M);
   StackPlan p12, p16;
