@@ -18,6 +18,7 @@ path mirrors every step in numpy (used on CPU and by the kernel tests).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -297,29 +298,41 @@ def _dev_struct(arr: np.ndarray, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
-    from .. import ops
-    E = ops.ext()
-    s = ops.stream_ptr(device)
-    live = [p for p in probs if p.rows is not None]
-    F = Zs[0].shape[1]
-    zcat = torch.cat([Zs[p.fit][p.rows].to(torch.float32) for p in live]).contiguous()
+_WS_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("Cp", "<f8"),
+                   ("Cn", "<f8"), ("ngl2e", "<f4"), ("pad", "<i4")])
+_WS_Q = 128              # working-set size compiled into svm_ws.hip
+_WS_STATE_BYTES = 80     # sizeof(WsState)
+
+# Device solver: "exact" = libsvm's pair sequence (smo_batch on a stored Gram), "ws" = working-set
+# decomposition with the RBF recomputed on the MFMA (ws_*: O(n) memory, no n² Gram).  Measured on
+# the bench's 36-problem batches (scripts/ws_diag.py, profiles/r1_svm_solvers.md): 10k rows exact
+# 67 ms vs ws 71 ms, 20k rows exact 272 ms vs ws 821 ms — the one-pair-per-iteration exact solver
+# stays the default ("auto"); "ws" is the low-memory path.
+SOLVER = os.environ.get("HFENS_SVM_SOLVER", "auto")
+WS_MIN_POINTS = int(os.environ.get("HFENS_SVM_WS_MIN", str(1 << 30)))
+
+
+def _pick_solver(max_l: int) -> str:
+    if SOLVER in ("exact", "ws"):
+        return SOLVER
+    return "ws" if max_l >= WS_MIN_POINTS else "exact"
+
+
+def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     g = np.zeros(len(live), _GRAM_DT)
     sm = np.zeros(len(live), _SMO_DT)
-    zoff = koff = aoff = 0
+    koff = 0
     for k, p in enumerate(live):
         l = int(p.rows.numel())
         ld = (l + 63) // 64 * 64
-        g[k] = (zoff, koff, l, ld, -p.gamma * 1.4426950408889634, 0)
-        sm[k] = (koff, aoff, l, ld, p.npos, 0, p.Cp, p.Cn)
-        zoff += l
+        g[k] = (zoffs[k], koff, l, ld, -p.gamma * 1.4426950408889634, 0)
+        sm[k] = (koff, aoffs[k], l, ld, p.npos, 0, p.Cp, p.Cn)
         koff += l * ld
-        aoff += l
     max_l = max(int(p.rows.numel()) for p in live)
     K = torch.empty(koff, dtype=torch.float32, device=device)
     gdev = _dev_struct(g, device)
     E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
-    alpha = torch.empty(aoff, dtype=torch.float64, device=device)
+    alpha = torch.empty(aoffs[-1], dtype=torch.float64, device=device)
     rho = torch.empty(len(live), dtype=torch.float64, device=device)
     iters = torch.empty(len(live), dtype=torch.int32, device=device)
     gap = torch.empty(len(live), dtype=torch.float64, device=device)
@@ -328,16 +341,89 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
     E.smo_batch(sdev.data_ptr(), len(live), max_l, K.data_ptr(), alpha.data_ptr(), eps, max_iter,
                 rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), s)
     del K
+    return alpha, rho, iters
+
+
+WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
+WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", str(8 * _WS_Q)))
+
+
+def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=16):
+    P = len(live)
+    arr = np.zeros(P, _WS_DT)
+    for k, p in enumerate(live):
+        arr[k] = (zoffs[k], aoffs[k], int(p.rows.numel()), p.npos, p.Cp, p.Cn,
+                  -p.gamma * 1.4426950408889634, 0)
+    max_l = int(arr["l"].max())
+    n = aoffs[-1]
+    pdev = _dev_struct(arr, device)
+    zn = torch.empty(n, dtype=torch.float32, device=device)
+    alpha = torch.empty(n, dtype=torch.float64, device=device)
+    G = torch.empty(n, dtype=torch.float64, device=device)
+    states = torch.zeros(P * _WS_STATE_BYTES // 4, dtype=torch.int32, device=device)
+    ks = (F + 1) // 2
+    Fp = 2 * (4 if ks <= 4 else 9 if ks <= 9 else 12 if ks <= 12 else 16 if ks <= 16 else 32)
+    wsz = torch.zeros(P * Fp * _WS_Q, dtype=torch.float32, device=device)
+    wsn = torch.zeros(P * _WS_Q, dtype=torch.float32, device=device)
+    wdc = torch.zeros(P * _WS_Q, dtype=torch.float32, device=device)
+    max_outer = 50_000 if max_iter_cap is None else int(max_iter_cap)
+    max_inner = WS_MAX_INNER
+    keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
+    hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
+    gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)
+    E.ws_init(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
+              states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
+    done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
+    outer = 0
+    while outer < max_outer:
+        E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
+                   states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), keys.data_ptr(), n,
+                   hist.data_ptr(), gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC, steps_per_check, s)
+        outer += steps_per_check
+        if bool((done_view != 0).all()):
+            break
+    rho = torch.empty(P, dtype=torch.float64, device=device)
+    iters = torch.empty(P, dtype=torch.int32, device=device)
+    inner = torch.empty(P, dtype=torch.int64, device=device)
+    gap = torch.empty(P, dtype=torch.float64, device=device)
+    E.ws_finalize(pdev.data_ptr(), P, states.data_ptr(), alpha.data_ptr(), G.data_ptr(), rho.data_ptr(),
+                  iters.data_ptr(), inner.data_ptr(), gap.data_ptr(), s)
+    cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 8:20].cpu().contiguous().view(torch.int64).numpy()
+    LAST_WS_STATS.update(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
+                         cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
+                         cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5])
+    return alpha, rho, iters
+
+
+LAST_WS_STATS: dict = {}
+
+
+def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
+    from .. import ops
+    E = ops.ext()
+    s = ops.stream_ptr(device)
+    live = [p for p in probs if p.rows is not None]
+    F = Zs[0].shape[1]
+    zcat = torch.cat([Zs[p.fit][p.rows].to(torch.float32) for p in live]).contiguous()
+    zoffs, aoffs = [], [0]
+    for p in live:
+        zoffs.append(aoffs[-1])
+        aoffs.append(aoffs[-1] + int(p.rows.numel()))
+    aoffs_start = aoffs[:-1]
+    max_l = max(int(p.rows.numel()) for p in live)
+    solver = _pick_solver(max_l)
+    solve = _solve_ws if solver == "ws" else _solve_exact
+    alpha, rho, iters = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)
     out = {}
     for k, p in enumerate(live):
-        a0 = int(sm[k]["aoff"])
-        out[id(p)] = (alpha[a0:a0 + int(sm[k]["l"])], rho[k], iters[k])
+        a0 = aoffs_start[k]
+        out[id(p)] = (alpha[a0:a0 + int(p.rows.numel())], rho[k], iters[k])
     # ---- Platt held-out decision values of every CV sub-model: one batched launch
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
     if platt:
-        sign = torch.empty(aoff, dtype=torch.float32, device=device)
+        sign = torch.empty(aoffs[-1], dtype=torch.float32, device=device)
         for k, p in enumerate(live):
-            a0, l = int(sm[k]["aoff"]), int(sm[k]["l"])
+            a0, l = aoffs_start[k], int(p.rows.numel())
             sign[a0:a0 + p.npos] = 1.0
             sign[a0 + p.npos:a0 + l] = -1.0
         coef = (sign * alpha.to(torch.float32)).contiguous()
@@ -348,7 +434,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
         hoff = 0
         for i, (k, p) in enumerate(platt):
             h = int(p.held_rows.numel())
-            dt[i] = (int(g[k]["zoff"]), hoff, int(g[k]["l"]), h, -p.gamma * 1.4426950408889634, per)
+            dt[i] = (zoffs[k], hoff, int(p.rows.numel()), h, -p.gamma * 1.4426950408889634, per)
             hoff += h
         part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
         ddev = _dev_struct(dt, device)

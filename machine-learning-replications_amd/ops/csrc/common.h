@@ -79,6 +79,42 @@ __device__ __forceinline__ float readlane_f32(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// Wave-wide u32 max on DPP + CDNA4 half-swaps (no LDS round trips): quad_perm xor 1 / xor 2,
+// row_half_mirror (8), row_mirror (16), v_permlane16_swap (32), v_permlane32_swap (64).
+// Every lane receives the result.
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = max((unsigned)r[0], (unsigned)r[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return max((unsigned)q[0], (unsigned)q[1]);
+}
+
+// order-preserving f32 ↔ u32 (larger float ⇒ larger key; finite floats map to ≥ 0x00800000)
+__device__ __forceinline__ unsigned f32_okey(float x) {
+  const unsigned u = __float_as_uint(x);
+  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+}
+__device__ __forceinline__ float f32_from_okey(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+
+// exact wave max of doubles: order-preserving u64 key, max of the high words, then of the low
+// words among the lanes holding that high word
+__device__ __forceinline__ double wave_max_f64_exact(double x) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  u ^= (u >> 63) ? ~0ull : 0x8000000000000000ull;
+  const unsigned hi = (unsigned)(u >> 32), lo = (unsigned)u;
+  const unsigned mh = wave_max_u32(hi);
+  const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
+  unsigned long long k = ((unsigned long long)mh << 32) | ml;
+  k = (k >> 63) ? (k ^ 0x8000000000000000ull) : ~k;
+  return __longlong_as_double((long long)k);
+}
+
 __device__ __forceinline__ float fast_exp(float x) {  // e^x via v_exp_f32 (2^x)
   return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
 }

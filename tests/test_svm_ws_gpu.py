@@ -1,0 +1,60 @@
+"""Working-set decomposition SMO (svm_ws.hip) vs libsvm (through sklearn): the solution must meet
+libsvm's KKT stopping rule, reach the same dual objective to O(eps), and give the same model."""
+import numpy as np
+import pytest
+import torch
+
+from hfens.models import smo
+from hfens.models.svc import SVC
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, F, seed):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, F, generator=g, dtype=torch.float64)
+    w = torch.randn(F, generator=g, dtype=torch.float64)
+    logit = X @ w / F ** 0.5 + 0.5 * torch.randn(n, generator=g, dtype=torch.float64) - 1.0
+    y = (logit > 0).to(torch.float64)
+    return X, y
+
+
+def _dual(Z, y_pm, coef_sv, sv_idx, gamma):
+    Zs = Z[sv_idx]
+    d2 = ((Zs[:, None, :] - Zs[None, :, :]) ** 2).sum(-1)
+    K = np.exp(-gamma * d2)
+    a = np.abs(coef_sv)
+    return 0.5 * coef_sv @ K @ coef_sv - a.sum()
+
+
+@pytest.mark.parametrize("n,F", [(1500, 17), (6000, 17), (4000, 40)])
+def test_ws_solver_matches_libsvm(dev, monkeypatch, n, F):
+    from sklearn.svm import SVC as SK
+    monkeypatch.setattr(smo, "SOLVER", "ws")
+    X, y = _data(n, F, n + F)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).numpy()
+    sk = SK(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.numpy())
+    m = SVC(class_weight="balanced", probability=True, random_state=2020)
+    m.fit(torch.as_tensor(Z).to(dev), y.to(dev))
+    st = smo.LAST_WS_STATS
+    assert (st["gap"] < 1e-3).all(), st["gap"]          # libsvm's stopping rule, over all points
+    gamma = 1.0 / (F * Z.var())
+    ours = _dual(Z, None, m._dual_coef_[0].cpu().numpy(), m.support_.cpu().numpy(), gamma)
+    theirs = _dual(Z, None, sk.dual_coef_[0], sk.support_, gamma)
+    assert abs(ours - theirs) <= 1e-3 * abs(theirs)
+    d = m.decision_function(torch.as_tensor(Z).to(dev)).cpu().numpy()
+    assert np.abs(d - sk.decision_function(Z)).max() < 2e-2
+    p = m.predict_proba(torch.as_tensor(Z).to(dev))[:, 1].cpu().numpy()
+    assert np.abs(p - sk.predict_proba(Z)[:, 1]).max() < 1e-2
+    assert abs(int(m._n_support.sum()) - int(sk.n_support_.sum())) <= 0.02 * n
+
+
+def test_ws_and_exact_solvers_agree(dev, monkeypatch):
+    X, y = _data(3000, 17, 5)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    out = {}
+    for solver in ("exact", "ws"):
+        monkeypatch.setattr(smo, "SOLVER", solver)
+        m = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.to(dev))
+        out[solver] = m.predict_proba(Z)[:, 1].cpu()
+    assert (out["exact"] - out["ws"]).abs().max() < 1e-2
