@@ -15,6 +15,7 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 import numpy as np
+import torch
 
 # (name, kind, params) — kind: "bin" p | "gauss" (mean, sd) | "ord" (lo, hi, p_nonzero)
 TABLE_S1: List[Tuple[str, str, tuple]] = [
@@ -141,7 +142,8 @@ def make_hf_cohort(n_rows: int, n_features: int = 40, seed: int = 0, nan_frac: f
         v = cols[nm]
         lin += c * (v - v.mean())
     extra = [nm for nm in full_names if nm not in MODEL_FEATURES][:5]
-    wts = np.random.default_rng(seed + 7919).normal(0, 0.3, len(extra))
+    # fixed label model: every draw (dev / held-out / any seed) shares the same outcome model
+    wts = np.random.default_rng(7919).normal(0, 0.3, len(extra))
     for nm, c in zip(extra, wts):
         v = cols[nm]
         lin += c * (v - v.mean()) / (v.std() + 1e-12)
@@ -169,3 +171,98 @@ def make_dev_select(n_rows: int, n_features: int = 40, seed: int = 2020, nan_fra
     Xd, yd, names = make_hf_cohort(n_rows, n_features, seed, nan_frac)
     Xs, ys, _ = make_hf_cohort(n_rows, n_features, seed + 1, nan_frac)
     return Xd, yd, Xs, ys, names
+
+
+# ----------------------------------------------------------------------------- device generator
+_CHUNK = 1 << 16
+
+
+def _label_model(n_features: int, seed: int):
+    """Coefficients (per model column, on standardized columns) and the intercept for ~20 %
+    positives — the same structure as ``make_hf_cohort``'s label model."""
+    names = feature_order(n_features)
+    spec = {r[0]: r for r in TABLE_S1}
+    coef = np.zeros(n_features)
+    for i, nm in enumerate(names):
+        if nm in MODEL_FEATURES:
+            coef[i] = MODEL_COEF[MODEL_FEATURES.index(nm)]
+    extra = [i for i, nm in enumerate(names) if nm not in MODEL_FEATURES][:5]
+    coef[extra] = np.random.default_rng(7919).normal(0, 0.3, len(extra))
+    mean = np.zeros(n_features)
+    sd = np.ones(n_features)
+    for i, nm in enumerate(names):
+        kind, params = spec[nm][1], spec[nm][2]
+        if kind == "bin":
+            mean[i], sd[i] = params[0], np.sqrt(params[0] * (1 - params[0]))
+        elif kind == "gauss":
+            mean[i], sd[i] = params
+        elif kind == "ord":
+            lo, hi, p = params
+            mean[i] = (1 - p) * lo + p * (max(lo, 1) + hi) / 2
+            sd[i] = max(1e-3, np.sqrt(p) * (hi - lo) / 2)
+        else:   # nyha = 1 + dyspnea
+            pd_ = spec["Dyspnea"][2][0]
+            mean[i], sd[i] = 1 + pd_, np.sqrt(pd_ * (1 - pd_))
+    # model features enter unstandardized in make_hf_cohort (× signal 2.5); extras standardized
+    scale = np.where([nm in MODEL_FEATURES for nm in names], 1.0, 1.0 / sd)
+    w = 2.5 * coef * scale
+    return names, w, mean
+
+
+def make_hf_cohort_device(n_total: int, n_features: int = 40, seed: int = 0, rows=None, device="cuda",
+                          prevalence: float = 0.2):
+    """Table-S1-shaped rows generated ON the device, without NaNs: ``(X f32 [e-s, F], y f32)``
+    for global rows ``rows = (s, e)`` of an ``n_total``-row cohort.  Rows come in fixed 64k-row
+    chunks each seeded by (seed, chunk), so any row range — a rank's data-parallel shard — is
+    the same slice of the same global cohort whatever the number of ranks (strong scaling)."""
+    s, e = (0, n_total) if rows is None else rows
+    names, w, mean = _label_model(n_features, seed)
+    spec = {r[0]: r for r in TABLE_S1}
+    kinds = [(spec[nm][1], spec[nm][2]) for nm in names]
+    dys = names.index("Dyspnea") if "Dyspnea" in names else None
+    wt = torch.as_tensor(w, dtype=torch.float32, device=device)
+    mu = torch.as_tensor(mean, dtype=torch.float32, device=device)
+    # intercept for the prevalence: bisection on a fixed 64k probe chunk
+    probe_X, _ = _device_chunk(kinds, dys, n_features, seed, -1, _CHUNK, device, None, 0.0)
+    lin = (probe_X - mu) @ wt
+    lo, hi = -20.0, 20.0
+    for _ in range(50):
+        mid = 0.5 * (lo + hi)
+        if float(torch.sigmoid(lin + mid).mean()) > prevalence:
+            hi = mid
+        else:
+            lo = mid
+    b0 = 0.5 * (lo + hi)
+    Xs, ys = [], []
+    for c in range(s // _CHUNK, (e + _CHUNK - 1) // _CHUNK):
+        Xc, yc = _device_chunk(kinds, dys, n_features, seed, c, _CHUNK, device, (wt, mu), b0)
+        c0 = c * _CHUNK
+        a, z = max(s, c0) - c0, min(e, c0 + _CHUNK) - c0
+        Xs.append(Xc[a:z])
+        ys.append(yc[a:z])
+    return torch.cat(Xs), torch.cat(ys)
+
+
+def _device_chunk(kinds, dys, F, seed, c, m, device, lab, b0):
+    g = torch.Generator(device=device).manual_seed((seed * 1_000_003 + c + 17) & 0x7FFFFFFFFFFFFFFF)
+    X = torch.empty(m, F, dtype=torch.float32, device=device)
+    U = torch.rand(m, F, generator=g, device=device)
+    N = torch.randn(m, F, generator=g, device=device)
+    for j, (kind, params) in enumerate(kinds):
+        if kind == "bin":
+            X[:, j] = (U[:, j] < params[0]).float()
+        elif kind == "gauss":
+            X[:, j] = torch.clamp(torch.round((params[0] + params[1] * N[:, j]) * 10) / 10, min=0.0)
+        elif kind == "ord":
+            lo_, hi_, p = params
+            k = torch.floor(N[:, j].abs() * 1e4 % (hi_ - max(lo_, 1) + 1)) + max(lo_, 1)
+            X[:, j] = torch.where(U[:, j] < p, k, torch.full_like(k, float(lo_)))
+    for j, (kind, _) in enumerate(kinds):
+        if kind == "nyha":
+            X[:, j] = 1.0 + (X[:, dys] if dys is not None else 0.0)
+    y = None
+    if lab is not None:
+        wt, mu = lab
+        p = torch.sigmoid((X - mu) @ wt + b0)
+        y = (torch.rand(m, generator=g, device=device) < p).float()
+    return X, y

@@ -36,13 +36,49 @@ def _qshift(n_total: int) -> int:
     return 40 if n_total <= (1 << 22) else 32
 
 
+# ============================================================================ bagging RNG
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64_t(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64 on int64 tensors (two's-complement wraparound = mod 2^64)."""
+    def srl(v, k):
+        return (v >> k) & ((1 << (64 - k)) - 1)
+    x = x + torch.tensor(0x9E3779B97F4A7C15 - (1 << 64), dtype=torch.int64, device=x.device)
+    x = (x ^ srl(x, 30)) * torch.tensor(0xBF58476D1CE4E5B9 - (1 << 64), dtype=torch.int64, device=x.device)
+    x = (x ^ srl(x, 27)) * torch.tensor(0x94D049BB133111EB - (1 << 64), dtype=torch.int64, device=x.device)
+    return x ^ srl(x, 31)
+
+
+def bag_mask(seeds: torch.Tensor, stage: int, gidx: torch.Tensor, subsample: float) -> torch.Tensor:
+    """[B, n] in-bag mask of stage ``stage`` (mirror of gbdt.hip ``gb_in_bag``)."""
+    thr = int(round(subsample * 16777216.0))
+    k = _splitmix64_t((torch.as_tensor(stage, dtype=torch.int64) << 40) ^ gidx.to(torch.int64))
+    h = _splitmix64_t(seeds.to(torch.int64)[:, None] ^ k[None, :])
+    return ((h >> 40) & 0xFFFFFF) < thr
+
+
+def _seed_u64(random_state) -> int:
+    """Per-model bagging seed (the counter-based stream is ours, not sklearn's RandomState)."""
+    v = 0 if random_state is None else int(random_state)
+    return (v * 0x9E3779B97F4A7C15 + 0xD1B54A32D192ED03) & _M64
+
+
 # ============================================================================ host mirror
 class _HostKernels:
     """Plain-PyTorch mirror of gbdt.hip (same fixed-point semantics)."""
 
     @staticmethod
     def apply_prep(st, prev, t):
-        raw, w, y = st.raw, st.w, st.y
+        raw, y = st.raw, st.y
+        w = wp = st.w
+        if st.subsample < 1.0:
+            gidx = torch.arange(st.n, device=raw.device) + st.row_off
+            w = st.w * bag_mask(st.seeds, t, gidx, st.subsample)
+            wp = st.w * bag_mask(st.seeds, t - 1, gidx, st.subsample) if t > 0 else st.w
+            st.wt = w
+            if t < st.T:
+                st.bagw[t] = w.double().sum(1)
         if prev is not None:
             feat, blo, value = prev
             nd = st.node
@@ -53,12 +89,12 @@ class _HostKernels:
             nd = torch.where(split, 2 * nd + side, nd)
             p0 = torch.sigmoid(raw)
             r0 = y[None] - p0
-            q = torch.round(w * r0 * r0 * st.qscale).to(torch.int64) * (w > 0)
+            q = torch.round(wp * r0 * r0 * st.qscale).to(torch.int64) * (wp > 0)
             st.r2[t - 1].scatter_add_(1, nd, q)
             raw = raw + st.lr * value.gather(1, nd)
             st.raw = raw
             l1p = torch.where(raw > 0, raw + torch.log1p(torch.exp(-raw)), torch.log1p(torch.exp(raw)))
-            dq = torch.round(w * (-2.0) * (y[None] * raw - l1p) * st.dscale).to(torch.int64) * (w > 0)
+            dq = torch.round(wp * (-2.0) * (y[None] * raw - l1p) * st.dscale).to(torch.int64) * (wp > 0)
             st.dev[t - 1] += dq.sum(1)
         p = torch.sigmoid(st.raw)
         r = y[None] - p
@@ -76,10 +112,10 @@ class _HostKernels:
         qs = st.qscale
         qg = torch.round(st.g.double() * qs).to(torch.int64)
         qh = torch.round(st.h.double() * qs).to(torch.int64)
-        qw = torch.round(st.w.double() * qs).to(torch.int64)
+        qw = torch.round(st.wcur.double() * qs).to(torch.int64)
         for b in range(B):
             nd = st.node[b] - node0
-            ok = (nd >= 0) & (nd < NL) & (st.w[b] > 0)
+            ok = (nd >= 0) & (nd < NL) & (st.wcur[b] > 0)
             rows = ok.nonzero().squeeze(1)
             if rows.numel() == 0:
                 continue
@@ -165,8 +201,8 @@ class _HostKernels:
         fb = st.bins[f.clamp(min=0).long(), torch.arange(st.n, device=nd.device)[None, :].expand_as(f)]
         child = 2 * nd + torch.where(fb.to(torch.int64) <= st.blo[t].gather(1, nd).to(torch.int64), 1, 2)
         new = torch.where(inl, child, nd)
-        r = torch.where(st.w > 0, st.g.double() / st.w.clamp(min=1e-30), torch.zeros_like(st.raw))
-        q = torch.round(st.w * r * r * st.qscale).to(torch.int64) * ((st.w > 0) & inl)
+        r = torch.where(st.wcur > 0, st.g.double() / st.wcur.clamp(min=1e-30), torch.zeros_like(st.raw))
+        q = torch.round(st.wcur * r * r * st.qscale).to(torch.int64) * ((st.wcur > 0) & inl)
         st.r2[t].scatter_add_(1, new, q)
         st.node = new
 
@@ -200,6 +236,15 @@ class _State:
     stats: torch.Tensor
     r2: torch.Tensor
     dev: torch.Tensor
+    subsample: float = 1.0
+    seeds: Optional[torch.Tensor] = None   # [B] int64 (u64 bit patterns) bagging seeds
+    row_off: int = 0                       # global index of local row 0 (DP shards)
+    wt: Optional[torch.Tensor] = None      # [B, n] this stage's in-bag weights (subsample < 1)
+    bagw: Optional[torch.Tensor] = None    # [T, B] Σ in-bag weight per stage (train_score_ norm.)
+
+    @property
+    def wcur(self) -> torch.Tensor:
+        return self.wt if self.wt is not None else self.w
 
 
 def _check_same(models, attrs):
@@ -222,8 +267,11 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
                          "min_samples_split", "subsample", "max_bins", "loss", "criterion"))
     if m0.loss not in ("deviance", "log_loss") or m0.criterion != "friedman_mse":
         raise NotImplementedError("binomial deviance with friedman_mse only")
-    if m0.subsample != 1.0 or m0.max_features not in (None, "auto"):
-        raise NotImplementedError("subsample<1 / max_features are not supported by the batched fit")
+    if m0.max_features not in (None, "auto"):
+        raise NotImplementedError("max_features is not supported by the batched fit")
+    subsample = float(m0.subsample)
+    if not 0.0 < subsample <= 1.0:
+        raise ValueError("subsample must be in (0, 1]")
     dev = X.device
     n, F = X.shape
     B = len(models)
@@ -267,6 +315,15 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         stats=torch.zeros(T, B, NN, 4, dtype=torch.int64, device=dev),
         r2=torch.zeros(T, B, NN, dtype=torch.int64, device=dev),
         dev=torch.zeros(T, B, dtype=torch.int64, device=dev))
+    if subsample < 1.0:
+        st.subsample = subsample
+        st.seeds = torch.tensor([_seed_u64(m.random_state) - (1 << 64) if _seed_u64(m.random_state) >= 1 << 63
+                                 else _seed_u64(m.random_state) for m in models], dtype=torch.int64, device=dev)
+        st.wt = torch.empty_like(w)
+        st.bagw = torch.zeros(T, B, dtype=torch.float64, device=dev)
+        if group is not None:
+            from ..parallel import dist as pdist
+            st.row_off = pdist.row_offset(n, group, dev)[0]
     if X.is_cuda:
         _run_device(st, group)
     else:
@@ -314,6 +371,9 @@ def _run_device(st: _State, group):
     nb_ptr = st.bm.nbins.data_ptr()
     H = torch.empty(st.B * (2 ** (st.D - 1)) * st.F * 256 * 3, dtype=torch.int64, device=st.raw.device)
     scratch = torch.zeros(st.B, st.NN, dtype=torch.int64, device=st.raw.device)
+    wt_ptr = st.wt.data_ptr() if st.wt is not None else 0
+    seeds_ptr = st.seeds.data_ptr() if st.seeds is not None else 0
+    wcur = st.wcur
     for t in range(st.T + 1):
         if t > 0:
             pf, pb, pv = st.feat[t - 1], st.blo[t - 1], st.value[t - 1]
@@ -325,9 +385,11 @@ def _run_device(st: _State, group):
         E.gbdt_apply_prep(st.B, st.n, st.F, st.NN, st.bins.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
                           st.raw.data_ptr(), st.g.data_ptr(), st.h.data_ptr(), st.node.data_ptr(),
                           prev[0], prev[1], prev[2], prev[3], prev[4], cur_r2.data_ptr(), st.lr,
-                          st.qscale, st.dscale, s)
+                          st.qscale, st.dscale, wt_ptr, st.subsample, seeds_ptr, st.row_off, t, s)
         if t == st.T:
             break
+        if st.bagw is not None:
+            st.bagw[t] = st.wt.double().sum(1)
         if group is not None:
             _allreduce_r2(st, t, group)
         for level in range(st.D):
@@ -335,7 +397,7 @@ def _run_device(st: _State, group):
             Hl = H[: st.B * NL * st.F * 768]
             Hl.zero_()
             E.gbdt_hist(st.B, st.n, st.F, st.bins.data_ptr(), nb_ptr, max_nb, st.g.data_ptr(),
-                        st.h.data_ptr(), st.w.data_ptr(), st.node.data_ptr(), node0, NL, Hl.data_ptr(),
+                        st.h.data_ptr(), wcur.data_ptr(), st.node.data_ptr(), node0, NL, Hl.data_ptr(),
                         st.qscale, s)
             if group is not None:
                 from ..parallel import dist as pdist
@@ -346,7 +408,7 @@ def _run_device(st: _State, group):
                          st.thr[t].data_ptr(), st.value[t].data_ptr(), st.stats[t].data_ptr(),
                          st.r2[t].data_ptr(), s)
             if level < st.D - 1:
-                E.gbdt_route(st.B, st.n, st.NN, st.bins.data_ptr(), st.g.data_ptr(), st.w.data_ptr(),
+                E.gbdt_route(st.B, st.n, st.NN, st.bins.data_ptr(), st.g.data_ptr(), wcur.data_ptr(),
                              st.node.data_ptr(), st.feat[t].data_ptr(), st.blo[t].data_ptr(),
                              st.r2[t].data_ptr(), node0, NL, st.qscale, s)
                 if group is not None:
@@ -364,7 +426,13 @@ def _finish(models, st: _State, sw, p1, group):
     mean = stats[..., 1] / wsum.clamp(min=1e-300)
     imp = (r2 / wsum.clamp(min=1e-300) - mean * mean).clamp(min=0.0)
     imp = torch.where(wsum > 0, imp, torch.zeros_like(imp))
-    train_score = (st.dev.double() / st.dscale) / sw[None, :]
+    if st.bagw is not None:
+        bagw = st.bagw
+        if group is not None:
+            bagw = pdist.all_reduce_sum_f64([bagw], group)[0]
+        train_score = (st.dev.double() / st.dscale) / bagw.clamp(min=1e-300)
+    else:
+        train_score = (st.dev.double() / st.dscale) / sw[None, :]
     heap_l = torch.arange(st.NN, device=st.feat.device) * 2 + 1
     for b, m in enumerate(models):
         feat = st.feat[:, b]
@@ -379,3 +447,4 @@ def _finish(models, st: _State, sw, p1, group):
                      n_features=st.F, rng_state=None, device=st.feat.device)
         m.tree_layout_ = "heap"
         m._bin_mapper = st.bm
+        m.tree_blo_ = st.blo[:, b]        # split bin per heap node (bins ≤ blo go left)

@@ -39,6 +39,29 @@ __device__ __forceinline__ long long wave_sum_i64(long long v) {
   return v;
 }
 
+// Stochastic gradient boosting (subsample < 1): row i of model b is in stage t's bag iff
+// splitmix64(seed_b ⊕ splitmix64(t, global row)) < subsample·2^64 (top 24 bits compared).
+// Counter-based: no RNG state, identical for any launch geometry and any row sharding.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ bool gb_in_bag(unsigned long long seed, int stage, long long gi, unsigned thr24) {
+  const unsigned long long k = splitmix64(((unsigned long long)stage << 40) ^ (unsigned long long)gi);
+  return (unsigned)(splitmix64(seed ^ k) >> 40) < thr24;
+}
+
+struct GbdtBag {
+  float* wt;                        // [B][n] this stage's in-bag weights (written when active)
+  const unsigned long long* seeds;  // [B]
+  long long row_off;                // global index of local row 0 (data-parallel shards)
+  unsigned thr24;                   // subsample·2^24
+  int stage;                        // current stage t
+  int active;                       // subsample < 1
+};
+
 // ------------------------------------------------------------------------------------------
 // A: apply previous tree (one pending routing level + leaf values) and prepare this stage.
 // prev_* are the previous tree's tables [B][NN] (heap), or nullptr for the first stage.
@@ -49,7 +72,7 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
     const int* __restrict__ prev_blo, const double* __restrict__ prev_value,
     long long* __restrict__ prev_r2 /*[B][NN] previous tree Σw r²*/, long long* __restrict__ dev_acc /*[B]*/,
     long long* __restrict__ cur_r2 /*[B][NN] this tree (root slot)*/, double lr, double qscale,
-    double dscale) {
+    double dscale, GbdtBag bag) {
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63;
   long long dev_q = 0, r2_q = 0;
@@ -60,7 +83,14 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
   __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += gridDim.x * blockDim.x) {
     const size_t bi = (size_t)b * S.n + i;
-    const float wi = w[bi];
+    const float w0 = w[bi];
+    float wi = w0, wp = w0;   // this stage's / the previous stage's in-bag weight
+    if (bag.active) {
+      const unsigned long long sd = bag.seeds[b];
+      wi = gb_in_bag(sd, bag.stage, bag.row_off + i, bag.thr24) ? w0 : 0.f;
+      wp = (prev_feat != nullptr && gb_in_bag(sd, bag.stage - 1, bag.row_off + i, bag.thr24)) ? w0 : 0.f;
+      bag.wt[bi] = wi;
+    }
     double rw = raw[bi];
     const double yi = y[i];
     if (prev_feat != nullptr) {
@@ -70,10 +100,10 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
         const int side = bins[(size_t)f * S.n + i] <= prev_blo[b * S.NN + nd] ? 1 : 2;
         nd = 2 * nd + side;
       }
-      if (wi > 0.f) {
+      if (wp > 0.f) {
         const double p0 = 1.0 / (1.0 + exp(-rw));
         const double r0 = yi - p0;
-        atomicAdd((unsigned long long*)&nacc[nd], (unsigned long long)q_of(wi * r0 * r0, qscale));
+        atomicAdd((unsigned long long*)&nacc[nd], (unsigned long long)q_of(wp * r0 * r0, qscale));
       }
       rw += lr * prev_value[b * S.NN + nd];
       raw[bi] = rw;
@@ -85,12 +115,13 @@ __global__ __launch_bounds__(256) void gbdt_apply_prep_kernel(
     g[bi] = gi;
     h[bi] = hi;
     node[bi] = 0;
-    if (wi > 0.f) {
-      // binomial deviance term −2(y·raw − log(1+e^raw)) (sklearn BinomialDeviance), after the update
+    if (wp > 0.f) {
+      // binomial deviance −2(y·raw − log(1+e^raw)) of the previous stage's bag, after its update
+      // (sklearn BinomialDeviance; train_score_ with subsample = in-bag loss)
       const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
-      dev_q += q_of(wi * (-2.0) * (yi * rw - l1p), dscale);
-      r2_q += q_of(wi * r * r, qscale);
+      dev_q += q_of(wp * (-2.0) * (yi * rw - l1p), dscale);
     }
+    if (wi > 0.f) r2_q += q_of(wi * r * r, qscale);
   }
   dev_q = wave_sum_i64(dev_q);
   r2_q = wave_sum_i64(r2_q);
@@ -373,13 +404,18 @@ void gbdt_apply_prep(int B, int n, int F, int NN, uintptr_t bins, uintptr_t y, u
                      uintptr_t raw, uintptr_t g, uintptr_t h, uintptr_t node, uintptr_t prev_feat,
                      uintptr_t prev_blo, uintptr_t prev_value, uintptr_t prev_r2,
                      uintptr_t dev_acc, uintptr_t cur_r2, double lr, double qscale, double dscale,
+                     uintptr_t wt, double subsample, uintptr_t seeds, long long row_off, int stage,
                      uintptr_t stream) {
   GbdtShape S{B, n, F, NN};
+  const bool active = subsample < 1.0;
+  HFENS_REQUIRE(!active || (wt != 0 && seeds != 0), "gbdt_apply_prep: subsample needs wt and seeds");
+  GbdtBag bag{(float*)wt, (const unsigned long long*)seeds, row_off,
+              (unsigned)llround(subsample * 16777216.0), stage, active ? 1 : 0};
   hipLaunchKernelGGL(gbdt_apply_prep_kernel, dim3(grid_rows(n), B), dim3(256), 0, as_stream(stream),
                      S, (const unsigned char*)bins, (const float*)y, (const float*)w, (double*)raw,
                      (float*)g, (float*)h, (int*)node, (const int*)prev_feat, (const int*)prev_blo,
                      (const double*)prev_value, (long long*)prev_r2, (long long*)dev_acc,
-                     (long long*)cur_r2, lr, qscale, dscale);
+                     (long long*)cur_r2, lr, qscale, dscale, bag);
   launch_check();
 }
 

@@ -75,6 +75,17 @@ def _gbdt(rank, world, group):
             for m in ms]
 
 
+def _gbdt_sub(rank, world, group):
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    from hfens.parallel.dist import shard_rows
+    X, y, _ = _data()
+    ms = [GradientBoostingClassifier(n_estimators=12, max_depth=2, subsample=0.6, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ms, shard_rows(X, rank, world), shard_rows(y, rank, world), group=group)
+    return [(m.tree_feature_.clone(), m.tree_threshold_.clone(), m.tree_value_.clone(), m.train_score_.clone())
+            for m in ms]
+
+
 def _logreg(rank, world, group):
     from hfens.models.linear import LogisticRegression
     from hfens.models.logreg_solver import fit_logreg_batch
@@ -113,6 +124,22 @@ def test_gbdt_dp_bit_identical():
     masks[0, ::4] = False
     ms = [GradientBoostingClassifier(n_estimators=15, max_depth=2) for _ in range(2)]
     fit_gbdt_batch(ms, X, y, masks)
+    for (f, t, v, ts), m in zip(got, ms):
+        assert torch.equal(f, m.tree_feature_)
+        assert torch.equal(t, m.tree_threshold_)
+        assert torch.equal(v, m.tree_value_)
+        assert torch.equal(ts, m.train_score_)
+
+
+def test_gbdt_subsample_dp_bit_identical():
+    """Counter-based bagging keyed by the global row index: the same stochastic GB for any sharding."""
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    got = _run("_gbdt_sub")
+    X, y, _ = _data()
+    ms = [GradientBoostingClassifier(n_estimators=12, max_depth=2, subsample=0.6, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ms, X, y)
+    assert not torch.equal(ms[0].tree_value_, ms[1].tree_value_)   # seeds give different bags
     for (f, t, v, ts), m in zip(got, ms):
         assert torch.equal(f, m.tree_feature_)
         assert torch.equal(t, m.tree_threshold_)

@@ -65,3 +65,18 @@ def test_auc_ap_match_sklearn():
     f2, t2, _ = skroc(y, s)
     np.testing.assert_allclose(fpr.numpy(), f2)
     np.testing.assert_allclose(tpr.numpy(), t2)
+
+
+def test_binned_stump_tables_host():
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models.forest_infer import ensemble_raw_binned, stump_bin_tables
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    X, y, _ = make_hf_cohort(800, 12, seed=4, nan_frac=0.0)
+    X, y = torch.as_tensor(X), torch.as_tensor(y)
+    ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ms, X, y)
+    T, init = stump_bin_tables(ms)
+    raw = ensemble_raw_binned(T, init, ms[0]._bin_mapper.transform(X))
+    for b, m in enumerate(ms):
+        assert torch.allclose(raw[b], m.decision_function(X), atol=1e-9)

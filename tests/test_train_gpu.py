@@ -85,3 +85,30 @@ def test_svc_device_matches_host_exactly(dev):
     assert torch.equal(mh.support_.cpu(), md.support_.cpu())
     assert abs(float(mh._intercept_[0]) - float(md._intercept_[0])) < 1e-4
     assert abs(mh._probA.item() - md._probA.item()) < 1e-3
+
+
+def test_gbdt_subsample_device_matches_host(dev):
+    X, y = _data(3000, 20, 31)
+    mh = [GradientBoostingClassifier(n_estimators=20, max_depth=2, subsample=0.7, random_state=s) for s in (3, 4)]
+    md = [GradientBoostingClassifier(n_estimators=20, max_depth=2, subsample=0.7, random_state=s) for s in (3, 4)]
+    fit_gbdt_batch(mh, X, y)
+    fit_gbdt_batch(md, X.to(dev), y.to(dev))
+    for a, b in zip(mh, md):
+        assert torch.equal(a.tree_feature_, b.tree_feature_.cpu())
+        assert torch.allclose(a.tree_value_, b.tree_value_.cpu(), rtol=1e-9, atol=1e-12)
+        assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-9)
+
+
+def test_binned_stump_tables_match_tree_walk(dev):
+    from hfens.models.forest_infer import ensemble_raw_binned, stump_bin_tables
+    X, y = _data(5003, 24, 41)
+    ms = [GradientBoostingClassifier(n_estimators=60, max_depth=1, subsample=0.8, random_state=s) for s in (1, 2, 3)]
+    fit_gbdt_batch(ms, X.to(dev), y.to(dev))
+    T, init = stump_bin_tables(ms)
+    bins = ms[0]._bin_mapper.transform(X.to(dev))
+    got = ensemble_raw_binned(T, init, bins).double().cpu()
+    ref = ensemble_raw_binned(T.cpu(), init.cpu(), bins.cpu())
+    assert torch.allclose(got, ref, atol=2e-5)
+    for b, m in enumerate(ms):
+        walk = m.decision_function(X.to(dev)).cpu()
+        assert torch.allclose(got[b], walk, atol=2e-5)
