@@ -14,8 +14,17 @@ Fit plan for the reference stack (3 base models × (5 OOF folds + full refit)):
 With a process group: rows are sharded; GBDT / LR / scaler moments reduce across
 ranks, the 36 SVM problems are split across ranks (task parallel) and the OOF
 meta-features all-gathered (:mod:`hfens.parallel.stack`).
+
+On the GPU the SVC batch (36 SMO problems = 36 workgroups: a few dozen of the 256 CUs, for
+most of the fit) runs on its own HIP stream from a helper thread while the main thread
+fits GBC and LR on the default stream — the idle CUs do that work concurrently.  Under a
+process group the SVC thread uses a second communicator (``pdist.aux_group``) so the two
+threads' collectives never interleave on one communicator.
 """
 from __future__ import annotations
+
+import os
+import threading
 
 import torch
 
@@ -31,6 +40,7 @@ from .stacking import Pipeline
 from .svc import SVC
 
 N_FOLDS = 5
+CONCURRENT_BASES = os.environ.get("HFENS_CONCURRENT_BASES", "1") != "0"
 
 
 def _kind(est):
@@ -78,6 +88,46 @@ def fit_base_batch(est, X, y, masks, group=None, timer=None):
     return clones
 
 
+def _fit_bases_concurrent(clf, X, y, masks, group, timer):
+    """SVC batch on a side stream (helper thread) ∥ the other base models on the default
+    stream.  Returns the fitted clone lists in estimator order, or None when not applicable."""
+    kinds = [_kind(e) for _, e in clf.estimators]
+    svc_cols = [i for i, k in enumerate(kinds) if k in ("svc", "svc_raw")]
+    if not (X.is_cuda and CONCURRENT_BASES and svc_cols and len(kinds) > len(svc_cols)):
+        return None
+    dev = X.device
+    g_svc = None
+    if group is not None:
+        from ..parallel import dist as pdist
+        g_svc = pdist.aux_group(group)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    out, err = {}, []
+
+    def work():
+        try:
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(side):
+                for i in svc_cols:
+                    out[i] = fit_base_batch(clf.estimators[i][1], X, y, masks, group=g_svc)
+        except BaseException as e:   # re-raised on the main thread
+            err.append(e)
+
+    with timer.stage("fit_bases(svc || gbc+lr)"):
+        th = threading.Thread(target=work, name="hfens-svc-fit", daemon=True)
+        th.start()
+        try:
+            for i, (_, est) in enumerate(clf.estimators):
+                if i not in svc_cols:
+                    out[i] = fit_base_batch(est, X, y, masks, group=group)
+        finally:
+            th.join()
+        if err:
+            raise err[0]
+        torch.cuda.current_stream(dev).wait_stream(side)
+    return [out[i] for i in range(len(kinds))]
+
+
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None):
     timer = timer or StageTimer(enabled=False)
     dev = X.device
@@ -90,9 +140,13 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     masks = fold_masks(folds.cpu().numpy(), N_FOLDS, device=dev)        # [6, n]
     full, oof = [], []
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer)
     for col, (name, est) in enumerate(clf.estimators):
-        with timer.stage(f"fit_{name}"):
-            fitted = fit_base_batch(est, X, y, masks, group=group)
+        if fitted_all is not None:
+            fitted = fitted_all[col]
+        else:
+            with timer.stage(f"fit_{name}"):
+                fitted = fit_base_batch(est, X, y, masks, group=group)
         with timer.stage(f"oof_{name}"):
             for k in range(N_FOLDS):
                 test = folds == k

@@ -102,6 +102,15 @@ __device__ __forceinline__ float f32_from_okey(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
 
+// order-preserving f64 ↔ u64
+__device__ __forceinline__ unsigned long long f64_okey(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  return u ^ ((u >> 63) ? ~0ull : 0x8000000000000000ull);
+}
+__device__ __forceinline__ double f64_from_okey(unsigned long long k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k ^ 0x8000000000000000ull) : ~k));
+}
+
 // exact wave max of doubles: order-preserving u64 key, max of the high words, then of the low
 // words among the lanes holding that high word
 __device__ __forceinline__ double wave_max_f64_exact(double x) {

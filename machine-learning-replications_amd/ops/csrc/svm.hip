@@ -137,22 +137,36 @@ __device__ __forceinline__ void red3_combine(Red3& x, double a, double b, int id
   if (b > x.b || (b == x.b && idx > x.idx)) { x.b = b; x.idx = idx; }
 }
 
-__device__ __forceinline__ Red3 block_red3(Red3 v, Red3* sh) {
+// Per-wave partial of a Red3 reduction: order-preserving u64 keys (exact for f64).
+struct Red3Part {
+  unsigned long long ka, kb;
+  int idx, pad;
+};
+
+// Block reduction: wave stage on DPP/permlane (u32 max of the key halves, then of the index among
+// the lanes holding the arg-max — no LDS round trips), one barrier, then every thread folds the
+// kSmoWaves partials.  Callers alternate two partial buffers so consecutive reductions need no
+// second barrier.
+__device__ __forceinline__ Red3 block_red3(Red3 v, Red3Part* sh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    red3_combine(v, __shfl_xor(v.a, o, kWave), __shfl_xor(v.b, o, kWave), __shfl_xor(v.idx, o, kWave));
-  if (lane == 0) sh[wave] = v;
+  const unsigned long long ka = f64_okey(v.a), kb = f64_okey(v.b);
+  const unsigned ah = wave_max_u32((unsigned)(ka >> 32));
+  const unsigned al = wave_max_u32((unsigned)(ka >> 32) == ah ? (unsigned)ka : 0u);
+  const unsigned bh = wave_max_u32((unsigned)(kb >> 32));
+  const unsigned bl = wave_max_u32((unsigned)(kb >> 32) == bh ? (unsigned)kb : 0u);
+  const bool top = (unsigned)(kb >> 32) == bh && (unsigned)kb == bl;
+  const unsigned bi = wave_max_u32(top ? (unsigned)(v.idx + 1) : 0u);
+  if (lane == 0) sh[wave] = Red3Part{((unsigned long long)ah << 32) | al, ((unsigned long long)bh << 32) | bl,
+                                     (int)bi - 1, 0};
   __syncthreads();
-  if (wave == 0) {
-    Red3 w = lane < kSmoWaves ? sh[lane] : Red3{-kInf, -kInf, -1};
+  Red3Part r = sh[0];
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1)  // kSmoWaves = 16 partials live in lanes 0..15
-      red3_combine(w, __shfl_xor(w.a, o, kWave), __shfl_xor(w.b, o, kWave), __shfl_xor(w.idx, o, kWave));
-    if (lane == 0) sh[kSmoWaves] = w;
+  for (int w = 1; w < kSmoWaves; ++w) {
+    const Red3Part p = sh[w];
+    r.ka = p.ka > r.ka ? p.ka : r.ka;
+    if (p.kb > r.kb || (p.kb == r.kb && p.idx > r.idx)) { r.kb = p.kb; r.idx = p.idx; }
   }
-  __syncthreads();
-  return sh[kSmoWaves];
+  return Red3{f64_from_okey(r.ka), f64_from_okey(r.kb), r.idx};
 }
 
 // Element ownership: thread `tid`, group g < K4, lane-of-vector e < 4 owns index
@@ -172,7 +186,7 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
   const float* Kp = K + P.koff;
   double* alpha = alpha_all + P.aoff;
   const int tid = threadIdx.x;
-  __shared__ Red3 sh[kSmoWaves + 1];
+  __shared__ Red3Part shA[kSmoWaves], shB[kSmoWaves];   // r1 / r2 partials (alternating)
   __shared__ double pub[4];
 
   double G[KM];
@@ -205,7 +219,7 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
       const int t = 4 * (tid + (k >> 2) * kSmoThreads) + (k & 3);
       red3_combine(r1, -kInf, ((ypos >> k) & 1ull) ? -G[k] : G[k], t);
     }
-  r1 = block_red3(r1, sh);
+  r1 = block_red3(r1, shA);
   long long iter = 0;
   double last_gap = 0.0;
   for (; iter < max_iter; ++iter) {
@@ -218,11 +232,16 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
     const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)i * P.ld);
     double gmax2 = -kInf, bnum = 0.0, bden = 1.0;
     int bj = -1;
+    // issue every row-i load before touching any of them: one HBM latency, not K4
+    float4 qv[K4];
+#pragma unroll
+    for (int g = 0; g < K4; ++g)
+      qv[g] = 4 * (tid + g * kSmoThreads) < P.l ? Ki4[tid + g * kSmoThreads] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int g = 0; g < K4; ++g) {
       const int t0 = 4 * (tid + g * kSmoThreads);
       if (t0 < P.l) {
-        const float4 q = Ki4[tid + g * kSmoThreads];
+        const float4 q = qv[g];
         Qi[4 * g] = q.x; Qi[4 * g + 1] = q.y; Qi[4 * g + 2] = q.z; Qi[4 * g + 3] = q.w;
       }
 #pragma unroll
@@ -244,7 +263,7 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
       }
     }
     Red3 r2{gmax2, bj >= 0 ? bnum / bden : -kInf, bj};
-    r2 = block_red3(r2, sh);
+    r2 = block_red3(r2, shB);
     const int j = r2.idx;
     last_gap = Gmax + r2.a;
     if (Gmax + r2.a < eps || j < 0) break;
@@ -331,11 +350,14 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
     // ---- fused: gradient update with rows i (registers) and j, then next step-1 candidates
     const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)j * P.ld);
     r1 = Red3{-kInf, -kInf, -1};
+    float4 qjv[K4];
+#pragma unroll
+    for (int g = 0; g < K4; ++g)
+      qjv[g] = 4 * (tid + g * kSmoThreads) < P.l ? Kj4[tid + g * kSmoThreads] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int g = 0; g < K4; ++g) {
       const int t0 = 4 * (tid + g * kSmoThreads);
-      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (t0 < P.l) q = Kj4[tid + g * kSmoThreads];
+      const float4 q = qjv[g];
       const float qj[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -346,7 +368,7 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
         if ((upm >> k) & 1ull) red3_combine(r1, -kInf, pos ? -G[k] : G[k], t0 + e);
       }
     }
-    r1 = block_red3(r1, sh);
+    r1 = block_red3(r1, shA);
   }
   // ---- calculate_rho
   Red3 ru{-kInf, -kInf, -1};   // a = max(−ub)
@@ -369,20 +391,21 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
       }
     }
   }
-  ru = block_red3(ru, sh);
-  rl = block_red3(rl, sh);
+  __syncthreads();   // the loop may exit right after an r1 fold that still reads shA
+  ru = block_red3(ru, shA);
+  rl = block_red3(rl, shB);
   Red3 rs{-kInf, sum_free, nfree};
   {
     // plain sums (not arg-max): reuse the shared buffer with a sum reduction
     double s = wave_sum(sum_free);
     double c = wave_sum((double)nfree);
     const int lane = tid & 63, wave = tid >> 6;
-    __syncthreads();
-    if (lane == 0) { sh[wave].a = s; sh[wave].b = c; }
+    __shared__ double ssum[2][kSmoWaves];
+    if (lane == 0) { ssum[0][wave] = s; ssum[1][wave] = c; }
     __syncthreads();
     if (tid == 0) {
       double S = 0, Cc = 0;
-      for (int w = 0; w < kSmoWaves; ++w) { S += sh[w].a; Cc += sh[w].b; }
+      for (int w = 0; w < kSmoWaves; ++w) { S += ssum[0][w]; Cc += ssum[1][w]; }
       const double ub = -ru.a, lb = rl.a;
       out.rho[blockIdx.x] = Cc > 0 ? S / Cc : (ub + lb) / 2;
       out.iters[blockIdx.x] = (int)iter;

@@ -213,14 +213,6 @@ struct WsAux {
   unsigned long long* gkey;    // [P][2] order-preserving keys of max(−yG, I_up), max(yG, I_low)
 };
 
-__device__ __forceinline__ unsigned long long f64_okey(double x) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
-  return u ^ ((u >> 63) ? ~0ull : 0x8000000000000000ull);
-}
-__device__ __forceinline__ double f64_from_okey(unsigned long long k) {
-  return __longlong_as_double((long long)((k >> 63) ? (k ^ 0x8000000000000000ull) : ~k));
-}
-
 // One point per thread (valid ⇔ t < l); wave-level only (every lane of the wave must call it).
 __device__ __forceinline__ void ws_publish_keys(const WsProb& P, int b, int t, bool valid, double a, double g,
                                                 const WsAux& X) {
