@@ -27,6 +27,8 @@ def _cd_path_host(G, q, yy, n, alphas, max_iter, tol):
     H = np.zeros(F)
     out = np.zeros((len(alphas), F))
     tol_s = tol * yy
+    diag = np.diag(G)
+    inv = np.where(diag != 0.0, 1.0 / np.where(diag != 0.0, diag, 1.0), 0.0)   # as the kernel: × 1/G_kk
     for a, alpha in enumerate(alphas):
         l1 = alpha * n
         for it in range(max_iter):
@@ -36,7 +38,7 @@ def _cd_path_host(G, q, yy, n, alphas, max_iter, tol):
                 if gkk == 0.0:
                     continue
                 tmp = q[k] - H[k] + gkk * w[k]
-                nw = np.sign(tmp) * (abs(tmp) - l1) / gkk if abs(tmp) > l1 else 0.0
+                nw = np.sign(tmp) * (abs(tmp) - l1) * inv[k] if abs(tmp) > l1 else 0.0
                 dw = nw - w[k]
                 if dw != 0.0:
                     H += G[:, k] * dw

@@ -45,12 +45,13 @@ def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
             mx = 0.0
             for k in range(F1):
                 a = max(Hb[k, k], 1e-300)
+                inv = 1.0 / a                      # as the kernel: reciprocal, then multiply
                 lin = gb[k] + Hd[k] - a * d[k]
-                z0 = wb[k] - lin / a
-                lk = lam if pn[k] else 0.0
+                z0 = wb[k] - lin * inv
+                thr = lam * inv if pn[k] else 0.0
                 z = z0
-                if lk > 0:
-                    z = z0 - lk / a if z0 > lk / a else (z0 + lk / a if z0 < -lk / a else 0.0)
+                if thr > 0:
+                    z = z0 - thr if z0 > thr else (z0 + thr if z0 < -thr else 0.0)
                 nd = z - wb[k]
                 step = nd - d[k]
                 if step != 0.0:

@@ -338,8 +338,12 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     gap = torch.empty(len(live), dtype=torch.float64, device=device)
     max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
     sdev = _dev_struct(sm, device)
+    prof = torch.zeros(len(live) * 5, dtype=torch.int64, device=device) if PROFILE_SMO else None
     E.smo_batch(sdev.data_ptr(), len(live), max_l, K.data_ptr(), alpha.data_ptr(), eps, max_iter,
-                rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), s)
+                rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
+    if prof is not None:
+        LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
+                             l=np.array([int(p.rows.numel()) for p in live]))
     del K
     return alpha, rho, iters
 
@@ -396,6 +400,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
 
 
 LAST_WS_STATS: dict = {}
+LAST_SMO_PROF: dict = {}
+PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
 
 
 def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):

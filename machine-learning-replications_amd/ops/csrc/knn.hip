@@ -6,9 +6,9 @@
 // registers, statically indexed up to FMAX features) and up to 8 missing-column slots.  Each
 // workgroup streams its donor range through LDS in 256-row tiles (row stride padded to 4 floats
 // so every lane reads the same 16-byte vector: broadcast ds_read_b128).  Per (receiver, donor) the
-// distance is the direct difference form Σ(x_r − x_d)² over zero-filled rows (no ‖x‖²+‖y‖²−2x·y
-// cancellation, so exact ties stay exact) minus the cross-missing corrections, which only loop
-// over the set bits of the two 64-bit missing masks.  Results merge across donor splits with a
+// distance is the direct difference form Σ(x_r − x_d)² over the features present in both rows
+// (masked by the two 64-bit missing masks; no ‖x‖²+‖y‖²−2x·y and no add-then-subtract
+// corrections, so exact ties stay exact).  Results merge across donor splits with a
 // 64-bit atomicMin on (float bits of d², donor index): smallest distance, then lowest donor index
 // — deterministic regardless of split count or arrival order.
 #include "common.h"
@@ -52,7 +52,6 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k)
     if (col[k] >= 0) need |= 1ull << col[k];
-  const float* xrs = R + (size_t)(active ? r : 0) * F;  // rare correction path reads global
   for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
     __syncthreads();
     const int nt = min(kKnnTile, d_end - d0);
@@ -67,33 +66,28 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
       const unsigned long long md = dm[t];
       if ((need & ~md) == 0ull) continue;  // donor lacks every column this receiver needs
       const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
+      // Σ over the features present in BOTH rows, as masked direct differences: no
+      // add-then-subtract cross-missing corrections, so rows whose common values agree get
+      // bit-identical distances (exact ties stay ties, as in the f64 reference)
+      const unsigned long long both = ~(mr | md);
+      const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
       float s0 = 0.f, s1 = 0.f;
 #pragma unroll
       for (int q = 0; q < LD / 4; ++q) {
         if (4 * q < F) {
           const float4 v = xd4[q];
-          const float a = xr[4 * q] - v.x, b = xr[4 * q + 1] - v.y;
-          const float c = xr[4 * q + 2] - v.z, d = xr[4 * q + 3] - v.w;
+          const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+          const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
+          const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
+          const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
+          const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
           s0 = fmaf(a, a, s0);
           s1 = fmaf(b, b, s1);
           s0 = fmaf(c, c, s0);
           s1 = fmaf(d, d, s1);
         }
       }
-      float s = s0 + s1;
-      // remove terms where exactly one side is missing (the other side's x² was added)
-      const float* xd = ds + t * LD;
-      unsigned long long only_r = mr & ~md, only_d = md & ~mr;
-      while (only_r) {
-        const int f = __builtin_ctzll(only_r);
-        only_r &= only_r - 1;
-        s -= xd[f] * xd[f];
-      }
-      while (only_d) {
-        const int f = __builtin_ctzll(only_d);
-        only_d &= only_d - 1;
-        s -= xrs[f] * xrs[f];
-      }
+      const float s = s0 + s1;
       const int present = F - __builtin_popcountll(mr | md);
       if (present <= 0) continue;  // undefined distance (sklearn: NaN, ignored)
       const float dist = fmaxf(s, 0.f) * ((float)F / (float)present);

@@ -29,27 +29,29 @@ __global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __re
   const double gj = j < F1 ? g[b * F1 + j] : 0.0;
   const double wj = j < F1 ? w[b * F1 + j] : 0.0;
   const double hjj = j < F1 ? Hs[j * F1 + j] : 0.0;
+  const double aj = hjj > 1e-300 ? hjj : 1e-300;
+  const double inv_a = 1.0 / aj;                                   // reciprocal once, not per sweep
+  const double thr = (j < F1 && penal[j]) ? lam * inv_a : 0.0;     // soft-threshold λ/a
   double Hd = 0.0;  // (H d)_j
   double dj = 0.0;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     double maxstep = 0.0;
     for (int k = 0; k < F1; ++k) {
-      // coordinate k: quantities owned by lane k
-      const double gk = readlane_f64(gj, k), wk = readlane_f64(wj, k);
-      const double Hdk = readlane_f64(Hd, k), dk = readlane_f64(dj, k);
-      const double hkk = readlane_f64(hjj, k);
-      const double a = hkk > 1e-300 ? hkk : 1e-300;
-      // 1-D problem in z = w_k + d_k:  (gk + Hdk − hkk·dk)(z − wk) + ½hkk(z − wk)² + λ|z|
-      const double lin = gk + Hdk - a * dk;
-      const double z0 = wk - lin / a;  // unpenalised minimiser
-      const double lk = penal[k] ? lam : 0.0;
-      double z = z0;
-      if (lk > 0) z = z0 > lk / a ? z0 - lk / a : (z0 < -lk / a ? z0 + lk / a : 0.0);
-      const double nd = z - wk;
-      const double step = nd - dk;
+      // the owner lane solves the 1-D problem in z = w_k + d_k
+      //   (g_k + (Hd)_k − a·d_k)(z − w_k) + ½a(z − w_k)² + λ|z|
+      // and broadcasts the step (one readlane pair on the dependent chain instead of five)
+      double step_l = 0.0;
+      if (j == k) {
+        const double lin = gj + Hd - aj * dj;
+        const double z0 = wj - lin * inv_a;  // unpenalised minimiser
+        const double z = thr > 0 ? (z0 > thr ? z0 - thr : (z0 < -thr ? z0 + thr : 0.0)) : z0;
+        const double nd = z - wj;
+        step_l = nd - dj;
+        dj = nd;
+      }
+      const double step = readlane_f64(step_l, k);
       if (step != 0.0) {
         if (j < F1) Hd += Hs[j * F1 + k] * step;
-        if (j == k) dj = nd;
         maxstep = fmax(maxstep, fabs(step));
       }
     }
@@ -91,6 +93,10 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
   const double n = nrows[p];
   const double qj = j < F ? q[p * F + j] : 0.0;
   const double gjj = j < F ? Gs[j * F + j] : 0.0;
+  // the coordinate step divides by G_kk every sweep of every alpha: take the reciprocal once
+  // (≤ 1 ulp from the division; the f64 divide sequence was half of each coordinate's latency)
+  const double inv_gjj = gjj != 0.0 ? 1.0 / gjj : 0.0;
+  const unsigned long long live = __ballot(j < F && gjj != 0.0);   // coordinates with G_kk ≠ 0
   const double yyp = yy[p];
   double wj = 0.0;   // coefficient owned by lane j
   double Hw = 0.0;   // (G w)_j
@@ -103,17 +109,18 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
     for (it = 0; it < max_iter; ++it) {
       double w_max = 0.0, d_w_max = 0.0;
       for (int k = 0; k < F; ++k) {
-        const double gkk = readlane_f64(gjj, k);
-        if (gkk == 0.0) continue;
-        const double wk = readlane_f64(wj, k), Hwk = readlane_f64(Hw, k), qk = readlane_f64(qj, k);
-        // tmp = q_k − (Gw)_k + G_kk w_k
-        const double tmp = qk - Hwk + gkk * wk;
-        double nw = fabs(tmp) > l1 ? copysign(fabs(tmp) - l1, tmp) / gkk : 0.0;
-        const double dw = nw - wk;
-        if (dw != 0.0) {
-          if (j < F) Hw += Gs[j * F + k] * dw;
-          if (j == k) wj = nw;
+        if (!((live >> k) & 1ull)) continue;
+        // the owner lane evaluates tmp = q_k − (Gw)_k + G_kk w_k and the soft-threshold step,
+        // then (nw, dw) are broadcast: two readlanes instead of four on the dependent chain
+        double nw_l = 0.0, dw_l = 0.0;
+        if (j == k) {
+          const double tmp = qj - Hw + gjj * wj;
+          nw_l = fabs(tmp) > l1 ? copysign(fabs(tmp) - l1, tmp) * inv_gjj : 0.0;
+          dw_l = nw_l - wj;
+          wj = nw_l;
         }
+        const double nw = readlane_f64(nw_l, k), dw = readlane_f64(dw_l, k);
+        if (dw != 0.0 && j < F) Hw += Gs[j * F + k] * dw;
         d_w_max = fmax(d_w_max, fabs(dw));
         w_max = fmax(w_max, fabs(nw));
       }

@@ -118,6 +118,7 @@ struct SmoOut {
   double* rho;      // [P]
   int* iters;       // [P]
   double* gap;      // [P]  final Gmax + Gmax2
+  long long* prof;  // [P][5] s_memtime phase totals (nullptr = off): step2, r2, pair, update, r1
 };
 
 constexpr int kSmoThreads = 1024;
@@ -222,6 +223,16 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
   r1 = block_red3(r1, shA);
   long long iter = 0;
   double last_gap = 0.0;
+  long long ph[5] = {0, 0, 0, 0, 0};
+  const bool prof = out.prof != nullptr;
+  long long tc = prof ? __builtin_amdgcn_s_memtime() : 0;
+  auto tick = [&](int k) {
+    if (prof) {
+      const long long now = __builtin_amdgcn_s_memtime();
+      ph[k] += now - tc;
+      tc = now;
+    }
+  };
   for (; iter < max_iter; ++iter) {
     const double Gmax = r1.b;
     const int i = r1.idx;
@@ -263,7 +274,9 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
       }
     }
     Red3 r2{gmax2, bj >= 0 ? bnum / bden : -kInf, bj};
+    tick(0);
     r2 = block_red3(r2, shB);
+    tick(1);
     const int j = r2.idx;
     last_gap = Gmax + r2.a;
     if (Gmax + r2.a < eps || j < 0) break;
@@ -347,6 +360,7 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
         lowm = low ? (lowm | bit) : (lowm & ~bit);
       }
     }
+    tick(2);
     // ---- fused: gradient update with rows i (registers) and j, then next step-1 candidates
     const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)j * P.ld);
     r1 = Red3{-kInf, -kInf, -1};
@@ -368,8 +382,12 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
         if ((upm >> k) & 1ull) red3_combine(r1, -kInf, pos ? -G[k] : G[k], t0 + e);
       }
     }
+    tick(3);
     r1 = block_red3(r1, shA);
+    tick(4);
   }
+  if (prof && tid == 0)
+    for (int k = 0; k < 5; ++k) out.prof[blockIdx.x * 5 + k] = ph[k];
   // ---- calculate_rho
   Red3 ru{-kInf, -kInf, -1};   // a = max(−ub)
   Red3 rl{-kInf, -kInf, -1};   // a = max(lb)
@@ -416,8 +434,9 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
 }
 
 void smo_batch(uintptr_t probs, int P, int max_l, uintptr_t K, uintptr_t alpha, double eps,
-               long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t stream) {
-  SmoOut o{(double*)rho, (int*)iters, (double*)gap};
+               long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t prof,
+               uintptr_t stream) {
+  SmoOut o{(double*)rho, (int*)iters, (double*)gap, (long long*)prof};
   auto pp = (const SmoProb*)probs;
   auto kp = (const float*)K;
   auto ap = (double*)alpha;

@@ -35,6 +35,13 @@ for spec in sys.argv[1:] or ["exact", "ws:0.1"]:
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     print(f"{spec}: {1000 * dt:.1f} ms  n_iter={[s.n_iter_ for s in svcs]}", flush=True)
+    if solver == "exact" and smo.LAST_SMO_PROF:
+        pr = smo.LAST_SMO_PROF
+        k = int(np.argmax(pr["iters"]))
+        it = max(1, int(pr["iters"][k]))
+        names = ["step2", "r2", "pair", "update", "r1"]
+        print(f"  largest problem l={pr['l'][k]} iters={it}: cycles/iter " +
+              ", ".join(f"{nm} {v / it:.0f}" for nm, v in zip(names, pr["phases"][k])))
     if solver == "ws":
         st = smo.LAST_WS_STATS
         print("  outer: max", int(st["outer"].max()), "mean", float(st["outer"].mean()))
