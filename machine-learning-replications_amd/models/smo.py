@@ -295,7 +295,13 @@ _DEC_DT = np.dtype([("zoff", "<i8"), ("hoff", "<i8"), ("l", "<i4"), ("h", "<i4")
 
 
 def _dev_struct(arr: np.ndarray, device) -> torch.Tensor:
-    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+    """Small descriptor table → device without blocking the host: a pageable H2D copy is
+    host-synchronous and waits for everything queued before it on the stream (e.g. the SMO
+    launch), which would serialise the caller's overlap with other streams."""
+    host = torch.from_numpy(arr.view(np.uint8).copy())
+    if torch.device(device).type != "cuda":
+        return host
+    return host.pin_memory().to(device, non_blocking=True)
 
 
 _WS_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("Cp", "<f8"),
@@ -471,6 +477,13 @@ def _solve_host(probs: List[_Prob], Zs, eps, max_iter_cap=None):
 # ----------------------------------------------------------------------------- public
 def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None):
     """Fit ``svcs[f]`` on (already scaled) ``Zs[f]`` with labels ``ys[f]`` ∈ {0,1}."""
+    return finish_svc_batch(launch_svc_batch(svcs, Zs, ys, max_iter_cap))
+
+
+def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None) -> dict:
+    """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
+    synchronisation after the SMO launch (so the caller can overlap other work); complete
+    with :func:`finish_svc_batch`."""
     from .. import ops
     device = Zs[0].device
     cuda = Zs[0].is_cuda
@@ -524,12 +537,22 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
             pdev = _dev_struct(arr, device)
             E.platt_batch(pdev.data_ptr(), len(pl), dcat.data_ptr(), lcat.data_ptr(), ABt.data_ptr(),
                           ops.stream_ptr(device))
-            ABc = ABt.cpu().numpy()
-            for k, f in enumerate(pl):
-                AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
-        else:
-            for k, f in enumerate(pl):
-                AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
+            return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
+                        keep=(pdev, dcat, lcat), device=device)
+        for k, f in enumerate(pl):
+            AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
+    return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=None,
+                device=device)
+
+
+def finish_svc_batch(st: dict):
+    """Platt parameters to the host, support-vector extraction, ``set_fitted``."""
+    svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
+                                                   st["sol"], st["AB"], st["device"])
+    if st["ABt"] is not None:
+        ABc = st["ABt"].cpu().numpy()
+        for k, f in enumerate(st["pl"]):
+            AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
     # ---- final models
     for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
         p = [q for q in all_probs if q.fit == f and q.fold < 0][0]

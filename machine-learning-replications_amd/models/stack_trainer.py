@@ -16,10 +16,12 @@ ranks, the 36 SVM problems are split across ranks (task parallel) and the OOF
 meta-features all-gathered (:mod:`hfens.parallel.stack`).
 
 On the GPU the SVC batch (36 SMO problems = 36 workgroups: a few dozen of the 256 CUs, for
-most of the fit) runs on its own HIP stream from a helper thread while the main thread
-fits GBC and LR on the default stream — the idle CUs do that work concurrently.  Under a
-process group the SVC thread uses a second communicator (``pdist.aux_group``) so the two
-threads' collectives never interleave on one communicator.
+most of the fit) runs on its own HIP stream while GBC and LR run on the default stream — the
+idle CUs do that work concurrently.  Single process: the SVC batch is enqueued first
+(``launch_svc_batch``: no host sync after the SMO launch) and collected after GBC/LR.  Under a
+process group the SVC fit (which has collectives inside) runs from a helper thread on a second
+communicator (``pdist.aux_group``) so the two threads' collectives never interleave on one
+communicator.
 """
 from __future__ import annotations
 
@@ -35,11 +37,12 @@ from .linear import LogisticRegression
 from .logreg_solver import fit_logreg_batch
 from .model_selection import fold_masks, stratified_kfold_test_folds
 from .scaler import StandardScaler
-from .smo import fit_svc_batch
+from .smo import finish_svc_batch, fit_svc_batch, launch_svc_batch
 from .stacking import Pipeline
 from .svc import SVC
 
 N_FOLDS = 5
+_TRACE_HOST = os.environ.get("HFENS_TRACE_HOST", "0") == "1"
 CONCURRENT_BASES = os.environ.get("HFENS_CONCURRENT_BASES", "1") != "0"
 
 
@@ -58,32 +61,40 @@ def _kind(est):
     raise NotImplementedError(f"unsupported base estimator {type(est).__name__}")
 
 
+def _svc_inputs(est, X, y, masks):
+    """Clones, their SVC objects and the scaled per-mask training matrices."""
+    kind = _kind(est)
+    clones = [est.clone() for _ in range(masks.shape[0])]
+    Zs, ys = [], []
+    for c, m in zip(clones, masks):
+        rows = torch.nonzero(m).squeeze(1)
+        Xm = X[rows]
+        if kind == "svc":
+            sc = c.steps[0][1]
+            sc.fit(Xm)
+            Zs.append(sc.transform(Xm))
+        else:
+            Zs.append(Xm)
+        ys.append(y[rows])
+    svcs = [c.steps[-1][1] if kind == "svc" else c for c in clones]
+    return clones, svcs, Zs, ys
+
+
 def fit_base_batch(est, X, y, masks, group=None, timer=None):
     """Fit ``masks.shape[0]`` clones of ``est`` on the masked row subsets; returns them."""
     kind = _kind(est)
-    B = masks.shape[0]
-    clones = [est.clone() for _ in range(B)]
     if kind in ("svc", "svc_raw"):
-        Zs, ys = [], []
-        for c, m in zip(clones, masks):
-            rows = torch.nonzero(m).squeeze(1)
-            Xm = X[rows]
-            if kind == "svc":
-                sc = c.steps[0][1]
-                sc.fit(Xm)
-                Zs.append(sc.transform(Xm))
-            else:
-                Zs.append(Xm)
-            ys.append(y[rows])
-        svcs = [c.steps[-1][1] if kind == "svc" else c for c in clones]
+        clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks)
         if group is None:
             fit_svc_batch(svcs, Zs, ys)
         else:
             from ..parallel.stack import fit_svc_batch_distributed
             fit_svc_batch_distributed(svcs, Zs, ys, group)
     elif kind == "gbc":
+        clones = [est.clone() for _ in range(masks.shape[0])]
         fit_gbdt_batch(clones, X, y, masks, group=group)
     else:
+        clones = [est.clone() for _ in range(masks.shape[0])]
         fit_logreg_batch(clones, X, y, masks, group=group)
     return clones
 
@@ -96,11 +107,48 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer):
     if not (X.is_cuda and CONCURRENT_BASES and svc_cols and len(kinds) > len(svc_cols)):
         return None
     dev = X.device
+    if group is None:
+        # one host thread: enqueue the SVC batch (scaling, Gram, SMO, Platt decisions) on a side
+        # stream first, then GBC / LR on the default stream; collect the SVC results last
+        # two pool streams (the legacy default stream would implicitly serialise with them); the
+        # SVC stream at high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware
+        # queues and two same-priority pool streams were measured landing on ONE queue
+        # (serialised); a different priority gets its own queue
+        main = torch.cuda.current_stream(dev)
+        side, other = torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        other.wait_stream(main)
+        out, pending = {}, {}
+        import time as _t
+        marks = [("start", _t.perf_counter())]
+        with timer.stage("fit_bases(svc || gbc+lr)"):
+            with torch.cuda.stream(side):
+                for i in svc_cols:
+                    clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks)
+                    marks.append(("svc_inputs", _t.perf_counter()))
+                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys))
+                    marks.append(("svc_launched", _t.perf_counter()))
+            with torch.cuda.stream(other):
+                for i, (name, est) in enumerate(clf.estimators):
+                    if i not in svc_cols:
+                        out[i] = fit_base_batch(est, X, y, masks)
+                        marks.append((f"{name}_host_done", _t.perf_counter()))
+            with torch.cuda.stream(side):
+                for i, (clones, st) in pending.items():
+                    finish_svc_batch(st)
+                    out[i] = clones
+            marks.append(("svc_finished", _t.perf_counter()))
+        if _TRACE_HOST:
+            import sys as _s
+            print("[host] " + " ".join(f"{k}={1e3 * (v - marks[0][1]):.1f}" for k, v in marks[1:]), file=_s.stderr)
+            main.wait_stream(side)
+            main.wait_stream(other)
+        return [out[i] for i in range(len(kinds))]
     g_svc = None
     if group is not None:
         from ..parallel import dist as pdist
         g_svc = pdist.aux_group(group)
-    side = torch.cuda.Stream(dev)
+    side = torch.cuda.Stream(dev, priority=-1)
     side.wait_stream(torch.cuda.current_stream(dev))
     out, err = {}, []
 
@@ -113,18 +161,22 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer):
         except BaseException as e:   # re-raised on the main thread
             err.append(e)
 
+    other = torch.cuda.Stream(dev)
+    other.wait_stream(torch.cuda.current_stream(dev))
     with timer.stage("fit_bases(svc || gbc+lr)"):
         th = threading.Thread(target=work, name="hfens-svc-fit", daemon=True)
         th.start()
         try:
-            for i, (_, est) in enumerate(clf.estimators):
-                if i not in svc_cols:
-                    out[i] = fit_base_batch(est, X, y, masks, group=group)
+            with torch.cuda.stream(other):
+                for i, (_, est) in enumerate(clf.estimators):
+                    if i not in svc_cols:
+                        out[i] = fit_base_batch(est, X, y, masks, group=group)
         finally:
             th.join()
         if err:
             raise err[0]
         torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.current_stream(dev).wait_stream(other)
     return [out[i] for i in range(len(kinds))]
 
 

@@ -109,7 +109,15 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
     for (it = 0; it < max_iter; ++it) {
       double w_max = 0.0, d_w_max = 0.0;
       for (int k = 0; k < F; ++k) {
-        if (!((live >> k) & 1ull)) continue;
+        // skip ahead over coordinates that provably stay at zero (w_k = 0 and |q_k − (Gw)_k| ≤ l1
+        // — exactly sklearn's "no update" branch): every lane tests its own coordinate against
+        // its current (Gw)_j in parallel, one ballot finds the next coordinate that can move
+        {
+          const bool can_move = ((live >> j) & 1ull) && j >= k && !(wj == 0.0 && !(fabs(qj - Hw) > l1));
+          const unsigned long long mv = __ballot(can_move);
+          if (mv == 0ull) break;
+          k = __builtin_ctzll(mv);
+        }
         // the owner lane evaluates tmp = q_k − (Gw)_k + G_kk w_k and the soft-threshold step,
         // then (nw, dw) are broadcast: two readlanes instead of four on the dependent chain
         double nw_l = 0.0, dw_l = 0.0;

@@ -1,0 +1,34 @@
+"""cProfile one development step of the headline bench (host-side hotspots)."""
+import cProfile
+import os
+import pstats
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hfens.io.synth import make_hf_cohort
+from hfens.pipeline import develop
+from hfens.utils.timing import StageTimer
+
+dev = torch.device("cuda")
+Xd, yd, names = make_hf_cohort(10000, 40, seed=2020, nan_frac=0.02)
+Xs, ys, _ = make_hf_cohort(10000, 40, seed=2021, nan_frac=0.02)
+Xd, yd, Xs, ys = (torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys))
+
+
+def step():
+    return develop(Xd, yd, Xs, ys, names, device=dev, timer=StageTimer(enabled=False))
+
+
+for _ in range(2):
+    step()
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+pr.enable()
+step()
+torch.cuda.synchronize()
+pr.disable()
+st = pstats.Stats(pr)
+st.sort_stats("tottime").print_stats(25)
+st.sort_stats("cumulative").print_stats(40)
