@@ -17,16 +17,14 @@ meta-features all-gathered (:mod:`hfens.parallel.stack`).
 
 On the GPU the SVC batch (36 SMO problems = 36 workgroups: a few dozen of the 256 CUs, for
 most of the fit) runs on its own HIP stream while GBC and LR run on the default stream — the
-idle CUs do that work concurrently.  Single process: the SVC batch is enqueued first
-(``launch_svc_batch``: no host sync after the SMO launch) and collected after GBC/LR.  Under a
-process group the SVC fit (which has collectives inside) runs from a helper thread on a second
-communicator (``pdist.aux_group``) so the two threads' collectives never interleave on one
-communicator.
+idle CUs do that work concurrently.  The SVC batch is enqueued first
+(``launch_svc_batch``: no host sync after the SMO launch) and collected after GBC/LR, all from
+one host thread — under a process group the SVC all-gathers, the GBC/LR all-reduces and the
+SVC broadcasts are therefore issued in the same order on every rank on one communicator.
 """
 from __future__ import annotations
 
 import os
-import threading
 
 import torch
 
@@ -100,83 +98,55 @@ def fit_base_batch(est, X, y, masks, group=None, timer=None):
 
 
 def _fit_bases_concurrent(clf, X, y, masks, group, timer):
-    """SVC batch on a side stream (helper thread) ∥ the other base models on the default
-    stream.  Returns the fitted clone lists in estimator order, or None when not applicable."""
+    """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
+    Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
     svc_cols = [i for i, k in enumerate(kinds) if k in ("svc", "svc_raw")]
     if not (X.is_cuda and CONCURRENT_BASES and svc_cols and len(kinds) > len(svc_cols)):
         return None
     dev = X.device
-    if group is None:
-        # one host thread: enqueue the SVC batch (scaling, Gram, SMO, Platt decisions) on a side
-        # stream first, then GBC / LR on the default stream; collect the SVC results last
-        # two pool streams (the legacy default stream would implicitly serialise with them); the
-        # SVC stream at high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware
-        # queues and two same-priority pool streams were measured landing on ONE queue
-        # (serialised); a different priority gets its own queue
-        main = torch.cuda.current_stream(dev)
-        side, other = torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev)
-        side.wait_stream(main)
-        other.wait_stream(main)
-        out, pending = {}, {}
-        import time as _t
-        marks = [("start", _t.perf_counter())]
-        with timer.stage("fit_bases(svc || gbc+lr)"):
-            with torch.cuda.stream(side):
-                for i in svc_cols:
-                    clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks)
-                    marks.append(("svc_inputs", _t.perf_counter()))
-                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys))
-                    marks.append(("svc_launched", _t.perf_counter()))
-            with torch.cuda.stream(other):
-                for i, (name, est) in enumerate(clf.estimators):
-                    if i not in svc_cols:
-                        out[i] = fit_base_batch(est, X, y, masks)
-                        marks.append((f"{name}_host_done", _t.perf_counter()))
-            with torch.cuda.stream(side):
-                for i, (clones, st) in pending.items():
-                    finish_svc_batch(st)
-                    out[i] = clones
-            marks.append(("svc_finished", _t.perf_counter()))
-        if _TRACE_HOST:
-            import sys as _s
-            print("[host] " + " ".join(f"{k}={1e3 * (v - marks[0][1]):.1f}" for k, v in marks[1:]), file=_s.stderr)
-            main.wait_stream(side)
-            main.wait_stream(other)
-        return [out[i] for i in range(len(kinds))]
-    g_svc = None
     if group is not None:
-        from ..parallel import dist as pdist
-        g_svc = pdist.aux_group(group)
-    side = torch.cuda.Stream(dev, priority=-1)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    out, err = {}, []
-
-    def work():
-        try:
-            torch.cuda.set_device(dev)
-            with torch.cuda.stream(side):
-                for i in svc_cols:
-                    out[i] = fit_base_batch(clf.estimators[i][1], X, y, masks, group=g_svc)
-        except BaseException as e:   # re-raised on the main thread
-            err.append(e)
-
-    other = torch.cuda.Stream(dev)
-    other.wait_stream(torch.cuda.current_stream(dev))
+        from ..parallel.stack import finish_svc_batch_distributed, launch_svc_batch_distributed
+    # two pool streams (the legacy default stream would implicitly serialise with them); the SVC
+    # stream at high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues and
+    # two same-priority pool streams were measured landing on ONE queue (serialised)
+    main = torch.cuda.current_stream(dev)
+    side, other = torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev)
+    side.wait_stream(main)
+    other.wait_stream(main)
+    out, pending = {}, {}
+    import time as _t
+    marks = [("start", _t.perf_counter())]
     with timer.stage("fit_bases(svc || gbc+lr)"):
-        th = threading.Thread(target=work, name="hfens-svc-fit", daemon=True)
-        th.start()
-        try:
-            with torch.cuda.stream(other):
-                for i, (_, est) in enumerate(clf.estimators):
-                    if i not in svc_cols:
-                        out[i] = fit_base_batch(est, X, y, masks, group=group)
-        finally:
-            th.join()
-        if err:
-            raise err[0]
-        torch.cuda.current_stream(dev).wait_stream(side)
-        torch.cuda.current_stream(dev).wait_stream(other)
+        # every collective is issued from this thread in the same order on every rank:
+        # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
+        with torch.cuda.stream(side):
+            for i in svc_cols:
+                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks)
+                marks.append(("svc_inputs", _t.perf_counter()))
+                if group is None:
+                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys))
+                else:
+                    pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
+                marks.append(("svc_launched", _t.perf_counter()))
+        with torch.cuda.stream(other):
+            for i, (name, est) in enumerate(clf.estimators):
+                if i not in svc_cols:
+                    out[i] = fit_base_batch(est, X, y, masks, group=group)
+                    marks.append((f"{name}_host_done", _t.perf_counter()))
+        with torch.cuda.stream(side):
+            for i, (clones, st) in pending.items():
+                if group is None:
+                    finish_svc_batch(st)
+                else:
+                    finish_svc_batch_distributed(st, group)
+                out[i] = clones
+        marks.append(("svc_finished", _t.perf_counter()))
+        main.wait_stream(side)
+        main.wait_stream(other)
+    if _TRACE_HOST:
+        import sys as _s
+        print("[host] " + " ".join(f"{k}={1e3 * (v - marks[0][1]):.1f}" for k, v in marks[1:]), file=_s.stderr)
     return [out[i] for i in range(len(kinds))]
 
 

@@ -53,21 +53,7 @@ def rank_device() -> torch.device:
     return torch.device("cuda", local_rank() % max(1, n))
 
 
-_AUX_GROUPS = {}
-
-
-def aux_group(group):
-    """A second communicator over the same ranks (created once, collectively), for work that
-    runs concurrently with ``group``'s collectives from another thread/stream."""
-    key = id(group)
-    g = _AUX_GROUPS.get(key)
-    if g is None:
-        g = _AUX_GROUPS[key] = dist.new_group(ranks=list(range(dist.get_world_size(group))))
-    return g
-
-
 def shutdown():
-    _AUX_GROUPS.clear()
     if dist.is_initialized():
         dist.destroy_process_group()
 

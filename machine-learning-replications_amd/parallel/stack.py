@@ -11,17 +11,33 @@ from __future__ import annotations
 
 import torch
 
-from ..models.smo import fit_svc_batch
+from ..models.smo import finish_svc_batch, launch_svc_batch
 from . import dist as pdist
 
 
 def fit_svc_batch_distributed(svcs, Zs, ys, group):
+    return finish_svc_batch_distributed(launch_svc_batch_distributed(svcs, Zs, ys, group), group)
+
+
+def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
+    """All-gather every fit's rows (collective), then enqueue this rank's fits on the current
+    stream (no host sync after the SMO launch).  Collectives stay on the calling thread, so all
+    ranks issue them in one order on one communicator."""
     world, rank = pdist.dist.get_world_size(group), pdist.dist.get_rank(group)
     full_Z = [pdist.all_gather_rows(Z, group) for Z in Zs]
     full_y = [pdist.all_gather_rows(y[:, None].to(torch.float64), group)[:, 0] for y in ys]
     mine = [f for f in range(len(svcs)) if f % world == rank]
+    st = None
     if mine:
-        fit_svc_batch([svcs[f] for f in mine], [full_Z[f] for f in mine], [full_y[f] for f in mine])
+        st = launch_svc_batch([svcs[f] for f in mine], [full_Z[f] for f in mine], [full_y[f] for f in mine])
+    return dict(svcs=svcs, Zs=Zs, st=st, world=world, rank=rank)
+
+
+def finish_svc_batch_distributed(pre: dict, group):
+    """Complete this rank's fits, then broadcast every fit from its owner (collectives)."""
+    svcs, Zs, world, rank = pre["svcs"], pre["Zs"], pre["world"], pre["rank"]
+    if pre["st"] is not None:
+        finish_svc_batch(pre["st"])
     for f, svc in enumerate(svcs):
         src = f % world
         if rank == src:
