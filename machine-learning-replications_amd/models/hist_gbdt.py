@@ -272,6 +272,9 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     subsample = float(m0.subsample)
     if not 0.0 < subsample <= 1.0:
         raise ValueError("subsample must be in (0, 1]")
+    from ..utils.guards import check_binary, check_finite
+    check_finite(X, "GradientBoostingClassifier.fit X")
+    check_binary(y, "GradientBoostingClassifier.fit y")
     dev = X.device
     n, F = X.shape
     B = len(models)
@@ -328,6 +331,7 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         _run_device(st, group)
     else:
         _run_host(st, group)
+    check_finite(st.value, "GBDT leaf values")
     _finish(models, st, sw, p1, group)
     return models
 

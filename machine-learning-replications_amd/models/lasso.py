@@ -98,8 +98,9 @@ class LassoCV(Estimator):
         return torch.stack(out).to(Gs.device)
 
     def fit(self, X, y, group=None):
-        X = as_tensor(X)
-        y = as_tensor(y, device=X.device)
+        from ..utils.guards import check_finite
+        X = check_finite(as_tensor(X), "LassoCV.fit X")
+        y = check_finite(as_tensor(y, device=X.device), "LassoCV.fit y")
         n, F = X.shape
         dev = X.device
         k = 5 if self.cv is None else int(self.cv)

@@ -77,6 +77,9 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
     _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
     if m0.penalty not in ("l1", "l2"):
         raise NotImplementedError("penalty must be 'l1' or 'l2'")
+    from ..utils.guards import check_binary, check_finite
+    check_finite(X, "LogisticRegression.fit X")
+    check_binary(y, "LogisticRegression.fit y")
     dev = X.device
     X = X.to(torch.float64)
     n, F = X.shape

@@ -485,6 +485,10 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`."""
     from .. import ops
+    from ..utils.guards import check_binary, check_finite
+    for f, (Z, y) in enumerate(zip(Zs, ys)):
+        check_finite(Z, f"SVC.fit X (fit {f})")
+        check_binary(y, f"SVC.fit y (fit {f})")
     device = Zs[0].device
     cuda = Zs[0].is_cuda
     all_probs, meta = [], []
@@ -550,6 +554,8 @@ def finish_svc_batch(st: dict):
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
                                                    st["sol"], st["AB"], st["device"])
     if st["ABt"] is not None:
+        from ..utils.guards import check_finite
+        check_finite(st["ABt"], "SVC Platt sigmoid (A, B)")
         ABc = st["ABt"].cpu().numpy()
         for k, f in enumerate(st["pl"]):
             AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))

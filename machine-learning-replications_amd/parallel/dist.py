@@ -16,6 +16,7 @@ reductions exact, so results are identical for 1, 2, 4 or 8 ranks.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from typing import List, Sequence
 
@@ -36,7 +37,9 @@ def init_from_env(backend: str = None):
         if backend == "nccl":
             torch.cuda.set_device(rank_device())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend)
+        # fail fast instead of hanging on a dead peer
+        timeout = datetime.timedelta(seconds=float(os.environ.get("HFENS_DIST_TIMEOUT", "600")))
+        dist.init_process_group(backend=backend, timeout=timeout)
     return dist.group.WORLD, dist.get_rank(), dist.get_world_size()
 
 

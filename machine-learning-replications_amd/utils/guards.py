@@ -1,0 +1,27 @@
+"""Fail-fast numeric guards: non-finite inputs or solver state raise at the
+stage that produced them instead of surfacing as a silently wrong model.  Each check is one
+fused reduction + one host read."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+ENABLED = os.environ.get("HFENS_GUARDS", "1") != "0"
+
+
+class NonFiniteError(FloatingPointError):
+    pass
+
+
+def check_finite(t: torch.Tensor, what: str) -> torch.Tensor:
+    if ENABLED and t.numel() and t.is_floating_point() and not bool(torch.isfinite(t).all()):
+        bad = int((~torch.isfinite(t)).sum())
+        raise NonFiniteError(f"{what}: {bad} non-finite value(s)")
+    return t
+
+
+def check_binary(y: torch.Tensor, what: str) -> torch.Tensor:
+    if ENABLED and y.numel() and not bool(((y == 0) | (y == 1)).all()):
+        raise ValueError(f"{what}: labels must be 0/1")
+    return y
