@@ -130,13 +130,56 @@ def evaluate(y_true, proba1) -> Dict[str, float]:
             "accuracy": (tp + tn) / max(1, tp + tn + fp + fn), "tp": tp, "fp": fp, "tn": tn, "fn": fn}
 
 
+def _svg_curve(path: str, x, y, lo, hi, xlabel: str, ylabel: str, label: str, diagonal: bool) -> str:
+    """Minimal dependency-free SVG line plot with a shaded ±band (headless nodes without
+    matplotlib): same content as the reference figures (T:66-90)."""
+    W, H, m = 480, 400, 50
+    def px(v):
+        return m + float(v) * (W - 2 * m)
+    def py(v):
+        return H - m - float(v) * (H - 2 * m)
+    xs = [float(v) for v in x]
+    pts = " ".join(f"{px(a):.2f},{py(b):.2f}" for a, b in zip(xs, y))
+    band = " ".join(f"{px(a):.2f},{py(min(1.0, max(0.0, float(b)))):.2f}" for a, b in zip(xs, hi))
+    band += " " + " ".join(f"{px(a):.2f},{py(min(1.0, max(0.0, float(b)))):.2f}"
+                           for a, b in zip(reversed(xs), reversed([float(v) for v in lo])))
+    parts = [f'<svg xmlns="http://www.w3.org/2000/svg" width="{W}" height="{H}" font-family="sans-serif" font-size="12">',
+             f'<rect x="{m}" y="{m}" width="{W - 2 * m}" height="{H - 2 * m}" fill="none" stroke="black"/>',
+             f'<polygon points="{band}" fill="grey" fill-opacity="0.2"/>',
+             f'<polyline points="{pts}" fill="none" stroke="#1f77b4" stroke-width="2"/>']
+    if diagonal:
+        parts.append(f'<line x1="{px(0)}" y1="{py(0)}" x2="{px(1)}" y2="{py(1)}" stroke="black" stroke-dasharray="5,4"/>')
+    for t in (0.0, 0.25, 0.5, 0.75, 1.0):
+        parts.append(f'<text x="{px(t) - 8:.1f}" y="{H - m + 16}">{t:g}</text>')
+        parts.append(f'<text x="{m - 34}" y="{py(t) + 4:.1f}">{t:g}</text>')
+    parts += [f'<text x="{W / 2 - 50}" y="{H - 12}">{xlabel}</text>',
+              f'<text x="12" y="{H / 2}" transform="rotate(-90 12 {H / 2})">{ylabel}</text>',
+              f'<text x="{m + 10}" y="{m + 18}">{label}</text>', "</svg>"]
+    with open(path, "w") as f:
+        f.write("\n".join(parts) + "\n")
+    return path
+
+
 def save_plots(y_true, proba1, prefix: str) -> Optional[Tuple[str, str]]:
+    """ROC and PR figures with the Wald ±band (reference T:66-90; saved instead of shown).
+    PNG through matplotlib when it is installed, otherwise self-contained SVG."""
     try:
         import matplotlib
         matplotlib.use("Agg")
         import matplotlib.pyplot as plt
-    except Exception:  # pragma: no cover
-        return None
+    except Exception:
+        y = _t(y_true).cpu()
+        p = _t(proba1).cpu()
+        n = y.numel()
+        fpr, tpr, _ = roc_curve(y, p)
+        lo, hi = wald_band(tpr, n)
+        roc = _svg_curve(prefix + "_roc.svg", fpr, tpr, lo, hi, "False Positive Rate", "True Positive Rate",
+                         f"ensemble (AUC = {auc(fpr, tpr):.2f})", True)
+        prec, rec, _ = precision_recall_curve(y, p)
+        lo, hi = wald_band(prec, n)
+        pr = _svg_curve(prefix + "_pr.svg", rec, prec, lo, hi, "Recall", "Precision",
+                        f"ensemble (AP = {average_precision(y, p):.2f})", False)
+        return roc, pr
     y = _t(y_true).cpu()
     p = _t(proba1).cpu()
     n = y.numel()

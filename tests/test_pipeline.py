@@ -80,3 +80,21 @@ def test_binned_stump_tables_host():
     raw = ensemble_raw_binned(T, init, ms[0]._bin_mapper.transform(X))
     for b, m in enumerate(ms):
         assert torch.allclose(raw[b], m.decision_function(X), atol=1e-9)
+
+
+def test_save_plots_png_and_svg_fallback(tmp_path, monkeypatch):
+    from hfens.utils import metrics
+    y = torch.tensor([0, 1, 0, 1, 1, 0, 0, 1.0])
+    p = torch.tensor([.1, .9, .3, .6, .8, .2, .55, .4])
+    out = metrics.save_plots(y, p, str(tmp_path / "a"))
+    assert out is not None and all(__import__("os").path.getsize(f) > 0 for f in out)
+    import builtins
+    real_import = builtins.__import__
+
+    def no_mpl(name, *args, **kw):
+        if name.startswith("matplotlib"):
+            raise ImportError("no matplotlib")
+        return real_import(name, *args, **kw)
+    monkeypatch.setattr(builtins, "__import__", no_mpl)
+    roc, pr = metrics.save_plots(y, p, str(tmp_path / "b"))
+    assert roc.endswith(".svg") and "<polyline" in open(roc).read() and "AP =" in open(pr).read()
