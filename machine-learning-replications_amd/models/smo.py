@@ -99,47 +99,74 @@ def sklearn_libsvm_seed(random_state) -> int:
 class _Prob:
     fit: int
     fold: int             # -1 = final solve
-    rows: torch.Tensor    # indices into the fit's Z, in problem order
+    rows: Optional[np.ndarray]   # int64 indices into the fit's Z, in problem order (None: constant fold)
     npos: int
     Cp: float
     Cn: float
     gamma: float
-    held: Optional[torch.Tensor] = None   # Platt: held-out grouped positions
-    held_rows: Optional[torch.Tensor] = None
+    held: Optional[np.ndarray] = None       # Platt: held-out grouped positions
+    held_rows: Optional[np.ndarray] = None  # … and their rows of Z
+    const: float = 0.0
+
+    @property
+    def l(self) -> int:
+        return 0 if self.rows is None else int(self.rows.shape[0])
 
 
-def _expand(fit_id, Z, y, svc, device):
-    """libsvm problem list of one SVC fit."""
-    yb = (y > 0.5)
-    idx0 = torch.nonzero(~yb).squeeze(1)
-    idx1 = torch.nonzero(yb).squeeze(1)
-    grouped = torch.cat([idx0, idx1])
-    n0, l = int(idx0.numel()), int(grouped.numel())
-    gamma = svc.resolve_gamma(Z)
-    cw = svc.class_weights(y.to(torch.float64)).cpu()
+def _expand(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
+    """libsvm problem list of one SVC fit — pure host index bookkeeping on the labels (numpy),
+    so preparing the 36 problems costs no device round trips."""
+    yb = y_np > 0.5
+    idx0 = np.nonzero(~yb)[0]
+    idx1 = np.nonzero(yb)[0]
+    grouped = np.concatenate([idx0, idx1]).astype(np.int64)
+    n0, l = int(idx0.shape[0]), int(grouped.shape[0])
     C0, C1 = float(svc.C * cw[0]), float(svc.C * cw[1])
     probs = []
-    platt = None
     if svc.probability:
         seed = sklearn_libsvm_seed(svc.random_state)
-        perm = torch.as_tensor(libsvm_perm(l, seed), device=grouped.device)
-        is_pos = torch.arange(l, device=grouped.device) < n0   # grouped position → class 0
+        perm = libsvm_perm(l, seed)
+        is_pos = np.arange(l) < n0   # grouped position → class 0
         for k in range(5):
             b, e = k * l // 5, (k + 1) * l // 5
-            train = torch.cat([perm[:b], perm[e:]])
+            train = np.concatenate([perm[:b], perm[e:]])
             cls1 = train[~is_pos[train]]
             cls0 = train[is_pos[train]]
             held = perm[b:e]
-            if cls1.numel() == 0 or cls0.numel() == 0:
-                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, grouped[held]))
-                probs[-1].const = 1.0 if cls1.numel() == 0 else -1.0
+            if cls1.shape[0] == 0 or cls0.shape[0] == 0:
+                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, grouped[held],
+                                   const=1.0 if cls1.shape[0] == 0 else -1.0))
                 continue
-            rows_pos = torch.cat([cls1, cls0])        # sub-problem order: label −1 (class 1) first
-            probs.append(_Prob(fit_id, k, grouped[rows_pos], int(cls1.numel()), C1, C0, gamma,
+            rows_pos = np.concatenate([cls1, cls0])        # sub-problem order: label −1 (class 1) first
+            probs.append(_Prob(fit_id, k, grouped[rows_pos], int(cls1.shape[0]), C1, C0, gamma,
                                held, grouped[held]))
-        platt = perm
     probs.append(_Prob(fit_id, -1, grouped, n0, C0, C1, gamma))
     return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
+
+
+def _to_dev(a: np.ndarray, device) -> torch.Tensor:
+    """Host index array → device without blocking the host (pinned, non-blocking)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if torch.device(device).type != "cuda":
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
+def _gather_rows(Zs, probs, attr, device) -> torch.Tensor:
+    """Concatenate Zs[p.fit][getattr(p, attr)] over ``probs`` with one gather per fit."""
+    parts = []
+    fits = sorted({p.fit for p in probs})
+    order = []
+    for f in fits:
+        idx = [getattr(p, attr) for p in probs if p.fit == f]
+        if not idx:
+            continue
+        ii = _to_dev(np.concatenate(idx), device)
+        parts.append(Zs[f].index_select(0, ii).to(torch.float32))
+        order += [p for p in probs if p.fit == f]
+    if [id(p) for p in order] != [id(p) for p in probs]:
+        raise AssertionError("problems must be grouped by fit")
+    return torch.cat(parts).contiguous()
 
 
 # ----------------------------------------------------------------------------- host solver
@@ -329,12 +356,12 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     sm = np.zeros(len(live), _SMO_DT)
     koff = 0
     for k, p in enumerate(live):
-        l = int(p.rows.numel())
+        l = p.l
         ld = (l + 63) // 64 * 64
         g[k] = (zoffs[k], koff, l, ld, -p.gamma * 1.4426950408889634, 0)
         sm[k] = (koff, aoffs[k], l, ld, p.npos, 0, p.Cp, p.Cn)
         koff += l * ld
-    max_l = max(int(p.rows.numel()) for p in live)
+    max_l = max(p.l for p in live)
     K = torch.empty(koff, dtype=torch.float32, device=device)
     gdev = _dev_struct(g, device)
     E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
@@ -349,7 +376,7 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
                 rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
     if prof is not None:
         LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
-                             l=np.array([int(p.rows.numel()) for p in live]))
+                             l=np.array([p.l for p in live]))
     del K
     return alpha, rho, iters
 
@@ -362,7 +389,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     P = len(live)
     arr = np.zeros(P, _WS_DT)
     for k, p in enumerate(live):
-        arr[k] = (zoffs[k], aoffs[k], int(p.rows.numel()), p.npos, p.Cp, p.Cn,
+        arr[k] = (zoffs[k], aoffs[k], p.l, p.npos, p.Cp, p.Cn,
                   -p.gamma * 1.4426950408889634, 0)
     max_l = int(arr["l"].max())
     n = aoffs[-1]
@@ -416,37 +443,37 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
     s = ops.stream_ptr(device)
     live = [p for p in probs if p.rows is not None]
     F = Zs[0].shape[1]
-    zcat = torch.cat([Zs[p.fit][p.rows].to(torch.float32) for p in live]).contiguous()
+    zcat = _gather_rows(Zs, live, "rows", device)
     zoffs, aoffs = [], [0]
     for p in live:
         zoffs.append(aoffs[-1])
-        aoffs.append(aoffs[-1] + int(p.rows.numel()))
+        aoffs.append(aoffs[-1] + p.l)
     aoffs_start = aoffs[:-1]
-    max_l = max(int(p.rows.numel()) for p in live)
+    max_l = max(p.l for p in live)
     solver = _pick_solver(max_l)
     solve = _solve_ws if solver == "ws" else _solve_exact
     alpha, rho, iters = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)
     out = {}
     for k, p in enumerate(live):
         a0 = aoffs_start[k]
-        out[id(p)] = (alpha[a0:a0 + int(p.rows.numel())], rho[k], iters[k])
+        out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
     # ---- Platt held-out decision values of every CV sub-model: one batched launch
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
     if platt:
         sign = torch.empty(aoffs[-1], dtype=torch.float32, device=device)
         for k, p in enumerate(live):
-            a0, l = aoffs_start[k], int(p.rows.numel())
+            a0, l = aoffs_start[k], p.l
             sign[a0:a0 + p.npos] = 1.0
             sign[a0 + p.npos:a0 + l] = -1.0
         coef = (sign * alpha.to(torch.float32)).contiguous()
-        hcat = torch.cat([Zs[p.fit][p.held_rows].to(torch.float32) for _, p in platt]).contiguous()
+        hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
         per = 1024
         S = (max_l + per - 1) // per
         dt = np.zeros(len(platt), _DEC_DT)
         hoff = 0
         for i, (k, p) in enumerate(platt):
-            h = int(p.held_rows.numel())
-            dt[i] = (zoffs[k], hoff, int(p.rows.numel()), h, -p.gamma * 1.4426950408889634, per)
+            h = int(p.held_rows.shape[0])
+            dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
             hoff += h
         part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
         ddev = _dev_struct(dt, device)
@@ -454,9 +481,14 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
         E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(platt),
                         max_h, S, part.data_ptr(), s)
         dec = part.to(torch.float64).sum(1)
+        # (index tensors uploaded pinned/non-blocking: a Python-list index would be a pageable,
+        # host-blocking copy queued behind the SMO)
+        ks = _to_dev(np.array([k for k, _ in platt], dtype=np.int64), device)
+        rho_h = torch.repeat_interleave(rho.index_select(0, ks), _to_dev(dt["h"].astype(np.int64), device),
+                                        output_size=hoff)
+        out["dec_all"] = dec - rho_h                      # held-out decisions, platt order
         for i, (k, p) in enumerate(platt):
-            h0, h = int(dt[i]["hoff"]), int(dt[i]["h"])
-            out[("dec", id(p))] = dec[h0:h0 + h] - rho[k]
+            out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
     return out
 
 
@@ -465,7 +497,7 @@ def _solve_host(probs: List[_Prob], Zs, eps, max_iter_cap=None):
     for p in probs:
         if p.rows is None:
             continue
-        Zp = Zs[p.fit][p.rows].double().cpu().numpy()
+        Zp = Zs[p.fit][torch.as_tensor(p.rows)].double().cpu().numpy()
         K = _gram_host(Zp, p.gamma)
         l = K.shape[0]
         mi = max(10_000_000, 100 * l) if max_iter_cap is None else max_iter_cap
@@ -491,9 +523,29 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         check_binary(y, f"SVC.fit y (fit {f})")
     device = Zs[0].device
     cuda = Zs[0].is_cuda
+    # one host read for every fit's labels and one for the 'scale' gamma statistics; the problem
+    # bookkeeping itself is numpy on the host
+    sizes = [int(y.numel()) for y in ys]
+    y_host = torch.cat([y.reshape(-1).to(torch.float64) for y in ys]).cpu().numpy()
+    need_var = [svc.gamma == "scale" for svc in svcs]
+    var = (torch.stack([Z.to(torch.float64).var(unbiased=False) for Z in Zs]).cpu().numpy()
+           if any(need_var) else None)
     all_probs, meta = [], []
-    for f, (svc, Z, y) in enumerate(zip(svcs, Zs, ys)):
-        pr, mt = _expand(f, Z, y.to(device), svc, device)
+    off = 0
+    for f, (svc, Z) in enumerate(zip(svcs, Zs)):
+        y_np = y_host[off:off + sizes[f]]
+        off += sizes[f]
+        if svc.gamma == "scale":
+            v = float(var[f])
+            gamma = 1.0 / (Z.shape[1] * v) if v != 0 else 1.0
+        else:
+            gamma = svc.resolve_gamma(Z)
+        if svc.class_weight == "balanced":
+            cnt = np.bincount((y_np > 0.5).astype(np.int64), minlength=2).astype(np.float64)
+            cw = y_np.shape[0] / (2 * cnt)
+        else:
+            cw = svc.class_weights(torch.as_tensor(y_np)).cpu().numpy()
+        pr, mt = _expand(f, y_np, gamma, cw, svc)
         all_probs += pr
         meta.append(mt)
     eps = float(svcs[0].tol)
@@ -506,23 +558,27 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             continue
         l = mt["l"]
         dec = torch.zeros(l, dtype=torch.float64, device=device)
-        for p in all_probs:
-            if p.fit != f or p.fold < 0:
-                continue
+        folds = [p for p in all_probs if p.fit == f and p.fold >= 0]
+        live_f = [p for p in folds if p.rows is not None]
+        if cuda and live_f:
+            # this fit's folds are contiguous in the batched decision vector: one scatter
+            h0 = sol[("hoff", id(live_f[0]))][0]
+            pos = np.concatenate([p.held for p in live_f])
+            for p in live_f:
+                assert sol[("hoff", id(p))][0] == h0 + sum(q.held.shape[0] for q in live_f[:live_f.index(p)])
+            dec.index_copy_(0, _to_dev(pos, device), -sol["dec_all"][h0:h0 + pos.shape[0]])  # × label[0] = −1
+        elif live_f:
+            from ..ops import reference as ref
+            for p in live_f:
+                a, r, _ = sol[id(p)]
+                yint = torch.where(torch.arange(a.numel()) < p.npos, 1.0, -1.0).to(torch.float64)
+                Zh = Z[torch.as_tensor(p.held_rows, device=Z.device)].double()
+                Zr = Z[torch.as_tensor(p.rows, device=Z.device)].double()
+                d = ref.rbf_decision(Zh, Zr, (yint * a.cpu()).to(Zh.device), p.gamma, 0.0) - r
+                dec[torch.as_tensor(p.held, device=device)] = -d.to(device)
+        for p in folds:
             if p.rows is None:
-                dec[p.held] = p.const
-                continue
-            a, r, _ = sol[id(p)]
-            a = a.to(device)
-            yint = torch.where(torch.arange(a.numel(), device=device) < p.npos, 1.0, -1.0).to(torch.float64)
-            coef = yint * a
-            Zh = Z[p.held_rows]
-            if cuda:
-                d = sol[("dec", id(p))]
-            else:
-                from ..ops import reference as ref
-                d = ref.rbf_decision(Zh.double(), Z[p.rows].double(), coef, p.gamma, 0.0) - r
-            dec[p.held] = -d    # × submodel label[0] (= −1)
+                dec[torch.as_tensor(p.held, device=device)] = p.const
         lab = torch.where(torch.arange(l, device=device) < mt["n0"], 1.0, -1.0)
         decs.append(dec)
         labs.append(lab)
@@ -568,7 +624,7 @@ def finish_svc_batch(st: dict):
         pos_idx = torch.nonzero(sv).squeeze(1)
         yint = torch.where(pos_idx < mt["n0"], 1.0, -1.0).to(torch.float64)
         coef = yint * a[pos_idx]
-        support = mt["grouped"][pos_idx]
+        support = torch.as_tensor(mt["grouped"], device=device)[pos_idx]
         n_sv0 = int((pos_idx < mt["n0"]).sum())
         A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
         svc.set_fitted(support=support, support_vectors=Z[support].to(torch.float64),

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from ..utils.timing import StageTimer
@@ -97,7 +98,14 @@ def fit_base_batch(est, X, y, masks, group=None, timer=None):
     return clones
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer):
+def _index_to(a, device) -> torch.Tensor:
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))
+    if torch.device(device).type != "cuda":
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
+def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -133,6 +141,8 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer):
             for i, (name, est) in enumerate(clf.estimators):
                 if i not in svc_cols:
                     out[i] = fit_base_batch(est, X, y, masks, group=group)
+                    if oof is not None:
+                        oof(i, out[i])
                     marks.append((f"{name}_host_done", _t.perf_counter()))
         with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
@@ -141,6 +151,8 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer):
                 else:
                     finish_svc_batch_distributed(st, group)
                 out[i] = clones
+                if oof is not None:
+                    oof(i, clones)
         marks.append(("svc_finished", _t.perf_counter()))
         main.wait_stream(side)
         main.wait_stream(other)
@@ -155,25 +167,32 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     dev = X.device
     n = X.shape[0]
     if group is None:
-        folds = torch.as_tensor(stratified_kfold_test_folds(y.cpu().numpy(), N_FOLDS), device=dev)
+        folds_np = stratified_kfold_test_folds(y.cpu().numpy(), N_FOLDS)
     else:
         from ..parallel import dist as pdist
-        folds = pdist.sharded_stratified_folds(y, N_FOLDS, group)
-    masks = fold_masks(folds.cpu().numpy(), N_FOLDS, device=dev)        # [6, n]
-    full, oof = [], []
+        folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
+    masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
+    # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
+    # gathers / scatters then need no host synchronisation
+    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+    full = []
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer)
+
+    def oof(col, fitted):
+        for k in range(N_FOLDS):
+            if test_idx[k].numel():
+                p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
+                meta[:, col].index_copy_(0, test_idx[k], p1)
+
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
-            fitted = fitted_all[col]
+            fitted = fitted_all[col]        # OOF column already filled on the fitting stream
         else:
             with timer.stage(f"fit_{name}"):
                 fitted = fit_base_batch(est, X, y, masks, group=group)
-        with timer.stage(f"oof_{name}"):
-            for k in range(N_FOLDS):
-                test = folds == k
-                if bool(test.any()):
-                    meta[test, col] = fitted[k].predict_proba(X[test])[:, 1].to(torch.float64)
+            with timer.stage(f"oof_{name}"):
+                oof(col, fitted)
         full.append(fitted[N_FOLDS])
     with timer.stage("fit_meta"):
         final = clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
