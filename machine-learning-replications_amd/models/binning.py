@@ -8,14 +8,21 @@ distinct values are grouped into ``max_bins`` quantile groups; a split between
 groups uses the midpoint of the left group's max and the right group's min.
 
 With a process group the distinct-value tables are merged across ranks so every
-rank bins identically (all-gather of the per-rank value sets).
+rank bins identically (all-gather of the per-rank value sets).  Single-process fits of up to
+``HOST_BIN_MAX_ROWS`` rows take the distinct values from ONE device→host copy (numpy) instead of a
+device ``unique`` + host read per feature; ``transform`` is one batched ``searchsorted`` against
+the +inf-padded edge table of all features.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
-from typing import List
+from typing import List, Optional
 
+import numpy as np
 import torch
+
+HOST_BIN_MAX_ROWS = int(os.environ.get("HFENS_HOST_BIN_ROWS", str(1 << 17)))
 
 
 @dataclass
@@ -25,20 +32,30 @@ class BinMapper:
     hi_val: torch.Tensor    # [F, 256] f64 (max value in bin)
     uppers: List[torch.Tensor]  # per feature f32 bin upper edges (= hi values)
     max_bins: int
+    nb_host: Optional[np.ndarray] = None   # host copy of nbins
+    edges: Optional[torch.Tensor] = None   # [F, max_nb] f32 upper edges, +inf padded
 
     @property
     def max_nb(self) -> int:
-        return int(self.nbins.max())
+        return int(self.nb_host.max()) if self.nb_host is not None else int(self.nbins.max())
 
     def transform(self, X: torch.Tensor) -> torch.Tensor:
-        """``X [n, F]`` → feature-major uint8 bins ``[F, n]``."""
-        n, F = X.shape
-        out = torch.empty(F, n, dtype=torch.uint8, device=X.device)
-        X32 = X.to(torch.float32)
-        for f in range(F):
-            idx = torch.searchsorted(self.uppers[f], X32[:, f].contiguous())
-            out[f] = idx.clamp_(max=int(self.nbins[f]) - 1).to(torch.uint8)
-        return out
+        """``X [n, F]`` → feature-major uint8 bins ``[F, n]`` (one batched searchsorted: a value
+        above every real edge lands on the first +inf pad = the edge count, then clamps to the
+        last bin exactly as a per-feature search would)."""
+        X32 = X.to(torch.float32).t().contiguous()
+        edges = self.edges if self.edges is not None else _pad_edges(self.uppers, X.device)
+        idx = torch.searchsorted(edges.to(X32.device), X32)
+        idx = torch.minimum(idx, (self.nbins.to(device=idx.device, dtype=idx.dtype) - 1)[:, None])
+        return idx.to(torch.uint8)
+
+
+def _pad_edges(uppers: List[torch.Tensor], device) -> torch.Tensor:
+    K = max(int(u.numel()) for u in uppers)
+    E = torch.full((len(uppers), K), float("inf"), dtype=torch.float32)
+    for f, u in enumerate(uppers):
+        E[f, :u.numel()] = u.cpu()
+    return E.to(device)
 
 
 def _distinct(v32: torch.Tensor, group=None):
@@ -55,14 +72,20 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
     n, F = X.shape
     dev = X.device
     X32 = X.to(torch.float32)
+    host = group is None and n <= HOST_BIN_MAX_ROWS
+    Xh = X32.cpu().numpy() if host else None
     nb = torch.empty(F, dtype=torch.int32)
     lo = torch.zeros(F, 256, dtype=torch.float64)
     hi = torch.zeros(F, 256, dtype=torch.float64)
-    uppers = []
+    ups = []
     for f in range(F):
-        u, c = _distinct(X32[:, f].contiguous(), group)
-        u = u.cpu()
-        c = c.cpu()
+        if host:
+            uu, cc = np.unique(Xh[:, f], return_counts=True)
+            u, c = torch.from_numpy(uu), torch.from_numpy(cc.astype(np.int64))
+        else:
+            u, c = _distinct(X32[:, f].contiguous(), group)
+            u = u.cpu()
+            c = c.cpu()
         k = u.numel()
         if k <= max_bins:
             nb[f] = k
@@ -82,5 +105,8 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
             lo[f, :g] = u[starts].double()
             hi[f, :g] = u[ends].double()
             up = u[ends].clone()
-        uppers.append(up.to(dev, torch.float32).contiguous())
-    return BinMapper(nb.to(dev), lo.to(dev), hi.to(dev), uppers, max_bins)
+        ups.append(up.to(torch.float32))
+    edges = _pad_edges(ups, dev)
+    uppers = [edges[f, :ups[f].numel()] for f in range(F)]
+    return BinMapper(nb.to(dev), lo.to(dev), hi.to(dev), uppers, max_bins, nb_host=nb.numpy().copy(),
+                     edges=edges)

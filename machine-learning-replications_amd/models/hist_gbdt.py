@@ -21,6 +21,7 @@ Exactness notes (vs sklearn ``GradientBoostingClassifier``):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -366,9 +367,42 @@ def _allreduce_r2(st, t, group):
     pdist.all_reduce_sum_(st.r2[t], group)
 
 
+# Depth-1 trees on up to FUSED_MAX_ROWS rows (one process) train in ONE launch
+# (gbdt.hip ``gbdt_stumps_fused``: a workgroup per model runs every stage's apply/hist/split with
+# the same fixed-point sums — bit-identical to the launch-per-step loop below, without its 4
+# launches and host round trips per stage).
+FUSED_STUMPS = os.environ.get("HFENS_GBDT_FUSED", "1") != "0"
+FUSED_MAX_ROWS = int(os.environ.get("HFENS_GBDT_FUSED_ROWS", str(1 << 16)))
+_FUSED_LDS = 120 * 1024
+LAST_PATH = {"path": None}
+
+
+def _fused_ok(st: _State, group) -> bool:
+    nbh = st.bm.nb_host
+    return (FUSED_STUMPS and group is None and st.D == 1 and st.F <= 128 and st.n <= FUSED_MAX_ROWS
+            and nbh is not None and 24 * int(nbh.sum()) <= _FUSED_LDS)
+
+
+def _run_fused(st: _State):
+    from .. import ops
+    bm = st.bm
+    ops.ext().gbdt_stumps_fused(
+        st.B, st.n, st.F, st.T, st.bins.data_ptr(), bm.nbins.data_ptr(), int(bm.nb_host.sum()),
+        bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(), st.raw.data_ptr(),
+        st.g.data_ptr(), st.h.data_ptr(), st.wt.data_ptr() if st.wt is not None else 0,
+        st.seeds.data_ptr() if st.seeds is not None else 0, st.row_off, st.subsample,
+        st.feat.data_ptr(), st.blo.data_ptr(), st.thr.data_ptr(), st.value.data_ptr(), st.stats.data_ptr(),
+        st.r2.data_ptr(), st.dev.data_ptr(), st.bagw.data_ptr() if st.bagw is not None else 0,
+        st.lr, st.qscale, st.dscale, st.min_leaf_q, st.min_split_q, ops.stream_ptr(st.raw.device))
+
+
 def _run_device(st: _State, group):
     from .. import ops
     from ..ops import stream_ptr
+    if _fused_ok(st, group):
+        LAST_PATH["path"] = "fused"
+        return _run_fused(st)
+    LAST_PATH["path"] = "launch"
     E = ops.ext()
     s = stream_ptr(st.raw.device)
     max_nb = st.bm.max_nb

@@ -14,9 +14,14 @@ Both converge to the unique optimum well below liblinear's / lbfgs's tolerance,
 so coefficients agree with sklearn to its own stopping accuracy.
 With ``group`` (rows sharded over ranks) the per-iteration g, H and line-search
 losses are all-reduced (F² + F + 8 doubles per model).
+
+On one GPU the whole solve runs as ONE launch (``ops/csrc/logreg.hip`` ``logreg_fused``: one
+workgroup per model, the same three passes per iteration, no host round trip); the loop below
+is the host / data-parallel path and the reference the fused kernel is tested against.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -64,6 +69,26 @@ def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
     return torch.as_tensor(out, dtype=g.dtype, device=g.device)
 
 
+FUSED = os.environ.get("HFENS_LOGREG_FUSED", "1") != "0"
+LAST_PATH = {"path": None}
+
+
+def _fit_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int):
+    """All B solves in one ``logreg_fused`` launch; returns (W [B, F1], n_iter [B] int32)."""
+    E = ops.ext()
+    B, n = s.shape
+    F1 = Xa.shape[1]
+    dev = Xa.device
+    Xc, sc, yc = Xa.contiguous(), s.contiguous(), ypm.contiguous()
+    W = torch.empty(B, F1, dtype=torch.float64, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    Z = torch.empty(B, n, dtype=torch.float64, device=dev)
+    Xd = torch.empty_like(Z)
+    E.logreg_fused(B, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C), int(l1),
+                   int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(), ops.stream_ptr(dev))
+    return W, iters
+
+
 def _allreduce(ts, group):
     if group is None:
         return ts
@@ -109,6 +134,15 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
     if not l1 and m0.fit_intercept:
         penal[-1] = 0  # lbfgs path: intercept not penalised
     pen_f = penal.to(torch.float64)
+    scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
+    if X.is_cuda and group is None and FUSED and F1 <= 64 and n > 0:
+        LAST_PATH["path"] = "fused"
+        W, iters = _fit_fused(Xa, s, ypm, penal, C, l1, max_outer)
+        for b, m in enumerate(models):
+            intercept = W[b, F] * scale if m0.fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
+            m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
+        return models
+    LAST_PATH["path"] = "loop"
     W = torch.zeros(B, F1, dtype=torch.float64, device=dev)
     alphas = 0.5 ** torch.arange(8, dtype=torch.float64, device=dev)
 
@@ -183,7 +217,6 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
         Z = Z + a[None, :] * Xd
         if bool(((a[:, None] * d).abs().max(1).values <= 1e-14 * (1 + W.abs().max(1).values)).all()):
             break
-    scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
     for b, m in enumerate(models):
         coef = W[b, :F]
         intercept = W[b, F] * scale if m0.fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)

@@ -351,6 +351,33 @@ def _pick_solver(max_l: int) -> str:
     return "ws" if max_l >= WS_MIN_POINTS else "exact"
 
 
+# Cooperative exact SMO (ops/csrc/svm_coop.hip): every problem's points are split over W
+# workgroups that exchange their WSS partials inside the launch — the same pair sequence as the
+# one-workgroup smo_kernel, with 1/W of the per-pair VALU work on each CU.  W is as large as the
+# CU count allows (at most one member per CU, ≤ 16) while keeping ≥ COOP_MIN_SLICE points per member.
+COOP = os.environ.get("HFENS_SMO_COOP", "1") != "0"
+COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
+_COOP_MAX_W = 16
+_COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)
+_COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
+                     ("S", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
+_NCU: dict = {}
+
+
+def _num_cus(device) -> int:
+    d = torch.device(device)
+    if d not in _NCU:
+        _NCU[d] = int(torch.cuda.get_device_properties(d).multi_processor_count)
+    return _NCU[d]
+
+
+def coop_members(P: int, max_l: int, ncu: int) -> int:
+    """Workgroups per problem for the cooperative SMO (1 = the one-workgroup kernel)."""
+    if not COOP or PROFILE_SMO or P <= 0:
+        return 1
+    return max(1, min(_COOP_MAX_W, ncu // P, -(-max_l // COOP_MIN_SLICE)))
+
+
 def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     g = np.zeros(len(live), _GRAM_DT)
     sm = np.zeros(len(live), _SMO_DT)
@@ -370,15 +397,30 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     iters = torch.empty(len(live), dtype=torch.int32, device=device)
     gap = torch.empty(len(live), dtype=torch.float64, device=device)
     max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
-    sdev = _dev_struct(sm, device)
-    prof = torch.zeros(len(live) * 5, dtype=torch.int64, device=device) if PROFILE_SMO else None
-    E.smo_batch(sdev.data_ptr(), len(live), max_l, K.data_ptr(), alpha.data_ptr(), eps, max_iter,
-                rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
-    if prof is not None:
-        LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
-                             l=np.array([p.l for p in live]))
+    W = coop_members(len(live), max_l, _num_cus(device))
+    err = None
+    if W > 1:
+        cp = np.zeros(len(live), _COOP_DT)
+        for k, p in enumerate(live):
+            S = -(-(-(-p.l // W)) // 4) * 4
+            cp[k] = (sm[k]["koff"], aoffs[k], p.l, sm[k]["ld"], p.npos, S, p.Cp, p.Cn)
+        cdev = _dev_struct(cp, device)
+        xchg = torch.empty(len(live) * _COOP_GRANULES, dtype=torch.int64, device=device)
+        err = torch.zeros(1, dtype=torch.int32, device=device)
+        E.smo_coop_batch(cdev.data_ptr(), len(live), W, int(cp["S"].max()), K.data_ptr(), alpha.data_ptr(),
+                         xchg.data_ptr(), eps, max_iter, rho.data_ptr(), iters.data_ptr(), gap.data_ptr(),
+                         err.data_ptr(), s)
+    else:
+        sdev = _dev_struct(sm, device)
+        prof = torch.zeros(len(live) * 5, dtype=torch.int64, device=device) if PROFILE_SMO else None
+        E.smo_batch(sdev.data_ptr(), len(live), max_l, K.data_ptr(), alpha.data_ptr(), eps, max_iter,
+                    rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
+        if prof is not None:
+            LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
+                                 l=np.array([p.l for p in live]))
+    LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l)
     del K
-    return alpha, rho, iters
+    return alpha, rho, iters, err
 
 
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
@@ -429,15 +471,56 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     LAST_WS_STATS.update(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
                          cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
                          cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5])
-    return alpha, rho, iters
+    return alpha, rho, iters, None
 
 
 LAST_WS_STATS: dict = {}
 LAST_SMO_PROF: dict = {}
+LAST_SMO_INFO: dict = {}
 PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
 
 
-def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
+def assign_problems(sizes, world: int) -> List[int]:
+    """Owner rank of every SMO problem: longest-processing-time-first (largest problem onto the
+    least-loaded rank; cost ∝ points, since pairs grow ~linearly with l and the cooperative
+    solver's per-pair time is ~flat).  Deterministic, identical on every rank."""
+    load = [0] * world
+    owner = [0] * len(sizes)
+    for k in sorted(range(len(sizes)), key=lambda k: (-sizes[k], k)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[k] = r
+        load[r] += sizes[k]
+    return owner
+
+
+def _solve_distributed(solve_local, live, n_alpha, aoffs, device, group):
+    """Task-parallel SMO (SURVEY.md §2.4 ensemble parallel, call site R9): rank r solves the
+    problems ``assign_problems`` gives it; one SUM all-reduce of a zero-filled
+    [α | ρ | iters | err] vector (every entry has exactly one non-zero contributor, so the sum is
+    exact) gives every rank every solution."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    owner = assign_problems([p.l for p in live], world)
+    mine = [k for k in range(len(live)) if owner[k] == rank]
+    P = len(live)
+    flat = torch.zeros(n_alpha + 2 * P + 1, dtype=torch.float64, device=device)
+    if mine:
+        sub = [live[k] for k in mine]
+        a_s, r_s, it_s, err_s = solve_local(sub)
+        so = np.concatenate([[0], np.cumsum([p.l for p in sub])]).astype(np.int64)
+        for i, k in enumerate(mine):
+            flat[aoffs[k]:aoffs[k] + live[k].l] = a_s[so[i]:so[i + 1]].to(torch.float64)
+        idx = _to_dev(np.asarray(mine, dtype=np.int64), device)
+        flat[n_alpha:n_alpha + P].index_copy_(0, idx, r_s.to(torch.float64).reshape(-1))
+        flat[n_alpha + P:n_alpha + 2 * P].index_copy_(0, idx, it_s.to(torch.float64).reshape(-1))
+        if err_s is not None:
+            flat[n_alpha + 2 * P:] += err_s.to(torch.float64)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    return (flat[:n_alpha], flat[n_alpha:n_alpha + P], flat[n_alpha + P:n_alpha + 2 * P].round().to(torch.int32),
+            flat[n_alpha + 2 * P:])
+
+
+def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None):
     from .. import ops
     E = ops.ext()
     s = ops.stream_ptr(device)
@@ -452,8 +535,17 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
     max_l = max(p.l for p in live)
     solver = _pick_solver(max_l)
     solve = _solve_ws if solver == "ws" else _solve_exact
-    alpha, rho, iters = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)
-    out = {}
+    if group is None:
+        alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)
+    else:
+        def solve_local(sub):
+            zsub = _gather_rows(Zs, sub, "rows", device)
+            so = [0]
+            for p in sub:
+                so.append(so[-1] + p.l)
+            return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s)
+        alpha, rho, iters, err = _solve_distributed(solve_local, live, aoffs[-1], aoffs, device, group)
+    out = {"smo_err": err}
     for k, p in enumerate(live):
         a0 = aoffs_start[k]
         out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
@@ -492,30 +584,48 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None):
     return out
 
 
-def _solve_host(probs: List[_Prob], Zs, eps, max_iter_cap=None):
+def _solve_host(probs: List[_Prob], Zs, eps, max_iter_cap=None, group=None):
+    live = [p for p in probs if p.rows is not None]
+
+    def solve_local(sub):
+        alphas, rhos, its = [], [], []
+        for p in sub:
+            Zp = Zs[p.fit][torch.as_tensor(p.rows)].double().cpu().numpy()
+            K = _gram_host(Zp, p.gamma)
+            l = K.shape[0]
+            mi = max(10_000_000, 100 * l) if max_iter_cap is None else max_iter_cap
+            a, r, it = _smo_host(K, p.npos, p.Cp, p.Cn, eps, mi)
+            alphas.append(torch.as_tensor(a))
+            rhos.append(r)
+            its.append(it)
+        return (torch.cat(alphas) if alphas else torch.zeros(0, dtype=torch.float64),
+                torch.tensor(rhos, dtype=torch.float64), torch.tensor(its, dtype=torch.int64), None)
+
+    aoffs = [0]
+    for p in live:
+        aoffs.append(aoffs[-1] + p.l)
+    if group is None:
+        alpha, rho, iters, _ = solve_local(live)
+    else:
+        alpha, rho, iters, _ = _solve_distributed(solve_local, live, aoffs[-1], aoffs, torch.device("cpu"), group)
     out = {}
-    for p in probs:
-        if p.rows is None:
-            continue
-        Zp = Zs[p.fit][torch.as_tensor(p.rows)].double().cpu().numpy()
-        K = _gram_host(Zp, p.gamma)
-        l = K.shape[0]
-        mi = max(10_000_000, 100 * l) if max_iter_cap is None else max_iter_cap
-        a, r, it = _smo_host(K, p.npos, p.Cp, p.Cn, eps, mi)
-        out[id(p)] = (torch.as_tensor(a), torch.tensor(r, dtype=torch.float64), torch.tensor(it))
+    for k, p in enumerate(live):
+        out[id(p)] = (alpha[aoffs[k]:aoffs[k + 1]].clone(), rho[k].clone(), iters[k].clone())
     return out
 
 
 # ----------------------------------------------------------------------------- public
-def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None):
+def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None):
     """Fit ``svcs[f]`` on (already scaled) ``Zs[f]`` with labels ``ys[f]`` ∈ {0,1}."""
-    return finish_svc_batch(launch_svc_batch(svcs, Zs, ys, max_iter_cap))
+    return finish_svc_batch(launch_svc_batch(svcs, Zs, ys, max_iter_cap, group=group))
 
 
-def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None) -> dict:
+def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
-    with :func:`finish_svc_batch`."""
+    with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
+    problems are solved task-parallel over the ranks (:func:`assign_problems`) and their
+    solutions all-reduced — one collective, issued from the calling thread."""
     from .. import ops
     from ..utils.guards import check_binary, check_finite
     for f, (Z, y) in enumerate(zip(Zs, ys)):
@@ -549,7 +659,8 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         all_probs += pr
         meta.append(mt)
     eps = float(svcs[0].tol)
-    sol = _solve_device(all_probs, Zs, device, eps, max_iter_cap) if cuda else _solve_host(all_probs, Zs, eps, max_iter_cap)
+    sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
+           else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
     AB = [None] * len(svcs)
     decs, labs, pl = [], [], []
@@ -609,6 +720,9 @@ def finish_svc_batch(st: dict):
     """Platt parameters to the host, support-vector extraction, ``set_fitted``."""
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
                                                    st["sol"], st["AB"], st["device"])
+    err = sol.get("smo_err")
+    if err is not None and float(err.max()) != 0.0:
+        raise RuntimeError("cooperative SMO: a member exchange timed out (members not co-resident?)")
     if st["ABt"] is not None:
         from ..utils.guards import check_finite
         check_finite(st["ABt"], "SVC Platt sigmoid (A, B)")

@@ -79,13 +79,15 @@ def _svc_inputs(est, X, y, masks):
     return clones, svcs, Zs, ys
 
 
-def fit_base_batch(est, X, y, masks, group=None, timer=None):
-    """Fit ``masks.shape[0]`` clones of ``est`` on the masked row subsets; returns them."""
+def fit_base_batch(est, X, y, masks, group=None, timer=None, svc_group=None):
+    """Fit ``masks.shape[0]`` clones of ``est`` on the masked row subsets; returns them.
+    ``group``: rows sharded over ranks (data parallel); ``svc_group``: rows replicated on every
+    rank, only the SMO problems are spread over the ranks (task parallel)."""
     kind = _kind(est)
     if kind in ("svc", "svc_raw"):
         clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks)
         if group is None:
-            fit_svc_batch(svcs, Zs, ys)
+            fit_svc_batch(svcs, Zs, ys, group=svc_group)
         else:
             from ..parallel.stack import fit_svc_batch_distributed
             fit_svc_batch_distributed(svcs, Zs, ys, group)
@@ -105,7 +107,7 @@ def _index_to(a, device) -> torch.Tensor:
     return t.pin_memory().to(device, non_blocking=True)
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None):
+def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -133,7 +135,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None):
                 clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks)
                 marks.append(("svc_inputs", _t.perf_counter()))
                 if group is None:
-                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys))
+                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group))
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
                 marks.append(("svc_launched", _t.perf_counter()))
@@ -162,7 +164,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None):
     return [out[i] for i in range(len(kinds))]
 
 
-def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None):
+def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None):
     timer = timer or StageTimer(enabled=False)
     dev = X.device
     n = X.shape[0]
@@ -184,13 +186,13 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof)
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream
         else:
             with timer.stage(f"fit_{name}"):
-                fitted = fit_base_batch(est, X, y, masks, group=group)
+                fitted = fit_base_batch(est, X, y, masks, group=group, svc_group=svc_group)
             with timer.stage(f"oof_{name}"):
                 oof(col, fitted)
         full.append(fitted[N_FOLDS])

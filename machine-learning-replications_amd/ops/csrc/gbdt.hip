@@ -457,4 +457,313 @@ void gbdt_route(int B, int n, int NN, uintptr_t bins, uintptr_t g, uintptr_t w, 
   launch_check();
 }
 
+// ------------------------------------------------------------------------------------------
+// E: depth-1 trees on few rows — the whole boosting run in ONE launch (gbdt_stumps_fused).
+//    One 1024-thread workgroup per model runs, for every stage, exactly A (apply_prep) → B (root
+//    histogram) → C (root split) above: same per-row arithmetic, same fixed-point sums, same
+//    split rule and tie-breaks, so trees, leaf values, impurities and train_score_ equal the
+//    launch-per-step path's.  What goes away is 4 launches and the host round trips of every stage
+//    (the bench's 6-model GBC: ≈18 ms of host enqueue for 100 stages).  The root histograms of all
+//    features live in LDS in a compact layout (feature f's bins start at off[f]); ≤ 8-bin features
+//    accumulate in registers and fold once per feature, wider ones use ds_add_u64.
+constexpr int kStThreads = 1024;
+constexpr int kStWaves = kStThreads / 64;
+constexpr int kStMaxF = 128;
+
+struct StumpJob {
+  const unsigned char* bins;          // [F][n]
+  const int* nbins;                   // [F]
+  const double* lo_val;               // [F][256]
+  const double* hi_val;               // [F][256]
+  const float* y;                     // [n]
+  const float* w;                     // [B][n]
+  double* raw;                        // [B][n]
+  float* g;                           // [B][n]
+  float* h;                           // [B][n]
+  float* wt;                          // [B][n] in-bag weights (bagging) or nullptr
+  const unsigned long long* seeds;    // [B] (bagging) or nullptr
+  int* feat;                          // [T][B][3]
+  int* blo;                           // [T][B][3]
+  double* thr;                        // [T][B][3]
+  double* value;                      // [T][B][3]
+  long long* stats;                   // [T][B][3][4]
+  long long* r2;                      // [T][B][3]
+  long long* dev;                     // [T][B]
+  double* bagw;                       // [T][B] (bagging) or nullptr
+  long long row_off;
+  double lr, qscale, dscale, min_leaf_q, min_split_q;
+  unsigned thr24;
+  int active, B, n, F, T, hist_len;   // hist_len = Σ_f nbins[f]
+};
+
+// Root histogram of one ≤ C-bin feature over the workgroup: per-thread registers, one fold.
+// g/h/w were written by this workgroup earlier in the launch (vector loads, no __restrict__).
+template <int C>
+__device__ __forceinline__ void stump_hist_regs(const unsigned char* __restrict__ col, const float* g,
+                                                const float* h, const float* w, int n, int nb, double qscale,
+                                                long long* out /*[nb][3] LDS*/, long long* red) {
+  long long ag[C], ah[C], aw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { ag[c] = 0; ah[c] = 0; aw[c] = 0; }
+  for (int i = threadIdx.x; i < n; i += kStThreads) {
+    const float wi = w[i];
+    if (!(wi > 0.f)) continue;
+    const int bb = col[i];
+    const long long qg = q_of(g[i], qscale), qh = q_of(h[i], qscale), qw = q_of(wi, qscale);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const bool m = bb == c;
+      ag[c] += m ? qg : 0;
+      ah[c] += m ? qh : 0;
+      aw[c] += m ? qw : 0;
+    }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const long long a = wave_sum_i64(ag[c]), b2 = wave_sum_i64(ah[c]), c2 = wave_sum_i64(aw[c]);
+    if (lane == 0) {
+      red[wave * 24 + 3 * c] = a;
+      red[wave * 24 + 3 * c + 1] = b2;
+      red[wave * 24 + 3 * c + 2] = c2;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < 3 * nb) {
+    long long s = 0;
+    for (int k = 0; k < kStWaves; ++k) s += red[k * 24 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kStThreads) void gbdt_stumps_fused_kernel(StumpJob J) {
+  extern __shared__ __attribute__((aligned(16))) long long hl[];   // [hist_len][3]
+  __shared__ long long red[kStWaves * 24];
+  __shared__ int s_nb[kStMaxF], s_off[kStMaxF];
+  __shared__ long long tot[3], root_r2;
+  __shared__ double wg[kStWaves];
+  __shared__ int wf[kStWaves], wbin[kStWaves];
+  __shared__ int tf0, tblo, bad;   // previous tree: root feature (−3 empty, −2 leaf) and split bin
+  __shared__ double tval[3];       // previous tree: node values
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = J.n, F = J.F, B = J.B;
+  if (tid == 0) {
+    int o = 0;
+    for (int f = 0; f < F; ++f) { s_nb[f] = J.nbins[f]; s_off[f] = o; o += s_nb[f]; }
+    bad = o != J.hist_len;   // host and device bin tables disagree: write nothing
+    tf0 = -3; tblo = 0; tval[0] = tval[1] = tval[2] = 0.0;
+  }
+  __syncthreads();
+  if (bad) return;
+  const size_t boff = (size_t)b * n;
+  const float* wb = J.w + boff;
+  double* raw = J.raw + boff;
+  float* g = J.g + boff;
+  float* h = J.h + boff;
+  float* wt = J.active ? J.wt + boff : nullptr;
+  const float* wcur = J.active ? wt : wb;
+  for (int t = 0; t <= J.T; ++t) {
+    // ---- A: apply the previous stump, this stage's residuals (gbdt_apply_prep_kernel)
+    const bool has_prev = t > 0;
+    const int pf = tf0, pblo = tblo;
+    const double pv0 = tval[0], pv1 = tval[1], pv2 = tval[2];
+    long long dev_q = 0, r2_q = 0, n0 = 0, n1 = 0, n2 = 0;
+    double bag = 0.0;
+    for (int i = tid; i < n; i += kStThreads) {
+      const float w0 = wb[i];
+      float wi = w0, wp = w0;
+      if (J.active) {
+        const unsigned long long sd = J.seeds[b];
+        wi = gb_in_bag(sd, t, J.row_off + i, J.thr24) ? w0 : 0.f;
+        wp = (has_prev && gb_in_bag(sd, t - 1, J.row_off + i, J.thr24)) ? w0 : 0.f;
+        wt[i] = wi;
+        bag += (double)wi;
+      }
+      double rw = raw[i];
+      const double yi = J.y[i];
+      if (has_prev) {
+        const int nd = pf >= 0 ? (J.bins[(size_t)pf * n + i] <= pblo ? 1 : 2) : 0;
+        if (wp > 0.f) {
+          const double p0 = 1.0 / (1.0 + exp(-rw));
+          const double r0 = yi - p0;
+          const long long q = q_of(wp * r0 * r0, J.qscale);
+          n0 += nd == 0 ? q : 0;
+          n1 += nd == 1 ? q : 0;
+          n2 += nd == 2 ? q : 0;
+        }
+        rw += J.lr * (nd == 0 ? pv0 : (nd == 1 ? pv1 : pv2));
+        raw[i] = rw;
+      }
+      const double p = 1.0 / (1.0 + exp(-rw));
+      const double r = yi - p;
+      g[i] = (float)(wi * r);
+      h[i] = (float)(wi * p * (1.0 - p));
+      if (wp > 0.f) {
+        const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
+        dev_q += q_of(wp * (-2.0) * (yi * rw - l1p), J.dscale);
+      }
+      if (wi > 0.f) r2_q += q_of(wi * r * r, J.qscale);
+    }
+    dev_q = wave_sum_i64(dev_q);
+    r2_q = wave_sum_i64(r2_q);
+    n0 = wave_sum_i64(n0);
+    n1 = wave_sum_i64(n1);
+    n2 = wave_sum_i64(n2);
+    bag = wave_sum(bag);   // in-bag weights are 0/1 masks: exact in any order
+    if (lane == 0) {
+      long long* rr = red + wave * 24;
+      rr[0] = dev_q; rr[1] = r2_q; rr[2] = n0; rr[3] = n1; rr[4] = n2; rr[5] = __double_as_longlong(bag);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      long long s[5] = {0, 0, 0, 0, 0};
+      double bs = 0.0;
+      for (int k = 0; k < kStWaves; ++k) {
+        for (int j = 0; j < 5; ++j) s[j] += red[k * 24 + j];
+        bs += __longlong_as_double(red[k * 24 + 5]);
+      }
+      if (has_prev) {
+        const size_t pb = (size_t)(t - 1) * B + b;
+        J.dev[pb] += s[0];
+        J.r2[pb * 3] += s[2];
+        J.r2[pb * 3 + 1] += s[3];
+        J.r2[pb * 3 + 2] += s[4];
+      }
+      if (t < J.T) {
+        const size_t tb = (size_t)t * B + b;
+        J.r2[tb * 3] += s[1];
+        root_r2 = J.r2[tb * 3];
+        if (J.active) J.bagw[tb] = bs;
+      }
+    }
+    __syncthreads();
+    if (t == J.T) break;
+    // ---- B: root histograms of every feature (gbdt_hist_kernel, NL = 1)
+    for (int k = tid; k < 3 * J.hist_len; k += kStThreads) hl[k] = 0;
+    __syncthreads();
+    for (int f = 0; f < F; ++f) {
+      const int nb = s_nb[f];
+      const unsigned char* col = J.bins + (size_t)f * n;
+      long long* out = hl + (size_t)s_off[f] * 3;
+      if (nb <= 2) stump_hist_regs<2>(col, g, h, wcur, n, nb, J.qscale, out, red);
+      else if (nb <= 4) stump_hist_regs<4>(col, g, h, wcur, n, nb, J.qscale, out, red);
+      else if (nb <= 8) stump_hist_regs<8>(col, g, h, wcur, n, nb, J.qscale, out, red);
+      else {
+        for (int i = tid; i < n; i += kStThreads) {
+          const float wi = wcur[i];
+          if (!(wi > 0.f)) continue;
+          long long* cell = out + (size_t)col[i] * 3;
+          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)q_of(g[i], J.qscale));
+          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)q_of(h[i], J.qscale));
+          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)q_of(wi, J.qscale));
+        }
+      }
+    }
+    __syncthreads();
+    // ---- C: root split (gbdt_split_kernel's rule; 16 waves scan features f ≡ wave mod 16)
+    if (wave == 0) {
+      long long a = 0, c = 0, d = 0;
+      for (int bb = lane; bb < s_nb[0]; bb += 64) { a += hl[bb * 3]; c += hl[bb * 3 + 1]; d += hl[bb * 3 + 2]; }
+      a = wave_sum_i64(a);
+      c = wave_sum_i64(c);
+      d = wave_sum_i64(d);
+      if (lane == 0) { tot[0] = a; tot[1] = c; tot[2] = d; }
+    }
+    __syncthreads();
+    const long long tg = tot[0], th = tot[1], tw = tot[2];
+    const size_t tb = (size_t)t * B + b;
+    if (tw <= 0) {   // empty root (block-uniform)
+      if (tid == 0) { J.feat[tb * 3] = -3; tf0 = -3; tblo = 0; tval[0] = tval[1] = tval[2] = 0.0; }
+      __syncthreads();
+      continue;
+    }
+    double bg = -1.0;
+    int bf = 0x7fffffff, bbin = 0;
+    if ((double)tw >= J.min_split_q) {
+      for (int f = wave; f < F; f += kStWaves) {
+        double gg;
+        int gb;
+        scan_feature(hl + (size_t)s_off[f] * 3, s_nb[f], lane, tw, tg, J.min_leaf_q, gg, gb);
+        if (gg > bg) { bg = gg; bf = f; bbin = gb; }   // f ascending within a wave
+      }
+    }
+    if (lane == 0) { wg[wave] = bg; wf[wave] = bf; wbin[wave] = bbin; }
+    __syncthreads();
+    if (tid == 0) {
+      bg = wg[0]; bf = wf[0]; bbin = wbin[0];
+      for (int k = 1; k < kStWaves; ++k)
+        if (wg[k] > bg || (wg[k] == bg && wf[k] < bf)) { bg = wg[k]; bf = wf[k]; bbin = wbin[k]; }
+      long long* st = J.stats + tb * 3 * 4;
+      st[0] = tw; st[1] = tg; st[2] = th;
+      const double inv = 1.0 / J.qscale;
+      const double dw = tw * inv, dg = tg * inv;
+      const double imp = root_r2 * inv / dw - (dg / dw) * (dg / dw);
+      const bool can_split = bg >= 0.0 && bf < F && imp > 2.220446049250313e-16;
+      tval[1] = 0.0;
+      tval[2] = 0.0;
+      if (!can_split) {
+        J.feat[tb * 3] = -2;
+        J.blo[tb * 3] = 0;
+        J.thr[tb * 3] = -2.0;
+        const double den = th * inv;
+        const double v = fabs(den) < 1e-150 ? 0.0 : dg / den;
+        J.value[tb * 3] = v;
+        tf0 = -2; tblo = 0; tval[0] = v;
+      } else {
+        const long long* hf = hl + (size_t)s_off[bf] * 3;
+        long long lw = 0, lg = 0, lh = 0;
+        for (int bb = 0; bb <= bbin; ++bb) { lg += hf[bb * 3]; lh += hf[bb * 3 + 1]; lw += hf[bb * 3 + 2]; }
+        int hi = bbin + 1;
+        const int nbf = s_nb[bf];
+        while (hi < nbf - 1 && hf[hi * 3 + 2] == 0) ++hi;
+        const double a = J.hi_val[bf * 256 + bbin], c = J.lo_val[bf * 256 + hi];
+        double tt = a / 2.0 + c / 2.0;
+        if (tt == c || isinf(tt)) tt = a;
+        J.feat[tb * 3] = bf;
+        J.blo[tb * 3] = bbin;
+        J.thr[tb * 3] = tt;
+        J.value[tb * 3] = dg / dw;   // internal node value: weighted mean residual
+        long long* sl = st + 4;
+        long long* sr = st + 8;
+        sl[0] = lw; sl[1] = lg; sl[2] = lh;
+        sr[0] = tw - lw; sr[1] = tg - lg; sr[2] = th - lh;
+        J.feat[tb * 3 + 1] = -2; J.feat[tb * 3 + 2] = -2;
+        J.blo[tb * 3 + 1] = 0; J.blo[tb * 3 + 2] = 0;
+        J.thr[tb * 3 + 1] = -2.0; J.thr[tb * 3 + 2] = -2.0;
+        const double dl = lh * inv, dr = (th - lh) * inv;
+        const double vl = fabs(dl) < 1e-150 ? 0.0 : lg * inv / dl;
+        const double vr = fabs(dr) < 1e-150 ? 0.0 : (tg - lg) * inv / dr;
+        J.value[tb * 3 + 1] = vl;
+        J.value[tb * 3 + 2] = vr;
+        tf0 = bf; tblo = bbin; tval[0] = dg / dw; tval[1] = vl; tval[2] = vr;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void gbdt_stumps_fused(int B, int n, int F, int T, uintptr_t bins, uintptr_t nbins, int hist_len,
+                       uintptr_t lo_val, uintptr_t hi_val, uintptr_t y, uintptr_t w, uintptr_t raw, uintptr_t g,
+                       uintptr_t h, uintptr_t wt, uintptr_t seeds, long long row_off, double subsample,
+                       uintptr_t feat, uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats,
+                       uintptr_t r2, uintptr_t dev, uintptr_t bagw, double lr, double qscale, double dscale,
+                       double min_leaf_q, double min_split_q, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stumps_fused: 1 <= F <= 128");
+  HFENS_REQUIRE(B >= 1 && n >= 1 && T >= 1, "gbdt_stumps_fused: empty problem");
+  const bool active = subsample < 1.0;
+  HFENS_REQUIRE(!active || (wt != 0 && seeds != 0 && bagw != 0),
+                "gbdt_stumps_fused: subsample needs wt, seeds and bagw");
+  const size_t lds = (size_t)hist_len * 3 * sizeof(long long);
+  HFENS_REQUIRE(hist_len >= F && lds <= 120 * 1024, "gbdt_stumps_fused: root histograms do not fit LDS");
+  StumpJob J{(const unsigned char*)bins, (const int*)nbins, (const double*)lo_val, (const double*)hi_val,
+             (const float*)y, (const float*)w, (double*)raw, (float*)g, (float*)h, (float*)wt,
+             (const unsigned long long*)seeds, (int*)feat, (int*)blo, (double*)thr, (double*)value,
+             (long long*)stats, (long long*)r2, (long long*)dev, (double*)bagw, row_off, lr, qscale, dscale,
+             min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
+             hist_len};
+  hipLaunchKernelGGL(gbdt_stumps_fused_kernel, dim3(B), dim3(kStThreads), lds, as_stream(stream), J);
+  launch_check();
+}
+
 }  // namespace hfens

@@ -238,10 +238,11 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
     const int i = r1.idx;
     if (i < 0) break;
     const int yi = i < P.npos ? 1 : -1;
-    // ---- WSS step 2 over row i (second order, libsvm's "last index wins" on ties).  Per thread
-    // the candidates compare by cross-multiplication (no divide); one divide per thread at the end.
+    // ---- WSS step 2 over row i (second order, libsvm's "last index wins" on ties).  Every
+    // candidate is ranked by the quotient num/quad itself (libsvm's obj_diff, negated exactly), so
+    // the choice never depends on how points are grouped over threads or workgroups.
     const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)i * P.ld);
-    double gmax2 = -kInf, bnum = 0.0, bden = 1.0;
+    double gmax2 = -kInf, bkey = -kInf;
     int bj = -1;
     // issue every row-i load before touching any of them: one HBM latency, not K4
     float4 qv[K4];
@@ -265,15 +266,13 @@ __global__ __launch_bounds__(kSmoThreads) void smo_kernel(const SmoProb* __restr
           if (gd > 0) {
             double quad = 2.0 - 2.0 * (double)Qi[k];
             if (quad <= 0) quad = kTau;
-            const double num = gd * gd;
-            // num/quad > bnum/bden  (ties → larger index = later k within the thread)
-            const double lhs = num * bden, rhs = bnum * quad;
-            if (bj < 0 || lhs >= rhs) { bnum = num; bden = quad; bj = t0 + e; }
+            const double key = (gd * gd) / quad;
+            if (bj < 0 || key >= bkey) { bkey = key; bj = t0 + e; }   // ties → later index
           }
         }
       }
     }
-    Red3 r2{gmax2, bj >= 0 ? bnum / bden : -kInf, bj};
+    Red3 r2{gmax2, bj >= 0 ? bkey : -kInf, bj};
     tick(0);
     r2 = block_red3(r2, shB);
     tick(1);

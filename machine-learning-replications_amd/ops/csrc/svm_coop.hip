@@ -1,0 +1,521 @@
+// Cooperative exact SMO: one libsvm C-SVC problem spread over W workgroups.
+//
+// The single-workgroup solver (svm.hip smo_kernel) is VALU-bound on ONE CU: every pair (i, j)
+// costs ~50 f64/bitmask instructions per point in the two WSS passes and the gradient update,
+// so at l = 8-10k points one CU spends most of its ~10 µs per pair issuing them.  Here each
+// problem's points are cut into W contiguous slices, one per workgroup ("member"), and the two
+// block arg-reductions of every iteration become two in-launch exchanges between the members:
+// every member publishes its partial (arg-max key, index and the owner's payload: α_i; α_j,
+// G_j, K_ij) as data-tagged 8-byte granules {epoch, value} written by agent-scope relaxed
+// atomic stores (write-through: no fence, no flag), and one wave per member sweeps all W
+// partials until every tag equals the exchange's epoch.  Every member then folds the same W
+// partials in the same order and performs the same pair update, so all members agree on
+// (i, j, α_i, α_j) with no further communication; each member updates only its own slice of G
+// with its own slices of Gram rows i and j (1/W of each row read).
+//
+// Exactness: the reductions are exact max / arg-max (ties → larger index) — independent of
+// how the points are partitioned — and the per-point arithmetic is smo_kernel's (libsvm order,
+// no FMA contraction), so the pair sequence, α and ρ match smo_kernel's.
+//
+// Liveness: every spin is bounded; a member that times out sets *err and leaves, its peers
+// then time out too and the launch drains (the host raises on err).  The launcher admits at
+// most one member per CU, so every member is resident at once; the members of one problem are
+// placed on one XCD (blocks b and b+8 share an XCD under round-robin dispatch — speed only,
+// never correctness).
+#include "common.h"
+
+namespace hfens {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+struct SmoCoopProb {
+  long long koff;   // K_p offset (floats)
+  long long aoff;   // alpha offset (doubles)
+  int l;            // problem size
+  int ld;           // K_p leading dimension
+  int npos;         // indices [0, npos) have y = +1, the rest y = −1
+  int S;            // points per member (multiple of 4): member w owns [w·S, min(l, (w+1)·S))
+  double Cp, Cn;
+};
+
+struct SmoCoopOut {
+  double* rho;      // [P]
+  int* iters;       // [P]
+  double* gap;      // [P]
+  unsigned* err;    // [1] set on a spin timeout
+};
+
+constexpr int kCoopThreads = 512;
+constexpr int kCoopWaves = kCoopThreads / 64;
+constexpr int kGran = 10;             // granules per member slot
+constexpr int kMaxMembers = 16;
+constexpr double kCTau = 1e-12;
+constexpr double kCInf = 1.0e300;
+constexpr unsigned kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoch, unsigned v) {
+  __hip_atomic_store((gu64_t*)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put_u64(unsigned long long* g, unsigned epoch, unsigned long long x) {
+  put_granule(g, epoch, (unsigned)x);
+  put_granule(g + 1, epoch, (unsigned)(x >> 32));
+}
+__device__ __forceinline__ unsigned long long u64_of(const unsigned* v) {
+  return (unsigned long long)v[0] | ((unsigned long long)v[1] << 32);
+}
+__device__ __forceinline__ double f64_of(const unsigned* v) {
+  return __longlong_as_double((long long)u64_of(v));
+}
+__device__ __forceinline__ unsigned long long bits_of(double x) {
+  return (unsigned long long)__double_as_longlong(x);
+}
+
+struct CoopPart {
+  unsigned long long ka, kb;
+  int idx, pad;
+};
+
+// Member-local exact reduction (a → max; (b, idx) → arg-max, ties → larger idx): DPP/permlane
+// wave maxima, one barrier, fold of the wave partials.  Every thread receives the result.
+__device__ __forceinline__ CoopPart coop_block_red(double a, double b, int idx, CoopPart* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long ka = f64_okey(a), kb = f64_okey(b);
+  const unsigned ah = wave_max_u32((unsigned)(ka >> 32));
+  const unsigned al = wave_max_u32((unsigned)(ka >> 32) == ah ? (unsigned)ka : 0u);
+  const unsigned bh = wave_max_u32((unsigned)(kb >> 32));
+  const unsigned bl = wave_max_u32((unsigned)(kb >> 32) == bh ? (unsigned)kb : 0u);
+  const bool top = (unsigned)(kb >> 32) == bh && (unsigned)kb == bl;
+  const unsigned bi = wave_max_u32(top ? (unsigned)(idx + 1) : 0u);
+  if (lane == 0)
+    sh[wave] = CoopPart{((unsigned long long)ah << 32) | al, ((unsigned long long)bh << 32) | bl, (int)bi - 1, 0};
+  __syncthreads();
+  CoopPart r = sh[0];
+#pragma unroll
+  for (int w = 1; w < kCoopWaves; ++w) {
+    const CoopPart p = sh[w];
+    r.ka = p.ka > r.ka ? p.ka : r.ka;
+    if (p.kb > r.kb || (p.kb == r.kb && p.idx > r.idx)) { r.kb = p.kb; r.idx = p.idx; }
+  }
+  return r;
+}
+
+// Wave 0 sweeps the first `ng` granules of every member's slot until all of them carry `epoch`
+// and leaves the values in vals[member][granule] (LDS); one barrier.  false = timed out.
+__device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int ng, unsigned epoch,
+                                            unsigned (*vals)[kGran], unsigned* err, int* sh_fail) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int tot = W * ng;
+    unsigned v[3] = {0u, 0u, 0u};
+    unsigned spins = 0;
+    bool fail = false;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int gi = lane + 64 * r;
+        if (gi < tot) {
+          const int m = gi / ng, k = gi - m * ng;
+          const unsigned long long x =
+              __hip_atomic_load((gu64_t*)(slot + m * kGran + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[r] = (unsigned)x;
+          ok = ok && (unsigned)(x >> 32) == epoch;
+        }
+      }
+      if (__all(ok)) break;
+      if (++spins > kSpinLimit) {
+        fail = true;
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int gi = lane + 64 * r;
+      if (gi < tot) {
+        const int m = gi / ng, k = gi - m * ng;
+        vals[m][k] = v[r];
+      }
+    }
+    if (lane == 0) *sh_fail = fail ? 1 : 0;
+  }
+  __syncthreads();
+  return *sh_fail == 0;
+}
+
+// Point ownership inside member w: thread tid, group g < K4, lane-of-vector e < 4 owns point
+// t = w·S + 4·(tid + g·kCoopThreads) + e  (valid while t < min(l, (w+1)·S)).
+template <int K4>
+__global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopProb* __restrict__ probs, int P,
+                                                                int W, const float* __restrict__ K,
+                                                                double* __restrict__ alpha_all,
+                                                                unsigned long long* __restrict__ xchg,
+                                                                double eps, long long max_iter, SmoCoopOut out) {
+  // libsvm's arithmetic (x86-64, no FMA): a*b + c*d stays un-contracted, as in smo_kernel
+#pragma clang fp contract(off)
+  constexpr int KM = 4 * K4;
+  static_assert(KM <= 64, "per-thread point masks are 64-bit");
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int p = xcd + 8 * (q / W), w = q % W;
+  if (p >= P) return;
+  const SmoCoopProb Pr = probs[p];
+  const float* Kp = K + Pr.koff;
+  const int tid = threadIdx.x;
+  const int base = w * Pr.S;
+  const int send = min(Pr.l, base + Pr.S);   // may be ≤ base: an empty member still exchanges
+  unsigned long long* slot0 = xchg + (size_t)p * 2 * kMaxMembers * kGran;
+  __shared__ CoopPart shA[kCoopWaves], shB[kCoopWaves];
+  __shared__ unsigned vals[2][kMaxMembers][kGran];
+  __shared__ int sh_fail;
+  __shared__ double ssum[2][kCoopWaves];
+  unsigned epoch = 0;
+
+  double G[KM], A[KM];
+  float Qi[KM];
+  unsigned long long ypos = 0ull, upm = 0ull, lowm = 0ull, freem = 0ull, upperm = 0ull, validm = 0ull;
+#pragma unroll
+  for (int g = 0; g < K4; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * g + e;
+      const int t = base + 4 * (tid + g * kCoopThreads) + e;
+      G[k] = -1.0;   // p_i = −1 for C-SVC, α = 0
+      A[k] = 0.0;
+      Qi[k] = 0.f;
+      if (t < send) {
+        validm |= 1ull << k;
+        if (t < Pr.npos) { ypos |= 1ull << k; upm |= 1ull << k; }   // α = 0 is at the lower bound
+        else lowm |= 1ull << k;
+      }
+    }
+  // (thread, register slot) of point t of this member
+  auto owner_thr = [&](int t) { return ((t - base) >> 2) % kCoopThreads; };
+  auto owner_k = [&](int t) { return 4 * (((t - base) >> 2) / kCoopThreads) + ((t - base) & 3); };
+  auto pick = [&](const double* arr, int kk) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k == kk) v = arr[k];
+    return v;
+  };
+  auto pickf = [&](const float* arr, int kk) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k == kk) v = arr[k];
+    return v;
+  };
+  // exchange 1: every member's step-1 partial (kb, idx, α_idx) → (Gmax key, i, α_i)
+  auto exchange1 = [&](const CoopPart& loc, unsigned long long& kb, int& idx, double& a_i) -> bool {
+    ++epoch;
+    unsigned long long* s = slot0 + (size_t)(epoch & 1) * kMaxMembers * kGran;
+    const bool has = loc.idx >= 0;
+    if (has ? tid == owner_thr(loc.idx) : tid == 0) {
+      unsigned long long* mine = s + w * kGran;
+      const double av = has ? pick(A, owner_k(loc.idx)) : 0.0;
+      put_u64(mine, epoch, loc.kb);
+      put_granule(mine + 2, epoch, (unsigned)loc.idx);
+      put_u64(mine + 3, epoch, bits_of(av));
+    }
+    if (!coop_gather(s, W, 5, epoch, vals[epoch & 1], out.err, &sh_fail)) return false;
+    const unsigned(*v)[kGran] = vals[epoch & 1];
+    kb = u64_of(&v[0][0]);
+    idx = (int)v[0][2];
+    a_i = f64_of(&v[0][3]);
+    for (int m = 1; m < W; ++m) {
+      const unsigned long long k2 = u64_of(&v[m][0]);
+      const int i2 = (int)v[m][2];
+      if (k2 > kb || (k2 == kb && i2 > idx)) { kb = k2; idx = i2; a_i = f64_of(&v[m][3]); }
+    }
+    return true;
+  };
+
+  // ---- WSS step 1 for the first iteration
+  CoopPart loc;
+  {
+    double bb = -kCInf;
+    int bi = -1;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if ((upm >> k) & 1ull) {
+        const int t = base + 4 * (tid + (k >> 2) * kCoopThreads) + (k & 3);
+        const double v = ((ypos >> k) & 1ull) ? -G[k] : G[k];
+        if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
+      }
+    loc = coop_block_red(-kCInf, bb, bi, shA);
+  }
+  unsigned long long r1kb = 0ull;
+  int i = -1;
+  double ai_old = 0.0;
+  if (!exchange1(loc, r1kb, i, ai_old)) return;
+  long long iter = 0;
+  double last_gap = 0.0;
+  for (; iter < max_iter; ++iter) {
+    if (i < 0) break;
+    const double Gmax = f64_from_okey(r1kb);
+    const int yi = i < Pr.npos ? 1 : -1;
+    // ---- WSS step 2 over this member's slice of row i
+    const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)i * Pr.ld + base);
+    double gmax2 = -kCInf, bkey = -kCInf;
+    int bj = -1;
+    float4 qv[K4];
+#pragma unroll
+    for (int g = 0; g < K4; ++g)
+      qv[g] = base + 4 * (tid + g * kCoopThreads) < send ? Ki4[tid + g * kCoopThreads] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int g = 0; g < K4; ++g) {
+      const int t0 = base + 4 * (tid + g * kCoopThreads);
+      const float4 qq = qv[g];
+      Qi[4 * g] = qq.x; Qi[4 * g + 1] = qq.y; Qi[4 * g + 2] = qq.z; Qi[4 * g + 3] = qq.w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * g + e;
+        if ((lowm >> k) & 1ull) {
+          const double yG = ((ypos >> k) & 1ull) ? G[k] : -G[k];
+          gmax2 = fmax(gmax2, yG);
+          const double gd = Gmax + yG;
+          if (gd > 0) {
+            double quad = 2.0 - 2.0 * (double)Qi[k];
+            if (quad <= 0) quad = kCTau;
+            const double key = (gd * gd) / quad;   // smo_kernel's rank: grouping-independent
+            if (bj < 0 || key >= bkey) { bkey = key; bj = t0 + e; }
+          }
+        }
+      }
+    }
+    loc = coop_block_red(gmax2, bj >= 0 ? bkey : -kCInf, bj, shB);
+    // ---- exchange 2: (max yG over I_low, best objective key, j, α_j, G_j, K_ij)
+    ++epoch;
+    unsigned long long* s2 = slot0 + (size_t)(epoch & 1) * kMaxMembers * kGran;
+    {
+      const bool has = loc.idx >= 0;
+      if (has ? tid == owner_thr(loc.idx) : tid == 0) {
+        unsigned long long* mine = s2 + w * kGran;
+        const int kk = has ? owner_k(loc.idx) : 0;
+        const double aj = has ? pick(A, kk) : 0.0;
+        const double gj = has ? pick(G, kk) : 0.0;
+        const float kij = has ? pickf(Qi, kk) : 0.f;
+        put_u64(mine, epoch, loc.ka);
+        put_u64(mine + 2, epoch, loc.kb);
+        put_granule(mine + 4, epoch, (unsigned)loc.idx);
+        put_u64(mine + 5, epoch, bits_of(aj));
+        put_u64(mine + 7, epoch, bits_of(gj));
+        put_granule(mine + 9, epoch, __float_as_uint(kij));
+      }
+    }
+    if (!coop_gather(s2, W, 10, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    unsigned long long ka2, kb2;
+    int j;
+    double aj_old, Gj, Kij;
+    {
+      const unsigned(*v)[kGran] = vals[epoch & 1];
+      ka2 = u64_of(&v[0][0]);
+      kb2 = u64_of(&v[0][2]);
+      j = (int)v[0][4];
+      aj_old = f64_of(&v[0][5]);
+      Gj = f64_of(&v[0][7]);
+      Kij = (double)__uint_as_float(v[0][9]);
+      for (int m = 1; m < W; ++m) {
+        const unsigned long long a2 = u64_of(&v[m][0]);
+        ka2 = a2 > ka2 ? a2 : ka2;
+        const unsigned long long k2 = u64_of(&v[m][2]);
+        const int j2 = (int)v[m][4];
+        if (k2 > kb2 || (k2 == kb2 && j2 > j)) {
+          kb2 = k2;
+          j = j2;
+          aj_old = f64_of(&v[m][5]);
+          Gj = f64_of(&v[m][7]);
+          Kij = (double)__uint_as_float(v[m][9]);
+        }
+      }
+    }
+    const double gmax2_all = f64_from_okey(ka2);
+    last_gap = Gmax + gmax2_all;
+    if (Gmax + gmax2_all < eps || j < 0) break;
+    // ---- pair update (identical in every member)
+    const int yj = j < Pr.npos ? 1 : -1;
+    const double Ci = yi > 0 ? Pr.Cp : Pr.Cn, Cj = yj > 0 ? Pr.Cp : Pr.Cn;
+    const double Qij = (double)(yi * yj) * Kij;
+    const double Gi = -(double)yi * Gmax;
+    double ai = ai_old, aj = aj_old;
+    if (yi != yj) {
+      double quad = 2.0 + 2.0 * Qij;
+      if (quad <= 0) quad = kCTau;
+      const double delta = (-Gi - Gj) / quad;
+      const double diff = ai - aj;
+      ai += delta;
+      aj += delta;
+      if (diff > 0) {
+        if (aj < 0) { aj = 0; ai = diff; }
+      } else {
+        if (ai < 0) { ai = 0; aj = -diff; }
+      }
+      if (diff > Ci - Cj) {
+        if (ai > Ci) { ai = Ci; aj = Ci - diff; }
+      } else {
+        if (aj > Cj) { aj = Cj; ai = Cj + diff; }
+      }
+    } else {
+      double quad = 2.0 - 2.0 * Qij;
+      if (quad <= 0) quad = kCTau;
+      const double delta = (Gi - Gj) / quad;
+      const double sum = ai + aj;
+      ai -= delta;
+      aj += delta;
+      if (sum > Ci) {
+        if (ai > Ci) { ai = Ci; aj = sum - Ci; }
+      } else {
+        if (aj < 0) { aj = 0; ai = sum; }
+      }
+      if (sum > Cj) {
+        if (aj > Cj) { aj = Cj; ai = sum - Cj; }
+      } else {
+        if (ai < 0) { ai = 0; aj = sum; }
+      }
+    }
+    const double ci = (double)yi * (ai - ai_old), cj = (double)yj * (aj - aj_old);
+    // owners in this member: α and the bound masks of i and j
+#pragma unroll
+    for (int wv = 0; wv < 2; ++wv) {
+      const int t = wv == 0 ? i : j;
+      if (t < base || t >= send || tid != owner_thr(t)) continue;
+      const int kk = owner_k(t);
+      const double a = wv == 0 ? ai : aj;
+      const double C = wv == 0 ? Ci : Cj;
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+        if (k == kk) A[k] = a;
+      const unsigned long long bit = 1ull << kk;
+      const bool pos = (ypos & bit) != 0ull;
+      const bool atU = a >= C, atL = a <= 0;
+      freem = (!atU && !atL) ? (freem | bit) : (freem & ~bit);
+      upperm = atU ? (upperm | bit) : (upperm & ~bit);
+      const bool up = pos ? !atU : !atL;
+      const bool low = pos ? !atL : !atU;
+      upm = up ? (upm | bit) : (upm & ~bit);
+      lowm = low ? (lowm | bit) : (lowm & ~bit);
+    }
+    // ---- gradient update of this member's slice (row i in registers, row j loaded now), fused
+    // with the next step-1 candidates
+    const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)j * Pr.ld + base);
+    float4 qjv[K4];
+#pragma unroll
+    for (int g = 0; g < K4; ++g)
+      qjv[g] = base + 4 * (tid + g * kCoopThreads) < send ? Kj4[tid + g * kCoopThreads] : make_float4(0.f, 0.f, 0.f, 0.f);
+    double bb = -kCInf;
+    int bi = -1;
+#pragma unroll
+    for (int g = 0; g < K4; ++g) {
+      const int t0 = base + 4 * (tid + g * kCoopThreads);
+      const float4 qq = qjv[g];
+      const float qj[4] = {qq.x, qq.y, qq.z, qq.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * g + e;
+        const bool pos = (ypos >> k) & 1ull;
+        const double upd = (double)Qi[k] * ci + (double)qj[e] * cj;
+        G[k] += pos ? upd : -upd;
+        if ((upm >> k) & 1ull) {
+          const double v = pos ? -G[k] : G[k];
+          if (v > bb || (v == bb && t0 + e > bi)) { bb = v; bi = t0 + e; }
+        }
+      }
+    }
+    loc = coop_block_red(-kCInf, bb, bi, shA);
+    if (!exchange1(loc, r1kb, i, ai_old)) return;
+  }
+  // ---- α out (owners) and calculate_rho over all members
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+    if ((validm >> k) & 1ull) alpha_all[Pr.aoff + base + 4 * (tid + (k >> 2) * kCoopThreads) + (k & 3)] = A[k];
+  double ru = -kCInf, rl = -kCInf, sum_free = 0.0;
+  int nfree = 0;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (!((validm >> k) & 1ull)) continue;
+    const bool pos = (ypos >> k) & 1ull;
+    const double yG = pos ? G[k] : -G[k];
+    if ((upperm >> k) & 1ull) {
+      if (!pos) ru = fmax(ru, -yG); else rl = fmax(rl, yG);
+    } else if ((freem >> k) & 1ull) {
+      ++nfree;
+      sum_free += yG;
+    } else {
+      if (pos) ru = fmax(ru, -yG); else rl = fmax(rl, yG);
+    }
+  }
+  __syncthreads();   // the loop may leave right after a fold that still reads shA
+  const CoopPart rr = coop_block_red(ru, rl, -1, shA);
+  {
+    const double s = wave_sum(sum_free), c = wave_sum((double)nfree);
+    if ((tid & 63) == 0) { ssum[0][tid >> 6] = s; ssum[1][tid >> 6] = c; }
+  }
+  __syncthreads();
+  double Sm = 0.0, Cm = 0.0;
+  for (int wv = 0; wv < kCoopWaves; ++wv) { Sm += ssum[0][wv]; Cm += ssum[1][wv]; }
+  ++epoch;
+  unsigned long long* s3 = slot0 + (size_t)(epoch & 1) * kMaxMembers * kGran;
+  if (tid == 0) {
+    unsigned long long* mine = s3 + w * kGran;
+    put_u64(mine, epoch, rr.ka);       // max(−yG) over the upper-bound candidates
+    put_u64(mine + 2, epoch, rr.kb);   // max(yG) over the lower-bound candidates
+    put_u64(mine + 4, epoch, bits_of(Sm));
+    put_u64(mine + 6, epoch, bits_of(Cm));
+  }
+  if (!coop_gather(s3, W, 8, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+  if (w == 0 && tid == 0) {
+    const unsigned(*v)[kGran] = vals[epoch & 1];
+    unsigned long long kru = u64_of(&v[0][0]), krl = u64_of(&v[0][2]);
+    double St = 0.0, Ct = 0.0;
+    for (int m = 0; m < W; ++m) {
+      const unsigned long long a2 = u64_of(&v[m][0]), b2 = u64_of(&v[m][2]);
+      kru = a2 > kru ? a2 : kru;
+      krl = b2 > krl ? b2 : krl;
+      St += f64_of(&v[m][4]);
+      Ct += f64_of(&v[m][6]);
+    }
+    const double ub = -f64_from_okey(kru), lb = f64_from_okey(krl);
+    out.rho[p] = Ct > 0 ? St / Ct : (ub + lb) / 2;
+    out.iters[p] = (int)iter;
+    out.gap[p] = last_gap;
+  }
+}
+
+void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintptr_t alpha, uintptr_t xchg,
+                    double eps, long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t err,
+                    uintptr_t stream) {
+  HFENS_REQUIRE(W >= 1 && W <= kMaxMembers, "smo_coop_batch: 1 <= W <= 16 members per problem");
+  HFENS_REQUIRE(P >= 1, "smo_coop_batch: no problems");
+  HFENS_REQUIRE(max_S >= 4 && max_S % 4 == 0, "smo_coop_batch: slice must be a positive multiple of 4");
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  // members spin on each other, so all of them must be resident at once: at most one member per
+  // CU (a 512-thread block always fits beside anything else's finished work); the padding
+  // blocks of an incomplete group of 8 problems exit at once
+  HFENS_REQUIRE((long long)P * W <= ncu, "smo_coop_batch: P·W exceeds the CU count (choose a smaller W)");
+  const int groups = (P + 7) / 8;
+  const long long blocks = 8LL * groups * W;
+  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err};
+  hipStream_t st = as_stream(stream);
+  // every polled granule starts at epoch 0 (epochs count from 1 within the call)
+  HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kGran * sizeof(unsigned long long), st));
+  auto pp = (const SmoCoopProb*)probs;
+  auto kp = (const float*)K;
+  auto ap = (double*)alpha;
+  auto xp = (unsigned long long*)xchg;
+#define COOP_CASE(K4)                                                                                       \
+  if (max_S <= 4 * K4 * kCoopThreads) {                                                                     \
+    hipLaunchKernelGGL(smo_coop_kernel<K4>, dim3((unsigned)blocks), dim3(kCoopThreads), 0, st, pp, P, W, kp, \
+                       ap, xp, eps, max_iter, o);                                                           \
+    launch_check();                                                                                         \
+    return;                                                                                                 \
+  }
+  COOP_CASE(1) COOP_CASE(2) COOP_CASE(4) COOP_CASE(8)
+#undef COOP_CASE
+  throw std::invalid_argument("smo_coop_batch: slice larger than 16384 points");
+}
+
+}  // namespace hfens

@@ -105,14 +105,33 @@ def _lasso(rank, world, group):
     return s.estimator_.alpha_, s.estimator_.coef_.clone(), s.get_support().copy()
 
 
-def _develop(rank, world, group):
+def _develop(rank, world, group, policy="dp"):
+    from hfens import pipeline
     from hfens.io.synth import make_dev_select
     from hfens.parallel.dist import shard_rows
     from hfens.pipeline import develop
+    pipeline.DP_POLICY = policy
     Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
     r = develop(shard_rows(Xd, rank, world), shard_rows(yd, rank, world), shard_rows(Xs, rank, world),
                 shard_rows(ys, rank, world), names, device="cpu", group=group)
     return r.selected.copy(), r.scores
+
+
+def _develop_task(rank, world, group):
+    sel, scores = _develop(rank, world, group, policy="task")
+    return sel, scores
+
+
+def _svc_task(rank, world, group):
+    """Task-parallel SMO: problems spread over the ranks by assign_problems, solutions all-reduced."""
+    from hfens.models.smo import fit_svc_batch
+    from hfens.models.svc import SVC
+    X, y, _ = _data(300, 8, seed=9)
+    Z = (X - X.mean(0)) / X.std(0, unbiased=False)
+    Zs, ys = [Z[:240], Z], [y[:240], y]
+    svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+    fit_svc_batch(svcs, Zs, ys, group=group)
+    return [(s._dual_coef_.clone(), float(s._intercept_[0]), s._probA.item(), s._probB.item()) for s in svcs]
 
 
 def test_gbdt_dp_bit_identical():
@@ -165,6 +184,38 @@ def test_lasso_dp():
     assert abs(alpha - s.estimator_.alpha_) < 1e-15
     assert np.array_equal(sup, s.get_support())
     assert torch.allclose(coef, s.estimator_.coef_, atol=1e-10)
+
+
+def test_assign_problems_lpt():
+    from hfens.models.smo import assign_problems
+    own = assign_problems([10, 8, 8, 8, 8, 8, 6, 6], 4)
+    assert own[0] == 0 and sorted(set(own)) == [0, 1, 2, 3]
+    loads = [sum(s for s, o in zip([10, 8, 8, 8, 8, 8, 6, 6], own) if o == r) for r in range(4)]
+    assert max(loads) - min(loads) <= 4
+
+
+def test_svc_task_parallel_matches_single():
+    from hfens.models.smo import fit_svc_batch
+    from hfens.models.svc import SVC
+    got = _run("_svc_task")
+    X, y, _ = _data(300, 8, seed=9)
+    Z = (X - X.mean(0)) / X.std(0, unbiased=False)
+    svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in range(2)]
+    fit_svc_batch(svcs, [Z[:240], Z], [y[:240], y])
+    for (coef, ic, a, b), s in zip(got, svcs):
+        assert torch.equal(coef, s._dual_coef_)
+        assert ic == float(s._intercept_[0]) and a == s._probA.item() and b == s._probB.item()
+
+
+@pytest.mark.slow
+def test_develop_task_matches_single():
+    from hfens.io.synth import make_dev_select
+    from hfens.pipeline import develop
+    sel, scores = _run("_develop_task")
+    Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
+    r = develop(Xd, yd, Xs, ys, names, device="cpu")
+    assert np.array_equal(sel, r.selected)
+    assert abs(scores["auroc"] - r.scores["auroc"]) < 1e-12   # replicated fits: same model
 
 
 @pytest.mark.slow

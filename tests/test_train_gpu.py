@@ -58,8 +58,32 @@ def test_logreg_device_matches_host(dev, pen):
     md = [LogisticRegression(**kw) for _ in range(2)]
     fit_logreg_batch(mh, X, y, masks)
     fit_logreg_batch(md, X.to(dev), y.to(dev), masks.to(dev))
+    from hfens.models import logreg_solver
+    assert logreg_solver.LAST_PATH["path"] == "fused"   # the one-launch kernel ran
     for a, b in zip(mh, md):
         assert torch.allclose(a.coef_, b.coef_.cpu(), atol=1e-6)
+        assert torch.allclose(a.intercept_, b.intercept_.cpu(), atol=1e-6)
+
+
+@pytest.mark.parametrize("pen", ["l1", "l2"])
+def test_logreg_fused_matches_device_loop(dev, monkeypatch, pen):
+    """logreg_fused (one launch, per-model stopping) reaches the same optimum as the host-driven
+    device loop (the data-parallel path) on the stacking shape: 6 masks, 17 features."""
+    from hfens.models import logreg_solver
+    X, y = _data(8000, 17, 17)
+    masks = torch.ones(6, 8000, dtype=torch.bool)
+    for k in range(5):
+        masks[k, k::5] = False
+    kw = dict(penalty=pen, solver="liblinear" if pen == "l1" else "lbfgs", class_weight="balanced")
+    out = {}
+    for fused in (False, True):
+        monkeypatch.setattr(logreg_solver, "FUSED", fused)
+        ms = [LogisticRegression(**kw) for _ in range(6)]
+        fit_logreg_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        out[fused] = ms
+    for a, b in zip(out[False], out[True]):
+        assert torch.allclose(a.coef_, b.coef_, atol=1e-7)
+        assert torch.allclose(a.intercept_, b.intercept_, atol=1e-7)
 
 
 def test_svc_device_matches_libsvm(dev):
@@ -99,6 +123,29 @@ def test_gbdt_subsample_device_matches_host(dev):
         assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-9)
 
 
+@pytest.mark.parametrize("subsample", [1.0, 0.7])
+def test_gbdt_stumps_fused_matches_launch_path(dev, monkeypatch, subsample):
+    """gbdt_stumps_fused (the whole boosting run in one launch) reproduces the launch-per-step
+    device path bit for bit: features, thresholds, leaf values, impurities, train_score_."""
+    from hfens.models import hist_gbdt
+    X, y = _data(6000, 17, 51)
+    masks = torch.ones(6, 6000, dtype=torch.bool)
+    for k in range(5):
+        masks[k, k::5] = False
+    out = {}
+    for fused in (False, True):
+        monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", fused)
+        ms = [GradientBoostingClassifier(n_estimators=60, max_depth=1, subsample=subsample, random_state=s)
+              for s in range(6)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        assert hist_gbdt.LAST_PATH["path"] == ("fused" if fused else "launch")
+        out[fused] = ms
+    for a, b in zip(out[False], out[True]):
+        for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
+                     "tree_weighted_n_node_samples_", "train_score_"):
+            assert torch.equal(getattr(a, attr), getattr(b, attr)), attr
+
+
 def test_binned_stump_tables_match_tree_walk(dev):
     from hfens.models.forest_infer import ensemble_raw_binned, stump_bin_tables
     X, y = _data(5003, 24, 41)
@@ -112,3 +159,35 @@ def test_binned_stump_tables_match_tree_walk(dev):
     for b, m in enumerate(ms):
         walk = m.decision_function(X.to(dev)).cpu()
         assert torch.allclose(got[b], walk, atol=2e-5)
+
+
+@pytest.mark.parametrize("rows,slice_", [(2500, 384), (6000, 384), (6000, 2048)])
+def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_):
+    """The cooperative SMO (W workgroups per problem, in-launch exchanges) follows the same pair
+    sequence as the one-workgroup kernel: identical iteration counts and support sets, α and ρ equal
+    to accumulated rounding (the members sum ρ's free-vector average in a different order)."""
+    from hfens.models import smo
+    X, y = _data(rows, 17, 21)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    yd = y.to(dev)
+    Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
+
+    def fit(coop):
+        monkeypatch.setattr(smo, "COOP", coop)
+        monkeypatch.setattr(smo, "COOP_MIN_SLICE", slice_)
+        svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+        smo.fit_svc_batch(svcs, Zs, ys)
+        return svcs, dict(smo.LAST_SMO_INFO)
+
+    one, info1 = fit(False)
+    many, info2 = fit(True)
+    assert info1["members"] == 1 and info2["members"] > 1
+    for a, b in zip(one, many):
+        assert a.n_iter_ == b.n_iter_
+        assert torch.equal(a.support_, b.support_)
+        # same pairs in the same order; α agree to accumulated rounding (≤ 1e-13 measured)
+        assert torch.allclose(a._dual_coef_, b._dual_coef_, rtol=1e-10, atol=1e-12)
+        assert float(a._intercept_[0]) == pytest.approx(float(b._intercept_[0]), rel=1e-10, abs=1e-12)
+        # Platt's Newton fit stops at |∇| < 1e-5, so rounding-level decision values move A, B by ~1e-6
+        assert a._probA.item() == pytest.approx(b._probA.item(), rel=1e-4)
+        assert a._probB.item() == pytest.approx(b._probB.item(), rel=1e-4, abs=1e-5)
