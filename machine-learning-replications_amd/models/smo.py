@@ -357,6 +357,7 @@ def _pick_solver(max_l: int) -> str:
 # CU count allows (at most one member per CU, ≤ 16) while keeping ≥ COOP_MIN_SLICE points per member.
 COOP = os.environ.get("HFENS_SMO_COOP", "1") != "0"
 COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
+COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "80"))   # CUs left to concurrent GBC/LR
 _COOP_MAX_W = 16
 _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)
 _COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
@@ -375,7 +376,7 @@ def coop_members(P: int, max_l: int, ncu: int) -> int:
     """Workgroups per problem for the cooperative SMO (1 = the one-workgroup kernel)."""
     if not COOP or PROFILE_SMO or P <= 0:
         return 1
-    return max(1, min(_COOP_MAX_W, ncu // P, -(-max_l // COOP_MIN_SLICE)))
+    return max(1, min(_COOP_MAX_W, max(ncu - COOP_RESERVE_CUS, P) // P, -(-max_l // COOP_MIN_SLICE)))
 
 
 def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
@@ -407,9 +408,14 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
         cdev = _dev_struct(cp, device)
         xchg = torch.empty(len(live) * _COOP_GRANULES, dtype=torch.int64, device=device)
         err = torch.zeros(1, dtype=torch.int32, device=device)
+        prof = torch.zeros(len(live) * 7, dtype=torch.int64, device=device) if PROFILE_COOP else None
         E.smo_coop_batch(cdev.data_ptr(), len(live), W, int(cp["S"].max()), K.data_ptr(), alpha.data_ptr(),
                          xchg.data_ptr(), eps, max_iter, rho.data_ptr(), iters.data_ptr(), gap.data_ptr(),
-                         err.data_ptr(), s)
+                         err.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
+        if prof is not None:
+            LAST_SMO_PROF.update(phases=prof.view(-1, 7).cpu().numpy(), iters=iters.cpu().numpy(),
+                                 l=np.array([p.l for p in live]),
+                                 names=["step2", "red2", "xchg2", "pair", "update", "red1", "xchg1"])
     else:
         sdev = _dev_struct(sm, device)
         prof = torch.zeros(len(live) * 5, dtype=torch.int64, device=device) if PROFILE_SMO else None
@@ -478,6 +484,7 @@ LAST_WS_STATS: dict = {}
 LAST_SMO_PROF: dict = {}
 LAST_SMO_INFO: dict = {}
 PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
+PROFILE_COOP = os.environ.get("HFENS_PROFILE_COOP", "0") == "1"   # in-kernel phase counters of the cooperative SMO
 
 
 def assign_problems(sizes, world: int) -> List[int]:

@@ -43,6 +43,8 @@ struct SmoCoopOut {
   int* iters;       // [P]
   double* gap;      // [P]
   unsigned* err;    // [1] set on a spin timeout
+  long long* prof;  // [P][7] s_memtime phase totals of member 0 (nullptr = off): step2, red2,
+                    // xchg2, pair, update, red1, xchg1
 };
 
 constexpr int kCoopThreads = 512;
@@ -252,6 +254,16 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   if (!exchange1(loc, r1kb, i, ai_old)) return;
   long long iter = 0;
   double last_gap = 0.0;
+  long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  const bool prof = out.prof != nullptr && w == 0 && tid == 0;
+  long long tc = prof ? __builtin_amdgcn_s_memtime() : 0;
+  auto tick = [&](int k) {
+    if (prof) {
+      const long long now = __builtin_amdgcn_s_memtime();
+      ph[k] += now - tc;
+      tc = now;
+    }
+  };
   for (; iter < max_iter; ++iter) {
     if (i < 0) break;
     const double Gmax = f64_from_okey(r1kb);
@@ -285,7 +297,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
         }
       }
     }
+    tick(0);
     loc = coop_block_red(gmax2, bj >= 0 ? bkey : -kCInf, bj, shB);
+    tick(1);
     // ---- exchange 2: (max yG over I_low, best objective key, j, α_j, G_j, K_ij)
     ++epoch;
     unsigned long long* s2 = slot0 + (size_t)(epoch & 1) * kMaxMembers * kGran;
@@ -306,6 +320,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       }
     }
     if (!coop_gather(s2, W, 10, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    tick(2);
     unsigned long long ka2, kb2;
     int j;
     double aj_old, Gj, Kij;
@@ -376,6 +391,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       }
     }
     const double ci = (double)yi * (ai - ai_old), cj = (double)yj * (aj - aj_old);
+    tick(3);
     // owners in this member: α and the bound masks of i and j
 #pragma unroll
     for (int wv = 0; wv < 2; ++wv) {
@@ -423,9 +439,14 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
         }
       }
     }
+    tick(4);
     loc = coop_block_red(-kCInf, bb, bi, shA);
+    tick(5);
     if (!exchange1(loc, r1kb, i, ai_old)) return;
+    tick(6);
   }
+  if (prof)
+    for (int k = 0; k < 7; ++k) out.prof[(size_t)p * 7 + k] = ph[k];
   // ---- α out (owners) and calculate_rho over all members
 #pragma unroll
   for (int k = 0; k < KM; ++k)
@@ -485,7 +506,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
 
 void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintptr_t alpha, uintptr_t xchg,
                     double eps, long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t err,
-                    uintptr_t stream) {
+                    uintptr_t prof, uintptr_t stream) {
   HFENS_REQUIRE(W >= 1 && W <= kMaxMembers, "smo_coop_batch: 1 <= W <= 16 members per problem");
   HFENS_REQUIRE(P >= 1, "smo_coop_batch: no problems");
   HFENS_REQUIRE(max_S >= 4 && max_S % 4 == 0, "smo_coop_batch: slice must be a positive multiple of 4");
@@ -498,7 +519,7 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
   HFENS_REQUIRE((long long)P * W <= ncu, "smo_coop_batch: P·W exceeds the CU count (choose a smaller W)");
   const int groups = (P + 7) / 8;
   const long long blocks = 8LL * groups * W;
-  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err};
+  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, (long long*)prof};
   hipStream_t st = as_stream(stream);
   // every polled granule starts at epoch 0 (epochs count from 1 within the call)
   HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kGran * sizeof(unsigned long long), st));

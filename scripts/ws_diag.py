@@ -39,7 +39,7 @@ for spec in sys.argv[1:] or ["exact", "ws:0.1"]:
         pr = smo.LAST_SMO_PROF
         k = int(np.argmax(pr["iters"]))
         it = max(1, int(pr["iters"][k]))
-        names = ["step2", "r2", "pair", "update", "r1"]
+        names = pr.get("names", ["step2", "r2", "pair", "update", "r1"])
         print(f"  largest problem l={pr['l'][k]} iters={it}: cycles/iter " +
               ", ".join(f"{nm} {v / it:.0f}" for nm, v in zip(names, pr["phases"][k])))
     if solver == "ws":
