@@ -29,8 +29,12 @@ struct GbdtShape {
   int B, n, F, NN;  // models, rows, features, heap nodes per tree
 };
 
+// rint(v·scale) as int64 for |v·scale| < 2^51 (every fixed-point use here: |g|, h, w ≤ 1 at scale
+// ≤ 2^40, deviance terms at 2^26): adding 1.5·2^52 rounds to nearest-even in the FPU and leaves
+// the integer in the low mantissa bits — 2 VALU ops instead of the f64→i64 conversion sequence.
 __device__ __forceinline__ long long q_of(double v, double scale) {
-  return (long long)rint(v * scale);
+  const double t = v * scale + 6755399441055744.0;
+  return (long long)__double_as_longlong(t) - 0x4338000000000000LL;
 }
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
@@ -537,6 +541,24 @@ __device__ __forceinline__ void stump_hist_regs(const unsigned char* __restrict_
   __syncthreads();
 }
 
+// Workgroup sums of NV int64 values (exact): out[0..NV) in LDS, valid for every thread on return.
+template <int NV>
+__device__ __forceinline__ void stump_block_sum(long long (&v)[NV], long long* red, long long* out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const long long t = wave_sum_i64(v[k]);
+    if (lane == 0) red[wave * 24 + k] = t;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NV) {
+    long long s = 0;
+    for (int k = 0; k < kStWaves; ++k) s += red[k * 24 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kStThreads) void gbdt_stumps_fused_kernel(StumpJob J) {
   extern __shared__ __attribute__((aligned(16))) long long hl[];   // [hist_len][3]
   __shared__ long long red[kStWaves * 24];
@@ -545,13 +567,24 @@ __global__ __launch_bounds__(kStThreads) void gbdt_stumps_fused_kernel(StumpJob 
   __shared__ double wg[kStWaves];
   __shared__ int wf[kStWaves], wbin[kStWaves];
   __shared__ int tf0, tblo, bad;   // previous tree: root feature (−3 empty, −2 leaf) and split bin
+  __shared__ int l_bin[kStMaxF], l_one[kStMaxF], l_mid[kStMaxF], l_wide[kStMaxF];   // features by bin count
+  __shared__ int n_bin, n_one, n_mid, n_wide;
+  __shared__ long long bsum[24];
   __shared__ double tval[3];       // previous tree: node values
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = J.n, F = J.F, B = J.B;
   if (tid == 0) {
     int o = 0;
-    for (int f = 0; f < F; ++f) { s_nb[f] = J.nbins[f]; s_off[f] = o; o += s_nb[f]; }
-    bad = o != J.hist_len;   // host and device bin tables disagree: write nothing
+    n_bin = n_one = n_mid = n_wide = 0;
+    for (int f = 0; f < F; ++f) {
+      const int nb = J.nbins[f];
+      s_nb[f] = nb; s_off[f] = o; o += nb;
+      if (nb == 2) l_bin[n_bin++] = f;
+      else if (nb <= 1) l_one[n_one++] = f;
+      else if (nb <= 8) l_mid[n_mid++] = f;
+      else l_wide[n_wide++] = f;
+    }
+    bad = o != J.hist_len || s_nb[0] < 1;   // host and device bin tables disagree: write nothing
     tf0 = -3; tblo = 0; tval[0] = tval[1] = tval[2] = 0.0;
   }
   __syncthreads();
@@ -639,24 +672,67 @@ __global__ __launch_bounds__(kStThreads) void gbdt_stumps_fused_kernel(StumpJob 
     }
     __syncthreads();
     if (t == J.T) break;
-    // ---- B: root histograms of every feature (gbdt_hist_kernel, NL = 1)
+    // ---- B: root histograms (gbdt_hist_kernel, NL = 1).  Integer sums are exact, so features
+    // may be grouped freely: node totals once; binary features 8 per row pass (bin 1 summed,
+    // bin 0 = total − bin 1); 3–8-bin features one per pass in registers; every wider feature
+    // in ONE row pass with ds_add_u64.
     for (int k = tid; k < 3 * J.hist_len; k += kStThreads) hl[k] = 0;
-    __syncthreads();
-    for (int f = 0; f < F; ++f) {
-      const int nb = s_nb[f];
+    {
+      long long v[3] = {0, 0, 0};
+      for (int i = tid; i < n; i += kStThreads) {
+        const float wi = wcur[i];
+        if (!(wi > 0.f)) continue;
+        v[0] += q_of(g[i], J.qscale);
+        v[1] += q_of(h[i], J.qscale);
+        v[2] += q_of(wi, J.qscale);
+      }
+      stump_block_sum<3>(v, red, tot);
+    }
+    for (int b0 = 0; b0 < n_bin; b0 += 8) {
+      const int nf = min(8, n_bin - b0);
+      long long acc[24];
+#pragma unroll
+      for (int k = 0; k < 24; ++k) acc[k] = 0;
+      for (int i = tid; i < n; i += kStThreads) {
+        const float wi = wcur[i];
+        if (!(wi > 0.f)) continue;
+        const long long qg = q_of(g[i], J.qscale), qh = q_of(h[i], J.qscale), qw = q_of(wi, J.qscale);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (u < nf && J.bins[(size_t)l_bin[b0 + u] * n + i]) {
+            acc[3 * u] += qg;
+            acc[3 * u + 1] += qh;
+            acc[3 * u + 2] += qw;
+          }
+        }
+      }
+      stump_block_sum<24>(acc, red, bsum);
+      if (tid < 3 * nf) {
+        const int u = tid / 3, k = tid - 3 * u;
+        const int off = s_off[l_bin[b0 + u]];
+        hl[(off + 1) * 3 + k] = bsum[tid];
+        hl[off * 3 + k] = tot[k] - bsum[tid];
+      }
+    }
+    for (int u = tid; u < 3 * n_one; u += kStThreads) hl[s_off[l_one[u / 3]] * 3 + u % 3] = tot[u % 3];
+    for (int u = 0; u < n_mid; ++u) {
+      const int f = l_mid[u], nb = s_nb[f];
       const unsigned char* col = J.bins + (size_t)f * n;
       long long* out = hl + (size_t)s_off[f] * 3;
-      if (nb <= 2) stump_hist_regs<2>(col, g, h, wcur, n, nb, J.qscale, out, red);
-      else if (nb <= 4) stump_hist_regs<4>(col, g, h, wcur, n, nb, J.qscale, out, red);
-      else if (nb <= 8) stump_hist_regs<8>(col, g, h, wcur, n, nb, J.qscale, out, red);
-      else {
-        for (int i = tid; i < n; i += kStThreads) {
-          const float wi = wcur[i];
-          if (!(wi > 0.f)) continue;
-          long long* cell = out + (size_t)col[i] * 3;
-          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)q_of(g[i], J.qscale));
-          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)q_of(h[i], J.qscale));
-          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)q_of(wi, J.qscale));
+      if (nb <= 4) stump_hist_regs<4>(col, g, h, wcur, n, nb, J.qscale, out, red);
+      else stump_hist_regs<8>(col, g, h, wcur, n, nb, J.qscale, out, red);
+    }
+    if (n_wide > 0) {
+      for (int i = tid; i < n; i += kStThreads) {
+        const float wi = wcur[i];
+        if (!(wi > 0.f)) continue;
+        const long long qg = q_of(g[i], J.qscale), qh = q_of(h[i], J.qscale), qw = q_of(wi, J.qscale);
+        for (int u = 0; u < n_wide; ++u) {
+          const int f = l_wide[u];
+          long long* cell = hl + ((size_t)s_off[f] + J.bins[(size_t)f * n + i]) * 3;
+          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)qg);
+          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)qh);
+          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)qw);
         }
       }
     }
