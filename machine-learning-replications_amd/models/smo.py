@@ -360,6 +360,15 @@ COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
 COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "80"))   # CUs left to concurrent GBC/LR
 _COOP_MAX_W = 16
 _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)
+# "otf" (default while a member's rows fit its registers: ≤ 2048 points per member, ≤ 20 features):
+# the cooperative kernel recomputes its Gram-row entries per pair with the Gram kernel's exact
+# expression instead of reading a stored Gram — no O(l²) matrix, no Gram launch, no HBM reads per
+# pair, and the same pair sequence.
+COOP_OTF = os.environ.get("HFENS_SMO_OTF", "1") != "0"
+_OTF_MAX_S, _OTF_MAX_F = 2048, 20
+_OTF_GRANULES = 2 * 16 * 32          # exchange slots per problem: 2 × kMaxMembers × kOtfGran (u64)
+_OTF_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("S", "<i4"),
+                    ("ngl2e", "<f4"), ("Cp", "<f8"), ("Cn", "<f8")])
 _COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
                      ("S", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
 _NCU: dict = {}
@@ -380,6 +389,25 @@ def coop_members(P: int, max_l: int, ncu: int) -> int:
 
 
 def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
+    max_l = max(p.l for p in live)
+    max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
+    W = coop_members(len(live), max_l, _num_cus(device))
+    if W > 1 and COOP_OTF and not PROFILE_COOP and F <= _OTF_MAX_F and -(-max_l // W) <= _OTF_MAX_S:
+        op = np.zeros(len(live), _OTF_DT)
+        for k, p in enumerate(live):
+            op[k] = (zoffs[k], aoffs[k], p.l, p.npos, -(-p.l // W), -p.gamma * 1.4426950408889634, p.Cp, p.Cn)
+        odev = _dev_struct(op, device)
+        alpha = torch.empty(aoffs[-1], dtype=torch.float64, device=device)
+        rho = torch.empty(len(live), dtype=torch.float64, device=device)
+        iters = torch.empty(len(live), dtype=torch.int32, device=device)
+        gap = torch.empty(len(live), dtype=torch.float64, device=device)
+        xchg = torch.empty(len(live) * _OTF_GRANULES, dtype=torch.int64, device=device)
+        err = torch.zeros(1, dtype=torch.int32, device=device)
+        E.smo_coop_otf_batch(odev.data_ptr(), len(live), W, F, int(op["S"].max()), zcat.data_ptr(),
+                             alpha.data_ptr(), xchg.data_ptr(), eps, max_iter, rho.data_ptr(), iters.data_ptr(),
+                             gap.data_ptr(), err.data_ptr(), s)
+        LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop-otf")
+        return alpha, rho, iters, err
     g = np.zeros(len(live), _GRAM_DT)
     sm = np.zeros(len(live), _SMO_DT)
     koff = 0
@@ -424,7 +452,7 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
         if prof is not None:
             LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
                                  l=np.array([p.l for p in live]))
-    LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l)
+    LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop" if W > 1 else "single")
     del K
     return alpha, rho, iters, err
 

@@ -102,25 +102,30 @@ __device__ __forceinline__ CoopPart coop_block_red(double a, double b, int idx, 
   return r;
 }
 
-// Wave 0 sweeps the first `ng` granules of every member's slot until all of them carry `epoch`
-// and leaves the values in vals[member][granule] (LDS); one barrier.  false = timed out.
-__device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int ng, unsigned epoch,
-                                            unsigned (*vals)[kGran], unsigned* err, int* sh_fail) {
+// Wave 0 sweeps the first `ng` granules of every member's slot (GS granules per slot) until all
+// of them carry `epoch` and leaves the values in vals[member][granule] (LDS); one barrier.
+// false = timed out.
+template <int GS>
+__device__ __forceinline__ bool coop_gather_t(unsigned long long* slot, int W, int ng, unsigned epoch,
+                                              unsigned (*vals)[GS], unsigned* err, int* sh_fail) {
+  constexpr int R = (kMaxMembers * GS + 63) / 64;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int tot = W * ng;
-    unsigned v[3] = {0u, 0u, 0u};
+    unsigned v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = 0u;
     unsigned spins = 0;
     bool fail = false;
     for (;;) {
       bool ok = true;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
+      for (int r = 0; r < R; ++r) {
         const int gi = lane + 64 * r;
         if (gi < tot) {
           const int m = gi / ng, k = gi - m * ng;
           const unsigned long long x =
-              __hip_atomic_load((gu64_t*)(slot + m * kGran + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_load((gu64_t*)(slot + m * GS + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           v[r] = (unsigned)x;
           ok = ok && (unsigned)(x >> 32) == epoch;
         }
@@ -134,7 +139,7 @@ __device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int
       __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < R; ++r) {
       const int gi = lane + 64 * r;
       if (gi < tot) {
         const int m = gi / ng, k = gi - m * ng;
@@ -145,6 +150,11 @@ __device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int
   }
   __syncthreads();
   return *sh_fail == 0;
+}
+
+__device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int ng, unsigned epoch,
+                                            unsigned (*vals)[kGran], unsigned* err, int* sh_fail) {
+  return coop_gather_t<kGran>(slot, W, ng, epoch, vals, err, sh_fail);
 }
 
 // Point ownership inside member w: thread tid, group g < K4, lane-of-vector e < 4 owns point
@@ -537,6 +547,426 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
   COOP_CASE(1) COOP_CASE(2) COOP_CASE(4) COOP_CASE(8)
 #undef COOP_CASE
   throw std::invalid_argument("smo_coop_batch: slice larger than 16384 points");
+}
+
+// ------------------------------------------------------------------------------------------
+// smo_coop_otf: the same cooperative solver with NO stored Gram.  Each thread keeps its points'
+// rows z_t and norms ‖z_t‖² in registers and re-evaluates its entries of Gram rows i and j per
+// pair with gram_rbf_kernel's exact expression — its f32-input MFMA dot product is bit-for-bit a
+// k-ordered fmaf chain, then the same norm sum, clamp and exp2 — so the values, and hence the
+// pair sequence, equal the stored-Gram solvers'.  z_i and z_j travel inside the two exchanges
+// (the candidate's owner publishes its row as F + 1 more granules), so a pair reads nothing from
+// HBM: two in-launch exchanges plus register arithmetic.  Memory is O(l·F) instead of O(l²) (the
+// bench's 36 problems: 7 GB of Gram neither written nor re-read) and the Gram launch goes away.
+// Points are strided over threads (t = base + tid + 512·m): no vector-load layout to keep.
+struct SmoOtfProb {
+  long long zoff;   // first row of this problem in zcat ([rows][F] f32, problem order)
+  long long aoff;   // alpha offset (doubles)
+  int l;            // problem size
+  int npos;         // indices [0, npos) have y = +1, the rest y = −1
+  int S;            // points per member: member w owns [w·S, min(l, (w+1)·S))
+  float ngl2e;      // −γ·log2(e)
+  double Cp, Cn;
+};
+
+constexpr int kOtfGran = 32;   // granules per member slot: exchange 2 carries 11 + F
+constexpr int kOtfMaxF = 20;
+
+__device__ __forceinline__ float rbf_entry(float dot, float nr, float nc, float ngl2e) {
+  float d2 = fmaf(-2.f, dot, nr + nc);   // gram_rbf_kernel's epilogue, operand for operand
+  d2 = fmaxf(d2, 0.f);
+  return __builtin_amdgcn_exp2f(ngl2e * d2);
+}
+
+template <int KM, int FP>
+__global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtfProb* __restrict__ probs, int P,
+                                                                    int W, int F, const float* __restrict__ zcat,
+                                                                    double* __restrict__ alpha_all,
+                                                                    unsigned long long* __restrict__ xchg,
+                                                                    double eps, long long max_iter, SmoCoopOut out) {
+#pragma clang fp contract(off)
+  static_assert(KM <= 64 && FP <= kOtfMaxF, "register tile");
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int p = xcd + 8 * (q / W), w = q % W;
+  if (p >= P) return;
+  const SmoOtfProb Pr = probs[p];
+  const int tid = threadIdx.x;
+  const int base = w * Pr.S;
+  const int send = min(Pr.l, base + Pr.S);   // may be ≤ base: an empty member still exchanges
+  unsigned long long* slot0 = xchg + (size_t)p * 2 * kMaxMembers * kOtfGran;
+  __shared__ CoopPart shA[kCoopWaves], shB[kCoopWaves];
+  __shared__ unsigned vals[2][kMaxMembers][kOtfGran];
+  __shared__ int sh_fail;
+  __shared__ double ssum[2][kCoopWaves];
+  unsigned epoch = 0;
+
+  float zr[KM][FP], nz[KM];   // this thread's points: rows and squared norms
+  double G[KM], A[KM];
+  float Qi[KM], Qj[KM];
+  unsigned long long ypos = 0ull, upm = 0ull, lowm = 0ull, freem = 0ull, upperm = 0ull, validm = 0ull;
+#pragma unroll
+  for (int m = 0; m < KM; ++m) {
+    const int t = base + tid + kCoopThreads * m;
+    const bool ok = t < send;
+    const float* zt = zcat + (size_t)(Pr.zoff + (ok ? t : 0)) * F;
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < FP; ++k) {
+      zr[m][k] = (ok && k < F) ? zt[k] : 0.f;
+      if (k < F) sq = fmaf(zr[m][k], zr[m][k], sq);
+    }
+    nz[m] = sq;
+    G[m] = -1.0;   // p_i = −1 for C-SVC, α = 0
+    A[m] = 0.0;
+    Qi[m] = 0.f;
+    Qj[m] = 0.f;
+    if (ok) {
+      validm |= 1ull << m;
+      if (t < Pr.npos) { ypos |= 1ull << m; upm |= 1ull << m; }   // α = 0 is at the lower bound
+      else lowm |= 1ull << m;
+    }
+  }
+  auto owner_thr = [&](int t) { return (t - base) % kCoopThreads; };
+  auto owner_m = [&](int t) { return (t - base) / kCoopThreads; };
+  auto pick = [&](const double* arr, int mm) {
+    double v = 0.0;
+#pragma unroll
+    for (int m = 0; m < KM; ++m)
+      if (m == mm) v = arr[m];
+    return v;
+  };
+  auto pickf = [&](const float* arr, int mm) {
+    float v = 0.f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m)
+      if (m == mm) v = arr[m];
+    return v;
+  };
+  // this thread's entries of Gram row r; the row's features and norm come from an exchange (LDS)
+  auto gram_row = [&](int r, const unsigned* zb, float nzr, float* Qo) {
+    float zrow[FP];
+#pragma unroll
+    for (int k = 0; k < FP; ++k) zrow[k] = k < F ? __uint_as_float(zb[k]) : 0.f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < FP; ++k)
+        if (k < F) dot = fmaf(zrow[k], zr[m][k], dot);
+      Qo[m] = base + tid + kCoopThreads * m == r ? 1.f : rbf_entry(dot, nzr, nz[m], Pr.ngl2e);
+    }
+  };
+  // owner of point t: granule 0 = ‖z_t‖², granules 1..F = z_t
+  auto publish_row = [&](unsigned long long* dst, int t) {
+    const int mm = owner_m(t);
+    float nn = 0.f, zz[FP];
+#pragma unroll
+    for (int k = 0; k < FP; ++k) zz[k] = 0.f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m)
+      if (m == mm) {
+        nn = nz[m];
+#pragma unroll
+        for (int k = 0; k < FP; ++k) zz[k] = zr[m][k];
+      }
+    put_granule(dst, epoch, __float_as_uint(nn));
+#pragma unroll
+    for (int k = 0; k < FP; ++k)
+      if (k < F) put_granule(dst + 1 + k, epoch, __float_as_uint(zz[k]));
+  };
+  auto publish_zero_row = [&](unsigned long long* dst) {
+    for (int k = 0; k <= F; ++k) put_granule(dst + k, epoch, 0u);
+  };
+  // exchange 1: (kb, idx, α_idx, ‖z_idx‖², z_idx) → (Gmax key, i, α_i, member holding z_i)
+  auto exchange1 = [&](const CoopPart& loc, unsigned long long& kb, int& idx, double& a_i, int& ms) -> bool {
+    ++epoch;
+    unsigned long long* s = slot0 + (size_t)(epoch & 1) * kMaxMembers * kOtfGran;
+    const bool has = loc.idx >= 0;
+    if (has ? tid == owner_thr(loc.idx) : tid == 0) {
+      unsigned long long* mine = s + w * kOtfGran;
+      put_u64(mine, epoch, loc.kb);
+      put_granule(mine + 2, epoch, (unsigned)loc.idx);
+      put_u64(mine + 3, epoch, bits_of(has ? pick(A, owner_m(loc.idx)) : 0.0));
+      if (has) publish_row(mine + 5, loc.idx);
+      else publish_zero_row(mine + 5);
+    }
+    if (!coop_gather_t<kOtfGran>(s, W, 6 + F, epoch, vals[epoch & 1], out.err, &sh_fail)) return false;
+    const unsigned(*v)[kOtfGran] = vals[epoch & 1];
+    kb = u64_of(&v[0][0]);
+    idx = (int)v[0][2];
+    a_i = f64_of(&v[0][3]);
+    ms = 0;
+    for (int m = 1; m < W; ++m) {
+      const unsigned long long k2 = u64_of(&v[m][0]);
+      const int i2 = (int)v[m][2];
+      if (k2 > kb || (k2 == kb && i2 > idx)) { kb = k2; idx = i2; a_i = f64_of(&v[m][3]); ms = m; }
+    }
+    return true;
+  };
+
+  // ---- WSS step 1 for the first iteration
+  CoopPart loc;
+  {
+    double bb = -kCInf;
+    int bi = -1;
+#pragma unroll
+    for (int m = 0; m < KM; ++m)
+      if ((upm >> m) & 1ull) {
+        const int t = base + tid + kCoopThreads * m;
+        const double v = ((ypos >> m) & 1ull) ? -G[m] : G[m];
+        if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
+      }
+    loc = coop_block_red(-kCInf, bb, bi, shA);
+  }
+  unsigned long long r1kb = 0ull;
+  int i = -1, mi = 0;
+  double ai_old = 0.0;
+  if (!exchange1(loc, r1kb, i, ai_old, mi)) return;
+  long long iter = 0;
+  double last_gap = 0.0;
+  for (; iter < max_iter; ++iter) {
+    if (i < 0) break;
+    const double Gmax = f64_from_okey(r1kb);
+    const int yi = i < Pr.npos ? 1 : -1;
+    {
+      const unsigned* zb = &vals[epoch & 1][mi][6];
+      gram_row(i, zb, __uint_as_float(vals[epoch & 1][mi][5]), Qi);
+    }
+    // ---- WSS step 2 over this member's entries of row i
+    double gmax2 = -kCInf, bkey = -kCInf;
+    int bj = -1;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+      if ((lowm >> m) & 1ull) {
+        const double yG = ((ypos >> m) & 1ull) ? G[m] : -G[m];
+        gmax2 = fmax(gmax2, yG);
+        const double gd = Gmax + yG;
+        if (gd > 0) {
+          double quad = 2.0 - 2.0 * (double)Qi[m];
+          if (quad <= 0) quad = kCTau;
+          const double key = (gd * gd) / quad;   // smo_kernel's rank: grouping-independent
+          if (bj < 0 || key >= bkey) { bkey = key; bj = base + tid + kCoopThreads * m; }
+        }
+      }
+    }
+    loc = coop_block_red(gmax2, bj >= 0 ? bkey : -kCInf, bj, shB);
+    // ---- exchange 2: (max yG over I_low, best key, j, α_j, G_j, K_ij, ‖z_j‖², z_j)
+    ++epoch;
+    unsigned long long* s2 = slot0 + (size_t)(epoch & 1) * kMaxMembers * kOtfGran;
+    {
+      const bool has = loc.idx >= 0;
+      if (has ? tid == owner_thr(loc.idx) : tid == 0) {
+        unsigned long long* mine = s2 + w * kOtfGran;
+        const int mm = has ? owner_m(loc.idx) : 0;
+        put_u64(mine, epoch, loc.ka);
+        put_u64(mine + 2, epoch, loc.kb);
+        put_granule(mine + 4, epoch, (unsigned)loc.idx);
+        put_u64(mine + 5, epoch, bits_of(has ? pick(A, mm) : 0.0));
+        put_u64(mine + 7, epoch, bits_of(has ? pick(G, mm) : 0.0));
+        put_granule(mine + 9, epoch, __float_as_uint(has ? pickf(Qi, mm) : 0.f));
+        if (has) publish_row(mine + 10, loc.idx);
+        else publish_zero_row(mine + 10);
+      }
+    }
+    if (!coop_gather_t<kOtfGran>(s2, W, 11 + F, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    unsigned long long ka2, kb2;
+    int j, mj;
+    double aj_old, Gj, Kij;
+    {
+      const unsigned(*v)[kOtfGran] = vals[epoch & 1];
+      ka2 = u64_of(&v[0][0]);
+      kb2 = u64_of(&v[0][2]);
+      j = (int)v[0][4];
+      aj_old = f64_of(&v[0][5]);
+      Gj = f64_of(&v[0][7]);
+      Kij = (double)__uint_as_float(v[0][9]);
+      mj = 0;
+      for (int m = 1; m < W; ++m) {
+        const unsigned long long a2 = u64_of(&v[m][0]);
+        ka2 = a2 > ka2 ? a2 : ka2;
+        const unsigned long long k2 = u64_of(&v[m][2]);
+        const int j2 = (int)v[m][4];
+        if (k2 > kb2 || (k2 == kb2 && j2 > j)) {
+          kb2 = k2;
+          j = j2;
+          aj_old = f64_of(&v[m][5]);
+          Gj = f64_of(&v[m][7]);
+          Kij = (double)__uint_as_float(v[m][9]);
+          mj = m;
+        }
+      }
+    }
+    const double gmax2_all = f64_from_okey(ka2);
+    last_gap = Gmax + gmax2_all;
+    if (Gmax + gmax2_all < eps || j < 0) break;
+    // ---- pair update (identical in every member; libsvm's clipping)
+    const int yj = j < Pr.npos ? 1 : -1;
+    const double Ci = yi > 0 ? Pr.Cp : Pr.Cn, Cj = yj > 0 ? Pr.Cp : Pr.Cn;
+    const double Qij = (double)(yi * yj) * Kij;
+    const double Gi = -(double)yi * Gmax;
+    double ai = ai_old, aj = aj_old;
+    if (yi != yj) {
+      double quad = 2.0 + 2.0 * Qij;
+      if (quad <= 0) quad = kCTau;
+      const double delta = (-Gi - Gj) / quad;
+      const double diff = ai - aj;
+      ai += delta;
+      aj += delta;
+      if (diff > 0) {
+        if (aj < 0) { aj = 0; ai = diff; }
+      } else {
+        if (ai < 0) { ai = 0; aj = -diff; }
+      }
+      if (diff > Ci - Cj) {
+        if (ai > Ci) { ai = Ci; aj = Ci - diff; }
+      } else {
+        if (aj > Cj) { aj = Cj; ai = Cj + diff; }
+      }
+    } else {
+      double quad = 2.0 - 2.0 * Qij;
+      if (quad <= 0) quad = kCTau;
+      const double delta = (Gi - Gj) / quad;
+      const double sum = ai + aj;
+      ai -= delta;
+      aj += delta;
+      if (sum > Ci) {
+        if (ai > Ci) { ai = Ci; aj = sum - Ci; }
+      } else {
+        if (aj < 0) { aj = 0; ai = sum; }
+      }
+      if (sum > Cj) {
+        if (aj > Cj) { aj = Cj; ai = sum - Cj; }
+      } else {
+        if (ai < 0) { ai = 0; aj = sum; }
+      }
+    }
+    const double ci = (double)yi * (ai - ai_old), cj = (double)yj * (aj - aj_old);
+#pragma unroll
+    for (int wv = 0; wv < 2; ++wv) {
+      const int t = wv == 0 ? i : j;
+      if (t < base || t >= send || tid != owner_thr(t)) continue;
+      const int mm = owner_m(t);
+      const double a = wv == 0 ? ai : aj;
+      const double C = wv == 0 ? Ci : Cj;
+#pragma unroll
+      for (int m = 0; m < KM; ++m)
+        if (m == mm) A[m] = a;
+      const unsigned long long bit = 1ull << mm;
+      const bool pos = (ypos & bit) != 0ull;
+      const bool atU = a >= C, atL = a <= 0;
+      freem = (!atU && !atL) ? (freem | bit) : (freem & ~bit);
+      upperm = atU ? (upperm | bit) : (upperm & ~bit);
+      const bool up = pos ? !atU : !atL;
+      const bool low = pos ? !atL : !atU;
+      upm = up ? (upm | bit) : (upm & ~bit);
+      lowm = low ? (lowm | bit) : (lowm & ~bit);
+    }
+    // ---- gradient update with rows i (registers) and j (recomputed now), fused with the next
+    // step-1 candidates
+    gram_row(j, &vals[epoch & 1][mj][11], __uint_as_float(vals[epoch & 1][mj][10]), Qj);
+    double bb = -kCInf;
+    int bi = -1;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+      const bool pos = (ypos >> m) & 1ull;
+      const double upd = (double)Qi[m] * ci + (double)Qj[m] * cj;
+      G[m] += pos ? upd : -upd;
+      if ((upm >> m) & 1ull) {
+        const int t = base + tid + kCoopThreads * m;
+        const double v = pos ? -G[m] : G[m];
+        if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
+      }
+    }
+    loc = coop_block_red(-kCInf, bb, bi, shA);
+    if (!exchange1(loc, r1kb, i, ai_old, mi)) return;
+  }
+  // ---- α out (owners) and calculate_rho over all members
+#pragma unroll
+  for (int m = 0; m < KM; ++m)
+    if ((validm >> m) & 1ull) alpha_all[Pr.aoff + base + tid + kCoopThreads * m] = A[m];
+  double ru = -kCInf, rl = -kCInf, sum_free = 0.0;
+  int nfree = 0;
+#pragma unroll
+  for (int m = 0; m < KM; ++m) {
+    if (!((validm >> m) & 1ull)) continue;
+    const bool pos = (ypos >> m) & 1ull;
+    const double yG = pos ? G[m] : -G[m];
+    if ((upperm >> m) & 1ull) {
+      if (!pos) ru = fmax(ru, -yG); else rl = fmax(rl, yG);
+    } else if ((freem >> m) & 1ull) {
+      ++nfree;
+      sum_free += yG;
+    } else {
+      if (pos) ru = fmax(ru, -yG); else rl = fmax(rl, yG);
+    }
+  }
+  __syncthreads();   // the loop may leave right after a fold that still reads shA
+  const CoopPart rr = coop_block_red(ru, rl, -1, shA);
+  {
+    const double sm = wave_sum(sum_free), c = wave_sum((double)nfree);
+    if ((tid & 63) == 0) { ssum[0][tid >> 6] = sm; ssum[1][tid >> 6] = c; }
+  }
+  __syncthreads();
+  double Sm = 0.0, Cm = 0.0;
+  for (int wv = 0; wv < kCoopWaves; ++wv) { Sm += ssum[0][wv]; Cm += ssum[1][wv]; }
+  ++epoch;
+  unsigned long long* s3 = slot0 + (size_t)(epoch & 1) * kMaxMembers * kOtfGran;
+  if (tid == 0) {
+    unsigned long long* mine = s3 + w * kOtfGran;
+    put_u64(mine, epoch, rr.ka);
+    put_u64(mine + 2, epoch, rr.kb);
+    put_u64(mine + 4, epoch, bits_of(Sm));
+    put_u64(mine + 6, epoch, bits_of(Cm));
+  }
+  if (!coop_gather_t<kOtfGran>(s3, W, 8, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+  if (w == 0 && tid == 0) {
+    const unsigned(*v)[kOtfGran] = vals[epoch & 1];
+    unsigned long long kru = u64_of(&v[0][0]), krl = u64_of(&v[0][2]);
+    double St = 0.0, Ct = 0.0;
+    for (int m = 0; m < W; ++m) {
+      const unsigned long long a2 = u64_of(&v[m][0]), b2 = u64_of(&v[m][2]);
+      kru = a2 > kru ? a2 : kru;
+      krl = b2 > krl ? b2 : krl;
+      St += f64_of(&v[m][4]);
+      Ct += f64_of(&v[m][6]);
+    }
+    const double ub = -f64_from_okey(kru), lb = f64_from_okey(krl);
+    out.rho[p] = Ct > 0 ? St / Ct : (ub + lb) / 2;
+    out.iters[p] = (int)iter;
+    out.gap[p] = last_gap;
+  }
+}
+
+void smo_coop_otf_batch(uintptr_t probs, int P, int W, int F, int max_S, uintptr_t zcat, uintptr_t alpha,
+                        uintptr_t xchg, double eps, long long max_iter, uintptr_t rho, uintptr_t iters,
+                        uintptr_t gap, uintptr_t err, uintptr_t stream) {
+  HFENS_REQUIRE(W >= 1 && W <= kMaxMembers, "smo_coop_otf_batch: 1 <= W <= 16 members per problem");
+  HFENS_REQUIRE(P >= 1, "smo_coop_otf_batch: no problems");
+  HFENS_REQUIRE(F >= 1 && F <= kOtfMaxF, "smo_coop_otf_batch: 1 <= F <= 20 (rows held in registers)");
+  HFENS_REQUIRE(max_S >= 1 && max_S <= 4 * kCoopThreads, "smo_coop_otf_batch: at most 2048 points per member");
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  HFENS_REQUIRE((long long)P * W <= ncu, "smo_coop_otf_batch: P·W exceeds the CU count (choose a smaller W)");
+  const long long blocks = 8LL * ((P + 7) / 8) * W;
+  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, nullptr};
+  hipStream_t st = as_stream(stream);
+  HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kOtfGran * sizeof(unsigned long long), st));
+  auto pp = (const SmoOtfProb*)probs;
+  auto zp = (const float*)zcat;
+  auto ap = (double*)alpha;
+  auto xp = (unsigned long long*)xchg;
+  const int KM = (max_S + kCoopThreads - 1) / kCoopThreads;
+#define OTF_CASE(KM_, FP_)                                                                                   \
+  if (KM <= KM_ && F <= FP_) {                                                                               \
+    hipLaunchKernelGGL((smo_coop_otf_kernel<KM_, FP_>), dim3((unsigned)blocks), dim3(kCoopThreads), 0, st, pp, \
+                       P, W, F, zp, ap, xp, eps, max_iter, o);                                              \
+    launch_check();                                                                                          \
+    return;                                                                                                  \
+  }
+  OTF_CASE(1, 8) OTF_CASE(1, 20) OTF_CASE(2, 8) OTF_CASE(2, 20) OTF_CASE(4, 8) OTF_CASE(4, 20)
+#undef OTF_CASE
+  throw std::invalid_argument("smo_coop_otf_batch: unsupported tile");
 }
 
 }  // namespace hfens

@@ -161,8 +161,9 @@ def test_binned_stump_tables_match_tree_walk(dev):
         assert torch.allclose(got[b], walk, atol=2e-5)
 
 
+@pytest.mark.parametrize("otf", [True, False])
 @pytest.mark.parametrize("rows,slice_", [(2500, 384), (6000, 384), (6000, 2048)])
-def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_):
+def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_, otf):
     """The cooperative SMO (W workgroups per problem, in-launch exchanges) follows the same pair
     sequence as the one-workgroup kernel: identical iteration counts and support sets, α and ρ equal
     to accumulated rounding (the members sum ρ's free-vector average in a different order)."""
@@ -171,6 +172,8 @@ def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_):
     Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
     yd = y.to(dev)
     Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
+
+    monkeypatch.setattr(smo, "COOP_OTF", otf)   # Gram rows recomputed per pair vs read from the stored Gram
 
     def fit(coop):
         monkeypatch.setattr(smo, "COOP", coop)
@@ -182,6 +185,7 @@ def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_):
     one, info1 = fit(False)
     many, info2 = fit(True)
     assert info1["members"] == 1 and info2["members"] > 1
+    assert info2["solver"] == ("coop-otf" if otf else "coop")
     for a, b in zip(one, many):
         assert a.n_iter_ == b.n_iter_
         assert torch.equal(a.support_, b.support_)
