@@ -365,7 +365,7 @@ _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMem
 # expression instead of reading a stored Gram — no O(l²) matrix, no Gram launch, no HBM reads per
 # pair, and the same pair sequence.
 COOP_OTF = os.environ.get("HFENS_SMO_OTF", "1") != "0"
-_OTF_MAX_S, _OTF_MAX_F = 2048, 20
+_OTF_MAX_S, _OTF_MAX_F = 1024, 20   # ≤ 2 points per thread: no register spill (measured)
 _OTF_GRANULES = 2 * 16 * 32          # exchange slots per problem: 2 × kMaxMembers × kOtfGran (u64)
 _OTF_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("S", "<i4"),
                     ("ngl2e", "<f4"), ("Cp", "<f8"), ("Cn", "<f8")])

@@ -559,6 +559,8 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
 // HBM: two in-launch exchanges plus register arithmetic.  Memory is O(l·F) instead of O(l²) (the
 // bench's 36 problems: 7 GB of Gram neither written nor re-read) and the Gram launch goes away.
 // Points are strided over threads (t = base + tid + 512·m): no vector-load layout to keep.
+// Measured: at ≤ 2 points per thread it runs with the stored-Gram kernel; at 4 points per thread
+// (256 VGPRs + spills) it is slower, so the host picks it only for slices of ≤ 1024 points.
 struct SmoOtfProb {
   long long zoff;   // first row of this problem in zcat ([rows][F] f32, problem order)
   long long aoff;   // alpha offset (doubles)
