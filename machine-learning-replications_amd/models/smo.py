@@ -353,18 +353,23 @@ def _pick_solver(max_l: int) -> str:
 
 # Cooperative exact SMO (ops/csrc/svm_coop.hip): every problem's points are split over W
 # workgroups that exchange their WSS partials inside the launch — the same pair sequence as the
-# one-workgroup smo_kernel, with 1/W of the per-pair VALU work on each CU.  W is as large as the
-# CU count allows (at most one member per CU, ≤ 16) while keeping ≥ COOP_MIN_SLICE points per member.
+# one-workgroup smo_kernel, with 1/W of each Gram row read per CU.  A pair is latency-bound either
+# way (profiles/r1_smo_latency.md): the one-workgroup kernel waits on two 40 KB row reads through
+# one CU, the members on two in-launch exchanges (≈2 µs each); W = 4 measured best on the bench
+# (87 vs 95 ms/step with one workgroup), more members add exchange skew.  W ≤ COOP_MAX_W, one
+# member per CU, COOP_RESERVE_CUS CUs left to the GBC/LR kernels of the concurrent stream, and
+# ≥ COOP_MIN_SLICE points per member.
 COOP = os.environ.get("HFENS_SMO_COOP", "1") != "0"
 COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
 COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "80"))   # CUs left to concurrent GBC/LR
-_COOP_MAX_W = 16
+_COOP_MAX_W = int(os.environ.get("HFENS_SMO_COOP_MAXW", "4"))   # more members: exchange skew outweighs the split (measured)
 _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)
-# "otf" (default while a member's rows fit its registers: ≤ 2048 points per member, ≤ 20 features):
-# the cooperative kernel recomputes its Gram-row entries per pair with the Gram kernel's exact
-# expression instead of reading a stored Gram — no O(l²) matrix, no Gram launch, no HBM reads per
-# pair, and the same pair sequence.
-COOP_OTF = os.environ.get("HFENS_SMO_OTF", "1") != "0"
+# "otf" (HFENS_SMO_OTF=1, while a member's rows fit its registers: ≤ 1024 points per member, ≤ 20
+# features): the cooperative kernel recomputes its Gram-row entries per pair with the Gram kernel's
+# exact expression instead of reading a stored Gram — no O(l²) matrix, no Gram launch, no HBM reads
+# per pair, the same pair sequence (tested).  Its exchanges carry the rows (28 granules per member
+# instead of 10), which cost more than the row reads they replace at the member counts that fit.
+COOP_OTF = os.environ.get("HFENS_SMO_OTF", "0") == "1"   # measured slower than the stored Gram at 4-16 members
 _OTF_MAX_S, _OTF_MAX_F = 1024, 20   # ≤ 2 points per thread: no register spill (measured)
 _OTF_GRANULES = 2 * 16 * 32          # exchange slots per problem: 2 × kMaxMembers × kOtfGran (u64)
 _OTF_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("S", "<i4"),

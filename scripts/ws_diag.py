@@ -22,6 +22,8 @@ Z = (X - X.mean(0)) / X.std(0, unbiased=False)
 folds = torch.arange(N, device=dev) % 5
 Zs = [Z[folds != k] for k in range(5)] + [Z]
 ys = [y[folds != k] for k in range(5)] + [y]
+nf = int(os.environ.get("WS_DIAG_FITS", "6"))   # the last nf fits (1 = the full-data fit: 6 problems)
+Zs, ys = Zs[-nf:], ys[-nf:]
 for spec in sys.argv[1:] or ["exact", "ws:0.1"]:
     solver, _, frac = spec.partition(":")
     smo.SOLVER = solver
@@ -34,7 +36,7 @@ for spec in sys.argv[1:] or ["exact", "ws:0.1"]:
         smo.fit_svc_batch(svcs, Zs, ys)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-    print(f"{spec}: {1000 * dt:.1f} ms  n_iter={[s.n_iter_ for s in svcs]}", flush=True)
+    print(f"{spec}: {1000 * dt:.1f} ms  n_iter={[s.n_iter_ for s in svcs]}  {smo.LAST_SMO_INFO}", flush=True)
     if solver == "exact" and smo.LAST_SMO_PROF:
         pr = smo.LAST_SMO_PROF
         k = int(np.argmax(pr["iters"]))
