@@ -118,6 +118,9 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
           if (mv == 0ull) break;
           k = __builtin_ctzll(mv);
         }
+        // column k of G is known once k is: issue its LDS read now so its latency hides under
+        // the owner's step and the two readlanes instead of sitting on the Hw chain after them
+        const double gjk = j < F ? Gs[j * F + k] : 0.0;
         // the owner lane evaluates tmp = q_k − (Gw)_k + G_kk w_k and the soft-threshold step,
         // then (nw, dw) are broadcast: two readlanes instead of four on the dependent chain
         double nw_l = 0.0, dw_l = 0.0;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
           wj = nw_l;
         }
         const double nw = readlane_f64(nw_l, k), dw = readlane_f64(dw_l, k);
-        if (dw != 0.0 && j < F) Hw += Gs[j * F + k] * dw;
+        if (dw != 0.0 && j < F) Hw += gjk * dw;
         d_w_max = fmax(d_w_max, fabs(dw));
         w_max = fmax(w_max, fabs(nw));
       }

@@ -80,11 +80,17 @@ struct CoopPart {
 
 // Member-local exact reduction (a → max; (b, idx) → arg-max, ties → larger idx): DPP/permlane
 // wave maxima, one barrier, fold of the wave partials.  Every thread receives the result.
+// WantA = false: the caller passes a uniform `a` and ignores the max (WSS step 1), so its two
+// wave-max chains are skipped (the result's ka is then f64_okey(a)).
+template <bool WantA = true>
 __device__ __forceinline__ CoopPart coop_block_red(double a, double b, int idx, CoopPart* sh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const unsigned long long ka = f64_okey(a), kb = f64_okey(b);
-  const unsigned ah = wave_max_u32((unsigned)(ka >> 32));
-  const unsigned al = wave_max_u32((unsigned)(ka >> 32) == ah ? (unsigned)ka : 0u);
+  unsigned ah = (unsigned)(ka >> 32), al = (unsigned)ka;
+  if constexpr (WantA) {
+    ah = wave_max_u32((unsigned)(ka >> 32));
+    al = wave_max_u32((unsigned)(ka >> 32) == ah ? (unsigned)ka : 0u);
+  }
   const unsigned bh = wave_max_u32((unsigned)(kb >> 32));
   const unsigned bl = wave_max_u32((unsigned)(kb >> 32) == bh ? (unsigned)kb : 0u);
   const bool top = (unsigned)(kb >> 32) == bh && (unsigned)kb == bl;
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
         const double v = ((ypos >> k) & 1ull) ? -G[k] : G[k];
         if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
       }
-    loc = coop_block_red(-kCInf, bb, bi, shA);
+    loc = coop_block_red<false>(-kCInf, bb, bi, shA);
   }
   unsigned long long r1kb = 0ull;
   int i = -1;
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       }
     }
     tick(4);
-    loc = coop_block_red(-kCInf, bb, bi, shA);
+    loc = coop_block_red<false>(-kCInf, bb, bi, shA);
     tick(5);
     if (!exchange1(loc, r1kb, i, ai_old)) return;
     tick(6);
@@ -718,7 +724,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
         const double v = ((ypos >> m) & 1ull) ? -G[m] : G[m];
         if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
       }
-    loc = coop_block_red(-kCInf, bb, bi, shA);
+    loc = coop_block_red<false>(-kCInf, bb, bi, shA);
   }
   unsigned long long r1kb = 0ull;
   int i = -1, mi = 0;
@@ -879,7 +885,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
         if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
       }
     }
-    loc = coop_block_red(-kCInf, bb, bi, shA);
+    loc = coop_block_red<false>(-kCInf, bb, bi, shA);
     if (!exchange1(loc, r1kb, i, ai_old, mi)) return;
   }
   // ---- α out (owners) and calculate_rho over all members
