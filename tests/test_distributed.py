@@ -19,6 +19,33 @@ def _free_port():
     return p
 
 
+def _plain(x):
+    """Tensors -> numpy before crossing the queue: a torch tensor is sent as a shared-memory
+    handle that dies with the worker, so the parent could read it after rank 0 exited."""
+    if isinstance(x, torch.Tensor):
+        return _T(x.detach().cpu().numpy())
+    if isinstance(x, (tuple, list)):
+        return type(x)(_plain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    return x
+
+
+class _T:
+    def __init__(self, a):
+        self.a = a
+
+
+def _unplain(x):
+    if isinstance(x, _T):
+        return torch.from_numpy(x.a)
+    if isinstance(x, (tuple, list)):
+        return type(x)(_unplain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _unplain(v) for k, v in x.items()}
+    return x
+
+
 def _worker(rank, world, port, fn_name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -27,7 +54,7 @@ def _worker(rank, world, port, fn_name, q):
     try:
         out = globals()[fn_name](rank, world, dist.group.WORLD)
         if rank == 0:
-            q.put(out)
+            q.put(_plain(out))
     finally:
         dist.destroy_process_group()
 
@@ -52,7 +79,7 @@ def _run(fn_name, world=2):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    return out
+    return _unplain(out)
 
 
 def _data(n=1200, F=20, seed=3):
