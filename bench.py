@@ -108,17 +108,30 @@ def main():
     for _ in range(a.warmup):
         step()
     barrier()
+    # every timed step carries an event-based stage timer (no host synchronisation: it costs
+    # the timed region nothing); the per-stage table below is the median over the timed steps
+    timers = [StageTimer(enabled=True, events=True) for _ in range(a.steps)]
+    cpu0 = time.process_time()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        res = step()
+    step_ends = []
+    for k in range(a.steps):
+        res = step(timer=timers[k])
+        step_ends.append(time.perf_counter())
     barrier()
     elapsed = time.perf_counter() - t0
+    cpu = time.process_time() - cpu0
     if group is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
         elapsed = float(t)
     n_total = res.n_train
-    # untimed: per-stage profile + held-out AUROC of a final fit
+    for tm in timers:
+        tm.collect()
+    stage_med = {k: round(float(np.median([tm.times.get(k, 0.0) for tm in timers])), 4)
+                 for k in timers[0].times}
+    host_med = {k: round(float(np.median([tm.host_times.get(k, 0.0) for tm in timers])), 4)
+                for k in timers[0].host_times}
+    # untimed: held-out AUROC of a final fit (+ the device-synchronised stage table for --timings)
     prof = StageTimer(enabled=True, device=dev if dev.type == "cuda" else None)
     final = step(evaluate=True, timer=prof)
     value = n_total * a.steps / elapsed
@@ -144,10 +157,41 @@ def main():
                                 "Stacking{Scaler+SVC(rbf,Platt), GBC(100 stumps), LR-L1} -> LR-L2",
                        "global_batch": n_total, "seq_len": a.features, "rows_per_gpu": a.rows // max(1, world),
                        "features": a.features, "parallelism": f"dp{world}",
-                       "stage_seconds": {k: round(v, 4) for k, v in prof.times.items()}},
+                       "stage_seconds": stage_med},
+            "diag": run_facts(dev, a.steps, elapsed, cpu, host_med, step_ends, t0),
         }
         print(json.dumps(out), flush=True)
     pdist.shutdown()
+
+
+def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
+    """Facts that explain a training-bench run (VERDICT r1 'next round' #1): device, which
+    solver / kernel paths ran, and how host-bound the timed steps were."""
+    import numpy as np
+    import torch
+    from hfens.models import hist_gbdt, logreg_solver, smo, stack_trainer
+    facts = {"host_cpu_s_per_step": round(cpu / steps, 4),
+             "host_cpu_fraction": round(cpu / max(elapsed, 1e-12), 3),
+             "stage_host_seconds": host_med,
+             "step_ms_min_med_max": [round(1e3 * x, 2) for x in _step_stats(step_ends, t0)],
+             "svm": dict(smo.LAST_SMO_INFO),
+             "gbdt_path": hist_gbdt.LAST_PATH.get("path"),
+             "logreg_path": logreg_solver.LAST_PATH.get("path"),
+             "concurrent_bases": bool(stack_trainer.CONCURRENT_BASES and dev.type == "cuda"),
+             "cpu_count": os.cpu_count(),
+             "cpu_affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+             "loadavg": [round(x, 2) for x in os.getloadavg()]}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        facts.update(gpu=p.name, arch=getattr(p, "gcnArchName", None), cus=p.multi_processor_count,
+                     hw_queues=os.environ.get("GPU_MAX_HW_QUEUES"))
+    return facts
+
+
+def _step_stats(ends, t0):
+    import numpy as np
+    d = np.diff(np.array([t0] + list(ends)))
+    return (float(d.min()), float(np.median(d)), float(d.max())) if d.size else (0.0, 0.0, 0.0)
 
 
 CPU_BASELINE_INFER_ROWS_PER_S = 158e3   # BASELINE.md (B): numpy full-stack batched inference

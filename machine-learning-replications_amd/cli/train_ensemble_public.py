@@ -63,6 +63,13 @@ def main(argv=None) -> int:
         X_dev, y_dev = pdist.shard_rows(X_dev, rank, world), pdist.shard_rows(y_dev, rank, world)
         X_sel, y_sel = pdist.shard_rows(X_sel, rank, world), pdist.shard_rows(y_sel, rank, world)
     res = develop(X_dev, y_dev, X_sel, y_sel, names, device=device, group=group)
+    if a.plots:
+        # collectives on EVERY rank (before the rank-0 block); only rank 0 draws
+        p_all = res.proba_sel
+        y_all = torch.as_tensor(y_sel, device=p_all.device)
+        if group is not None:
+            p_all = pdist.all_gather_rows(p_all[:, None], group)[:, 0]
+            y_all = pdist.all_gather_rows(y_all.to(p_all.dtype)[:, None], group)[:, 0]
     if rank == 0:
         print("Important Features")
         print(np.array(res.selected_names, dtype=object))
@@ -72,9 +79,6 @@ def main(argv=None) -> int:
         if a.timings:
             print(res.timer.table())
         if a.plots:
-            p_all = res.proba_sel if group is None else pdist.all_gather_rows(res.proba_sel[:, None], group)[:, 0]
-            y_all = torch.as_tensor(y_sel) if group is None else pdist.all_gather_rows(
-                torch.as_tensor(y_sel, device=p_all.device)[:, None], group)[:, 0]
             print("plots:", metrics.save_plots(y_all, p_all, a.plots))
         if a.save_model:
             from ..io.checkpoint import save_checkpoint

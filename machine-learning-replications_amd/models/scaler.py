@@ -33,8 +33,10 @@ class StandardScaler(Estimator):
         self.mean_ = mean.to(torch.float64)
         self.var_ = var.to(torch.float64)
         scale = torch.sqrt(self.var_)
-        self.scale_ = torch.where(scale < 10 * torch.finfo(torch.float64).eps,
-                                  torch.ones_like(scale), scale)
+        # sklearn 0.23.2 (the checkpoint's version) ``_handle_zeros_in_scale`` maps only an exact
+        # zero to 1; the ``< 10·eps`` rule is sklearn ≥ 1.0 and would rescale near-constant
+        # columns (e.g. a binary flag nearly constant inside one CV fold) differently
+        self.scale_ = torch.where(scale == 0.0, torch.ones_like(scale), scale)
         return self
 
     def transform(self, X):

@@ -377,6 +377,9 @@ _OTF_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i
 _COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
                      ("S", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
 _NCU: dict = {}
+# set while re-solving a batch whose cooperative launch reported a member-exchange timeout: the
+# one-workgroup solver needs no co-residency (same pair sequence, so the same result)
+_FORCE_SINGLE = [False]
 
 
 def _num_cus(device) -> int:
@@ -388,7 +391,7 @@ def _num_cus(device) -> int:
 
 def coop_members(P: int, max_l: int, ncu: int) -> int:
     """Workgroups per problem for the cooperative SMO (1 = the one-workgroup kernel)."""
-    if not COOP or PROFILE_SMO or P <= 0:
+    if not COOP or PROFILE_SMO or P <= 0 or _FORCE_SINGLE[0]:
         return 1
     return max(1, min(_COOP_MAX_W, max(ncu - COOP_RESERVE_CUS, P) // P, -(-max_l // COOP_MIN_SLICE)))
 
@@ -423,7 +426,8 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
         sm[k] = (koff, aoffs[k], l, ld, p.npos, 0, p.Cp, p.Cn)
         koff += l * ld
     max_l = max(p.l for p in live)
-    K = torch.empty(koff, dtype=torch.float32, device=device)
+    from .. import runtime
+    K = runtime.workspace(device, "svm_gram", koff, torch.float32)   # process-lifetime, grown only
     gdev = _dev_struct(g, device)
     E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
     alpha = torch.empty(aoffs[-1], dtype=torch.float64, device=device)
@@ -699,6 +703,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         all_probs += pr
         meta.append(mt)
     eps = float(svcs[0].tol)
+    args = (svcs, Zs, ys, max_iter_cap, group)
     sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
            else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
@@ -749,11 +754,11 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             E.platt_batch(pdev.data_ptr(), len(pl), dcat.data_ptr(), lcat.data_ptr(), ABt.data_ptr(),
                           ops.stream_ptr(device))
             return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
-                        keep=(pdev, dcat, lcat), device=device)
+                        keep=(pdev, dcat, lcat), device=device, args=args)
         for k, f in enumerate(pl):
             AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
     return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=None,
-                device=device)
+                device=device, args=args)
 
 
 def finish_svc_batch(st: dict):
@@ -762,7 +767,21 @@ def finish_svc_batch(st: dict):
                                                    st["sol"], st["AB"], st["device"])
     err = sol.get("smo_err")
     if err is not None and float(err.max()) != 0.0:
-        raise RuntimeError("cooperative SMO: a member exchange timed out (members not co-resident?)")
+        # a member exchange timed out (members not co-resident beside concurrent work): re-solve
+        # the whole batch with the one-workgroup kernel.  Under a process group err is part of
+        # the all-reduced solution vector, so every rank takes this branch together.
+        if st.get("retried"):
+            raise RuntimeError("SMO: member exchange timed out again on the one-workgroup re-solve")
+        import warnings
+        warnings.warn("cooperative SMO timed out waiting for a member; re-solving with one workgroup per problem")
+        _FORCE_SINGLE[0] = True
+        try:
+            st2 = launch_svc_batch(*st["args"])
+        finally:
+            _FORCE_SINGLE[0] = False
+        st2["retried"] = True
+        LAST_SMO_INFO["coop_fallback"] = True
+        return finish_svc_batch(st2)
     if st["ABt"] is not None:
         from ..utils.guards import check_finite
         check_finite(st["ABt"], "SVC Platt sigmoid (A, B)")

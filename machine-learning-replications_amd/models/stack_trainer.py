@@ -60,17 +60,36 @@ def _kind(est):
     raise NotImplementedError(f"unsupported base estimator {type(est).__name__}")
 
 
-def _svc_inputs(est, X, y, masks):
-    """Clones, their SVC objects and the scaled per-mask training matrices."""
+def _global_scaler_moments(X, masks, group):
+    """Per-mask column mean / population variance over the rows of EVERY rank (two-pass, f64):
+    one all-reduce of [count | Σx] per mask, then one of Σ(x − mean)² — 2 collectives for all
+    masks.  A rank-local fit would scale each shard differently."""
+    from ..parallel import dist as pdist
+    Xd = X.to(torch.float64)
+    m = masks.to(torch.float64)                                   # [K, n]
+    cnt, s1 = pdist.all_reduce_sum_f64([m.sum(1), m @ Xd], group)
+    mean = s1 / cnt[:, None]
+    sq = torch.stack([(m[k][:, None] * (Xd - mean[k]) ** 2).sum(0) for k in range(m.shape[0])])
+    (sq,) = pdist.all_reduce_sum_f64([sq], group)
+    return mean, sq / cnt[:, None], cnt
+
+
+def _svc_inputs(est, X, y, masks, group=None):
+    """Clones, their SVC objects and the scaled per-mask training matrices.  ``group`` (rows
+    sharded): the scalers are fitted on the global masked rows, as a single process would."""
     kind = _kind(est)
     clones = [est.clone() for _ in range(masks.shape[0])]
     Zs, ys = [], []
-    for c, m in zip(clones, masks):
+    gm = _global_scaler_moments(X, masks, group) if (group is not None and kind == "svc") else None
+    for k, (c, m) in enumerate(zip(clones, masks)):
         rows = torch.nonzero(m).squeeze(1)
         Xm = X[rows]
         if kind == "svc":
             sc = c.steps[0][1]
-            sc.fit(Xm)
+            if gm is None:
+                sc.fit(Xm)
+            else:
+                sc._set(gm[0][k], gm[1][k], int(gm[2][k]))
             Zs.append(sc.transform(Xm))
         else:
             Zs.append(Xm)
@@ -85,7 +104,7 @@ def fit_base_batch(est, X, y, masks, group=None, timer=None, svc_group=None):
     rank, only the SMO problems are spread over the ranks (task parallel)."""
     kind = _kind(est)
     if kind in ("svc", "svc_raw"):
-        clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks)
+        clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks, group)
         if group is None:
             fit_svc_batch(svcs, Zs, ys, group=svc_group)
         else:
@@ -120,8 +139,11 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     # two pool streams (the legacy default stream would implicitly serialise with them); the SVC
     # stream at high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues and
     # two same-priority pool streams were measured landing on ONE queue (serialised)
+    # process-lifetime streams: fresh pool streams per fit defeat the caching allocator's
+    # per-stream block reuse (hfens/runtime.py)
+    from .. import runtime
     main = torch.cuda.current_stream(dev)
-    side, other = torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev)
+    side, other = runtime.stream(dev, "svc", priority=-1), runtime.stream(dev, "bases")
     side.wait_stream(main)
     other.wait_stream(main)
     out, pending = {}, {}
@@ -132,7 +154,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
         with torch.cuda.stream(side):
             for i in svc_cols:
-                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks)
+                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group)
                 marks.append(("svc_inputs", _t.perf_counter()))
                 if group is None:
                     pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group))

@@ -1,0 +1,68 @@
+"""Device runtime helpers: persistent HIP streams and persistent workspaces.
+
+Why this exists (measured, ``profiles/r2_driver_gap.md``): the concurrent base-model fit used
+to create fresh ``torch.cuda.Stream`` objects every fit.  PyTorch hands those out round-robin
+from a pool, and its caching allocator keys cached blocks by stream, so the 7 GB batched SVM
+Gram allocated on "the" side stream was a NEW block almost every fit.  Cached blocks piled up
+on ~30 pool streams until HBM was full, then the allocator synchronised and released
+everything — a 0.3–2 s stall every few fits (the driver's 285 ms/fit mean over a 88 ms median).
+
+Here every role gets ONE stream per device for the life of the process, and the big per-fit
+buffers (Gram matrices, SMO exchange slots) are process-lifetime workspaces that only grow.
+A workspace remembers the stream that last used it; handing it to another stream makes that
+stream wait for everything already enqueued on the previous one.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+
+_STREAMS: Dict[Tuple[torch.device, str], torch.cuda.Stream] = {}
+_WS: Dict[Tuple[torch.device, str], list] = {}
+
+
+def stream(device, role: str, priority: int = 0) -> "torch.cuda.Stream":
+    """The process-lifetime stream for ``role`` on ``device`` (created on first use)."""
+    d = torch.device(device)
+    key = (d, role)
+    s = _STREAMS.get(key)
+    if s is None:
+        s = torch.cuda.Stream(d, priority=priority)
+        _STREAMS[key] = s
+    return s
+
+
+def workspace(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+    """A ``numel``-element view of a process-lifetime buffer (grown, never shrunk).
+
+    Contents are undefined.  Ordering: the caller's current stream is made to wait for the work
+    already enqueued on the stream that last took this workspace (host program order means every
+    earlier user's kernels are enqueued by now)."""
+    d = torch.device(device)
+    key = (d, name)
+    ent = _WS.get(key)
+    nbytes = int(numel) * torch.empty(0, dtype=dtype).element_size()
+    cur = torch.cuda.current_stream(d) if d.type == "cuda" else None
+    if ent is not None and cur is not None and ent[1] is not None and ent[1] != cur:
+        ev = torch.cuda.Event()
+        ev.record(ent[1])
+        cur.wait_event(ev)
+    if ent is None or ent[0].numel() < nbytes:
+        if ent is not None:
+            ent[0] = None          # drop the old buffer first: peak = one copy (record_stream
+            #                        below keeps the allocator from recycling it under live work)
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=d)
+        ent = [buf, cur]
+        _WS[key] = ent
+    elif cur is not None and ent[1] != cur:
+        ent[0].record_stream(cur)
+    ent[1] = cur
+    return ent[0][:nbytes].view(dtype)[:numel]
+
+
+def release_workspaces(device=None):
+    """Free every workspace (of ``device``, or all)."""
+    for key in list(_WS):
+        if device is None or key[0] == torch.device(device):
+            del _WS[key]
