@@ -664,13 +664,50 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
     return finish_svc_batch(launch_svc_batch(svcs, Zs, ys, max_iter_cap, group=group))
 
 
+# Exact (libsvm pair sequence) vs large-problem path (``svc_lowrank``: Nyström reduced-set SVC,
+# interior-point dual).  "auto": exact while every problem has ≤ EXACT_MAX_POINTS points and the
+# batch's stored Grams (Σ l² f32) fit GRAM_BUDGET bytes; otherwise low-rank.  The bench's 10k-row
+# configuration (max l = 10,000, 7 GB of Grams) stays exact.
+EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "20480"))
+GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(64 << 30)))
+
+
+def use_lowrank(sizes) -> bool:
+    if SOLVER == "lowrank":
+        return True
+    if SOLVER in ("exact", "ws"):
+        return False
+    # problem sizes ≈ 0.8·l (Platt folds) and l (final) per fit
+    gram = sum(4.0 * (5 * (0.8 * l) ** 2 + l * l) for l in sizes)
+    return max(sizes) > EXACT_MAX_POINTS or gram > GRAM_BUDGET
+
+
 def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
     problems are solved task-parallel over the ranks (:func:`assign_problems`) and their
-    solutions all-reduced — one collective, issued from the calling thread."""
+    solutions all-reduced — one collective, issued from the calling thread.
+
+    Fits above the exact solver's size/memory limits (:func:`use_lowrank`) are solved by the
+    Nyström reduced-set SVC (:mod:`svc_lowrank`) instead, synchronously; with ``group`` fit ``f``
+    is solved on rank ``f mod world`` and broadcast."""
     from .. import ops
+    if use_lowrank([int(y.numel()) for y in ys]):
+        from .svc_lowrank import fit_svc_lowrank_batch
+        LAST_SMO_INFO.clear()
+        LAST_SMO_INFO.update(solver="nystrom-ipm", problems=6 * len(svcs), max_l=max(int(y.numel()) for y in ys))
+        if group is None:
+            fit_svc_lowrank_batch(svcs, Zs, ys)
+        else:
+            from ..parallel.stack import broadcast_svc_fits
+            import torch.distributed as dist
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+            mine = [f for f in range(len(svcs)) if f % world == rank]
+            if mine:
+                fit_svc_lowrank_batch([svcs[f] for f in mine], [Zs[f] for f in mine], [ys[f] for f in mine])
+            broadcast_svc_fits(svcs, Zs, group)
+        return dict(done=True, svcs=svcs)
     from ..utils.guards import check_binary, check_finite
     for f, (Z, y) in enumerate(zip(Zs, ys)):
         check_finite(Z, f"SVC.fit X (fit {f})")
@@ -763,6 +800,8 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
 
 def finish_svc_batch(st: dict):
     """Platt parameters to the host, support-vector extraction, ``set_fitted``."""
+    if st.get("done"):
+        return st["svcs"]
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
                                                    st["sol"], st["AB"], st["device"])
     err = sol.get("smo_err")

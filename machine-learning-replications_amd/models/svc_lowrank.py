@@ -1,0 +1,264 @@
+"""Large-problem C-SVC: Nyström reduced-set RBF SVC solved exactly by an interior-point method.
+
+Why (SURVEY.md §7.3 hard part #1): libsvm's SMO needs ≈ 0.5·l pairs on this
+cohort (measured with sklearn: 5.9k / 10.3k / 20.3k iterations at 10k / 20k / 40k rows, about
+33 % support vectors). At 1M rows that is ≈ 5·10⁵ strictly sequential pair updates per problem,
+and there are 36 problems per stacking fit. The stored-Gram solvers need 4 TB per problem.
+Both exact routes are out of reach at config-3 scale, so above ``EXACT_MAX_POINTS`` every SVC
+fit switches to this path (documented, AUROC-guarded).
+
+Model
+-----
+* Landmarks: ``m`` training rows drawn without replacement (seeded by ``random_state``).
+* Nyström feature map φ(x) = Λ^{-1/2} Uᵀ k_L(x), with K(L, L) = U Λ Uᵀ. This is the exact
+  map for the rank-r kernel K̃ = K_{·L} K_{LL}⁺ K_{L·}. Eigenvalues below
+  1e-10·λ_max are dropped.
+* The C-SVC dual of libsvm (per-class C = C·class_weight, Σ y_i α_i = 0, 0 ≤ α_i ≤ C_i) with
+  K̃ in place of K. It is solved to high accuracy, not to SMO's 1e-3 KKT gap, by a
+  Mehrotra predictor–corrector interior-point method.
+  - Every Newton system is (D + V Vᵀ) Δα + y Δb = h, with V = diag(y)Φ (l × r).
+  - It is solved through the Sherman–Morrison–Woodbury identity with one r × r Cholesky
+    per iteration (Ferris & Munson, "Interior-point methods for massive SVMs", 2002).
+  - The work is one l×r×r GEMM per iteration plus GEMVs: hipBLASLt/rocBLAS on the MI355X, f64.
+  - About 20–40 iterations, independent of l.
+* The solution is itself an RBF kernel expansion on the landmarks:
+  decision(x) = w·φ(x) − ρ = Σ_j β_j K(l_j, x) − ρ with β = U Λ^{-1/2} w.
+  So the fitted SVC has exactly libsvm's form: ``support_vectors_`` = landmarks,
+  ``dual_coef_`` = β. The fused inference kernel, the checkpoint writer and ``predict_hf.py``
+  all read it unchanged.
+* Platt scaling is unchanged: libsvm's 5-fold CV split (same RNG and permutation) and
+  ``sigmoid_train`` on the held-out decision values. All 6 problems of a fit share that
+  fit's landmarks and feature map.
+
+Accuracy guard (``profiles/r2_svc_lowrank.md``, ``tests/test_svc_lowrank.py``):
+- held-out AUROC vs the exact solver (sklearn/libsvm) was measured at 40k and 100k rows;
+- GPU tests compare it with the exact cooperative SMO at 20k rows.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+N_LANDMARKS = int(os.environ.get("HFENS_SVC_LANDMARKS", "512"))
+IPM_MAX_ITER = 80
+IPM_TOL = 1e-9
+
+
+def _rbf(A: torch.Tensor, B: torch.Tensor, gamma: float) -> torch.Tensor:
+    """exp(−γ‖a − b‖²) for all row pairs, f64 (GEMM form, clamped at 0)."""
+    d2 = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
+    return torch.exp(-gamma * d2.clamp_(min=0.0))
+
+
+def nystrom_map(Z: torch.Tensor, idx: torch.Tensor, gamma: float):
+    """(Φ [l, r], T [m, r]) with Φ = K(Z, L) T and T = U Λ^{-1/2} (dropped tiny eigenvalues)."""
+    L = Z[idx]
+    W = _rbf(L, L, gamma)
+    lam, U = torch.linalg.eigh(W)
+    keep = lam > 1e-10 * lam.max()
+    T = U[:, keep] / torch.sqrt(lam[keep])[None, :]
+    return _rbf(Z, L, gamma) @ T, T
+
+
+_SYRK_CHUNK = 8192
+
+
+def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+    """Φᵀ diag(d) Φ as a split-K batched GEMM: a plain [r × r] GEMM over a 10⁵–10⁶-long K has
+    only (r/128)² output tiles — a few dozen workgroups on a 256-CU part — so the rows are cut
+    into 8192-row slabs (one batched GEMM, ~100 slabs × tiles in flight) and the slab products
+    summed."""
+    l, r = Phi.shape
+    k = l // _SYRK_CHUNK
+    S = torch.zeros(r, r, dtype=Phi.dtype, device=Phi.device)
+    if k > 0:
+        P = Phi[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, r)
+        Pd = P * d[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, 1)
+        S += torch.bmm(P.transpose(1, 2), Pd).sum(0)
+    if k * _SYRK_CHUNK < l:
+        T = Phi[k * _SYRK_CHUNK:]
+        S += T.T @ (T * d[k * _SYRK_CHUNK:, None])
+    return S
+
+
+def _phit(Phi: torch.Tensor, V: torch.Tensor) -> torch.Tensor:
+    """Φᵀ V for a skinny V [l, k] as a split-K batched GEMM (the library's transposed GEMV over
+    a 10⁶-long reduction ran 50× below HBM rate: one output tile, no K split)."""
+    l, r = Phi.shape
+    k = l // _SYRK_CHUNK
+    out = torch.zeros(r, V.shape[1], dtype=Phi.dtype, device=Phi.device)
+    if k > 0:
+        P = Phi[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, r)
+        Vc = V[: k * _SYRK_CHUNK].reshape(k, _SYRK_CHUNK, V.shape[1])
+        out += torch.bmm(P.transpose(1, 2), Vc).sum(0)
+    if k * _SYRK_CHUNK < l:
+        out += Phi[k * _SYRK_CHUNK:].T @ V[k * _SYRK_CHUNK:]
+    return out
+
+
+def _max_step(v, dv):
+    """Largest t ≤ 1 with v + t·dv ≥ 0 (device scalar, no host sync)."""
+    ratio = torch.where(dv < 0, -v / torch.where(dv < 0, dv, -torch.ones_like(dv)), torch.full_like(v, 1.0))
+    return ratio.min().clamp(max=1.0)
+
+
+def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int = IPM_MAX_ITER,
+                 tol: float = IPM_TOL):
+    """Solve min ½αᵀQα − 1ᵀα, yᵀα = 0, 0 ≤ α ≤ c, Q = diag(y) Φ Φᵀ diag(y), to high accuracy.
+
+    Mehrotra predictor–corrector on (α, ν ≥ 0 for α ≥ 0, μ ≥ 0 for α ≤ c, b). Returns
+    (α, ρ, iterations), ρ in libsvm's convention (decision = Σ y_i α_i K(x_i, ·) − ρ).
+    Per iteration: one split-K weighted Gram (:func:`_weighted_gram`), one r × r Cholesky, six
+    skinny GEMMs over Φ, and ONE host synchronisation (the convergence test)."""
+    l, r = Phi.shape
+    dt = torch.float64
+    Phi = Phi.to(dt)
+    y = y.to(dt)
+    c = c.to(dt)
+    a = 0.5 * c
+    nu = torch.ones(l, dtype=dt, device=Phi.device)
+    mu = torch.ones(l, dtype=dt, device=Phi.device)
+    b = torch.zeros((), dtype=dt, device=Phi.device)
+    eye = torch.eye(r, dtype=dt, device=Phi.device)
+    csum = float(c.sum())
+    it = 0
+    for it in range(1, max_iter + 1):
+        s = c - a
+        w = _phit(Phi, (y * a)[:, None])[:, 0]       # Φᵀ Y α
+        g = y * (Phi @ w) - 1.0                      # Qα − 1
+        rd = g + b * y - nu + mu
+        re = torch.dot(y, a)
+        gap = (torch.dot(a, nu) + torch.dot(s, mu)) / (2 * l)
+        chk = torch.stack([gap, rd.abs().max(), re.abs()]).cpu()
+        if float(chk[0]) < tol and float(chk[1]) < 1e-8 and float(chk[2]) < 1e-8 * csum:
+            break
+        D = nu / a + mu / s
+        Dinv = 1.0 / D
+        # S = I + Vᵀ D⁻¹ V  (V = YΦ, so Vᵀ D⁻¹ V = Φᵀ D⁻¹ Φ).  Free points drive D → 0, so S spans
+        # many decades: equilibrate symmetrically before the Cholesky (exact); a relative jitter on
+        # the unit diagonal is added only if it still fails.
+        S = eye + _weighted_gram(Phi, Dinv)
+        sc = torch.rsqrt(torch.diagonal(S))
+        Ss = S * sc[:, None] * sc[None, :]
+        Lc, info = torch.linalg.cholesky_ex(Ss)
+        jit = 1e-14
+        while int(info) != 0 and jit < 1e-6:
+            Lc, info = torch.linalg.cholesky_ex(Ss + jit * eye)
+            jit *= 100.0
+
+        def Minv(u):  # (D + V Vᵀ)⁻¹ u for u [l, k], V = YΦ
+            du = Dinv[:, None] * u
+            t = sc[:, None] * torch.cholesky_solve(sc[:, None] * _phit(Phi, y[:, None] * du), Lc)
+            return du - Dinv[:, None] * (y[:, None] * (Phi @ t))
+
+        def dirs(Mh, My, yMy, rnu, rmu):
+            db = (torch.dot(y, Mh) + re) / yMy
+            da = Mh - db * My
+            dnu = (-rnu - nu * da) / a
+            dmu = (-rmu + mu * da) / s
+            return da, db, dnu, dmu
+
+        def step_len(da, dnu, dmu):
+            return torch.minimum(torch.minimum(_max_step(a, da), _max_step(s, -da)),
+                                 torch.minimum(_max_step(nu, dnu), _max_step(mu, dmu)))
+
+        # predictor (affine scaling): its right-hand side and y share one pass over Φ
+        rnu, rmu = a * nu, s * mu
+        h = -rd - rnu / a + rmu / s
+        M2 = Minv(torch.stack([h, y], 1))
+        Mh, My = M2[:, 0], M2[:, 1]
+        yMy = torch.dot(y, My)
+        da, db, dnu, dmu = dirs(Mh, My, yMy, rnu, rmu)
+        ta = step_len(da, dnu, dmu)
+        gap_aff = (torch.dot(a + ta * da, nu + ta * dnu) + torch.dot(s - ta * da, mu + ta * dmu)) / (2 * l)
+        sigma = (gap_aff / gap) ** 3
+        # corrector (centring + second-order terms)
+        tau = sigma * gap
+        rnu, rmu = a * nu + da * dnu - tau, s * mu - da * dmu - tau
+        h = -rd - rnu / a + rmu / s
+        da, db, dnu, dmu = dirs(Minv(h[:, None])[:, 0], My, yMy, rnu, rmu)
+        t = 0.995 * step_len(da, dnu, dmu)
+        a = a + t * da
+        b = b + t * db
+        nu = nu + t * dnu
+        mu = mu + t * dmu
+    a = torch.where(a < 1e-12 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-12), c, a))
+    # ρ as libsvm computes it from the final gradient: mean of y_i G_i over free points, else the
+    # midpoint of the bound range (ρ = −b at the optimum)
+    g = y * (Phi @ _phit(Phi, (y * a)[:, None])[:, 0]) - 1.0
+    yg = y * g
+    free = (a > 1e-8 * c) & (a < c * (1 - 1e-8))
+    if bool(free.any()):
+        rho = yg[free].mean()
+    else:
+        rho = -b
+    return a, float(rho), it
+
+
+def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
+    """Fit every ``svcs[f]`` on (already scaled) ``Zs[f]`` with labels ``ys[f]`` ∈ {0, 1}:
+    Platt CV problems + final problem per fit, as libsvm, on the fit's Nyström map."""
+    from .smo import _expand, _sigmoid_train_host
+    from ..utils.guards import check_binary, check_finite
+    m = int(n_landmarks or N_LANDMARKS)
+    for f, (svc, Z, y) in enumerate(zip(svcs, Zs, ys)):
+        check_finite(Z, f"SVC.fit X (fit {f})")
+        check_binary(y, f"SVC.fit y (fit {f})")
+        dev = Z.device
+        Zd = Z.to(torch.float64)
+        y_np = y.reshape(-1).to(torch.float64).cpu().numpy()
+        l = y_np.shape[0]
+        gamma = svc.resolve_gamma(Zd)
+        if svc.class_weight == "balanced":
+            cnt = np.bincount((y_np > 0.5).astype(np.int64), minlength=2).astype(np.float64)
+            cw = l / (2 * cnt)
+        else:
+            cw = svc.class_weights(torch.as_tensor(y_np)).cpu().numpy()
+        probs, mt = _expand(f, y_np, gamma, cw, svc)
+        grouped = mt["grouped"]
+        n0 = mt["n0"]
+        # landmarks: a seeded draw of the fit's rows, grouped class 0 first (libsvm SV order)
+        g = torch.Generator().manual_seed(int(svc.random_state or 0) * 1000003 + l)
+        k = min(m, l)
+        pick = torch.randperm(l, generator=g)[:k].numpy()
+        cls1 = y_np[pick] > 0.5
+        pick = np.concatenate([np.sort(pick[~cls1]), np.sort(pick[cls1])])
+        idx = torch.as_tensor(pick, device=dev)
+        Phi, T = nystrom_map(Zd, idx, gamma)
+        # libsvm-internal labels: class 0 = +1 (grouped order); per-point C
+        yint = torch.as_tensor(np.where(y_np > 0.5, -1.0, 1.0), dtype=torch.float64, device=dev)
+        cvec = torch.where(yint > 0, torch.full_like(yint, mt["C0"]), torch.full_like(yint, mt["C1"]))
+        dec_cv = np.zeros(l)
+        lab = np.where(np.arange(l) < n0, 1.0, -1.0)          # grouped-position labels
+        iters = []
+        for p in probs:
+            if p.fold < 0:
+                continue
+            if p.rows is None:
+                dec_cv[p.held] = p.const
+                continue
+            rows = torch.as_tensor(p.rows, device=dev)
+            a, rho, it = ipm_svc_dual(Phi[rows], yint[rows], cvec[rows])
+            iters.append(it)
+            wv = _phit(Phi[rows], (yint[rows] * a)[:, None])[:, 0]
+            held = torch.as_tensor(p.held_rows, device=dev)
+            dec_cv[p.held] = (Phi[held] @ wv - rho).cpu().numpy()
+        A, B = _sigmoid_train_host(dec_cv, lab) if svc.probability else (0.0, 0.0)
+        a, rho, it = ipm_svc_dual(Phi, yint, cvec)
+        iters.append(it)
+        wv = _phit(Phi, (yint * a)[:, None])[:, 0]
+        beta = T @ wv                                          # coefficients on the landmarks
+        n_sv0 = int((~cls1).sum())
+        svc.set_fitted(support=idx, support_vectors=Zd[idx], n_support=[n_sv0, k - n_sv0],
+                       dual_coef_libsvm=beta, rho=rho, probA=A, probB=B, gamma=gamma,
+                       class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
+                       shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=dev)
+        svc.n_iter_ = int(it)
+        svc.solver_ = "nystrom-ipm"
+        LAST_INFO.update(solver="nystrom-ipm", landmarks=k, rank=int(T.shape[1]), ipm_iters=iters)
+    return svcs
+
+
+LAST_INFO: dict = {}

@@ -35,9 +35,15 @@ def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
 
 def finish_svc_batch_distributed(pre: dict, group):
     """Complete this rank's fits, then broadcast every fit from its owner (collectives)."""
-    svcs, Zs, world, rank = pre["svcs"], pre["Zs"], pre["world"], pre["rank"]
+    svcs, Zs = pre["svcs"], pre["Zs"]
     if pre["st"] is not None:
         finish_svc_batch(pre["st"])
+    return broadcast_svc_fits(svcs, Zs, group)
+
+
+def broadcast_svc_fits(svcs, Zs, group):
+    """Every rank receives fit ``f`` from its owner, rank ``f mod world`` (collectives)."""
+    world, rank = pdist.dist.get_world_size(group), pdist.dist.get_rank(group)
     for f, svc in enumerate(svcs):
         src = f % world
         if rank == src:

@@ -1,10 +1,15 @@
 #!/bin/bash
-# Full-ensemble development fit at growing row counts (cfg 3 path): per-stage timings.
+# Full-ensemble development fit at growing row counts (BASELINE config 3 path, one GPU):
+# per-stage medians and the SVC solver that ran.  Each step has its own limit; stop at the first
+# failure.
 set -o pipefail
-mkdir -p gpurun_out/rows
-timeout -k 10 300 python bench.py --rows 30000 --steps 1 --warmup 1 --timings > gpurun_out/rows/r30k.json 2> gpurun_out/rows/r30k.err || { echo "30k failed"; tail -20 gpurun_out/rows/r30k.err; exit 1; }
-grep -v amdgpu.ids gpurun_out/rows/r30k.err; cat gpurun_out/rows/r30k.json
-HFENS_SVM_SOLVER=ws timeout -k 10 300 python bench.py --rows 30000 --steps 1 --warmup 0 --timings > gpurun_out/rows/r30k_ws.json 2> gpurun_out/rows/r30k_ws.err || { echo "30k ws failed"; tail -20 gpurun_out/rows/r30k_ws.err; exit 1; }
-grep -v amdgpu.ids gpurun_out/rows/r30k_ws.err; cat gpurun_out/rows/r30k_ws.json
-HFENS_SVM_SOLVER=ws timeout -k 10 500 python bench.py --rows 100000 --steps 1 --warmup 0 --timings > gpurun_out/rows/r100k_ws.json 2> gpurun_out/rows/r100k_ws.err || { echo "100k ws failed"; tail -20 gpurun_out/rows/r100k_ws.err; exit 1; }
-grep -v amdgpu.ids gpurun_out/rows/r100k_ws.err; cat gpurun_out/rows/r100k_ws.json
+D=gpurun_out/rows
+mkdir -p $D
+run() {  # run TAG SECONDS ARGS...
+  local tag=$1 secs=$2; shift 2
+  timeout -k 10 $secs python3 -u bench.py "$@" > $D/$tag.json 2> $D/$tag.err || { echo "$tag failed"; tail -30 $D/$tag.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$D/$tag.json')); print('$tag', d['ms_per_step'], d['value'], d['auroc'], d['config']['stage_seconds'], d['diag']['svm'])"
+}
+run r30k 200 --rows 30000 --steps 1 --warmup 1
+run r100k 300 --rows 100000 --steps 1 --warmup 1
+run r1m 600 --rows 1000000 --steps 1 --warmup 0

@@ -49,7 +49,7 @@ def _unplain(x):
 def _worker(rank, world, port, fn_name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, 4 // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         out = globals()[fn_name](rank, world, dist.group.WORLD)
@@ -59,11 +59,35 @@ def _worker(rank, world, port, fn_name, q):
         dist.destroy_process_group()
 
 
-def _run(fn_name, world=2):
+def _worker_nccl(rank, world, port, fn_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), HFENS_DIST_BACKEND="nccl")
+    from hfens.parallel import dist as pdist
+    group, r, w = pdist.init_from_env()
+    try:
+        out = globals()[fn_name](r, w, group)
+        if rank == 0:
+            q.put(_plain(out))
+    finally:
+        pdist.shutdown()
+
+
+def _nccl_sum(rank, world, group):
+    from hfens.parallel import dist as pdist
+    t = torch.full((2,), float(rank + 1), device=pdist.rank_device())
+    pdist.all_reduce_sum_(t, group)
+    return t.cpu().tolist()
+
+
+def _run_nccl(fn_name, world):
+    return _run(fn_name, world, target=_worker_nccl)
+
+
+def _run(fn_name, world=2, target=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    procs = [ctx.Process(target=target or _worker, args=(r, world, port, fn_name, q)) for r in range(world)]
     for p in procs:
         p.start()
     import queue as _q
@@ -161,10 +185,11 @@ def _svc_task(rank, world, group):
     return [(s._dual_coef_.clone(), float(s._intercept_[0]), s._probA.item(), s._probB.item()) for s in svcs]
 
 
-def test_gbdt_dp_bit_identical():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gbdt_dp_bit_identical(world):
     from hfens.models.gbdt import GradientBoostingClassifier
     from hfens.models.hist_gbdt import fit_gbdt_batch
-    got = _run("_gbdt")
+    got = _run("_gbdt", world)
     X, y, _ = _data()
     masks = torch.ones(2, X.shape[0], dtype=torch.bool)
     masks[0, ::4] = False
@@ -193,19 +218,21 @@ def test_gbdt_subsample_dp_bit_identical():
         assert torch.equal(ts, m.train_score_)
 
 
-def test_logreg_dp():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_logreg_dp(world):
     from hfens.models.linear import LogisticRegression
     from hfens.models.logreg_solver import fit_logreg_batch
-    coef, ic = _run("_logreg")
+    coef, ic = _run("_logreg", world)
     X, y, _ = _data()
     m = LogisticRegression(penalty="l1", solver="liblinear", class_weight="balanced")
     fit_logreg_batch([m], X, y)
     assert torch.allclose(coef, m.coef_, atol=1e-8)
 
 
-def test_lasso_dp():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_lasso_dp(world):
     from hfens.models.lasso import LassoCV, SelectFromModel
-    alpha, coef, sup = _run("_lasso")
+    alpha, coef, sup = _run("_lasso", world)
     X, y, _ = _data()
     s = SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=8).fit(X, y)
     assert abs(alpha - s.estimator_.alpha_) < 1e-15
@@ -221,10 +248,11 @@ def test_assign_problems_lpt():
     assert max(loads) - min(loads) <= 4
 
 
-def test_svc_task_parallel_matches_single():
+@pytest.mark.parametrize("world", [2, 4])
+def test_svc_task_parallel_matches_single(world):
     from hfens.models.smo import fit_svc_batch
     from hfens.models.svc import SVC
-    got = _run("_svc_task")
+    got = _run("_svc_task", world)
     X, y, _ = _data(300, 8, seed=9)
     Z = (X - X.mean(0)) / X.std(0, unbiased=False)
     svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in range(2)]
@@ -254,3 +282,71 @@ def test_develop_dp_matches_single():
     r = develop(Xd, yd, Xs, ys, names, device="cpu")
     assert np.array_equal(sel, r.selected)
     assert abs(scores["auroc"] - r.scores["auroc"]) < 1e-3  # f64 reduction order differs per rank
+
+
+def _stack_dp(rank, world, group, lowrank=False):
+    from hfens.models import smo
+    from hfens.models.stacking import StackingClassifier
+    from hfens.config import EnsembleConfig, build_estimators
+    from hfens.parallel.dist import shard_rows
+    if lowrank:
+        smo.SOLVER = "lowrank"
+    X, y, _ = _data(480, 8, seed=13)
+    clf = build_estimators(EnsembleConfig())
+    clf.fit(shard_rows(X, rank, world), shard_rows(y, rank, world), group=group)
+    sc = clf.estimators_[0].steps[0][1]
+    svc = clf.estimators_[0].steps[-1][1]
+    return (sc.mean_.clone(), sc.scale_.clone(), svc._dual_coef_.clone(), float(svc._intercept_[0]),
+            svc.support_.clone(), clf.final_estimator_.coef_.clone())
+
+
+def _stack_dp_lowrank(rank, world, group):
+    return _stack_dp(rank, world, group, lowrank=True)
+
+
+def _stack_single(lowrank=False):
+    from hfens.models import smo
+    from hfens.config import EnsembleConfig, build_estimators
+    old = smo.SOLVER
+    smo.SOLVER = "lowrank" if lowrank else old
+    try:
+        X, y, _ = _data(480, 8, seed=13)
+        clf = build_estimators(EnsembleConfig())
+        clf.fit(X, y)
+    finally:
+        smo.SOLVER = old
+    sc = clf.estimators_[0].steps[0][1]
+    svc = clf.estimators_[0].steps[-1][1]
+    return sc, svc, clf
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_stack_dp_scaler_and_svc_match_single(world):
+    """the DP stack's StandardScaler moments are reduced over ALL ranks, so the
+    scaled rows, the SVC solution and the meta-learner equal the single-process fit."""
+    mean, scale, coef, ic, sup, meta = _run("_stack_dp", world)
+    sc, svc, clf = _stack_single()
+    assert torch.allclose(mean, sc.mean_, rtol=0, atol=1e-12)
+    assert torch.allclose(scale, sc.scale_, rtol=0, atol=1e-12)
+    assert torch.equal(sup, svc.support_)
+    assert torch.allclose(coef, svc._dual_coef_, atol=1e-9)
+    assert abs(ic - float(svc._intercept_[0])) < 1e-9
+    assert torch.allclose(meta, clf.final_estimator_.coef_, atol=1e-6)
+
+
+def test_stack_dp_lowrank_svc_matches_single():
+    """The large-problem SVC path (Nyström + IPM) under DP: fits solved on their owner rank and
+    broadcast; identical to the single-process low-rank fit."""
+    mean, scale, coef, ic, sup, meta = _run("_stack_dp_lowrank", 4)
+    sc, svc, clf = _stack_single(lowrank=True)
+    assert torch.equal(sup, svc.support_)
+    assert torch.allclose(coef, svc._dual_coef_, atol=1e-8)
+    assert abs(ic - float(svc._intercept_[0])) < 1e-8
+
+
+def test_nccl_all_reduce_two_gpus():
+    """The RCCL (backend "nccl") branch of hfens.parallel.dist with ≥ 2 visible GPUs."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    got = _run_nccl("_nccl_sum", 2)
+    assert got == [3.0, 3.0]
