@@ -296,15 +296,20 @@ class _W:
                ("min_impurity_split", self.v(m.min_impurity_split)), ("class_weight", self.v(None)),
                ("presort", self.s(m.presort)), ("ccp_alpha", self.v(m.ccp_alpha)),
                ("n_features_", self.v(nf)), ("n_outputs_", self.v(1)), ("max_features_", self.v(nf))]
+        order = _preorder(m, t, c)            # sklearn DepthFirstTreeBuilder node ids
+        c = len(order)
+        remap = {h: i for i, h in enumerate(order)}
+        left = _np(m.tree_left_[t], np.int64)
+        right = _np(m.tree_right_[t], np.int64)
         nodes = np.zeros(c, dtype=NODE_DTYPE)
-        nodes["left_child"] = _np(m.tree_left_[t, :c], np.int64)
-        nodes["right_child"] = _np(m.tree_right_[t, :c], np.int64)
-        nodes["feature"] = _np(m.tree_feature_[t, :c], np.int64)
-        nodes["threshold"] = _np(m.tree_threshold_[t, :c], np.float64)
-        nodes["impurity"] = _np(m.tree_impurity_[t, :c], np.float64)
-        nodes["n_node_samples"] = _np(m.tree_n_node_samples_[t, :c], np.int64)
-        nodes["weighted_n_node_samples"] = _np(m.tree_weighted_n_node_samples_[t, :c], np.float64)
-        values = _np(m.tree_value_[t, :c], np.float64).reshape(c, 1, 1)
+        nodes["left_child"] = [remap[left[h]] if left[h] >= 0 else -1 for h in order]
+        nodes["right_child"] = [remap[right[h]] if right[h] >= 0 else -1 for h in order]
+        nodes["feature"] = _np(m.tree_feature_[t], np.int64)[order]
+        nodes["threshold"] = _np(m.tree_threshold_[t], np.float64)[order]
+        nodes["impurity"] = _np(m.tree_impurity_[t], np.float64)[order]
+        nodes["n_node_samples"] = _np(m.tree_n_node_samples_[t], np.int64)[order]
+        nodes["weighted_n_node_samples"] = _np(m.tree_weighted_n_node_samples_[t], np.float64)[order]
+        values = _np(m.tree_value_[t], np.float64)[order].reshape(c, 1, 1)
         tree_state = sp.DictN([(self.s("max_depth"), sp.Prim(int(depth))),
                                (self.s("node_count"), sp.Prim(c)),
                                (self.s("nodes"), b.array(nodes)),
@@ -330,6 +335,25 @@ class _W:
         if isinstance(e, LogisticRegression):
             return self.lr(e, fitted, liblinear_iter_dtype=(e.solver == "liblinear"))
         raise TypeError(type(e))
+
+
+def _preorder(m, t, c):
+    """Node order of sklearn's depth-first builder (parent, then left subtree, then right; ids in
+    creation order) over the REACHABLE nodes.  A loaded checkpoint is already in that order (the
+    identity); a fresh histogram-GBDT tree is a heap layout (children of node h at 2h+1, 2h+2,
+    unreachable slots under leaves) and is compacted to sklearn's layout here."""
+    left = _np(m.tree_left_[t], np.int64)
+    right = _np(m.tree_right_[t], np.int64)
+    order, stack = [], [0]
+    while stack:
+        h = stack.pop()
+        order.append(h)
+        if left[h] >= 0:
+            stack.append(int(right[h]))
+            stack.append(int(left[h]))
+    if getattr(m, "tree_layout_", None) != "heap" and order != list(range(c)):
+        raise ValueError(f"tree {t}: node order is not sklearn's depth-first order")
+    return order
 
 
 def _depth(m, t):

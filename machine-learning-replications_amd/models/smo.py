@@ -668,8 +668,8 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
 # interior-point dual).  "auto": exact while every problem has ≤ EXACT_MAX_POINTS points and the
 # batch's stored Grams (Σ l² f32) fit GRAM_BUDGET bytes; otherwise low-rank.  The bench's 10k-row
 # configuration (max l = 10,000, 7 GB of Grams) stays exact.
-EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "20480"))
-GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(64 << 30)))
+EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "32768"))
+GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 
 
 def use_lowrank(sizes) -> bool:

@@ -43,7 +43,7 @@ import torch
 
 N_LANDMARKS = int(os.environ.get("HFENS_SVC_LANDMARKS", "512"))
 IPM_MAX_ITER = 80
-IPM_TOL = 1e-9
+IPM_TOL = 1e-8
 
 
 def _rbf(A: torch.Tensor, B: torch.Tensor, gamma: float) -> torch.Tensor:

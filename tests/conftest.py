@@ -11,6 +11,10 @@ CKPT = os.path.join(ROOT, "assets", "hf_predict_model.pkl")
 
 
 def pytest_configure(config):
+    # host mirrors run many tiny tensor ops: with 8 intra-op threads this container's OpenMP pool
+    # costs ~10 ms per op (measured: torch.round on 2,400 doubles 10 ms vs 10 µs single-threaded)
+    import torch
+    torch.set_num_threads(1)
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP extension")
     config.addinivalue_line("markers", "slow: long-running")
 

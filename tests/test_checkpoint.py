@@ -103,3 +103,69 @@ def test_svc_parity_with_installed_libsvm(ckpt_path):
     ours = m.predict_proba(torch.as_tensor(Z))[:, 1].numpy()
     theirs = sk.predict_proba(Z)[:, 1]
     np.testing.assert_allclose(ours, theirs, atol=2e-8)
+
+
+def _schema(v, path="root", out=None):
+    """(path, class / dtype) signature of a value graph: state-dict key ORDER, estimator classes,
+    array dtypes and ranks (shapes vary with the data)."""
+    out = [] if out is None else out
+    if isinstance(v, sp.SkObject):
+        out.append((path, "obj", v.cls))
+        if isinstance(v.state, dict):
+            out.append((path, "keys", tuple(v.state)))
+            for k, x in v.state.items():
+                if k in ("estimators_",) and isinstance(x, np.ndarray) and x.dtype == object:
+                    _schema(x.flat[0], f"{path}.{k}[0]", out)   # trees: one representative
+                else:
+                    _schema(x, f"{path}.{k}", out)
+        if v.items:
+            for k, x in v.items.items():
+                _schema(x, f"{path}[{k}]", out)
+    elif isinstance(v, np.ndarray):
+        out.append((path, "arr", v.dtype.str if v.dtype != object else "O", v.ndim,
+                    v.dtype.names or ()))
+    elif isinstance(v, (list, tuple)):
+        for i, x in enumerate(v):
+            _schema(x, f"{path}[{i}]", out)
+    elif isinstance(v, dict):
+        out.append((path, "dict", tuple(v)))
+        for k, x in v.items():
+            _schema(x, f"{path}.{k}", out)
+    elif isinstance(v, sp.NpRandomState):
+        out.append((path, "rng", v.key.dtype.str, v.key.shape))
+    else:
+        out.append((path, "val", type(v).__name__))
+    return out
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_trained_checkpoint_roundtrip(depth, tmp_path, ckpt_path):
+    """develop-style fit → save_checkpoint → load_checkpoint gives identical f64
+    predict_proba; depth > 1 trees are written in sklearn's compact depth-first node order; the
+    fresh file's schema (classes, key order, dtypes) equals the shipped 0.23.2 checkpoint's."""
+    from hfens.config import EnsembleConfig, build_estimators
+    from hfens.io.synth import make_hf_cohort
+    X, y, _ = make_hf_cohort(400, 17, seed=31, nan_frac=0.0)
+    X, y = torch.as_tensor(X), torch.as_tensor(y)
+    clf = build_estimators(EnsembleConfig(gbc_depth=depth))
+    clf.fit(X, y)
+    path = str(tmp_path / "fresh.pkl")
+    save_checkpoint(clf, path)
+    back = load_checkpoint(path)
+    Xt, _, _ = make_hf_cohort(300, 17, seed=32, nan_frac=0.0)
+    Xt = torch.as_tensor(Xt)
+    assert torch.equal(back.predict_proba(Xt), clf.predict_proba(Xt))
+    fresh = sp.to_py(sp.parse(_bytes(path)))
+    shipped = sp.to_py(sp.parse(_bytes(ckpt_path)))
+    assert _schema(fresh) == _schema(shipped)
+    # compact depth-first trees: every node reachable, children after their parent, left first
+    for est in fresh.state["estimators_"][1].state["estimators_"][:, 0]:
+        nodes = est.state["tree_"].state["nodes"]
+        assert est.state["tree_"].state["node_count"] == len(nodes)
+        for i, nd in enumerate(nodes):
+            if nd["left_child"] >= 0:
+                assert nd["left_child"] == i + 1 and nd["right_child"] > nd["left_child"]
+            else:
+                assert nd["feature"] == -2 and nd["right_child"] == -1
+    # and a re-save of the loaded model reproduces the fresh file byte for byte
+    assert save_checkpoint(back, str(tmp_path / "again.pkl")) == _bytes(path)

@@ -49,7 +49,7 @@ def _unplain(x):
 def _worker(rank, world, port, fn_name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    torch.set_num_threads(max(1, 4 // world))
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         out = globals()[fn_name](rank, world, dist.group.WORLD)
