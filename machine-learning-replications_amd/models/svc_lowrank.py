@@ -184,16 +184,10 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         b = b + t * db
         nu = nu + t * dnu
         mu = mu + t * dmu
-    a = torch.where(a < 1e-12 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-12), c, a))
-    # ρ as libsvm computes it from the final gradient: mean of y_i G_i over free points, else the
-    # midpoint of the bound range (ρ = −b at the optimum)
-    g = y * (Phi @ _phit(Phi, (y * a)[:, None])[:, 0]) - 1.0
-    yg = y * g
-    free = (a > 1e-8 * c) & (a < c * (1 - 1e-8))
-    if bool(free.any()):
-        rho = yg[free].mean()
-    else:
-        rho = -b
+    # snap points the interior point left within 1e-9·C of a bound (their multiplier carries the
+    # gap); ρ = −b: stationarity gives y_i G_i = −b on every free point, which is libsvm's ρ
+    a = torch.where(a < 1e-9 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-9), c, a))
+    rho = -b
     return a, float(rho), it
 
 
