@@ -145,8 +145,9 @@ class _HostKernels:
                     feat[b, hn] = -3
                     continue
                 best = (-1.0, 1 << 30, 0)
+                rk = st.frank[t, b].tolist() if st.frank is not None else list(range(st.F))
                 if tw >= st.min_split_q:
-                    for f in range(st.F):
+                    for f in sorted(range(st.F), key=lambda f: rk[f]):   # sklearn visit order
                         nb = int(nbins[f])
                         cw = torch.cumsum(hb[f, :nb, 2], 0)[:-1]
                         cg = torch.cumsum(hb[f, :nb, 0], 0)[:-1]
@@ -242,6 +243,8 @@ class _State:
     row_off: int = 0                       # global index of local row 0 (DP shards)
     wt: Optional[torch.Tensor] = None      # [B, n] this stage's in-bag weights (subsample < 1)
     bagw: Optional[torch.Tensor] = None    # [T, B] Σ in-bag weight per stage (train_score_ norm.)
+    frank: Optional[torch.Tensor] = None   # [T, B, F] int32 tie-break rank (sklearn visit order)
+    reduced: bool = False                  # r2 / dev / bagw already global (stage path)
 
     @property
     def wcur(self) -> torch.Tensor:
@@ -328,6 +331,9 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         if group is not None:
             from ..parallel import dist as pdist
             st.row_off = pdist.row_offset(n, group, dev)[0]
+    if D == 1 and SKLEARN_TIES and subsample == 1.0 and all(
+            isinstance(m.random_state, (int, np.integer)) for m in models):
+        st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group)
     if X.is_cuda:
         _run_device(st, group)
     else:
@@ -337,6 +343,76 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     return models
 
 
+# sklearn's tie-break between features with EXACTLY equal split gain (SURVEY.md §7.3 #3, E15): its
+# BestSplitter visits features in a per-node Fisher-Yates order drawn from the tree's rand_r state
+# and keeps the first strictly better one.  Depth-1 trees with an int random_state and no
+# subsampling reproduce that order (ops/csrc/host.hip sklearn_stump_ranks); otherwise ties go to
+# the lowest feature index.
+SKLEARN_TIES = os.environ.get("HFENS_GBDT_SKLEARN_TIES", "1") != "0"
+RAND_R_MAX = 2147483647
+
+
+def sklearn_stump_ranks(models, bins: torch.Tensor, masks: torch.Tensor, T: int, group=None) -> torch.Tensor:
+    """[T, B, F] int32: rank of each feature in sklearn's root visit order for every tree of every
+    model.  Constant features (one occupied bin over the model's rows, across all ranks) are
+    set aside exactly as sklearn does and never visited (rank F)."""
+    F, n = bins.shape
+    B = len(models)
+    big = torch.iinfo(torch.int32).max
+    bmin = torch.full((B, F), big, dtype=torch.int32, device=bins.device)
+    bmax = torch.full((B, F), -1, dtype=torch.int32, device=bins.device)
+    bi = bins.to(torch.int32)
+    for b in range(B):
+        sel = masks[b] > 0
+        if bool(sel.any()):
+            bmin[b] = bi[:, sel].amin(1)
+            bmax[b] = bi[:, sel].amax(1)
+    if group is not None:
+        import torch.distributed as dist
+        dist.all_reduce(bmin, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(bmax, op=dist.ReduceOp.MAX, group=group)
+    const = (bmax <= bmin).to(torch.uint8).cpu().numpy()
+    out = np.empty((T, B, F), dtype=np.int32)
+    for b, m in enumerate(models):
+        # GradientBoostingClassifier._rng = RandomState(random_state); each tree's splitter draws
+        # one randint(0, RAND_R_MAX) (checkpoint: MT position = n_estimators)
+        seeds = np.random.RandomState(int(m.random_state)).randint(0, RAND_R_MAX, size=T).astype(np.int64)
+        rk = np.empty((T, F), dtype=np.int32)
+        _stump_ranks(T, F, seeds, np.ascontiguousarray(const[b]), rk)
+        out[:, b, :] = rk
+    return torch.from_numpy(out).to(bins.device)
+
+
+def _stump_ranks(T, F, seeds, const, out):
+    from .. import ops
+    if ops.has_ext():
+        ops.ext().sklearn_stump_ranks(T, F, seeds.ctypes.data, const.ctypes.data, out.ctypes.data)
+        return
+    for t in range(T):
+        s = int(seeds[t]) & 0xFFFFFFFF
+        feats = list(range(F))
+        out[t] = F
+        f_i, n_found, n_total, visited, pos = F, 0, 0, 0, 0
+        while f_i > n_total and (visited < F or visited <= n_found):
+            visited += 1
+            if s == 0:
+                s = 1
+            s ^= (s << 13) & 0xFFFFFFFF
+            s ^= s >> 17
+            s ^= (s << 5) & 0xFFFFFFFF
+            f_j = (s % (RAND_R_MAX + 1)) % (f_i - n_found) + n_found
+            cur = feats[f_j]
+            if const[cur]:
+                feats[f_j], feats[n_total] = feats[n_total], cur
+                n_found += 1
+                n_total += 1
+                continue
+            f_i -= 1
+            feats[f_j], feats[f_i] = feats[f_i], cur
+            out[t, cur] = pos
+            pos += 1
+
+
 def _run_host(st: _State, group):
     K = _HostKernels
     st.node = st.node.to(torch.int64)
@@ -344,11 +420,21 @@ def _run_host(st: _State, group):
         prev = None
         if t > 0:
             prev = (st.feat[t - 1].to(torch.int64), st.blo[t - 1].to(torch.int64), st.value[t - 1])
+        snap = st.r2[t - 1].clone() if (group is not None and t > 0) else None
         K.apply_prep(st, prev, t)
+        if snap is not None:
+            # the previous tree's leaf Σw r² is a rank-local partial: reduce it with this stage's
+            # root slot in ONE collective (the device launch path does the same)
+            delta = st.r2[t - 1] - snap
+            red = torch.cat([st.r2[t], delta]) if t < st.T else delta
+            pdist_all_reduce(red, group)
+            st.r2[t - 1] = snap + red[-st.B:]
+            if t < st.T:
+                st.r2[t] = red[:st.B]
+        elif group is not None:
+            _allreduce_r2(st, t, group)
         if t == st.T:
             break
-        if group is not None:
-            _allreduce_r2(st, t, group)
         for level in range(st.D):
             node0, NL = 2 ** level - 1, 2 ** level
             H = K.hist(st, node0, NL)
@@ -357,9 +443,23 @@ def _run_host(st: _State, group):
                 pdist.all_reduce_sum_(H, group)
             K.split(st, H, node0, NL, level == st.D - 1, t)
             if level < st.D - 1:
+                snap = st.r2[t].clone() if group is not None else None
                 K.route(st, node0, NL, t)
                 if group is not None:
-                    _allreduce_r2(st, t, group)
+                    _reduce_delta(st.r2[t], snap, group)
+
+
+def pdist_all_reduce(t, group):
+    from ..parallel import dist as pdist
+    pdist.all_reduce_sum_(t, group)
+
+
+def _reduce_delta(buf, snap, group):
+    """``buf`` = global ``snap`` + this rank's new contributions → global: only the delta is
+    reduced (re-reducing ``buf`` would multiply its already-global entries by the world size)."""
+    delta = buf - snap
+    pdist_all_reduce(delta, group)
+    buf.copy_(snap + delta)
 
 
 def _allreduce_r2(st, t, group):
@@ -379,7 +479,7 @@ LAST_PATH = {"path": None}
 
 def _fused_ok(st: _State, group) -> bool:
     nbh = st.bm.nb_host
-    return (FUSED_STUMPS and group is None and st.D == 1 and st.F <= 128 and st.n <= FUSED_MAX_ROWS
+    return (FUSED_STUMPS and STUMP_PATH != "launch" and group is None and st.D == 1 and st.F <= 128 and st.n <= FUSED_MAX_ROWS
             and nbh is not None and 24 * int(nbh.sum()) <= _FUSED_LDS)
 
 
@@ -396,9 +496,57 @@ def _run_fused(st: _State):
         st.lr, st.qscale, st.dscale, st.min_leaf_q, st.min_split_q, ops.stream_ptr(st.raw.device))
 
 
+# Depth-1 trees (any row count, single process or data parallel): one gbdt_stump_stage launch per
+# boosting stage over (row tiles × models) workgroups + one int64 all-reduce per stage under DP.
+STUMP_PATH = os.environ.get("HFENS_GBDT_STUMPS", "stage")     # stage | fused | launch
+_STAGE_LDS = 150 * 1024
+COLLECTIVES = {"per_stage": None}
+
+
+def _stage_ok(st: _State) -> bool:
+    nbh = st.bm.nb_host
+    return (STUMP_PATH == "stage" and st.D == 1 and st.F <= 128 and nbh is not None
+            and (3 * int(nbh.sum()) + 3 * 1024) * 8 <= _STAGE_LDS)
+
+
+def _run_stage(st: _State, group):
+    from .. import ops, runtime
+    bm = st.bm
+    dev = st.raw.device
+    hist_len = int(bm.nb_host.sum())
+    slot = st.B * (3 * hist_len + 8)
+    comm = runtime.workspace(dev, "gbdt_stage_comm", 3 * slot, torch.int64)
+    comm.zero_()
+    E = ops.ext()
+    s = ops.stream_ptr(dev)
+    ptr = lambda x: x.data_ptr() if x is not None else 0   # noqa: E731
+    n_coll = 0
+    for t in range(st.T + 2):
+        E.gbdt_stump_stage(t, st.B, st.n, st.F, st.T, st.bins.data_ptr(), bm.nbins.data_ptr(), hist_len,
+                           bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
+                           st.raw.data_ptr(), ptr(st.wt), ptr(st.seeds), st.row_off, st.subsample,
+                           comm.data_ptr(), st.feat.data_ptr(), st.blo.data_ptr(), st.thr.data_ptr(),
+                           st.value.data_ptr(), st.stats.data_ptr(), st.r2.data_ptr(), st.dev.data_ptr(),
+                           ptr(st.bagw), ptr(st.frank), st.lr, st.qscale, st.dscale, st.min_leaf_q,
+                           st.min_split_q, s)
+        if group is not None and t <= st.T:
+            # stage t's histogram + root Σw r² + previous tree's leaf Σw r² + deviance + bag count:
+            # ONE exact int64 SUM per stage (SURVEY.md §5.8 R1/R2 merged)
+            k = t % 3
+            import torch.distributed as dist
+            dist.all_reduce(comm[k * slot:(k + 1) * slot], op=dist.ReduceOp.SUM, group=group)
+            n_coll += 1
+    COLLECTIVES["per_stage"] = n_coll / (st.T + 1) if group is not None else 0.0
+    st.reduced = True      # r2 / dev / bagw were booked from the all-reduced slots
+
+
 def _run_device(st: _State, group):
     from .. import ops
     from ..ops import stream_ptr
+    if _stage_ok(st):
+        LAST_PATH["path"] = "stage"
+        return _run_stage(st, group)
+    st.frank = None   # the fused / launch kernels break ties by the lowest feature index
     if _fused_ok(st, group):
         LAST_PATH["path"] = "fused"
         return _run_fused(st)
@@ -412,11 +560,16 @@ def _run_device(st: _State, group):
     wt_ptr = st.wt.data_ptr() if st.wt is not None else 0
     seeds_ptr = st.seeds.data_ptr() if st.seeds is not None else 0
     wcur = st.wcur
+    # under data parallelism the previous tree's leaf Σw r² (added by apply_prep) goes to a scratch
+    # that is reduced in the SAME collective as this stage's root slot, then booked
+    leafacc = torch.zeros(st.B, st.NN, dtype=torch.int64, device=st.raw.device) if group is not None else None
     for t in range(st.T + 1):
         if t > 0:
             pf, pb, pv = st.feat[t - 1], st.blo[t - 1], st.value[t - 1]
-            prev = (pf.data_ptr(), pb.data_ptr(), pv.data_ptr(), st.r2[t - 1].data_ptr(),
-                    st.dev[t - 1].data_ptr())
+            if leafacc is not None:
+                leafacc.zero_()
+            prev = (pf.data_ptr(), pb.data_ptr(), pv.data_ptr(),
+                    (leafacc if leafacc is not None else st.r2[t - 1]).data_ptr(), st.dev[t - 1].data_ptr())
         else:
             prev = (0, 0, 0, 0, 0)
         cur_r2 = st.r2[t] if t < st.T else scratch
@@ -424,12 +577,21 @@ def _run_device(st: _State, group):
                           st.raw.data_ptr(), st.g.data_ptr(), st.h.data_ptr(), st.node.data_ptr(),
                           prev[0], prev[1], prev[2], prev[3], prev[4], cur_r2.data_ptr(), st.lr,
                           st.qscale, st.dscale, wt_ptr, st.subsample, seeds_ptr, st.row_off, t, s)
+        if group is not None and t > 0:
+            if t < st.T:
+                red = torch.cat([st.r2[t], leafacc])
+                pdist_all_reduce(red, group)
+                st.r2[t].copy_(red[:st.B])
+                st.r2[t - 1] += red[st.B:]
+            else:
+                pdist_all_reduce(leafacc, group)
+                st.r2[t - 1] += leafacc
+        elif group is not None and t == 0:
+            _allreduce_r2(st, t, group)
         if t == st.T:
             break
         if st.bagw is not None:
             st.bagw[t] = st.wt.double().sum(1)
-        if group is not None:
-            _allreduce_r2(st, t, group)
         for level in range(st.D):
             node0, NL = 2 ** level - 1, 2 ** level
             Hl = H[: st.B * NL * st.F * 768]
@@ -446,15 +608,16 @@ def _run_device(st: _State, group):
                          st.thr[t].data_ptr(), st.value[t].data_ptr(), st.stats[t].data_ptr(),
                          st.r2[t].data_ptr(), s)
             if level < st.D - 1:
+                snap = st.r2[t].clone() if group is not None else None
                 E.gbdt_route(st.B, st.n, st.NN, st.bins.data_ptr(), st.g.data_ptr(), wcur.data_ptr(),
                              st.node.data_ptr(), st.feat[t].data_ptr(), st.blo[t].data_ptr(),
                              st.r2[t].data_ptr(), node0, NL, st.qscale, s)
                 if group is not None:
-                    _allreduce_r2(st, t, group)
+                    _reduce_delta(st.r2[t], snap, group)
 
 
 def _finish(models, st: _State, sw, p1, group):
-    if group is not None:
+    if group is not None and not st.reduced:
         from ..parallel import dist as pdist
         pdist.all_reduce_sum_(st.dev, group)
     inv = 1.0 / st.qscale
@@ -466,7 +629,8 @@ def _finish(models, st: _State, sw, p1, group):
     imp = torch.where(wsum > 0, imp, torch.zeros_like(imp))
     if st.bagw is not None:
         bagw = st.bagw
-        if group is not None:
+        if group is not None and not st.reduced:
+            from ..parallel import dist as pdist
             bagw = pdist.all_reduce_sum_f64([bagw], group)[0]
         train_score = (st.dev.double() / st.dscale) / bagw.clamp(min=1e-300)
     else:

@@ -842,4 +842,398 @@ void gbdt_stumps_fused(int B, int n, int F, int T, uintptr_t bins, uintptr_t nbi
   launch_check();
 }
 
+
+// ------------------------------------------------------------------------------------------
+// F: depth-1 trees, ONE launch per boosting stage over MANY workgroups (gbdt_stump_stage).
+//
+// The fused kernel above gives each model one workgroup for the whole run (6 CUs busy on the
+// bench) and cannot take a collective between stages.  Here launch t runs over a grid of
+// (row tiles × models) and does, per workgroup:
+//   1. the SPLIT of tree t−1 from the fully reduced stage-(t−1) histogram (every workgroup of the
+//      model computes the same split redundantly from the same integers — no grid sync; workgroup
+//      0 of the model writes the tree record and the previous stage's bookkeeping);
+//   2. APPLY of tree t−1 to its row tile (raw += lr·leaf, leaf Σw·r², stage deviance) and stage
+//      t's residual/hessian, quantised once into an LDS row cache;
+//   3. the stage-t HISTOGRAM of its tile (binary features 8 per register pass, ≤ 8-bin features in
+//      registers, wider ones with ds_add_u64), flushed with int64 atomics into comm slot t mod 3,
+//      plus the model's extras (root Σw·r², the previous tree's leaf Σw·r², deviance, bag count).
+// Slots rotate over 3 buffers: launch t reads slot t−1, accumulates slot t and zeroes slot t+1.
+// Between launches the host runs ONE all-reduce of slot t under data parallelism (histogram +
+// extras in one int64 SUM: exact, so every rank computes the identical split) — the whole stage
+// costs one launch and one collective.  Sums, split rule, thresholds and leaf values are the
+// fused kernel's (same fixed-point integers), so trees are bit-identical to it; the only
+// addition is an optional per-tree feature RANK for tie-breaks (sklearn's Fisher–Yates visit
+// order, computed on the host) instead of the lowest feature index.
+constexpr int kSgThreads = 512;
+constexpr int kSgWaves = kSgThreads / 64;
+constexpr int kSgTile = 1024;       // rows per workgroup (LDS row cache: 3 × 8 B per row)
+constexpr int kSgExtra = 8;         // int64 extras per model and slot
+
+struct StageJob {
+  const unsigned char* bins;          // [F][n]
+  const int* nbins;                   // [F]
+  const double* lo_val;               // [F][256]
+  const double* hi_val;               // [F][256]
+  const float* y;                     // [n]
+  const float* w;                     // [B][n]
+  double* raw;                        // [B][n]
+  float* wt;                          // [B][n] in-bag weights (bagging) or nullptr
+  const unsigned long long* seeds;    // [B] (bagging) or nullptr
+  long long* comm;                    // [3][B][3·hist_len + kSgExtra]
+  int* feat;                          // [T][B][3]
+  int* blo;                           // [T][B][3]
+  double* thr;                        // [T][B][3]
+  double* value;                      // [T][B][3]
+  long long* stats;                   // [T][B][3][4]
+  long long* r2;                      // [T][B][3]
+  long long* dev;                     // [T][B]
+  double* bagw;                       // [T][B] (bagging) or nullptr
+  const int* frank;                   // [T][B][F] tie-break rank of each feature, or nullptr
+  long long row_off;
+  double lr, qscale, dscale, min_leaf_q, min_split_q;
+  unsigned thr24;
+  int active, B, n, F, T, hist_len, t;
+};
+
+template <int NV>
+__device__ __forceinline__ void sg_block_sum(long long (&v)[NV], long long* red, long long* out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const long long s = wave_sum_i64(v[k]);
+    if (lane == 0) red[wave * 24 + k] = s;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NV) {
+    long long s = 0;
+    for (int k = 0; k < kSgWaves; ++k) s += red[k * 24 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+// ≤ C-bin feature over the tile from the quantised row cache: registers, one fold into LDS.
+template <int C>
+__device__ __forceinline__ void sg_hist_regs(const unsigned char* __restrict__ col, const long long* qg,
+                                             const long long* qh, const long long* qw, int m, int nb,
+                                             long long* out /*[nb][3] LDS*/, long long* red) {
+  long long ag[C], ah[C], aw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { ag[c] = 0; ah[c] = 0; aw[c] = 0; }
+  for (int i = threadIdx.x; i < m; i += kSgThreads) {
+    const long long w = qw[i];
+    if (w == 0) continue;
+    const int bb = col[i];
+    const long long g = qg[i], h = qh[i];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const bool k = bb == c;
+      ag[c] += k ? g : 0;
+      ah[c] += k ? h : 0;
+      aw[c] += k ? w : 0;
+    }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const long long a = wave_sum_i64(ag[c]), b2 = wave_sum_i64(ah[c]), c2 = wave_sum_i64(aw[c]);
+    if (lane == 0) {
+      red[wave * 24 + 3 * c] = a;
+      red[wave * 24 + 3 * c + 1] = b2;
+      red[wave * 24 + 3 * c + 2] = c2;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < 3 * nb) {
+    long long s = 0;
+    for (int k = 0; k < kSgWaves; ++k) s += red[k * 24 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J) {
+  extern __shared__ __attribute__((aligned(16))) long long sg_lds[];
+  long long* hl = sg_lds;                                   // [hist_len][3]
+  long long* qg = sg_lds + 3 * (size_t)J.hist_len;          // [kSgTile] quantised g, h, w
+  long long* qh = qg + kSgTile;
+  long long* qw = qh + kSgTile;
+  __shared__ long long red[kSgWaves * 24];
+  __shared__ int s_nb[kStMaxF], s_off[kStMaxF];
+  __shared__ int l_bin[kStMaxF], l_one[kStMaxF], l_mid[kStMaxF], l_wide[kStMaxF];
+  __shared__ int n_bin, n_one, n_mid, n_wide;
+  __shared__ long long tot[3], bsum[24], ext[8];
+  __shared__ double wg[kSgWaves];
+  __shared__ int wf[kSgWaves], wbin[kSgWaves], wrk[kSgWaves];
+  __shared__ int pf_s, pblo_s;
+  __shared__ double pv_s[3];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = J.n, F = J.F, B = J.B, t = J.t, T = J.T;
+  const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
+  const size_t slot_sz = (size_t)B * slot_m;
+  long long* slot_prev = J.comm + (size_t)((t + 2) % 3) * slot_sz + (size_t)b * slot_m;
+  long long* slot_cur = J.comm + (size_t)(t % 3) * slot_sz + (size_t)b * slot_m;
+  long long* slot_next = J.comm + (size_t)((t + 1) % 3) * slot_sz;
+  if (tid == 0) {
+    int o = 0;
+    n_bin = n_one = n_mid = n_wide = 0;
+    for (int f = 0; f < F; ++f) {
+      const int nb = J.nbins[f];
+      s_nb[f] = nb; s_off[f] = o; o += nb;
+      if (nb == 2) l_bin[n_bin++] = f;
+      else if (nb <= 1) l_one[n_one++] = f;
+      else if (nb <= 8) l_mid[n_mid++] = f;
+      else l_wide[n_wide++] = f;
+    }
+    pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0;
+  }
+  // zero the slot that launch t+1 accumulates (nobody reads or writes it during launch t)
+  {
+    const size_t nwg = (size_t)gridDim.x * gridDim.y, wid = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    for (size_t k = wid * kSgThreads + tid; k < slot_sz; k += nwg * kSgThreads) slot_next[k] = 0;
+  }
+  __syncthreads();
+  const bool lead = blockIdx.x == 0;
+  const double inv = 1.0 / J.qscale;
+  // ---- bookkeeping of the reduced previous slot (launch t−1's extras), by the model's leader
+  if (lead && tid == 0 && t >= 1) {
+    const long long* E = slot_prev + 3 * (size_t)J.hist_len;
+    if (t - 1 < T) {
+      const size_t tb = (size_t)(t - 1) * B + b;
+      J.r2[tb * 3] = E[0];
+      if (J.active) J.bagw[tb] = (double)E[5] * inv;
+    }
+    if (t - 2 >= 0 && t - 2 < T) {
+      const size_t pb = (size_t)(t - 2) * B + b;
+      J.r2[pb * 3] += E[1];
+      J.r2[pb * 3 + 1] += E[2];
+      J.r2[pb * 3 + 2] += E[3];
+      J.dev[pb] += E[4];
+    }
+  }
+  if (t > T) return;   // the closing launch only books the last slot
+  // ---- 1: split of tree t−1 from the reduced stage-(t−1) histogram
+  if (t >= 1) {
+    const long long* hp = slot_prev;
+    const long long root_r2 = slot_prev[3 * (size_t)J.hist_len];
+    if (wave == 0) {
+      long long a = 0, c = 0, d = 0;
+      for (int bb = lane; bb < s_nb[0]; bb += 64) { a += hp[bb * 3]; c += hp[bb * 3 + 1]; d += hp[bb * 3 + 2]; }
+      a = wave_sum_i64(a); c = wave_sum_i64(c); d = wave_sum_i64(d);
+      if (lane == 0) { tot[0] = a; tot[1] = c; tot[2] = d; }
+    }
+    __syncthreads();
+    const long long tg = tot[0], th = tot[1], tw = tot[2];
+    const size_t tb = (size_t)(t - 1) * B + b;
+    const int* rk = J.frank ? J.frank + tb * F : nullptr;
+    if (tw <= 0) {
+      if (tid == 0) {
+        if (lead) J.feat[tb * 3] = -3;
+        pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0;
+      }
+    } else {
+      double bg = -1.0;
+      int bf = 0x7fffffff, bbin = 0, brk = 0x7fffffff;
+      if ((double)tw >= J.min_split_q) {
+        for (int f = wave; f < F; f += kSgWaves) {
+          double gg;
+          int gb;
+          scan_feature(hp + (size_t)s_off[f] * 3, s_nb[f], lane, tw, tg, J.min_leaf_q, gg, gb);
+          const int r = rk ? rk[f] : f;
+          if (gg > bg || (gg == bg && gg >= 0.0 && r < brk)) { bg = gg; bf = f; bbin = gb; brk = r; }
+        }
+      }
+      if (lane == 0) { wg[wave] = bg; wf[wave] = bf; wbin[wave] = bbin; wrk[wave] = brk; }
+      __syncthreads();
+      if (tid == 0) {
+        bg = wg[0]; bf = wf[0]; bbin = wbin[0]; brk = wrk[0];
+        for (int k = 1; k < kSgWaves; ++k)
+          if (wg[k] > bg || (wg[k] == bg && wrk[k] < brk)) { bg = wg[k]; bf = wf[k]; bbin = wbin[k]; brk = wrk[k]; }
+        const double dw = tw * inv, dg = tg * inv;
+        const double imp = root_r2 * inv / dw - (dg / dw) * (dg / dw);
+        const bool can_split = bg >= 0.0 && bf < F && imp > 2.220446049250313e-16;
+        long long* st = J.stats + tb * 3 * 4;
+        if (lead) { st[0] = tw; st[1] = tg; st[2] = th; }
+        if (!can_split) {
+          const double den = th * inv;
+          const double v = fabs(den) < 1e-150 ? 0.0 : dg / den;
+          if (lead) { J.feat[tb * 3] = -2; J.blo[tb * 3] = 0; J.thr[tb * 3] = -2.0; J.value[tb * 3] = v; }
+          pf_s = -2; pblo_s = 0; pv_s[0] = v; pv_s[1] = 0.0; pv_s[2] = 0.0;
+        } else {
+          const long long* hf = hp + (size_t)s_off[bf] * 3;
+          long long lw = 0, lg = 0, lh = 0;
+          for (int bb = 0; bb <= bbin; ++bb) { lg += hf[bb * 3]; lh += hf[bb * 3 + 1]; lw += hf[bb * 3 + 2]; }
+          const double dl = lh * inv, dr = (th - lh) * inv;
+          const double vl = fabs(dl) < 1e-150 ? 0.0 : lg * inv / dl;
+          const double vr = fabs(dr) < 1e-150 ? 0.0 : (tg - lg) * inv / dr;
+          if (lead) {
+            int hi = bbin + 1;
+            const int nbf = s_nb[bf];
+            while (hi < nbf - 1 && hf[hi * 3 + 2] == 0) ++hi;
+            const double a = J.hi_val[bf * 256 + bbin], c = J.lo_val[bf * 256 + hi];
+            double tt = a / 2.0 + c / 2.0;
+            if (tt == c || isinf(tt)) tt = a;
+            J.feat[tb * 3] = bf; J.blo[tb * 3] = bbin; J.thr[tb * 3] = tt; J.value[tb * 3] = dg / dw;
+            long long* sl = st + 4;
+            long long* sr = st + 8;
+            sl[0] = lw; sl[1] = lg; sl[2] = lh;
+            sr[0] = tw - lw; sr[1] = tg - lg; sr[2] = th - lh;
+            J.feat[tb * 3 + 1] = -2; J.feat[tb * 3 + 2] = -2;
+            J.blo[tb * 3 + 1] = 0; J.blo[tb * 3 + 2] = 0;
+            J.thr[tb * 3 + 1] = -2.0; J.thr[tb * 3 + 2] = -2.0;
+            J.value[tb * 3 + 1] = vl; J.value[tb * 3 + 2] = vr;
+          }
+          pf_s = bf; pblo_s = bbin; pv_s[0] = dg / dw; pv_s[1] = vl; pv_s[2] = vr;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- 2: apply tree t−1 to the tile, stage t's residuals into the LDS row cache
+  const int r0 = blockIdx.x * kSgTile;
+  const int m = min(kSgTile, n - r0);
+  if (m <= 0) return;
+  const bool has_prev = t >= 1, has_cur = t < T;
+  const int pf = pf_s, pblo = pblo_s;
+  const double pv0 = pv_s[0], pv1 = pv_s[1], pv2 = pv_s[2];
+  long long acc6[6] = {0, 0, 0, 0, 0, 0};   // dev(t−1), r2 root(t), leaf r2 n0..n2 (t−1), bag(t)
+  for (int k = tid; k < m; k += kSgThreads) {
+    const int i = r0 + k;
+    const size_t bi = (size_t)b * n + i;
+    const float w0 = J.w[bi];
+    float wi = w0, wp = w0;
+    if (J.active) {
+      const unsigned long long sd = J.seeds[b];
+      wi = (has_cur && gb_in_bag(sd, t, J.row_off + i, J.thr24)) ? w0 : 0.f;
+      wp = (has_prev && gb_in_bag(sd, t - 1, J.row_off + i, J.thr24)) ? w0 : 0.f;
+      if (has_cur) J.wt[bi] = wi;
+    }
+    double rw = J.raw[bi];
+    const double yi = J.y[i];
+    if (has_prev) {
+      const int nd = pf >= 0 ? (J.bins[(size_t)pf * n + i] <= pblo ? 1 : 2) : 0;
+      if (wp > 0.f) {
+        const double p0 = 1.0 / (1.0 + exp(-rw));
+        const double r0d = yi - p0;
+        const long long q = q_of(wp * r0d * r0d, J.qscale);
+        acc6[2] += nd == 0 ? q : 0;
+        acc6[3] += nd == 1 ? q : 0;
+        acc6[4] += nd == 2 ? q : 0;
+      }
+      rw += J.lr * (nd == 0 ? pv0 : (nd == 1 ? pv1 : pv2));
+      J.raw[bi] = rw;
+      if (wp > 0.f) {
+        const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
+        acc6[0] += q_of(wp * (-2.0) * (yi * rw - l1p), J.dscale);
+      }
+    }
+    if (has_cur) {
+      const double p = 1.0 / (1.0 + exp(-rw));
+      const double r = yi - p;
+      const float gf = (float)(wi * r);
+      const float hf = (float)(wi * p * (1.0 - p));
+      const bool in = wi > 0.f;
+      qg[k] = in ? q_of(gf, J.qscale) : 0;
+      qh[k] = in ? q_of(hf, J.qscale) : 0;
+      qw[k] = in ? q_of(wi, J.qscale) : 0;
+      if (in) acc6[1] += q_of(wi * r * r, J.qscale);
+      if (J.active) acc6[5] += in ? q_of(wi, J.qscale) : 0;
+    }
+  }
+  sg_block_sum<6>(acc6, red, ext);
+  if (tid < 6) {
+    // extras layout: [0] root Σw r² (t), [1..3] leaf Σw r² (t−1), [4] deviance (t−1), [5] bag (t)
+    const int dst = tid == 0 ? 4 : (tid == 1 ? 0 : (tid <= 4 ? tid - 1 : 5));
+    if (ext[tid] != 0)
+      atomicAdd((unsigned long long*)&slot_cur[3 * (size_t)J.hist_len + dst], (unsigned long long)ext[tid]);
+  }
+  if (!has_cur) return;
+  // ---- 3: stage-t histogram of the tile (fused kernel's feature grouping)
+  for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) hl[k] = 0;
+  {
+    long long v[3] = {0, 0, 0};
+    for (int k = tid; k < m; k += kSgThreads) { v[0] += qg[k]; v[1] += qh[k]; v[2] += qw[k]; }
+    sg_block_sum<3>(v, red, tot);
+  }
+  const unsigned char* bt = J.bins + r0;
+  for (int b0 = 0; b0 < n_bin; b0 += 8) {
+    const int nf = min(8, n_bin - b0);
+    long long acc[24];
+#pragma unroll
+    for (int k = 0; k < 24; ++k) acc[k] = 0;
+    for (int k = tid; k < m; k += kSgThreads) {
+      const long long w = qw[k];
+      if (w == 0) continue;
+      const long long g = qg[k], h = qh[k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u < nf && bt[(size_t)l_bin[b0 + u] * n + k]) {
+          acc[3 * u] += g;
+          acc[3 * u + 1] += h;
+          acc[3 * u + 2] += w;
+        }
+      }
+    }
+    sg_block_sum<24>(acc, red, bsum);
+    if (tid < 3 * nf) {
+      const int u = tid / 3, k = tid - 3 * u;
+      const int off = s_off[l_bin[b0 + u]];
+      hl[(off + 1) * 3 + k] = bsum[tid];
+      hl[off * 3 + k] = tot[k] - bsum[tid];
+    }
+  }
+  for (int u = tid; u < 3 * n_one; u += kSgThreads) hl[s_off[l_one[u / 3]] * 3 + u % 3] = tot[u % 3];
+  for (int u = 0; u < n_mid; ++u) {
+    const int f = l_mid[u], nb = s_nb[f];
+    const unsigned char* col = bt + (size_t)f * n;
+    long long* out = hl + (size_t)s_off[f] * 3;
+    if (nb <= 4) sg_hist_regs<4>(col, qg, qh, qw, m, nb, out, red);
+    else sg_hist_regs<8>(col, qg, qh, qw, m, nb, out, red);
+  }
+  if (n_wide > 0) {
+    for (int k = tid; k < m; k += kSgThreads) {
+      const long long w = qw[k];
+      if (w == 0) continue;
+      const long long g = qg[k], h = qh[k];
+      for (int u = 0; u < n_wide; ++u) {
+        const int f = l_wide[u];
+        long long* cell = hl + ((size_t)s_off[f] + bt[(size_t)f * n + k]) * 3;
+        atomicAdd((unsigned long long*)&cell[0], (unsigned long long)g);
+        atomicAdd((unsigned long long*)&cell[1], (unsigned long long)h);
+        atomicAdd((unsigned long long*)&cell[2], (unsigned long long)w);
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) {
+    const long long v = hl[k];
+    if (v != 0) atomicAdd((unsigned long long*)&slot_cur[k], (unsigned long long)v);
+  }
+}
+
+size_t gbdt_stump_stage_lds(int hist_len) { return (3 * (size_t)hist_len + 3 * kSgTile) * sizeof(long long); }
+
+void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, uintptr_t nbins, int hist_len,
+                      uintptr_t lo_val, uintptr_t hi_val, uintptr_t y, uintptr_t w, uintptr_t raw, uintptr_t wt,
+                      uintptr_t seeds, long long row_off, double subsample, uintptr_t comm, uintptr_t feat,
+                      uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t dev,
+                      uintptr_t bagw, uintptr_t frank, double lr, double qscale, double dscale,
+                      double min_leaf_q, double min_split_q, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stump_stage: 1 <= F <= 128");
+  HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
+  const bool active = subsample < 1.0;
+  HFENS_REQUIRE(!active || (wt != 0 && seeds != 0 && bagw != 0), "gbdt_stump_stage: subsample needs wt, seeds, bagw");
+  const size_t lds = gbdt_stump_stage_lds(hist_len);
+  HFENS_REQUIRE(hist_len >= F && lds <= 150 * 1024, "gbdt_stump_stage: histogram + row cache exceed LDS");
+  StageJob J{(const unsigned char*)bins, (const int*)nbins, (const double*)lo_val, (const double*)hi_val,
+             (const float*)y, (const float*)w, (double*)raw, (float*)wt, (const unsigned long long*)seeds,
+             (long long*)comm, (int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
+             (long long*)r2, (long long*)dev, (double*)bagw, (const int*)frank, row_off, lr, qscale, dscale,
+             min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
+             hist_len, t};
+  const int tiles = (n + kSgTile - 1) / kSgTile;
+  hipLaunchKernelGGL(gbdt_stump_stage_kernel, dim3(tiles, B), dim3(kSgThreads), lds, as_stream(stream), J);
+  launch_check();
+}
+
 }  // namespace hfens

@@ -122,8 +122,8 @@ def _gbdt(rank, world, group):
     ms = [GradientBoostingClassifier(n_estimators=15, max_depth=2) for _ in range(2)]
     fit_gbdt_batch(ms, shard_rows(X, rank, world), shard_rows(y, rank, world),
                    shard_rows(masks.t(), rank, world).t().contiguous(), group=group)
-    return [(m.tree_feature_.clone(), m.tree_threshold_.clone(), m.tree_value_.clone(), m.train_score_.clone())
-            for m in ms]
+    return [(m.tree_feature_.clone(), m.tree_threshold_.clone(), m.tree_value_.clone(), m.train_score_.clone(),
+             m.tree_impurity_.clone()) for m in ms]
 
 
 def _gbdt_sub(rank, world, group):
@@ -195,11 +195,12 @@ def test_gbdt_dp_bit_identical(world):
     masks[0, ::4] = False
     ms = [GradientBoostingClassifier(n_estimators=15, max_depth=2) for _ in range(2)]
     fit_gbdt_batch(ms, X, y, masks)
-    for (f, t, v, ts), m in zip(got, ms):
+    for (f, t, v, ts, imp), m in zip(got, ms):
         assert torch.equal(f, m.tree_feature_)
         assert torch.equal(t, m.tree_threshold_)
         assert torch.equal(v, m.tree_value_)
         assert torch.equal(ts, m.train_score_)
+        assert torch.equal(imp, m.tree_impurity_)   # leaf impurities are global sums too
 
 
 def test_gbdt_subsample_dp_bit_identical():

@@ -124,26 +124,104 @@ def test_gbdt_subsample_device_matches_host(dev):
 
 
 @pytest.mark.parametrize("subsample", [1.0, 0.7])
-def test_gbdt_stumps_fused_matches_launch_path(dev, monkeypatch, subsample):
-    """gbdt_stumps_fused (the whole boosting run in one launch) reproduces the launch-per-step
-    device path bit for bit: features, thresholds, leaf values, impurities, train_score_."""
+def test_gbdt_stump_paths_bit_identical(dev, monkeypatch, subsample):
+    """The three depth-1 device paths — launch-per-step, gbdt_stumps_fused (one launch, one
+    workgroup per model) and gbdt_stump_stage (one launch per stage over row tiles × models) —
+    produce the same trees bit for bit: features, thresholds, leaf values, impurities,
+    node weights, train_score_."""
     from hfens.models import hist_gbdt
+    monkeypatch.setattr(hist_gbdt, "SKLEARN_TIES", False)
     X, y = _data(6000, 17, 51)
     masks = torch.ones(6, 6000, dtype=torch.bool)
     for k in range(5):
         masks[k, k::5] = False
     out = {}
-    for fused in (False, True):
-        monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", fused)
+    for path in ("launch", "fused", "stage"):
+        monkeypatch.setattr(hist_gbdt, "STUMP_PATH", path)
+        monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", path == "fused")
         ms = [GradientBoostingClassifier(n_estimators=60, max_depth=1, subsample=subsample, random_state=s)
               for s in range(6)]
         fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
-        assert hist_gbdt.LAST_PATH["path"] == ("fused" if fused else "launch")
-        out[fused] = ms
-    for a, b in zip(out[False], out[True]):
-        for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
-                     "tree_weighted_n_node_samples_", "train_score_"):
-            assert torch.equal(getattr(a, attr), getattr(b, attr)), attr
+        assert hist_gbdt.LAST_PATH["path"] == path
+        out[path] = ms
+    for other in ("fused", "stage"):
+        for a, b in zip(out["launch"], out[other]):
+            for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
+                         "tree_weighted_n_node_samples_", "train_score_"):
+                assert torch.equal(getattr(a, attr), getattr(b, attr)), (other, attr)
+
+
+@pytest.mark.parametrize("rows", [2500, 70000])
+def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
+    """gbdt_stump_stage with sklearn's feature-visit tie-break (duplicated columns force exact
+    gain ties) equals the host mirror, which visits features in the same order; large row counts
+    spread each model over many workgroups."""
+    from hfens.models import hist_gbdt
+    X, y = _data(rows, 12, 52)
+    X[:, 6] = X[:, 3] + 1.0
+    X[:, 9] = 2.0 * X[:, 2]
+    mh = [GradientBoostingClassifier(n_estimators=40, max_depth=1, random_state=s) for s in (2020, 7)]
+    md = [GradientBoostingClassifier(n_estimators=40, max_depth=1, random_state=s) for s in (2020, 7)]
+    fit_gbdt_batch(mh, X, y)
+    fit_gbdt_batch(md, X.to(dev), y.to(dev))
+    assert hist_gbdt.LAST_PATH["path"] == "stage"
+    for a, b in zip(mh, md):
+        assert torch.equal(a.tree_feature_, b.tree_feature_.cpu())
+        assert torch.equal(a.tree_threshold_, b.tree_threshold_.cpu())
+        assert torch.allclose(a.tree_value_, b.tree_value_.cpu(), rtol=1e-12, atol=1e-15)
+        assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-12)
+
+
+def _dp_stage_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from hfens.models import hist_gbdt
+    from hfens.parallel.dist import shard_rows
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        X, y = _data(9000, 17, 53)
+        ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+        fit_gbdt_batch(ms, shard_rows(X, rank, world).to(dev), shard_rows(y, rank, world).to(dev),
+                       group=dist.group.WORLD)
+        if rank == 0:
+            q.put((hist_gbdt.LAST_PATH["path"], hist_gbdt.COLLECTIVES["per_stage"],
+                   [(m.tree_feature_.cpu().numpy(), m.tree_threshold_.cpu().numpy(), m.tree_value_.cpu().numpy(),
+                     m.tree_impurity_.cpu().numpy(), m.train_score_.cpu().numpy()) for m in ms]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gbdt_stage_data_parallel_bit_identical(dev):
+    """Two ranks on the card (gloo carries the int64 all-reduce of device tensors): the sharded
+    stage path issues exactly ONE collective per boosting stage and reproduces the single-process
+    fit bit for bit, impurities included."""
+    import socket
+    import torch.multiprocessing as mp
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_stage_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    path, per_stage, got = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert path == "stage" and per_stage == 1.0
+    X, y = _data(9000, 17, 53)
+    ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ms, X.to(dev), y.to(dev))
+    for (f, t, v, imp, ts), m in zip(got, ms):
+        assert np.array_equal(f, m.tree_feature_.cpu().numpy())
+        assert np.array_equal(t, m.tree_threshold_.cpu().numpy())
+        assert np.array_equal(v, m.tree_value_.cpu().numpy())
+        assert np.array_equal(imp, m.tree_impurity_.cpu().numpy())
+        assert np.array_equal(ts, m.train_score_.cpu().numpy())
 
 
 def test_binned_stump_tables_match_tree_walk(dev):
