@@ -501,12 +501,14 @@ def _run_fused(st: _State):
 STUMP_PATH = os.environ.get("HFENS_GBDT_STUMPS", "stage")     # stage | fused | launch
 _STAGE_LDS = 150 * 1024
 COLLECTIVES = {"per_stage": None}
+PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage whose s_memtime stamps to keep
+LAST_STAGE_PROF: dict = {}
 
 
 def _stage_ok(st: _State) -> bool:
     nbh = st.bm.nb_host
     return (STUMP_PATH == "stage" and st.D == 1 and st.F <= 128 and nbh is not None
-            and (3 * int(nbh.sum()) + 3 * 1024) * 8 <= _STAGE_LDS)
+            and (3 * int(nbh.sum()) + 3 * 1088) * 8 <= _STAGE_LDS)
 
 
 def _run_stage(st: _State, group):
@@ -520,15 +522,32 @@ def _run_stage(st: _State, group):
     E = ops.ext()
     s = ops.stream_ptr(dev)
     ptr = lambda x: x.data_ptr() if x is not None else 0   # noqa: E731
+    # bins padded to a 1024-multiple row stride: every lane reads 16 rows of a feature with ONE
+    # 16-byte load (pad bins are 0, their rows carry no weight)
+    ldb = -(-st.n // 1024) * 1024
+    if ldb == st.n and st.bins.data_ptr() % 16 == 0:
+        binsp = st.bins
+    else:
+        binsp = runtime.workspace(dev, "gbdt_stage_bins", st.F * ldb, torch.uint8).view(st.F, ldb)
+        binsp[:, st.n:].zero_()
+        binsp[:, :st.n].copy_(st.bins)
+    # per-workgroup partial slots (the kernel reduces them in a second small launch when a model
+    # spans more than 16 workgroups; sized for ≤ 2 workgroups per CU per model)
+    from .smo import _num_cus
+    groups = min(-(-st.n // 1024), 2 * _num_cus(dev))
+    plen = st.B * groups * (3 * hist_len + 8)
+    partials = runtime.workspace(dev, "gbdt_stage_partials", plen, torch.int64)
+    prof = torch.zeros(st.B * groups * 6, dtype=torch.int64, device=dev) if PROFILE_STAGE_T >= 0 else None
     n_coll = 0
     for t in range(st.T + 2):
-        E.gbdt_stump_stage(t, st.B, st.n, st.F, st.T, st.bins.data_ptr(), bm.nbins.data_ptr(), hist_len,
+        E.gbdt_stump_stage(t, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
                            bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
                            st.raw.data_ptr(), ptr(st.wt), ptr(st.seeds), st.row_off, st.subsample,
                            comm.data_ptr(), st.feat.data_ptr(), st.blo.data_ptr(), st.thr.data_ptr(),
                            st.value.data_ptr(), st.stats.data_ptr(), st.r2.data_ptr(), st.dev.data_ptr(),
-                           ptr(st.bagw), ptr(st.frank), st.lr, st.qscale, st.dscale, st.min_leaf_q,
-                           st.min_split_q, s)
+                           ptr(st.bagw), ptr(st.frank), partials.data_ptr(), plen, st.lr, st.qscale,
+                           st.dscale, st.min_leaf_q,
+                           st.min_split_q, ptr(prof) if (prof is not None and t == PROFILE_STAGE_T) else 0, s)
         if group is not None and t <= st.T:
             # stage t's histogram + root Σw r² + previous tree's leaf Σw r² + deviance + bag count:
             # ONE exact int64 SUM per stage (SURVEY.md §5.8 R1/R2 merged)
@@ -537,6 +556,8 @@ def _run_stage(st: _State, group):
             dist.all_reduce(comm[k * slot:(k + 1) * slot], op=dist.ReduceOp.SUM, group=group)
             n_coll += 1
     COLLECTIVES["per_stage"] = n_coll / (st.T + 1) if group is not None else 0.0
+    if prof is not None:
+        LAST_STAGE_PROF["stamps"] = prof.view(-1, 6).cpu().numpy()
     st.reduced = True      # r2 / dev / bagw were booked from the all-reduced slots
 
 

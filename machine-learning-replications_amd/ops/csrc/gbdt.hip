@@ -868,6 +868,8 @@ constexpr int kSgThreads = 512;
 constexpr int kSgWaves = kSgThreads / 64;
 constexpr int kSgTile = 1024;       // rows per workgroup (LDS row cache: 3 × 8 B per row)
 constexpr int kSgExtra = 8;         // int64 extras per model and slot
+constexpr int kSgRowPad = kSgTile + kSgTile / 16;   // padded row-cache length
+__device__ __forceinline__ int sg_ri(int r) { return r + (r >> 4); }
 
 struct StageJob {
   const unsigned char* bins;          // [F][n]
@@ -892,7 +894,10 @@ struct StageJob {
   long long row_off;
   double lr, qscale, dscale, min_leaf_q, min_split_q;
   unsigned thr24;
-  int active, B, n, F, T, hist_len, t;
+  int active, B, n, F, T, hist_len, t, rows_per_wg;
+  long long ldb;                      // row stride of bins (≥ n, multiple of 1024: 16-byte lane loads)
+  long long* partials;                // [B][G][3·hist_len + kSgExtra] per-workgroup slots, or nullptr
+  long long* prof;                    // diagnostics: [B][G][6] s_memtime phase stamps, or nullptr
 };
 
 template <int NV>
@@ -947,7 +952,7 @@ __device__ __forceinline__ void sg_hist_regs(const unsigned char* __restrict__ c
   if ((int)threadIdx.x < 3 * nb) {
     long long s = 0;
     for (int k = 0; k < kSgWaves; ++k) s += red[k * 24 + threadIdx.x];
-    out[threadIdx.x] = s;
+    out[threadIdx.x] += s;
   }
   __syncthreads();
 }
@@ -955,9 +960,11 @@ __device__ __forceinline__ void sg_hist_regs(const unsigned char* __restrict__ c
 __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J) {
   extern __shared__ __attribute__((aligned(16))) long long sg_lds[];
   long long* hl = sg_lds;                                   // [hist_len][3]
-  long long* qg = sg_lds + 3 * (size_t)J.hist_len;          // [kSgTile] quantised g, h, w
-  long long* qh = qg + kSgTile;
-  long long* qw = qh + kSgTile;
+  // row cache: quantised g, h, w of 1024 rows, row r at r + r/16 (one pad word per 16 rows: lane ℓ
+  // reading row 16ℓ + j then strides 17 words — conflict-free — instead of 16, a 32-way conflict)
+  long long* qg = sg_lds + 3 * (size_t)J.hist_len;
+  long long* qh = qg + kSgRowPad;
+  long long* qw = qh + kSgRowPad;
   __shared__ long long red[kSgWaves * 24];
   __shared__ int s_nb[kStMaxF], s_off[kStMaxF];
   __shared__ int l_bin[kStMaxF], l_one[kStMaxF], l_mid[kStMaxF], l_wide[kStMaxF];
@@ -995,6 +1002,8 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   __syncthreads();
   const bool lead = blockIdx.x == 0;
   const double inv = 1.0 / J.qscale;
+  long long* pst = J.prof ? J.prof + ((size_t)b * gridDim.x + blockIdx.x) * 6 : nullptr;
+  const long long t_0 = pst ? (long long)__builtin_amdgcn_s_memtime() : 0;
   // ---- bookkeeping of the reduced previous slot (launch t−1's extras), by the model's leader
   if (lead && tid == 0 && t >= 1) {
     const long long* E = slot_prev + 3 * (size_t)J.hist_len;
@@ -1049,9 +1058,26 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
         bg = wg[0]; bf = wf[0]; bbin = wbin[0]; brk = wrk[0];
         for (int k = 1; k < kSgWaves; ++k)
           if (wg[k] > bg || (wg[k] == bg && wrk[k] < brk)) { bg = wg[k]; bf = wf[k]; bbin = wbin[k]; brk = wrk[k]; }
-        const double dw = tw * inv, dg = tg * inv;
-        const double imp = root_r2 * inv / dw - (dg / dw) * (dg / dw);
-        const bool can_split = bg >= 0.0 && bf < F && imp > 2.220446049250313e-16;
+        wg[0] = bg; wf[0] = bf; wbin[0] = bbin;
+      }
+      __syncthreads();
+      bg = wg[0]; bf = wf[0]; bbin = wbin[0];
+      const double dw = tw * inv, dg = tg * inv;
+      const double imp = root_r2 * inv / dw - (dg / dw) * (dg / dw);
+      const bool can_split = bg >= 0.0 && bf < F && imp > 2.220446049250313e-16;
+      if (can_split && wave == 0) {
+        // the chosen bin's left sums: one parallel pass of wave 0 (a serial loop over up to 256
+        // bins × 3 global loads by one thread cost more than the rest of the split)
+        const long long* hf = hp + (size_t)s_off[bf] * 3;
+        long long lw = 0, lg = 0, lh = 0;
+        for (int bb = lane; bb <= bbin; bb += 64) { lg += hf[bb * 3]; lh += hf[bb * 3 + 1]; lw += hf[bb * 3 + 2]; }
+        lg = wave_sum_i64(lg);
+        lh = wave_sum_i64(lh);
+        lw = wave_sum_i64(lw);
+        if (lane == 0) { tot[0] = lg; tot[1] = lh; tot[2] = lw; }
+      }
+      __syncthreads();
+      if (tid == 0) {
         long long* st = J.stats + tb * 3 * 4;
         if (lead) { st[0] = tw; st[1] = tg; st[2] = th; }
         if (!can_split) {
@@ -1061,8 +1087,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
           pf_s = -2; pblo_s = 0; pv_s[0] = v; pv_s[1] = 0.0; pv_s[2] = 0.0;
         } else {
           const long long* hf = hp + (size_t)s_off[bf] * 3;
-          long long lw = 0, lg = 0, lh = 0;
-          for (int bb = 0; bb <= bbin; ++bb) { lg += hf[bb * 3]; lh += hf[bb * 3 + 1]; lw += hf[bb * 3 + 2]; }
+          const long long lg = tot[0], lh = tot[1], lw = tot[2];
           const double dl = lh * inv, dr = (th - lh) * inv;
           const double vl = fabs(dl) < 1e-150 ? 0.0 : lg * inv / dl;
           const double vr = fabs(dr) < 1e-150 ? 0.0 : (tg - lg) * inv / dr;
@@ -1089,136 +1114,199 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     }
     __syncthreads();
   }
-  // ---- 2: apply tree t−1 to the tile, stage t's residuals into the LDS row cache
-  const int r0 = blockIdx.x * kSgTile;
-  const int m = min(kSgTile, n - r0);
-  if (m <= 0) return;
+  if (pst && tid == 0) pst[0] = (long long)__builtin_amdgcn_s_memtime() - t_0;
+  // ---- 2+3 over this workgroup's rows, 1024 at a time: apply tree t−1, stage t's residuals into
+  // the LDS row cache, the stage-t histogram accumulated in LDS across sub-tiles (flushed once)
   const bool has_prev = t >= 1, has_cur = t < T;
   const int pf = pf_s, pblo = pblo_s;
   const double pv0 = pv_s[0], pv1 = pv_s[1], pv2 = pv_s[2];
   long long acc6[6] = {0, 0, 0, 0, 0, 0};   // dev(t−1), r2 root(t), leaf r2 n0..n2 (t−1), bag(t)
-  for (int k = tid; k < m; k += kSgThreads) {
-    const int i = r0 + k;
-    const size_t bi = (size_t)b * n + i;
-    const float w0 = J.w[bi];
-    float wi = w0, wp = w0;
-    if (J.active) {
-      const unsigned long long sd = J.seeds[b];
-      wi = (has_cur && gb_in_bag(sd, t, J.row_off + i, J.thr24)) ? w0 : 0.f;
-      wp = (has_prev && gb_in_bag(sd, t - 1, J.row_off + i, J.thr24)) ? w0 : 0.f;
-      if (has_cur) J.wt[bi] = wi;
-    }
-    double rw = J.raw[bi];
-    const double yi = J.y[i];
-    if (has_prev) {
-      const int nd = pf >= 0 ? (J.bins[(size_t)pf * n + i] <= pblo ? 1 : 2) : 0;
-      if (wp > 0.f) {
-        const double p0 = 1.0 / (1.0 + exp(-rw));
-        const double r0d = yi - p0;
-        const long long q = q_of(wp * r0d * r0d, J.qscale);
-        acc6[2] += nd == 0 ? q : 0;
-        acc6[3] += nd == 1 ? q : 0;
-        acc6[4] += nd == 2 ? q : 0;
-      }
-      rw += J.lr * (nd == 0 ? pv0 : (nd == 1 ? pv1 : pv2));
-      J.raw[bi] = rw;
-      if (wp > 0.f) {
-        const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
-        acc6[0] += q_of(wp * (-2.0) * (yi * rw - l1p), J.dscale);
-      }
-    }
-    if (has_cur) {
-      const double p = 1.0 / (1.0 + exp(-rw));
-      const double r = yi - p;
-      const float gf = (float)(wi * r);
-      const float hf = (float)(wi * p * (1.0 - p));
-      const bool in = wi > 0.f;
-      qg[k] = in ? q_of(gf, J.qscale) : 0;
-      qh[k] = in ? q_of(hf, J.qscale) : 0;
-      qw[k] = in ? q_of(wi, J.qscale) : 0;
-      if (in) acc6[1] += q_of(wi * r * r, J.qscale);
-      if (J.active) acc6[5] += in ? q_of(wi, J.qscale) : 0;
-    }
-  }
-  sg_block_sum<6>(acc6, red, ext);
-  if (tid < 6) {
-    // extras layout: [0] root Σw r² (t), [1..3] leaf Σw r² (t−1), [4] deviance (t−1), [5] bag (t)
-    const int dst = tid == 0 ? 4 : (tid == 1 ? 0 : (tid <= 4 ? tid - 1 : 5));
-    if (ext[tid] != 0)
-      atomicAdd((unsigned long long*)&slot_cur[3 * (size_t)J.hist_len + dst], (unsigned long long)ext[tid]);
-  }
-  if (!has_cur) return;
-  // ---- 3: stage-t histogram of the tile (fused kernel's feature grouping)
-  for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) hl[k] = 0;
-  {
-    long long v[3] = {0, 0, 0};
-    for (int k = tid; k < m; k += kSgThreads) { v[0] += qg[k]; v[1] += qh[k]; v[2] += qw[k]; }
-    sg_block_sum<3>(v, red, tot);
-  }
-  const unsigned char* bt = J.bins + r0;
-  for (int b0 = 0; b0 < n_bin; b0 += 8) {
-    const int nf = min(8, n_bin - b0);
-    long long acc[24];
-#pragma unroll
-    for (int k = 0; k < 24; ++k) acc[k] = 0;
+  if (has_cur)
+    for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) hl[k] = 0;
+  const int w0r = blockIdx.x * J.rows_per_wg;
+  const int w1r = min(n, w0r + J.rows_per_wg);
+  for (int r0 = w0r; r0 < w1r; r0 += kSgTile) {
+    const int m = min(kSgTile, w1r - r0);
+    __syncthreads();   // the previous sub-tile's histogram passes are done with the row cache
     for (int k = tid; k < m; k += kSgThreads) {
-      const long long w = qw[k];
-      if (w == 0) continue;
-      const long long g = qg[k], h = qh[k];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (u < nf && bt[(size_t)l_bin[b0 + u] * n + k]) {
-          acc[3 * u] += g;
-          acc[3 * u + 1] += h;
-          acc[3 * u + 2] += w;
+      const int i = r0 + k;
+      const size_t bi = (size_t)b * n + i;
+      const float w0 = J.w[bi];
+      float wi = w0, wp = w0;
+      if (J.active) {
+        const unsigned long long sd = J.seeds[b];
+        wi = (has_cur && gb_in_bag(sd, t, J.row_off + i, J.thr24)) ? w0 : 0.f;
+        wp = (has_prev && gb_in_bag(sd, t - 1, J.row_off + i, J.thr24)) ? w0 : 0.f;
+        if (has_cur) J.wt[bi] = wi;
+      }
+      double rw = J.raw[bi];
+      const double yi = J.y[i];
+      if (has_prev) {
+        const int nd = pf >= 0 ? (J.bins[(size_t)pf * J.ldb + i] <= pblo ? 1 : 2) : 0;
+        if (wp > 0.f) {
+          const double p0 = 1.0 / (1.0 + exp(-rw));
+          const double r0d = yi - p0;
+          const long long q = q_of(wp * r0d * r0d, J.qscale);
+          acc6[2] += nd == 0 ? q : 0;
+          acc6[3] += nd == 1 ? q : 0;
+          acc6[4] += nd == 2 ? q : 0;
+        }
+        rw += J.lr * (nd == 0 ? pv0 : (nd == 1 ? pv1 : pv2));
+        J.raw[bi] = rw;
+        if (wp > 0.f) {
+          const double l1p = rw > 0 ? rw + log1p(exp(-rw)) : log1p(exp(rw));
+          acc6[0] += q_of(wp * (-2.0) * (yi * rw - l1p), J.dscale);
         }
       }
-    }
-    sg_block_sum<24>(acc, red, bsum);
-    if (tid < 3 * nf) {
-      const int u = tid / 3, k = tid - 3 * u;
-      const int off = s_off[l_bin[b0 + u]];
-      hl[(off + 1) * 3 + k] = bsum[tid];
-      hl[off * 3 + k] = tot[k] - bsum[tid];
-    }
-  }
-  for (int u = tid; u < 3 * n_one; u += kSgThreads) hl[s_off[l_one[u / 3]] * 3 + u % 3] = tot[u % 3];
-  for (int u = 0; u < n_mid; ++u) {
-    const int f = l_mid[u], nb = s_nb[f];
-    const unsigned char* col = bt + (size_t)f * n;
-    long long* out = hl + (size_t)s_off[f] * 3;
-    if (nb <= 4) sg_hist_regs<4>(col, qg, qh, qw, m, nb, out, red);
-    else sg_hist_regs<8>(col, qg, qh, qw, m, nb, out, red);
-  }
-  if (n_wide > 0) {
-    for (int k = tid; k < m; k += kSgThreads) {
-      const long long w = qw[k];
-      if (w == 0) continue;
-      const long long g = qg[k], h = qh[k];
-      for (int u = 0; u < n_wide; ++u) {
-        const int f = l_wide[u];
-        long long* cell = hl + ((size_t)s_off[f] + bt[(size_t)f * n + k]) * 3;
-        atomicAdd((unsigned long long*)&cell[0], (unsigned long long)g);
-        atomicAdd((unsigned long long*)&cell[1], (unsigned long long)h);
-        atomicAdd((unsigned long long*)&cell[2], (unsigned long long)w);
+      if (has_cur) {
+        const double p = 1.0 / (1.0 + exp(-rw));
+        const double r = yi - p;
+        const float gf = (float)(wi * r);
+        const float hf = (float)(wi * p * (1.0 - p));
+        const bool in = wi > 0.f;
+        qg[sg_ri(k)] = in ? q_of(gf, J.qscale) : 0;
+        qh[sg_ri(k)] = in ? q_of(hf, J.qscale) : 0;
+        qw[sg_ri(k)] = in ? q_of(wi, J.qscale) : 0;
+        if (in) acc6[1] += q_of(wi * r * r, J.qscale);
+        if (J.active) acc6[5] += in ? q_of(wi, J.qscale) : 0;
       }
     }
+    if (!has_cur) continue;
+    for (int k = m + tid; k < kSgTile; k += kSgThreads) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
+    __syncthreads();
+    if (pst && tid == 0 && r0 == w0r) pst[1] = (long long)__builtin_amdgcn_s_memtime() - t_0;
+    // stage-t histogram of the sub-tile.  Every wave covers ALL 1024 rows (lane ℓ owns rows
+    // 16ℓ … 16ℓ+15, their quantised g/h/w in registers) and takes features f ≡ wave (mod 8): one
+    // 16-byte load per lane and feature, sums in registers, wave reductions, lane 0 adds the
+    // feature's bins into the LDS histogram (features are disjoint across waves: no barrier).
+    long long rg[16], rh[16], rv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int ri = 17 * lane + j;   // sg_ri(16·lane + j)
+      rg[j] = qg[ri]; rh[j] = qh[ri]; rv[j] = qw[ri];
+    }
+    long long tg3 = 0, th3 = 0, tw3 = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { tg3 += rg[j]; th3 += rh[j]; tw3 += rv[j]; }
+    tg3 = wave_sum_i64(tg3);
+    th3 = wave_sum_i64(th3);
+    tw3 = wave_sum_i64(tw3);
+    const unsigned char* bt = J.bins + r0 + 16 * lane;
+    // this wave's features in groups of 4: the group's four 16-byte tiles are loaded together
+    for (int fg = wave; fg < F; fg += 4 * kSgWaves) {
+      uint4 pre[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int f = fg + u * kSgWaves;
+        pre[u] = f < F ? *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+      const int f = fg + u * kSgWaves;
+      if (f >= F) break;
+      const int nb = s_nb[f], off = s_off[f];
+      const uint4 v4 = pre[u];
+      const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
+      if (nb <= 1) {
+        if (lane == 0) { hl[off * 3] += tg3; hl[off * 3 + 1] += th3; hl[off * 3 + 2] += tw3; }
+      } else if (nb == 2) {
+        long long a = 0, c = 0, d = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const bool one = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          a += one ? rg[j] : 0;
+          c += one ? rh[j] : 0;
+          d += one ? rv[j] : 0;
+        }
+        a = wave_sum_i64(a);
+        c = wave_sum_i64(c);
+        d = wave_sum_i64(d);
+        if (lane == 0) {
+          hl[(off + 1) * 3] += a; hl[(off + 1) * 3 + 1] += c; hl[(off + 1) * 3 + 2] += d;
+          hl[off * 3] += tg3 - a; hl[off * 3 + 1] += th3 - c; hl[off * 3 + 2] += tw3 - d;
+        }
+      } else if (nb <= 8) {
+        long long acc[24];
+#pragma unroll
+        for (int k = 0; k < 24; ++k) acc[k] = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const bool hit = bb == (unsigned)c;
+            acc[3 * c] += hit ? rg[j] : 0;
+            acc[3 * c + 1] += hit ? rh[j] : 0;
+            acc[3 * c + 2] += hit ? rv[j] : 0;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 24; ++k) {
+          if (k < 3 * nb) {
+            const long long sv = wave_sum_i64(acc[k]);
+            if (lane == 0) hl[off * 3 + k] += sv;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (rv[j] == 0) continue;
+          const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          long long* cell = hl + ((size_t)off + bb) * 3;
+          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)rg[j]);
+          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)rh[j]);
+          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)rv[j]);
+        }
+      }
+      }
+    }
+  }
+  if (pst && tid == 0) pst[2] = (long long)__builtin_amdgcn_s_memtime() - t_0;
+  sg_block_sum<6>(acc6, red, ext);
+  // publish: with many workgroups per model, plain stores of the whole partial slot (reduced by
+  // gbdt_stage_reduce_kernel — hundreds of workgroups' int64 atomics on the same ~50 KB of
+  // histogram serialise at the memory side); with few, atomics straight into the slot
+  long long* part = J.partials ? J.partials + ((size_t)b * gridDim.x + blockIdx.x) * slot_m : nullptr;
+  if (tid < kSgExtra) {
+    // extras layout: [0] root Σw r² (t), [1..3] leaf Σw r² (t−1), [4] deviance (t−1), [5] bag (t)
+    const int src = tid == 4 ? 0 : (tid == 0 ? 1 : (tid <= 3 ? tid + 1 : (tid == 5 ? 5 : -1)));
+    const long long v = src >= 0 ? ext[src] : 0;
+    if (part) part[3 * (size_t)J.hist_len + tid] = v;
+    else if (v != 0) atomicAdd((unsigned long long*)&slot_cur[3 * (size_t)J.hist_len + tid], (unsigned long long)v);
   }
   __syncthreads();
   for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) {
-    const long long v = hl[k];
-    if (v != 0) atomicAdd((unsigned long long*)&slot_cur[k], (unsigned long long)v);
+    const long long v = has_cur ? hl[k] : 0;
+    if (part) part[k] = v;
+    else if (v != 0) atomicAdd((unsigned long long*)&slot_cur[k], (unsigned long long)v);
   }
+  if (pst && tid == 0) pst[3] = (long long)__builtin_amdgcn_s_memtime() - t_0;
 }
 
-size_t gbdt_stump_stage_lds(int hist_len) { return (3 * (size_t)hist_len + 3 * kSgTile) * sizeof(long long); }
+// Sum of the per-workgroup partial slots into the stage's comm slot: grid (slot chunks, G splits, B)
+constexpr int kRdSplit = 16;
+__global__ __launch_bounds__(256) void gbdt_stage_reduce_kernel(const long long* __restrict__ partials,
+                                                                long long* __restrict__ slot, int G,
+                                                                long long slot_m) {
+  const int b = blockIdx.z;
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= slot_m) return;
+  const int g0 = blockIdx.y * G / kRdSplit, g1 = (blockIdx.y + 1) * G / kRdSplit;
+  const long long* p = partials + ((size_t)b * G) * slot_m + k;
+  long long s = 0;
+  for (int g = g0; g < g1; ++g) s += p[(size_t)g * slot_m];
+  if (s != 0) atomicAdd((unsigned long long*)&slot[(size_t)b * slot_m + k], (unsigned long long)s);
+}
 
-void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, uintptr_t nbins, int hist_len,
+size_t gbdt_stump_stage_lds(int hist_len) { return (3 * (size_t)hist_len + 3 * kSgRowPad) * sizeof(long long); }
+
+void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long long ldb, uintptr_t nbins, int hist_len,
                       uintptr_t lo_val, uintptr_t hi_val, uintptr_t y, uintptr_t w, uintptr_t raw, uintptr_t wt,
                       uintptr_t seeds, long long row_off, double subsample, uintptr_t comm, uintptr_t feat,
                       uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t dev,
-                      uintptr_t bagw, uintptr_t frank, double lr, double qscale, double dscale,
-                      double min_leaf_q, double min_split_q, uintptr_t stream) {
+                      uintptr_t bagw, uintptr_t frank, uintptr_t partials, long long partials_len, double lr,
+                      double qscale, double dscale, double min_leaf_q, double min_split_q, uintptr_t prof,
+                      uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stump_stage: 1 <= F <= 128");
   HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
   const bool active = subsample < 1.0;
@@ -1230,10 +1318,29 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, uintptr
              (long long*)comm, (int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
              (long long*)r2, (long long*)dev, (double*)bagw, (const int*)frank, row_off, lr, qscale, dscale,
              min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
-             hist_len, t};
-  const int tiles = (n + kSgTile - 1) / kSgTile;
-  hipLaunchKernelGGL(gbdt_stump_stage_kernel, dim3(tiles, B), dim3(kSgThreads), lds, as_stream(stream), J);
+             hist_len, t, 0, ldb, (long long*)partials, (long long*)prof};
+  HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");
+  // rows per workgroup: 1024-row sub-tiles, as many per workgroup as keeps the grid near 2
+  // workgroups per CU (the redundant split and the histogram flush are per workgroup)
+  int dev_id = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev_id));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id));
+  const long long tiles = (n + kSgTile - 1) / kSgTile;
+  const long long want = (2LL * ncu + B - 1) / B;                  // workgroups per model
+  const long long per = (tiles + want - 1) / want;                 // sub-tiles per workgroup
+  J.rows_per_wg = (int)(per * kSgTile);
+  const int groups = (int)((n + J.rows_per_wg - 1) / J.rows_per_wg);
+  const long long slot_m = 3LL * hist_len + kSgExtra;
+  if (groups <= kRdSplit || partials == 0) J.partials = nullptr;
+  else HFENS_REQUIRE(partials_len >= (long long)B * groups * slot_m, "gbdt_stump_stage: partials buffer too small");
+  hipLaunchKernelGGL(gbdt_stump_stage_kernel, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   launch_check();
+  if (J.partials != nullptr && t <= T) {
+    long long* slot = (long long*)comm + (size_t)(t % 3) * B * slot_m;
+    hipLaunchKernelGGL(gbdt_stage_reduce_kernel, dim3((unsigned)((slot_m + 255) / 256), kRdSplit, B), dim3(256), 0,
+                       as_stream(stream), (const long long*)J.partials, slot, groups, slot_m);
+    launch_check();
+  }
 }
 
 }  // namespace hfens
