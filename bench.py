@@ -265,10 +265,32 @@ def bench_gbdt(a):
         raw = torch.stack([m.decision_function(Xh) for m in ms])
         t_inf = float("nan")
     score = torch.sigmoid(raw.double()).mean(0)
+    # fp8 leaf values on the matrix cores (BASELINE config 5): the same ensemble as a leaf one-hot ×
+    # two-term e4m3 leaf-value GEMV (ops/csrc/forest_fp8.hip), timed, with its AUROC delta
+    fp8 = None
+    if dev.type == "cuda" and seeds <= 8:
+        from hfens.models.forest_infer import Fp8Forest
+        f8 = Fp8Forest(ms)
+        raw8 = f8.raw(bins_h)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        for _ in range(5):
+            raw8 = f8.raw(bins_h)
+        torch.cuda.synchronize(dev)
+        t_f8 = (time.perf_counter() - t2) / 5
+        score8 = torch.sigmoid(raw8.double()).mean(0)
+        fp8 = dict(score=score8, t=t_f8, max_raw_err=float((raw8.double() - raw.double()).abs().max()))
+    yh_local = yh
     if group is not None:
         score = pdist.all_gather_rows(score[:, None], group)[:, 0]
         yh = pdist.all_gather_rows(yh[:, None].to(score.dtype), group)[:, 0]
     auc = metrics.roc_auc(yh.double(), score)
+    if fp8 is not None:
+        s8 = fp8["score"]
+        if group is not None:
+            s8 = pdist.all_gather_rows(s8[:, None], group)[:, 0]
+        fp8["auroc"] = metrics.roc_auc(yh.double(), s8)
+    del yh_local
     value = rows * seeds * a.steps / elapsed
     if rank == 0:
         base = CPU_BASELINE_DEEP_ROWS_SEEDS_PER_S if deep else CPU_BASELINE_GBDT_ROWS_PER_S
@@ -277,10 +299,18 @@ def bench_gbdt(a):
             "value": round(value, 1), "unit": "rows*seeds/s" if deep else "rows/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1000 * elapsed / a.steps, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": round(value / base, 2), "dtype": "fp32",
+            "scaling": "strong", "vs_baseline": round(value / base, 2),
+            "dtype": "fp8" if (deep and fp8 is not None) else "fp32",
+            "train_dtype": "fp32 gradients, int64 fixed-point histograms, f64 leaf values",
             "data": "synthetic Table S1-shaped cohort (device generator), no NaN",
             "auroc": round(float(auc), 4),
             "infer_rows_x_models_per_sec": round(n_hold * seeds / max(t_inf, 1e-12), 1) if t_inf == t_inf else None,
+            "fp8_leaf_inference": None if fp8 is None else {
+                "leaf_dtype": "fp8 e4m3 two-term (hi + lo), per-model power-of-two scale",
+                "kernel": "forest_fp8: leaf one-hot x fp8 leaf values, v_mfma_f32_16x16x32_fp8_fp8",
+                "auroc": round(float(fp8["auroc"]), 5), "auroc_fp32_tables": round(float(auc), 5),
+                "auroc_delta": round(float(fp8["auroc"] - auc), 6), "max_abs_raw_err": fp8["max_raw_err"],
+                "rows_x_models_per_sec": round(n_hold * seeds / max(fp8["t"], 1e-12), 1)},
             "config": {"model": f"hist GBDT {trees} trees depth {a.depth} x {seeds} seeds, subsample {a.subsample}",
                        "global_batch": rows, "seq_len": a.features, "parallelism": f"dp{world}"},
         }), flush=True)

@@ -50,6 +50,23 @@ class BinMapper:
         return idx.to(torch.uint8)
 
 
+def _threshold_edges(lo: torch.Tensor, hi: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """Upper bin edges AT the split thresholds the trees use (gbdt.hip: t = hi[b]/2 + lo[b+1]/2,
+    t == lo[b+1] → hi[b]; sklearn's midpoint rule), so ``bin(x) ≤ blo ⟺ x ≤ threshold`` for ANY x —
+    binned inference (folded tables, the fp8 MFMA forest) then equals threshold inference on new
+    data, not only on the training values.  Training values bin identically either way."""
+    k = int(lo.numel())
+    e = up.to(torch.float32).clone()
+    if k >= 2:
+        a, c = hi[:-1].double(), lo[1:].double()
+        t = a / 2.0 + c / 2.0
+        t = torch.where((t == c) | torch.isinf(t), a, t)
+        t32 = t.to(torch.float32)
+        t32 = torch.where(t32.double() >= c, a.to(torch.float32), t32)
+        e[:-1] = t32
+    return e
+
+
 def _pad_edges(uppers: List[torch.Tensor], device) -> torch.Tensor:
     K = max(int(u.numel()) for u in uppers)
     E = torch.full((len(uppers), K), float("inf"), dtype=torch.float32)
@@ -105,7 +122,7 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
             lo[f, :g] = u[starts].double()
             hi[f, :g] = u[ends].double()
             up = u[ends].clone()
-        ups.append(up.to(torch.float32))
+        ups.append(_threshold_edges(lo[f, :int(nb[f])], hi[f, :int(nb[f])], up))
     edges = _pad_edges(ups, dev)
     uppers = [edges[f, :ups[f].numel()] for f in range(F)]
     return BinMapper(nb.to(dev), lo.to(dev), hi.to(dev), uppers, max_bins, nb_host=nb.numpy().copy(),

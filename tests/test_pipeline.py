@@ -98,3 +98,27 @@ def test_save_plots_png_and_svg_fallback(tmp_path, monkeypatch):
     monkeypatch.setattr(builtins, "__import__", no_mpl)
     roc, pr = metrics.save_plots(y, p, str(tmp_path / "b"))
     assert roc.endswith(".svg") and "<polyline" in open(roc).read() and "AP =" in open(pr).read()
+
+
+def test_binned_inference_equals_threshold_inference_on_new_rows():
+    """Bins are cut at the trees' split thresholds: binned (folded-table / fp8-forest) inference
+    on rows the model never saw equals the threshold walk — exactly for f64 tables, to the fp8
+    two-term quantisation for the MFMA forest's operands."""
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models.forest_infer import Fp8Forest, ensemble_raw_binned, stump_bin_tables
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    X, y, _ = make_hf_cohort(1500, 12, seed=71, nan_frac=0.0)
+    Xn, _, _ = make_hf_cohort(700, 12, seed=72, nan_frac=0.0)
+    X, y, Xn = torch.as_tensor(X), torch.as_tensor(y), torch.as_tensor(Xn)
+    ms = [GradientBoostingClassifier(n_estimators=50, max_depth=1, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ms, X, y)
+    bins = ms[0]._bin_mapper.transform(Xn)
+    T, init = stump_bin_tables(ms)
+    raw = ensemble_raw_binned(T, init, bins)
+    for b, m in enumerate(ms):
+        assert torch.allclose(raw[b], m.decision_function(Xn), atol=1e-9)
+    m3 = [GradientBoostingClassifier(n_estimators=30, max_depth=3, random_state=3)]
+    fit_gbdt_batch(m3, X, y)
+    r8 = Fp8Forest(m3).reference_raw(m3[0]._bin_mapper.transform(Xn))
+    assert float((r8[0] - m3[0].decision_function(Xn)).abs().max()) < 5e-3
