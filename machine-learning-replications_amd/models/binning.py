@@ -42,12 +42,90 @@ class BinMapper:
     def transform(self, X: torch.Tensor) -> torch.Tensor:
         """``X [n, F]`` → feature-major uint8 bins ``[F, n]`` (one batched searchsorted: a value
         above every real edge lands on the first +inf pad = the edge count, then clamps to the
-        last bin exactly as a per-feature search would)."""
+        last bin exactly as a per-feature search would).  On the GPU: the ``quantize_bins`` kernel
+        (edge table in LDS, row-major input read once, feature-major output)."""
+        if X.is_cuda and X.dim() == 2 and X.shape[1] <= 128:
+            from .. import ops
+            Xc = X.contiguous() if X.dtype in (torch.float32, torch.float64) else X.to(torch.float32).contiguous()
+            edges = (self.edges if self.edges is not None else _pad_edges(self.uppers, X.device)).to(X.device)
+            edges = edges.contiguous()
+            n, F = Xc.shape
+            out = torch.empty(F, n, dtype=torch.uint8, device=X.device)
+            ops.ext().quantize_bins(Xc.data_ptr(), int(Xc.dtype == torch.float64), n, F, edges.data_ptr(),
+                                    int(edges.shape[1]), self.nbins.to(X.device).contiguous().data_ptr(),
+                                    out.data_ptr(), n, ops.stream_ptr(X.device))
+            return out
         X32 = X.to(torch.float32).t().contiguous()
         edges = self.edges if self.edges is not None else _pad_edges(self.uppers, X.device)
         idx = torch.searchsorted(edges.to(X32.device), X32)
         idx = torch.minimum(idx, (self.nbins.to(device=idx.device, dtype=idx.dtype) - 1)[:, None])
         return idx.to(torch.uint8)
+
+
+def _fit_bins_device(X32: torch.Tensor, max_bins: int) -> BinMapper:
+    """All features at once on the device: one segmented sort of [F, n], run starts, distinct
+    counts, the ≤ max_bins distinct values or the quantile group ends (hi = the value of rank
+    ⌈i·n/max_bins⌉, lo of the next group = the next distinct value), then ONE device→host copy of
+    the [F, max_bins] tables.  Same bins as the per-feature path (run-rank ⇔ cumulative count)."""
+    n, F = X32.shape
+    dev = X32.device
+    Xt = X32.t().contiguous()
+    srt = torch.empty_like(Xt)                                           # [F, n]
+    for f in range(F):   # F one-dimensional radix sorts beat one segmented [F, n] sort (measured)
+        srt[f] = torch.sort(Xt[f])[0]
+    new = torch.ones_like(srt, dtype=torch.bool)
+    new[:, 1:] = srt[:, 1:] != srt[:, :-1]
+    k_h = new.sum(1).cpu()                                               # one sync: distinct counts
+    small_f = [f for f in range(F) if int(k_h[f]) <= max_bins]
+    big_f = [f for f in range(F) if int(k_h[f]) > max_bins]
+    small_h = torch.full((F, max_bins), float("nan"), dtype=torch.float32)
+    if small_f:
+        vals = [srt[f][new[f]] for f in small_f]                          # ≤ max_bins each
+        packed = torch.full((len(small_f), max_bins), float("nan"), dtype=torch.float32, device=dev)
+        for i_, v in enumerate(vals):
+            packed[i_, :v.numel()] = v
+        small_h[small_f] = packed.cpu()
+    hi_h = torch.zeros(F, max_bins, dtype=torch.float32)
+    lo_h = torch.zeros(F, max_bins, dtype=torch.float32)
+    mn_h = srt[:, 0].cpu()
+    if big_f:
+        bi = torch.as_tensor(big_f, device=dev)
+        sb = srt.index_select(0, bi)
+        tau = torch.arange(1, max_bins, dtype=torch.float64, device=dev) * (n / max_bins)
+        idx = torch.cat([torch.ceil(tau).to(torch.int64) - 1, torch.tensor([n - 1], device=dev)]).clamp(0, n - 1)
+        hq = sb[:, idx].contiguous()                                     # quantile group ends
+        pos = torch.searchsorted(sb, hq, right=True).clamp(max=n - 1)
+        hi_h[big_f] = hq.cpu()
+        lo_h[big_f] = sb.gather(1, pos).cpu()                           # next distinct values
+    nb = torch.empty(F, dtype=torch.int32)
+    lo = torch.zeros(F, 256, dtype=torch.float64)
+    hi = torch.zeros(F, 256, dtype=torch.float64)
+    ups = []
+    for f in range(F):
+        kf = int(k_h[f])
+        if kf <= max_bins:
+            u = small_h[f, :kf]
+            nb[f] = kf
+            lo[f, :kf] = u.double()
+            hi[f, :kf] = u.double()
+            up = u.clone()
+        else:
+            h = hi_h[f]
+            keep = torch.ones(max_bins, dtype=torch.bool)
+            keep[1:] = h[1:] != h[:-1]
+            ends = h[keep]
+            nxt = lo_h[f][keep]
+            g = int(ends.numel())
+            nb[f] = g
+            hi[f, :g] = ends.double()
+            lo[f, 0] = float(mn_h[f])
+            lo[f, 1:g] = nxt[:-1].double()
+            up = ends.clone()
+        ups.append(_threshold_edges(lo[f, :int(nb[f])], hi[f, :int(nb[f])], up))
+    edges = _pad_edges(ups, dev)
+    uppers = [edges[f, :ups[f].numel()] for f in range(F)]
+    return BinMapper(nb.to(dev), lo.to(dev), hi.to(dev), uppers, max_bins, nb_host=nb.numpy().copy(),
+                     edges=edges)
 
 
 def _threshold_edges(lo: torch.Tensor, hi: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
@@ -90,6 +168,8 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
     dev = X.device
     X32 = X.to(torch.float32)
     host = group is None and n <= HOST_BIN_MAX_ROWS
+    if group is None and not host and X32.is_cuda:
+        return _fit_bins_device(X32, max_bins)
     Xh = X32.cpu().numpy() if host else None
     nb = torch.empty(F, dtype=torch.int32)
     lo = torch.zeros(F, 256, dtype=torch.float64)

@@ -69,4 +69,57 @@ void binned_stump_raw(uintptr_t bins, long long n, int F, uintptr_t tables, int 
   launch_check();
 }
 
+// ------------------------------------------------------------------------------------------
+// K7 quantize_bins: rows [n][F] (f64 or f32, row-major as the pipeline holds them) → feature-major
+// u8 bins [F][ldb] against the per-feature +inf-padded edge table (bin = first edge ≥ float32(x),
+// clamped to the feature's bin count — torch.searchsorted's left rule).  The edge table sits in
+// LDS; each thread bins one row over all features (binary search, ≤ 8 probes), and the stores of
+// one feature by consecutive threads are consecutive bytes.
+template <typename T>
+__global__ __launch_bounds__(256) void quantize_bins_kernel(const T* __restrict__ X, long long n, int F,
+                                                            const float* __restrict__ edges, int K,
+                                                            const int* __restrict__ nbins,
+                                                            unsigned char* __restrict__ out, long long ldb) {
+  extern __shared__ float qe[];   // [F][K]
+  __shared__ int qnb[128];
+  for (int i = threadIdx.x; i < F * K; i += blockDim.x) qe[i] = edges[i];
+  for (int i = threadIdx.x; i < F; i += blockDim.x) qnb[i] = nbins[i];
+  __syncthreads();
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
+    const T* xr = X + (size_t)r * F;
+    for (int f = 0; f < F; ++f) {
+      const float x = (float)xr[f];
+      const float* e = qe + f * K;
+      int lo = 0, hi = K;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (e[mid] < x) lo = mid + 1;
+        else hi = mid;
+      }
+      const int b = lo < qnb[f] - 1 ? lo : qnb[f] - 1;
+      out[(size_t)f * ldb + r] = (unsigned char)b;
+    }
+  }
+}
+
+void quantize_bins(uintptr_t X, int f64, long long n, int F, uintptr_t edges, int K, uintptr_t nbins, uintptr_t out,
+                   long long ldb, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 128 && K >= 1 && K <= 256, "quantize_bins: F <= 128 features, K <= 256 edges");
+  HFENS_REQUIRE(ldb >= n, "quantize_bins: ldb < n");
+  if (n == 0) return;
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  long long g = (n + 255) / 256;
+  if (g > 8LL * ncu) g = 8LL * ncu;
+  const size_t lds = (size_t)F * K * sizeof(float);
+  if (f64)
+    hipLaunchKernelGGL(quantize_bins_kernel<double>, dim3((unsigned)g), dim3(256), lds, as_stream(stream),
+                       (const double*)X, n, F, (const float*)edges, K, (const int*)nbins, (unsigned char*)out, ldb);
+  else
+    hipLaunchKernelGGL(quantize_bins_kernel<float>, dim3((unsigned)g), dim3(256), lds, as_stream(stream),
+                       (const float*)X, n, F, (const float*)edges, K, (const int*)nbins, (unsigned char*)out, ldb);
+  launch_check();
+}
+
 }  // namespace hfens

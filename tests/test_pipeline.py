@@ -122,3 +122,20 @@ def test_binned_inference_equals_threshold_inference_on_new_rows():
     fit_gbdt_batch(m3, X, y)
     r8 = Fp8Forest(m3).reference_raw(m3[0]._bin_mapper.transform(Xn))
     assert float((r8[0] - m3[0].decision_function(Xn)).abs().max()) < 5e-3
+
+
+def test_batched_bin_fit_matches_per_feature():
+    """K7: the one-sort batched bin fit (device path) equals the per-feature distinct/quantile fit."""
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import binning
+    X, _, _ = make_hf_cohort(5000, 20, seed=81, nan_frac=0.0)
+    X = torch.as_tensor(X)
+    X[:, 0] = torch.round(X[:, 0] * 3)          # few distinct values
+    X32 = X.to(torch.float32)
+    a = binning._fit_bins_device(X32, 256)
+    b = binning.fit_bins(X, 256)
+    assert torch.equal(a.nbins.cpu(), b.nbins.cpu())
+    assert torch.equal(a.lo_val.cpu(), b.lo_val.cpu())
+    assert torch.equal(a.hi_val.cpu(), b.hi_val.cpu())
+    assert torch.equal(a.edges.cpu(), b.edges.cpu())
+    assert int(a.nbins.max()) == 256 and int(a.nbins.min()) <= 8

@@ -274,3 +274,20 @@ def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_, otf):
         # Platt's Newton fit stops at |∇| < 1e-5, so rounding-level decision values move A, B by ~1e-6
         assert a._probA.item() == pytest.approx(b._probA.item(), rel=1e-4)
         assert a._probB.item() == pytest.approx(b._probB.item(), rel=1e-4, abs=1e-5)
+
+
+def test_quantize_bins_kernel_matches_searchsorted(dev):
+    """K7 quantize_bins (LDS edge table, binary search) = torch.searchsorted on the same edges,
+    for f64 and f32 rows, values on and between edges, above the last edge."""
+    from hfens.models.binning import fit_bins
+    X, _ = _data(70000, 30, 91)
+    X[:, 3] = torch.round(X[:, 3] * 2)
+    bm = fit_bins(X.to(dev), 256)
+    Xn, _ = _data(5000, 30, 92)
+    Xn[:7, :] = 1e9
+    for Z in (Xn.to(dev), Xn.to(dev).float()):
+        got = bm.transform(Z)
+        X32 = Z.to(torch.float32).t().contiguous()
+        ref = torch.searchsorted(bm.edges, X32)
+        ref = torch.minimum(ref, (bm.nbins.to(ref.dtype) - 1)[:, None]).to(torch.uint8)
+        assert torch.equal(got, ref)
