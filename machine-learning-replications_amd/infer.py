@@ -14,7 +14,8 @@ The whole stack runs as ONE fused HIP kernel per chunk (:func:`hfens.ops.stack_i
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Tuple
+from collections import OrderedDict
+from typing import Optional, Tuple
 
 import torch
 
@@ -33,7 +34,9 @@ class BatchedPredictor:
             raise ValueError("model is not an HF-shaped stack (scaler+SVC, GBC, LR -> LR)")
         self.chunk = int(chunk_rows)
         self.use_graph = use_graph
-        self._graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self._graphs: "OrderedDict[Tuple, Tuple[torch.cuda.CUDAGraph, torch.Tensor]]" = OrderedDict()
+
+    MAX_GRAPHS = 4   # captured (input, size, dtype, output) combinations kept, least recently used evicted
 
     @property
     def n_features(self) -> int:
@@ -56,11 +59,15 @@ class BatchedPredictor:
             out = out if out is not None else torch.empty(n, dtype=torch.float32, device=X.device)
             self._launch_all(X, out)
             return out[:n]
+        # a captured graph replays on fixed pointers: keyed by (input, size, dtype, output); with no
+        # ``out`` the graph writes a buffer of its own and the caller gets a COPY (a later call would
+        # overwrite a returned view); pass ``out`` to skip the copy
         key = (X.data_ptr(), n, X.dtype, None if out is None else out.data_ptr())
         hit = self._graphs.get(key)
         if hit is None:
             buf = out if out is not None else torch.empty(n, dtype=torch.float32, device=X.device)
-            side = torch.cuda.Stream(X.device)
+            from . import runtime
+            side = runtime.stream(X.device, "infer_warmup")
             side.wait_stream(torch.cuda.current_stream(X.device))
             with torch.cuda.stream(side):      # warm-up launch outside capture
                 self._launch_all(X, buf)
@@ -69,9 +76,13 @@ class BatchedPredictor:
             with torch.cuda.graph(g):
                 self._launch_all(X, buf)
             hit = self._graphs[key] = (g, buf)
+            while len(self._graphs) > self.MAX_GRAPHS:
+                self._graphs.popitem(last=False)
+        else:
+            self._graphs.move_to_end(key)
         g, buf = hit
         g.replay()
-        return buf[:n]
+        return buf[:n] if out is not None else buf[:n].clone()
 
     # ------------------------------------------------------------------ host streaming
     def predict_host(self, X_host: torch.Tensor, out_host: Optional[torch.Tensor] = None,

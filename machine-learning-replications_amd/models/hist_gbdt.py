@@ -277,6 +277,8 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     if not 0.0 < subsample <= 1.0:
         raise ValueError("subsample must be in (0, 1]")
     from ..utils.guards import check_binary, check_finite
+    from ..utils.timing import hmark
+    hmark("gbc_start")
     check_finite(X, "GradientBoostingClassifier.fit X")
     check_binary(y, "GradientBoostingClassifier.fit y")
     dev = X.device
@@ -295,6 +297,7 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         bins = bm.transform(X).contiguous()
     else:
         bm, bins = binned
+    hmark("gbc_binned")
     n_total = n
     if group is not None:
         from ..parallel import dist as pdist
@@ -334,10 +337,12 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     if D == 1 and SKLEARN_TIES and subsample == 1.0 and all(
             isinstance(m.random_state, (int, np.integer)) for m in models):
         st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group)
+    hmark("gbc_ranks")
     if X.is_cuda:
         _run_device(st, group)
     else:
         _run_host(st, group)
+    hmark("gbc_enqueued")
     check_finite(st.value, "GBDT leaf values")
     _finish(models, st, sw, p1, group)
     return models

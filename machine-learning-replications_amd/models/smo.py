@@ -430,6 +430,8 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     K = runtime.workspace(device, "svm_gram", koff, torch.float32)   # process-lifetime, grown only
     gdev = _dev_struct(g, device)
     E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
+    from ..utils.timing import hmark
+    hmark("svc_gram_launched")
     alpha = torch.empty(aoffs[-1], dtype=torch.float64, device=device)
     rho = torch.empty(len(live), dtype=torch.float64, device=device)
     iters = torch.empty(len(live), dtype=torch.int32, device=device)
@@ -571,6 +573,8 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     live = [p for p in probs if p.rows is not None]
     F = Zs[0].shape[1]
     zcat = _gather_rows(Zs, live, "rows", device)
+    from ..utils.timing import hmark
+    hmark("svc_gather")
     zoffs, aoffs = [], [0]
     for p in live:
         zoffs.append(aoffs[-1])
@@ -712,6 +716,8 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     for f, (Z, y) in enumerate(zip(Zs, ys)):
         check_finite(Z, f"SVC.fit X (fit {f})")
         check_binary(y, f"SVC.fit y (fit {f})")
+    from ..utils.timing import hmark
+    hmark("svc_checks")
     device = Zs[0].device
     cuda = Zs[0].is_cuda
     # one host read for every fit's labels and one for the 'scale' gamma statistics; the problem
@@ -721,6 +727,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     need_var = [svc.gamma == "scale" for svc in svcs]
     var = (torch.stack([Z.to(torch.float64).var(unbiased=False) for Z in Zs]).cpu().numpy()
            if any(need_var) else None)
+    hmark("svc_y_var_host")
     all_probs, meta = [], []
     off = 0
     for f, (svc, Z) in enumerate(zip(svcs, Zs)):
@@ -739,10 +746,12 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         pr, mt = _expand(f, y_np, gamma, cw, svc)
         all_probs += pr
         meta.append(mt)
+    hmark("svc_expand")
     eps = float(svcs[0].tol)
     args = (svcs, Zs, ys, max_iter_cap, group)
     sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
            else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
+    hmark("svc_solve_enqueued")
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
     AB = [None] * len(svcs)
     decs, labs, pl = [], [], []

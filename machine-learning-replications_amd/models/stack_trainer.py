@@ -148,26 +148,28 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     other.wait_stream(main)
     out, pending = {}, {}
     import time as _t
+    from ..utils.timing import hmark, hmarks_flush
     marks = [("start", _t.perf_counter())]
+    hmark("fit_bases")
     with timer.stage("fit_bases(svc || gbc+lr)"):
         # every collective is issued from this thread in the same order on every rank:
         # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
         with torch.cuda.stream(side):
             for i in svc_cols:
                 clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group)
-                marks.append(("svc_inputs", _t.perf_counter()))
+                hmark("svc_inputs")
                 if group is None:
                     pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group))
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
-                marks.append(("svc_launched", _t.perf_counter()))
+                hmark("svc_launched")
         with torch.cuda.stream(other):
             for i, (name, est) in enumerate(clf.estimators):
                 if i not in svc_cols:
                     out[i] = fit_base_batch(est, X, y, masks, group=group)
                     if oof is not None:
                         oof(i, out[i])
-                    marks.append((f"{name}_host_done", _t.perf_counter()))
+                    hmark(f"{name}_host_done")
         with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
                 if group is None:
@@ -177,12 +179,10 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                 out[i] = clones
                 if oof is not None:
                     oof(i, clones)
-        marks.append(("svc_finished", _t.perf_counter()))
+        hmark("svc_finished")
         main.wait_stream(side)
         main.wait_stream(other)
-    if _TRACE_HOST:
-        import sys as _s
-        print("[host] " + " ".join(f"{k}={1e3 * (v - marks[0][1]):.1f}" for k, v in marks[1:]), file=_s.stderr)
+    hmarks_flush()
     return [out[i] for i in range(len(kinds))]
 
 
@@ -203,6 +203,8 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
 
     def oof(col, fitted):
+        from ..utils.timing import hmark
+        hmark(f"oof{col}")
         for k in range(N_FOLDS):
             if test_idx[k].numel():
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)

@@ -111,9 +111,77 @@ class StackingClassifier(Estimator):
                 return ops.stack_infer(X, pk)
         return self.final_estimator_.predict_proba(self.transform(X))[:, 1]
 
+    # below this many rows the GPU takes the per-model f64 path: a single patient gets the exact
+    # (1e-7 golden) probability, and the fused f32 kernel pays off only on batches
+    FUSED_MIN_ROWS = 1024
+
+    # ≤ this many host rows of an HF-shaped stack go through the native f64 host predictor
+    # (ops/csrc/host.hip stack_predict_host: single-patient latency, no tensor dispatch)
+    HOST_NATIVE_MAX_ROWS = 256
+
+    def _host_pack(self):
+        """numpy operands of the native host predictor, or None (not HF-shaped / no extension)."""
+        cached = getattr(self, "_hpack", None)
+        key = (id(self.estimators_), id(self.final_estimator_))
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        pk = None
+        try:
+            from .. import ops
+            from .gbdt import GradientBoostingClassifier
+            from .linear import LogisticRegression
+            from .scaler import StandardScaler
+            from .svc import SVC
+            e = self.estimators_
+            if (ops.has_ext() and len(e) == 3 and isinstance(e[0], Pipeline) and len(e[0].steps) == 2
+                    and isinstance(e[0].steps[0][1], StandardScaler) and isinstance(e[0].steps[1][1], SVC)
+                    and isinstance(e[1], GradientBoostingClassifier) and isinstance(e[2], LogisticRegression)
+                    and isinstance(self.final_estimator_, LogisticRegression)):
+                import numpy as np
+                sc, svc = e[0].steps[0][1], e[0].steps[1][1]
+                g, lr, mt = e[1], e[2], self.final_estimator_
+                c = lambda t, dt=np.float64: np.ascontiguousarray(t.detach().cpu().numpy(), dtype=dt)  # noqa: E731
+                K = int(g.tree_feature_.shape[1])
+                pk = dict(mean=c(sc.mean_), scale=c(sc.scale_), sv=c(svc.support_vectors_),
+                          coef=c(svc._dual_coef_[0]), gamma=float(svc._gamma), icpt=float(svc._intercept_[0]),
+                          A=float(svc._probA[0]), B=float(svc._probB[0]), T=int(g.tree_feature_.shape[0]), K=K,
+                          feat=c(g.tree_feature_, np.int64), thr=c(g.tree_threshold_),
+                          left=c(g.tree_left_, np.int64), right=c(g.tree_right_, np.int64),
+                          value=c(g.tree_value_.reshape(g.tree_value_.shape[0], -1)[:, :K]),
+                          init=float(g.init_raw_), lr=float(g.learning_rate), lrc=c(lr.coef_[0]),
+                          lri=float(lr.intercept_[0]), meta=c(mt.coef_[0]), metai=float(mt.intercept_[0]),
+                          F=int(sc.mean_.numel()))
+                if pk["meta"].size != 3 or pk["lrc"].size != pk["F"] or pk["sv"].shape[1] != pk["F"]:
+                    pk = None
+        except Exception:   # pragma: no cover - any mismatch: the generic per-model path
+            pk = None
+        self._hpack = (key, pk)
+        return pk
+
+    def _host_native_p1(self, X: torch.Tensor):
+        pk = self._host_pack()
+        if pk is None or X.dim() != 2 or X.shape[1] != pk["F"]:
+            return None
+        import numpy as np
+        from .. import ops
+        x = np.ascontiguousarray(X.detach().numpy(), dtype=np.float64)
+        out = np.empty(x.shape[0], dtype=np.float64)
+        ops.ext().stack_predict_host(
+            x.shape[0], pk["F"], x.ctypes.data, pk["mean"].ctypes.data, pk["scale"].ctypes.data, pk["sv"].shape[0],
+            pk["sv"].ctypes.data, pk["coef"].ctypes.data, pk["gamma"], pk["icpt"], pk["A"], pk["B"], pk["T"],
+            pk["K"], pk["feat"].ctypes.data, pk["thr"].ctypes.data, pk["left"].ctypes.data, pk["right"].ctypes.data,
+            pk["value"].ctypes.data, pk["init"], pk["lr"], pk["lrc"].ctypes.data, pk["lri"], pk["meta"].ctypes.data,
+            pk["metai"], out.ctypes.data)
+        return torch.from_numpy(out)
+
     def predict_proba(self, X) -> torch.Tensor:
         X = as_tensor(X)
-        if X.is_cuda and self.fused_inference and self._packed_stack(X.device) is not None:
+        if not X.is_cuda and X.shape[0] <= self.HOST_NATIVE_MAX_ROWS:
+            p1 = self._host_native_p1(X)
+            if p1 is not None:
+                return torch.stack([1 - p1, p1], dim=1)
+        if (X.is_cuda and self.fused_inference and X.shape[0] >= self.FUSED_MIN_ROWS
+                and self._packed_stack(X.device) is not None):
             p1 = self.predict_p1(X).to(torch.float64)
             return torch.stack([1 - p1, p1], dim=1)
         return self.final_estimator_.predict_proba(self.transform(X))

@@ -88,4 +88,92 @@ void sklearn_stump_ranks(int T, int F, uintptr_t seeds_ptr, uintptr_t constant_p
   }
 }
 
+// stack_predict_host : the HF stack (StandardScaler → RBF-SVC + Platt + libsvm iterative coupling,
+//                      GBC tree walk, L1-LR, meta-LR) in f64 for a few rows on the host — the
+//                      single-patient path of predict_hf.py (BASELINE config 1: 85 µs p50 with
+//                      numpy).  Same arithmetic as ops/reference.py (decision rule float32(x) ≤
+//                      threshold, trees added in order, coupling eps 0.005/k), no tensor dispatch.
+#include <cmath>
+static inline double hf_sigmoid(double v) { return 1.0 / (1.0 + std::exp(-v)); }
+
+static double hf_couple2(double r01) {
+  const double r10 = 1.0 - r01, q00 = r10 * r10, q11 = r01 * r01, q01 = -r10 * r01;
+  double p0 = 0.5, p1 = 0.5;
+  const double eps = 0.005 / 2;
+  for (int it = 0; it < 100; ++it) {
+    const double qp0 = q00 * p0 + q01 * p1, qp1 = q01 * p0 + q11 * p1;
+    const double pqp = p0 * qp0 + p1 * qp1;
+    const double err = std::fmax(std::fabs(qp0 - pqp), std::fabs(qp1 - pqp));
+    if (err < eps) break;
+    double d = (-qp0 + pqp) / q00;
+    double np0 = p0 + d;
+    const double npqp = (pqp + d * (d * q00 + 2 * qp0)) / (1 + d) / (1 + d);
+    const double nqp1 = (qp1 + d * q01) / (1 + d);
+    np0 = np0 / (1 + d);
+    double np1 = p1 / (1 + d);
+    d = (-nqp1 + npqp) / q11;
+    np1 = np1 + d;
+    np0 = np0 / (1 + d);
+    np1 = np1 / (1 + d);
+    p0 = np0;
+    p1 = np1;
+  }
+  return p1;
+}
+
+void stack_predict_host(int n, int F, uintptr_t X_, uintptr_t mean_, uintptr_t scale_, int nsv, uintptr_t sv_,
+                        uintptr_t coef_, double gamma, double svc_icpt, double probA, double probB, int T, int K,
+                        uintptr_t feat_, uintptr_t thr_, uintptr_t left_, uintptr_t right_, uintptr_t value_,
+                        double gbc_init, double lr, uintptr_t lrc_, double lr_icpt, uintptr_t meta_,
+                        double meta_icpt, uintptr_t out_) {
+  const double* X = reinterpret_cast<const double*>(X_);
+  const double* mean = reinterpret_cast<const double*>(mean_);
+  const double* scale = reinterpret_cast<const double*>(scale_);
+  const double* sv = reinterpret_cast<const double*>(sv_);
+  const double* coef = reinterpret_cast<const double*>(coef_);
+  const int64_t* feat = reinterpret_cast<const int64_t*>(feat_);
+  const double* thr = reinterpret_cast<const double*>(thr_);
+  const int64_t* left = reinterpret_cast<const int64_t*>(left_);
+  const int64_t* right = reinterpret_cast<const int64_t*>(right_);
+  const double* value = reinterpret_cast<const double*>(value_);
+  const double* lrc = reinterpret_cast<const double*>(lrc_);
+  const double* meta = reinterpret_cast<const double*>(meta_);
+  double* out = reinterpret_cast<double*>(out_);
+  double z[256];
+  for (int r = 0; r < n; ++r) {
+    const double* x = X + (size_t)r * F;
+    for (int f = 0; f < F; ++f) z[f] = (x[f] - mean[f]) / scale[f];
+    double dec = 0.0;
+    for (int j = 0; j < nsv; ++j) {
+      const double* s = sv + (size_t)j * F;
+      double d2 = 0.0;
+      for (int f = 0; f < F; ++f) {
+        const double t = z[f] - s[f];
+        d2 += t * t;
+      }
+      dec += std::exp(-gamma * d2) * coef[j];
+    }
+    dec += svc_icpt;
+    const double fApB = dec * probA + probB;
+    double r01 = fApB >= 0 ? std::exp(-fApB) / (1.0 + std::exp(-fApB)) : 1.0 / (1.0 + std::exp(fApB));
+    r01 = std::fmin(std::fmax(r01, 1e-7), 1 - 1e-7);
+    const double p_svc = hf_couple2(r01);
+    double raw = gbc_init;
+    for (int t = 0; t < T; ++t) {
+      int64_t nd = 0;
+      const int64_t* ft = feat + (size_t)t * K;
+      while (ft[nd] >= 0) {
+        const double xv = (double)(float)x[ft[nd]];
+        nd = xv <= thr[(size_t)t * K + nd] ? left[(size_t)t * K + nd] : right[(size_t)t * K + nd];
+      }
+      raw += lr * value[(size_t)t * K + nd];
+    }
+    const double p_gbc = hf_sigmoid(raw);
+    double dl = 0.0;
+    for (int f = 0; f < F; ++f) dl += x[f] * lrc[f];
+    const double p_lr = hf_sigmoid(dl + lr_icpt);
+    out[r] = hf_sigmoid(p_svc * meta[0] + p_gbc * meta[1] + p_lr * meta[2] + meta_icpt);
+  }
+}
+
 }  // namespace hfens

@@ -90,21 +90,24 @@ def tree_raw(x: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor, le
     x32 = x.to(torch.float32).to(torch.float64)
     n = x.shape[0]
     T = feature.shape[0]
-    raw = torch.full((n,), float(init), dtype=torch.float64, device=x.device)
-    rows = torch.arange(n, device=x.device)
-    for t in range(T):
-        node = torch.zeros(n, dtype=torch.long, device=x.device)
-        while True:
-            f = feature[t, node]
-            leaf = f < 0
-            if bool(leaf.all()):
-                break
-            fv = x32[rows, f.clamp(min=0).long()]
-            go_left = fv <= threshold[t, node]
-            nxt = torch.where(go_left, left[t, node], right[t, node]).long()
-            node = torch.where(leaf, node, nxt)
-        raw += lr * value[t, node].to(torch.float64)
-    return raw
+    # all trees walk together ([T, n] node ids, one step per level: a handful of tensor ops
+    # instead of ~10 per tree), then the per-tree contributions are added in tree order
+    # (cumsum over [init, lr·v_0, …] reproduces sklearn's sequential raw += lr·v_t rounding)
+    node = torch.zeros(T, n, dtype=torch.long, device=x.device)
+    cols = torch.arange(n, device=x.device)[None, :].expand(T, n)
+    feature = feature.long()
+    for _ in range(feature.shape[1]):
+        f = feature.gather(1, node)
+        leaf = f < 0
+        if bool(leaf.all()):
+            break
+        fv = x32[cols, f.clamp(min=0)]
+        go_left = fv <= threshold.gather(1, node)
+        nxt = torch.where(go_left, left.long().gather(1, node), right.long().gather(1, node))
+        node = torch.where(leaf, node, nxt)
+    v = value.to(torch.float64).reshape(T, -1).gather(1, node)          # [T, n]
+    terms = torch.cat([torch.full((1, n), float(init), dtype=torch.float64, device=x.device), lr * v])
+    return torch.cumsum(terms, 0)[-1]
 
 
 def expit(x: torch.Tensor) -> torch.Tensor:

@@ -96,3 +96,25 @@ class StageTimer:
 
     def json(self) -> str:
         return json.dumps({k: round(v, 6) for k, v in self.times.items()})
+
+
+# ---------------------------------------------------------------------------- host timeline marks
+# HFENS_TRACE_HOST=1: ``hmark(name)`` records host wall-clock points anywhere in the fit; the
+# stacking trainer prints them per fit (ms since the first mark).  Zero cost when disabled.
+import os as _os
+
+TRACE_HOST = _os.environ.get("HFENS_TRACE_HOST", "0") == "1"
+_MARKS: list = []
+
+
+def hmark(name: str) -> None:
+    if TRACE_HOST:
+        _MARKS.append((name, time.perf_counter()))
+
+
+def hmarks_flush(prefix: str = "[host]") -> None:
+    if TRACE_HOST and _MARKS:
+        import sys
+        t0 = _MARKS[0][1]
+        print(prefix + " " + " ".join(f"{k}={1e3 * (v - t0):.1f}" for k, v in _MARKS), file=sys.stderr)
+        _MARKS.clear()

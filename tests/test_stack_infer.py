@@ -138,3 +138,44 @@ def test_batched_predictor_graph_and_stream(dev, ckpt_path):
     assert torch.equal(a, want) and torch.equal(b, want)
     h = bp.predict_host(X.pin_memory(), chunk_rows=50000)
     assert torch.equal(h, want)
+
+
+def _force_generic(clf, fn):
+    old = clf.HOST_NATIVE_MAX_ROWS
+    clf.HOST_NATIVE_MAX_ROWS = -1
+    try:
+        return fn()
+    finally:
+        clf.HOST_NATIVE_MAX_ROWS = old
+
+
+def test_native_host_predictor_matches_per_model_path(ckpt_path):
+    """Small host batches go through ops/csrc/host.hip stack_predict_host (config 1 latency):
+    f64 throughout, so it matches the per-model torch path to rounding."""
+    if not ops.has_ext():
+        pytest.skip("HIP extension not built")
+    clf = load_checkpoint(ckpt_path)
+    assert clf._host_pack() is not None
+    X = _patients(200, seed=9)
+    got = clf.predict_proba(X)[:, 1]
+    want = _force_generic(clf, lambda: clf.predict_proba(X)[:, 1])
+    assert float((got - want).abs().max()) < 1e-12
+    one = clf.predict_proba(X[:1])
+    assert abs(float(one[0, 1]) - 0.2709003008994077) < 1e-12
+    assert f"{100 * float(one[0, 1]):.2f}" == "27.09"
+
+
+def test_native_host_predictor_deep_trees():
+    """A freshly trained stack with depth-3 GBC trees (general node walk, not stumps)."""
+    if not ops.has_ext():
+        pytest.skip("HIP extension not built")
+    from hfens.config import EnsembleConfig, build_estimators
+    from hfens.io.synth import make_hf_cohort
+    X, y, _ = make_hf_cohort(400, 9, seed=4, nan_frac=0.0)
+    X, y = torch.as_tensor(X), torch.as_tensor(y)
+    clf = build_estimators(EnsembleConfig(gbc_estimators=20, gbc_depth=3)).fit(X, y)
+    assert clf._host_pack() is not None
+    Xt = torch.as_tensor(make_hf_cohort(150, 9, seed=5, nan_frac=0.0)[0])
+    got = clf.predict_proba(Xt)[:, 1]
+    want = _force_generic(clf, lambda: clf.predict_proba(Xt)[:, 1])
+    assert float((got - want).abs().max()) < 1e-12
