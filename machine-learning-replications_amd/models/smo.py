@@ -361,8 +361,11 @@ def _pick_solver(max_l: int) -> str:
 # ≥ COOP_MIN_SLICE points per member.
 COOP = os.environ.get("HFENS_SMO_COOP", "1") != "0"
 COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
-COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "80"))   # CUs left to concurrent GBC/LR
-_COOP_MAX_W = int(os.environ.get("HFENS_SMO_COOP_MAXW", "4"))   # more members: exchange skew outweighs the split (measured)
+COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "60"))   # CUs left to concurrent GBC/LR
+# more members: exchange skew outweighs the split.  Measured on the bench (36 problems, max l 10k,
+# L2 row prefetch on, scripts/gpu_coop_sweep.sh): W=2 89.4, 3 85.0, 4 81.8-85.3, 5 79.8-80.9,
+# 6 84.9, 7 125.6 ms/fit (7 leaves 4 CUs to GBC/LR)
+_COOP_MAX_W = int(os.environ.get("HFENS_SMO_COOP_MAXW", "5"))
 _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)
 # "otf" (HFENS_SMO_OTF=1, while a member's rows fit its registers: ≤ 1024 points per member, ≤ 20
 # features): the cooperative kernel recomputes its Gram-row entries per pair with the Gram kernel's

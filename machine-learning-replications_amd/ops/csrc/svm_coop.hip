@@ -22,6 +22,8 @@
 // most one member per CU, so every member is resident at once; the members of one problem are
 // placed on one XCD (blocks b and b+8 share an XCD under round-robin dispatch — speed only,
 // never correctness).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace hfens {
@@ -45,6 +47,7 @@ struct SmoCoopOut {
   unsigned* err;    // [1] set on a spin timeout
   long long* prof;  // [P][7] s_memtime phase totals of member 0 (nullptr = off): step2, red2,
                     // xchg2, pair, update, red1, xchg1
+  int prefetch;     // 1: pull the member's candidate Gram row into L2 while the exchange runs
 };
 
 constexpr int kCoopThreads = 512;
@@ -225,6 +228,30 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       if (k == kk) v = arr[k];
     return v;
   };
+  // While wave 0 polls an exchange, waves 1.. touch one dword per 128-byte line of the FULL Gram
+  // row of this member's own candidate: the winning candidate's row — whichever member proposed
+  // it — is then in this XCD's L2 (members of a problem share an XCD) when every member reads its
+  // slice after the exchange, so the two dependent row reads of a pair cost an L2 hit instead of
+  // an HBM round trip.  Issued after the owner's granule stores (a stalled owner would delay the
+  // exchange itself) and consumed only after the exchange (the barrier waits on LDS traffic only,
+  // so nothing waits for these loads until the data is long there).  Rows of ≤ 4·448·32 points
+  // are covered entirely; longer rows only partly (a hint, never a correctness matter).
+  struct Pf { float v[4]; };
+  auto prefetch_issue = [&](int r) {
+    Pf pf{{0.f, 0.f, 0.f, 0.f}};
+    if (out.prefetch && r >= 0 && tid >= 64) {
+      const float* row = Kp + (size_t)r * Pr.ld;
+      const int lines = (Pr.l + 31) >> 5;
+      constexpr int kPf = kCoopThreads - 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = tid - 64 + u * kPf;
+        if (c < lines) pf.v[u] = row[(size_t)c << 5];
+      }
+    }
+    return pf;
+  };
+  auto prefetch_retire = [&](const Pf& pf) { asm volatile("" ::"v"(pf.v[0]), "v"(pf.v[1]), "v"(pf.v[2]), "v"(pf.v[3])); };
   // exchange 1: every member's step-1 partial (kb, idx, α_idx) → (Gmax key, i, α_i)
   auto exchange1 = [&](const CoopPart& loc, unsigned long long& kb, int& idx, double& a_i) -> bool {
     ++epoch;
@@ -237,7 +264,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       put_granule(mine + 2, epoch, (unsigned)loc.idx);
       put_u64(mine + 3, epoch, bits_of(av));
     }
+    const Pf pf = prefetch_issue(loc.idx);
     if (!coop_gather(s, W, 5, epoch, vals[epoch & 1], out.err, &sh_fail)) return false;
+    prefetch_retire(pf);
     const unsigned(*v)[kGran] = vals[epoch & 1];
     kb = u64_of(&v[0][0]);
     idx = (int)v[0][2];
@@ -335,7 +364,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
         put_granule(mine + 9, epoch, __float_as_uint(kij));
       }
     }
+    const Pf pf2 = prefetch_issue(loc.idx);
     if (!coop_gather(s2, W, 10, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    prefetch_retire(pf2);
     tick(2);
     unsigned long long ka2, kb2;
     int j;
@@ -535,7 +566,9 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
   HFENS_REQUIRE((long long)P * W <= ncu, "smo_coop_batch: P·W exceeds the CU count (choose a smaller W)");
   const int groups = (P + 7) / 8;
   const long long blocks = 8LL * groups * W;
-  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, (long long*)prof};
+  const char* pfe = std::getenv("HFENS_SMO_PREFETCH");
+  SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, (long long*)prof,
+               (pfe && pfe[0] == '0') ? 0 : 1};
   hipStream_t st = as_stream(stream);
   // every polled granule starts at epoch 0 (epochs count from 1 within the call)
   HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kGran * sizeof(unsigned long long), st));
