@@ -83,8 +83,17 @@ def libsvm_perm_py(l: int, seed: int) -> np.ndarray:
     return perm
 
 
+_SEED_CACHE: dict = {}
+
+
 def sklearn_libsvm_seed(random_state) -> int:
-    """``check_random_state(random_state).randint(np.iinfo('i').max)`` (sklearn svm/_base.py)."""
+    """``check_random_state(random_state).randint(np.iinfo('i').max)`` (sklearn svm/_base.py).
+    An int seed always gives the same draw: cached (a RandomState construction costs ~0.2 ms)."""
+    if isinstance(random_state, (int, np.integer)) and not isinstance(random_state, bool):
+        k = int(random_state)
+        if k not in _SEED_CACHE:
+            _SEED_CACHE[k] = int(np.random.RandomState(k).randint(INT_MAX))
+        return _SEED_CACHE[k]
     if random_state is None:
         rs = np.random.mtrand._rand
     elif isinstance(random_state, (int, np.integer)):
@@ -126,20 +135,24 @@ def _expand(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
     if svc.probability:
         seed = sklearn_libsvm_seed(svc.random_state)
         perm = libsvm_perm(l, seed)
-        is_pos = np.arange(l) < n0   # grouped position → class 0
+        gp = grouped[perm]                     # rows in permutation order
+        cls0_at = perm < n0                    # grouped position < n0 ⇔ class 0
+        i1, i0 = np.nonzero(~cls0_at)[0], np.nonzero(cls0_at)[0]   # perm positions per class
+        g1, g0 = gp[i1], gp[i0]
         for k in range(5):
             b, e = k * l // 5, (k + 1) * l // 5
-            train = np.concatenate([perm[:b], perm[e:]])
-            cls1 = train[~is_pos[train]]
-            cls0 = train[is_pos[train]]
+            # training rows = perm minus [b, e), in perm order, class 1 (label −1) first
+            lo1, hi1 = np.searchsorted(i1, (b, e))
+            lo0, hi0 = np.searchsorted(i0, (b, e))
+            n1 = int(lo1 + i1.shape[0] - hi1)
+            nn0 = int(lo0 + i0.shape[0] - hi0)
             held = perm[b:e]
-            if cls1.shape[0] == 0 or cls0.shape[0] == 0:
-                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, grouped[held],
-                                   const=1.0 if cls1.shape[0] == 0 else -1.0))
+            if n1 == 0 or nn0 == 0:
+                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, gp[b:e],
+                                   const=1.0 if n1 == 0 else -1.0))
                 continue
-            rows_pos = np.concatenate([cls1, cls0])        # sub-problem order: label −1 (class 1) first
-            probs.append(_Prob(fit_id, k, grouped[rows_pos], int(cls1.shape[0]), C1, C0, gamma,
-                               held, grouped[held]))
+            rows = np.concatenate([g1[:lo1], g1[hi1:], g0[:lo0], g0[hi0:]])
+            probs.append(_Prob(fit_id, k, rows, n1, C1, C0, gamma, held, gp[b:e]))
     probs.append(_Prob(fit_id, -1, grouped, n0, C0, C1, gamma))
     return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
 
@@ -715,21 +728,37 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
                 fit_svc_lowrank_batch([svcs[f] for f in mine], [Zs[f] for f in mine], [ys[f] for f in mine])
             broadcast_svc_fits(svcs, Zs, group)
         return dict(done=True, svcs=svcs)
-    from ..utils.guards import check_binary, check_finite
-    for f, (Z, y) in enumerate(zip(Zs, ys)):
-        check_finite(Z, f"SVC.fit X (fit {f})")
-        check_binary(y, f"SVC.fit y (fit {f})")
+    from ..utils import guards
     from ..utils.timing import hmark
-    hmark("svc_checks")
     device = Zs[0].device
     cuda = Zs[0].is_cuda
-    # one host read for every fit's labels and one for the 'scale' gamma statistics; the problem
-    # bookkeeping itself is numpy on the host
+    # ONE device→host read for everything the host bookkeeping needs: the finite / 0-1 guard
+    # flags, the 'scale' gamma statistics and every fit's labels (the problem bookkeeping itself
+    # is numpy on the host)
     sizes = [int(y.numel()) for y in ys]
-    y_host = torch.cat([y.reshape(-1).to(torch.float64) for y in ys]).cpu().numpy()
     need_var = [svc.gamma == "scale" for svc in svcs]
-    var = (torch.stack([Z.to(torch.float64).var(unbiased=False) for Z in Zs]).cpu().numpy()
-           if any(need_var) else None)
+    f64 = torch.float64
+    parts = []
+    if guards.ENABLED:
+        parts.append(torch.stack([torch.isfinite(Z).all() for Z in Zs]).to(f64))
+        parts.append(torch.stack([((y == 0) | (y == 1)).all() for y in ys]).to(f64))
+    if any(need_var):
+        parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
+    parts.append(torch.cat([y.reshape(-1).to(f64) for y in ys]))
+    host = torch.cat(parts).cpu().numpy()
+    o = 0
+    if guards.ENABLED:
+        for f in range(len(Zs)):
+            if host[f] == 0.0:
+                guards.check_finite(Zs[f], f"SVC.fit X (fit {f})")
+            if host[len(Zs) + f] == 0.0:
+                guards.check_binary(ys[f], f"SVC.fit y (fit {f})")
+        o = 2 * len(Zs)
+    var = None
+    if any(need_var):
+        var = host[o:o + len(Zs)]
+        o += len(Zs)
+    y_host = host[o:]
     hmark("svc_y_var_host")
     all_probs, meta = [], []
     off = 0

@@ -74,15 +74,16 @@ def _global_scaler_moments(X, masks, group):
     return mean, sq / cnt[:, None], cnt
 
 
-def _svc_inputs(est, X, y, masks, group=None):
+def _svc_inputs(est, X, y, masks, group=None, rows_host=None):
     """Clones, their SVC objects and the scaled per-mask training matrices.  ``group`` (rows
-    sharded): the scalers are fitted on the global masked rows, as a single process would."""
+    sharded): the scalers are fitted on the global masked rows, as a single process would.
+    ``rows_host``: the masks' row indices, known on the host (no ``nonzero`` synchronisation)."""
     kind = _kind(est)
     clones = [est.clone() for _ in range(masks.shape[0])]
     Zs, ys = [], []
     gm = _global_scaler_moments(X, masks, group) if (group is not None and kind == "svc") else None
     for k, (c, m) in enumerate(zip(clones, masks)):
-        rows = torch.nonzero(m).squeeze(1)
+        rows = _index_to(rows_host[k], X.device) if rows_host is not None else torch.nonzero(m).squeeze(1)
         Xm = X[rows]
         if kind == "svc":
             sc = c.steps[0][1]
@@ -98,13 +99,13 @@ def _svc_inputs(est, X, y, masks, group=None):
     return clones, svcs, Zs, ys
 
 
-def fit_base_batch(est, X, y, masks, group=None, timer=None, svc_group=None):
+def fit_base_batch(est, X, y, masks, group=None, timer=None, svc_group=None, rows_host=None):
     """Fit ``masks.shape[0]`` clones of ``est`` on the masked row subsets; returns them.
     ``group``: rows sharded over ranks (data parallel); ``svc_group``: rows replicated on every
     rank, only the SMO problems are spread over the ranks (task parallel)."""
     kind = _kind(est)
     if kind in ("svc", "svc_raw"):
-        clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks, group)
+        clones, svcs, Zs, ys = _svc_inputs(est, X, y, masks, group, rows_host)
         if group is None:
             fit_svc_batch(svcs, Zs, ys, group=svc_group)
         else:
@@ -126,7 +127,7 @@ def _index_to(a, device) -> torch.Tensor:
     return t.pin_memory().to(device, non_blocking=True)
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None):
+def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -156,7 +157,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
         with torch.cuda.stream(side):
             for i in svc_cols:
-                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group)
+                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
                 hmark("svc_inputs")
                 if group is None:
                     pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group))
@@ -196,6 +197,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
         from ..parallel import dist as pdist
         folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
     masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
+    rows_host = [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)]
     # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
     # gathers / scatters then need no host synchronisation
     test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
@@ -210,13 +212,13 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group)
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream
         else:
             with timer.stage(f"fit_{name}"):
-                fitted = fit_base_batch(est, X, y, masks, group=group, svc_group=svc_group)
+                fitted = fit_base_batch(est, X, y, masks, group=group, svc_group=svc_group, rows_host=rows_host)
             with timer.stage(f"oof_{name}"):
                 oof(col, fitted)
         full.append(fitted[N_FOLDS])
