@@ -15,9 +15,12 @@ so coefficients agree with sklearn to its own stopping accuracy.
 With ``group`` (rows sharded over ranks) the per-iteration g, H and line-search
 losses are all-reduced (F² + F + 8 doubles per model).
 
-On one GPU the whole solve runs as ONE launch (``ops/csrc/logreg.hip`` ``logreg_fused``: one
-workgroup per model, the same three passes per iteration, no host round trip); the loop below
-is the host / data-parallel path and the reference the fused kernel is tested against.
+On one GPU the whole solve runs as ONE launch (``ops/csrc/logreg.hip``): ``logreg_coop`` spreads
+every model over up to 16 workgroups (row slabs; the per-iteration H/g/loss and line-search sums
+are exchanged between them in a fixed member order), ``logreg_fused`` is the one-workgroup form
+(used when a cooperative SMO shares the device and too few CUs are free for the members, or
+``HFENS_LOGREG_MEMBERS=1``).  The loop below is the host / data-parallel path and the reference
+the fused kernels are tested against.
 """
 from __future__ import annotations
 
@@ -70,11 +73,24 @@ def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
 
 
 FUSED = os.environ.get("HFENS_LOGREG_FUSED", "1") != "0"
+MEMBERS = int(os.environ.get("HFENS_LOGREG_MEMBERS", "0"))   # 0 = auto
+MIN_ROWS_PER_MEMBER = 512
 LAST_PATH = {"path": None}
+# workgroups a cooperative LR launch may occupy (None = all CUs).  The stacking trainer lowers it
+# while a cooperative SMO holds most CUs on another stream: LR members spin on each other, so all of
+# them must fit on the CUs the SMO leaves free (stack_trainer._fit_bases_concurrent).
+BLOCK_BUDGET = [None]
+
+
+def lr_members(B: int, n: int, ncu: int) -> int:
+    if MEMBERS > 0:
+        return max(1, min(16, MEMBERS, ncu // B))
+    budget = ncu if BLOCK_BUDGET[0] is None else min(ncu, BLOCK_BUDGET[0])
+    return max(1, min(16, budget // B, -(-n // MIN_ROWS_PER_MEMBER)))
 
 
 def _fit_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int):
-    """All B solves in one ``logreg_fused`` launch; returns (W [B, F1], n_iter [B] int32)."""
+    """All B solves in one launch; returns (W [B, F1], n_iter [B] int32)."""
     E = ops.ext()
     B, n = s.shape
     F1 = Xa.shape[1]
@@ -84,6 +100,23 @@ def _fit_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int):
     iters = torch.empty(B, dtype=torch.int32, device=dev)
     Z = torch.empty(B, n, dtype=torch.float64, device=dev)
     Xd = torch.empty_like(Z)
+    from .smo import _num_cus
+    M = lr_members(B, n, _num_cus(dev))
+    if M > 1:
+        nv = F1 * (F1 + 1) // 2 + F1 + 1
+        xchg = torch.empty(B * 2 * M * nv * 2, dtype=torch.int64, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        E.logreg_coop(B, M, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C), int(l1),
+                      int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(), xchg.data_ptr(),
+                      err.data_ptr(), ops.stream_ptr(dev))
+        LAST_PATH["members"] = M
+        if int(err.item()) == 0:
+            return W, iters
+        import warnings
+        warnings.warn("cooperative logistic regression timed out waiting for a member; re-solving with one "
+                      "workgroup per model")
+        LAST_PATH["coop_fallback"] = True
+    LAST_PATH["members"] = 1
     E.logreg_fused(B, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C), int(l1),
                    int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(), ops.stream_ptr(dev))
     return W, iters

@@ -164,13 +164,21 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
                 hmark("svc_launched")
-        with torch.cuda.stream(other):
-            for i, (name, est) in enumerate(clf.estimators):
-                if i not in svc_cols:
-                    out[i] = fit_base_batch(est, X, y, masks, group=group)
-                    if oof is not None:
-                        oof(i, out[i])
-                    hmark(f"{name}_host_done")
+        # cooperative LR members must all fit on the CUs a cooperative SMO leaves free
+        from . import logreg_solver, smo as _smo
+        lr_budget = logreg_solver.BLOCK_BUDGET[0]
+        if _smo.LAST_SMO_INFO.get("solver") in ("coop", "coop-otf"):
+            logreg_solver.BLOCK_BUDGET[0] = max(1, _smo.COOP_RESERVE_CUS // 2)
+        try:
+            with torch.cuda.stream(other):
+                for i, (name, est) in enumerate(clf.estimators):
+                    if i not in svc_cols:
+                        out[i] = fit_base_batch(est, X, y, masks, group=group)
+                        if oof is not None:
+                            oof(i, out[i])
+                        hmark(f"{name}_host_done")
+        finally:
+            logreg_solver.BLOCK_BUDGET[0] = lr_budget
         with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
                 if group is None:

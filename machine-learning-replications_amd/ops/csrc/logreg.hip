@@ -34,7 +34,73 @@ struct LrJob {
   int* iters;                  // [B] outer iterations
   double C;
   int n, F1, l1, max_outer, CR;  // CR: rows per LDS chunk
+  // cooperative variant (logreg_coop): M members per model, member w owns rows [w·S, (w+1)·S)
+  int B, M, S, nvmax;            // M members per model; nvmax: exchange values per member slot
+  unsigned long long* xchg;      // [B][2][M][nvmax][2] epoch-tagged granules
+  unsigned* err;                 // [1] set on a member-exchange timeout
 };
+
+constexpr int kLrMaxMembers = 16;
+constexpr unsigned kLrSpinLimit = 1u << 22;
+typedef __attribute__((address_space(1))) unsigned long long lr_gu64_t;
+
+__device__ __forceinline__ void lr_put(unsigned long long* g, unsigned epoch, unsigned v) {
+  __hip_atomic_store((lr_gu64_t*)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Member exchange of NV doubles (LDS v[0..NV): this member's partials in, the sums over all
+// members out).  Each value is published as two epoch-tagged granules (agent-scope relaxed
+// atomic stores: data and tag travel together, no fence or flag); every thread then polls the W
+// members' granules of its values and sums them in member order 0..W−1, so every member gets
+// bit-identical totals.  Slots alternate by epoch parity: a member reaches exchange e+2 only after
+// every member published e+1, i.e. finished reading e.  false = a peer never arrived (timeout).
+__device__ bool lr_exchange(double* v, int NV, const LrJob& J, int b, int w, unsigned& epoch, int* fail) {
+  ++epoch;
+  unsigned long long* slot = J.xchg + ((size_t)b * 2 + (epoch & 1)) * J.M * J.nvmax * 2;
+  for (int k = threadIdx.x; k < NV; k += kLrThreads) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v[k]);
+    unsigned long long* g = slot + ((size_t)w * J.nvmax + k) * 2;
+    lr_put(g, epoch, (unsigned)x);
+    lr_put(g + 1, epoch, (unsigned)(x >> 32));
+  }
+  bool ok_all = true;
+  for (int k = threadIdx.x; k < NV && ok_all; k += kLrThreads) {
+    unsigned lo[kLrMaxMembers], hi[kLrMaxMembers];
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int m = 0; m < kLrMaxMembers; ++m) {
+        if (m >= J.M) break;
+        const unsigned long long* g = slot + ((size_t)m * J.nvmax + k) * 2;
+        const unsigned long long a = __hip_atomic_load((lr_gu64_t*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c = __hip_atomic_load((lr_gu64_t*)(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lo[m] = (unsigned)a;
+        hi[m] = (unsigned)c;
+        ok = ok && (unsigned)(a >> 32) == epoch && (unsigned)(c >> 32) == epoch;
+      }
+      if (ok) break;
+      if (++spins > kLrSpinLimit) {
+        atomicOr(J.err, 1u);
+        ok_all = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok_all) break;
+    double tot = 0.0;
+#pragma unroll
+    for (int m = 0; m < kLrMaxMembers; ++m) {
+      if (m >= J.M) break;
+      tot += __longlong_as_double((long long)((unsigned long long)lo[m] | ((unsigned long long)hi[m] << 32)));
+    }
+    v[k] = tot;
+  }
+  if (!ok_all) *fail = 1;
+  __syncthreads();
+  return *fail == 0;
+}
 
 __device__ __forceinline__ double lr_softplus(double x) {  // log(1 + e^x), overflow-free
   return x > 0 ? x + log1p(exp(-x)) : log1p(exp(x));
@@ -58,10 +124,28 @@ __device__ __forceinline__ void lr_block_sum(const double (&v)[NV], double* red,
   __syncthreads();
 }
 
+// Coop = false: logreg_fused, one workgroup per model (blockIdx.x = model).  Coop = true:
+// logreg_coop, W workgroups ("members") per model on one XCD (blocks b, b+8, … share an XCD under
+// round-robin dispatch — speed only), each owning a row slab; the two row reductions of an
+// iteration (A: H, g, loss; C: the 8 trial losses) become member exchanges with ordered sums, and
+// every member runs the small subproblem B itself on identical data, so all members take the same
+// steps.  Members spin on each other: the host admits B·W ≤ CUs and launches it only when no other
+// cooperative kernel shares the device.
+template <bool Coop>
 __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int b = blockIdx.x, w = 0;
+  if constexpr (Coop) {
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+    b = xcd + 8 * (q / J.M);
+    w = q % J.M;
+    if (b >= J.B) return;
+  }
   const int n = J.n, F1 = J.F1, CR = J.CR;
+  const int r0 = Coop ? min(n, w * J.S) : 0, r1 = Coop ? min(n, r0 + J.S) : n;
+  __shared__ int xfail;
+  unsigned epoch = 0;
   const int npairs = F1 * (F1 + 1) / 2, T = npairs + F1;
   double* xs = sm;                          // [CR][F1] row chunk
   double* dv = xs + (size_t)CR * F1;        // [CR] Hessian weights of the chunk's rows
@@ -73,7 +157,8 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
   double* part = Wl + F1;                   // [kLrThreads] row-group partials
   double* red = part + kLrThreads;          // [kLrWaves][kLrSteps]
   double* sc = red + kLrWaves * kLrSteps;   // [16] scalars: 0 stop, 1 delta, 2 reg0, 8.. sums
-  unsigned char* pi = reinterpret_cast<unsigned char*>(sc + 16);
+  double* mv = sc + 16;                     // [T + 1] member partials of H, g and the loss
+  unsigned char* pi = reinterpret_cast<unsigned char*>(mv + T + 1);
   unsigned char* pj = pi + npairs;
   const double* s = J.s + (size_t)b * n;
   double* Z = J.Z + (size_t)b * n;
@@ -86,7 +171,8 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
     pj[k] = (unsigned char)(i + rem);
   }
   for (int f = tid; f < F1; f += kLrThreads) Wl[f] = 0.0;
-  for (int r = tid; r < n; r += kLrThreads) Z[r] = 0.0;
+  for (int r = r0 + tid; r < r1; r += kLrThreads) Z[r] = 0.0;
+  if (tid == 0) xfail = 0;
   // moment tasks: T ≤ kLrThreads → G row groups of T tasks each; otherwise ≤ 3 tasks per thread
   const int G = T >= kLrThreads ? 1 : kLrThreads / T;
   const int grp = T >= kLrThreads ? 0 : tid / T;
@@ -99,8 +185,8 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
     // ---- A: H, g and the loss at the current margins
     double acc[3] = {0.0, 0.0, 0.0};
     double loss[1] = {0.0};
-    for (int c0 = 0; c0 < n; c0 += CR) {
-      const int nr = min(CR, n - c0);
+    for (int c0 = r0; c0 < r1; c0 += CR) {
+      const int nr = min(CR, r1 - c0);
       const double* Xc = J.X + (size_t)c0 * F1;
       for (int e = tid; e < nr * F1; e += kLrThreads) xs[e] = Xc[e];
       for (int r = tid; r < nr; r += kLrThreads) {
@@ -143,21 +229,29 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
         gr[k - npairs] = v;
       }
     };
+    // this workgroup's partial of every task → mv (row groups folded in a fixed order)
     if (G > 1) {
       if (grp < G) part[grp * T + task0] = acc[0];
       __syncthreads();
       if (tid < T) {
         double t = 0.0;
         for (int g = 0; g < G; ++g) t += part[g * T + tid];
-        store(tid, C * t);
+        mv[tid] = t;
       }
     } else {
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        if (q < ntask) store(task0 + q * kLrThreads, C * acc[q]);
+        if (q < ntask) mv[task0 + q * kLrThreads] = acc[q];
     }
     lr_block_sum<1>(loss, red, sc + 8);
-    const double data0 = C * sc[8];
+    if (tid == 0) mv[T] = sc[8];
+    __syncthreads();
+    if constexpr (Coop) {
+      if (!lr_exchange(mv, T + 1, J, b, w, epoch, &xfail)) return;
+    }
+    for (int k = tid; k < T; k += kLrThreads) store(k, C * mv[k]);
+    __syncthreads();
+    const double data0 = C * mv[T];
     // ---- B: stopping rule and subproblem
     if (J.l1) {
       if (wave == 0) {
@@ -263,7 +357,7 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
     double tk[kLrSteps];
 #pragma unroll
     for (int k = 0; k < kLrSteps; ++k) tk[k] = 0.0;
-    for (int r = tid; r < n; r += kLrThreads) {
+    for (int r = r0 + tid; r < r1; r += kLrThreads) {
       const double* xr = J.X + (size_t)r * F1;
       double xd = 0.0;
       for (int f = 0; f < F1; ++f) xd = fma(xr[f], dd[f], xd);
@@ -280,6 +374,9 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
       }
     }
     lr_block_sum<kLrSteps>(tk, red, sc + 8);
+    if constexpr (Coop) {
+      if (!lr_exchange(sc + 8, kLrSteps, J, b, w, epoch, &xfail)) return;
+    }
     // Armijo: largest 2^-k with F(w + a d) ≤ F(w) + 0.01·a·Δ; none → the smallest step if it
     // still decreases F, else stop (every thread evaluates the same rule on LDS values)
     const double F0 = data0 + sc[2], delta = sc[1];
@@ -303,7 +400,7 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
     if (step == 0.0) { nit = it + 1; break; }
     __syncthreads();   // every thread has read Wl, dd and sc
     if (tid < F1) Wl[tid] += step * dd[tid];
-    for (int r = tid; r < n; r += kLrThreads) Z[r] += step * Xd[r];
+    for (int r = r0 + tid; r < r1; r += kLrThreads) Z[r] += step * Xd[r];
     __syncthreads();
     double mstep = 0.0, mw = 0.0;
     for (int f = 0; f < F1; ++f) {
@@ -313,8 +410,24 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
     if (mstep <= 1e-14 * (1.0 + mw)) { nit = it + 1; break; }
   }
   __syncthreads();
-  if (tid < F1) J.W[(size_t)b * F1 + tid] = Wl[tid];
-  if (tid == 0) J.iters[b] = nit;
+  if (w == 0) {
+    if (tid < F1) J.W[(size_t)b * F1 + tid] = Wl[tid];
+    if (tid == 0) J.iters[b] = nit;
+  }
+}
+
+static size_t logreg_lds_plan(int F1, int* CR_out) {
+  const int npairs = F1 * (F1 + 1) / 2, T = npairs + F1;
+  // ≤ 32 KiB of staged rows keeps the whole plan near 48 KiB, so a workgroup still fits beside
+  // the SMO members that run concurrently on the other stream
+  int CR = (32 * 1024) / (F1 * (int)sizeof(double));
+  CR = CR > 1024 ? 1024 : CR / 64 * 64;
+  if (CR < 64) CR = 64;
+  *CR_out = CR;
+  const size_t lds = ((size_t)CR * F1 + 2 * CR + F1 * F1 + 3 * F1 + kLrThreads + kLrWaves * kLrSteps + 16 +
+                      (T + 1)) * sizeof(double) + 2 * (size_t)npairs;
+  HFENS_REQUIRE(lds <= 160 * 1024, "logreg_fused: LDS plan exceeds 160 KiB");
+  return lds;
 }
 
 void logreg_fused(int B, int n, int F1, uintptr_t X, uintptr_t s, uintptr_t ypm, uintptr_t penal, double C,
@@ -322,18 +435,44 @@ void logreg_fused(int B, int n, int F1, uintptr_t X, uintptr_t s, uintptr_t ypm,
                   uintptr_t stream) {
   HFENS_REQUIRE(F1 >= 1 && F1 <= 64, "logreg_fused: 1 <= F+1 <= 64");
   HFENS_REQUIRE(B >= 1 && n >= 1 && max_outer >= 1, "logreg_fused: empty problem");
-  const int npairs = F1 * (F1 + 1) / 2;
-  // ≤ 32 KiB of staged rows keeps the whole plan near 48 KiB, so a workgroup still fits beside
-  // the SMO members that run concurrently on the other stream
-  int CR = (32 * 1024) / (F1 * (int)sizeof(double));
-  CR = CR > 1024 ? 1024 : CR / 64 * 64;
-  if (CR < 64) CR = 64;
-  const size_t lds = ((size_t)CR * F1 + 2 * CR + F1 * F1 + 3 * F1 + kLrThreads + kLrWaves * kLrSteps + 16) *
-                         sizeof(double) + 2 * (size_t)npairs;
-  HFENS_REQUIRE(lds <= 160 * 1024, "logreg_fused: LDS plan exceeds 160 KiB");
+  int CR = 0;
+  const size_t lds = logreg_lds_plan(F1, &CR);
   LrJob J{(const double*)X, (const double*)s, (const double*)ypm, (const unsigned char*)penal, (double*)Z,
-          (double*)Xd, (double*)W, (int*)iters, C, n, F1, l1 ? 1 : 0, max_outer, CR};
-  hipLaunchKernelGGL(logreg_fused_kernel, dim3(B), dim3(kLrThreads), lds, as_stream(stream), J);
+          (double*)Xd, (double*)W, (int*)iters, C, n, F1, l1 ? 1 : 0, max_outer, CR, B, 1, n, 0, nullptr, nullptr};
+  hipLaunchKernelGGL(logreg_fused_kernel<false>, dim3(B), dim3(kLrThreads), lds, as_stream(stream), J);
+  launch_check();
+}
+
+// exchange slots (u64 granules); models/logreg_solver.py sizes its buffer with the same formula
+static size_t logreg_coop_xchg_bytes(int B, int members, int F1) {
+  const int nvmax = F1 * (F1 + 1) / 2 + F1 + 1;
+  return (size_t)B * 2 * members * nvmax * 2 * sizeof(unsigned long long);
+}
+
+void logreg_coop(int B, int members, int n, int F1, uintptr_t X, uintptr_t s, uintptr_t ypm, uintptr_t penal,
+                 double C, int l1, int max_outer, uintptr_t Z, uintptr_t Xd, uintptr_t W, uintptr_t iters,
+                 uintptr_t xchg, uintptr_t err, uintptr_t stream) {
+  HFENS_REQUIRE(F1 >= 1 && F1 <= 64, "logreg_coop: 1 <= F+1 <= 64");
+  HFENS_REQUIRE(B >= 1 && n >= 1 && max_outer >= 1, "logreg_coop: empty problem");
+  HFENS_REQUIRE(members >= 1 && members <= kLrMaxMembers, "logreg_coop: 1 <= members <= 16");
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  // members spin on each other: all of them must be resident at once (one per CU at most)
+  HFENS_REQUIRE((long long)B * members <= ncu, "logreg_coop: B·members exceeds the CU count");
+  int CR = 0;
+  const size_t lds = logreg_lds_plan(F1, &CR);
+  const int npairs = F1 * (F1 + 1) / 2;
+  const int nvmax = npairs + F1 + 1;
+  const int S = (n + members - 1) / members;
+  hipStream_t st = as_stream(stream);
+  // every polled granule starts at epoch 0 (epochs count from 1 within the launch)
+  HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, logreg_coop_xchg_bytes(B, members, F1), st));
+  LrJob J{(const double*)X, (const double*)s, (const double*)ypm, (const unsigned char*)penal, (double*)Z,
+          (double*)Xd, (double*)W, (int*)iters, C, n, F1, l1 ? 1 : 0, max_outer, CR, B, members, S, nvmax,
+          (unsigned long long*)xchg, (unsigned*)err};
+  const long long blocks = 8LL * ((B + 7) / 8) * members;
+  hipLaunchKernelGGL(logreg_fused_kernel<true>, dim3((unsigned)blocks), dim3(kLrThreads), lds, st, J);
   launch_check();
 }
 

@@ -86,6 +86,33 @@ def test_logreg_fused_matches_device_loop(dev, monkeypatch, pen):
         assert torch.allclose(a.intercept_, b.intercept_, atol=1e-7)
 
 
+@pytest.mark.parametrize("pen,n,members", [("l1", 8000, 5), ("l2", 10007, 16), ("l1", 300, 3), ("l2", 2000, 1)])
+def test_logreg_coop_matches_single_workgroup(dev, monkeypatch, pen, n, members):
+    """logreg_coop (members exchange ordered partial sums of H, g and the line-search losses) takes
+    the same Newton steps as the one-workgroup kernel up to summation order; members=1 is the
+    one-workgroup kernel itself.  Also a model with fewer rows than members×1024 threads."""
+    from hfens.models import logreg_solver
+    X, y = _data(n, 17, 23)
+    B = 6 if pen == "l1" else 1
+    masks = torch.ones(B, n, dtype=torch.bool)
+    for k in range(min(B, 5)):
+        masks[k, k::5] = False
+    kw = dict(penalty=pen, solver="liblinear" if pen == "l1" else "lbfgs", class_weight="balanced")
+    out = {}
+    for m in (1, members):
+        monkeypatch.setattr(logreg_solver, "MEMBERS", m)
+        ms = [LogisticRegression(**kw) for _ in range(B)]
+        fit_logreg_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        assert logreg_solver.LAST_PATH["members"] == min(m, 256 // B)
+        assert not logreg_solver.LAST_PATH.get("coop_fallback")
+        out[m] = ms
+    for a, b in zip(out[1], out[members]):
+        # both stop at the solver tolerance (the fused-vs-loop test's 1e-7)
+        d = float((a.coef_ - b.coef_).abs().max())
+        assert d < 1e-7, d
+        assert torch.allclose(a.intercept_, b.intercept_, atol=1e-7)
+
+
 def test_svc_device_matches_libsvm(dev):
     from sklearn.preprocessing import StandardScaler
     from sklearn.svm import SVC as SK
