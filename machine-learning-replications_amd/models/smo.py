@@ -862,28 +862,39 @@ def finish_svc_batch(st: dict):
         st2["retried"] = True
         LAST_SMO_INFO["coop_fallback"] = True
         return finish_svc_batch(st2)
+    # ---- final models: ONE device→host read of the Platt (A, B) pairs and every final solve's
+    # support mask, ρ and iteration count; the bookkeeping is then numpy, the gathers non-blocking
+    finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
+    sols = [sol[id(p)] for p in finals]
+    ls = [int(a.numel()) for a, _, _ in sols]
+    host = torch.cat([torch.cat([(a > 0).to(torch.float64).reshape(-1) for a, _, _ in sols]),
+                      torch.stack([torch.as_tensor(r).to(device=device, dtype=torch.float64).reshape(()) for _, r, _ in sols]),
+                      torch.stack([torch.as_tensor(it).to(device=device, dtype=torch.float64).reshape(()) for _, _, it in sols])]
+                     + ([st["ABt"].to(device=device, dtype=torch.float64)] if st["ABt"] is not None else [])
+                     ).cpu().numpy()
+    nl = sum(ls)
     if st["ABt"] is not None:
-        from ..utils.guards import check_finite
-        check_finite(st["ABt"], "SVC Platt sigmoid (A, B)")
-        ABc = st["ABt"].cpu().numpy()
+        ABc = host[nl + 2 * len(svcs):]
+        if not np.isfinite(ABc).all():
+            from ..utils.guards import NonFiniteError
+            raise NonFiniteError(f"SVC Platt sigmoid (A, B): {int((~np.isfinite(ABc)).sum())} non-finite value(s)")
         for k, f in enumerate(st["pl"]):
             AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
-    # ---- final models
+    off = 0
     for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
-        p = [q for q in all_probs if q.fit == f and q.fold < 0][0]
-        a, r, it = sol[id(p)]
-        a = a.to(device)
-        sv = a > 0
-        pos_idx = torch.nonzero(sv).squeeze(1)
+        a = sols[f][0].to(device)
+        pos_np = np.nonzero(host[off:off + ls[f]] > 0.5)[0]
+        off += ls[f]
+        pos_idx = _to_dev(pos_np.astype(np.int64), device)
         yint = torch.where(pos_idx < mt["n0"], 1.0, -1.0).to(torch.float64)
         coef = yint * a[pos_idx]
-        support = torch.as_tensor(mt["grouped"], device=device)[pos_idx]
-        n_sv0 = int((pos_idx < mt["n0"]).sum())
+        support = _to_dev(mt["grouped"][pos_np].astype(np.int64), device)
+        n_sv0 = int((pos_np < mt["n0"]).sum())
         A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
         svc.set_fitted(support=support, support_vectors=Z[support].to(torch.float64),
-                       n_support=[n_sv0, int(pos_idx.numel()) - n_sv0], dual_coef_libsvm=coef,
-                       rho=float(r), probA=A, probB=B, gamma=mt["gamma"],
+                       n_support=[n_sv0, int(pos_np.shape[0]) - n_sv0], dual_coef_libsvm=coef,
+                       rho=float(host[nl + f]), probA=A, probB=B, gamma=mt["gamma"],
                        class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
                        shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
-        svc.n_iter_ = int(it)
+        svc.n_iter_ = int(host[nl + len(svcs) + f])
     return svcs

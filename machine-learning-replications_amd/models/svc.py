@@ -75,7 +75,15 @@ class SVC(Estimator):
             if packed is None or packed.svt.device != X.device:
                 packed = self._packed = ops.pack_svs(self.support_vectors_, self._dual_coef_[0], X.device)
         return ops.rbf_decision(X, self.support_vectors_, self._dual_coef_[0], self._gamma,
-                                float(self._intercept_[0]), packed=packed)
+                                self._host_scalars()[0], packed=packed)
+
+    def _host_scalars(self):
+        """(libsvm intercept, probA, probB) as host floats — cached by set_fitted, so predicting
+        on device tensors costs no device→host reads."""
+        hs = getattr(self, "_hs", None)
+        if hs is None:
+            hs = self._hs = (float(self._intercept_[0]), float(self._probA[0]), float(self._probB[0]))
+        return hs
 
     def decision_function(self, X) -> torch.Tensor:
         # sklearn flips libsvm's sign for the binary case
@@ -85,7 +93,8 @@ class SVC(Estimator):
         if not self.probability:
             raise AttributeError("predict_proba requires probability=True")
         dec = self._libsvm_dec(X)
-        p1 = ops.svc_proba1(dec, float(self._probA[0]), float(self._probB[0])).to(torch.float64)
+        _, pa, pb = self._host_scalars()
+        p1 = ops.svc_proba1(dec, pa, pb).to(torch.float64)
         return torch.stack([1 - p1, p1], dim=1)
 
     def predict(self, X) -> torch.Tensor:
@@ -107,6 +116,7 @@ class SVC(Estimator):
         c = as_tensor(dual_coef_libsvm, dev).reshape(1, -1)
         self._dual_coef_ = c
         self.dual_coef_ = -c
+        self._hs = (-float(rho), float(probA), float(probB))
         self._intercept_ = as_tensor([-float(rho)], dev)
         self.intercept_ = -self._intercept_
         self._probA = as_tensor([probA], dev)
