@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -506,6 +507,30 @@ def _run_fused(st: _State):
 STUMP_PATH = os.environ.get("HFENS_GBDT_STUMPS", "stage")     # stage | fused | launch
 _STAGE_LDS = 150 * 1024
 COLLECTIVES = {"per_stage": None}
+# Stage-loop HIP graphs: "auto" = on for the device stage path when no stamps are
+# collected and the process group (if any) is NCCL/RCCL (capturable collectives); "0" / "1".
+STAGE_GRAPH = os.environ.get("HFENS_GBDT_GRAPH", "auto")
+GRAPH_MIN_STAGES = 9
+GRAPH_INFO: dict = {}
+_GRAPH_KEEP: list = []
+
+
+def _graph_units(st, group, prof) -> int:
+    if STAGE_GRAPH == "0" or prof is not None or st.T + 2 < GRAPH_MIN_STAGES:
+        return 0
+    if group is not None:
+        import torch.distributed as dist
+        if dist.get_backend(group) != "nccl":
+            return 0
+    elif STAGE_GRAPH != "1":
+        return 0     # single process: the eager loop is GPU-bound already (measured), keep it
+    # units of 3 stages t ≡ 0, 1, 2 (mod 3) while every stage of the unit still all-reduces (t ≤ T)
+    return (st.T + 1) // 3
+
+
+def _prune_graphs():
+    while _GRAPH_KEEP and _GRAPH_KEEP[0][1].query():
+        _GRAPH_KEEP.pop(0)
 PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage whose s_memtime stamps to keep
 LAST_STAGE_PROF: dict = {}
 
@@ -543,23 +568,69 @@ def _run_stage(st: _State, group):
     plen = st.B * groups * (3 * hist_len + 8)
     partials = runtime.workspace(dev, "gbdt_stage_partials", plen, torch.int64)
     prof = torch.zeros(st.B * groups * 6, dtype=torch.int64, device=dev) if PROFILE_STAGE_T >= 0 else None
-    n_coll = 0
-    for t in range(st.T + 2):
-        E.gbdt_stump_stage(t, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
+    n_coll = [0]
+
+    def stage(t, host_t, t_dev=None):
+        E.gbdt_stump_stage(host_t, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
                            bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
                            st.raw.data_ptr(), ptr(st.wt), ptr(st.seeds), st.row_off, st.subsample,
                            comm.data_ptr(), st.feat.data_ptr(), st.blo.data_ptr(), st.thr.data_ptr(),
                            st.value.data_ptr(), st.stats.data_ptr(), st.r2.data_ptr(), st.dev.data_ptr(),
                            ptr(st.bagw), ptr(st.frank), partials.data_ptr(), plen, st.lr, st.qscale,
                            st.dscale, st.min_leaf_q,
-                           st.min_split_q, ptr(prof) if (prof is not None and t == PROFILE_STAGE_T) else 0, s)
-        if group is not None and t <= st.T:
+                           st.min_split_q, ptr(prof) if (prof is not None and t == PROFILE_STAGE_T) else 0,
+                           ptr(t_dev), s)
+        if t_dev is not None:
+            E.gbdt_stage_tick(t_dev.data_ptr(), s)
+        if group is not None and (t_dev is not None or t <= st.T):
             # stage t's histogram + root Σw r² + previous tree's leaf Σw r² + deviance + bag count:
             # ONE exact int64 SUM per stage (SURVEY.md §5.8 R1/R2 merged)
-            k = t % 3
+            k = host_t % 3
             import torch.distributed as dist
             dist.all_reduce(comm[k * slot:(k + 1) * slot], op=dist.ReduceOp.SUM, group=group)
-            n_coll += 1
+            n_coll[0] += 1
+
+    t0 = time.perf_counter()
+    units = _graph_units(st, group, prof)
+    if units:
+        # HIP graph of one 3-stage unit (stage kernel [+ partial reduce] + counter tick [+ the
+        # stage's all-reduce], × 3 — the comm slots rotate with period 3), captured once per fit
+        # on a side stream and replayed for t = 0 … 3·units−1; the stage index comes from device
+        # memory, so every replay advances the boosting.  The last stages run eagerly.
+        tdev = runtime.workspace(dev, "gbdt_stage_t", 1, torch.int32)
+        tdev.zero_()
+        cap = runtime.stream(dev, "gbdt_graph")
+        cur = torch.cuda.current_stream(dev)
+        cap.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cap):
+            s = ops.stream_ptr(dev)
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                for k in range(3):
+                    stage(k, k, tdev)
+            finally:
+                g.capture_end()
+        s = ops.stream_ptr(dev)
+        for _ in range(units):
+            g.replay()
+        n_coll[0] = 3 * units if group is not None else 0   # the capture issued one unit's worth
+        GRAPH_INFO.update(units=units, nodes_per_unit=3, stages_eager=st.T + 2 - 3 * units)
+        start = 3 * units
+        keep_graph = g
+    else:
+        start = 0
+        keep_graph = None
+        GRAPH_INFO.update(units=0, stages_eager=st.T + 2)
+    for t in range(start, st.T + 2):
+        stage(t, t)
+    GRAPH_INFO["host_s"] = time.perf_counter() - t0
+    if keep_graph is not None:
+        # the graph's launches must not outlive it: keep it referenced until the work is done
+        _GRAPH_KEEP.append((keep_graph, torch.cuda.Event()))
+        _GRAPH_KEEP[-1][1].record()
+        _prune_graphs()
+    n_coll = n_coll[0]
     COLLECTIVES["per_stage"] = n_coll / (st.T + 1) if group is not None else 0.0
     if prof is not None:
         LAST_STAGE_PROF["stamps"] = prof.view(-1, 6).cpu().numpy()

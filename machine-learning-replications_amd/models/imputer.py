@@ -51,52 +51,115 @@ class KNNImputer(Estimator):
         return self.fit(X).transform(X)
 
     def transform(self, X):
-        X = as_tensor(X, device=self._fit_X.device).clone()
-        miss = torch.isnan(X)
-        rows = torch.nonzero(miss.any(1)).squeeze(1)
-        if rows.numel() > 0:
-            if X.is_cuda and self.n_neighbors == 1:
-                self._impute_device(X, miss, rows)
-            else:
+        return self.transform_many([X])[0]
+
+    def transform_many(self, Xs, streams=None):
+        """Impute several matrices with ONE device→host read for all of them (the per-row
+        missing-column bitmasks).  ``streams[i]`` (device path): the stream matrix i's donor
+        search is queued on (it waits for the current stream first)."""
+        Xs = [as_tensor(X, device=self._fit_X.device).clone() for X in Xs]
+        if Xs and Xs[0].is_cuda and self.n_neighbors == 1:
+            return self._impute_device_many(Xs, streams)
+        for X in Xs:
+            miss = torch.isnan(X)
+            rows = torch.nonzero(miss.any(1)).squeeze(1)
+            if rows.numel() > 0:
                 self._impute_host(X, miss, rows)
-        return X[:, self._valid]
+        return [X[:, self._valid] for X in Xs]
 
     # ------------------------------------------------------------------ device
-    def _impute_device(self, X, miss, rows):
-        from .. import ops
-        E = ops.ext()
-        F = X.shape[1]
+    def _fit_prep(self):
+        """Donor-side operands of the kernel (centred f32 rows, missing-column bitmasks), built
+        once per fit and shared by every transform."""
+        pr = getattr(self, "_prep", None)
+        if pr is None or pr[0] is not self._fit_X:
+            D = torch.where(self._mask_fit, torch.zeros_like(self._fit_X), self._fit_X)
+            center = self._col_mean  # centring improves f32 accuracy; distances are shift-invariant
+            D32 = (D - center).where(~self._mask_fit, torch.zeros_like(D)).to(torch.float32).contiguous()
+            dm = _masks_u64(self._mask_fit).contiguous()
+            pr = self._prep = (self._fit_X, D32, dm)
+        return pr[1], pr[2]
+
+    def _impute_device_many(self, Xs, streams):
+        """The (row, column) work lists are built with numpy from the bitmasks and uploaded
+        non-blocking, so the donor launches and the scatters queue without further host
+        synchronisation."""
+        F = Xs[0].shape[1]
         if F > 64:
             raise ValueError("KNNImputer device path supports at most 64 features")
-        D = torch.where(self._mask_fit, torch.zeros_like(self._fit_X), self._fit_X)
-        center = self._col_mean  # centring improves f32 accuracy; distances are shift-invariant
-        D32 = (D - center).where(~self._mask_fit, torch.zeros_like(D)).to(torch.float32).contiguous()
-        dm = _masks_u64(self._mask_fit).contiguous()
-        Rm = miss[rows]
-        R = torch.where(Rm, torch.zeros_like(X[rows]), X[rows] - center)
-        R32 = R.to(torch.float32).contiguous()
-        rm = _masks_u64(Rm).contiguous()
-        nmiss = Rm.sum(1)
-        order = torch.argsort((~Rm).to(torch.int8), dim=1, stable=True)   # missing columns first
-        max_m = int(nmiss.max())
-        for s0 in range(0, max_m, SLOTS):
-            cols = order[:, s0:s0 + SLOTS]
-            if cols.shape[1] < SLOTS:
-                cols = torch.cat([cols, torch.zeros(cols.shape[0], SLOTS - cols.shape[1], dtype=cols.dtype,
-                                                    device=cols.device)], 1)
-            k = torch.arange(s0, s0 + SLOTS, device=X.device)
-            valid = k[None, :] < nmiss[:, None]
-            slot = torch.where(valid, cols, torch.full_like(cols, -1)).to(torch.int32).contiguous()
-            best = torch.empty(slot.shape, dtype=torch.int64, device=X.device)
-            E.knn_donors(R32.data_ptr(), rm.data_ptr(), rows.numel(), D32.data_ptr(), dm.data_ptr(),
-                         D32.shape[0], F, slot.data_ptr(), best.data_ptr(), ops.stream_ptr(X.device))
-            # packed (d² float bits << 32 | donor); all-ones = no donor with a defined distance
-            donor = torch.where(best == -1, torch.full_like(best, -1), best & 0xFFFFFFFF)
-            r_idx = rows[:, None].expand_as(slot)[valid]
-            c_idx = slot[valid].long()
-            donor = donor[valid]
-            vals = torch.where(donor >= 0, self._fit_X[donor.clamp(min=0), c_idx], self._col_mean[c_idx])
-            X[r_idx, c_idx] = vals
+        host = torch.cat([_masks_u64(torch.isnan(X)) for X in Xs] + [self._valid.to(torch.int64)]).cpu().numpy()
+        bits_all = host[:-F].view(np.uint64)
+        from .smo import _to_dev
+        dev = Xs[0].device
+        keep = _to_dev(np.nonzero(host[-F:])[0].astype(np.int64), dev)   # columns with a fit value
+        D32, dm = self._fit_prep()
+        main = torch.cuda.current_stream(dev)
+        off, out = 0, []
+        for i, X in enumerate(Xs):
+            bits = bits_all[off:off + X.shape[0]]
+            off += X.shape[0]
+            st = streams[i] if streams is not None and streams[i] is not None else None
+            if st is None:
+                self._impute_device(X, bits, D32, dm)
+                out.append(X.index_select(1, keep))
+            else:
+                # everything that touches X — the imputation AND the column selection — is queued
+                # on st; the caller joins st before reading the result
+                st.wait_stream(main)
+                # X, keep and the fit operands were allocated on the current stream: without
+                # record_stream their blocks could be handed to new current-stream tensors while st
+                # still reads / writes them
+                for t in (X, keep, D32, dm, self._fit_X, self._col_mean):
+                    t.record_stream(st)
+                with torch.cuda.stream(st):
+                    self._impute_device(X, bits, D32, dm)
+                    out.append(X.index_select(1, keep))
+        return out
+
+    def _impute_device(self, X, bits, D32, dm):
+        from .. import ops
+        from .smo import _to_dev
+        E = ops.ext()
+        n, F = X.shape
+        rows_np = np.nonzero(bits)[0]
+        if rows_np.size == 0:
+            return
+        center = self._col_mean
+        Rm_np = ((bits[rows_np, None] >> np.arange(F, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+        rl, cc = np.nonzero(Rm_np)                       # missing cells, row-major, columns ascending
+        nm = Rm_np.sum(1)
+        start = np.concatenate([[0], np.cumsum(nm)[:-1]])
+        kk = np.arange(rl.shape[0]) - start[rl]          # slot of each cell within its row
+        nslot = -(-int(nm.max()) // SLOTS) * SLOTS
+        slot_all = np.full((rows_np.shape[0], nslot), -1, dtype=np.int32)
+        slot_all[rl, kk] = cc
+        dev = X.device
+        # every index array in ONE pinned host buffer → one H2D copy, sliced on the device
+        nr, nc = rows_np.shape[0], rl.shape[0]
+        parts = [rows_np, Rm_np.reshape(-1), bits[rows_np].view(np.int64), slot_all.reshape(-1),
+                 rl * nslot + kk, rows_np[rl], cc]
+        sizes = [a.shape[0] for a in parts]
+        buf = _to_dev(np.concatenate([a.astype(np.int64, copy=False) for a in parts]), dev)
+        o = np.concatenate([[0], np.cumsum(sizes)])
+        rows, Rm, rm, slot_dev, flat, r_idx, c_idx = (buf[o[i]:o[i + 1]] for i in range(7))
+        Rm = (Rm != 0).view(nr, F)
+        slot_dev = slot_dev.view(nr, nslot).to(torch.int32)
+        Xr = X.index_select(0, rows)
+        R32 = torch.where(Rm, torch.zeros_like(Xr), Xr - center).to(torch.float32).contiguous()
+        rm = rm.contiguous()
+        best = torch.empty(nr, nslot, dtype=torch.int64, device=dev)
+        for s0 in range(0, nslot, SLOTS):
+            slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
+            blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)
+            E.knn_donors(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(),
+                         D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), ops.stream_ptr(dev))
+            if nslot != SLOTS:
+                best[:, s0:s0 + SLOTS] = blk
+        # packed (d² float bits << 32 | donor); all-ones = no donor with a defined distance
+        b = best.view(-1).index_select(0, flat)
+        donor = torch.where(b == -1, torch.full_like(b, -1), b & 0xFFFFFFFF)
+        vals = torch.where(donor >= 0, self._fit_X[donor.clamp(min=0), c_idx], self._col_mean[c_idx])
+        X.index_put_((r_idx, c_idx), vals)
 
     # ------------------------------------------------------------------ host
     def _impute_host(self, X, miss, rows):

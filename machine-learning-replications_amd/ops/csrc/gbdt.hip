@@ -898,6 +898,7 @@ struct StageJob {
   long long ldb;                      // row stride of bins (≥ n, multiple of 1024: 16-byte lane loads)
   long long* partials;                // [B][G][3·hist_len + kSgExtra] per-workgroup slots, or nullptr
   long long* prof;                    // diagnostics: [B][G][6] s_memtime phase stamps, or nullptr
+  const int* t_dev;                   // stage index read from device memory (graph replay), or nullptr: t
 };
 
 template <int NV>
@@ -975,7 +976,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   __shared__ int pf_s, pblo_s;
   __shared__ double pv_s[3];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = J.n, F = J.F, B = J.B, t = J.t, T = J.T;
+  const int n = J.n, F = J.F, B = J.B, t = J.t_dev != nullptr ? *J.t_dev : J.t, T = J.T;
   const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
   const size_t slot_sz = (size_t)B * slot_m;
   long long* slot_prev = J.comm + (size_t)((t + 2) % 3) * slot_sz + (size_t)b * slot_m;
@@ -1306,7 +1307,7 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
                       uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t dev,
                       uintptr_t bagw, uintptr_t frank, uintptr_t partials, long long partials_len, double lr,
                       double qscale, double dscale, double min_leaf_q, double min_split_q, uintptr_t prof,
-                      uintptr_t stream) {
+                      uintptr_t t_dev, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stump_stage: 1 <= F <= 128");
   HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
   const bool active = subsample < 1.0;
@@ -1318,7 +1319,9 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
              (long long*)comm, (int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
              (long long*)r2, (long long*)dev, (double*)bagw, (const int*)frank, row_off, lr, qscale, dscale,
              min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
-             hist_len, t, 0, ldb, (long long*)partials, (long long*)prof};
+             hist_len, t, 0, ldb, (long long*)partials, (long long*)prof, (const int*)t_dev};
+  // t_dev (graph replay): the kernel takes the stage index from device memory; the host t still
+  // selects the comm slot of the reduce launch, so a captured unit must start at t ≡ 0 (mod 3)
   HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");
   // rows per workgroup: 1024-row sub-tiles, as many per workgroup as keeps the grid near 2
   // workgroups per CU (the redundant split and the histogram flush are per workgroup)
@@ -1341,6 +1344,16 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
                        as_stream(stream), (const long long*)J.partials, slot, groups, slot_m);
     launch_check();
   }
+}
+
+// Advance the device stage counter read by graph-replayed gbdt_stump_stage launches.
+__global__ void gbdt_stage_tick_kernel(int* t) {
+  if (threadIdx.x == 0) t[0] = t[0] + 1;
+}
+
+void gbdt_stage_tick(uintptr_t t_dev, uintptr_t stream) {
+  hipLaunchKernelGGL(gbdt_stage_tick_kernel, dim3(1), dim3(64), 0, as_stream(stream), (int*)t_dev);
+  launch_check();
 }
 
 }  // namespace hfens

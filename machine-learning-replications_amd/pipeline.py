@@ -75,8 +75,15 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(X_dev)
         else:
             imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(pdist.all_gather_rows(X_dev, group))
-        X_dev = imputer.transform(X_dev)          # this rank's rows: the O(n²) donor search is sharded
-        X_sel = imputer.transform(X_sel)
+        # this rank's rows (the O(n²) donor search is sharded) and the held-out rows, planned from
+        # ONE host read; the held-out rows are only needed for the evaluation, so on the GPU
+        # their donor search runs on a side stream, overlapped with LassoCV and the stacking fit
+        # (joined before the evaluation below)
+        aux = None
+        if dev.type == "cuda":
+            from . import runtime
+            aux = runtime.stream(dev, "aux")
+        X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
@@ -86,10 +93,14 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         mask = sfm.get_support()
         mt = torch.as_tensor(mask, device=dev)
         X_dev_optm = X_dev[:, mt]
-        X_sel_optm = X_sel[:, mt]
         fn_new = [n for n, m in zip(names, mask) if m]
     clf = build_estimators(cfg)
     clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None)
+    if aux is not None:
+        # join the side stream while the imputer and X_sel are alive (their blocks are not reused
+        # by the main stream before this point)
+        torch.cuda.current_stream(dev).wait_stream(aux)
+    X_sel_optm = X_sel[:, mt]
     proba = None
     report = ""
     scores: Dict[str, float] = {}

@@ -251,6 +251,57 @@ def test_gbdt_stage_data_parallel_bit_identical(dev):
         assert np.array_equal(ts, m.train_score_.cpu().numpy())
 
 
+def _gbdt_outputs(ms):
+    return [(m.tree_feature_.cpu().numpy(), m.tree_threshold_.cpu().numpy(), m.tree_value_.cpu().numpy(),
+             m.tree_impurity_.cpu().numpy(), m.train_score_.cpu().numpy()) for m in ms]
+
+
+@pytest.mark.parametrize("T,subsample", [(20, 1.0), (100, 0.8)])
+def test_gbdt_stage_graph_bit_identical(dev, monkeypatch, T, subsample):
+    """The HIP-graph stage loop (3-stage units replayed with a device stage counter) gives the
+    eager loop's model bit for bit."""
+    from hfens.models import hist_gbdt
+    X, y = _data(20000, 17, 61)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(hist_gbdt, "STAGE_GRAPH", mode)
+        ms = [GradientBoostingClassifier(n_estimators=T, max_depth=1, subsample=subsample, random_state=s)
+              for s in (3, 4)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev))
+        assert hist_gbdt.LAST_PATH["path"] == "stage"
+        assert hist_gbdt.GRAPH_INFO["units"] == (0 if mode == "0" else (T + 1) // 3)
+        out[mode] = _gbdt_outputs(ms)
+    for a, b in zip(out["0"], out["1"]):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
+def test_gbdt_stage_graph_rccl_world1(dev):
+    """The RCCL branch (backend "nccl") on a one-rank group: its per-stage all-reduces are captured
+    in the stage graph, one collective per stage, and the model equals the single-process fit."""
+    import tempfile
+    import torch.distributed as dist
+    from hfens.models import hist_gbdt
+    store = tempfile.mktemp(prefix="hfens_pg_")   # file store: no TCP port to race for
+    dist.init_process_group("nccl", init_method=f"file://{store}", rank=0, world_size=1,
+                            device_id=torch.device(dev))
+    try:
+        g = dist.new_group([0], backend="nccl")
+        X, y = _data(9000, 17, 53)
+        ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev), group=g)
+        assert hist_gbdt.LAST_PATH["path"] == "stage" and hist_gbdt.COLLECTIVES["per_stage"] == 1.0
+        assert hist_gbdt.GRAPH_INFO["units"] == 31 // 3
+        got = _gbdt_outputs(ms)
+    finally:
+        dist.destroy_process_group()
+    ref = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+    fit_gbdt_batch(ref, X.to(dev), y.to(dev))
+    for a, b in zip(got, _gbdt_outputs(ref)):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
 def test_binned_stump_tables_match_tree_walk(dev):
     from hfens.models.forest_infer import ensemble_raw_binned, stump_bin_tables
     X, y = _data(5003, 24, 41)
