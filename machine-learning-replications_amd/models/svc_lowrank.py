@@ -41,6 +41,8 @@ import os
 import numpy as np
 import torch
 
+from .. import ops
+
 N_LANDMARKS = int(os.environ.get("HFENS_SVC_LANDMARKS", "512"))
 IPM_MAX_ITER = 80
 IPM_TOL = 1e-8
@@ -123,6 +125,15 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     b = torch.zeros((), dtype=dt, device=Phi.device)
     eye = torch.eye(r, dtype=dt, device=Phi.device)
     csum = float(c.sum())
+    # on the GPU the r × r factor / solves are the native single-workgroup kernels (ops/csrc/
+    # linalg.hip: equilibration and jitter retries on the device, no library workspace, no host
+    # read of `info`); the host path keeps torch.linalg
+    native = Phi.is_cuda and ops.has_ext()
+    if native:
+        E = ops.ext()
+        Lc = torch.empty(r, r, dtype=dt, device=Phi.device)
+        scv = torch.empty(r, dtype=dt, device=Phi.device)
+        info = torch.zeros(1, dtype=torch.int32, device=Phi.device)
     it = 0
     for it in range(1, max_iter + 1):
         s = c - a
@@ -131,7 +142,11 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         rd = g + b * y - nu + mu
         re = torch.dot(y, a)
         gap = (torch.dot(a, nu) + torch.dot(s, mu)) / (2 * l)
-        chk = torch.stack([gap, rd.abs().max(), re.abs()]).cpu()
+        parts = [gap, rd.abs().max(), re.abs()] + ([info[0].to(dt)] if native else [])
+        chk = torch.stack(parts).cpu()
+        if native and float(chk[3]) < 0:
+            raise FloatingPointError("interior-point SVC: Woodbury system not positive definite "
+                                     "even with 1e-6 jitter")
         if float(chk[0]) < tol and float(chk[1]) < 1e-8 and float(chk[2]) < 1e-8 * csum:
             break
         D = nu / a + mu / s
@@ -140,17 +155,28 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         # many decades: equilibrate symmetrically before the Cholesky (exact); a relative jitter on
         # the unit diagonal is added only if it still fails.
         S = eye + _weighted_gram(Phi, Dinv)
-        sc = torch.rsqrt(torch.diagonal(S))
-        Ss = S * sc[:, None] * sc[None, :]
-        Lc, info = torch.linalg.cholesky_ex(Ss)
-        jit = 1e-14
-        while int(info) != 0 and jit < 1e-6:
-            Lc, info = torch.linalg.cholesky_ex(Ss + jit * eye)
-            jit *= 100.0
+        if native:
+            E.chol_spd(S.contiguous().data_ptr(), r, Lc.data_ptr(), scv.data_ptr(), info.data_ptr(),
+                       ops.stream_ptr(Phi.device))
+        else:
+            sc = torch.rsqrt(torch.diagonal(S))
+            Ss = S * sc[:, None] * sc[None, :]
+            Lc, inf = torch.linalg.cholesky_ex(Ss)
+            jit = 1e-14
+            while int(inf) != 0 and jit < 1e-6:
+                Lc, inf = torch.linalg.cholesky_ex(Ss + jit * eye)
+                jit *= 100.0
 
         def Minv(u):  # (D + V Vᵀ)⁻¹ u for u [l, k], V = YΦ
             du = Dinv[:, None] * u
-            t = sc[:, None] * torch.cholesky_solve(sc[:, None] * _phit(Phi, y[:, None] * du), Lc)
+            rhs = _phit(Phi, y[:, None] * du)
+            if native:
+                rhs = rhs.contiguous()
+                E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, rhs.shape[1], rhs.data_ptr(),
+                             ops.stream_ptr(Phi.device))
+                t = rhs
+            else:
+                t = sc[:, None] * torch.cholesky_solve(sc[:, None] * rhs, Lc)
             return du - Dinv[:, None] * (y[:, None] * (Phi @ t))
 
         def dirs(Mh, My, yMy, rnu, rmu):

@@ -1,0 +1,228 @@
+// Small dense SPD factor / solve for the interior-point SVC (models/svc_lowrank.py): the r × r
+// Woodbury system S = I + Φᵀ D⁻¹ Φ (r ≤ 1024 landmarks) is factored every IPM iteration.
+//
+// Library potrf/potrs stalled the solve: the profile of one 1M-row solve (profiles/
+// r2_ipm_native.md) shows 5–14 ms GPU-idle gaps before rocSOLVER/rocBLAS kernels (their workspace
+// handling) and a blocking read of potrf's `info` every iteration.  Here:
+//
+//  chol_spd  : ONE workgroup (1024 threads), r ≤ 1024.  Symmetric equilibration sc = diag(S)^-½,
+//              then a right-looking blocked Cholesky of sc·S·sc (+ jit·I) into L (row-major, lower
+//              triangle): NB-column diagonal blocks (NB = 32, 16 above r = 512) factored in LDS by
+//              all threads, the panel below solved one row per thread into a transposed LDS copy,
+//              the trailing lower triangle updated from it by all 16 waves.  A non-positive or non-finite pivot
+//              restarts the factorisation from S with jit = 1e-14, 1e-12, … 1e-6 — on the device,
+//              so the host never reads `info`.  out_info[0] = retries used (−1 = still failed).
+//  chol_solve: x = sc ∘ (L Lᵀ)⁻¹ (sc ∘ b) for k ≤ 4 right-hand sides, one workgroup: blocked
+//              forward / backward substitution, 64-row diagonal blocks solved by wave 0 (readlane
+//              chain), the off-diagonal updates by all threads.
+#include "common.h"
+
+namespace hfens {
+
+constexpr int kChThreads = 1024;
+constexpr int kChWaves = kChThreads / 64;
+constexpr int kChNB = 64;   // solve block (wave 0 substitution chains)
+constexpr int kChMaxK = 4;
+
+__device__ __forceinline__ double ch_readlane(double v, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, lane);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+size_t chol_spd_lds(int r, int NB) { return ((size_t)NB * (NB + 1) + (size_t)NB * r + NB) * sizeof(double); }
+
+// LDS: Dg [NB][NB+1] the diagonal block; PT [NB][r] the panel, TRANSPOSED (lanes of a wave read
+// consecutive rows: conflict-free), dgl [NB] the block's pivots.
+template <int NB>
+__global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __restrict__ S, int r,
+                                                              double* __restrict__ L, double* __restrict__ sc,
+                                                              int* __restrict__ out_info) {
+  extern __shared__ __attribute__((aligned(16))) double chsm[];
+  double* Dg = chsm;
+  double* PT = Dg + NB * (NB + 1);
+  double* dgl = PT + (size_t)NB * r;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < r; i += kChThreads) {
+    const double d = S[(size_t)i * r + i];
+    sc[i] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
+  }
+  __syncthreads();
+  double jit = 0.0;
+  int tries = 0;
+  for (;;) {
+    // L ← lower triangle of sc·S·sc + jit·I (upper triangle zeroed: potrf's output convention)
+    for (size_t e = tid; e < (size_t)r * r; e += kChThreads) {
+      const int i = (int)(e / r), j = (int)(e % r);
+      L[e] = j <= i ? S[e] * sc[i] * sc[j] + (i == j ? jit : 0.0) : 0.0;
+    }
+    __syncthreads();
+    bool bad = false;
+    for (int k0 = 0; k0 < r && !bad; k0 += NB) {
+      const int nb = min(NB, r - k0), m0 = k0 + nb, m = r - m0;
+      for (int e = tid; e < nb * nb; e += kChThreads) {
+        const int a = e / nb, b = e % nb;
+        Dg[a * (NB + 1) + b] = b <= a ? L[(size_t)(k0 + a) * r + k0 + b] : 0.0;
+      }
+      __syncthreads();
+      // ---- diagonal block, right-looking, all threads (the pivot test is uniform)
+      for (int j = 0; j < nb; ++j) {
+        const double pj = Dg[j * (NB + 1) + j];
+        if (!(pj > 0.0) || !isfinite(pj)) { bad = true; break; }
+        const double dj = sqrt(pj);
+        for (int a = j + 1 + tid; a < nb; a += kChThreads) Dg[a * (NB + 1) + j] /= dj;
+        if (tid == 0) dgl[j] = dj;
+        __syncthreads();
+        for (int a = j + 1 + wave; a < nb; a += kChWaves)
+          for (int b = j + 1 + lane; b <= a; b += 64)
+            Dg[a * (NB + 1) + b] -= Dg[a * (NB + 1) + j] * Dg[b * (NB + 1) + j];
+        __syncthreads();
+      }
+      if (bad) break;
+      for (int j = tid; j < nb; j += kChThreads) Dg[j * (NB + 1) + j] = dgl[j];
+      __syncthreads();
+      for (int e = tid; e < nb * nb; e += kChThreads) {
+        const int a = e / nb, b = e % nb;
+        if (b <= a) L[(size_t)(k0 + a) * r + k0 + b] = Dg[a * (NB + 1) + b];
+      }
+      // ---- panel: row m0+t ← A[m0+t][k0:k0+nb] · L_blockᵀ⁻¹ (one row per thread)
+      for (int t = tid; t < m; t += kChThreads) {
+        double x[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) x[b] = b < nb ? L[(size_t)(m0 + t) * r + k0 + b] : 0.0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          if (b < nb) {
+            double v = x[b];
+#pragma unroll
+            for (int p = 0; p < b; ++p) v -= x[p] * Dg[b * (NB + 1) + p];
+            x[b] = v / Dg[b * (NB + 1) + b];
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          if (b < nb) {
+            L[(size_t)(m0 + t) * r + k0 + b] = x[b];
+            PT[(size_t)b * r + t] = x[b];
+          }
+      }
+      __syncthreads();
+      // ---- trailing lower triangle: A[m0+i][m0+j] −= Σ_b PT[b][i]·PT[b][j], j ≤ i (waves take
+      //      rows, lanes take columns; each lane keeps 2 rows: PT[b][j] read once per 2 FMAs)
+      for (int i = 2 * wave; i < m; i += 2 * kChWaves) {
+        const int i2 = i + 1;
+        for (int j = lane; j <= (i2 < m ? i2 : i); j += 64) {
+          double a0 = 0.0, a1 = 0.0;
+          for (int b = 0; b < nb; ++b) {
+            const double pj = PT[(size_t)b * r + j];
+            a0 = fma(PT[(size_t)b * r + i], pj, a0);
+            if (i2 < m) a1 = fma(PT[(size_t)b * r + i2], pj, a1);
+          }
+          if (j <= i) L[(size_t)(m0 + i) * r + m0 + j] -= a0;
+          if (i2 < m) L[(size_t)(m0 + i2) * r + m0 + j] -= a1;
+        }
+      }
+      __syncthreads();
+    }
+    if (!bad) break;
+    ++tries;
+    jit = jit == 0.0 ? 1e-14 : jit * 100.0;
+    if (jit > 1e-6) {
+      if (tid == 0) out_info[0] = -1;
+      return;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) out_info[0] = tries;
+}
+
+// x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.
+__global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __restrict__ L, const double* __restrict__ sc,
+                                                                int r, int k, double* __restrict__ B) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < r * k; e += kChThreads) B[e] *= sc[e / k];
+  __syncthreads();
+  // forward: L y = b
+  for (int k0 = 0; k0 < r; k0 += kChNB) {
+    const int nb = min(kChNB, r - k0);
+    if (wave == 0) {
+      double y[kChMaxK];
+      for (int q = 0; q < kChMaxK; ++q) y[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
+      for (int j = 0; j < nb; ++j) {
+        const double ljj = lane == j ? L[(size_t)(k0 + j) * r + k0 + j] : 1.0;
+        const double lij = (lane > j && lane < nb) ? L[(size_t)(k0 + lane) * r + k0 + j] : 0.0;
+        for (int q = 0; q < k; ++q) {
+          if (lane == j) y[q] /= ljj;
+          const double yj = ch_readlane(y[q], j);
+          if (lane > j) y[q] -= lij * yj;
+        }
+      }
+      if (lane < nb)
+        for (int q = 0; q < k; ++q) B[(size_t)(k0 + lane) * k + q] = y[q];
+    }
+    __syncthreads();
+    for (int i = k0 + nb + tid; i < r; i += kChThreads) {
+      const double* li = L + (size_t)i * r + k0;
+      for (int q = 0; q < k; ++q) {
+        double acc = 0.0;
+        for (int b = 0; b < nb; ++b) acc = fma(li[b], B[(size_t)(k0 + b) * k + q], acc);
+        B[(size_t)i * k + q] -= acc;
+      }
+    }
+    __syncthreads();
+  }
+  // backward: Lᵀ x = y (blocks from the bottom)
+  const int nblk = (r + kChNB - 1) / kChNB;
+  for (int bi = nblk - 1; bi >= 0; --bi) {
+    const int k0 = bi * kChNB, nb = min(kChNB, r - k0);
+    if (wave == 0) {
+      double x[kChMaxK];
+      for (int q = 0; q < kChMaxK; ++q) x[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
+      for (int j = nb - 1; j >= 0; --j) {
+        const double ljj = lane == j ? L[(size_t)(k0 + j) * r + k0 + j] : 1.0;
+        // Lᵀ[lane][j] = L[j][lane] for lane < j
+        const double lji = lane < j ? L[(size_t)(k0 + j) * r + k0 + lane] : 0.0;
+        for (int q = 0; q < k; ++q) {
+          if (lane == j) x[q] /= ljj;
+          const double xj = ch_readlane(x[q], j);
+          if (lane < j) x[q] -= lji * xj;
+        }
+      }
+      if (lane < nb)
+        for (int q = 0; q < k; ++q) B[(size_t)(k0 + lane) * k + q] = x[q];
+    }
+    __syncthreads();
+    // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j
+    for (int i = tid; i < k0; i += kChThreads) {
+      for (int q = 0; q < k; ++q) {
+        double acc = 0.0;
+        for (int b = 0; b < nb; ++b) acc = fma(L[(size_t)(k0 + b) * r + i], B[(size_t)(k0 + b) * k + q], acc);
+        B[(size_t)i * k + q] -= acc;
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < r * k; e += kChThreads) B[e] *= sc[e / k];
+}
+
+void chol_spd(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uintptr_t stream) {
+  HFENS_REQUIRE(r >= 1 && r <= 1024, "chol_spd: 1 <= r <= 1024");
+  if (r <= 512) {
+    hipLaunchKernelGGL(chol_spd_kernel<32>, dim3(1), dim3(kChThreads), chol_spd_lds(r, 32), as_stream(stream),
+                       (const double*)S, r, (double*)L, (double*)sc, (int*)info);
+  } else {
+    hipLaunchKernelGGL(chol_spd_kernel<16>, dim3(1), dim3(kChThreads), chol_spd_lds(r, 16), as_stream(stream),
+                       (const double*)S, r, (double*)L, (double*)sc, (int*)info);
+  }
+  launch_check();
+}
+
+void chol_solve(uintptr_t L, uintptr_t sc, int r, int k, uintptr_t B, uintptr_t stream) {
+  HFENS_REQUIRE(r >= 1 && r <= 1024 && k >= 1 && k <= kChMaxK, "chol_solve: 1 <= r <= 1024, 1 <= k <= 4");
+  hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(kChThreads), 0, as_stream(stream), (const double*)L,
+                     (const double*)sc, r, k, (double*)B);
+  launch_check();
+}
+
+}  // namespace hfens

@@ -32,7 +32,16 @@ def main():
     Phi, T = nystrom_map(Z, idx, 1 / 17)
     torch.cuda.synchronize()
     print(f"rows {n} landmarks {m}: nystrom map {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
+    only_ipm = len(sys.argv) > 3 and sys.argv[3] == "ipm-only"
     d = torch.rand(n, device=dev, dtype=torch.float64)
+    if only_ipm:
+        c = torch.where(y > 0, 0.625, 2.5).to(torch.float64)
+        t0 = time.perf_counter()
+        a, rho, it = ipm_svc_dual(Phi, y, c)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"  ipm solve {1e3 * dt:.1f} ms, {it} iterations ({1e3 * dt / it:.2f} ms/iter), rho {rho:.4f}", flush=True)
+        return
     print(f"  weighted gram (split-K) {tm(lambda: _weighted_gram(Phi, d)):.2f} ms", flush=True)
     print(f"  weighted gram (one GEMM) {tm(lambda: Phi.T @ (d[:, None] * Phi)):.2f} ms", flush=True)
     S = torch.eye(Phi.shape[1], device=dev, dtype=torch.float64) + _weighted_gram(Phi, d)

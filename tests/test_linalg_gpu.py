@@ -1,0 +1,60 @@
+"""Native single-workgroup SPD factor / solve (ops/csrc/linalg.hip) vs torch.linalg in f64: the
+interior-point SVC's r × r Woodbury systems (equilibrated, jitter retries on the device)."""
+import pytest
+import torch
+
+from hfens import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _spd(r, cond_decades, seed):
+    g = torch.Generator().manual_seed(seed)
+    Q, _ = torch.linalg.qr(torch.randn(r, r, generator=g, dtype=torch.float64))
+    ev = torch.logspace(0, cond_decades, r, dtype=torch.float64)
+    S = (Q * ev) @ Q.T
+    # badly scaled rows/columns, as I + ΦᵀD⁻¹Φ near the end of the interior-point solve
+    dsc = torch.logspace(-4, 4, r, dtype=torch.float64)[torch.randperm(r, generator=g)]
+    return dsc[:, None] * S * dsc[None, :]
+
+
+@pytest.mark.parametrize("r", [1, 17, 33, 64, 65, 200, 512, 600, 1024])
+def test_chol_spd_and_solve_match_torch(dev, r):
+    E = ops.ext()
+    S = _spd(r, 8, r).to(dev)
+    L = torch.empty(r, r, dtype=torch.float64, device=dev)
+    sc = torch.empty(r, dtype=torch.float64, device=dev)
+    info = torch.full((1,), 99, dtype=torch.int32, device=dev)
+    E.chol_spd(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), ops.stream_ptr(dev))
+    assert int(info) == 0
+    # L is the Cholesky factor of the equilibrated matrix
+    Ss = S * sc[:, None] * sc[None, :]
+    assert torch.allclose(L @ L.T, Ss, atol=1e-10, rtol=0)
+    assert torch.equal(torch.triu(L, 1), torch.zeros_like(L))
+    for k in (1, 2, 3):
+        B = torch.randn(r, k, dtype=torch.float64, device=dev)
+        X = B.clone()
+        E.chol_solve(L.data_ptr(), sc.data_ptr(), r, k, X.data_ptr(), ops.stream_ptr(dev))
+        # the same factor through torch's triangular solves
+        want = sc[:, None] * torch.cholesky_solve(sc[:, None] * B, L)
+        assert float((X - want).abs().max() / want.abs().max()) < 1e-9
+        # backward error on the equilibrated system (what the Woodbury step needs)
+        Y = X / sc[:, None]
+        res = (Ss @ Y - sc[:, None] * B).abs().max() / (Ss.abs().max() * Y.abs().max())
+        assert float(res) < 1e-13, float(res)
+
+
+def test_chol_spd_jitter_retry_on_semidefinite(dev):
+    """A rank-deficient PSD matrix fails the plain factorisation; the kernel retries with jitter on
+    the device and reports how many retries it took."""
+    E = ops.ext()
+    r = 96
+    A = torch.randn(r, 40, dtype=torch.float64)
+    S = (A @ A.T).to(dev)                   # rank 40
+    L = torch.empty(r, r, dtype=torch.float64, device=dev)
+    sc = torch.empty(r, dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    E.chol_spd(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), ops.stream_ptr(dev))
+    assert int(info) >= 1
+    Ss = S * sc[:, None] * sc[None, :]
+    assert torch.allclose(L @ L.T, Ss, atol=1e-5)
