@@ -67,12 +67,40 @@ def nystrom_map(Z: torch.Tensor, idx: torch.Tensor, gamma: float):
 _SYRK_CHUNK = 8192
 
 
+def _native(Phi: torch.Tensor) -> bool:
+    return Phi.is_cuda and Phi.dtype == torch.float64 and Phi.is_contiguous() and ops.has_ext()
+
+
+def _wsyrk_part_len(n: int, r: int, ncu: int) -> int:
+    """Partial-tile buffer of ops/csrc/lowrank.hip wsyrk_f64 (same rule as wsyrk_groups)."""
+    nt = -(-r // 128)
+    T = nt * (nt + 1) // 2
+    G = max(1, min(-(-2 * ncu // T), -(-n // 64)))
+    return G * T * 128 * 128
+
+
+# The native f64-MFMA weighted SYRK (ops/csrc/lowrank.hip) computes only the upper tiles and never
+# materialises diag(d)·Φ, but runs at ~42 % of the f64 matrix peak: 10.4 ms per 1M × 512 product
+# against 8.1 + 1.4 ms for the split-K library bmm plus the scaled copy (profiles/r2_ipm_native.md),
+# so the library path stays the default until the kernel is tuned.
+NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
+
+
 def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     """Φᵀ diag(d) Φ as a split-K batched GEMM: a plain [r × r] GEMM over a 10⁵–10⁶-long K has
     only (r/128)² output tiles — a few dozen workgroups on a 256-CU part — so the rows are cut
     into 8192-row slabs (one batched GEMM, ~100 slabs × tiles in flight) and the slab products
-    summed."""
+    summed.  ``HFENS_WSYRK=1``: the native upper-tile f64-MFMA kernel (deterministic split-K)."""
     l, r = Phi.shape
+    if NATIVE_SYRK and _native(Phi) and r <= 2048:
+        from .. import runtime
+        from .smo import _num_cus
+        plen = _wsyrk_part_len(l, r, _num_cus(Phi.device))
+        part = runtime.workspace(Phi.device, "wsyrk_part", plen, torch.float64)
+        S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
+        ops.ext().wsyrk_f64(Phi.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
+                            ops.stream_ptr(Phi.device))
+        return S
     k = l // _SYRK_CHUNK
     S = torch.zeros(r, r, dtype=Phi.dtype, device=Phi.device)
     if k > 0:
@@ -98,6 +126,18 @@ def _phit(Phi: torch.Tensor, V: torch.Tensor) -> torch.Tensor:
     if k * _SYRK_CHUNK < l:
         out += Phi[k * _SYRK_CHUNK:].T @ V[k * _SYRK_CHUNK:]
     return out
+
+
+def _phi_mv(Phi: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """Φ W for a skinny W [r, k] (k ≤ 4): GPU one native pass over Φ (ops/csrc/lowrank.hip
+    phi_gemv), else the library product."""
+    l, r = Phi.shape
+    if _native(Phi) and r <= 512 and W.shape[1] <= 4:
+        Wc = W.to(torch.float64).contiguous()
+        Y = torch.empty(l, W.shape[1], dtype=torch.float64, device=Phi.device)
+        ops.ext().phi_gemv(Phi.data_ptr(), Wc.data_ptr(), l, r, W.shape[1], Y.data_ptr(), ops.stream_ptr(Phi.device))
+        return Y
+    return Phi @ W
 
 
 def _max_step(v, dv):
@@ -138,7 +178,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     for it in range(1, max_iter + 1):
         s = c - a
         w = _phit(Phi, (y * a)[:, None])[:, 0]       # Φᵀ Y α
-        g = y * (Phi @ w) - 1.0                      # Qα − 1
+        g = y * _phi_mv(Phi, w[:, None])[:, 0] - 1.0   # Qα − 1
         rd = g + b * y - nu + mu
         re = torch.dot(y, a)
         gap = (torch.dot(a, nu) + torch.dot(s, mu)) / (2 * l)
@@ -177,7 +217,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                 t = rhs
             else:
                 t = sc[:, None] * torch.cholesky_solve(sc[:, None] * rhs, Lc)
-            return du - Dinv[:, None] * (y[:, None] * (Phi @ t))
+            return du - Dinv[:, None] * (y[:, None] * _phi_mv(Phi, t))
 
         def dirs(Mh, My, yMy, rnu, rmu):
             db = (torch.dot(y, Mh) + re) / yMy

@@ -52,6 +52,10 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k)
     if (col[k] >= 0) need |= 1ull << col[k];
+  // largest current best over the active slots: a donor at distance ≥ it can improve no slot
+  // (the slot test is strict), so the 8-slot update is skipped for it — once the bests settle,
+  // almost every donor (exact: skipping changes no comparison)
+  float bmax = INFINITY;
   for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
     __syncthreads();
     const int nt = min(kKnnTile, d_end - d0);
@@ -91,11 +95,15 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
       const int present = F - __builtin_popcountll(mr | md);
       if (present <= 0) continue;  // undefined distance (sklearn: NaN, ignored)
       const float dist = fmaxf(s, 0.f) * ((float)F / (float)present);
+      if (!(dist < bmax)) continue;
       const int di = d0 + t;
+      float m = 0.f;
 #pragma unroll
       for (int k = 0; k < kKnnSlots; ++k) {
         if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < bd[k]) { bd[k] = dist; bi[k] = di; }
+        if (col[k] >= 0) m = fmaxf(m, bd[k]);
       }
+      bmax = m;
     }
   }
   if (active) {

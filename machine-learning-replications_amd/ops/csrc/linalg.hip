@@ -9,7 +9,8 @@
 //              then a right-looking blocked Cholesky of sc·S·sc (+ jit·I) into L (row-major, lower
 //              triangle): NB-column diagonal blocks (NB = 32, 16 above r = 512) factored in LDS by
 //              all threads, the panel below solved one row per thread into a transposed LDS copy,
-//              the trailing lower triangle updated from it by all 16 waves.  A non-positive or non-finite pivot
+//              the trailing lower triangle updated from it on v_mfma_f64_16x16x4_f64 (16×16 blocks
+//              over the 16 waves; f64 MFMA maps A[l&15][l>>4], B[l>>4][l&15], C row (l>>4)+4·reg).  A non-positive or non-finite pivot
 //              restarts the factorisation from S with jit = 1e-14, 1e-12, … 1e-6 — on the device,
 //              so the host never reads `info`.  out_info[0] = retries used (−1 = still failed).
 //  chol_solve: x = sc ∘ (L Lᵀ)⁻¹ (sc ∘ b) for k ≤ 4 right-hand sides, one workgroup: blocked
@@ -18,6 +19,8 @@
 #include "common.h"
 
 namespace hfens {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kChThreads = 1024;
 constexpr int kChWaves = kChThreads / 64;
@@ -108,19 +111,31 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
           }
       }
       __syncthreads();
-      // ---- trailing lower triangle: A[m0+i][m0+j] −= Σ_b PT[b][i]·PT[b][j], j ≤ i (waves take
-      //      rows, lanes take columns; each lane keeps 2 rows: PT[b][j] read once per 2 FMAs)
-      for (int i = 2 * wave; i < m; i += 2 * kChWaves) {
-        const int i2 = i + 1;
-        for (int j = lane; j <= (i2 < m ? i2 : i); j += 64) {
-          double a0 = 0.0, a1 = 0.0;
-          for (int b = 0; b < nb; ++b) {
-            const double pj = PT[(size_t)b * r + j];
-            a0 = fma(PT[(size_t)b * r + i], pj, a0);
-            if (i2 < m) a1 = fma(PT[(size_t)b * r + i2], pj, a1);
-          }
-          if (j <= i) L[(size_t)(m0 + i) * r + m0 + j] -= a0;
-          if (i2 < m) L[(size_t)(m0 + i2) * r + m0 + j] -= a1;
+      // ---- trailing lower triangle: A[m0+i][m0+j] −= Σ_b P[i][b]·P[j][b] (j ≤ i) on the f64 matrix
+      //      cores: 16×16 output blocks (bj ≤ bi) round-robin over the 16 waves, NB/4 MFMAs each with
+      //      both operands read from the transposed panel (rows past m are zero-padded)
+      const int m16 = (m + 15) & ~15;
+      for (int e = m + tid; e < m16; e += kChThreads)
+        for (int b = 0; b < NB; ++b) PT[(size_t)b * r + e] = 0.0;
+      __syncthreads();
+      const int nbk = m16 / 16;
+      const int nblocks = nbk * (nbk + 1) / 2;
+      for (int blk = wave; blk < nblocks; blk += kChWaves) {
+        int bi = 0, rem = blk;
+        while (rem > bi) { rem -= bi + 1; ++bi; }
+        const int bj = rem;                               // 0 ≤ bj ≤ bi
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < NB / 4; ++ks) {
+          const int kb = 4 * ks + (lane >> 4);
+          const double a = PT[(size_t)kb * r + 16 * bi + (lane & 15)];
+          const double b = PT[(size_t)kb * r + 16 * bj + (lane & 15)];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * bj + (lane & 15);
+          if (i < m && j <= i) L[(size_t)(m0 + i) * r + m0 + j] -= acc[reg];
         }
       }
       __syncthreads();
@@ -137,21 +152,30 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
   if (tid == 0) out_info[0] = tries;
 }
 
-// x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.
+// x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.  Each
+// 64-row step stages its diagonal block of L in LDS (the substitution chain of wave 0 then waits on
+// LDS, not on a global load per column) and the solved block of x in LDS for the row updates.
 __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __restrict__ L, const double* __restrict__ sc,
                                                                 int r, int k, double* __restrict__ B) {
+  __shared__ double Db[kChNB][kChNB + 1];
+  __shared__ double Xb[kChNB][kChMaxK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int e = tid; e < r * k; e += kChThreads) B[e] *= sc[e / k];
   __syncthreads();
   // forward: L y = b
   for (int k0 = 0; k0 < r; k0 += kChNB) {
     const int nb = min(kChNB, r - k0);
+    for (int e = tid; e < nb * nb; e += kChThreads) {
+      const int a = e / nb, c = e % nb;
+      Db[a][c] = c <= a ? L[(size_t)(k0 + a) * r + k0 + c] : 0.0;
+    }
+    __syncthreads();
     if (wave == 0) {
       double y[kChMaxK];
       for (int q = 0; q < kChMaxK; ++q) y[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
       for (int j = 0; j < nb; ++j) {
-        const double ljj = lane == j ? L[(size_t)(k0 + j) * r + k0 + j] : 1.0;
-        const double lij = (lane > j && lane < nb) ? L[(size_t)(k0 + lane) * r + k0 + j] : 0.0;
+        const double ljj = Db[j][j];
+        const double lij = (lane > j && lane < nb) ? Db[lane][j] : 0.0;
         for (int q = 0; q < k; ++q) {
           if (lane == j) y[q] /= ljj;
           const double yj = ch_readlane(y[q], j);
@@ -159,16 +183,20 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
         }
       }
       if (lane < nb)
-        for (int q = 0; q < k; ++q) B[(size_t)(k0 + lane) * k + q] = y[q];
+        for (int q = 0; q < k; ++q) {
+          B[(size_t)(k0 + lane) * k + q] = y[q];
+          Xb[lane][q] = y[q];
+        }
     }
     __syncthreads();
     for (int i = k0 + nb + tid; i < r; i += kChThreads) {
       const double* li = L + (size_t)i * r + k0;
-      for (int q = 0; q < k; ++q) {
-        double acc = 0.0;
-        for (int b = 0; b < nb; ++b) acc = fma(li[b], B[(size_t)(k0 + b) * k + q], acc);
-        B[(size_t)i * k + q] -= acc;
+      double acc[kChMaxK] = {0.0, 0.0, 0.0, 0.0};
+      for (int b = 0; b < nb; ++b) {
+        const double l = li[b];
+        for (int q = 0; q < k; ++q) acc[q] = fma(l, Xb[b][q], acc[q]);
       }
+      for (int q = 0; q < k; ++q) B[(size_t)i * k + q] -= acc[q];
     }
     __syncthreads();
   }
@@ -176,13 +204,18 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
   const int nblk = (r + kChNB - 1) / kChNB;
   for (int bi = nblk - 1; bi >= 0; --bi) {
     const int k0 = bi * kChNB, nb = min(kChNB, r - k0);
+    for (int e = tid; e < nb * nb; e += kChThreads) {
+      const int a = e / nb, c = e % nb;
+      Db[a][c] = c <= a ? L[(size_t)(k0 + a) * r + k0 + c] : 0.0;
+    }
+    __syncthreads();
     if (wave == 0) {
       double x[kChMaxK];
       for (int q = 0; q < kChMaxK; ++q) x[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
       for (int j = nb - 1; j >= 0; --j) {
-        const double ljj = lane == j ? L[(size_t)(k0 + j) * r + k0 + j] : 1.0;
+        const double ljj = Db[j][j];
         // Lᵀ[lane][j] = L[j][lane] for lane < j
-        const double lji = lane < j ? L[(size_t)(k0 + j) * r + k0 + lane] : 0.0;
+        const double lji = lane < j ? Db[j][lane] : 0.0;
         for (int q = 0; q < k; ++q) {
           if (lane == j) x[q] /= ljj;
           const double xj = ch_readlane(x[q], j);
@@ -190,16 +223,20 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
         }
       }
       if (lane < nb)
-        for (int q = 0; q < k; ++q) B[(size_t)(k0 + lane) * k + q] = x[q];
+        for (int q = 0; q < k; ++q) {
+          B[(size_t)(k0 + lane) * k + q] = x[q];
+          Xb[lane][q] = x[q];
+        }
     }
     __syncthreads();
-    // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j
+    // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j  (lanes read consecutive i: coalesced)
     for (int i = tid; i < k0; i += kChThreads) {
-      for (int q = 0; q < k; ++q) {
-        double acc = 0.0;
-        for (int b = 0; b < nb; ++b) acc = fma(L[(size_t)(k0 + b) * r + i], B[(size_t)(k0 + b) * k + q], acc);
-        B[(size_t)i * k + q] -= acc;
+      double acc[kChMaxK] = {0.0, 0.0, 0.0, 0.0};
+      for (int b = 0; b < nb; ++b) {
+        const double l = L[(size_t)(k0 + b) * r + i];
+        for (int q = 0; q < k; ++q) acc[q] = fma(l, Xb[b][q], acc[q]);
       }
+      for (int q = 0; q < k; ++q) B[(size_t)i * k + q] -= acc[q];
     }
     __syncthreads();
   }

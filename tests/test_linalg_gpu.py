@@ -58,3 +58,31 @@ def test_chol_spd_jitter_retry_on_semidefinite(dev):
     assert int(info) >= 1
     Ss = S * sc[:, None] * sc[None, :]
     assert torch.allclose(L @ L.T, Ss, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,r", [(1, 1), (37, 17), (1000, 128), (20011, 509), (70000, 512), (5000, 700)])
+def test_wsyrk_f64_matches_torch(dev, monkeypatch, n, r):
+    """Native f64-MFMA weighted SYRK (upper tiles, deterministic split-K) vs Φᵀ diag(d) Φ."""
+    from hfens.models import svc_lowrank
+    from hfens.models.svc_lowrank import _weighted_gram
+    monkeypatch.setattr(svc_lowrank, "NATIVE_SYRK", True)
+    g = torch.Generator(device=dev).manual_seed(n + r)
+    Phi = torch.randn(n, r, generator=g, device=dev, dtype=torch.float64)
+    d = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 10 ** torch.randint(-6, 6, (n,), generator=g, device=dev)
+    S = _weighted_gram(Phi, d)
+    want = Phi.T @ (d[:, None] * Phi)
+    assert torch.equal(S, S.T)
+    err = float((S - want).abs().max() / want.abs().max())
+    assert err < 1e-12, err
+    assert torch.equal(S, _weighted_gram(Phi, d))          # deterministic
+
+
+@pytest.mark.parametrize("n,r,k", [(1, 1, 1), (999, 17, 2), (100003, 509, 1), (4096, 512, 4), (3, 64, 3)])
+def test_phi_gemv_matches_torch(dev, n, r, k):
+    from hfens.models.svc_lowrank import _phi_mv
+    g = torch.Generator(device=dev).manual_seed(n * 7 + r)
+    Phi = torch.randn(n, r, generator=g, device=dev, dtype=torch.float64)
+    W = torch.randn(r, k, generator=g, device=dev, dtype=torch.float64)
+    Y = _phi_mv(Phi, W)
+    want = Phi @ W
+    assert float((Y - want).abs().max() / want.abs().max()) < 1e-13
