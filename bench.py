@@ -169,12 +169,13 @@ def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
     solver / kernel paths ran, and how host-bound the timed steps were."""
     import numpy as np
     import torch
-    from hfens.models import hist_gbdt, logreg_solver, smo, stack_trainer
+    from hfens.models import hist_gbdt, logreg_solver, smo, stack_trainer, svc_lowrank
     facts = {"host_cpu_s_per_step": round(cpu / steps, 4),
              "host_cpu_fraction": round(cpu / max(elapsed, 1e-12), 3),
              "stage_host_seconds": host_med,
              "step_ms_min_med_max": [round(1e3 * x, 2) for x in _step_stats(step_ends, t0)],
-             "svm": dict(smo.LAST_SMO_INFO),
+             "svm": dict(smo.LAST_SMO_INFO, **({"lowrank": {k: v for k, v in svc_lowrank.LAST_INFO.items()}}
+                                              if smo.LAST_SMO_INFO.get("solver") == "nystrom-ipm" else {})),
              "gbdt_path": hist_gbdt.LAST_PATH.get("path"),
              "logreg_path": logreg_solver.LAST_PATH.get("path"),
              "concurrent_bases": bool(stack_trainer.CONCURRENT_BASES and dev.type == "cuda"),

@@ -185,8 +185,9 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         parts = [gap, rd.abs().max(), re.abs()] + ([info[0].to(dt)] if native else [])
         chk = torch.stack(parts).cpu()
         if native and float(chk[3]) < 0:
-            raise FloatingPointError("interior-point SVC: Woodbury system not positive definite "
-                                     "even with 1e-6 jitter")
+            raise FloatingPointError("interior-point SVC: Woodbury system not factorisable (non-finite)")
+        if native:
+            LAST_INFO["max_chol_retries"] = max(LAST_INFO.get("max_chol_retries", 0), int(chk[3]))
         if float(chk[0]) < tol and float(chk[1]) < 1e-8 and float(chk[2]) < 1e-8 * csum:
             break
         D = nu / a + mu / s

@@ -11,7 +11,7 @@
 //              all threads, the panel below solved one row per thread into a transposed LDS copy,
 //              the trailing lower triangle updated from it on v_mfma_f64_16x16x4_f64 (16×16 blocks
 //              over the 16 waves; f64 MFMA maps A[l&15][l>>4], B[l>>4][l&15], C row (l>>4)+4·reg).  A non-positive or non-finite pivot
-//              restarts the factorisation from S with jit = 1e-14, 1e-12, … 1e-6 — on the device,
+//              restarts the factorisation from S with jit = 1e-14, 1e-12, … 1 — on the device,
 //              so the host never reads `info`.  out_info[0] = retries used (−1 = still failed).
 //  chol_solve: x = sc ∘ (L Lᵀ)⁻¹ (sc ∘ b) for k ≤ 4 right-hand sides, one workgroup: blocked
 //              forward / backward substitution, 64-row diagonal blocks solved by wave 0 (readlane
@@ -142,8 +142,10 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
     }
     if (!bad) break;
     ++tries;
+    // 1e-14 … 1e-6 are numerical repairs; beyond that the step is a damped (regularised) Newton
+    // step, which the interior-point iteration tolerates — only a non-finite S ends the ladder
     jit = jit == 0.0 ? 1e-14 : jit * 100.0;
-    if (jit > 1e-6) {
+    if (jit > 1.0) {
       if (tid == 0) out_info[0] = -1;
       return;
     }

@@ -10,6 +10,6 @@ run() {  # run TAG SECONDS ARGS...
   timeout -k 10 $secs python3 -u bench.py "$@" > $D/$tag.json 2> $D/$tag.err || { echo "$tag failed"; tail -30 $D/$tag.err; exit 1; }
   python3 -c "import json; d=json.load(open('$D/$tag.json')); print('$tag', d['ms_per_step'], d['value'], d['auroc'], d['config']['stage_seconds'], d['diag']['svm'])"
 }
-run r30k 200 --rows 30000 --steps 1 --warmup 1
-run r100k 300 --rows 100000 --steps 1 --warmup 1
+[ -z "$ONLY1M" ] && run r30k 200 --rows 30000 --steps 1 --warmup 1
+[ -z "$ONLY1M" ] && run r100k 300 --rows 100000 --steps 1 --warmup 1
 run r1m 600 --rows 1000000 --steps 1 --warmup 0

@@ -139,3 +139,41 @@ def test_batched_bin_fit_matches_per_feature():
     assert torch.equal(a.hi_val.cpu(), b.hi_val.cpu())
     assert torch.equal(a.edges.cpu(), b.edges.cpu())
     assert int(a.nbins.max()) == 256 and int(a.nbins.min()) <= 8
+
+
+def test_knn_transform_many_equals_single_transforms():
+    """transform_many (one host read for several matrices on the device path) is transform applied
+    to each matrix."""
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models.imputer import KNNImputer
+    Xa, _, _ = make_hf_cohort(400, 9, seed=5, nan_frac=0.05)
+    Xb, _, _ = make_hf_cohort(150, 9, seed=6, nan_frac=0.05)
+    imp = KNNImputer(n_neighbors=1).fit(torch.as_tensor(Xa))
+    a, b = imp.transform_many([torch.as_tensor(Xa), torch.as_tensor(Xb)])
+    assert torch.equal(a, imp.transform(torch.as_tensor(Xa)))
+    assert torch.equal(b, imp.transform(torch.as_tensor(Xb)))
+    assert not torch.isnan(a).any() and not torch.isnan(b).any()
+
+
+def test_cooperative_solver_member_policies(monkeypatch):
+    """Member counts of the cooperative LR (CU budget while a cooperative SMO runs) and the GBDT
+    stage-graph unit count (3-stage units while every stage still all-reduces)."""
+    from hfens.models import hist_gbdt, logreg_solver
+    monkeypatch.setattr(logreg_solver, "MEMBERS", 0)
+    assert logreg_solver.lr_members(1, 10000, 256) == 16          # meta-LR: 16 row slabs
+    assert logreg_solver.lr_members(6, 10000, 256) == 16
+    assert logreg_solver.lr_members(1, 700, 256) == 2              # ≥ 512 rows per member
+    monkeypatch.setattr(logreg_solver, "BLOCK_BUDGET", [30])
+    assert logreg_solver.lr_members(6, 10000, 256) == 5            # 30 CUs left beside the SMO
+    monkeypatch.setattr(logreg_solver, "MEMBERS", 1)
+    assert logreg_solver.lr_members(6, 10000, 256) == 1
+
+    class St:
+        T = 100
+    monkeypatch.setattr(hist_gbdt, "STAGE_GRAPH", "auto")
+    assert hist_gbdt._graph_units(St, None, None) == 0            # single process: eager loop
+    monkeypatch.setattr(hist_gbdt, "STAGE_GRAPH", "1")
+    assert hist_gbdt._graph_units(St, None, None) == 33           # t = 0 … 98 replayed, 99 … 101 eager
+    assert hist_gbdt._graph_units(St, None, object()) == 0        # stamps requested: eager
+    St.T = 5
+    assert hist_gbdt._graph_units(St, None, None) == 0            # too short to pay for a capture
