@@ -84,6 +84,10 @@ def main():
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
         ops.ext()  # the HIP extension must be there; no silent fallback
+        # the host side of a GPU step is bookkeeping on small arrays: intra-op thread pools only
+        # wake OpenMP workers that then spin (measured: 15 workers at ~12 % CPU each, host CPU
+        # fraction 2.9 — they compete with the submitting thread on a loaded box)
+        torch.set_num_threads(int(os.environ.get("HFENS_HOST_THREADS", "1")))
     # strong scaling: every rank draws the same cohort and keeps its contiguous row block
     Xd, yd, names = make_hf_cohort(a.rows, a.features, seed=a.seed, nan_frac=0.02)
     Xs, ys, _ = make_hf_cohort(a.rows, a.features, seed=a.seed + 1, nan_frac=0.02)
@@ -111,6 +115,7 @@ def main():
     # every timed step carries an event-based stage timer (no host synchronisation: it costs
     # the timed region nothing); the per-stage table below is the median over the timed steps
     timers = [StageTimer(enabled=True, events=True) for _ in range(a.steps)]
+    threads0 = _thread_cpu()
     cpu0 = time.process_time()
     t0 = time.perf_counter()
     step_ends = []
@@ -120,6 +125,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     cpu = time.process_time() - cpu0
+    threads1 = _thread_cpu()
     if group is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
@@ -158,7 +164,8 @@ def main():
                        "global_batch": n_total, "seq_len": a.features, "rows_per_gpu": a.rows // max(1, world),
                        "features": a.features, "parallelism": f"dp{world}",
                        "stage_seconds": stage_med},
-            "diag": run_facts(dev, a.steps, elapsed, cpu, host_med, step_ends, t0),
+            "diag": dict(run_facts(dev, a.steps, elapsed, cpu, host_med, step_ends, t0),
+                         busiest_threads_cpu_s=_thread_delta(threads0, threads1)),
         }
         print(json.dumps(out), flush=True)
     pdist.shutdown()
@@ -187,6 +194,37 @@ def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
         facts.update(gpu=p.name, arch=getattr(p, "gcnArchName", None), cus=p.multi_processor_count,
                      hw_queues=os.environ.get("GPU_MAX_HW_QUEUES"))
     return facts
+
+
+def _thread_cpu():
+    """{(tid, name): CPU seconds} of this process's threads (Linux /proc), {} elsewhere."""
+    out = {}
+    try:
+        tick = os.sysconf("SC_CLK_TCK")
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                with open(f"/proc/self/task/{tid}/stat") as f:
+                    st = f.read()
+                fields = st[st.rindex(")") + 2:].split()
+                with open(f"/proc/self/task/{tid}/comm") as f:
+                    name = f.read().strip()
+                out[(tid, name)] = (int(fields[11]) + int(fields[12])) / tick
+            except OSError:
+                continue
+    except OSError:
+        pass
+    return out
+
+
+def _thread_delta(a, b, top=5):
+    """CPU seconds per thread name over the timed steps, the busiest few (explains host load)."""
+    main = str(os.getpid())
+    agg = {}
+    for k, v in b.items():
+        d = v - a.get(k, 0.0)
+        if d > 0:
+            agg[f"{k[1]}{'(main)' if k[0] == main else ''}#{k[0]}"] = d
+    return {k: round(v, 3) for k, v in sorted(agg.items(), key=lambda x: -x[1])[:top]}
 
 
 def _step_stats(ends, t0):

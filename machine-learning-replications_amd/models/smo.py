@@ -157,6 +157,13 @@ def _expand(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
     return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
 
 
+def _class_weights_host(svc, y_np: np.ndarray) -> np.ndarray:
+    if svc.class_weight == "balanced":
+        cnt = np.bincount((y_np > 0.5).astype(np.int64), minlength=2).astype(np.float64)
+        return y_np.shape[0] / (2 * cnt)
+    return svc.class_weights(torch.as_tensor(y_np)).cpu().numpy()
+
+
 def _to_dev(a: np.ndarray, device) -> torch.Tensor:
     """Host index array → device without blocking the host (pinned, non-blocking)."""
     t = torch.from_numpy(np.ascontiguousarray(a))
@@ -702,7 +709,8 @@ def use_lowrank(sizes) -> bool:
     return max(sizes) > EXACT_MAX_POINTS or gram > GRAM_BUDGET
 
 
-def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None) -> dict:
+def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None,
+                     y_host=None) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
@@ -711,7 +719,11 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
 
     Fits above the exact solver's size/memory limits (:func:`use_lowrank`) are solved by the
     Nyström reduced-set SVC (:mod:`svc_lowrank`) instead, synchronously; with ``group`` fit ``f``
-    is solved on rank ``f mod world`` and broadcast."""
+    is solved on rank ``f mod world`` and broadcast.
+
+    ``y_host``: the fits' labels as host arrays (the caller already has them): the libsvm problem
+    expansion then runs on the host while the device computes the guards and γ statistics, and
+    only those are read back."""
     from .. import ops
     if use_lowrank([int(y.numel()) for y in ys]):
         from .svc_lowrank import fit_svc_lowrank_batch
@@ -744,8 +756,17 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         parts.append(torch.stack([((y == 0) | (y == 1)).all() for y in ys]).to(f64))
     if any(need_var):
         parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
-    parts.append(torch.cat([y.reshape(-1).to(f64) for y in ys]))
-    host = torch.cat(parts).cpu().numpy()
+    pre = None
+    if y_host is not None and all(np.isin(np.unique(yh), (0.0, 1.0)).all() for yh in y_host):
+        # host labels: expand the problems now (γ filled in below), overlapping the device work
+        pre = []
+        for f, (svc, yh) in enumerate(zip(svcs, y_host)):
+            y_np = np.asarray(yh, dtype=np.float64).reshape(-1)
+            pre.append((y_np,) + _expand(f, y_np, None, _class_weights_host(svc, y_np), svc))
+        hmark("svc_expand_early")
+    else:
+        parts.append(torch.cat([y.reshape(-1).to(f64) for y in ys]))
+    host = torch.cat(parts).cpu().numpy() if parts else np.zeros(0)
     o = 0
     if guards.ENABLED:
         for f in range(len(Zs)):
@@ -758,24 +779,25 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     if any(need_var):
         var = host[o:o + len(Zs)]
         o += len(Zs)
-    y_host = host[o:]
+    y_all = host[o:]
     hmark("svc_y_var_host")
     all_probs, meta = [], []
     off = 0
     for f, (svc, Z) in enumerate(zip(svcs, Zs)):
-        y_np = y_host[off:off + sizes[f]]
-        off += sizes[f]
         if svc.gamma == "scale":
             v = float(var[f])
             gamma = 1.0 / (Z.shape[1] * v) if v != 0 else 1.0
         else:
             gamma = svc.resolve_gamma(Z)
-        if svc.class_weight == "balanced":
-            cnt = np.bincount((y_np > 0.5).astype(np.int64), minlength=2).astype(np.float64)
-            cw = y_np.shape[0] / (2 * cnt)
+        if pre is not None:
+            _, pr, mt = pre[f]
+            for p in pr:
+                p.gamma = gamma
+            mt["gamma"] = gamma
         else:
-            cw = svc.class_weights(torch.as_tensor(y_np)).cpu().numpy()
-        pr, mt = _expand(f, y_np, gamma, cw, svc)
+            y_np = y_all[off:off + sizes[f]]
+            off += sizes[f]
+            pr, mt = _expand(f, y_np, gamma, _class_weights_host(svc, y_np), svc)
         all_probs += pr
         meta.append(mt)
     hmark("svc_expand")

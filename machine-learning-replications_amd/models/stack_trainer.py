@@ -127,7 +127,7 @@ def _index_to(a, device) -> torch.Tensor:
     return t.pin_memory().to(device, non_blocking=True)
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None):
+def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -160,7 +160,8 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                 clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
                 hmark("svc_inputs")
                 if group is None:
-                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group))
+                    yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
+                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh))
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
                 hmark("svc_launched")
@@ -199,8 +200,10 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     timer = timer or StageTimer(enabled=False)
     dev = X.device
     n = X.shape[0]
+    y_np = None
     if group is None:
-        folds_np = stratified_kfold_test_folds(y.cpu().numpy(), N_FOLDS)
+        y_np = y.cpu().numpy().astype(np.float64)
+        folds_np = stratified_kfold_test_folds(y_np, N_FOLDS)
     else:
         from ..parallel import dist as pdist
         folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
@@ -220,7 +223,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host)
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream

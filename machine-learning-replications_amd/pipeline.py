@@ -33,6 +33,7 @@ from .utils.timing import StageTimer
 #            latency exceeds the compute they split), dp above.
 DP_POLICY = os.environ.get("HFENS_DP_POLICY", "auto")
 TASK_MAX_ROWS = int(os.environ.get("HFENS_TASK_MAX_ROWS", str(1 << 18)))
+AUX_STREAM = os.environ.get("HFENS_AUX_STREAM", "1") != "0"   # held-out imputation on a side stream
 
 
 def choose_policy(n_total: int) -> str:
@@ -80,7 +81,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         # their donor search runs on a side stream, overlapped with LassoCV and the stacking fit
         # (joined before the evaluation below)
         aux = None
-        if dev.type == "cuda":
+        if dev.type == "cuda" and AUX_STREAM:
             from . import runtime
             aux = runtime.stream(dev, "aux")
         X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
