@@ -12,4 +12,4 @@ run() {  # run TAG SECONDS ARGS...
 }
 [ -z "$ONLY1M" ] && run r30k 200 --rows 30000 --steps 1 --warmup 1
 [ -z "$ONLY1M" ] && run r100k 300 --rows 100000 --steps 1 --warmup 1
-run r1m 600 --rows 1000000 --steps 1 --warmup 0
+run r1m 900 --rows 1000000 --steps 1 --warmup 0
