@@ -22,8 +22,14 @@ class StandardScaler(Estimator):
         if sample_mask is not None:
             X = X[sample_mask]
         n = X.shape[0]
-        mean = X.mean(0)
-        var = ((X - mean) ** 2).mean(0)
+        # Σx / n and Σ(x − mean)² / n with a TRUE division, as sklearn's _incremental_mean_and_var
+        # (nansum / n, nanvar).  On the GPU, torch divides a tensor by a Python scalar as a multiply
+        # by its reciprocal (measured: 14396.0 / 7198 → 1.9999999999999998), which turns a constant
+        # column's variance into 5e-32 and its scale into 2e-16 instead of the exact 0 → 1 of the
+        # 0.23.2 rule; dividing by a tensor of n is an IEEE division
+        nt = torch.full((X.shape[1],), float(n), dtype=X.dtype, device=X.device)
+        mean = X.sum(0) / nt
+        var = ((X - mean) ** 2).sum(0) / nt
         self._set(mean, var, n)
         return self
 

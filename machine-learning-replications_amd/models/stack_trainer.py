@@ -74,13 +74,53 @@ def _global_scaler_moments(X, masks, group):
     return mean, sq / cnt[:, None], cnt
 
 
+def scaler_batch_device(X: torch.Tensor, rows_host):
+    """The K fold scalers of the SVC pipeline in ONE native pass (ops/csrc/scaler.hip, SURVEY.md
+    K2): per-subset mean / population variance (two-pass f64, deterministic) and every subset's
+    scaled rows in one concatenated matrix.  Returns (means [K, F], vars [K, F], Z [Σ l, F],
+    offsets, device row index)."""
+    from .. import ops
+    K = len(rows_host)
+    lens = [int(r.shape[0]) for r in rows_host]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n, F = X.shape
+    dev = X.device
+    idx = _index_to(np.concatenate(rows_host).astype(np.int64), dev)
+    offs_d = _index_to(offs, dev)
+    max_rows = max(lens)
+    S = min(64, max(1, -(-max_rows // 1024)))
+    part = torch.empty(2 * K * S * 64, dtype=torch.float64, device=dev)
+    mean = torch.empty(K, F, dtype=torch.float64, device=dev)
+    var = torch.empty(K, F, dtype=torch.float64, device=dev)
+    Z = torch.empty(int(offs[-1]), F, dtype=torch.float64, device=dev)
+    Xc = X.to(torch.float64).contiguous()
+    ops.ext().scaler_batch(Xc.data_ptr(), n, F, idx.data_ptr(), offs_d.data_ptr(), K, max_rows, part.data_ptr(),
+                           mean.data_ptr(), var.data_ptr(), Z.data_ptr(), ops.stream_ptr(dev))
+    return mean, var, Z, offs, idx
+
+
+NATIVE_SCALER = os.environ.get("HFENS_NATIVE_SCALER", "1") != "0"
+
+
 def _svc_inputs(est, X, y, masks, group=None, rows_host=None):
     """Clones, their SVC objects and the scaled per-mask training matrices.  ``group`` (rows
     sharded): the scalers are fitted on the global masked rows, as a single process would.
-    ``rows_host``: the masks' row indices, known on the host (no ``nonzero`` synchronisation)."""
+    ``rows_host``: the masks' row indices, known on the host (no ``nonzero`` synchronisation);
+    on the GPU the fold scalers then run as one native batched fit + transform."""
     kind = _kind(est)
     clones = [est.clone() for _ in range(masks.shape[0])]
     Zs, ys = [], []
+    if (kind == "svc" and group is None and rows_host is not None and X.is_cuda and NATIVE_SCALER
+            and X.shape[1] <= 64):
+        from .. import ops
+        if ops.has_ext():
+            mean, var, Z, offs, idx = scaler_batch_device(X, rows_host)
+            ycat = y.index_select(0, idx)
+            for k, c in enumerate(clones):
+                c.steps[0][1]._set(mean[k], var[k], int(offs[k + 1] - offs[k]))
+                Zs.append(Z[offs[k]:offs[k + 1]])
+                ys.append(ycat[offs[k]:offs[k + 1]])
+            return clones, [c.steps[-1][1] for c in clones], Zs, ys
     gm = _global_scaler_moments(X, masks, group) if (group is not None and kind == "svc") else None
     for k, (c, m) in enumerate(zip(clones, masks)):
         rows = _index_to(rows_host[k], X.device) if rows_host is not None else torch.nonzero(m).squeeze(1)

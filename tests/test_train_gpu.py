@@ -369,3 +369,27 @@ def test_quantize_bins_kernel_matches_searchsorted(dev):
         ref = torch.searchsorted(bm.edges, X32)
         ref = torch.minimum(ref, (bm.nbins.to(ref.dtype) - 1)[:, None]).to(torch.uint8)
         assert torch.equal(got, ref)
+
+
+def test_scaler_batch_matches_per_fold_scalers(dev):
+    """K2: the native batched fold scalers (mean / population variance / scaled rows of every
+    fold subset in one pass) equal StandardScaler fitted per fold."""
+    from hfens.models.scaler import StandardScaler
+    from hfens.models.stack_trainer import scaler_batch_device
+    X, _ = _data(9001, 17, 91)
+    X[:, 3] = 2.0                                   # a constant column: scale 1
+    Xd = X.to(dev)
+    rng = np.random.default_rng(3)
+    folds = rng.integers(0, 5, 9001)
+    rows = [np.nonzero(folds != k)[0] for k in range(5)] + [np.arange(9001)]
+    mean, var, Z, offs, _ = scaler_batch_device(Xd, rows)
+    for k, r in enumerate(rows):
+        sc = StandardScaler().fit(Xd[torch.as_tensor(r, device=dev)])
+        assert torch.allclose(mean[k], sc.mean_, rtol=1e-13, atol=1e-13)
+        assert torch.allclose(var[k], sc.var_, rtol=1e-11, atol=1e-13)
+        Zk = sc.transform(Xd[torch.as_tensor(r, device=dev)])
+        dz = (Z[offs[k]:offs[k + 1]] - Zk).abs().max(0).values
+        assert float(dz.max()) < 1e-11, (k, dz.tolist(), sc.scale_.tolist())
+        # the constant column: exact mean, variance 0, scale 1 (sklearn 0.23.2), in both paths
+        assert float(var[k, 3]) == 0.0 and float(sc.var_[3]) == 0.0
+    assert torch.all(Z[:, 3] == 0)
