@@ -63,6 +63,49 @@ def roc_auc(y_true, score) -> float:
     return auc(fpr, tpr)
 
 
+def roc_auc_sharded(y_local, score_local, group, bins: int = 1 << 16) -> float:
+    """Exact AUROC of rows sharded over a process group without gathering them (SURVEY.md §5.8
+    R8): scores are bucketed on a global [min, max] grid and every rank's per-bucket positive /
+    negative counts are summed in ONE int64 all-reduce; pairs in different buckets are then
+    ordered by their buckets.  Only the rows of buckets holding both classes (few at 2^16 buckets)
+    are all-gathered to order the pairs inside them exactly (ties count ½, as sklearn)."""
+    from ..parallel import dist as pdist
+    import torch.distributed as dist
+    y = _t(y_local).to(torch.float64).reshape(-1)
+    s = _t(score_local).to(torch.float64).reshape(-1).to(y.device)
+    dev = s.device
+    big = torch.tensor([float("inf")], dtype=torch.float64, device=dev)
+    mm = torch.cat([s.min().reshape(1) if s.numel() else big, (-s.max()).reshape(1) if s.numel() else big])
+    dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
+    lo, hi = float(mm[0]), -float(mm[1])
+    width = (hi - lo) / bins if hi > lo else 1.0
+    b = torch.clamp(((s - lo) / width).floor().to(torch.int64), 0, bins - 1)
+    pos = y > 0.5
+    cnt = torch.zeros(2, bins, dtype=torch.int64, device=dev)
+    cnt[1].index_add_(0, b[pos], torch.ones_like(b[pos]))
+    cnt[0].index_add_(0, b[~pos], torch.ones_like(b[~pos]))
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+    neg_c, pos_c = cnt[0].to(torch.float64), cnt[1].to(torch.float64)
+    n_pos, n_neg = float(pos_c.sum()), float(neg_c.sum())
+    if n_pos == 0 or n_neg == 0:
+        return float("nan")
+    neg_below = torch.cumsum(neg_c, 0) - neg_c
+    cross = float((pos_c * neg_below).sum())
+    mixed = (pos_c > 0) & (neg_c > 0)
+    mine = mixed[b]
+    rows = pdist.all_gather_rows(torch.stack([s[mine], y[mine]], 1), group)
+    within = 0.0
+    if rows.shape[0]:
+        bb = torch.clamp(((rows[:, 0] - lo) / width).floor().to(torch.int64), 0, bins - 1)
+        for k in torch.unique(bb).tolist():
+            r = rows[bb == k]
+            sp, sn = r[r[:, 1] > 0.5, 0], r[r[:, 1] <= 0.5, 0]
+            gt = (sp[:, None] > sn[None, :]).sum()
+            eq = (sp[:, None] == sn[None, :]).sum()
+            within += float(gt) + 0.5 * float(eq)
+    return (cross + within) / (n_pos * n_neg)
+
+
 def precision_recall_curve(y_true, score):
     fps, tps, thr = _binary_clf_curve(y_true, score)
     ps = tps + fps

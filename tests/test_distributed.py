@@ -351,3 +351,26 @@ def test_nccl_all_reduce_two_gpus():
         pytest.skip("needs 2 GPUs")
     got = _run_nccl("_nccl_sum", 2)
     assert got == [3.0, 3.0]
+
+
+def _auc_sharded(rank, world, group):
+    from hfens.parallel.dist import shard_rows
+    from hfens.utils import metrics
+    rng = np.random.default_rng(17)
+    y = (rng.random(3001) < 0.3).astype(np.float64)
+    s = np.round(rng.random(3001) * 0.6 + 0.3 * y, 3)          # heavy ties, some cross-class
+    s[:40] = 0.5                                               # one big tie block
+    out = []
+    for bins in (1 << 16, 8):                                  # fine grid, and a grid of all-mixed buckets
+        out.append(metrics.roc_auc_sharded(shard_rows(torch.as_tensor(y), rank, world),
+                                           shard_rows(torch.as_tensor(s), rank, world), group, bins=bins))
+    return torch.tensor(out), torch.tensor([metrics.roc_auc(torch.as_tensor(y), torch.as_tensor(s))])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_roc_auc_sharded_is_exact(world):
+    """R8: the bucket-count all-reduce AUROC equals the single-process (sklearn-equal) AUROC exactly
+    (ties inside mixed buckets resolved from their gathered rows)."""
+    got, want = _run("_auc_sharded", world)
+    assert abs(float(got[0]) - float(want[0])) < 1e-15
+    assert abs(float(got[1]) - float(want[0])) < 1e-15
