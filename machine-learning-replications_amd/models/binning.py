@@ -7,8 +7,9 @@ candidates and thresholds are midpoints of adjacent present values.  Otherwise
 distinct values are grouped into ``max_bins`` quantile groups; a split between
 groups uses the midpoint of the left group's max and the right group's min.
 
-With a process group the distinct-value tables are merged across ranks so every
-rank bins identically (all-gather of the per-rank value sets).  Single-process fits of up to
+With a process group every rank bins identically, and exactly as one process on the concatenated
+rows would: quantile-group ends are global order statistics found by bisection over
+all-reduced counts (``_fit_bins_dp``), so no value table larger than [F, max_bins] is exchanged.  Single-process fits of up to
 ``HOST_BIN_MAX_ROWS`` rows take the distinct values from ONE device→host copy (numpy) instead of a
 device ``unique`` + host read per feature; ``transform`` is one batched ``searchsorted`` against
 the +inf-padded edge table of all features.
@@ -23,6 +24,8 @@ import numpy as np
 import torch
 
 HOST_BIN_MAX_ROWS = int(os.environ.get("HFENS_HOST_BIN_ROWS", str(1 << 17)))
+# per-feature distinct-value all-gathers under DP (round-1 path, kept for A/B)
+LEGACY_DP_BINS = os.environ.get("HFENS_DP_BINS", "") == "legacy"
 
 
 @dataclass
@@ -97,6 +100,103 @@ def _fit_bins_device(X32: torch.Tensor, max_bins: int) -> BinMapper:
         pos = torch.searchsorted(sb, hq, right=True).clamp(max=n - 1)
         hi_h[big_f] = hq.cpu()
         lo_h[big_f] = sb.gather(1, pos).cpu()                           # next distinct values
+    return _assemble(k_h, small_h, hi_h, lo_h, mn_h, max_bins, dev)
+
+
+def _keys(v32: torch.Tensor) -> torch.Tensor:
+    """float32 → int64 keys in [0, 2³²) with the float order (negatives bit-flipped)."""
+    b = v32.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return torch.where(b >= 0x80000000, 0xFFFFFFFF - b, b + 0x80000000)
+
+
+def _unkey(k: torch.Tensor) -> torch.Tensor:
+    b = torch.where(k >= 0x80000000, k - 0x80000000, 0xFFFFFFFF - k)
+    b = torch.where(b >= 0x80000000, b - (1 << 32), b)
+    return b.to(torch.int32).view(torch.float32)
+
+
+def _fit_bins_dp(X32: torch.Tensor, max_bins: int, group) -> BinMapper:
+    """Row-sharded binning, the same bins as a single-process fit on the concatenated rows, with no
+    row or value table crossing the ranks:
+
+    * each rank sorts its shard per feature; one MAX all-reduce of the local distinct counts and one
+      SUM of the row counts;
+    * features whose every shard has ≤ max_bins distinct values all-gather those ≤ max_bins tables
+      (the union decides: ≤ max_bins distinct → one bin per value, else quantile groups);
+    * quantile-group ends are global order statistics (value of rank ⌈i·n/max_bins⌉ − 1), found for
+      all features and groups at once by bisection on order-preserving 32-bit keys: 32 rounds of
+      local ``searchsorted`` counts + one SUM all-reduce of an [F, max_bins] int64 table;
+    * the next distinct value above each end and the minima: one MIN all-reduce each."""
+    import torch.distributed as dist
+    n_loc, F = X32.shape
+    dev = X32.device
+    inf = float("inf")
+    srt = torch.sort((X32 + 0.0).t().contiguous(), dim=1)[0]            # +0.0: −0 → +0 (one value)
+    new = torch.ones_like(srt, dtype=torch.bool)
+    new[:, 1:] = srt[:, 1:] != srt[:, :-1]
+    k_loc = new.sum(1).to(torch.int64)
+    kmax = k_loc.clone()
+    dist.all_reduce(kmax, op=dist.ReduceOp.MAX, group=group)
+    n_t = torch.tensor([n_loc], dtype=torch.int64, device=dev)
+    dist.all_reduce(n_t, op=dist.ReduceOp.SUM, group=group)
+    n = int(n_t.item())
+    kmax_h = kmax.cpu()
+    k_h = torch.full((F,), max_bins + 1, dtype=torch.int64)
+    small_h = torch.full((F, max_bins), float("nan"), dtype=torch.float32)
+    cand = [f for f in range(F) if int(kmax_h[f]) <= max_bins]
+    if cand:
+        tab = torch.full((len(cand), max_bins), float("nan"), dtype=torch.float32, device=dev)
+        for i_, f in enumerate(cand):
+            v = srt[f][new[f]]
+            tab[i_, :v.numel()] = v
+        world = dist.get_world_size(group)
+        bufs = [torch.empty_like(tab) for _ in range(world)]
+        dist.all_gather(bufs, tab, group=group)
+        allv = torch.cat(bufs, 1).cpu()
+        for i_, f in enumerate(cand):
+            u = torch.unique(allv[i_][~torch.isnan(allv[i_])], sorted=True)
+            if u.numel() <= max_bins:
+                k_h[f] = u.numel()
+                small_h[f, :u.numel()] = u
+    big_f = [f for f in range(F) if int(k_h[f]) > max_bins]
+    hi_h = torch.zeros(F, max_bins, dtype=torch.float32)
+    lo_h = torch.zeros(F, max_bins, dtype=torch.float32)
+    mn = srt[:, 0].clone() if n_loc > 0 else torch.full((F,), inf, dtype=torch.float32, device=dev)
+    dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+    mn_h = mn.cpu()
+    if big_f:
+        bi = torch.as_tensor(big_f, device=dev)
+        sb = srt.index_select(0, bi).contiguous()
+        kb = _keys(sb)                                                    # sorted like sb
+        tau = torch.arange(1, max_bins, dtype=torch.float64) * (n / max_bins)
+        r = torch.cat([torch.ceil(tau).to(torch.int64) - 1, torch.tensor([n - 1])]).clamp(0, n - 1)
+        need = (r + 1).to(dev).expand(len(big_f), max_bins).contiguous()
+        lo_k = torch.zeros_like(need)
+        hi_k = torch.full_like(need, 0xFFFFFFFF)
+        for _ in range(32):   # smallest key K with #(key ≤ K) ≥ rank + 1, over all ranks
+            mid = (lo_k + hi_k) // 2
+            cnt = torch.searchsorted(kb, mid, right=True) if n_loc > 0 else torch.zeros_like(mid)
+            dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+            ge = cnt >= need
+            hi_k = torch.where(ge, mid, hi_k)
+            lo_k = torch.where(ge, lo_k, mid + 1)
+        hq = _unkey(lo_k)                                                 # quantile group ends
+        if n_loc > 0:
+            pos = torch.searchsorted(sb, hq, right=True)
+            nxt = torch.where(pos < n_loc, sb.gather(1, pos.clamp(max=n_loc - 1)), torch.full_like(hq, inf))
+        else:
+            nxt = torch.full_like(hq, inf)
+        dist.all_reduce(nxt, op=dist.ReduceOp.MIN, group=group)        # next distinct values
+        hi_h[big_f] = hq.cpu()
+        lo_h[big_f] = nxt.cpu()
+    return _assemble(k_h, small_h, hi_h, lo_h, mn_h, max_bins, dev)
+
+
+def _assemble(k_h, small_h, hi_h, lo_h, mn_h, max_bins: int, dev) -> BinMapper:
+    """BinMapper from per-feature host tables: ``k_h`` distinct counts; ``small_h`` the sorted
+    distinct values of features with ≤ max_bins of them; ``hi_h`` the quantile group ends and
+    ``lo_h`` the next distinct value above each end (features with more); ``mn_h`` the minima."""
+    F = int(k_h.numel())
     nb = torch.empty(F, dtype=torch.int32)
     lo = torch.zeros(F, 256, dtype=torch.float64)
     hi = torch.zeros(F, 256, dtype=torch.float64)
@@ -170,6 +270,8 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
     host = group is None and n <= HOST_BIN_MAX_ROWS
     if group is None and not host and X32.is_cuda:
         return _fit_bins_device(X32, max_bins)
+    if group is not None and not LEGACY_DP_BINS:
+        return _fit_bins_dp(X32, max_bins, group)
     Xh = X32.cpu().numpy() if host else None
     nb = torch.empty(F, dtype=torch.int32)
     lo = torch.zeros(F, 256, dtype=torch.float64)

@@ -374,3 +374,43 @@ def test_roc_auc_sharded_is_exact(world):
     got, want = _run("_auc_sharded", world)
     assert abs(float(got[0]) - float(want[0])) < 1e-15
     assert abs(float(got[1]) - float(want[0])) < 1e-15
+
+
+def _bin_data():
+    g = np.random.default_rng(11)
+    n = 1003
+    X = np.empty((n, 6), dtype=np.float64)
+    X[:, 0] = g.normal(size=n) * 1e3                          # continuous, negatives
+    X[:, 1] = g.integers(0, 2, n)                             # binary
+    X[:, 2] = np.where(np.arange(n) < n // 2, g.integers(0, 200, n), g.integers(200, 400, n))  # ≤ 256 per shard, 400 total
+    X[:, 3] = np.round(g.normal(size=n), 1)                   # heavy ties across shards
+    X[:, 4] = np.where(g.random(n) < 0.5, 0.0, -0.0)          # ±0: one value
+    X[:, 5] = np.sort(g.exponential(size=n))                  # sorted: each shard holds a value range
+    return torch.as_tensor(X)
+
+
+def _bins_dp(rank, world, group):
+    from hfens.models.binning import fit_bins
+    from hfens.parallel.dist import shard_rows
+    X = _bin_data()
+    out = []
+    for mb in (256, 16):
+        bm = fit_bins(shard_rows(X, rank, world), mb, group=group)
+        out.append((bm.nbins.clone(), bm.lo_val.clone(), bm.hi_val.clone(), bm.edges.clone()))
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fit_bins_dp_equals_single_process(world):
+    """K7 under DP: order-statistic bisection over all-reduced counts gives the single-process bins
+    (quantile and one-bin-per-value features, ties across shards, ±0, a 400-value union of two
+    ≤ 256-value shards, value ranges split by shard)."""
+    from hfens.models.binning import fit_bins
+    got = _run("_bins_dp", world)
+    X = _bin_data()
+    for (nb, lo, hi, e), mb in zip(got, (256, 16)):
+        bm = fit_bins(X, mb)
+        assert torch.equal(nb, bm.nbins)
+        assert torch.equal(lo, bm.lo_val)
+        assert torch.equal(hi, bm.hi_val)
+        assert torch.equal(e, bm.edges)
