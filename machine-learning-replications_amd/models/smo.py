@@ -397,8 +397,14 @@ _OTF_MAX_S, _OTF_MAX_F = 1024, 20   # ≤ 2 points per thread: no register spill
 _OTF_GRANULES = 2 * 16 * 32          # exchange slots per problem: 2 × kMaxMembers × kOtfGran (u64)
 _OTF_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("S", "<i4"),
                     ("ngl2e", "<f4"), ("Cp", "<f8"), ("Cn", "<f8")])
-_COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
-                     ("S", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
+_COOP_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("moff", "<i8"), ("l", "<i4"), ("ld", "<i4"),
+                     ("npos", "<i4"), ("S", "<i4"), ("lphys", "<i4"), ("pad", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
+# Platt-CV sub-problems read their fit's final-problem Gram through a column map (svm_coop.hip
+# smo_coop_kernel<K4, Mapped>): a sub-problem's rows are a subset of the same scaled rows with the
+# same γ, so its Gram is a principal submatrix of the parent's, entry for entry.  Only the 6 final
+# problems' Grams are computed (bench: 1.7 instead of 7 GB written); cooperative solver only.
+SHARE_GRAM = os.environ.get("HFENS_SMO_SHARE_GRAM", "1") != "0"
+_MAP_MAX = 1 << 15   # column / index keys are packed into 15 bits each
 _NCU: dict = {}
 # set while re-solving a batch whose cooperative launch reported a member-exchange timeout: the
 # one-workgroup solver needs no co-residency (same pair sequence, so the same result)
@@ -417,6 +423,32 @@ def coop_members(P: int, max_l: int, ncu: int) -> int:
     if not COOP or PROFILE_SMO or P <= 0 or _FORCE_SINGLE[0]:
         return 1
     return max(1, min(_COOP_MAX_W, max(ncu - COOP_RESERVE_CUS, P) // P, -(-max_l // COOP_MIN_SLICE)))
+
+
+def _gram_parents(live) -> List[int]:
+    """For every problem, the index in ``live`` of the problem whose stored Gram it reads (−1: its
+    own): a Platt sub-problem (fold ≥ 0) reads its fit's final problem's, when that one is in the
+    same launch and both fit the 15-bit keys."""
+    final = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
+    out = []
+    for p in live:
+        q = final.get(p.fit, -1) if p.fold >= 0 else -1
+        if q >= 0 and (live[q].l > _MAP_MAX or p.l > _MAP_MAX):
+            q = -1
+        out.append(q)
+    return out
+
+
+def _column_map(par: _Prob, sub: _Prob) -> np.ndarray:
+    """int32 [par.l]: the sub-problem's index of each parent column (−1: not in the sub-problem)."""
+    inv = np.full(int(par.rows.max()) + 1, -1, dtype=np.int64)
+    inv[par.rows] = np.arange(par.l)
+    cols = inv[sub.rows]
+    if (cols < 0).any():
+        raise AssertionError("Platt sub-problem rows must be rows of the final problem")
+    m = np.full(par.l, -1, dtype=np.int32)
+    m[cols] = np.arange(sub.l, dtype=np.int32)
+    return m
 
 
 def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
@@ -439,20 +471,27 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
                              gap.data_ptr(), err.data_ptr(), s)
         LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop-otf")
         return alpha, rho, iters, err
-    g = np.zeros(len(live), _GRAM_DT)
+    W = coop_members(len(live), max_l, _num_cus(device))
+    parent = _gram_parents(live) if (W > 1 and SHARE_GRAM) else [-1] * len(live)
+    own = [k for k in range(len(live)) if parent[k] < 0]
+    g = np.zeros(len(own), _GRAM_DT)
     sm = np.zeros(len(live), _SMO_DT)
     koff = 0
-    for k, p in enumerate(live):
+    for r, k in enumerate(own):
+        p = live[k]
         l = p.l
         ld = (l + 63) // 64 * 64
-        g[k] = (zoffs[k], koff, l, ld, -p.gamma * 1.4426950408889634, 0)
+        g[r] = (zoffs[k], koff, l, ld, -p.gamma * 1.4426950408889634, 0)
         sm[k] = (koff, aoffs[k], l, ld, p.npos, 0, p.Cp, p.Cn)
         koff += l * ld
-    max_l = max(p.l for p in live)
+    for k, q in enumerate(parent):
+        if q >= 0:
+            sm[k] = (sm[q]["koff"], aoffs[k], live[k].l, sm[q]["ld"], live[k].npos, 0, live[k].Cp, live[k].Cn)
+    max_own = max(live[k].l for k in own)
     from .. import runtime
     K = runtime.workspace(device, "svm_gram", koff, torch.float32)   # process-lifetime, grown only
     gdev = _dev_struct(g, device)
-    E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(live), max_l, K.data_ptr(), s)
+    E.gram_rbf_batch(zcat.data_ptr(), F, gdev.data_ptr(), len(own), max_own, K.data_ptr(), s)
     from ..utils.timing import hmark
     hmark("svc_gram_launched")
     alpha = torch.empty(aoffs[-1], dtype=torch.float64, device=device)
@@ -460,20 +499,29 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     iters = torch.empty(len(live), dtype=torch.int32, device=device)
     gap = torch.empty(len(live), dtype=torch.float64, device=device)
     max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
-    W = coop_members(len(live), max_l, _num_cus(device))
     err = None
     if W > 1:
         cp = np.zeros(len(live), _COOP_DT)
+        maps, moff = [], 0
         for k, p in enumerate(live):
-            S = -(-(-(-p.l // W)) // 4) * 4
-            cp[k] = (sm[k]["koff"], aoffs[k], p.l, sm[k]["ld"], p.npos, S, p.Cp, p.Cn)
+            q = parent[k]
+            lphys = p.l if q < 0 else live[q].l
+            S = -(-(-(-lphys // W)) // 4) * 4
+            m = -1
+            if q >= 0:
+                m = moff
+                maps.append(_column_map(live[q], p))
+                moff += lphys
+            cp[k] = (sm[k]["koff"], aoffs[k], m, p.l, sm[k]["ld"], p.npos, S, lphys, 0, p.Cp, p.Cn)
         cdev = _dev_struct(cp, device)
+        mdev = _to_dev(np.concatenate(maps), device) if maps else None
         xchg = torch.empty(len(live) * _COOP_GRANULES, dtype=torch.int64, device=device)
         err = torch.zeros(1, dtype=torch.int32, device=device)
         prof = torch.zeros(len(live) * 7, dtype=torch.int64, device=device) if PROFILE_COOP else None
-        E.smo_coop_batch(cdev.data_ptr(), len(live), W, int(cp["S"].max()), K.data_ptr(), alpha.data_ptr(),
-                         xchg.data_ptr(), eps, max_iter, rho.data_ptr(), iters.data_ptr(), gap.data_ptr(),
-                         err.data_ptr(), prof.data_ptr() if prof is not None else 0, s)
+        E.smo_coop_batch(cdev.data_ptr(), len(live), W, int(cp["S"].max()), K.data_ptr(),
+                         mdev.data_ptr() if mdev is not None else 0, alpha.data_ptr(), xchg.data_ptr(), eps,
+                         max_iter, rho.data_ptr(), iters.data_ptr(), gap.data_ptr(), err.data_ptr(),
+                         prof.data_ptr() if prof is not None else 0, s)
         if prof is not None:
             LAST_SMO_PROF.update(phases=prof.view(-1, 7).cpu().numpy(), iters=iters.cpu().numpy(),
                                  l=np.array([p.l for p in live]),
@@ -486,7 +534,8 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
         if prof is not None:
             LAST_SMO_PROF.update(phases=prof.view(-1, 5).cpu().numpy(), iters=iters.cpu().numpy(),
                                  l=np.array([p.l for p in live]))
-    LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop" if W > 1 else "single")
+    LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop" if W > 1 else "single",
+                         grams=len(own))
     del K
     return alpha, rho, iters, err
 

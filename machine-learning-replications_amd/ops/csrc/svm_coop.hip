@@ -33,10 +33,13 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 struct SmoCoopProb {
   long long koff;   // K_p offset (floats)
   long long aoff;   // alpha offset (doubles)
+  long long moff;   // Mapped: offset of this problem's column map in `maps` (see smo_coop_kernel)
   int l;            // problem size
   int ld;           // K_p leading dimension
   int npos;         // indices [0, npos) have y = +1, the rest y = −1
-  int S;            // points per member (multiple of 4): member w owns [w·S, min(l, (w+1)·S))
+  int S;            // points per member (multiple of 4): member w owns columns [w·S, min(lphys, (w+1)·S))
+  int lphys;        // columns of K_p's rows (= l unless Mapped)
+  int pad;
   double Cp, Cn;
 };
 
@@ -53,6 +56,8 @@ struct SmoCoopOut {
 constexpr int kCoopThreads = 512;
 constexpr int kCoopWaves = kCoopThreads / 64;
 constexpr int kGran = 10;             // granules per member slot
+constexpr int kPkBits = 15;           // Mapped: point key = libsvm index << 15 | column
+constexpr int kPkMask = (1 << kPkBits) - 1;
 constexpr int kMaxMembers = 16;
 constexpr double kCTau = 1e-12;
 constexpr double kCInf = 1.0e300;
@@ -166,11 +171,21 @@ __device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int
   return coop_gather_t<kGran>(slot, W, ng, epoch, vals, err, sh_fail);
 }
 
-// Point ownership inside member w: thread tid, group g < K4, lane-of-vector e < 4 owns point
-// t = w·S + 4·(tid + g·kCoopThreads) + e  (valid while t < min(l, (w+1)·S)).
-template <int K4>
+// Point ownership inside member w: thread tid, group g < K4, lane-of-vector e < 4 owns column
+// c = w·S + 4·(tid + g·kCoopThreads) + e  (valid while c < min(lphys, (w+1)·S)).
+//
+// Mapped = false: column c of the stored Gram K_p is point c of the problem.
+// Mapped = true: the problem is a Platt-CV sub-problem whose Gram is a principal submatrix of its
+// parent's (the fit's final problem: same scaled rows, same γ, so the same f32 entries) — no Gram
+// of its own is computed or stored.  K_p is the parent's; maps[moff + c] is the sub-problem's
+// (libsvm-order) index of parent column c, or −1 when that row is in the held-out fold.  Members
+// own contiguous PARENT columns, so row slices stay one float4 load; every point carries the key
+// pk = index << 15 | column through the reductions and exchanges: comparing keys compares libsvm
+// indices (ties → larger index, as unmapped), and the column locates its Gram row and its owner.
+template <int K4, bool Mapped>
 __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopProb* __restrict__ probs, int P,
                                                                 int W, const float* __restrict__ K,
+                                                                const int* __restrict__ maps,
                                                                 double* __restrict__ alpha_all,
                                                                 unsigned long long* __restrict__ xchg,
                                                                 double eps, long long max_iter, SmoCoopOut out) {
@@ -184,8 +199,12 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   const SmoCoopProb Pr = probs[p];
   const float* Kp = K + Pr.koff;
   const int tid = threadIdx.x;
+  if (Mapped && (Pr.lphys > kPkMask + 1 || Pr.l > kPkMask + 1)) {   // keys would overflow: every member leaves
+    if (threadIdx.x == 0) atomicOr(out.err, 2u);
+    return;
+  }
   const int base = w * Pr.S;
-  const int send = min(Pr.l, base + Pr.S);   // may be ≤ base: an empty member still exchanges
+  const int send = min(Pr.lphys, base + Pr.S);   // may be ≤ base: an empty member still exchanges
   unsigned long long* slot0 = xchg + (size_t)p * 2 * kMaxMembers * kGran;
   __shared__ CoopPart shA[kCoopWaves], shB[kCoopWaves];
   __shared__ unsigned vals[2][kMaxMembers][kGran];
@@ -195,25 +214,38 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
 
   double G[KM], A[KM];
   float Qi[KM];
+  int PK[Mapped ? KM : 1];   // Mapped: key of the point in each slot
   unsigned long long ypos = 0ull, upm = 0ull, lowm = 0ull, freem = 0ull, upperm = 0ull, validm = 0ull;
 #pragma unroll
   for (int g = 0; g < K4; ++g)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = 4 * g + e;
-      const int t = base + 4 * (tid + g * kCoopThreads) + e;
+      const int c = base + 4 * (tid + g * kCoopThreads) + e;
       G[k] = -1.0;   // p_i = −1 for C-SVC, α = 0
       A[k] = 0.0;
       Qi[k] = 0.f;
-      if (t < send) {
+      int t = c;
+      if constexpr (Mapped) {
+        t = c >= send ? -1 : Pr.moff >= 0 ? maps[Pr.moff + c] : c;   // moff < 0: the problem's own Gram
+        PK[k] = t >= 0 ? (t << kPkBits) | c : -1;
+      }
+      if (c < send && t >= 0) {
         validm |= 1ull << k;
         if (t < Pr.npos) { ypos |= 1ull << k; upm |= 1ull << k; }   // α = 0 is at the lower bound
         else lowm |= 1ull << k;
       }
     }
-  // (thread, register slot) of point t of this member
-  auto owner_thr = [&](int t) { return ((t - base) >> 2) % kCoopThreads; };
-  auto owner_k = [&](int t) { return 4 * (((t - base) >> 2) / kCoopThreads) + ((t - base) & 3); };
+  // key of slot k (unmapped: its column), and the column and libsvm index of a key
+  auto key_of = [&](int k) {
+    if constexpr (Mapped) return PK[k];
+    else return base + 4 * (tid + (k >> 2) * kCoopThreads) + (k & 3);
+  };
+  auto col_of = [&](int t) { return Mapped ? (t & kPkMask) : t; };
+  auto idx_of = [&](int t) { return Mapped ? (t >> kPkBits) : t; };
+  // (thread, register slot) of the point with key t of this member
+  auto owner_thr = [&](int t) { return ((col_of(t) - base) >> 2) % kCoopThreads; };
+  auto owner_k = [&](int t) { return 4 * (((col_of(t) - base) >> 2) / kCoopThreads) + ((col_of(t) - base) & 3); };
   auto pick = [&](const double* arr, int kk) {
     double v = 0.0;
 #pragma unroll
@@ -240,8 +272,8 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   auto prefetch_issue = [&](int r) {
     Pf pf{{0.f, 0.f, 0.f, 0.f}};
     if (out.prefetch && r >= 0 && tid >= 64) {
-      const float* row = Kp + (size_t)r * Pr.ld;
-      const int lines = (Pr.l + 31) >> 5;
+      const float* row = Kp + (size_t)col_of(r) * Pr.ld;
+      const int lines = (Pr.lphys + 31) >> 5;
       constexpr int kPf = kCoopThreads - 64;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -287,7 +319,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
 #pragma unroll
     for (int k = 0; k < KM; ++k)
       if ((upm >> k) & 1ull) {
-        const int t = base + 4 * (tid + (k >> 2) * kCoopThreads) + (k & 3);
+        const int t = key_of(k);
         const double v = ((ypos >> k) & 1ull) ? -G[k] : G[k];
         if (v > bb || (v == bb && t > bi)) { bb = v; bi = t; }
       }
@@ -312,9 +344,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   for (; iter < max_iter; ++iter) {
     if (i < 0) break;
     const double Gmax = f64_from_okey(r1kb);
-    const int yi = i < Pr.npos ? 1 : -1;
+    const int yi = idx_of(i) < Pr.npos ? 1 : -1;
     // ---- WSS step 2 over this member's slice of row i
-    const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)i * Pr.ld + base);
+    const float4* Ki4 = reinterpret_cast<const float4*>(Kp + (size_t)col_of(i) * Pr.ld + base);
     double gmax2 = -kCInf, bkey = -kCInf;
     int bj = -1;
     float4 qv[K4];
@@ -337,7 +369,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
             double quad = 2.0 - 2.0 * (double)Qi[k];
             if (quad <= 0) quad = kCTau;
             const double key = (gd * gd) / quad;   // smo_kernel's rank: grouping-independent
-            if (bj < 0 || key >= bkey) { bkey = key; bj = t0 + e; }
+            if constexpr (Mapped) {   // slots are in column order, not index order
+              if (bj < 0 || key > bkey || (key == bkey && key_of(k) > bj)) { bkey = key; bj = key_of(k); }
+            } else if (bj < 0 || key >= bkey) { bkey = key; bj = t0 + e; }
           }
         }
       }
@@ -397,7 +431,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
     last_gap = Gmax + gmax2_all;
     if (Gmax + gmax2_all < eps || j < 0) break;
     // ---- pair update (identical in every member)
-    const int yj = j < Pr.npos ? 1 : -1;
+    const int yj = idx_of(j) < Pr.npos ? 1 : -1;
     const double Ci = yi > 0 ? Pr.Cp : Pr.Cn, Cj = yj > 0 ? Pr.Cp : Pr.Cn;
     const double Qij = (double)(yi * yj) * Kij;
     const double Gi = -(double)yi * Gmax;
@@ -443,7 +477,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
 #pragma unroll
     for (int wv = 0; wv < 2; ++wv) {
       const int t = wv == 0 ? i : j;
-      if (t < base || t >= send || tid != owner_thr(t)) continue;
+      if (col_of(t) < base || col_of(t) >= send || tid != owner_thr(t)) continue;
       const int kk = owner_k(t);
       const double a = wv == 0 ? ai : aj;
       const double C = wv == 0 ? Ci : Cj;
@@ -462,7 +496,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
     }
     // ---- gradient update of this member's slice (row i in registers, row j loaded now), fused
     // with the next step-1 candidates
-    const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)j * Pr.ld + base);
+    const float4* Kj4 = reinterpret_cast<const float4*>(Kp + (size_t)col_of(j) * Pr.ld + base);
     float4 qjv[K4];
 #pragma unroll
     for (int g = 0; g < K4; ++g)
@@ -482,7 +516,8 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
         G[k] += pos ? upd : -upd;
         if ((upm >> k) & 1ull) {
           const double v = pos ? -G[k] : G[k];
-          if (v > bb || (v == bb && t0 + e > bi)) { bb = v; bi = t0 + e; }
+          const int tk = Mapped ? key_of(k) : t0 + e;
+          if (v > bb || (v == bb && tk > bi)) { bb = v; bi = tk; }
         }
       }
     }
@@ -497,7 +532,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   // ---- α out (owners) and calculate_rho over all members
 #pragma unroll
   for (int k = 0; k < KM; ++k)
-    if ((validm >> k) & 1ull) alpha_all[Pr.aoff + base + 4 * (tid + (k >> 2) * kCoopThreads) + (k & 3)] = A[k];
+    if ((validm >> k) & 1ull) alpha_all[Pr.aoff + idx_of(key_of(k))] = A[k];
   double ru = -kCInf, rl = -kCInf, sum_free = 0.0;
   int nfree = 0;
 #pragma unroll
@@ -551,9 +586,9 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   }
 }
 
-void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintptr_t alpha, uintptr_t xchg,
-                    double eps, long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap, uintptr_t err,
-                    uintptr_t prof, uintptr_t stream) {
+void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintptr_t maps, uintptr_t alpha,
+                    uintptr_t xchg, double eps, long long max_iter, uintptr_t rho, uintptr_t iters, uintptr_t gap,
+                    uintptr_t err, uintptr_t prof, uintptr_t stream) {
   HFENS_REQUIRE(W >= 1 && W <= kMaxMembers, "smo_coop_batch: 1 <= W <= 16 members per problem");
   HFENS_REQUIRE(P >= 1, "smo_coop_batch: no problems");
   HFENS_REQUIRE(max_S >= 4 && max_S % 4 == 0, "smo_coop_batch: slice must be a positive multiple of 4");
@@ -576,12 +611,19 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
   auto kp = (const float*)K;
   auto ap = (double*)alpha;
   auto xp = (unsigned long long*)xchg;
-#define COOP_CASE(K4)                                                                                       \
-  if (max_S <= 4 * K4 * kCoopThreads) {                                                                     \
-    hipLaunchKernelGGL(smo_coop_kernel<K4>, dim3((unsigned)blocks), dim3(kCoopThreads), 0, st, pp, P, W, kp, \
-                       ap, xp, eps, max_iter, o);                                                           \
-    launch_check();                                                                                         \
-    return;                                                                                                 \
+  auto mp = (const int*)maps;
+  // maps != 0: Platt sub-problems index their parents' Grams (columns < 2^15: checked per problem
+  // in the kernel, which flags err and leaves — the host then re-solves unmapped)
+#define COOP_CASE(K4)                                                                                           \
+  if (max_S <= 4 * K4 * kCoopThreads) {                                                                         \
+    if (mp != nullptr)                                                                                          \
+      hipLaunchKernelGGL((smo_coop_kernel<K4, true>), dim3((unsigned)blocks), dim3(kCoopThreads), 0, st, pp, P, \
+                         W, kp, mp, ap, xp, eps, max_iter, o);                                                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((smo_coop_kernel<K4, false>), dim3((unsigned)blocks), dim3(kCoopThreads), 0, st, pp,   \
+                         P, W, kp, mp, ap, xp, eps, max_iter, o);                                               \
+    launch_check();                                                                                             \
+    return;                                                                                                     \
   }
   COOP_CASE(1) COOP_CASE(2) COOP_CASE(4) COOP_CASE(8)
 #undef COOP_CASE

@@ -393,3 +393,39 @@ def test_scaler_batch_matches_per_fold_scalers(dev):
         # the constant column: exact mean, variance 0, scale 1 (sklearn 0.23.2), in both paths
         assert float(var[k, 3]) == 0.0 and float(sc.var_[3]) == 0.0
     assert torch.all(Z[:, 3] == 0)
+
+
+@pytest.mark.parametrize("rows", [2500, 6000])
+def test_smo_shared_gram_matches_own_grams(dev, monkeypatch, rows):
+    """Platt sub-problems reading their fit's final-problem Gram through a column map
+    (smo_coop_kernel<K4, true>) take the same pairs as with Grams of their own: identical iteration
+    counts and α of EVERY problem (the Platt ones included), ρ to its member-sum order."""
+    from hfens.models import smo
+    X, y = _data(rows, 17, 23)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    yd = y.to(dev)
+    Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
+    monkeypatch.setattr(smo, "COOP_OTF", False)
+    monkeypatch.setattr(smo, "COOP_MIN_SLICE", 384)
+
+    def run(share):
+        monkeypatch.setattr(smo, "SHARE_GRAM", share)
+        svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+        st = smo.launch_svc_batch(svcs, Zs, ys)
+        res = [(p.fit, p.fold, st["sol"][id(p)]) for p in st["all_probs"] if p.rows is not None]
+        res = [(f, k, a.cpu().clone(), float(r), int(it)) for f, k, (a, r, it) in res]
+        info = dict(smo.LAST_SMO_INFO)
+        smo.finish_svc_batch(st)
+        return res, info, svcs
+
+    own, i_own, s_own = run(False)
+    sh, i_sh, s_sh = run(True)
+    assert i_own["members"] > 1 and i_own["grams"] == 12 and i_sh["grams"] == 2
+    for (f, k, a, r, it), (f2, k2, b, r2, it2) in zip(own, sh):
+        assert (f, k, it) == (f2, k2, it2)
+        assert torch.equal(a, b)
+        assert r == pytest.approx(r2, rel=1e-12, abs=1e-14)
+    for a, b in zip(s_own, s_sh):
+        assert torch.equal(a.support_, b.support_)
+        assert a._probA.item() == pytest.approx(b._probA.item(), rel=1e-9)
+        assert a._probB.item() == pytest.approx(b._probB.item(), rel=1e-9, abs=1e-12)
