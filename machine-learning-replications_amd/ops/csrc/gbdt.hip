@@ -21,6 +21,9 @@
 //                     (= sklearn's exact splitter on the model's own training rows), Newton leaf
 //                     values Σr/Σh for children of the last level.
 //   gbdt_route      : move rows of split nodes one level down, accumulating child Σw·r².
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace hfens {
@@ -958,6 +961,37 @@ __device__ __forceinline__ void sg_hist_regs(const unsigned char* __restrict__ c
   __syncthreads();
 }
 
+// MF = true: the histogram of every feature with 2–8 bins (binary features, small ordinals) is an
+// integer GEMM on the matrix cores instead of int64 VALU sums.  The stage's quantised g, h, w
+// (int64 fixed point, |q| < 2^49) are cut into 7 slices of 7 bits (the top slice signed), so
+// B[row][slice] is an i8 matrix of 21 columns; A[indicator][row] is the 0/1 byte (bin == c) of one
+// (feature, bin c ≥ 1) pair per row of A, plus an all-ones row (the node totals, whence bin 0).
+// v_mfma_i32_32x32x32_i8 sums A·B over 32 rows per instruction into exact int32 slice sums
+// (|slice| ≤ 127: exact up to 16.9M rows per workgroup), folded once per sub-tile into an LDS
+// table and recombined as Σ_k S_k·2^{7k} in int64 — the same integers as the VALU path, so the
+// histogram, the split and the trees are bit-identical to it.  Features with more bins keep the
+// LDS int64 atomics.
+constexpr int kSgMaxInd = 128;      // indicator rows (4 M-blocks of 32)
+constexpr int kSgSlices = 7;        // 7-bit slices per value
+typedef int sg_v4i __attribute__((ext_vector_type(4)));
+typedef int sg_v16i __attribute__((ext_vector_type(16)));
+
+// 0x01 in every byte of x equal to c, 0x00 elsewhere (SWAR zero-byte test; no carries across bytes)
+__device__ __forceinline__ int sg_eq_bytes(unsigned x, unsigned c) {
+  const unsigned t = x ^ (c * 0x01010101u);
+  const unsigned nz = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;
+  return (int)((~nz >> 7) & 0x01010101u);
+}
+
+__device__ __forceinline__ long long sg_comb(const int* T, int ind, int v) {
+  const int* r = T + ind * 32 + kSgSlices * v;
+  long long s = 0;
+#pragma unroll
+  for (int k = 0; k < kSgSlices - 1; ++k) s += (long long)r[k] << (7 * k);
+  return s + ((long long)r[kSgSlices - 1] << (7 * (kSgSlices - 1)));
+}
+
+template <bool MF>
 __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J) {
   extern __shared__ __attribute__((aligned(16))) long long sg_lds[];
   long long* hl = sg_lds;                                   // [hist_len][3]
@@ -975,6 +1009,11 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   __shared__ int wf[kSgWaves], wbin[kSgWaves], wrk[kSgWaves];
   __shared__ int pf_s, pblo_s;
   __shared__ double pv_s[3];
+  // MF: indicator rows (feature, bin; −1 = all ones, −2 = padding), MFMA features and their first row
+  __shared__ int s_indf[MF ? kSgMaxInd : 1], s_indc[MF ? kSgMaxInd : 1];
+  __shared__ int l_mf[MF ? kStMaxF : 1], l_mfi[MF ? kStMaxF : 1];
+  __shared__ int n_mf, n_mb;
+  int* Tsl = reinterpret_cast<int*>(qw + kSgRowPad);   // MF: [n_mb·32 indicators][32 slice columns] int32
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = J.n, F = J.F, B = J.B, t = J.t_dev != nullptr ? *J.t_dev : J.t, T = J.T;
   const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
@@ -992,6 +1031,22 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       else if (nb <= 1) l_one[n_one++] = f;
       else if (nb <= 8) l_mid[n_mid++] = f;
       else l_wide[n_wide++] = f;
+    }
+    if constexpr (MF) {
+      int ni = 1;
+      s_indf[0] = -1; s_indc[0] = 0;
+      n_mf = 0; n_wide = 0;
+      for (int f = 0; f < F; ++f) {
+        const int nb = s_nb[f];
+        if (nb >= 2 && nb <= 8 && ni + nb - 1 <= kSgMaxInd) {
+          l_mf[n_mf] = f; l_mfi[n_mf] = ni; ++n_mf;
+          for (int c = 1; c < nb; ++c) { s_indf[ni] = f; s_indc[ni] = c; ++ni; }
+        } else if (nb > 1) {
+          l_wide[n_wide++] = f;
+        }
+      }
+      n_mb = (ni + 31) / 32;
+      for (int i = ni; i < n_mb * 32; ++i) { s_indf[i] = -2; s_indc[i] = 0; }
     }
     pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0;
   }
@@ -1122,8 +1177,11 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   const int pf = pf_s, pblo = pblo_s;
   const double pv0 = pv_s[0], pv1 = pv_s[1], pv2 = pv_s[2];
   long long acc6[6] = {0, 0, 0, 0, 0, 0};   // dev(t−1), r2 root(t), leaf r2 n0..n2 (t−1), bag(t)
-  if (has_cur)
+  if (has_cur) {
     for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) hl[k] = 0;
+    if constexpr (MF)
+      for (int k = tid; k < n_mb * 32 * 32; k += kSgThreads) Tsl[k] = 0;
+  }
   const int w0r = blockIdx.x * J.rows_per_wg;
   const int w1r = min(n, w0r + J.rows_per_wg);
   for (int r0 = w0r; r0 < w1r; r0 += kSgTile) {
@@ -1176,89 +1234,191 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     for (int k = m + tid; k < kSgTile; k += kSgThreads) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
     __syncthreads();
     if (pst && tid == 0 && r0 == w0r) pst[1] = (long long)__builtin_amdgcn_s_memtime() - t_0;
-    // stage-t histogram of the sub-tile.  Every wave covers ALL 1024 rows (lane ℓ owns rows
-    // 16ℓ … 16ℓ+15, their quantised g/h/w in registers) and takes features f ≡ wave (mod 8): one
-    // 16-byte load per lane and feature, sums in registers, wave reductions, lane 0 adds the
-    // feature's bins into the LDS histogram (features are disjoint across waves: no barrier).
-    long long rg[16], rh[16], rv[16];
+    if constexpr (MF) {
+      // (a) binary / ≤ 8-bin features on the matrix cores: wave w takes rows [128w, 128w + 128) of
+      // the sub-tile in 4 K-steps of 32; lane (c = lane & 31, h = lane >> 5) holds, for the 16 rows
+      // 16h … 16h + 15 of the step, slice c % 7 of value c / 7 (B, c < 21) and the indicator bytes
+      // of A-row c of every M-block (A and B bytes j of half h are the same row: the product sums
+      // the same row set whatever the hardware's k order inside a fragment)
+      const int c = lane & 31, hh = lane >> 5;
+      const int vsel = c / kSgSlices, ks = c - kSgSlices * vsel;
+      const long long* qv = vsel == 0 ? qg : (vsel == 1 ? qh : qw);
+      const int nmb = n_mb;
+      sg_v16i acc[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int ri = 17 * lane + j;   // sg_ri(16·lane + j)
-      rg[j] = qg[ri]; rh[j] = qh[ri]; rv[j] = qw[ri];
-    }
-    long long tg3 = 0, th3 = 0, tw3 = 0;
+      for (int mb = 0; mb < 4; ++mb) acc[mb] = sg_v16i{};
 #pragma unroll
-    for (int j = 0; j < 16; ++j) { tg3 += rg[j]; th3 += rh[j]; tw3 += rv[j]; }
-    tg3 = wave_sum_i64(tg3);
-    th3 = wave_sum_i64(th3);
-    tw3 = wave_sum_i64(tw3);
-    const unsigned char* bt = J.bins + r0 + 16 * lane;
-    // this wave's features in groups of 4: the group's four 16-byte tiles are loaded together
-    for (int fg = wave; fg < F; fg += 4 * kSgWaves) {
-      uint4 pre[4];
+      for (int kst = 0; kst < 4; ++kst) {
+        const int k0 = 128 * wave + 32 * kst + 16 * hh;   // 16-aligned: rows k0 … k0+15 are contiguous in the padded cache
+        sg_v4i bf = sg_v4i{0, 0, 0, 0};
+        if (c < 3 * kSgSlices) {
+          const long long* src = qv + sg_ri(k0);
+          const int sh = 7 * ks;
+          const unsigned msk = ks < kSgSlices - 1 ? 127u : 255u;
+          int wd[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int f = fg + u * kSgWaves;
-        pre[u] = f < F ? *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb) : make_uint4(0, 0, 0, 0);
+          for (int d = 0; d < 4; ++d) {
+            unsigned x = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x |= ((unsigned)(src[4 * d + e] >> sh) & msk) << (8 * e);
+            wd[d] = (int)x;
+          }
+          bf = sg_v4i{wd[0], wd[1], wd[2], wd[3]};
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          if (mb >= nmb) break;
+          const int f = s_indf[mb * 32 + c];
+          sg_v4i af;
+          if (f >= 0) {
+            const uint4 x = *reinterpret_cast<const uint4*>(J.bins + (size_t)f * J.ldb + r0 + k0);
+            const unsigned cc = (unsigned)s_indc[mb * 32 + c];
+            af = sg_v4i{sg_eq_bytes(x.x, cc), sg_eq_bytes(x.y, cc), sg_eq_bytes(x.z, cc), sg_eq_bytes(x.w, cc)};
+          } else {
+            const int o = f == -1 ? 0x01010101 : 0;
+            af = sg_v4i{o, o, o, o};
+          }
+          acc[mb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, acc[mb], 0, 0, 0);
+        }
       }
+      // fold this wave's 32×32 slice sums into the workgroup table (D: col = lane & 31,
+      // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-      const int f = fg + u * kSgWaves;
-      if (f >= F) break;
-      const int nb = s_nb[f], off = s_off[f];
-      const uint4 v4 = pre[u];
-      const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
-      if (nb <= 1) {
-        if (lane == 0) { hl[off * 3] += tg3; hl[off * 3 + 1] += th3; hl[off * 3 + 2] += tw3; }
-      } else if (nb == 2) {
-        long long a = 0, c = 0, d = 0;
+      for (int mb = 0; mb < 4; ++mb) {
+        if (mb >= nmb) break;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int v = acc[mb][r];
+          if (v != 0) atomicAdd(&Tsl[(mb * 32 + row) * 32 + c], v);
+        }
+      }
+      // (b) wider features: LDS int64 atomics, lane ℓ owns rows 16ℓ … 16ℓ+15, features split over waves
+      const unsigned char* bt = J.bins + r0 + 16 * lane;
+      for (int fi = wave; fi < n_wide; fi += kSgWaves) {
+        const int f = l_wide[fi], off = s_off[f];
+        const uint4 v4 = *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb);
+        const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const bool one = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          a += one ? rg[j] : 0;
-          c += one ? rh[j] : 0;
-          d += one ? rv[j] : 0;
-        }
-        a = wave_sum_i64(a);
-        c = wave_sum_i64(c);
-        d = wave_sum_i64(d);
-        if (lane == 0) {
-          hl[(off + 1) * 3] += a; hl[(off + 1) * 3 + 1] += c; hl[(off + 1) * 3 + 2] += d;
-          hl[off * 3] += tg3 - a; hl[off * 3 + 1] += th3 - c; hl[off * 3 + 2] += tw3 - d;
-        }
-      } else if (nb <= 8) {
-        long long acc[24];
-#pragma unroll
-        for (int k = 0; k < 24; ++k) acc[k] = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const bool hit = bb == (unsigned)c;
-            acc[3 * c] += hit ? rg[j] : 0;
-            acc[3 * c + 1] += hit ? rh[j] : 0;
-            acc[3 * c + 2] += hit ? rv[j] : 0;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 24; ++k) {
-          if (k < 3 * nb) {
-            const long long sv = wave_sum_i64(acc[k]);
-            if (lane == 0) hl[off * 3 + k] += sv;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (rv[j] == 0) continue;
+          const int ri = 17 * lane + j;   // sg_ri(16·lane + j)
+          const long long wq = qw[ri];
+          if (wq == 0) continue;
           const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
           long long* cell = hl + ((size_t)off + bb) * 3;
-          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)rg[j]);
-          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)rh[j]);
-          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)rv[j]);
+          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)qg[ri]);
+          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)qh[ri]);
+          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)wq);
         }
       }
+    } else {
+      // stage-t histogram of the sub-tile.  Every wave covers ALL 1024 rows (lane ℓ owns rows
+      // 16ℓ … 16ℓ+15, their quantised g/h/w in registers) and takes features f ≡ wave (mod 8): one
+      // 16-byte load per lane and feature, sums in registers, wave reductions, lane 0 adds the
+      // feature's bins into the LDS histogram (features are disjoint across waves: no barrier).
+      long long rg[16], rh[16], rv[16];
+  #pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int ri = 17 * lane + j;   // sg_ri(16·lane + j)
+        rg[j] = qg[ri]; rh[j] = qh[ri]; rv[j] = qw[ri];
+      }
+      long long tg3 = 0, th3 = 0, tw3 = 0;
+  #pragma unroll
+      for (int j = 0; j < 16; ++j) { tg3 += rg[j]; th3 += rh[j]; tw3 += rv[j]; }
+      tg3 = wave_sum_i64(tg3);
+      th3 = wave_sum_i64(th3);
+      tw3 = wave_sum_i64(tw3);
+      const unsigned char* bt = J.bins + r0 + 16 * lane;
+      // this wave's features in groups of 4: the group's four 16-byte tiles are loaded together
+      for (int fg = wave; fg < F; fg += 4 * kSgWaves) {
+        uint4 pre[4];
+  #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int f = fg + u * kSgWaves;
+          pre[u] = f < F ? *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb) : make_uint4(0, 0, 0, 0);
+        }
+  #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+        const int f = fg + u * kSgWaves;
+        if (f >= F) break;
+        const int nb = s_nb[f], off = s_off[f];
+        const uint4 v4 = pre[u];
+        const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
+        if (nb <= 1) {
+          if (lane == 0) { hl[off * 3] += tg3; hl[off * 3 + 1] += th3; hl[off * 3 + 2] += tw3; }
+        } else if (nb == 2) {
+          long long a = 0, c = 0, d = 0;
+  #pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const bool one = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            a += one ? rg[j] : 0;
+            c += one ? rh[j] : 0;
+            d += one ? rv[j] : 0;
+          }
+          a = wave_sum_i64(a);
+          c = wave_sum_i64(c);
+          d = wave_sum_i64(d);
+          if (lane == 0) {
+            hl[(off + 1) * 3] += a; hl[(off + 1) * 3 + 1] += c; hl[(off + 1) * 3 + 2] += d;
+            hl[off * 3] += tg3 - a; hl[off * 3 + 1] += th3 - c; hl[off * 3 + 2] += tw3 - d;
+          }
+        } else if (nb <= 8) {
+          long long acc[24];
+  #pragma unroll
+          for (int k = 0; k < 24; ++k) acc[k] = 0;
+  #pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+  #pragma unroll
+            for (int c = 0; c < 8; ++c) {
+              const bool hit = bb == (unsigned)c;
+              acc[3 * c] += hit ? rg[j] : 0;
+              acc[3 * c + 1] += hit ? rh[j] : 0;
+              acc[3 * c + 2] += hit ? rv[j] : 0;
+            }
+          }
+  #pragma unroll
+          for (int k = 0; k < 24; ++k) {
+            if (k < 3 * nb) {
+              const long long sv = wave_sum_i64(acc[k]);
+              if (lane == 0) hl[off * 3 + k] += sv;
+            }
+          }
+        } else {
+  #pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            if (rv[j] == 0) continue;
+            const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            long long* cell = hl + ((size_t)off + bb) * 3;
+            atomicAdd((unsigned long long*)&cell[0], (unsigned long long)rg[j]);
+            atomicAdd((unsigned long long*)&cell[1], (unsigned long long)rh[j]);
+            atomicAdd((unsigned long long*)&cell[2], (unsigned long long)rv[j]);
+          }
+        }
+        }
+      }
+    }
+  }
+  if constexpr (MF) {
+    if (has_cur) {
+      // slice sums → int64 bins: bin c ≥ 1 of an MFMA feature is its indicator row, bin 0 the node
+      // total (all-ones row) minus the others; constant features get the total
+      __syncthreads();
+      for (int u = tid; u < 3 * (n_mf + n_one); u += kSgThreads) {
+        const int fi = u / 3, v = u - 3 * fi;
+        const long long tot_v = sg_comb(Tsl, 0, v);
+        if (fi < n_mf) {
+          const int f = l_mf[fi], i0 = l_mfi[fi], off = s_off[f], nb = s_nb[f];
+          long long rest = 0;
+          for (int cb = 1; cb < nb; ++cb) {
+            const long long sv = sg_comb(Tsl, i0 + cb - 1, v);
+            hl[(off + cb) * 3 + v] += sv;
+            rest += sv;
+          }
+          hl[off * 3 + v] += tot_v - rest;
+        } else {
+          hl[s_off[l_one[fi - n_mf]] * 3 + v] += tot_v;
+        }
       }
     }
   }
@@ -1299,7 +1459,9 @@ __global__ __launch_bounds__(256) void gbdt_stage_reduce_kernel(const long long*
   if (s != 0) atomicAdd((unsigned long long*)&slot[(size_t)b * slot_m + k], (unsigned long long)s);
 }
 
-size_t gbdt_stump_stage_lds(int hist_len) { return (3 * (size_t)hist_len + 3 * kSgRowPad) * sizeof(long long); }
+size_t gbdt_stump_stage_lds(int hist_len, bool mf) {
+  return (3 * (size_t)hist_len + 3 * kSgRowPad) * sizeof(long long) + (mf ? kSgMaxInd * 32 * sizeof(int) : 0);
+}
 
 void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long long ldb, uintptr_t nbins, int hist_len,
                       uintptr_t lo_val, uintptr_t hi_val, uintptr_t y, uintptr_t w, uintptr_t raw, uintptr_t wt,
@@ -1312,8 +1474,12 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
   const bool active = subsample < 1.0;
   HFENS_REQUIRE(!active || (wt != 0 && seeds != 0 && bagw != 0), "gbdt_stump_stage: subsample needs wt, seeds, bagw");
-  const size_t lds = gbdt_stump_stage_lds(hist_len);
-  HFENS_REQUIRE(hist_len >= F && lds <= 150 * 1024, "gbdt_stump_stage: histogram + row cache exceed LDS");
+  // MF: binary / ≤ 8-bin features on the i8 matrix cores (HFENS_GBDT_MFMA=0: int64 VALU sums)
+  const char* mfe = std::getenv("HFENS_GBDT_MFMA");   // read per launch: tests toggle it
+  const bool mf_env = !(mfe && mfe[0] == '0');
+  bool mf = mf_env && gbdt_stump_stage_lds(hist_len, true) <= 150 * 1024;
+  HFENS_REQUIRE(hist_len >= F && gbdt_stump_stage_lds(hist_len, false) <= 150 * 1024,
+                "gbdt_stump_stage: histogram + row cache exceed LDS");
   StageJob J{(const unsigned char*)bins, (const int*)nbins, (const double*)lo_val, (const double*)hi_val,
              (const float*)y, (const float*)w, (double*)raw, (float*)wt, (const unsigned long long*)seeds,
              (long long*)comm, (int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
@@ -1323,20 +1489,30 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   // t_dev (graph replay): the kernel takes the stage index from device memory; the host t still
   // selects the comm slot of the reduce launch, so a captured unit must start at t ≡ 0 (mod 3)
   HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");
-  // rows per workgroup: 1024-row sub-tiles, as many per workgroup as keeps the grid near 2
-  // workgroups per CU (the redundant split and the histogram flush are per workgroup)
+  // rows per workgroup: 1024-row sub-tiles, as many per workgroup as keeps the whole grid within
+  // k workgroups per CU (default 1: the kernel holds one workgroup per CU, so a grid one workgroup
+  // over the CU count runs a second full round; the redundant split and the histogram flush are
+  // per workgroup, so fewer, longer workgroups also do less of both)
   int dev_id = 0, ncu = 256;
   HFENS_CHECK(hipGetDevice(&dev_id));
   HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id));
+  static const int wgs_per_cu = [] {
+    const char* e = std::getenv("HFENS_SG_WGS_PER_CU");
+    return e ? std::min(2, std::max(1, std::atoi(e))) : 1;
+  }();
   const long long tiles = (n + kSgTile - 1) / kSgTile;
-  const long long want = (2LL * ncu + B - 1) / B;                  // workgroups per model
-  const long long per = (tiles + want - 1) / want;                 // sub-tiles per workgroup
+  const long long want = std::max(1LL, (long long)wgs_per_cu * ncu / B);   // workgroups per model
+  const long long per = (tiles + want - 1) / want;                          // sub-tiles per workgroup
   J.rows_per_wg = (int)(per * kSgTile);
   const int groups = (int)((n + J.rows_per_wg - 1) / J.rows_per_wg);
+  // exact int32 slice sums: |slice| ≤ 127 per row
+  if ((long long)J.rows_per_wg * 127 >= (1LL << 31)) mf = false;
+  const size_t lds = gbdt_stump_stage_lds(hist_len, mf);
   const long long slot_m = 3LL * hist_len + kSgExtra;
   if (groups <= kRdSplit || partials == 0) J.partials = nullptr;
   else HFENS_REQUIRE(partials_len >= (long long)B * groups * slot_m, "gbdt_stump_stage: partials buffer too small");
-  hipLaunchKernelGGL(gbdt_stump_stage_kernel, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+  if (mf) hipLaunchKernelGGL(gbdt_stump_stage_kernel<true>, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+  else hipLaunchKernelGGL(gbdt_stump_stage_kernel<false>, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   launch_check();
   if (J.partials != nullptr && t <= T) {
     long long* slot = (long long*)comm + (size_t)(t % 3) * B * slot_m;

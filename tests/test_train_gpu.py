@@ -178,6 +178,37 @@ def test_gbdt_stump_paths_bit_identical(dev, monkeypatch, subsample):
                 assert torch.equal(getattr(a, attr), getattr(b, attr)), (other, attr)
 
 
+@pytest.mark.parametrize("rows,subsample", [(6000, 1.0), (150000, 0.7)])
+def test_gbdt_stage_mfma_hist_bit_identical(dev, monkeypatch, rows, subsample):
+    """gbdt_stump_stage with the i8-MFMA histogram (binary and <= 8-bin features as 7-bit slice
+    GEMMs, HFENS_GBDT_MFMA=1) equals the int64 VALU histogram (=0) bit for bit; the data mixes
+    binary, 3- to 6-bin ordinal, constant and wide continuous features, and 150k rows spread each
+    model over many workgroups and sub-tiles."""
+    from hfens.models import hist_gbdt
+    monkeypatch.setattr(hist_gbdt, "STUMP_PATH", "stage")
+    monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", False)
+    X, y = _data(rows, 24, 53)
+    g = torch.Generator().manual_seed(5)
+    X[:, 4] = torch.randint(0, 3, (rows,), generator=g).double()
+    X[:, 5] = torch.randint(0, 6, (rows,), generator=g).double() * 0.5
+    X[:, 7] = 1.0
+    masks = torch.ones(3, rows, dtype=torch.bool)
+    masks[1, ::4] = False
+    masks[2, 1::3] = False
+    out = {}
+    for mf in ("0", "1"):
+        monkeypatch.setenv("HFENS_GBDT_MFMA", mf)
+        ms = [GradientBoostingClassifier(n_estimators=40, max_depth=1, subsample=subsample, random_state=s)
+              for s in range(3)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        assert hist_gbdt.LAST_PATH["path"] == "stage"
+        out[mf] = ms
+    for a, b in zip(out["0"], out["1"]):
+        for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
+                     "tree_weighted_n_node_samples_", "train_score_"):
+            assert torch.equal(getattr(a, attr), getattr(b, attr)), attr
+
+
 @pytest.mark.parametrize("rows", [2500, 70000])
 def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
     """gbdt_stump_stage with sklearn's feature-visit tie-break (duplicated columns force exact
