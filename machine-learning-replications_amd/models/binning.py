@@ -65,41 +65,86 @@ class BinMapper:
         return idx.to(torch.uint8)
 
 
-def _fit_bins_device(X32: torch.Tensor, max_bins: int) -> BinMapper:
-    """All features at once on the device: one segmented sort of [F, n], run starts, distinct
-    counts, the ≤ max_bins distinct values or the quantile group ends (hi = the value of rank
-    ⌈i·n/max_bins⌉, lo of the next group = the next distinct value), then ONE device→host copy of
-    the [F, max_bins] tables.  Same bins as the per-feature path (run-rank ⇔ cumulative count)."""
+def _fit_bins_device(X32: torch.Tensor, max_bins: int, guard=None) -> BinMapper:
+    """All features at once on the device, then ONE device→host copy of the [F, max_bins] tables.
+
+    * Features whose values are all integers in [0, 255] (binary flags, small ordinals — most of a
+      Table-S1 cohort) need no sort: one batched ``bincount`` of the values gives their occupied
+      values, i.e. the sorted distinct values.
+    * The other features are sorted (one radix sort each), then run starts give the distinct counts
+      and the ≤ max_bins distinct values, or the quantile group ends (hi = the value of rank
+      ⌈i·n/max_bins⌉, lo of the next group = the next distinct value).
+    Same bins as the per-feature path (run-rank ⇔ cumulative count)."""
     n, F = X32.shape
     dev = X32.device
     Xt = X32.t().contiguous()
-    srt = torch.empty_like(Xt)                                           # [F, n]
-    for f in range(F):   # F one-dimensional radix sorts beat one segmented [F, n] sort (measured)
-        srt[f] = torch.sort(Xt[f])[0]
-    new = torch.ones_like(srt, dtype=torch.bool)
-    new[:, 1:] = srt[:, 1:] != srt[:, :-1]
-    k_h = new.sum(1).cpu()                                               # one sync: distinct counts
-    small_f = [f for f in range(F) if int(k_h[f]) <= max_bins]
-    big_f = [f for f in range(F) if int(k_h[f]) > max_bins]
+    is_small_int = ((Xt == torch.round(Xt)) & (Xt >= 0) & (Xt <= 255)).all(1)
+    occ = None
+    if guard is not None:   # the caller's deferred input guards ride on this read (one sync, not three)
+        flags, specs = guard
+        h = torch.cat([is_small_int, torch.stack(list(flags))]).cpu()
+        from ..utils.guards import raise_flags
+        raise_flags(h[F:].tolist(), specs)
+        si_h = h[:F]
+    else:
+        si_h = is_small_int.cpu()                                        # one sync: which features
+    int_f = [f for f in range(F) if bool(si_h[f])]
+    if int_f and max_bins < 256:
+        # 256 distinct integers would exceed max_bins: those features go to the sorted path
+        ii = torch.as_tensor(int_f, device=dev)
+        codes = Xt.index_select(0, ii).to(torch.int64) + 256 * torch.arange(len(int_f), device=dev)[:, None]
+        nocc = (torch.bincount(codes.reshape(-1), minlength=256 * len(int_f)).view(len(int_f), 256) > 0).sum(1).cpu()
+        int_f = [f for j, f in enumerate(int_f) if int(nocc[j]) <= max_bins]
+    sort_f = [f for f in range(F) if f not in set(int_f)]
+    occ_d = None
+    if int_f:
+        ii = torch.as_tensor(int_f, device=dev)
+        codes = Xt.index_select(0, ii).to(torch.int64) + 256 * torch.arange(len(int_f), device=dev)[:, None]
+        occ_d = torch.bincount(codes.reshape(-1), minlength=256 * len(int_f)).view(len(int_f), 256) > 0
+    srt = new = None
+    if sort_f:
+        srt = torch.empty(len(sort_f), n, dtype=X32.dtype, device=dev)   # [F_sort, n]
+        for i_, f in enumerate(sort_f):   # one-dimensional radix sorts beat one segmented sort (measured)
+            srt[i_] = torch.sort(Xt[f])[0]
+        new = torch.ones_like(srt, dtype=torch.bool)
+        new[:, 1:] = srt[:, 1:] != srt[:, :-1]
+    # one read for both paths: occupied small integers, distinct counts of the sorted features
+    parts = ([occ_d.reshape(-1).to(torch.int64)] if int_f else []) + ([new.sum(1)] if sort_f else [])
+    hv = torch.cat(parts).cpu() if parts else torch.zeros(0, dtype=torch.int64)
+    if int_f:
+        occ = hv[:256 * len(int_f)].view(len(int_f), 256) > 0
+    ks = hv[256 * len(int_f):] if int_f else hv
+    k_h = torch.zeros(F, dtype=torch.int64)
     small_h = torch.full((F, max_bins), float("nan"), dtype=torch.float32)
-    if small_f:
-        vals = [srt[f][new[f]] for f in small_f]                          # ≤ max_bins each
-        packed = torch.full((len(small_f), max_bins), float("nan"), dtype=torch.float32, device=dev)
-        for i_, v in enumerate(vals):
-            packed[i_, :v.numel()] = v
-        small_h[small_f] = packed.cpu()
     hi_h = torch.zeros(F, max_bins, dtype=torch.float32)
     lo_h = torch.zeros(F, max_bins, dtype=torch.float32)
-    mn_h = srt[:, 0].cpu()
-    if big_f:
-        bi = torch.as_tensor(big_f, device=dev)
-        sb = srt.index_select(0, bi)
-        tau = torch.arange(1, max_bins, dtype=torch.float64, device=dev) * (n / max_bins)
-        idx = torch.cat([torch.ceil(tau).to(torch.int64) - 1, torch.tensor([n - 1], device=dev)]).clamp(0, n - 1)
-        hq = sb[:, idx].contiguous()                                     # quantile group ends
-        pos = torch.searchsorted(sb, hq, right=True).clamp(max=n - 1)
-        hi_h[big_f] = hq.cpu()
-        lo_h[big_f] = sb.gather(1, pos).cpu()                           # next distinct values
+    mn_h = torch.zeros(F, dtype=torch.float32)
+    for j, f in enumerate(int_f):
+        vals = torch.nonzero(occ[j])[:, 0].to(torch.float32)
+        k_h[f] = vals.numel()
+        small_h[f, :vals.numel()] = vals
+        mn_h[f] = vals[0]
+    if sort_f:
+        k_h[sort_f] = ks
+        small_s = [i_ for i_ in range(len(sort_f)) if int(ks[i_]) <= max_bins]
+        big_s = [i_ for i_ in range(len(sort_f)) if int(ks[i_]) > max_bins]
+        if small_s:
+            packed = torch.full((len(small_s), max_bins), float("nan"), dtype=torch.float32, device=dev)
+            for r_, i_ in enumerate(small_s):
+                v = srt[i_][new[i_]]                                     # ≤ max_bins values
+                packed[r_, :v.numel()] = v
+            small_h[[sort_f[i_] for i_ in small_s]] = packed.cpu()
+        mn_h[sort_f] = srt[:, 0].cpu()
+        if big_s:
+            bi = torch.as_tensor(big_s, device=dev)
+            sb = srt.index_select(0, bi)
+            tau = torch.arange(1, max_bins, dtype=torch.float64, device=dev) * (n / max_bins)
+            idx = torch.cat([torch.ceil(tau).to(torch.int64) - 1, torch.tensor([n - 1], device=dev)]).clamp(0, n - 1)
+            hq = sb[:, idx].contiguous()                                 # quantile group ends
+            pos = torch.searchsorted(sb, hq, right=True).clamp(max=n - 1)
+            big_f = [sort_f[i_] for i_ in big_s]
+            hi_h[big_f] = hq.cpu()
+            lo_h[big_f] = sb.gather(1, pos).cpu()                       # next distinct values
     return _assemble(k_h, small_h, hi_h, lo_h, mn_h, max_bins, dev)
 
 
@@ -261,7 +306,10 @@ def _distinct(v32: torch.Tensor, group=None):
     return u, c
 
 
-def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
+def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None, guard=None) -> BinMapper:
+    """``guard``: optional (device bool flags, specs) of deferred input checks
+    (``utils.guards.finite_flag``/``binary_flag``), read with the device bin fit's first transfer;
+    on other paths they are read here."""
     if not 2 <= max_bins <= 256:
         raise ValueError("max_bins must be in [2, 256]")
     n, F = X.shape
@@ -269,7 +317,10 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None) -> BinMapper:
     X32 = X.to(torch.float32)
     host = group is None and n <= HOST_BIN_MAX_ROWS
     if group is None and not host and X32.is_cuda:
-        return _fit_bins_device(X32, max_bins)
+        return _fit_bins_device(X32, max_bins, guard)
+    if guard is not None:
+        from ..utils.guards import raise_flags
+        raise_flags(torch.stack(list(guard[0])).cpu().tolist(), guard[1])
     if group is not None and not LEGACY_DP_BINS:
         return _fit_bins_dp(X32, max_bins, group)
     Xh = X32.cpu().numpy() if host else None

@@ -280,8 +280,15 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     from ..utils.guards import check_binary, check_finite
     from ..utils.timing import hmark
     hmark("gbc_start")
-    check_finite(X, "GradientBoostingClassifier.fit X")
-    check_binary(y, "GradientBoostingClassifier.fit y")
+    guard = None
+    if binned is None and X.is_cuda:
+        # deferred: read with the bin fit's first transfer (one host sync instead of three)
+        from ..utils.guards import binary_flag, finite_flag
+        guard = ([finite_flag(X), binary_flag(y)],
+                 [("finite", "GradientBoostingClassifier.fit X"), ("binary", "GradientBoostingClassifier.fit y")])
+    else:
+        check_finite(X, "GradientBoostingClassifier.fit X")
+        check_binary(y, "GradientBoostingClassifier.fit y")
     dev = X.device
     n, F = X.shape
     B = len(models)
@@ -294,7 +301,7 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     w = masks.to(device=dev, dtype=torch.float32).contiguous()
     yv = y.to(device=dev, dtype=torch.float32).contiguous()
     if binned is None:
-        bm = fit_bins(X, int(m0.max_bins), group)
+        bm = fit_bins(X, int(m0.max_bins), group, guard=guard)
         bins = bm.transform(X).contiguous()
     else:
         bm, bins = binned

@@ -282,6 +282,28 @@ __device__ __forceinline__ void scan_feature(const long long* __restrict__ hf, i
   }
 }
 
+// scan_feature for nb ≤ 4 bins (binary and small features: every bin is lane 0's in scan_feature):
+// each lane computes lane 0's result itself from the same (broadcast) reads — no cross-lane scan and
+// no argmax shuffles; same arithmetic in the same order, so the same (gain, bin).
+__device__ __forceinline__ void scan_feature_small(const long long* hf, int nb, long long tw, long long tg,
+                                                   double min_leaf_q, double& best_gain, int& best_bin) {
+  best_gain = -1.0;
+  best_bin = 0x7fffffff;
+  long long lw = 0, lg = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= nb - 1) break;
+    lw += hf[j * 3 + 2];
+    lg += hf[j * 3 + 0];
+    const long long rw = tw - lw, rg = tg - lg;
+    if ((double)lw < min_leaf_q || (double)rw < min_leaf_q) continue;
+    const double dlw = (double)lw, drw = (double)rw;
+    const double diff = drw * (double)lg - dlw * (double)rg;
+    const double gain = diff / dlw * diff / drw;
+    if (gain > best_gain) { best_gain = gain; best_bin = j; }
+  }
+}
+
 __global__ __launch_bounds__(256) void gbdt_split_kernel(
     GbdtShape S, const long long* __restrict__ hist, const int* __restrict__ nbins,
     const double* __restrict__ lo_val, const double* __restrict__ hi_val, int node0, int NL,
@@ -872,6 +894,7 @@ constexpr int kSgWaves = kSgThreads / 64;
 constexpr int kSgTile = 1024;       // rows per workgroup (LDS row cache: 3 × 8 B per row)
 constexpr int kSgExtra = 8;         // int64 extras per model and slot
 constexpr int kSgRowPad = kSgTile + kSgTile / 16;   // padded row-cache length
+constexpr int kSgArrSkew = 4;                       // int64 skew between the qg / qh / qw arrays
 __device__ __forceinline__ int sg_ri(int r) { return r + (r >> 4); }
 
 struct StageJob {
@@ -997,9 +1020,11 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   long long* hl = sg_lds;                                   // [hist_len][3]
   // row cache: quantised g, h, w of 1024 rows, row r at r + r/16 (one pad word per 16 rows: lane ℓ
   // reading row 16ℓ + j then strides 17 words — conflict-free — instead of 16, a 32-way conflict)
+  // (the three arrays are 4 words apart modulo the 64 banks: the MFMA B-fragment build reads row
+  // k of all three in one instruction — 3-way bank conflicts with a plain kSgRowPad stride)
   long long* qg = sg_lds + 3 * (size_t)J.hist_len;
-  long long* qh = qg + kSgRowPad;
-  long long* qw = qh + kSgRowPad;
+  long long* qh = qg + kSgRowPad + kSgArrSkew;
+  long long* qw = qh + kSgRowPad + kSgArrSkew;
   __shared__ long long red[kSgWaves * 24];
   __shared__ int s_nb[kStMaxF], s_off[kStMaxF];
   __shared__ int l_bin[kStMaxF], l_one[kStMaxF], l_mid[kStMaxF], l_wide[kStMaxF];
@@ -1013,7 +1038,8 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   __shared__ int s_indf[MF ? kSgMaxInd : 1], s_indc[MF ? kSgMaxInd : 1];
   __shared__ int l_mf[MF ? kStMaxF : 1], l_mfi[MF ? kStMaxF : 1];
   __shared__ int n_mf, n_mb;
-  int* Tsl = reinterpret_cast<int*>(qw + kSgRowPad);   // MF: [n_mb·32 indicators][32 slice columns] int32
+  __shared__ int s_ord[kStMaxF];   // split-scan order: features with > 4 bins first (spread over waves)
+  int* Tsl = reinterpret_cast<int*>(qw + kSgRowPad + kSgArrSkew);   // MF: [n_mb·32 indicators][32 slice columns] int32
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = J.n, F = J.F, B = J.B, t = J.t_dev != nullptr ? *J.t_dev : J.t, T = J.T;
   const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
@@ -1031,6 +1057,11 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       else if (nb <= 1) l_one[n_one++] = f;
       else if (nb <= 8) l_mid[n_mid++] = f;
       else l_wide[n_wide++] = f;
+    }
+    {
+      int o2 = 0;
+      for (int f = 0; f < F; ++f) if (s_nb[f] > 4) s_ord[o2++] = f;
+      for (int f = 0; f < F; ++f) if (s_nb[f] <= 4) s_ord[o2++] = f;
     }
     if constexpr (MF) {
       int ni = 1;
@@ -1079,8 +1110,27 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   if (t > T) return;   // the closing launch only books the last slot
   // ---- 1: split of tree t−1 from the reduced stage-(t−1) histogram
   if (t >= 1) {
-    const long long* hp = slot_prev;
+    // stage the reduced histogram in LDS first (one bulk round of loads, 8 in flight per thread):
+    // the scans below then cost LDS latency instead of a dependent global round per feature
     const long long root_r2 = slot_prev[3 * (size_t)J.hist_len];
+    {
+      const int len = 3 * J.hist_len;
+      for (int k0 = tid; k0 < len; k0 += 8 * kSgThreads) {
+        long long v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * kSgThreads;
+          v[u] = k < len ? slot_prev[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * kSgThreads;
+          if (k < len) hl[k] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+    const long long* hp = hl;
     if (wave == 0) {
       long long a = 0, c = 0, d = 0;
       for (int bb = lane; bb < s_nb[0]; bb += 64) { a += hp[bb * 3]; c += hp[bb * 3 + 1]; d += hp[bb * 3 + 2]; }
@@ -1100,10 +1150,12 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       double bg = -1.0;
       int bf = 0x7fffffff, bbin = 0, brk = 0x7fffffff;
       if ((double)tw >= J.min_split_q) {
-        for (int f = wave; f < F; f += kSgWaves) {
+        for (int fo = wave; fo < F; fo += kSgWaves) {
+          const int f = s_ord[fo];
           double gg;
           int gb;
-          scan_feature(hp + (size_t)s_off[f] * 3, s_nb[f], lane, tw, tg, J.min_leaf_q, gg, gb);
+          if (s_nb[f] <= 4) scan_feature_small(hp + (size_t)s_off[f] * 3, s_nb[f], tw, tg, J.min_leaf_q, gg, gb);
+          else scan_feature(hp + (size_t)s_off[f] * 3, s_nb[f], lane, tw, tg, J.min_leaf_q, gg, gb);
           const int r = rk ? rk[f] : f;
           if (gg > bg || (gg == bg && gg >= 0.0 && r < brk)) { bg = gg; bf = f; bbin = gb; brk = r; }
         }
@@ -1184,13 +1236,38 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   }
   const int w0r = blockIdx.x * J.rows_per_wg;
   const int w1r = min(n, w0r + J.rows_per_wg);
+  // a sub-tile's row inputs (this thread's two rows: kSgTile = 2 × threads) are loaded one sub-tile
+  // ahead — issued before the previous sub-tile's histogram, consumed by the next apply — so their
+  // global latencies overlap the histogram instead of stalling the apply
+  static_assert(kSgTile == 2 * kSgThreads, "two rows per thread");
+  float w0v[2];
+  double rwv[2], yv[2];
+  int bnv[2];
+  auto load_rows = [&](int rs) {
+    const int ms = min(kSgTile, w1r - rs);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = tid + u * kSgThreads;
+      const bool ok = k < ms;
+      const int i = rs + (ok ? k : 0);
+      const size_t bi = (size_t)b * n + i;
+      w0v[u] = ok ? J.w[bi] : 0.f;
+      rwv[u] = ok ? J.raw[bi] : 0.0;
+      yv[u] = ok ? (double)J.y[i] : 0.0;
+      bnv[u] = (ok && has_prev && pf >= 0) ? (int)J.bins[(size_t)pf * J.ldb + i] : 0;
+    }
+  };
+  if (w0r < w1r) load_rows(w0r);
   for (int r0 = w0r; r0 < w1r; r0 += kSgTile) {
     const int m = min(kSgTile, w1r - r0);
     __syncthreads();   // the previous sub-tile's histogram passes are done with the row cache
-    for (int k = tid; k < m; k += kSgThreads) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = tid + u * kSgThreads;
+      if (k >= m) continue;
       const int i = r0 + k;
       const size_t bi = (size_t)b * n + i;
-      const float w0 = J.w[bi];
+      const float w0 = w0v[u];
       float wi = w0, wp = w0;
       if (J.active) {
         const unsigned long long sd = J.seeds[b];
@@ -1198,10 +1275,10 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
         wp = (has_prev && gb_in_bag(sd, t - 1, J.row_off + i, J.thr24)) ? w0 : 0.f;
         if (has_cur) J.wt[bi] = wi;
       }
-      double rw = J.raw[bi];
-      const double yi = J.y[i];
+      double rw = rwv[u];
+      const double yi = yv[u];
       if (has_prev) {
-        const int nd = pf >= 0 ? (J.bins[(size_t)pf * J.ldb + i] <= pblo ? 1 : 2) : 0;
+        const int nd = pf >= 0 ? (bnv[u] <= pblo ? 1 : 2) : 0;
         if (wp > 0.f) {
           const double p0 = 1.0 / (1.0 + exp(-rw));
           const double r0d = yi - p0;
@@ -1230,6 +1307,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
         if (J.active) acc6[5] += in ? q_of(wi, J.qscale) : 0;
       }
     }
+    if (r0 + kSgTile < w1r) load_rows(r0 + kSgTile);
     if (!has_cur) continue;
     for (int k = m + tid; k < kSgTile; k += kSgThreads) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
     __syncthreads();
@@ -1247,9 +1325,25 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       sg_v16i acc[4];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) acc[mb] = sg_v16i{};
+      // A bytes of every M-block, one K-step ahead (the global loads overlap the B build and MFMAs)
+      const unsigned char* arow[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int f = mb < nmb ? s_indf[mb * 32 + c] : -2;
+        arow[mb] = f >= 0 ? J.bins + (size_t)f * J.ldb + r0 + 128 * wave + 16 * hh : nullptr;
+      }
+      uint4 araw[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+        araw[mb] = arow[mb] ? *reinterpret_cast<const uint4*>(arow[mb]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int kst = 0; kst < 4; ++kst) {
         const int k0 = 128 * wave + 32 * kst + 16 * hh;   // 16-aligned: rows k0 … k0+15 are contiguous in the padded cache
+        uint4 anext[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+          anext[mb] = (kst < 3 && arow[mb]) ? *reinterpret_cast<const uint4*>(arow[mb] + 32 * (kst + 1))
+                                            : make_uint4(0, 0, 0, 0);
         sg_v4i bf = sg_v4i{0, 0, 0, 0};
         if (c < 3 * kSgSlices) {
           const long long* src = qv + sg_ri(k0);
@@ -1267,25 +1361,27 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
         }
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
-          if (mb >= nmb) break;
-          const int f = s_indf[mb * 32 + c];
-          sg_v4i af;
-          if (f >= 0) {
-            const uint4 x = *reinterpret_cast<const uint4*>(J.bins + (size_t)f * J.ldb + r0 + k0);
-            const unsigned cc = (unsigned)s_indc[mb * 32 + c];
-            af = sg_v4i{sg_eq_bytes(x.x, cc), sg_eq_bytes(x.y, cc), sg_eq_bytes(x.z, cc), sg_eq_bytes(x.w, cc)};
-          } else {
-            const int o = f == -1 ? 0x01010101 : 0;
-            af = sg_v4i{o, o, o, o};
+          if (mb < nmb) {
+            const int f = s_indf[mb * 32 + c];
+            sg_v4i af;
+            if (f >= 0) {
+              const uint4 x = araw[mb];
+              const unsigned cc = (unsigned)s_indc[mb * 32 + c];
+              af = sg_v4i{sg_eq_bytes(x.x, cc), sg_eq_bytes(x.y, cc), sg_eq_bytes(x.z, cc), sg_eq_bytes(x.w, cc)};
+            } else {
+              const int o = f == -1 ? 0x01010101 : 0;
+              af = sg_v4i{o, o, o, o};
+            }
+            acc[mb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, acc[mb], 0, 0, 0);
           }
-          acc[mb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, acc[mb], 0, 0, 0);
+          araw[mb] = anext[mb];
         }
       }
       // fold this wave's 32×32 slice sums into the workgroup table (D: col = lane & 31,
       // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
-        if (mb >= nmb) break;
+        if (mb >= nmb) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -1460,7 +1556,8 @@ __global__ __launch_bounds__(256) void gbdt_stage_reduce_kernel(const long long*
 }
 
 size_t gbdt_stump_stage_lds(int hist_len, bool mf) {
-  return (3 * (size_t)hist_len + 3 * kSgRowPad) * sizeof(long long) + (mf ? kSgMaxInd * 32 * sizeof(int) : 0);
+  return (3 * (size_t)hist_len + 3 * (kSgRowPad + kSgArrSkew)) * sizeof(long long) +
+         (mf ? kSgMaxInd * 32 * sizeof(int) : 0);
 }
 
 void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long long ldb, uintptr_t nbins, int hist_len,

@@ -25,3 +25,26 @@ def check_binary(y: torch.Tensor, what: str) -> torch.Tensor:
     if ENABLED and y.numel() and not bool(((y == 0) | (y == 1)).all()):
         raise ValueError(f"{what}: labels must be 0/1")
     return y
+
+
+def finite_flag(t: torch.Tensor) -> torch.Tensor:
+    """Deferred form of ``check_finite``: a device bool (no host read) for a caller that reads it
+    together with other device results in ONE transfer, then calls ``raise_flags``."""
+    if not (ENABLED and t.numel() and t.is_floating_point()):
+        return torch.ones((), dtype=torch.bool, device=t.device)
+    return torch.isfinite(t).all()
+
+
+def binary_flag(y: torch.Tensor) -> torch.Tensor:
+    if not (ENABLED and y.numel()):
+        return torch.ones((), dtype=torch.bool, device=y.device)
+    return ((y == 0) | (y == 1)).all()
+
+
+def raise_flags(vals, specs) -> None:
+    """``vals``: host bools read from ``finite_flag``/``binary_flag``; ``specs``: (kind, what) per flag."""
+    for ok, (kind, what) in zip(vals, specs):
+        if not bool(ok):
+            if kind == "finite":
+                raise NonFiniteError(f"{what}: non-finite value(s)")
+            raise ValueError(f"{what}: labels must be 0/1")

@@ -130,15 +130,19 @@ def test_batched_bin_fit_matches_per_feature():
     from hfens.models import binning
     X, _, _ = make_hf_cohort(5000, 20, seed=81, nan_frac=0.0)
     X = torch.as_tensor(X)
-    X[:, 0] = torch.round(X[:, 0] * 3)          # few distinct values
+    X[:, 0] = torch.round(X[:, 0] * 3)          # few distinct values (some negative: sorted path)
+    X[:, 1] = torch.arange(5000) % 40 + 3.0      # small non-negative integers: bincount path
+    X[:, 2] = torch.arange(5000) % 300.0         # integers beyond 255: sorted path
     X32 = X.to(torch.float32)
+    for mb in (256, 16):
+        a = binning._fit_bins_device(X32, mb)
+        b = binning.fit_bins(X, mb)
+        assert torch.equal(a.nbins.cpu(), b.nbins.cpu())
+        assert torch.equal(a.lo_val.cpu(), b.lo_val.cpu())
+        assert torch.equal(a.hi_val.cpu(), b.hi_val.cpu())
+        assert torch.equal(a.edges.cpu(), b.edges.cpu())
     a = binning._fit_bins_device(X32, 256)
-    b = binning.fit_bins(X, 256)
-    assert torch.equal(a.nbins.cpu(), b.nbins.cpu())
-    assert torch.equal(a.lo_val.cpu(), b.lo_val.cpu())
-    assert torch.equal(a.hi_val.cpu(), b.hi_val.cpu())
-    assert torch.equal(a.edges.cpu(), b.edges.cpu())
-    assert int(a.nbins.max()) == 256 and int(a.nbins.min()) <= 8
+    assert int(a.nbins.max()) == 256 and int(a.nbins.min()) <= 8 and int(a.nbins[1]) == 40
 
 
 def test_knn_transform_many_equals_single_transforms():
