@@ -927,7 +927,7 @@ struct StageJob {
   const int* t_dev;                   // stage index read from device memory (graph replay), or nullptr: t
 };
 
-template <int NV>
+template <int NV, int NW = kSgWaves>
 __device__ __forceinline__ void sg_block_sum(long long (&v)[NV], long long* red, long long* out) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -938,7 +938,7 @@ __device__ __forceinline__ void sg_block_sum(long long (&v)[NV], long long* red,
   __syncthreads();
   if ((int)threadIdx.x < NV) {
     long long s = 0;
-    for (int k = 0; k < kSgWaves; ++k) s += red[k * 24 + threadIdx.x];
+    for (int k = 0; k < NW; ++k) s += red[k * 24 + threadIdx.x];
     out[threadIdx.x] = s;
   }
   __syncthreads();
@@ -1014,8 +1014,13 @@ __device__ __forceinline__ long long sg_comb(const int* T, int ind, int v) {
   return s + ((long long)r[kSgSlices - 1] << (7 * (kSgSlices - 1)));
 }
 
-template <bool MF>
-__global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J) {
+template <bool MF, int NT>
+__global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
+  constexpr int kT = NT, kW = NT / 64;       // threads, waves
+  constexpr int RPT = kSgTile / kT;           // rows per thread in the apply
+  constexpr int RPW = kSgTile / kW;           // rows per wave in the MFMA histogram
+  constexpr int KS = RPW / 32;                // its K-steps of 32 rows
+  static_assert(RPT * kT == kSgTile && KS * 32 * kW == kSgTile, "tile shape");
   extern __shared__ __attribute__((aligned(16))) long long sg_lds[];
   long long* hl = sg_lds;                                   // [hist_len][3]
   // row cache: quantised g, h, w of 1024 rows, row r at r + r/16 (one pad word per 16 rows: lane ℓ
@@ -1025,13 +1030,13 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   long long* qg = sg_lds + 3 * (size_t)J.hist_len;
   long long* qh = qg + kSgRowPad + kSgArrSkew;
   long long* qw = qh + kSgRowPad + kSgArrSkew;
-  __shared__ long long red[kSgWaves * 24];
+  __shared__ long long red[kW * 24];
   __shared__ int s_nb[kStMaxF], s_off[kStMaxF];
   __shared__ int l_bin[kStMaxF], l_one[kStMaxF], l_mid[kStMaxF], l_wide[kStMaxF];
   __shared__ int n_bin, n_one, n_mid, n_wide;
   __shared__ long long tot[3], bsum[24], ext[8];
-  __shared__ double wg[kSgWaves];
-  __shared__ int wf[kSgWaves], wbin[kSgWaves], wrk[kSgWaves];
+  __shared__ double wg[kW];
+  __shared__ int wf[kW], wbin[kW], wrk[kW];
   __shared__ int pf_s, pblo_s;
   __shared__ double pv_s[3];
   // MF: indicator rows (feature, bin; −1 = all ones, −2 = padding), MFMA features and their first row
@@ -1084,7 +1089,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   // zero the slot that launch t+1 accumulates (nobody reads or writes it during launch t)
   {
     const size_t nwg = (size_t)gridDim.x * gridDim.y, wid = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    for (size_t k = wid * kSgThreads + tid; k < slot_sz; k += nwg * kSgThreads) slot_next[k] = 0;
+    for (size_t k = wid * kT + tid; k < slot_sz; k += nwg * kT) slot_next[k] = 0;
   }
   __syncthreads();
   const bool lead = blockIdx.x == 0;
@@ -1115,16 +1120,16 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     const long long root_r2 = slot_prev[3 * (size_t)J.hist_len];
     {
       const int len = 3 * J.hist_len;
-      for (int k0 = tid; k0 < len; k0 += 8 * kSgThreads) {
+      for (int k0 = tid; k0 < len; k0 += 8 * kT) {
         long long v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u * kSgThreads;
+          const int k = k0 + u * kT;
           v[u] = k < len ? slot_prev[k] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u * kSgThreads;
+          const int k = k0 + u * kT;
           if (k < len) hl[k] = v[u];
         }
       }
@@ -1150,7 +1155,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       double bg = -1.0;
       int bf = 0x7fffffff, bbin = 0, brk = 0x7fffffff;
       if ((double)tw >= J.min_split_q) {
-        for (int fo = wave; fo < F; fo += kSgWaves) {
+        for (int fo = wave; fo < F; fo += kW) {
           const int f = s_ord[fo];
           double gg;
           int gb;
@@ -1164,7 +1169,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       __syncthreads();
       if (tid == 0) {
         bg = wg[0]; bf = wf[0]; bbin = wbin[0]; brk = wrk[0];
-        for (int k = 1; k < kSgWaves; ++k)
+        for (int k = 1; k < kW; ++k)
           if (wg[k] > bg || (wg[k] == bg && wrk[k] < brk)) { bg = wg[k]; bf = wf[k]; bbin = wbin[k]; brk = wrk[k]; }
         wg[0] = bg; wf[0] = bf; wbin[0] = bbin;
       }
@@ -1230,24 +1235,23 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
   const double pv0 = pv_s[0], pv1 = pv_s[1], pv2 = pv_s[2];
   long long acc6[6] = {0, 0, 0, 0, 0, 0};   // dev(t−1), r2 root(t), leaf r2 n0..n2 (t−1), bag(t)
   if (has_cur) {
-    for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) hl[k] = 0;
+    for (int k = tid; k < 3 * J.hist_len; k += kT) hl[k] = 0;
     if constexpr (MF)
-      for (int k = tid; k < n_mb * 32 * 32; k += kSgThreads) Tsl[k] = 0;
+      for (int k = tid; k < n_mb * 32 * 32; k += kT) Tsl[k] = 0;
   }
   const int w0r = blockIdx.x * J.rows_per_wg;
   const int w1r = min(n, w0r + J.rows_per_wg);
   // a sub-tile's row inputs (this thread's two rows: kSgTile = 2 × threads) are loaded one sub-tile
   // ahead — issued before the previous sub-tile's histogram, consumed by the next apply — so their
   // global latencies overlap the histogram instead of stalling the apply
-  static_assert(kSgTile == 2 * kSgThreads, "two rows per thread");
-  float w0v[2];
-  double rwv[2], yv[2];
-  int bnv[2];
+  float w0v[RPT];
+  double rwv[RPT], yv[RPT];
+  int bnv[RPT];
   auto load_rows = [&](int rs) {
     const int ms = min(kSgTile, w1r - rs);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = tid + u * kSgThreads;
+    for (int u = 0; u < RPT; ++u) {
+      const int k = tid + u * kT;
       const bool ok = k < ms;
       const int i = rs + (ok ? k : 0);
       const size_t bi = (size_t)b * n + i;
@@ -1262,8 +1266,8 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     const int m = min(kSgTile, w1r - r0);
     __syncthreads();   // the previous sub-tile's histogram passes are done with the row cache
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = tid + u * kSgThreads;
+    for (int u = 0; u < RPT; ++u) {
+      const int k = tid + u * kT;
       if (k >= m) continue;
       const int i = r0 + k;
       const size_t bi = (size_t)b * n + i;
@@ -1309,7 +1313,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     }
     if (r0 + kSgTile < w1r) load_rows(r0 + kSgTile);
     if (!has_cur) continue;
-    for (int k = m + tid; k < kSgTile; k += kSgThreads) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
+    for (int k = m + tid; k < kSgTile; k += kT) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
     __syncthreads();
     if (pst && tid == 0 && r0 == w0r) pst[1] = (long long)__builtin_amdgcn_s_memtime() - t_0;
     if constexpr (MF) {
@@ -1330,19 +1334,19 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
         const int f = mb < nmb ? s_indf[mb * 32 + c] : -2;
-        arow[mb] = f >= 0 ? J.bins + (size_t)f * J.ldb + r0 + 128 * wave + 16 * hh : nullptr;
+        arow[mb] = f >= 0 ? J.bins + (size_t)f * J.ldb + r0 + RPW * wave + 16 * hh : nullptr;
       }
       uint4 araw[4];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
         araw[mb] = arow[mb] ? *reinterpret_cast<const uint4*>(arow[mb]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int kst = 0; kst < 4; ++kst) {
-        const int k0 = 128 * wave + 32 * kst + 16 * hh;   // 16-aligned: rows k0 … k0+15 are contiguous in the padded cache
+      for (int kst = 0; kst < KS; ++kst) {
+        const int k0 = RPW * wave + 32 * kst + 16 * hh;   // 16-aligned: rows k0 … k0+15 are contiguous in the padded cache
         uint4 anext[4];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
-          anext[mb] = (kst < 3 && arow[mb]) ? *reinterpret_cast<const uint4*>(arow[mb] + 32 * (kst + 1))
+          anext[mb] = (kst < KS - 1 && arow[mb]) ? *reinterpret_cast<const uint4*>(arow[mb] + 32 * (kst + 1))
                                             : make_uint4(0, 0, 0, 0);
         sg_v4i bf = sg_v4i{0, 0, 0, 0};
         if (c < 3 * kSgSlices) {
@@ -1391,7 +1395,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       }
       // (b) wider features: LDS int64 atomics, lane ℓ owns rows 16ℓ … 16ℓ+15, features split over waves
       const unsigned char* bt = J.bins + r0 + 16 * lane;
-      for (int fi = wave; fi < n_wide; fi += kSgWaves) {
+      for (int fi = wave; fi < n_wide; fi += kW) {
         const int f = l_wide[fi], off = s_off[f];
         const uint4 v4 = *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb);
         const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -1426,16 +1430,16 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       tw3 = wave_sum_i64(tw3);
       const unsigned char* bt = J.bins + r0 + 16 * lane;
       // this wave's features in groups of 4: the group's four 16-byte tiles are loaded together
-      for (int fg = wave; fg < F; fg += 4 * kSgWaves) {
+      for (int fg = wave; fg < F; fg += 4 * kW) {
         uint4 pre[4];
   #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int f = fg + u * kSgWaves;
+          const int f = fg + u * kW;
           pre[u] = f < F ? *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb) : make_uint4(0, 0, 0, 0);
         }
   #pragma unroll
         for (int u = 0; u < 4; ++u) {
-        const int f = fg + u * kSgWaves;
+        const int f = fg + u * kW;
         if (f >= F) break;
         const int nb = s_nb[f], off = s_off[f];
         const uint4 v4 = pre[u];
@@ -1500,7 +1504,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
       // slice sums → int64 bins: bin c ≥ 1 of an MFMA feature is its indicator row, bin 0 the node
       // total (all-ones row) minus the others; constant features get the total
       __syncthreads();
-      for (int u = tid; u < 3 * (n_mf + n_one); u += kSgThreads) {
+      for (int u = tid; u < 3 * (n_mf + n_one); u += kT) {
         const int fi = u / 3, v = u - 3 * fi;
         const long long tot_v = sg_comb(Tsl, 0, v);
         if (fi < n_mf) {
@@ -1519,7 +1523,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     }
   }
   if (pst && tid == 0) pst[2] = (long long)__builtin_amdgcn_s_memtime() - t_0;
-  sg_block_sum<6>(acc6, red, ext);
+  sg_block_sum<6, kW>(acc6, red, ext);
   // publish: with many workgroups per model, plain stores of the whole partial slot (reduced by
   // gbdt_stage_reduce_kernel — hundreds of workgroups' int64 atomics on the same ~50 KB of
   // histogram serialise at the memory side); with few, atomics straight into the slot
@@ -1532,7 +1536,7 @@ __global__ __launch_bounds__(kSgThreads) void gbdt_stump_stage_kernel(StageJob J
     else if (v != 0) atomicAdd((unsigned long long*)&slot_cur[3 * (size_t)J.hist_len + tid], (unsigned long long)v);
   }
   __syncthreads();
-  for (int k = tid; k < 3 * J.hist_len; k += kSgThreads) {
+  for (int k = tid; k < 3 * J.hist_len; k += kT) {
     const long long v = has_cur ? hl[k] : 0;
     if (part) part[k] = v;
     else if (v != 0) atomicAdd((unsigned long long*)&slot_cur[k], (unsigned long long)v);
@@ -1574,6 +1578,8 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   // MF: binary / ≤ 8-bin features on the i8 matrix cores (HFENS_GBDT_MFMA=0: int64 VALU sums)
   const char* mfe = std::getenv("HFENS_GBDT_MFMA");   // read per launch: tests toggle it
   const bool mf_env = !(mfe && mfe[0] == '0');
+  const char* nte = std::getenv("HFENS_SG_THREADS");   // MFMA path: 512 or 1024 threads per workgroup
+  const int nt = nte && std::atoi(nte) == 1024 ? 1024 : kSgThreads;
   bool mf = mf_env && gbdt_stump_stage_lds(hist_len, true) <= 150 * 1024;
   HFENS_REQUIRE(hist_len >= F && gbdt_stump_stage_lds(hist_len, false) <= 150 * 1024,
                 "gbdt_stump_stage: histogram + row cache exceed LDS");
@@ -1608,8 +1614,9 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   const long long slot_m = 3LL * hist_len + kSgExtra;
   if (groups <= kRdSplit || partials == 0) J.partials = nullptr;
   else HFENS_REQUIRE(partials_len >= (long long)B * groups * slot_m, "gbdt_stump_stage: partials buffer too small");
-  if (mf) hipLaunchKernelGGL(gbdt_stump_stage_kernel<true>, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
-  else hipLaunchKernelGGL(gbdt_stump_stage_kernel<false>, dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+  if (mf && nt == 1024) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, 1024>), dim3(groups, B), dim3(1024), lds, as_stream(stream), J);
+  else if (mf) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+  else hipLaunchKernelGGL((gbdt_stump_stage_kernel<false, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   launch_check();
   if (J.partials != nullptr && t <= T) {
     long long* slot = (long long*)comm + (size_t)(t % 3) * B * slot_m;

@@ -196,17 +196,19 @@ def test_gbdt_stage_mfma_hist_bit_identical(dev, monkeypatch, rows, subsample):
     masks[1, ::4] = False
     masks[2, 1::3] = False
     out = {}
-    for mf in ("0", "1"):
+    for mf, nt in (("0", "512"), ("1", "512"), ("1", "1024")):
         monkeypatch.setenv("HFENS_GBDT_MFMA", mf)
+        monkeypatch.setenv("HFENS_SG_THREADS", nt)
         ms = [GradientBoostingClassifier(n_estimators=40, max_depth=1, subsample=subsample, random_state=s)
               for s in range(3)]
         fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
         assert hist_gbdt.LAST_PATH["path"] == "stage"
-        out[mf] = ms
-    for a, b in zip(out["0"], out["1"]):
-        for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
-                     "tree_weighted_n_node_samples_", "train_score_"):
-            assert torch.equal(getattr(a, attr), getattr(b, attr)), attr
+        out[mf + nt] = ms
+    for key in ("1512", "11024"):
+        for a, b in zip(out["0512"], out[key]):
+            for attr in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_",
+                         "tree_weighted_n_node_samples_", "train_score_"):
+                assert torch.equal(getattr(a, attr), getattr(b, attr)), (key, attr)
 
 
 @pytest.mark.parametrize("rows", [2500, 70000])
