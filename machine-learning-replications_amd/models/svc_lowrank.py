@@ -88,6 +88,7 @@ def _wsyrk_part_len(n: int, r: int, ncu: int) -> int:
 NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
+F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
 
 
 def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
@@ -117,10 +118,21 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     return S
 
 
-def _phit(Phi: torch.Tensor, V: torch.Tensor) -> torch.Tensor:
+def _phit(Phi: torch.Tensor, V: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
     """Φᵀ V for a skinny V [l, k] as a split-K batched GEMM (the library's transposed GEMV over
-    a 10⁶-long reduction ran 50× below HBM rate: one output tile, no K split)."""
+    a 10⁶-long reduction ran 50× below HBM rate: one output tile, no K split).  ``P32``: the same
+    Φ stored in f32 (Φ = f64(P32) exactly): the native split-K pass reads half the bytes."""
     l, r = Phi.shape
+    if P32 is not None and r <= 512 and r % 4 == 0 and V.shape[1] <= 4 and P32.data_ptr() % 16 == 0:
+        from .. import runtime
+        k = V.shape[1]
+        G = (l + 63) // 64 if l < 1024 * 64 else 1024
+        part = runtime.workspace(Phi.device, "phit_part", G * r * k, torch.float64)
+        Vc = V.to(torch.float64).contiguous()
+        out = torch.empty(r, k, dtype=torch.float64, device=Phi.device)
+        ops.ext().phit_f32(P32.data_ptr(), Vc.data_ptr(), l, r, k, part.data_ptr(), G * r * k, out.data_ptr(),
+                           ops.stream_ptr(Phi.device))
+        return out
     k = l // _SYRK_CHUNK
     out = torch.zeros(r, V.shape[1], dtype=Phi.dtype, device=Phi.device)
     if k > 0:
@@ -132,16 +144,26 @@ def _phit(Phi: torch.Tensor, V: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _phi_mv(Phi: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+def _phi_mv(Phi: torch.Tensor, W: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
     """Φ W for a skinny W [r, k] (k ≤ 4): GPU one native pass over Φ (ops/csrc/lowrank.hip
-    phi_gemv), else the library product."""
+    phi_gemv; over the f32 copy ``P32`` when given), else the library product."""
     l, r = Phi.shape
     if _native(Phi) and r <= 512 and W.shape[1] <= 4:
         Wc = W.to(torch.float64).contiguous()
         Y = torch.empty(l, W.shape[1], dtype=torch.float64, device=Phi.device)
-        ops.ext().phi_gemv(Phi.data_ptr(), Wc.data_ptr(), l, r, W.shape[1], Y.data_ptr(), ops.stream_ptr(Phi.device))
+        fn = ops.ext().phi_gemv_f32 if P32 is not None else ops.ext().phi_gemv
+        fn((P32 if P32 is not None else Phi).data_ptr(), Wc.data_ptr(), l, r, W.shape[1], Y.data_ptr(),
+           ops.stream_ptr(Phi.device))
         return Y
     return Phi @ W
+
+
+def _bc(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """A 0-dim device scalar as a dense vector shaped like ``like``: torch runs vector ⊙ 0-dim-tensor
+    ops through its strided broadcast kernel, ≈ 10× slower on 10⁶-long f64 vectors than the
+    vectorised same-shape kernel (measured: 63 vs 6 µs), so the IPM's scalar-times-vector updates
+    expand the scalar once instead."""
+    return t.reshape(1).expand(like.shape[0]).contiguous()
 
 
 def _max_step(v, dv):
@@ -161,6 +183,13 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     l, r = Phi.shape
     dt = torch.float64
     Phi = Phi.to(dt)
+    # the skinny passes read an f32 copy when Φ is exactly f32-representable (fit_svc_lowrank_batch
+    # rounds the Nyström map once, so every product below sees the same matrix)
+    P32 = None
+    if F32_PHI and _native(Phi) and r <= 512:
+        p32 = Phi.to(torch.float32)
+        if bool((p32.to(dt) == Phi).all()):
+            P32 = p32
     y = y.to(dt)
     c = c.to(dt)
     a = 0.5 * c
@@ -178,12 +207,13 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         Lc = torch.empty(r, r, dtype=dt, device=Phi.device)
         scv = torch.empty(r, dtype=dt, device=Phi.device)
         info = torch.zeros(1, dtype=torch.int32, device=Phi.device)
+    yk = {1: y[:, None], 2: torch.stack([y, y], 1)}
     it = 0
     for it in range(1, max_iter + 1):
         s = c - a
-        w = _phit(Phi, (y * a)[:, None])[:, 0]       # Φᵀ Y α
-        g = y * _phi_mv(Phi, w[:, None])[:, 0] - 1.0   # Qα − 1
-        rd = g + b * y - nu + mu
+        w = _phit(Phi, (y * a)[:, None], P32)[:, 0]       # Φᵀ Y α
+        g = y * _phi_mv(Phi, w[:, None], P32)[:, 0] - 1.0   # Qα − 1
+        rd = g + _bc(b, y) * y - nu + mu
         re = torch.dot(y, a)
         gap = (torch.dot(a, nu) + torch.dot(s, mu)) / (2 * l)
         parts = [gap, rd.abs().max(), re.abs()] + ([info[0].to(dt)] if native else [])
@@ -232,9 +262,16 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                 Lc, inf = torch.linalg.cholesky_ex(Ss + jit * eye)
                 jit *= 100.0
 
+        # same-shape operands in Minv (no [l, k] × [l, 1] broadcasting: torch's broadcast kernels ran
+        # ~10× below the vectorised same-shape ones on these 10⁶-row vectors)
+        Dk = {1: Dinv[:, None], 2: torch.stack([Dinv, Dinv], 1)}
+
         def Minv(u):  # (D + V Vᵀ)⁻¹ u for u [l, k], V = YΦ
-            du = Dinv[:, None] * u
-            rhs = _phit(Phi, y[:, None] * du)
+            kk = u.shape[1]
+            Dinv_k = Dk[kk] if kk in Dk else Dinv[:, None]
+            y_k = yk[kk] if kk in yk else y[:, None]
+            du = Dinv_k * u
+            rhs = _phit(Phi, y_k * du, P32)
             if native:
                 rhs = rhs.contiguous()
                 E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, rhs.shape[1], rhs.data_ptr(),
@@ -242,11 +279,11 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                 t = rhs
             else:
                 t = sc[:, None] * torch.cholesky_solve(sc[:, None] * rhs, Lc)
-            return du - Dinv[:, None] * (y[:, None] * _phi_mv(Phi, t))
+            return du - Dinv_k * (y_k * _phi_mv(Phi, t, P32))
 
         def dirs(Mh, My, yMy, rnu, rmu):
             db = (torch.dot(y, Mh) + re) / yMy
-            da = Mh - db * My
+            da = Mh - _bc(db, My) * My
             dnu = (-rnu - nu * da) / a
             dmu = (-rmu + mu * da) / s
             return da, db, dnu, dmu
@@ -263,11 +300,13 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         yMy = torch.dot(y, My)
         da, db, dnu, dmu = dirs(Mh, My, yMy, rnu, rmu)
         ta = step_len(da, dnu, dmu)
-        gap_aff = (torch.dot(a + ta * da, nu + ta * dnu) + torch.dot(s - ta * da, mu + ta * dmu)) / (2 * l)
+        tav = _bc(ta, a)
+        gap_aff = (torch.dot(a + tav * da, nu + tav * dnu) + torch.dot(s - tav * da, mu + tav * dmu)) / (2 * l)
         sigma = (gap_aff / gap) ** 3
         # corrector (centring + second-order terms)
         tau = sigma * gap
-        rnu, rmu = a * nu + da * dnu - tau, s * mu - da * dmu - tau
+        tauv = _bc(tau, a)
+        rnu, rmu = a * nu + da * dnu - tauv, s * mu - da * dmu - tauv
         h = -rd - rnu / a + rmu / s
         Mc = Minv(h[:, None])[:, 0]
         if CHECK:
@@ -287,30 +326,32 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         # large SVM duals otherwise crawl at step lengths of 0.25–0.5 (profiles/r2_ipm_native.md).
         # Accept / reject stays on the device (no host synchronisation).
         for _ in range(N_CORRECTORS):
-            at = torch.clamp(1.5 * alpha + 0.1, max=1.0)
-            va = (a + at * da) * (nu + at * dnu)
-            vs = (s - at * da) * (mu + at * dmu)
-            lo, hi = 0.1 * tau, 10.0 * tau
-            ta_c = torch.clamp(torch.clamp(va, lo, hi) - va, min=-hi)
-            ts_c = torch.clamp(torch.clamp(vs, lo, hi) - vs, min=-hi)
+            atv = _bc(torch.clamp(1.5 * alpha + 0.1, max=1.0), a)
+            va = (a + atv * da) * (nu + atv * dnu)
+            vs = (s - atv * da) * (mu + atv * dmu)
+            lo, hi = 0.1 * tauv, 10.0 * tauv
+            ta_c = torch.maximum(torch.minimum(torch.maximum(va, lo), hi) - va, -hi)
+            ts_c = torch.maximum(torch.minimum(torch.maximum(vs, lo), hi) - vs, -hi)
             Mh = Minv((ta_c / a - ts_c / s)[:, None])[:, 0]
             dbc = torch.dot(y, Mh) / yMy
-            dac = Mh - dbc * My
+            dac = Mh - _bc(dbc, My) * My
             nda, ndb = da + dac, db + dbc
             ndnu = dnu + (ta_c - nu * dac) / a
             ndmu = dmu + (ts_c + mu * dac) / s
             nalpha = step_len(nda, ndnu, ndmu)
             ok = nalpha >= 1.01 * alpha
-            da, db = torch.where(ok, nda, da), torch.where(ok, ndb, db)
-            dnu, dmu = torch.where(ok, ndnu, dnu), torch.where(ok, ndmu, dmu)
+            okv = _bc(ok, a)
+            da, db = torch.where(okv, nda, da), torch.where(ok, ndb, db)
+            dnu, dmu = torch.where(okv, ndnu, dnu), torch.where(okv, ndmu, dmu)
             alpha = torch.where(ok, nalpha, alpha)
         t = 0.995 * alpha
         if DEBUG:
             print(f"[ipm]   step ta {float(ta):.3e} t {float(t):.3e} sigma {float(sigma):.3e}", flush=True)
-        a = a + t * da
+        tv = _bc(t, a)
+        a = a + tv * da
         b = b + t * db
-        nu = nu + t * dnu
-        mu = mu + t * dmu
+        nu = nu + tv * dnu
+        mu = mu + tv * dmu
     # snap points the interior point left within 1e-9·C of a bound (their multiplier carries the
     # gap); ρ = −b: stationarity gives y_i G_i = −b on every free point, which is libsvm's ρ
     a = torch.where(a < 1e-9 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-9), c, a))
@@ -348,6 +389,10 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
         pick = np.concatenate([np.sort(pick[~cls1]), np.sort(pick[cls1])])
         idx = torch.as_tensor(pick, device=dev)
         Phi, T = nystrom_map(Zd, idx, gamma)
+        if F32_PHI and _native(Phi) and Phi.shape[1] <= 512:
+            # Φ rounded to f32 once (≈ 6e-8 relative, far inside the Nyström approximation's own
+            # error): the IPM's HBM-bound skinny passes then read an f32 copy, half the bytes
+            Phi = Phi.to(torch.float32).to(torch.float64)
         # libsvm-internal labels: class 0 = +1 (grouped order); per-point C
         yint = torch.as_tensor(np.where(y_np > 0.5, -1.0, 1.0), dtype=torch.float64, device=dev)
         cvec = torch.where(yint > 0, torch.full_like(yint, mt["C0"]), torch.full_like(yint, mt["C1"]))

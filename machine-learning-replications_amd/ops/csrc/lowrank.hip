@@ -173,13 +173,15 @@ void wsyrk_f64(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, l
 // Y[i][q] = Σ_c Φ[i][c]·W[c][q], q < k ≤ 4.  Waves stride over rows (one 4 KB row per wave step:
 // lane l owns columns 8l … 8l+7, r ≤ 512, with its W slice in registers); wave-sum per (row, q).
 constexpr int kGvMaxK = 4;
+constexpr int kGvRows = 4;
 
-template <int K>
-__global__ __launch_bounds__(256) void phi_gemv_kernel(const double* __restrict__ Phi, const double* __restrict__ W,
+template <int K, typename TP>
+__global__ __launch_bounds__(256) void phi_gemv_kernel(const TP* __restrict__ Phi, const double* __restrict__ W,
                                                        long long n, int r, double* __restrict__ Y) {
   const int lane = threadIdx.x & 63;
   const long long wave = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
   const long long waves = (long long)gridDim.x * 4;
+  const bool vec4 = (r & 3) == 0 && (reinterpret_cast<uintptr_t>(Phi) & 15) == 0;
   double w[8][K];
 #pragma unroll
   for (int e = 0; e < 8; ++e)
@@ -188,51 +190,192 @@ __global__ __launch_bounds__(256) void phi_gemv_kernel(const double* __restrict_
       const int c = 8 * lane + e;
       w[e][q] = c < r ? W[(size_t)c * K + q] : 0.0;
     }
-  for (long long i = wave; i < n; i += waves) {
-    const double* pr = Phi + i * r;
-    double x[8];
+  // kGvRows rows per wave step: their loads are issued together (the pass is bound by bytes in
+  // flight per wave, not by arithmetic)
+  for (long long i0 = wave * kGvRows; i0 < n; i0 += waves * kGvRows) {
+    double x[kGvRows][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = 8 * lane + e;
-      x[e] = c < r ? pr[c] : 0.0;
+    for (int u = 0; u < kGvRows; ++u) {
+      const long long i = i0 + u;
+      const TP* pr = Phi + (i < n ? i : 0) * r;
+      if constexpr (sizeof(TP) == 4) {
+        if (vec4) {   // two 16-byte loads per lane (8 columns): the pass is load-instruction bound
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = 8 * lane + 4 * h;
+            const float4 v = (i < n && c < r) ? *reinterpret_cast<const float4*>(pr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            x[u][4 * h] = v.x; x[u][4 * h + 1] = v.y; x[u][4 * h + 2] = v.z; x[u][4 * h + 3] = v.w;
+          }
+          continue;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * lane + e;
+        x[u][e] = (i < n && c < r) ? (double)pr[c] : 0.0;
+      }
     }
-    double s[K];
 #pragma unroll
-    for (int q = 0; q < K; ++q) {
-      double v = 0.0;
+    for (int u = 0; u < kGvRows; ++u) {
+      const long long i = i0 + u;
+      double s[K];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v = fma(x[e], w[e][q], v);
-      s[q] = wave_sum(v);
-    }
-    if (lane < K) {
-      double o = s[0];
+      for (int q = 0; q < K; ++q) {
+        double v = 0.0;
 #pragma unroll
-      for (int q = 1; q < K; ++q)
-        if (lane == q) o = s[q];
-      Y[i * K + lane] = o;
+        for (int e = 0; e < 8; ++e) v = fma(x[u][e], w[e][q], v);
+        s[q] = wave_sum(v);
+      }
+      if (lane < K && i < n) {
+        double o = s[0];
+#pragma unroll
+        for (int q = 1; q < K; ++q)
+          if (lane == q) o = s[q];
+        Y[i * K + lane] = o;
+      }
     }
   }
 }
 
-void phi_gemv(uintptr_t Phi, uintptr_t W, long long n, int r, int k, uintptr_t Y, uintptr_t stream) {
+static void phi_gemv_any(const void* Phi, bool f32, uintptr_t W, long long n, int r, int k, uintptr_t Y,
+                         uintptr_t stream) {
   HFENS_REQUIRE(n >= 1 && r >= 1 && r <= 512 && k >= 1 && k <= kGvMaxK, "phi_gemv: r <= 512, 1 <= k <= 4");
   int dev = 0, ncu = 256;
   HFENS_CHECK(hipGetDevice(&dev));
   HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   long long blocks = (long long)ncu * 8;
-  const long long need = (n + 3) / 4;
+  const long long need = (n + 4 * kGvRows - 1) / (4 * kGvRows);
   if (blocks > need) blocks = need;
   hipStream_t st = as_stream(stream);
   auto go = [&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    hipLaunchKernelGGL(phi_gemv_kernel<K>, dim3((unsigned)blocks), dim3(256), 0, st, (const double*)Phi,
-                       (const double*)W, n, r, (double*)Y);
+    if (f32)
+      hipLaunchKernelGGL((phi_gemv_kernel<K, float>), dim3((unsigned)blocks), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)W, n, r, (double*)Y);
+    else
+      hipLaunchKernelGGL((phi_gemv_kernel<K, double>), dim3((unsigned)blocks), dim3(256), 0, st, (const double*)Phi,
+                         (const double*)W, n, r, (double*)Y);
     launch_check();
   };
   if (k == 1) go(std::integral_constant<int, 1>{});
   else if (k == 2) go(std::integral_constant<int, 2>{});
   else if (k == 3) go(std::integral_constant<int, 3>{});
   else go(std::integral_constant<int, 4>{});
+}
+
+void phi_gemv(uintptr_t Phi, uintptr_t W, long long n, int r, int k, uintptr_t Y, uintptr_t stream) {
+  phi_gemv_any((const void*)Phi, false, W, n, r, k, Y, stream);
+}
+
+// Φ stored as f32 (the IPM's skinny passes are HBM-bound: half the bytes), f64 arithmetic.
+void phi_gemv_f32(uintptr_t Phi, uintptr_t W, long long n, int r, int k, uintptr_t Y, uintptr_t stream) {
+  phi_gemv_any((const void*)Phi, true, W, n, r, k, Y, stream);
+}
+
+// out[c][q] = Σ_i Φ[i][c]·V[i][q] (Φᵀ V, V [n][k], k ≤ 4) with Φ in f32, f64 arithmetic: workgroup g
+// sums its row slab (thread t owns columns t and t + 256; 4 rows in flight; V rows are uniform loads)
+// into a partial [r][k] slot, and a second launch adds the G slots in slot order (deterministic).
+constexpr int kPtRows = 4;
+
+template <int K>
+__global__ __launch_bounds__(256) void phit_f32_kernel(const float* __restrict__ Phi, const double* __restrict__ V,
+                                                       long long n, int r, long long per, double* __restrict__ part) {
+  // thread t: columns 4·(t % 128) … +3 (one 16-byte load per row), row stream t / 128 (rows of the
+  // slab alternate between the two halves of the workgroup: waves 0–1 and 2–3, so each wave's V
+  // reads are uniform); kPtRows rows in flight per thread
+  const int t = threadIdx.x, cb = t & 127, rs = t >> 7;
+  const int c = 4 * cb;
+  const bool act = c < r;
+  const long long i0 = (long long)blockIdx.x * per, i1 = i0 + per < n ? i0 + per : n;
+  double acc[4][K];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int q = 0; q < K; ++q) acc[e][q] = 0.0;
+  long long i = i0 + rs;
+  for (; i + 2 * (kPtRows - 1) < i1; i += 2 * kPtRows) {
+    float4 x[kPtRows];
+    double v[kPtRows][K];
+#pragma unroll
+    for (int u = 0; u < kPtRows; ++u) {
+      x[u] = act ? *reinterpret_cast<const float4*>(Phi + (i + 2 * u) * r + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < K; ++q) v[u][q] = V[(i + 2 * u) * K + q];
+    }
+#pragma unroll
+    for (int u = 0; u < kPtRows; ++u)
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        acc[0][q] = fma((double)x[u].x, v[u][q], acc[0][q]);
+        acc[1][q] = fma((double)x[u].y, v[u][q], acc[1][q]);
+        acc[2][q] = fma((double)x[u].z, v[u][q], acc[2][q]);
+        acc[3][q] = fma((double)x[u].w, v[u][q], acc[3][q]);
+      }
+  }
+  for (; i < i1; i += 2) {
+    const float4 x = act ? *reinterpret_cast<const float4*>(Phi + i * r + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const double vq = V[i * K + q];
+      acc[0][q] = fma((double)x.x, vq, acc[0][q]);
+      acc[1][q] = fma((double)x.y, vq, acc[1][q]);
+      acc[2][q] = fma((double)x.z, vq, acc[2][q]);
+      acc[3][q] = fma((double)x.w, vq, acc[3][q]);
+    }
+  }
+  // row stream 1 hands its sums to stream 0 through LDS (fixed order: deterministic)
+  __shared__ double sh[128][4 * kGvMaxK];
+  if (rs == 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int q = 0; q < K; ++q) sh[cb][e * K + q] = acc[e][q];
+  __syncthreads();
+  if (rs == 0 && act) {
+    double* slot = part + (size_t)blockIdx.x * r * K;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (c + e < r) slot[(size_t)(c + e) * K + q] = acc[e][q] + sh[cb][e * K + q];
+  }
+}
+
+// one wave per output element: lanes take every 64th partial, then a wave sum (fixed order:
+// deterministic)
+__global__ __launch_bounds__(256) void phit_reduce_kernel(const double* __restrict__ part, int G, long long m,
+                                                          double* __restrict__ out) {
+  const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (e >= m) return;
+  double s = 0.0;
+  for (int g = lane; g < G; g += 64) s += part[(size_t)g * m + e];
+  s = wave_sum(s);
+  if (lane == 0) out[e] = s;
+}
+
+void phit_f32(uintptr_t Phi, uintptr_t V, long long n, int r, int k, uintptr_t part, long long part_len, uintptr_t out,
+              uintptr_t stream) {
+  HFENS_REQUIRE(n >= 1 && r >= 1 && r <= 512 && r % 4 == 0 && k >= 1 && k <= kGvMaxK && (Phi & 15) == 0,
+                "phit_f32: r <= 512, r % 4 == 0, 16-byte aligned Φ, 1 <= k <= 4");
+  const long long G = n < 1024 * 64 ? (n + 63) / 64 : 1024;
+  HFENS_REQUIRE(part_len >= G * r * k, "phit_f32: partial buffer too small");
+  const long long per = (n + G - 1) / G;
+  hipStream_t st = as_stream(stream);
+  auto go = [&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    hipLaunchKernelGGL(phit_f32_kernel<K>, dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi, (const double*)V,
+                       n, r, per, (double*)part);
+    launch_check();
+  };
+  if (k == 1) go(std::integral_constant<int, 1>{});
+  else if (k == 2) go(std::integral_constant<int, 2>{});
+  else if (k == 3) go(std::integral_constant<int, 3>{});
+  else go(std::integral_constant<int, 4>{});
+  const long long m = (long long)r * k;
+  hipLaunchKernelGGL(phit_reduce_kernel, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, st, (const double*)part,
+                     (int)G, m, (double*)out);
+  launch_check();
 }
 
 }  // namespace hfens

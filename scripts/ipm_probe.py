@@ -36,11 +36,16 @@ def main():
     d = torch.rand(n, device=dev, dtype=torch.float64)
     if only_ipm:
         c = torch.where(y > 0, 0.625, 2.5).to(torch.float64)
-        t0 = time.perf_counter()
-        a, rho, it = ipm_svc_dual(Phi, y, c)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        print(f"  ipm solve {1e3 * dt:.1f} ms, {it} iterations ({1e3 * dt / it:.2f} ms/iter), rho {rho:.4f}", flush=True)
+        # f64 Φ (skinny passes over f64) and Φ rounded to f32 (skinny passes over the f32 copy)
+        for tag, P in (("f64 map", Phi), ("f32-rounded map", Phi.to(torch.float32).to(torch.float64))):
+            ipm_svc_dual(P, y, c, max_iter=3)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            a, rho, it = ipm_svc_dual(P, y, c)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"  ipm solve [{tag}] {1e3 * dt:.1f} ms, {it} iterations ({1e3 * dt / it:.2f} ms/iter), "
+                  f"rho {rho:.6f}, sum(a) {float(a.sum()):.6f}", flush=True)
         return
     print(f"  weighted gram (split-K) {tm(lambda: _weighted_gram(Phi, d)):.2f} ms", flush=True)
     print(f"  weighted gram (one GEMM) {tm(lambda: Phi.T @ (d[:, None] * Phi)):.2f} ms", flush=True)

@@ -86,3 +86,22 @@ def test_phi_gemv_matches_torch(dev, n, r, k):
     Y = _phi_mv(Phi, W)
     want = Phi @ W
     assert float((Y - want).abs().max() / want.abs().max()) < 1e-13
+
+
+@pytest.mark.parametrize("n,r,k", [(1, 1, 1), (999, 17, 2), (100003, 428, 1), (70001, 512, 4), (65, 300, 3)])
+def test_f32_phi_passes_match_torch_f64(dev, n, r, k):
+    """The IPM's skinny passes over the f32 copy of Φ (phi_gemv_f32: Φ W; phit_f32: Φᵀ V, split-K
+    with an ordered partial sum) equal the f64 products of the same (f32-representable) Φ."""
+    from hfens.models.svc_lowrank import _phi_mv, _phit
+    g = torch.Generator(device=dev).manual_seed(n * 5 + r)
+    P32 = torch.randn(n, r, generator=g, device=dev, dtype=torch.float32)
+    Phi = P32.double()
+    W = torch.randn(r, k, generator=g, device=dev, dtype=torch.float64)
+    V = torch.randn(n, k, generator=g, device=dev, dtype=torch.float64)
+    Y = _phi_mv(Phi, W, P32)
+    want = Phi @ W
+    assert float((Y - want).abs().max() / want.abs().max()) < 1e-13
+    O = _phit(Phi, V, P32)
+    want = Phi.T @ V
+    assert float((O - want).abs().max() / want.abs().max()) < 1e-12
+    assert torch.equal(O, _phit(Phi, V, P32))              # deterministic
