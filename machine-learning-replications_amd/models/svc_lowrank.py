@@ -60,7 +60,10 @@ def nystrom_map(Z: torch.Tensor, idx: torch.Tensor, gamma: float):
     """(Φ [l, r], T [m, r]) with Φ = K(Z, L) T and T = U Λ^{-1/2} (dropped tiny eigenvalues)."""
     L = Z[idx]
     W = _rbf(L, L, gamma)
-    lam, U = torch.linalg.eigh(W)
+    # the m × m (m ≤ 1024) eigendecomposition on the host: the device solver took ≈ 350 ms of a 1M-row
+    # map's 384 ms (rocSOLVER syevd on one small matrix); LAPACK on the host takes tens of ms
+    lam, U = torch.linalg.eigh(W.cpu())
+    lam, U = lam.to(W.device), U.to(W.device)
     keep = lam > 1e-10 * lam.max()
     T = U[:, keep] / torch.sqrt(lam[keep])[None, :]
     return _rbf(Z, L, gamma) @ T, T
@@ -161,9 +164,15 @@ def _phi_mv(Phi: torch.Tensor, W: torch.Tensor, P32: torch.Tensor = None) -> tor
 def _bc(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
     """A 0-dim device scalar as a dense vector shaped like ``like``: torch runs vector ⊙ 0-dim-tensor
     ops through its strided broadcast kernel, ≈ 10× slower on 10⁶-long f64 vectors than the
-    vectorised same-shape kernel (measured: 63 vs 6 µs), so the IPM's scalar-times-vector updates
-    expand the scalar once instead."""
-    return t.reshape(1).expand(like.shape[0]).contiguous()
+    vectorised same-shape kernel (measured: 63 vs 6 µs; its expand-copy 193 µs), so the IPM's
+    scalar-times-vector updates fill a dense copy natively (ops/csrc/lowrank.hip fill_dev)."""
+    n = like.shape[0]
+    if like.is_cuda and ops.has_ext():
+        src = t.to(torch.float64).reshape(1).contiguous()
+        out = torch.empty(n, dtype=torch.float64, device=like.device)
+        ops.ext().fill_dev(out.data_ptr(), n, src.data_ptr(), ops.stream_ptr(like.device))
+        return out if t.dtype == torch.float64 else out.to(t.dtype)
+    return t.reshape(1).expand(n).contiguous()
 
 
 def _max_step(v, dv):
