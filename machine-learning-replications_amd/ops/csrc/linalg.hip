@@ -16,6 +16,8 @@
 //  chol_solve: x = sc ∘ (L Lᵀ)⁻¹ (sc ∘ b) for k ≤ 4 right-hand sides, one workgroup: blocked
 //              forward / backward substitution, 64-row diagonal blocks solved by wave 0 (readlane
 //              chain), the off-diagonal updates by all threads.
+#include <type_traits>
+
 #include "common.h"
 
 namespace hfens {
@@ -157,12 +159,17 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
 // x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.  Each
 // 64-row step stages its diagonal block of L in LDS (the substitution chain of wave 0 then waits on
 // LDS, not on a global load per column) and the solved block of x in LDS for the row updates.
+// K = right-hand sides (compile time: the per-lane vectors stay in registers).  The diagonal blocks'
+// pivots are inverted in parallel first (the substitution chain then multiplies), and the
+// off-diagonal updates issue their row loads 16 at a time (one load round per 16 columns instead
+// of one per column: the runtime-bound loop had serialised 64 L2 round trips per block).
+template <int K>
 __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __restrict__ L, const double* __restrict__ sc,
-                                                                int r, int k, double* __restrict__ B) {
+                                                                int r, double* __restrict__ B) {
   __shared__ double Db[kChNB][kChNB + 1];
   __shared__ double Xb[kChNB][kChMaxK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < r * k; e += kChThreads) B[e] *= sc[e / k];
+  for (int e = tid; e < r * K; e += kChThreads) B[e] *= sc[e / K];
   __syncthreads();
   // forward: L y = b
   for (int k0 = 0; k0 < r; k0 += kChNB) {
@@ -173,32 +180,44 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
     }
     __syncthreads();
     if (wave == 0) {
-      double y[kChMaxK];
-      for (int q = 0; q < kChMaxK; ++q) y[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
+      double y[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) y[q] = lane < nb ? B[(size_t)(k0 + lane) * K + q] : 0.0;
+      const double dinv = lane < nb ? 1.0 / Db[lane][lane] : 0.0;
       for (int j = 0; j < nb; ++j) {
-        const double ljj = Db[j][j];
+        const double dj = ch_readlane(dinv, j);
         const double lij = (lane > j && lane < nb) ? Db[lane][j] : 0.0;
-        for (int q = 0; q < k; ++q) {
-          if (lane == j) y[q] /= ljj;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          if (lane == j) y[q] *= dj;
           const double yj = ch_readlane(y[q], j);
           if (lane > j) y[q] -= lij * yj;
         }
       }
       if (lane < nb)
-        for (int q = 0; q < k; ++q) {
-          B[(size_t)(k0 + lane) * k + q] = y[q];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          B[(size_t)(k0 + lane) * K + q] = y[q];
           Xb[lane][q] = y[q];
         }
     }
     __syncthreads();
     for (int i = k0 + nb + tid; i < r; i += kChThreads) {
       const double* li = L + (size_t)i * r + k0;
-      double acc[kChMaxK] = {0.0, 0.0, 0.0, 0.0};
-      for (int b = 0; b < nb; ++b) {
-        const double l = li[b];
-        for (int q = 0; q < k; ++q) acc[q] = fma(l, Xb[b][q], acc[q]);
+      double acc[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) acc[q] = 0.0;
+      for (int b0 = 0; b0 < nb; b0 += 16) {
+        double l[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) l[u] = b0 + u < nb ? li[b0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], b0 + u < nb ? Xb[b0 + u][q] : 0.0, acc[q]);
       }
-      for (int q = 0; q < k; ++q) B[(size_t)i * k + q] -= acc[q];
+#pragma unroll
+      for (int q = 0; q < K; ++q) B[(size_t)i * K + q] -= acc[q];
     }
     __syncthreads();
   }
@@ -212,37 +231,49 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
     }
     __syncthreads();
     if (wave == 0) {
-      double x[kChMaxK];
-      for (int q = 0; q < kChMaxK; ++q) x[q] = (lane < nb && q < k) ? B[(size_t)(k0 + lane) * k + q] : 0.0;
+      double x[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) x[q] = lane < nb ? B[(size_t)(k0 + lane) * K + q] : 0.0;
+      const double dinv = lane < nb ? 1.0 / Db[lane][lane] : 0.0;
       for (int j = nb - 1; j >= 0; --j) {
-        const double ljj = Db[j][j];
+        const double dj = ch_readlane(dinv, j);
         // Lᵀ[lane][j] = L[j][lane] for lane < j
         const double lji = lane < j ? Db[j][lane] : 0.0;
-        for (int q = 0; q < k; ++q) {
-          if (lane == j) x[q] /= ljj;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          if (lane == j) x[q] *= dj;
           const double xj = ch_readlane(x[q], j);
           if (lane < j) x[q] -= lji * xj;
         }
       }
       if (lane < nb)
-        for (int q = 0; q < k; ++q) {
-          B[(size_t)(k0 + lane) * k + q] = x[q];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          B[(size_t)(k0 + lane) * K + q] = x[q];
           Xb[lane][q] = x[q];
         }
     }
     __syncthreads();
     // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j  (lanes read consecutive i: coalesced)
     for (int i = tid; i < k0; i += kChThreads) {
-      double acc[kChMaxK] = {0.0, 0.0, 0.0, 0.0};
-      for (int b = 0; b < nb; ++b) {
-        const double l = L[(size_t)(k0 + b) * r + i];
-        for (int q = 0; q < k; ++q) acc[q] = fma(l, Xb[b][q], acc[q]);
+      double acc[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) acc[q] = 0.0;
+      for (int b0 = 0; b0 < nb; b0 += 16) {
+        double l[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) l[u] = b0 + u < nb ? L[(size_t)(k0 + b0 + u) * r + i] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], b0 + u < nb ? Xb[b0 + u][q] : 0.0, acc[q]);
       }
-      for (int q = 0; q < k; ++q) B[(size_t)i * k + q] -= acc[q];
+#pragma unroll
+      for (int q = 0; q < K; ++q) B[(size_t)i * K + q] -= acc[q];
     }
     __syncthreads();
   }
-  for (int e = tid; e < r * k; e += kChThreads) B[e] *= sc[e / k];
+  for (int e = tid; e < r * K; e += kChThreads) B[e] *= sc[e / K];
 }
 
 void chol_spd(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uintptr_t stream) {
@@ -259,9 +290,16 @@ void chol_spd(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uin
 
 void chol_solve(uintptr_t L, uintptr_t sc, int r, int k, uintptr_t B, uintptr_t stream) {
   HFENS_REQUIRE(r >= 1 && r <= 1024 && k >= 1 && k <= kChMaxK, "chol_solve: 1 <= r <= 1024, 1 <= k <= 4");
-  hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(kChThreads), 0, as_stream(stream), (const double*)L,
-                     (const double*)sc, r, k, (double*)B);
-  launch_check();
+  auto go = [&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    hipLaunchKernelGGL(chol_solve_kernel<K>, dim3(1), dim3(kChThreads), 0, as_stream(stream), (const double*)L,
+                       (const double*)sc, r, (double*)B);
+    launch_check();
+  };
+  if (k == 1) go(std::integral_constant<int, 1>{});
+  else if (k == 2) go(std::integral_constant<int, 2>{});
+  else if (k == 3) go(std::integral_constant<int, 3>{});
+  else go(std::integral_constant<int, 4>{});
 }
 
 }  // namespace hfens
