@@ -296,6 +296,7 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     if not 1 <= D <= 5:
         raise ValueError("max_depth must be in [1, 5]")
     NN = 2 ** (D + 1) - 1
+    all_rows = masks is None and binned is None   # every model sees every row of the bin map's own matrix
     if masks is None:
         masks = torch.ones(B, n, dtype=torch.bool, device=dev)
     w = masks.to(device=dev, dtype=torch.float32).contiguous()
@@ -344,7 +345,8 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
             st.row_off = pdist.row_offset(n, group, dev)[0]
     if D == 1 and SKLEARN_TIES and subsample == 1.0 and all(
             isinstance(m.random_state, (int, np.integer)) for m in models):
-        st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group)
+        st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group,
+                                       nb_host=bm.nb_host if (all_rows and group is None) else None)
     hmark("gbc_ranks")
     if X.is_cuda:
         _run_device(st, group)
@@ -365,26 +367,29 @@ SKLEARN_TIES = os.environ.get("HFENS_GBDT_SKLEARN_TIES", "1") != "0"
 RAND_R_MAX = 2147483647
 
 
-def sklearn_stump_ranks(models, bins: torch.Tensor, masks: torch.Tensor, T: int, group=None) -> torch.Tensor:
+def sklearn_stump_ranks(models, bins: torch.Tensor, masks: torch.Tensor, T: int, group=None,
+                        nb_host=None) -> torch.Tensor:
     """[T, B, F] int32: rank of each feature in sklearn's root visit order for every tree of every
     model.  Constant features (one occupied bin over the model's rows, across all ranks) are
-    set aside exactly as sklearn does and never visited (rank F)."""
+    set aside exactly as sklearn does and never visited (rank F).  ``nb_host``: the bin counts,
+    given when every model sees every row of a single-process fit — every bin of a fitted bin map
+    is occupied, so the constant features are those with one bin and no device pass is needed."""
     F, n = bins.shape
     B = len(models)
-    big = torch.iinfo(torch.int32).max
-    bmin = torch.full((B, F), big, dtype=torch.int32, device=bins.device)
-    bmax = torch.full((B, F), -1, dtype=torch.int32, device=bins.device)
-    bi = bins.to(torch.int32)
-    for b in range(B):
-        sel = masks[b] > 0
-        if bool(sel.any()):
-            bmin[b] = bi[:, sel].amin(1)
-            bmax[b] = bi[:, sel].amax(1)
-    if group is not None:
-        import torch.distributed as dist
-        dist.all_reduce(bmin, op=dist.ReduceOp.MIN, group=group)
-        dist.all_reduce(bmax, op=dist.ReduceOp.MAX, group=group)
-    const = (bmax <= bmin).to(torch.uint8).cpu().numpy()
+    if nb_host is not None:
+        const = np.repeat((np.asarray(nb_host) <= 1).astype(np.uint8)[None, :], B, axis=0)
+    else:
+        big = torch.iinfo(torch.int32).max
+        bi = bins.to(torch.int32)
+        # masked min / max per model without boolean indexing (no nonzero sync, no row gather);
+        # a model with no rows keeps (big, −1): constant, as before
+        bmin = torch.stack([torch.where(masks[b][None, :] > 0, bi, big).amin(1) for b in range(B)])
+        bmax = torch.stack([torch.where(masks[b][None, :] > 0, bi, -1).amax(1) for b in range(B)])
+        if group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(bmin, op=dist.ReduceOp.MIN, group=group)
+            dist.all_reduce(bmax, op=dist.ReduceOp.MAX, group=group)
+        const = (bmax <= bmin).to(torch.uint8).cpu().numpy()
     out = np.empty((T, B, F), dtype=np.int32)
     for b, m in enumerate(models):
         # GradientBoostingClassifier._rng = RandomState(random_state); each tree's splitter draws
