@@ -97,7 +97,9 @@ class LassoCV(Estimator):
                                              float(self.tol))) for p in range(P)]
         return torch.stack(out).to(Gs.device)
 
-    def fit(self, X, y, group=None):
+    def fit(self, X, y, group=None, overlap=None):
+        """``overlap``: optional host callable run while the device solves the CV path (between its
+        launch and the first read of its result) — host work hidden under the path's GPU time."""
         from ..utils.guards import check_finite
         X = check_finite(as_tensor(X), "LassoCV.fit X")
         y = check_finite(as_tensor(y, device=X.device), "LassoCV.fit y")
@@ -136,6 +138,8 @@ class LassoCV(Estimator):
             grid = torch.as_tensor(np.sort(np.asarray(self.alphas, dtype=np.float64))[::-1].copy())
         grid = grid.to(dev)
         coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+        if overlap is not None:
+            overlap()
         # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
         inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
         # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
@@ -170,8 +174,13 @@ class SelectFromModel(Estimator):
         self.threshold = threshold
         self.max_features = max_features
 
-    def fit(self, X, y, group=None):
-        self.estimator_ = self.estimator.fit(X, y, group=group)
+    def fit(self, X, y, group=None, overlap=None):
+        if overlap is not None and isinstance(self.estimator, LassoCV):
+            self.estimator_ = self.estimator.fit(X, y, group=group, overlap=overlap)
+        else:
+            self.estimator_ = self.estimator.fit(X, y, group=group)
+            if overlap is not None:
+                overlap()
         scores = self.estimator_.coef_.abs().cpu().numpy()
         F = scores.size
         mask = np.ones(F, dtype=bool)

@@ -116,6 +116,7 @@ class _Prob:
     held: Optional[np.ndarray] = None       # Platt: held-out grouped positions
     held_rows: Optional[np.ndarray] = None  # … and their rows of Z
     const: float = 0.0
+    colmap: Optional[np.ndarray] = None     # Platt sub-problem: column map into its fit's final Gram (planned ahead)
 
     @property
     def l(self) -> int:
@@ -155,6 +156,28 @@ def _expand(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
             probs.append(_Prob(fit_id, k, rows, n1, C1, C0, gamma, held, gp[b:e]))
     probs.append(_Prob(fit_id, -1, grouped, n0, C0, C1, gamma))
     return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
+
+
+def plan_svc_problems(svc, y_fits) -> Optional[list]:
+    """The label-only half of :func:`launch_svc_batch`, computable before the fit's inputs exist:
+    every fit's libsvm problem expansion (γ filled in at launch) and, for each Platt sub-problem,
+    the column map into its fit's final-problem Gram (:func:`_column_map`).  ``None`` when the labels
+    are not 0/1 (the launch then reads them from the device as usual)."""
+    pre = []
+    for f, yh in enumerate(y_fits):
+        y_np = np.asarray(yh, dtype=np.float64).reshape(-1)
+        if not np.isin(np.unique(y_np), (0.0, 1.0)).all():
+            return None
+        probs, mt = _expand(f, y_np, None, _class_weights_host(svc, y_np), svc)
+        final = probs[-1]
+        if final.l <= _MAP_MAX:
+            inv = np.full(int(final.rows.max()) + 1, -1, dtype=np.int64)
+            inv[final.rows] = np.arange(final.l)
+            for p in probs[:-1]:
+                if p.rows is not None and p.l <= _MAP_MAX:
+                    p.colmap = _column_map(final, p, inv)
+        pre.append((y_np, probs, mt))
+    return pre
 
 
 def _class_weights_host(svc, y_np: np.ndarray) -> np.ndarray:
@@ -439,10 +462,12 @@ def _gram_parents(live) -> List[int]:
     return out
 
 
-def _column_map(par: _Prob, sub: _Prob) -> np.ndarray:
-    """int32 [par.l]: the sub-problem's index of each parent column (−1: not in the sub-problem)."""
-    inv = np.full(int(par.rows.max()) + 1, -1, dtype=np.int64)
-    inv[par.rows] = np.arange(par.l)
+def _column_map(par: _Prob, sub: _Prob, inv: Optional[np.ndarray] = None) -> np.ndarray:
+    """int32 [par.l]: the sub-problem's index of each parent column (−1: not in the sub-problem).
+    ``inv``: the parent's row → column inverse, when already built (shared by its sub-problems)."""
+    if inv is None:
+        inv = np.full(int(par.rows.max()) + 1, -1, dtype=np.int64)
+        inv[par.rows] = np.arange(par.l)
     cols = inv[sub.rows]
     if (cols < 0).any():
         raise AssertionError("Platt sub-problem rows must be rows of the final problem")
@@ -510,7 +535,8 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
             m = -1
             if q >= 0:
                 m = moff
-                maps.append(_column_map(live[q], p))
+                cm = getattr(p, "colmap", None)
+                maps.append(cm if cm is not None and cm.shape[0] == lphys else _column_map(live[q], p))
                 moff += lphys
             cp[k] = (sm[k]["koff"], aoffs[k], m, p.l, sm[k]["ld"], p.npos, S, lphys, 0, p.Cp, p.Cn)
         cdev = _dev_struct(cp, device)
@@ -759,7 +785,7 @@ def use_lowrank(sizes) -> bool:
 
 
 def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None,
-                     y_host=None) -> dict:
+                     y_host=None, plan=None) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
@@ -806,7 +832,10 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     if any(need_var):
         parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
     pre = None
-    if y_host is not None and all(np.isin(np.unique(yh), (0.0, 1.0)).all() for yh in y_host):
+    if plan is not None and len(plan) == len(svcs) and all(int(p[0].shape[0]) == int(y.numel()) for p, y in zip(plan, ys)):
+        pre = plan   # expanded ahead of time (plan_svc_problems), overlapped with earlier device work
+        hmark("svc_expand_planned")
+    elif y_host is not None and all(np.isin(np.unique(yh), (0.0, 1.0)).all() for yh in y_host):
         # host labels: expand the problems now (γ filled in below), overlapping the device work
         pre = []
         for f, (svc, yh) in enumerate(zip(svcs, y_host)):

@@ -167,7 +167,27 @@ def _index_to(a, device) -> torch.Tensor:
     return t.pin_memory().to(device, non_blocking=True)
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None):
+def plan_stacking(clf, y_np: np.ndarray) -> dict:
+    """The label-only bookkeeping of :func:`fit_stacking` — StratifiedKFold test folds, the fold row
+    sets and every SVC fit's libsvm problem expansion with its Platt column maps — computed from the
+    development labels alone, so the caller can run it on the host while earlier device work (the
+    LassoCV path) is in flight, off the SVC launch's critical path."""
+    from .smo import plan_svc_problems
+    y_np = np.asarray(y_np, dtype=np.float64).reshape(-1)
+    folds_np = stratified_kfold_test_folds(y_np, N_FOLDS)
+    n = y_np.shape[0]
+    rows_host = [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)]
+    svc_pre = {}
+    for i, (_, est) in enumerate(clf.estimators):
+        if _kind(est) == "svc":
+            pre = plan_svc_problems(est.steps[-1][1], [y_np[r] for r in rows_host])
+            if pre is not None:
+                svc_pre[i] = pre
+    return dict(y_np=y_np, folds_np=folds_np, rows_host=rows_host, svc_pre=svc_pre)
+
+
+def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
+                          svc_pre=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -201,7 +221,8 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                 hmark("svc_inputs")
                 if group is None:
                     yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
-                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh))
+                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh,
+                                                           plan=(svc_pre or {}).get(i)))
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
                 hmark("svc_launched")
@@ -236,19 +257,25 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     return [out[i] for i in range(len(kinds))]
 
 
-def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None):
+def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
+                 plan=None):
     timer = timer or StageTimer(enabled=False)
     dev = X.device
     n = X.shape[0]
     y_np = None
-    if group is None:
+    svc_pre = None
+    if plan is not None and group is None and svc_group is None and int(plan["y_np"].shape[0]) == n:
+        # folds, row sets and SVC problem expansions computed ahead from the same labels (plan_stacking)
+        y_np, folds_np, svc_pre = plan["y_np"], plan["folds_np"], plan["svc_pre"]
+    elif group is None:
         y_np = y.cpu().numpy().astype(np.float64)
         folds_np = stratified_kfold_test_folds(y_np, N_FOLDS)
     else:
         from ..parallel import dist as pdist
         folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
     masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
-    rows_host = [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)]
+    rows_host = (plan["rows_host"] if svc_pre is not None
+                 else [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)])
     # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
     # gathers / scatters then need no host synchronisation
     test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
@@ -263,7 +290,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np)
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream

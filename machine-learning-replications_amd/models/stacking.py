@@ -80,9 +80,9 @@ class StackingClassifier(Estimator):
     def named_estimators_(self):
         return {n: e for (n, _), e in zip(self.estimators, self.estimators_)}
 
-    def fit(self, X, y, timer=None, group=None, svc_group=None):
+    def fit(self, X, y, timer=None, group=None, svc_group=None, plan=None):
         from .stack_trainer import fit_stacking
-        fit_stacking(self, as_tensor(X), as_tensor(y), timer=timer, group=group, svc_group=svc_group)
+        fit_stacking(self, as_tensor(X), as_tensor(y), timer=timer, group=group, svc_group=svc_group, plan=plan)
         return self
 
     def transform(self, X) -> torch.Tensor:

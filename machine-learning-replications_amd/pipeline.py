@@ -34,6 +34,7 @@ from .utils.timing import StageTimer
 DP_POLICY = os.environ.get("HFENS_DP_POLICY", "auto")
 TASK_MAX_ROWS = int(os.environ.get("HFENS_TASK_MAX_ROWS", str(1 << 18)))
 AUX_STREAM = os.environ.get("HFENS_AUX_STREAM", "1") != "0"   # held-out imputation on a side stream
+PLAN_AHEAD = os.environ.get("HFENS_PLAN_AHEAD", "1") != "0"   # stacking bookkeeping under the LassoCV path
 
 
 def choose_policy(n_total: int) -> str:
@@ -71,6 +72,22 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
     if group is not None:
         from .parallel import dist as pdist
         task = choose_policy(pdist.all_reduce_int(X_dev.shape[0], group)) == "task"
+    clf = build_estimators(cfg)
+    # the stacking fit's label-only bookkeeping (folds, SVC problem expansions, Platt column maps)
+    # is computed on the host while the LassoCV path runs on the device (stack_trainer.plan_stacking);
+    # the labels come over in a non-blocking copy issued now, long finished by then
+    plan_box = {}
+    overlap = None
+    if group is None and dev.type == "cuda" and PLAN_AHEAD:
+        y_pin = torch.empty(y_dev.shape[0], dtype=torch.float64, pin_memory=True)
+        y_pin.copy_(y_dev, non_blocking=True)
+        y_ev = torch.cuda.Event()
+        y_ev.record()
+
+        def overlap():
+            from .models.stack_trainer import plan_stacking
+            y_ev.synchronize()
+            plan_box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
     with timer.stage("impute"):
         if group is None:
             imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(X_dev)
@@ -90,13 +107,13 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
     fit_group = None if task else group
     with timer.stage("select"):
-        sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group)
+        sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=overlap)
         mask = sfm.get_support()
         mt = torch.as_tensor(mask, device=dev)
         X_dev_optm = X_dev[:, mt]
         fn_new = [n for n, m in zip(names, mask) if m]
-    clf = build_estimators(cfg)
-    clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None)
+    clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None,
+            plan=plan_box.get("plan"))
     if aux is not None:
         # join the side stream while the imputer and X_sel are alive (their blocks are not reused
         # by the main stream before this point)

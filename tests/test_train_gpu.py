@@ -462,3 +462,22 @@ def test_smo_shared_gram_matches_own_grams(dev, monkeypatch, rows):
         assert torch.equal(a.support_, b.support_)
         assert a._probA.item() == pytest.approx(b._probA.item(), rel=1e-9)
         assert a._probB.item() == pytest.approx(b._probB.item(), rel=1e-9, abs=1e-12)
+
+
+def test_develop_plan_ahead_identical(dev, monkeypatch):
+    """The stacking bookkeeping computed under the LassoCV path (folds, SVC problem expansions,
+    Platt column maps: pipeline.PLAN_AHEAD) gives the same fit as computing it in line."""
+    from hfens import pipeline
+    from hfens.io.synth import make_hf_cohort
+    Xd, yd, names = make_hf_cohort(3000, 40, seed=77, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(1000, 40, seed=78, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for ahead in (False, True):
+        monkeypatch.setattr(pipeline, "PLAN_AHEAD", ahead)
+        r = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+        out[ahead] = r
+    assert np.array_equal(out[False].selected, out[True].selected)
+    assert torch.equal(out[False].proba_sel, out[True].proba_sel)
+    m0, m1 = out[False].model, out[True].model
+    assert torch.equal(m0.oof_meta_, m1.oof_meta_)
