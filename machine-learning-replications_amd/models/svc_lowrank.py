@@ -92,6 +92,8 @@ NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
 F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
+IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
+IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 
 
 def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
@@ -201,9 +203,9 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
             P32 = p32
     y = y.to(dt)
     c = c.to(dt)
-    a = 0.5 * c
-    nu = torch.ones(l, dtype=dt, device=Phi.device)
-    mu = torch.ones(l, dtype=dt, device=Phi.device)
+    a = IPM_A0 * c
+    nu = torch.full((l,), IPM_NU0, dtype=dt, device=Phi.device)
+    mu = torch.full((l,), IPM_NU0, dtype=dt, device=Phi.device)
     b = torch.zeros((), dtype=dt, device=Phi.device)
     eye = torch.eye(r, dtype=dt, device=Phi.device)
     csum = float(c.sum())
