@@ -1,12 +1,12 @@
 #!/bin/bash
 # PMC counters for the GBDT stage kernel (1M x 40, 100 stumps): one pass per counter group.
 set -o pipefail
-D=gpurun_out/pmc_gbdt
+D=${PMC_DIR:-gpurun_out/pmc_gbdt}
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 pass() {  # pass TAG COUNTERS...
   local tag=$1; shift
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $D/$tag -o p --output-format csv -- python3 bench.py --config gbdt --steps 1 --warmup 0 > $D/$tag.log 2>&1 || { echo "$tag failed"; tail -5 $D/$tag.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $D/$tag -o p --output-format csv -- python3 bench.py ${BENCH_ARGS:---config gbdt --steps 1 --warmup 0} > $D/$tag.log 2>&1 || { echo "$tag failed"; tail -5 $D/$tag.log; exit 1; }
   f=$(find $D/$tag -name "*counter_collection.csv" | head -1)
   python3 scripts/pmc_summary.py $f $D/$tag.csv "${PMC_MATCH:-}" && rm -rf $D/$tag && cat $D/$tag.csv | cut -c1-400
 }
