@@ -37,6 +37,7 @@ Accuracy guard (``profiles/r2_svc_lowrank.md``, ``tests/test_svc_lowrank.py``):
 from __future__ import annotations
 
 import os
+import threading
 
 import numpy as np
 import torch
@@ -93,6 +94,7 @@ DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (s
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
 F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
 IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
+IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "2"))   # concurrent Platt-CV solves per fit
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 
 
@@ -106,7 +108,7 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
         from .. import runtime
         from .smo import _num_cus
         plen = _wsyrk_part_len(l, r, _num_cus(Phi.device))
-        part = runtime.workspace(Phi.device, "wsyrk_part", plen, torch.float64)
+        part = runtime.workspace(Phi.device, _ws_name("wsyrk_part"), plen, torch.float64)
         S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
         ops.ext().wsyrk_f64(Phi.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
                             ops.stream_ptr(Phi.device))
@@ -132,7 +134,7 @@ def _phit(Phi: torch.Tensor, V: torch.Tensor, P32: torch.Tensor = None) -> torch
         from .. import runtime
         k = V.shape[1]
         G = (l + 63) // 64 if l < 1024 * 64 else 1024
-        part = runtime.workspace(Phi.device, "phit_part", G * r * k, torch.float64)
+        part = runtime.workspace(Phi.device, _ws_name("phit_part"), G * r * k, torch.float64)
         Vc = V.to(torch.float64).contiguous()
         out = torch.empty(r, k, dtype=torch.float64, device=Phi.device)
         ops.ext().phit_f32(P32.data_ptr(), Vc.data_ptr(), l, r, k, part.data_ptr(), G * r * k, out.data_ptr(),
@@ -161,6 +163,13 @@ def _phi_mv(Phi: torch.Tensor, W: torch.Tensor, P32: torch.Tensor = None) -> tor
            ops.stream_ptr(Phi.device))
         return Y
     return Phi @ W
+
+
+_TL = threading.local()   # per-thread workspace tag: concurrent solves must not share a scratch buffer
+
+
+def _ws_name(base: str) -> str:
+    return base + getattr(_TL, "tag", "")
 
 
 def _bc(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
@@ -410,18 +419,44 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
         dec_cv = np.zeros(l)
         lab = np.where(np.arange(l) < n0, 1.0, -1.0)          # grouped-position labels
         iters = []
-        for p in probs:
-            if p.fold < 0:
-                continue
-            if p.rows is None:
-                dec_cv[p.held] = p.const
-                continue
+
+        def solve_cv(p):
             rows = torch.as_tensor(p.rows, device=dev)
             a, rho, it = ipm_svc_dual(Phi[rows], yint[rows], cvec[rows])
-            iters.append(it)
             wv = _phit(Phi[rows], (yint[rows] * a)[:, None])[:, 0]
             held = torch.as_tensor(p.held_rows, device=dev)
-            dec_cv[p.held] = (Phi[held] @ wv - rho).cpu().numpy()
+            return (Phi[held] @ wv - rho).cpu().numpy(), it
+
+        cv = [p for p in probs if p.fold >= 0 and p.rows is not None]
+        for p in probs:
+            if p.fold >= 0 and p.rows is None:
+                dec_cv[p.held] = p.const
+        nthr = min(IPM_THREADS, len(cv)) if Z.is_cuda else 1
+        if nthr > 1:
+            # the Platt CV solves are independent: two host threads, each on its own stream and
+            # scratch buffers, so one solve's latency-bound steps (the single-workgroup factor and
+            # triangular solves, the per-iteration convergence read) overlap the other's
+            # bandwidth-bound passes; the same kernels on the same inputs: identical results
+            from concurrent.futures import ThreadPoolExecutor
+            from .. import runtime
+            main = torch.cuda.current_stream(dev)
+
+            def worker(jp):
+                j, p = jp
+                _TL.tag = f"#t{j % nthr}"
+                with torch.cuda.device(dev):
+                    st = runtime.stream(dev, f"ipm{j % nthr}")
+                    st.wait_stream(main)
+                    with torch.cuda.stream(st):
+                        return solve_cv(p)
+
+            with ThreadPoolExecutor(nthr) as ex:
+                outs = list(ex.map(worker, enumerate(cv)))
+        else:
+            outs = [solve_cv(p) for p in cv]
+        for p, (dec, it) in zip(cv, outs):
+            dec_cv[p.held] = dec
+            iters.append(it)
         A, B = _sigmoid_train_host(dec_cv, lab) if svc.probability else (0.0, 0.0)
         a, rho, it = ipm_svc_dual(Phi, yint, cvec)
         iters.append(it)

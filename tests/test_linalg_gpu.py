@@ -105,3 +105,24 @@ def test_f32_phi_passes_match_torch_f64(dev, n, r, k):
     want = Phi.T @ V
     assert float((O - want).abs().max() / want.abs().max()) < 1e-12
     assert torch.equal(O, _phit(Phi, V, P32))              # deterministic
+
+
+def test_lowrank_svc_threaded_platt_cv_identical(dev, monkeypatch):
+    """The Platt-CV interior-point solves on two host threads / streams (svc_lowrank.IPM_THREADS)
+    give the same fitted SVC as one at a time: the same kernels on the same inputs."""
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import svc_lowrank
+    from hfens.models.svc import SVC
+    X, y, _ = make_hf_cohort(6000, 17, seed=12, nan_frac=0.0)
+    Z = torch.as_tensor(X, device=dev)
+    Z = (Z - Z.mean(0)) / Z.std(0).clamp(min=1e-12)
+    yt = torch.as_tensor(y, device=dev)
+    out = {}
+    for nt in (1, 2):
+        monkeypatch.setattr(svc_lowrank, "IPM_THREADS", nt)
+        s = SVC(kernel="rbf", probability=True, class_weight="balanced", random_state=0)
+        svc_lowrank.fit_svc_lowrank_batch([s], [Z], [yt], n_landmarks=128)
+        out[nt] = s
+    a, b = out[1], out[2]
+    assert a._hs == b._hs                                   # (intercept, Platt A, Platt B)
+    assert torch.equal(a.dual_coef_, b.dual_coef_)
