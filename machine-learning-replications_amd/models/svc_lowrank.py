@@ -94,7 +94,7 @@ DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (s
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
 F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
 IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
-IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "2"))   # concurrent Platt-CV solves per fit
+IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "3"))   # concurrent Platt-CV solves per fit (+ the final)
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 
 
@@ -450,18 +450,38 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
                     with torch.cuda.stream(st):
                         return solve_cv(p)
 
-            with ThreadPoolExecutor(nthr) as ex:
+            def final_worker():
+                # the final problem (the largest) is independent of the CV solves: it runs on its
+                # own thread and stream beside them, submitted first
+                _TL.tag = "#final"
+                with torch.cuda.device(dev):
+                    st = runtime.stream(dev, "ipm_final")
+                    st.wait_stream(main)
+                    with torch.cuda.stream(st):
+                        a_f, rho_f, it_f = ipm_svc_dual(Phi, yint, cvec)
+                        wv_f = _phit(Phi, (yint * a_f)[:, None])[:, 0]
+                        return rho_f, it_f, (T @ wv_f).cpu()
+
+            with ThreadPoolExecutor(nthr + 1) as ex:
+                fin = ex.submit(final_worker)
                 outs = list(ex.map(worker, enumerate(cv)))
+                rho, it_final, beta_h = fin.result()
         else:
             outs = [solve_cv(p) for p in cv]
+            rho = None
         for p, (dec, it) in zip(cv, outs):
             dec_cv[p.held] = dec
             iters.append(it)
         A, B = _sigmoid_train_host(dec_cv, lab) if svc.probability else (0.0, 0.0)
-        a, rho, it = ipm_svc_dual(Phi, yint, cvec)
-        iters.append(it)
-        wv = _phit(Phi, (yint * a)[:, None])[:, 0]
-        beta = T @ wv                                          # coefficients on the landmarks
+        if rho is None:
+            a, rho, it = ipm_svc_dual(Phi, yint, cvec)
+            iters.append(it)
+            wv = _phit(Phi, (yint * a)[:, None])[:, 0]
+            beta = T @ wv                                      # coefficients on the landmarks
+        else:
+            it = it_final
+            iters.append(it)
+            beta = beta_h.to(dev)
         n_sv0 = int((~cls1).sum())
         svc.set_fitted(support=idx, support_vectors=Zd[idx], n_support=[n_sv0, k - n_sv0],
                        dual_coef_libsvm=beta, rho=rho, probA=A, probB=B, gamma=gamma,
