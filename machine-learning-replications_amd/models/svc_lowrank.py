@@ -95,6 +95,7 @@ CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-fin
 F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
 IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
 IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "3"))   # concurrent Platt-CV solves per fit (+ the final)
+FIT_THREADS = int(os.environ.get("HFENS_IPM_FITS", "1"))      # fits solved at a time (2: no gain measured, GPU saturated)
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 
 
@@ -385,7 +386,8 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
     from .smo import _expand, _sigmoid_train_host
     from ..utils.guards import check_binary, check_finite
     m = int(n_landmarks or N_LANDMARKS)
-    for f, (svc, Z, y) in enumerate(zip(svcs, Zs, ys)):
+
+    def fit_one(f, svc, Z, y, slot):
         check_finite(Z, f"SVC.fit X (fit {f})")
         check_binary(y, f"SVC.fit y (fit {f})")
         dev = Z.device
@@ -443,9 +445,9 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
 
             def worker(jp):
                 j, p = jp
-                _TL.tag = f"#t{j % nthr}"
+                _TL.tag = f"#s{slot}t{j % nthr}"
                 with torch.cuda.device(dev):
-                    st = runtime.stream(dev, f"ipm{j % nthr}")
+                    st = runtime.stream(dev, f"ipm{slot}_{j % nthr}")
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
                         return solve_cv(p)
@@ -453,9 +455,9 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
             def final_worker():
                 # the final problem (the largest) is independent of the CV solves: it runs on its
                 # own thread and stream beside them, submitted first
-                _TL.tag = "#final"
+                _TL.tag = f"#s{slot}final"
                 with torch.cuda.device(dev):
-                    st = runtime.stream(dev, "ipm_final")
+                    st = runtime.stream(dev, f"ipm_final{slot}")
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
                         a_f, rho_f, it_f = ipm_svc_dual(Phi, yint, cvec)
@@ -490,6 +492,43 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
         svc.n_iter_ = int(it)
         svc.solver_ = "nystrom-ipm"
         LAST_INFO.update(solver="nystrom-ipm", landmarks=k, rank=int(T.shape[1]), ipm_iters=iters)
+
+    cuda = bool(Zs) and Zs[0].is_cuda
+    nfit = min(FIT_THREADS, len(svcs)) if cuda else 1
+    if nfit > 1:
+        # fits are independent too: FIT_THREADS of them at a time, each on its own stream with its
+        # own slot of per-thread streams and scratch buffers (a slot is held for a whole fit), so
+        # one fit's tail (its final solve alone) overlaps the next fit's solves
+        import queue
+        from concurrent.futures import ThreadPoolExecutor
+        from .. import runtime
+        dev = Zs[0].device
+        caller = torch.cuda.current_stream(dev)
+        slots = queue.Queue()
+        for q in range(nfit):
+            slots.put(q)
+
+        def run(f):
+            slot = slots.get()
+            try:
+                with torch.cuda.device(dev):
+                    fs = runtime.stream(dev, f"ipm_fit{slot}")
+                    fs.wait_stream(caller)
+                    with torch.cuda.stream(fs):
+                        fit_one(f, svcs[f], Zs[f], ys[f], slot)
+                    ev = torch.cuda.Event()
+                    ev.record(fs)
+                    return ev
+            finally:
+                slots.put(slot)
+
+        with ThreadPoolExecutor(nfit) as ex:
+            evs = list(ex.map(run, range(len(svcs))))
+        for ev in evs:
+            caller.wait_event(ev)
+    else:
+        for f, (svc, Z, y) in enumerate(zip(svcs, Zs, ys)):
+            fit_one(f, svc, Z, y, 0)
     return svcs
 
 

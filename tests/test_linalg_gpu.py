@@ -108,8 +108,9 @@ def test_f32_phi_passes_match_torch_f64(dev, n, r, k):
 
 
 def test_lowrank_svc_threaded_platt_cv_identical(dev, monkeypatch):
-    """The Platt-CV interior-point solves on two host threads / streams (svc_lowrank.IPM_THREADS)
-    give the same fitted SVC as one at a time: the same kernels on the same inputs."""
+    """The Platt-CV interior-point solves on host threads / streams (svc_lowrank.IPM_THREADS), the
+    final solve beside them, and two fits at a time (FIT_THREADS) give the same fitted SVCs as one
+    solve at a time: the same kernels on the same inputs."""
     from hfens.io.synth import make_hf_cohort
     from hfens.models import svc_lowrank
     from hfens.models.svc import SVC
@@ -118,11 +119,13 @@ def test_lowrank_svc_threaded_platt_cv_identical(dev, monkeypatch):
     Z = (Z - Z.mean(0)) / Z.std(0).clamp(min=1e-12)
     yt = torch.as_tensor(y, device=dev)
     out = {}
-    for nt in (1, 2):
+    for nt, nf in ((1, 1), (2, 1), (3, 2)):
         monkeypatch.setattr(svc_lowrank, "IPM_THREADS", nt)
-        s = SVC(kernel="rbf", probability=True, class_weight="balanced", random_state=0)
-        svc_lowrank.fit_svc_lowrank_batch([s], [Z], [yt], n_landmarks=128)
-        out[nt] = s
-    a, b = out[1], out[2]
-    assert a._hs == b._hs                                   # (intercept, Platt A, Platt B)
-    assert torch.equal(a.dual_coef_, b.dual_coef_)
+        monkeypatch.setattr(svc_lowrank, "FIT_THREADS", nf)
+        ss = [SVC(kernel="rbf", probability=True, class_weight="balanced", random_state=r) for r in range(3)]
+        svc_lowrank.fit_svc_lowrank_batch(ss, [Z, Z[:5000], Z[1000:]], [yt, yt[:5000], yt[1000:]], n_landmarks=128)
+        out[(nt, nf)] = ss
+    for key in ((2, 1), (3, 2)):
+        for a, b in zip(out[(1, 1)], out[key]):
+            assert a._hs == b._hs, key                      # (intercept, Platt A, Platt B)
+            assert torch.equal(a.dual_coef_, b.dual_coef_), key
