@@ -125,7 +125,14 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   hipStream_t st = as_stream(stream);
   HFENS_CHECK(hipMemsetAsync((void*)best, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned long long), st));
   const int rb = (nr + 255) / 256;
+  // enough splits for ≥ 2048 workgroups, and donor ranges of ≤ 16k rows per workgroup: a
+  // workgroup then runs for milliseconds, not the whole search, so kernels of other streams (the
+  // LassoCV path beside the held-out imputation at 10⁶ rows) get CUs as workgroups retire instead
+  // of waiting for the donor search to drain.  The (distance, index) atomicMin merge makes the
+  // result independent of the split count.
   int splits = 2048 / rb;
+  const int by_range = (nd + 16383) / 16384;
+  if (splits < by_range) splits = by_range;
   const int max_splits = (nd + kKnnTile - 1) / kKnnTile;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
