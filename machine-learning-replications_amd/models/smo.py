@@ -381,7 +381,7 @@ _WS_STATE_BYTES = 80     # sizeof(WsState)
 
 # Device solver: "exact" = libsvm's pair sequence (smo_batch on a stored Gram), "ws" = working-set
 # decomposition with the RBF recomputed on the MFMA (ws_*: O(n) memory, no n² Gram).  Measured on
-# the bench's 36-problem batches (scripts/ws_diag.py, profiles/r1_svm_solvers.md): 10k rows exact
+# the bench's 36-problem batches (scripts/probes/ws_diag.py, profiles/r1_svm_solvers.md): 10k rows exact
 # 67 ms vs ws 71 ms, 20k rows exact 272 ms vs ws 821 ms — the one-pair-per-iteration exact solver
 # stays the default ("auto"); "ws" is the low-memory path.
 SOLVER = os.environ.get("HFENS_SVM_SOLVER", "auto")
@@ -406,7 +406,7 @@ COOP = os.environ.get("HFENS_SMO_COOP", "1") != "0"
 COOP_MIN_SLICE = int(os.environ.get("HFENS_SMO_COOP_SLICE", "384"))
 COOP_RESERVE_CUS = int(os.environ.get("HFENS_SMO_COOP_RESERVE", "60"))   # CUs left to concurrent GBC/LR
 # more members: exchange skew outweighs the split.  Measured on the bench (36 problems, max l 10k,
-# L2 row prefetch on, scripts/gpu_coop_sweep.sh): W=2 89.4, 3 85.0, 4 81.8-85.3, 5 79.8-80.9,
+# L2 row prefetch on, scripts/probes/gpu_coop_sweep.sh): W=2 89.4, 3 85.0, 4 81.8-85.3, 5 79.8-80.9,
 # 6 84.9, 7 125.6 ms/fit (7 leaves 4 CUs to GBC/LR)
 _COOP_MAX_W = int(os.environ.get("HFENS_SMO_COOP_MAXW", "5"))
 _COOP_GRANULES = 2 * 16 * 10          # exchange slots per problem: 2 × kMaxMembers × kGran (u64)

@@ -3,7 +3,7 @@ import os
 import sys
 import time
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models import binning  # noqa: E402
 dev = torch.device("cuda")

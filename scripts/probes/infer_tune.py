@@ -4,7 +4,7 @@ import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 rows = sys.argv[1] if len(sys.argv) > 1 else "100000000"
 for w in ("8", "12", "16"):
     env = dict(os.environ, HFENS_STACK_WAVES=w)

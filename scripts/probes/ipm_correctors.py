@@ -7,7 +7,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models import svc_lowrank  # noqa: E402
 from hfens.models.smo import _expand  # noqa: E402

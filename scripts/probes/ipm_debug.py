@@ -6,7 +6,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 os.environ.setdefault("HFENS_IPM_DEBUG", "1")
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models import svc_lowrank  # noqa: E402

@@ -6,7 +6,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.models.svc_lowrank import _weighted_gram, ipm_svc_dual, nystrom_map  # noqa: E402
 
 

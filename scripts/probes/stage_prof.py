@@ -3,7 +3,7 @@ import os
 import sys
 import numpy as np
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 os.environ.setdefault("HFENS_GBDT_STAGE_PROF", "50")
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models import hist_gbdt  # noqa: E402
