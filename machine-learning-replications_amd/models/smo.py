@@ -376,22 +376,36 @@ def _dev_struct(arr: np.ndarray, device) -> torch.Tensor:
 
 _WS_DT = np.dtype([("zoff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("npos", "<i4"), ("Cp", "<f8"),
                    ("Cn", "<f8"), ("ngl2e", "<f4"), ("pad", "<i4")])
-_WS_Q = 128              # working-set size compiled into svm_ws.hip
-_WS_STATE_BYTES = 80     # sizeof(WsState)
+_WS_STATE_BYTES = 88     # sizeof(WsState) in svm_ws.hip
 
-# Device solver: "exact" = libsvm's pair sequence (smo_batch on a stored Gram), "ws" = working-set
-# decomposition with the RBF recomputed on the MFMA (ws_*: O(n) memory, no n² Gram).  Measured on
-# the bench's 36-problem batches (scripts/probes/ws_diag.py, profiles/r1_svm_solvers.md): 10k rows exact
-# 67 ms vs ws 71 ms, 20k rows exact 272 ms vs ws 821 ms — the one-pair-per-iteration exact solver
-# stays the default ("auto"); "ws" is the low-memory path.
+
+WS_MAX_F = 48            # features the working-set kernel's register/LDS budget admits
+
+
+def ws_q(F: int) -> int:
+    """Working-set size of svm_ws.hip for F features (one slot per thread; z_B must fit LDS)."""
+    return 1024 if F <= 24 else 512
+
+
+def _ws_ks(F: int) -> int:
+    ks = (F + 1) // 2
+    return 4 if ks <= 4 else 9 if ks <= 9 else 12 if ks <= 12 else 24
+
+# Device solver: "exact" = libsvm's pair sequence on a stored Gram (svm.hip / svm_coop.hip), "ws" =
+# working-set decomposition (svm_ws.hip: q = 1024 slots solved inside one CU with the RBF recomputed
+# in registers, half of each working set reused, MFMA gradient updates; O(n) memory).  On the
+# bench's 10k problem the exact sequence is ~7.6k pairs at ~7.7 µs (cross-CU hand-offs), the
+# working-set solver ~35 rounds of ~250 in-CU pairs (scripts/ws_sim.py).  "auto": ws from
+# WS_MIN_POINTS points on (the exact sequence stays for small problems, where it is cheap and
+# libsvm-identical), exact when F exceeds the working-set kernel's register budget.
 SOLVER = os.environ.get("HFENS_SVM_SOLVER", "auto")
-WS_MIN_POINTS = int(os.environ.get("HFENS_SVM_WS_MIN", str(1 << 30)))
+WS_MIN_POINTS = int(os.environ.get("HFENS_SVM_WS_MIN", "4096"))
 
 
-def _pick_solver(max_l: int) -> str:
+def _pick_solver(max_l: int, F: int = 17) -> str:
     if SOLVER in ("exact", "ws"):
         return SOLVER
-    return "ws" if max_l >= WS_MIN_POINTS else "exact"
+    return "ws" if (max_l >= WS_MIN_POINTS and F <= WS_MAX_F) else "exact"
 
 
 # Cooperative exact SMO (ops/csrc/svm_coop.hip): every problem's points are split over W
@@ -567,10 +581,10 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
 
 
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
-WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", str(8 * _WS_Q)))
+WS_INNER_PER_Q = int(os.environ.get("HFENS_SVM_WS_INNER", "4"))        # inner pair cap = this × q
 
 
-def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=16):
+def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None):
     P = len(live)
     arr = np.zeros(P, _WS_DT)
     for k, p in enumerate(live):
@@ -578,18 +592,19 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
                   -p.gamma * 1.4426950408889634, 0)
     max_l = int(arr["l"].max())
     n = aoffs[-1]
+    Q = ws_q(F)
+    Fp2 = 2 * _ws_ks(F)
     pdev = _dev_struct(arr, device)
     zn = torch.empty(n, dtype=torch.float32, device=device)
     alpha = torch.empty(n, dtype=torch.float64, device=device)
     G = torch.empty(n, dtype=torch.float64, device=device)
     states = torch.zeros(P * _WS_STATE_BYTES // 4, dtype=torch.int32, device=device)
-    ks = (F + 1) // 2
-    Fp = 2 * (4 if ks <= 4 else 9 if ks <= 9 else 12 if ks <= 12 else 16 if ks <= 16 else 32)
-    wsz = torch.zeros(P * Fp * _WS_Q, dtype=torch.float32, device=device)
-    wsn = torch.zeros(P * _WS_Q, dtype=torch.float32, device=device)
-    wdc = torch.zeros(P * _WS_Q, dtype=torch.float32, device=device)
-    max_outer = 50_000 if max_iter_cap is None else int(max_iter_cap)
-    max_inner = WS_MAX_INNER
+    wsz = torch.zeros(P * Fp2 * Q, dtype=torch.float32, device=device)
+    wsn = torch.zeros(P * Q, dtype=torch.float32, device=device)
+    wdc = torch.zeros(P * Q, dtype=torch.float32, device=device)
+    wsprev = torch.zeros(P * (Q // 2), dtype=torch.int32, device=device)
+    max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
+    max_inner = WS_INNER_PER_Q * Q
     keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
     hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
     gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)
@@ -597,11 +612,15 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
               states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
     done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
     outer = 0
+    # ~35 outer rounds on the bench's 10k problem (scripts/ws_sim.py): one host check after the
+    # first 24, then every 8 (finished problems return at once from the launches in between)
+    chunk = steps_per_check or 24
     while outer < max_outer:
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
-                   states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), keys.data_ptr(), n,
-                   hist.data_ptr(), gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC, steps_per_check, s)
-        outer += steps_per_check
+                   states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
+                   keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC, chunk, s)
+        outer += chunk
+        chunk = steps_per_check or 8
         if bool((done_view != 0).all()):
             break
     rho = torch.empty(P, dtype=torch.float64, device=device)
@@ -610,10 +629,12 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     gap = torch.empty(P, dtype=torch.float64, device=device)
     E.ws_finalize(pdev.data_ptr(), P, states.data_ptr(), alpha.data_ptr(), G.data_ptr(), rho.data_ptr(),
                   iters.data_ptr(), inner.data_ptr(), gap.data_ptr(), s)
-    cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 8:20].cpu().contiguous().view(torch.int64).numpy()
+    cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 10:22].cpu().contiguous().view(torch.int64).numpy()
     LAST_WS_STATS.update(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
                          cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
-                         cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5])
+                         cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5], q=Q)
+    LAST_SMO_INFO.clear()
+    LAST_SMO_INFO.update(problems=P, max_l=max_l, solver="ws", q=Q, outer_max=int(iters.max().item()))
     return alpha, rho, iters, None
 
 
@@ -679,7 +700,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         aoffs.append(aoffs[-1] + p.l)
     aoffs_start = aoffs[:-1]
     max_l = max(p.l for p in live)
-    solver = _pick_solver(max_l)
+    solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
     if group is None:
         alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)

@@ -1,28 +1,34 @@
-// Working-set decomposition SMO for batches of C-SVC duals (SURVEY.md §2.3 K4-train; the reference
-// fits libsvm through sklearn SVC, train_ensemble_public.py:43-48).
+// Working-set decomposition SMO for batches of C-SVC duals (SURVEY.md §2.3 K4/K5; the reference
+// fits libsvm through sklearn SVC, train_ensemble_public.py:43-48, 61).
 //
-// libsvm's SMO (svm.hip: smo_kernel) moves ONE pair per iteration and every iteration is a chain of
-// two block reductions and two dependent Gram-row reads: on a 10k-point problem that is ~9 µs of
-// latency per pair and ~7k pairs.  This solver keeps libsvm's dual, WSS3 pair rule inside the
-// working set and libsvm's global stopping rule (m(α) − M(α) < eps, evaluated in f64 over ALL
-// points), but restructures the work for the MI355X:
+// libsvm's SMO moves ONE pair per iteration, and every iteration is a chain of two global
+// reductions and two dependent kernel-row reads.  Spread over CUs (svm_coop.hip) each reduction is
+// a cross-workgroup hand-off, so a pair costs ~7.7 µs and the bench's 10k-point problem (~7.6k
+// pairs) ~56 ms.  This solver keeps libsvm's dual, its WSS3 pair rule INSIDE a large working set
+// and libsvm's global stopping rule (m(α) − M(α) < eps over ALL points, f64), and moves the
+// sequential part into one CU:
 //
 //   ws_select_solve (one 1024-thread workgroup per problem)
-//     1. global gap m − M (f64), convergence test;
-//     2. working set B = the q/2 most violating points of I_up and of I_low (two-level 11-bit
-//        radix histograms in LDS + index-ordered tie compaction: deterministic);
-//     3. K_BB (q×q) from the rows' features into LDS;
-//     4. inner SMO on B by one wave — libsvm's WSS3 pair rule and clipping on the local gradient,
-//        K rows from LDS, α/G in registers, wave-level reductions only (no barriers, no HBM);
+//     1. global gap m − M (f64) from the maxima the gradient kernel published; convergence test;
+//     2. working set B (q = 1024, or 512 for F > 24): the q/4 most violating points of I_up and
+//        of I_low (two-level 11-bit radix histograms in LDS, index-ordered tie compaction:
+//        deterministic), plus the previous round's new picks that were not picked again
+//        (ThunderSVM-style half reuse: on the bench's 10k problem 35 outer rounds instead of
+//        ~280 without reuse, scripts/ws_sim.py);
+//     3. the features of B into LDS; every thread owns ONE slot of B, its features in registers;
+//     4. inner SMO on B: libsvm's WSS3 pair rule and clipping on the local gradient; each kernel
+//        row K(x_i, ·) is recomputed in registers (F fmas + one exp2 per slot, the same f32
+//        expression as the gradient kernel's MFMA, bit for bit), so a pair is two block
+//        reductions (DPP/permlane wave max + one barrier each) and no memory traffic beyond LDS;
 //     5. publishes the changed coefficients y_i·Δα_i and their feature rows (MFMA layout).
 //   ws_gupdate (grid = row tiles × problems)
-//     G_t += y_t Σ_{i∈B} y_i Δα_i K(x_t, x_i) for every t: an RBF "GEMM + exp + GEMV" on the
-//     f32-input MFMA (rows of the problem = B operand, changed working-set rows = A operand),
-//     i.e. the kernel matrix is recomputed instead of stored — O(n·F) memory instead of O(n²).
+//     G_t += y_t Σ_{c changed} y_c Δα_c K(x_t, x_c) for every t: an RBF "GEMM + exp + GEMV" on the
+//     f32-input MFMA in 256-coefficient chunks — the kernel matrix is recomputed, never stored:
+//     O(n·F) memory instead of the exact solver's O(n²) Gram.
 //
-// Results satisfy the same KKT tolerance as libsvm but follow a different pair sequence, so α
-// agrees with libsvm to O(eps) rather than bit-for-bit (the exact-sequence solver stays in
-// svm.hip for small problems and for parity tests).
+// Results meet libsvm's KKT tolerance but follow a different pair sequence, so α agrees with
+// libsvm to O(eps), not bit for bit (the exact-sequence solvers stay in svm.hip / svm_coop.hip for
+// small problems and parity tests).  Deterministic: no order-dependent atomics.
 #include "common.h"
 
 namespace hfens {
@@ -43,24 +49,19 @@ struct WsState {
   long long inner;  // pair updates
   double gap;       // last global m − M
   int nc;           // changed working-set entries published for ws_gupdate (0 ⇒ nothing to do)
-  int nws;
+  int nws;          // size of the last working set
+  int nprev;        // new picks of the last round (kept in wsprev for the next working set)
+  int pad;
   long long cyc_select, cyc_build, cyc_inner;   // s_memtime phase totals (diagnostics)
   long long cyc_p0, cyc_p1, cyc_p2;             // selection sub-phases: gap pass, level-1, level-2
 };
+static_assert(sizeof(WsState) == 88, "WsState layout is mirrored in models/smo.py");
 
-constexpr int kWsQ = 128;          // working-set size (q/2 from each side)
-constexpr int kWsHalf = kWsQ / 2;
 constexpr int kWsThreads = 1024;
 constexpr int kWsWaves = kWsThreads / 64;
+constexpr int kWsChunk = 256;      // changed coefficients staged per LDS pass of ws_gupdate
 constexpr double kWsTau = 1e-12;
 constexpr double kWsInf = 1.0e300;
-
-// order-preserving f32 → u32 (larger float ⇒ larger key; every finite float maps to ≥ 0x00800000,
-// so 0 can mean "not a member")
-__device__ __forceinline__ unsigned ws_key(double v) {
-  const unsigned u = __float_as_uint((float)v);
-  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
-}
 
 __device__ __forceinline__ double block_max_f64(double v, double* sh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -126,48 +127,6 @@ __device__ __forceinline__ void ws_find_bin(const int* hist, int k_up, int k_low
   }
 }
 
-// libsvm's two-variable update (Solver::Solve, "update alpha[i] and alpha[j]").
-__device__ __forceinline__ void ws_pair_update(double& ai, double& aj, int yi, int yj, double Ci, double Cj,
-                                               double Gi, double Gj, double Kij) {
-#pragma clang fp contract(off)
-  const double Qij = (double)(yi * yj) * Kij;
-  if (yi != yj) {
-    double quad = 2.0 + 2.0 * Qij;
-    if (quad <= 0) quad = kWsTau;
-    const double delta = (-Gi - Gj) / quad;
-    const double diff = ai - aj;
-    ai += delta;
-    aj += delta;
-    if (diff > 0) {
-      if (aj < 0) { aj = 0; ai = diff; }
-    } else {
-      if (ai < 0) { ai = 0; aj = -diff; }
-    }
-    if (diff > Ci - Cj) {
-      if (ai > Ci) { ai = Ci; aj = Ci - diff; }
-    } else {
-      if (aj > Cj) { aj = Cj; ai = Cj + diff; }
-    }
-  } else {
-    double quad = 2.0 - 2.0 * Qij;
-    if (quad <= 0) quad = kWsTau;
-    const double delta = (Gi - Gj) / quad;
-    const double sum = ai + aj;
-    ai -= delta;
-    aj += delta;
-    if (sum > Ci) {
-      if (ai > Ci) { ai = Ci; aj = sum - Ci; }
-    } else {
-      if (aj < 0) { aj = 0; ai = sum; }
-    }
-    if (sum > Cj) {
-      if (aj > Cj) { aj = Cj; ai = sum - Cj; }
-    } else {
-      if (ai < 0) { ai = 0; aj = sum; }
-    }
-  }
-}
-
 // Wave-level helpers for the selector: lanes below this one, and an exclusive prefix over the
 // 16 waves of per-wave totals (one barrier).
 __device__ __forceinline__ unsigned long long lanes_below() {
@@ -213,6 +172,8 @@ struct WsAux {
   unsigned long long* gkey;    // [P][2] order-preserving keys of max(−yG, I_up), max(yG, I_low)
 };
 
+__device__ __forceinline__ unsigned ws_key(double v) { return f32_okey((float)v); }
+
 // One point per thread (valid ⇔ t < l); wave-level only (every lane of the wave must call it).
 __device__ __forceinline__ void ws_publish_keys(const WsProb& P, int b, int t, bool valid, double a, double g,
                                                 const WsAux& X) {
@@ -244,7 +205,7 @@ __global__ __launch_bounds__(256) void ws_init_kernel(const WsProb* __restrict__
   const WsProb P = probs[b];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x * blockDim.x >= P.l) return;   // whole workgroup past the end
-  if (blockIdx.x == 0 && threadIdx.x == 0) states[b] = WsState{0, 0, 0, 0.0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (blockIdx.x == 0 && threadIdx.x == 0) states[b] = WsState{0, 0, 0, 0.0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool valid = t < P.l;
   if (valid) {
     const float* z = zcat + (P.zoff + t) * F;
@@ -257,31 +218,51 @@ __global__ __launch_bounds__(256) void ws_init_kernel(const WsProb* __restrict__
   ws_publish_keys(P, b, t, valid, 0.0, -1.0, X);
 }
 
-// M = points per lane.  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L its points
-// w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots give
-// index-ordered ranks.
-template <int M>
+// LDS carve of ws_select_solve (dynamic region only, every block a multiple of 16 bytes):
+//   [small]  256 ints: scan scratch (16), bin info (8), reduction slots (4 × 2 parities × 16 u32)
+//   [A]      selection: hist [2][2048] int + membership bitmap [1024] u32; then z_B [q][FP] f32
+//   [snB]    γ'·‖z‖² of B [q]      [widx] point index of each slot [q]
+//   [mirror] g, α, K(x_i,·) of every slot, 2 parities each: [3][2][q] f32
+__host__ __device__ constexpr size_t ws_lds_bytes(int Q, int FP) {
+  return 256 * 4 + ((size_t)Q * FP * 4 > 20480 ? (size_t)Q * FP * 4 : 20480) + (size_t)Q * 4 * 2 +
+         (size_t)6 * Q * 4;
+}
+
+// M = points per lane (selection).  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L
+// its points w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots
+// give index-ordered ranks.  FP = features padded to a multiple of 4; Q = working-set size (one
+// slot per thread).  FP: F rounded up to 4 (Q = 1024) or to 8 (Q = 512).
+template <int M, int FP, int Q>
 __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
     const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
-    float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc, int Fp, double eps,
-    int max_outer, int max_inner, double inner_frac, WsAux X) {
+    float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc, int Fp2,
+    int* __restrict__ wsprev, double eps, int max_outer, int max_inner, double inner_frac, WsAux X) {
+  static_assert(Q <= kWsThreads && (Q & (Q - 1)) == 0, "one slot per thread, power of two");
+  static_assert(FP % 4 == 0, "z rows are read as float4");
+  constexpr unsigned kIdx = Q - 1;   // slot bits packed under the selection keys
   const int b = blockIdx.x;
   WsState* S = states + b;
   if (S->done) return;
   const WsProb P = probs[b];
+  const int nprev = S->nprev;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l = P.l;
-  const int ldz = F | 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
-  int* hist = reinterpret_cast<int*>(ws_lds);                          // [2][2048]
-  float* KB = reinterpret_cast<float*>(hist + 4096);                   // [q][q+1]
-  float* zB = KB + kWsQ * (kWsQ + 1);                                  // [q][F|1]
-  float* znB = zB + kWsQ * ldz;                                        // [q]
-  int* widx = reinterpret_cast<int*>(znB + kWsQ);                      // [q]
-  __shared__ int shi[kWsWaves];
-  __shared__ int binfo[8];
+  int* shi = reinterpret_cast<int*>(ws_lds);                     // [16]
+  int* binfo = shi + 16;                                         // [8]
+  unsigned* red = reinterpret_cast<unsigned*>(binfo + 8);        // [4][2][16]
+  unsigned char* regA = ws_lds + 256 * 4;
+  int* hist = reinterpret_cast<int*>(regA);                      // [2][2048]
+  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);       // [1024]: points picked this round
+  float* zB = reinterpret_cast<float*>(regA);                    // [Q][FP] (after the selection)
+  const size_t szA = (size_t)Q * FP * 4 > 20480 ? (size_t)Q * FP * 4 : 20480;
+  float* snB = reinterpret_cast<float*>(regA + szA);             // [Q]
+  int* widx = reinterpret_cast<int*>(snB + Q);                   // [Q]
+  float* gl = reinterpret_cast<float*>(widx + Q);                // [2][Q]
+  float* al = gl + 2 * Q;                                        // [2][Q]
+  float* kil = al + 2 * Q;                                       // [2][Q]
   const int t0 = wave * 64 * M + lane;
 
   const double* Gp = G_all + P.aoff;
@@ -292,10 +273,9 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
   const double Gmax = gku ? f64_from_okey(gku) : -kWsInf;
   const double Gmax2 = gkl ? f64_from_okey(gkl) : -kWsInf;
   const double gap = Gmax + Gmax2;
-  // keys of this lane's points (coalesced: t = wave·64M + m·64 + lane) + member counts
+  // keys of this lane's points + member counts; all loads issued before any use
   unsigned ku[M], kl[M];
   int nu = 0, nl = 0;
-  // all loads issued before any use (one memory latency, not M of them)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int t = t0 + 64 * m;
@@ -307,7 +287,7 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     nu += __popcll(__ballot(ku[m] != 0u));
     nl += __popcll(__ballot(kl[m] != 0u));
   }
-  for (int i = tid; i < 4096; i += kWsThreads) hist[i] = 0;
+  for (int i = tid; i < 4096 + 1024; i += kWsThreads) hist[i] = 0;   // hist + bitmap
   if (tid < 8) binfo[tid] = 0;
   int n_up;
   wave_base(nu | (nl << 16), shi, &n_up);
@@ -325,7 +305,7 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     hist_add(hist, kl[m] != 0u, 2048 + (int)(kl[m] >> 21));
   }
   __syncthreads();
-  const int k_up = min(kWsHalf, n_up), k_low = min(kWsHalf, n_low);
+  const int k_up = min(Q / 4, n_up), k_low = min(Q / 4, n_low);
   const long long c0a = __builtin_amdgcn_s_memtime();
   ws_find_bin(hist, k_up, k_low, shi, binfo);
   __syncthreads();
@@ -345,14 +325,13 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
   const long long c0c = __builtin_amdgcn_s_memtime();
   const unsigned Tu = (bu1 << 11) | (unsigned)binfo[4], Tl = (bl1 << 11) | (unsigned)binfo[6];
   const int need_u = k_up - au1 - binfo[5], need_l = k_low - al1 - binfo[7];
-  // ---- pass 3: index-ordered compaction (up list, then low list without the up picks)
+  // ---- index-ordered compaction of the new picks (up list, then low list without the up picks)
   unsigned selm = 0u;
   int base = 0;
 #pragma unroll
   for (int side = 0; side < 2; ++side) {
     const unsigned T = side ? Tl : Tu;
     const int need = side ? need_l : need_u;
-    // ranks of the boundary-prefix ties, in index order
     int wt = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -380,117 +359,137 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     for (int m = 0; m < M; ++m) {
       const bool take = (pick >> m) & 1u;
       const unsigned long long tb = __ballot(take);
-      if (take) widx[pos + __popcll(tb & lanes_below())] = t0 + 64 * m;
+      if (take) {
+        const int t = t0 + 64 * m;
+        widx[pos + __popcll(tb & lanes_below())] = t;
+        atomicOr(&bm[t >> 5], 1u << (t & 31));
+      }
       pos += __popcll(tb);
     }
     selm |= pick;
     base += stot;
   }
+  const int nnew = base;
   __syncthreads();
+  // ---- the previous round's new picks that were not picked again (index-ordered by their old slot)
+  {
+    const int pv = tid < nprev ? wsprev[(size_t)b * (Q / 2) + tid] : -1;
+    const bool keep = pv >= 0 && !((bm[pv >> 5] >> (pv & 31)) & 1u);
+    const unsigned long long kb = __ballot(keep);
+    int ktot;
+    const int kpos = nnew + wave_base(__popcll(kb), shi, &ktot) + __popcll(kb & lanes_below());
+    if (keep) widx[kpos] = pv;
+    __syncthreads();   // every old entry was read before the new picks overwrite the list
+    for (int w = tid; w < nnew; w += kWsThreads) wsprev[(size_t)b * (Q / 2) + w] = widx[w];
+    base = nnew + ktot;
+  }
   const int nws = base;
   const long long c1 = __builtin_amdgcn_s_memtime();
-  // ---- gather features of B and build K_BB in LDS (f32-input MFMA, one 32×32 tile per wave)
-  for (int e = tid; e < nws * F; e += kWsThreads) {
-    const int w = e / F, c = e - w * F;
-    zB[w * ldz + c] = zcat[(P.zoff + widx[w]) * F + c];
+  // ---- features of B into LDS (zero-padded to FP: the padded terms of the dot are exact no-ops)
+  for (int e = tid; e < nws * FP; e += kWsThreads) {
+    const int w = e / FP, c = e - w * FP;
+    zB[e] = c < F ? zcat[(P.zoff + widx[w]) * F + c] : 0.f;
   }
-  for (int w = tid; w < nws; w += kWsThreads) znB[w] = zn_all[P.aoff + widx[w]];
+  for (int w = tid; w < nws; w += kWsThreads) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
   __syncthreads();
-  {
-    const int r32 = lane & 31, hi = lane >> 5;
-    const int tr = wave >> 2, tc = wave & 3;   // 4 × 4 tiles of the 128 × 128 block
-    if (tr * 32 < nws && tc * 32 < nws) {
-      f32x16 acc = {0.f};
-      const int ra = tr * 32 + r32, cb = tc * 32 + r32;
-      for (int k0 = 0; k0 < F; k0 += 2) {
-        const int k = k0 + hi;
-        const float av = (k < F && ra < nws) ? zB[ra * ldz + k] : 0.f;
-        const float bv = (k < F && cb < nws) ? zB[cb * ldz + k] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-      }
-      // acc reg q ↔ row tr·32 + (q&3) + 8(q>>2) + 4·hi, column tc·32 + r32
-      const int c = tc * 32 + r32;
-      const float znc = c < nws ? znB[c] : 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int r = tr * 32 + (q & 3) + 8 * (q >> 2) + 4 * hi;
-        if (r < nws && c < nws) {
-          const float d2 = fmaxf(znB[r] + znc - 2.f * acc[q], 0.f);
-          KB[r * (kWsQ + 1) + c] = r == c ? 1.f : __builtin_amdgcn_exp2f(P.ngl2e * d2);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (tid >= 64) return;
   const long long c2 = __builtin_amdgcn_s_memtime();
-  // ---- inner SMO on B: one wave, lane owns slots w = lane and lane + 64, local α/G in f32.
-  // Pair selection uses u32 keys (order-preserving f32 with the slot in the low 7 bits) reduced
-  // on DPP/permlane; libsvm's clipped two-variable step in f32.  The global state stays f64: the
-  // published change is α_new − α_old with exact bound values (0 or C) kept exact.
-  float a[2], g[2], Cw[2], ys[2];
-  double a0[2];
-  int tw[2];
-  bool val[2];
+  // ---- inner SMO on B: thread s owns slot s (f32 local state, features in registers)
+  const int s = tid;
+  const bool valid = s < nws;
+  const int t = valid ? widx[s] : 0;
+  const bool pos = t < P.npos;
+  const float y = pos ? 1.f : -1.f;
+  const float Cw = (float)(pos ? P.Cp : P.Cn);
+  const double a0 = valid ? ap[t] : 0.0;
+  float a = (float)a0;
+  float g = valid ? (float)Gp[t] : 0.f;
+  float zr[FP];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int w = lane + 64 * s;
-    val[s] = w < nws;
-    tw[s] = val[s] ? widx[w] : 0;
-    const bool pos = tw[s] < P.npos;
-    ys[s] = pos ? 1.f : -1.f;
-    a0[s] = val[s] ? ap[tw[s]] : 0.0;
-    a[s] = (float)a0[s];
-    g[s] = val[s] ? (float)Gp[tw[s]] : 0.f;
-    Cw[s] = (float)(pos ? P.Cp : P.Cn);
+  for (int k = 0; k < FP; k += 4) {
+    const f32x4 v = valid ? *reinterpret_cast<const f32x4*>(&zB[s * FP + k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    zr[k] = v[0]; zr[k + 1] = v[1]; zr[k + 2] = v[2]; zr[k + 3] = v[3];
   }
+  const float sn_own = valid ? snB[s] : 0.f;
+  const float k2c = -2.f * P.ngl2e;
+  const float Cpf = (float)P.Cp, Cnf = (float)P.Cn;
+  // K(x_r, x_s) for this thread's slot s: the gradient kernel's expression (MFMA = k-ordered fma
+  // chain from 0), so the inner solver and ws_gupdate see the same f32 kernel values
+  auto krow = [&](int r) {
+    float d = 0.f;
+#pragma unroll
+    for (int k = 0; k < FP; k += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(&zB[r * FP + k]);
+      d = fmaf(v[0], zr[k], d);
+      d = fmaf(v[1], zr[k + 1], d);
+      d = fmaf(v[2], zr[k + 2], d);
+      d = fmaf(v[3], zr[k + 3], d);
+    }
+    return __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d, snB[r] + sn_own), 0.f));
+  };
   float tol_in = -1.f;
   const float epsf = (float)eps;
   int it = 0;
   for (; it < max_inner; ++it) {
-    // step 1: i = argmax_{I_up ∩ B} −y·G
-    unsigned k1 = 0u;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool up = val[s] && (ys[s] > 0.f ? a[s] < Cw[s] : a[s] > 0.f);
-      if (up) k1 = max(k1, (f32_okey(-ys[s] * g[s]) & ~0x7Fu) | (unsigned)(lane + 64 * s));
-    }
+    const int par = it & 1;
+    float* glp = gl + par * Q;
+    float* alp = al + par * Q;
+    float* kip = kil + par * Q;
+    unsigned* r1 = red + par * 16;          // step-1 keys
+    unsigned* r3 = red + 32 + par * 16;     // I_low maxima (local gap)
+    unsigned* r2 = red + 64 + par * 16;     // step-2 keys
+    unsigned* r4 = red + 96 + par * 16;     // I_up maxima, unmasked (local gap)
+    if (valid) { glp[s] = g; alp[s] = a; }
+    const bool up = valid && (pos ? a < Cw : a > 0.f);
+    const bool low = valid && (pos ? a > 0.f : a < Cw);
+    // step 1: i = argmax_{I_up ∩ B} −y·G.  The slot rides in the key's low bits (a ~1e-4
+    // relative tie window for the pick); the stopping test uses the unmasked maxima.
+    const unsigned kv = up ? f32_okey(-y * g) : 0u;
+    unsigned k1 = up ? ((kv & ~kIdx) | (unsigned)s) : 0u;
+    unsigned k3 = low ? f32_okey(y * g) : 0u;
     k1 = wave_max_u32(k1);
-    if (k1 == 0u) break;
-    const int i = (int)(k1 & 0x7Fu);
-    const float Gi = readlane_f32(i < 64 ? g[0] : g[1], i & 63);
-    const float yi = readlane_f32(i < 64 ? ys[0] : ys[1], i & 63);
-    const float GmaxB = -yi * Gi;
-    // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / quad; K row i cached for the update
-    float Ki[2];
-    unsigned k2 = 0u, k3 = 0u;
+    k3 = wave_max_u32(k3);
+    const unsigned k4 = wave_max_u32(kv);
+    if (lane == 0) { r1[wave] = k1; r3[wave] = k3; r4[wave] = k4; }
+    __syncthreads();
+    unsigned K1 = 0u, K3 = 0u, K4 = 0u;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      Ki[s] = KB[i * (kWsQ + 1) + lane + 64 * s];
-      const bool low = val[s] && (ys[s] > 0.f ? a[s] > 0.f : a[s] < Cw[s]);
-      if (!low) continue;
-      const float yG = ys[s] * g[s];
-      k3 = max(k3, f32_okey(yG));
-      const float gd = GmaxB + yG;
+    for (int w = 0; w < kWsWaves; ++w) { K1 = max(K1, r1[w]); K3 = max(K3, r3[w]); K4 = max(K4, r4[w]); }
+    if (K1 == 0u || K3 == 0u) break;
+    const int i = (int)(K1 & kIdx);
+    const float Gi = glp[i];
+    const bool ipos = widx[i] < P.npos;
+    const float yi = ipos ? 1.f : -1.f;
+    const float GmaxB = -yi * Gi;
+    const float lgap = f32_from_okey(K4) + f32_from_okey(K3);
+    // (0.9999: the f32 local gap of a problem whose f64 gap is still ≥ eps always takes a pair)
+    if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
+    if (lgap < tol_in) break;
+    // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / (2 − 2 K_it)
+    const float Ki = valid ? krow(i) : 0.f;
+    if (valid) kip[s] = Ki;
+    unsigned k2 = 0u;
+    if (low) {
+      const float gd = GmaxB + y * g;
       if (gd > 0.f) {
-        float quad = 2.f - 2.f * Ki[s];
+        float quad = 2.f - 2.f * Ki;
         if (quad <= 0.f) quad = 1e-12f;
-        k2 = max(k2, (f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~0x7Fu) | (unsigned)(lane + 64 * s));
+        k2 = (f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~kIdx) | (unsigned)s;
       }
     }
     k2 = wave_max_u32(k2);
-    k3 = wave_max_u32(k3);
-    const float lgap = GmaxB + f32_from_okey(k3);
-    if (tol_in < 0.f) tol_in = fmaxf(epsf, (float)inner_frac * lgap);
-    if (lgap < tol_in || k2 == 0u) break;
-    const int j = (int)(k2 & 0x7Fu);
-    const float ai_old = readlane_f32(i < 64 ? a[0] : a[1], i & 63);
-    const float aj_old = readlane_f32(j < 64 ? a[0] : a[1], j & 63);
-    const float Gj = readlane_f32(j < 64 ? g[0] : g[1], j & 63);
-    const float yj = readlane_f32(j < 64 ? ys[0] : ys[1], j & 63);
-    const float Ci = readlane_f32(i < 64 ? Cw[0] : Cw[1], i & 63);
-    const float Cj = readlane_f32(j < 64 ? Cw[0] : Cw[1], j & 63);
-    const float Kij = KB[i * (kWsQ + 1) + j];
+    if (lane == 0) r2[wave] = k2;
+    __syncthreads();
+    unsigned K2 = 0u;
+#pragma unroll
+    for (int w = 0; w < kWsWaves; ++w) K2 = max(K2, r2[w]);
+    if (K2 == 0u) break;
+    const int j = (int)(K2 & kIdx);
+    const float Gj = glp[j];
+    const float ai_old = alp[i], aj_old = alp[j];
+    const float Kij = kip[j];
+    const bool jpos = widx[j] < P.npos;
+    const float yj = jpos ? 1.f : -1.f;
+    const float Ci = ipos ? Cpf : Cnf, Cj = jpos ? Cpf : Cnf;
     float ai = ai_old, aj = aj_old;
     if (yi != yj) {
       float quad = 2.f + 2.f * (yi * yj) * Kij;
@@ -516,44 +515,35 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
       else { if (ai < 0.f) { ai = 0.f; aj = sum; } }
     }
     const float ci = yi * (ai - ai_old), cj = yj * (aj - aj_old);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int w = lane + 64 * s;
-      if (w == i) a[s] = ai;
-      if (w == j) a[s] = aj;
-      const float Kj = KB[j * (kWsQ + 1) + w];
-      g[s] += ys[s] * fmaf(Ki[s], ci, Kj * cj);
-    }
+    const float Kj = valid ? krow(j) : 0.f;
+    if (s == i) a = ai;
+    if (s == j) a = aj;
+    g += y * fmaf(Ki, ci, Kj * cj);
   }
   // ---- publish: α of B, changed entries (slot order) for the global gradient update
-  int nc = 0;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    double anew = a0[s];
-    if (val[s] && a[s] != (float)a0[s]) {
-      const double C = ys[s] > 0.f ? P.Cp : P.Cn;
-      anew = a[s] <= 0.f ? 0.0 : (a[s] >= Cw[s] ? C : a0[s] + ((double)a[s] - (double)(float)a0[s]));
-    }
-    const bool ch = val[s] && anew != a0[s];
-    const unsigned long long mask = __ballot(ch);
-    const int pos = nc + __popcll(mask & ((1ull << lane) - 1ull));
-    if (ch) {
-      const int w = lane + 64 * s;
-      ap[tw[s]] = anew;
-      for (int k = 0; k < Fp; ++k) wsz[((size_t)b * Fp + k) * kWsQ + pos] = k < F ? zB[w * ldz + k] : 0.f;
-      wsn[(size_t)b * kWsQ + pos] = P.ngl2e * znB[w];
-      wdc[(size_t)b * kWsQ + pos] = (float)((double)ys[s] * (anew - a0[s]));
-    }
-    nc += __popcll(mask);
+  double anew = a0;
+  if (valid && a != (float)a0) {
+    const double C = pos ? P.Cp : P.Cn;
+    anew = a <= 0.f ? 0.0 : (a >= Cw ? C : a0 + ((double)a - (double)(float)a0));
+  }
+  const bool ch = valid && anew != a0;
+  const unsigned long long cm = __ballot(ch);
+  int nc;
+  const int cpos = wave_base(__popcll(cm), shi, &nc) + __popcll(cm & lanes_below());
+  if (ch) {
+    ap[t] = anew;
+    for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + cpos] = k < F ? zB[s * FP + k] : 0.f;
+    wsn[(size_t)b * Q + cpos] = sn_own;
+    wdc[(size_t)b * Q + cpos] = (float)((double)y * (anew - a0));
   }
   const int ncp = (nc + 31) & ~31;
-  for (int pos = nc + lane; pos < ncp; pos += 64) {
-    for (int k = 0; k < Fp; ++k) wsz[((size_t)b * Fp + k) * kWsQ + pos] = 0.f;
-    wsn[(size_t)b * kWsQ + pos] = 0.f;
-    wdc[(size_t)b * kWsQ + pos] = 0.f;
+  for (int p = nc + tid; p < ncp; p += kWsThreads) {
+    for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + p] = 0.f;
+    wsn[(size_t)b * Q + p] = 0.f;
+    wdc[(size_t)b * Q + p] = 0.f;
   }
   const long long c3 = __builtin_amdgcn_s_memtime();
-  if (lane == 0) {
+  if (tid == 0) {
     S->cyc_select += c1 - c0;
     S->cyc_p0 += c0a - c0;
     S->cyc_p1 += c0b - c0a;
@@ -564,6 +554,7 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     if (it == 0 || nc == 0) S->done = 1;
     S->nc = nc;
     S->nws = nws;
+    S->nprev = nnew;
     S->outer += 1;
     S->inner += it;
     S->gap = gap;
@@ -571,7 +562,8 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
 }
 
 // G_t += y_t · Σ_c dc_c · exp2(γ'‖x_t − x_c‖²) for every point t of every active problem, then t's
-// selection keys for the next working set.
+// selection keys for the next working set.  The changed coefficients are staged through LDS in
+// chunks of kWsChunk; every wave takes part in every barrier (waves past the end compute nothing).
 template <int KS>
 __global__ __launch_bounds__(256) void ws_gupdate_kernel(const WsProb* __restrict__ probs,
                                                          const WsState* __restrict__ states,
@@ -581,7 +573,7 @@ __global__ __launch_bounds__(256) void ws_gupdate_kernel(const WsProb* __restric
                                                          double* __restrict__ G_all,
                                                          const float* __restrict__ wsz,
                                                          const float* __restrict__ wsn,
-                                                         const float* __restrict__ wdc, int Fp, WsAux X) {
+                                                         const float* __restrict__ wdc, int Fp2, int Q, WsAux X) {
   const int b = blockIdx.y;
   const int nc = states[b].nc;
   if (nc == 0) return;
@@ -589,64 +581,70 @@ __global__ __launch_bounds__(256) void ws_gupdate_kernel(const WsProb* __restric
   const int row_blk = blockIdx.x * 256;
   if (row_blk >= P.l) return;
   const int ncp = (nc + 31) & ~31;
-  __shared__ __attribute__((aligned(16))) float sv_l[2 * KS * kWsQ];
-  __shared__ __attribute__((aligned(16))) float sn_l[kWsQ];
-  __shared__ __attribute__((aligned(16))) float cf_l[kWsQ];
-  for (int i = threadIdx.x; i < 2 * KS * ncp; i += blockDim.x) {
-    const int k = i / ncp, c = i - k * ncp;
-    sv_l[k * kWsQ + c] = k < Fp ? wsz[((size_t)b * Fp + k) * kWsQ + c] : 0.f;
-  }
-  for (int c = threadIdx.x; c < ncp; c += blockDim.x) {
-    sn_l[c] = wsn[(size_t)b * kWsQ + c];
-    cf_l[c] = wdc[(size_t)b * kWsQ + c];
-  }
-  __syncthreads();
+  __shared__ __attribute__((aligned(16))) float sv_l[2 * KS * kWsChunk];
+  __shared__ __attribute__((aligned(16))) float sn_l[kWsChunk];
+  __shared__ __attribute__((aligned(16))) float cf_l[kWsChunk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r32 = lane & 31, hi = lane >> 5;
   const int r0 = row_blk + wave * 64;
   const int row = r0 + lane;
   const bool valid = row < P.l;
-  if (r0 >= P.l) return;   // wave-uniform
-  // issue this lane's G/α loads first: their latency hides under the MFMA work
+  const bool live = r0 < P.l;   // wave-uniform
+  // this lane's G/α loads first: their latency hides under the MFMA work
   const double gold = valid ? G_all[P.aoff + row] : 0.0;
   const double a = valid ? alpha_all[P.aoff + row] : 0.0;
-  double gnew = 0.0;
   const int ra = r0 + r32, rb = r0 + 32 + r32;
   float za[KS], zb[KS];
   const float* zA = zcat + (P.zoff + ra) * F;
   const float* zBp = zcat + (P.zoff + rb) * F;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 2 * s + hi;
-    za[s] = (k < F && ra < P.l) ? zA[k] : 0.f;
-    zb[s] = (k < F && rb < P.l) ? zBp[k] : 0.f;
+  for (int q = 0; q < KS; ++q) {
+    const int k = 2 * q + hi;
+    za[q] = (k < F && ra < P.l) ? zA[k] : 0.f;
+    zb[q] = (k < F && rb < P.l) ? zBp[k] : 0.f;
   }
   const float zsa = ra < P.l ? P.ngl2e * zn_all[P.aoff + ra] : 0.f;
   const float zsb = rb < P.l ? P.ngl2e * zn_all[P.aoff + rb] : 0.f;
   const float k2 = -2.f * P.ngl2e;
   float pa = 0.f, pb = 0.f;
-  for (int t = 0; t < ncp; t += 32) {
-    f32x16 A = {0.f}, B = {0.f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const float sv = sv_l[(2 * s + hi) * kWsQ + t + r32];
-      A = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, za[s], A, 0, 0, 0);
-      B = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, zb[s], B, 0, 0, 0);
+  for (int c0 = 0; c0 < ncp; c0 += kWsChunk) {
+    const int cn = min(kWsChunk, ncp - c0);
+    __syncthreads();   // the previous chunk is consumed
+    for (int i = threadIdx.x; i < 2 * KS * cn; i += blockDim.x) {
+      const int k = i / cn, c = i - k * cn;
+      sv_l[k * kWsChunk + c] = k < Fp2 ? wsz[((size_t)b * Fp2 + k) * Q + c0 + c] : 0.f;
     }
+    for (int c = threadIdx.x; c < cn; c += blockDim.x) {
+      sn_l[c] = wsn[(size_t)b * Q + c0 + c];
+      cf_l[c] = wdc[(size_t)b * Q + c0 + c];
+    }
+    __syncthreads();
+    if (!live) continue;
+    for (int t = 0; t < cn; t += 32) {
+      f32x16 A = {0.f}, B = {0.f};
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int c0 = t + 8 * g + 4 * hi;
-      const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[c0]);
-      const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[c0]);
+      for (int q = 0; q < KS; ++q) {
+        const float sv = sv_l[(2 * q + hi) * kWsChunk + t + r32];
+        A = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, za[q], A, 0, 0, 0);
+        B = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, zb[q], B, 0, 0, 0);
+      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        pa = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, A[4 * g + q], snv[q] + zsa), 0.f)), pa);
-        pb = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, B[4 * g + q], snv[q] + zsb), 0.f)), pb);
+      for (int gq = 0; gq < 4; ++gq) {
+        const int cc = t + 8 * gq + 4 * hi;
+        const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[cc]);
+        const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[cc]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pa = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, A[4 * gq + q], snv[q] + zsa), 0.f)), pa);
+          pb = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, B[4 * gq + q], snv[q] + zsb), 0.f)), pb);
+        }
       }
     }
   }
+  if (!live) return;
   pa += __shfl_xor(pa, 32, kWave);
   pb += __shfl_xor(pb, 32, kWave);
+  double gnew = 0.0;
   if (valid) {
     const double upd = (double)(lane < 32 ? pa : pb);
     gnew = gold + (row < P.npos ? upd : -upd);
@@ -693,45 +691,46 @@ __global__ __launch_bounds__(kWsThreads) void ws_finalize_kernel(const WsProb* _
 }
 
 // ------------------------------------------------------------------------------------------
-static size_t ws_lds_bytes(int F) {
-  return (size_t)4096 * 4 + (size_t)kWsQ * (kWsQ + 1) * 4 + (size_t)kWsQ * (F | 1) * 4 + kWsQ * 4 + kWsQ * 4;
-}
-
 static int ws_ks(int F) {
   const int ks = (F + 1) / 2;
-  return ks <= 4 ? 4 : ks <= 9 ? 9 : ks <= 12 ? 12 : ks <= 16 ? 16 : 32;
+  return ks <= 4 ? 4 : ks <= 9 ? 9 : ks <= 12 ? 12 : 24;
 }
 
-static WsAux ws_aux(uintptr_t keys, long long n, uintptr_t hist, uintptr_t gkey) {
-  (void)hist;
+// Working-set size for F features: 1024 slots while z_B fits (F ≤ 24), else 512 (F ≤ 48).
+static int ws_q(int F) { return F <= 24 ? 1024 : 512; }
+
+static WsAux ws_aux(uintptr_t keys, long long n, uintptr_t gkey) {
   return WsAux{(unsigned*)keys, n, (unsigned long long*)gkey};
 }
 
 void ws_init(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
              uintptr_t G, uintptr_t states, uintptr_t keys, long long n, uintptr_t hist, uintptr_t gkey,
              uintptr_t stream) {
-  HFENS_REQUIRE(F >= 1 && F <= 64, "ws_init: 1 <= F <= 64");
+  (void)hist;
+  HFENS_REQUIRE(F >= 1 && F <= 48, "ws_init: 1 <= F <= 48");
   if (P == 0 || max_l == 0) return;
   hipLaunchKernelGGL(ws_init_kernel, dim3((max_l + 255) / 256, P), dim3(256), 0, as_stream(stream),
                      (const WsProb*)probs, (const float*)zcat, F, (float*)zn, (double*)alpha, (double*)G,
-                     (WsState*)states, ws_aux(keys, n, hist, gkey));
+                     (WsState*)states, ws_aux(keys, n, gkey));
   launch_check();
 }
 
-// n_iter outer iterations (select+solve, then the gradient update) enqueued back to back.
+// n_iter outer iterations (select+solve, then the gradient update) enqueued back to back; finished
+// problems return at once.  wsz/wsn/wdc hold [P][2·KS][q] / [P][q] / [P][q]; wsprev [P][q/2].
 void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
-              uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t keys,
-              long long n, uintptr_t hist, uintptr_t gkey, double eps, int max_outer, int max_inner,
+              uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
+              uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
               double inner_frac, int n_iter, uintptr_t stream) {
-  const WsAux X = ws_aux(keys, n, hist, gkey);
-  HFENS_REQUIRE(F >= 1 && F <= 64, "ws_steps: 1 <= F <= 64");
+  const WsAux X = ws_aux(keys, n, gkey);
+  HFENS_REQUIRE(F >= 1 && F <= 48, "ws_steps: 1 <= F <= 48");
   // (< 32768: the packed 16|16-bit member counts of the radix selector)
   HFENS_REQUIRE(max_l < 32 * kWsThreads, "ws_steps: problems of 32768+ points need the multi-workgroup selector");
   if (P == 0 || max_l == 0) return;
   hipStream_t st = as_stream(stream);
   const int KS = ws_ks(F);
-  const int Fp = 2 * KS;
-  const size_t lds = ws_lds_bytes(F);
+  const int Fp2 = 2 * KS;
+  const int Q = ws_q(F);
+  const int FP = F <= 24 ? (F + 3) / 4 * 4 : (F + 7) / 8 * 8;
   auto pp = (const WsProb*)probs;
   auto sp = (WsState*)states;
   auto zp = (const float*)zcat;
@@ -741,22 +740,30 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
   auto wz = (float*)wsz;
   auto wn = (float*)wsn;
   auto wd = (float*)wdc;
+  auto wp = (int*)wsprev;
+  const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
   for (int it = 0; it < n_iter; ++it) {
-#define WS_SEL(MM)                                                                                      \
-  if (max_l <= MM * kWsThreads) {                                                                       \
-    hipLaunchKernelGGL(ws_select_solve_kernel<MM>, dim3(P), dim3(kWsThreads), lds, st, pp, sp, zp, F,  \
-                       np_, ap, gp, wz, wn, wd, Fp, eps, max_outer, max_inner, inner_frac, X);          \
+#define WS_SEL(MM, FF, QQ)                                                                              \
+  if (M == MM && FP == FF) {                                                                            \
+    hipLaunchKernelGGL((ws_select_solve_kernel<MM, FF, QQ>), dim3(P), dim3(kWsThreads),                 \
+                       ws_lds_bytes(QQ, FF), st, pp, sp, zp, F, np_, ap, gp, wz, wn, wd, Fp2, wp, eps,  \
+                       max_outer, max_inner, inner_frac, X);                                            \
   } else
-    WS_SEL(1) WS_SEL(2) WS_SEL(4) WS_SEL(8) WS_SEL(16) WS_SEL(32) {}
+#define WS_SEL_M(FF, QQ) WS_SEL(4, FF, QQ) WS_SEL(16, FF, QQ) WS_SEL(32, FF, QQ)
+    WS_SEL_M(4, 1024) WS_SEL_M(8, 1024) WS_SEL_M(12, 1024) WS_SEL_M(16, 1024) WS_SEL_M(20, 1024)
+    WS_SEL_M(24, 1024) WS_SEL_M(32, 512) WS_SEL_M(40, 512) WS_SEL_M(48, 512) {
+      HFENS_REQUIRE(false, "ws_steps: no select/solve instance for this F");
+    }
+#undef WS_SEL_M
 #undef WS_SEL
     launch_check();
     const dim3 grid((max_l + 255) / 256, P);
 #define WS_UPD(K)                                                                                    \
   case K:                                                                                           \
     hipLaunchKernelGGL(ws_gupdate_kernel<K>, grid, dim3(256), 0, st, pp, sp, zp, F, np_, ap, gp, wz, \
-                       wn, wd, Fp, X);                                                              \
+                       wn, wd, Fp2, Q, X);                                                          \
     break;
-    switch (KS) { WS_UPD(4) WS_UPD(9) WS_UPD(12) WS_UPD(16) WS_UPD(32) }
+    switch (KS) { WS_UPD(4) WS_UPD(9) WS_UPD(12) WS_UPD(24) }
 #undef WS_UPD
     launch_check();
   }

@@ -362,6 +362,7 @@ def test_smo_coop_matches_single_workgroup(dev, monkeypatch, rows, slice_, otf):
     yd = y.to(dev)
     Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
 
+    monkeypatch.setattr(smo, "SOLVER", "exact")
     monkeypatch.setattr(smo, "COOP_OTF", otf)   # Gram rows recomputed per pair vs read from the stored Gram
 
     def fit(coop):
@@ -438,6 +439,7 @@ def test_smo_shared_gram_matches_own_grams(dev, monkeypatch, rows):
     Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
     yd = y.to(dev)
     Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
+    monkeypatch.setattr(smo, "SOLVER", "exact")
     monkeypatch.setattr(smo, "COOP_OTF", False)
     monkeypatch.setattr(smo, "COOP_MIN_SLICE", 384)
 
