@@ -188,7 +188,10 @@ def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
              "stage_host_seconds": host_med,
              "step_ms_min_med_max": [round(1e3 * x, 2) for x in _step_stats(step_ends, t0)],
              "svm": dict(smo.LAST_SMO_INFO, **({"lowrank": {k: v for k, v in svc_lowrank.LAST_INFO.items()}}
-                                              if smo.LAST_SMO_INFO.get("solver") == "nystrom-ipm" else {})),
+                                              if smo.LAST_SMO_INFO.get("solver") == "nystrom-ipm" else {}),
+                         **({"ws_rounds_max": int(smo.LAST_WS_STATS["outer"].max()),
+                             "ws_pairs_max": int(smo.LAST_WS_STATS["inner"].max())}
+                            if smo.LAST_SMO_INFO.get("solver") == "ws" else {})),
              "gbdt_path": hist_gbdt.LAST_PATH.get("path"),
              "logreg_path": logreg_solver.LAST_PATH.get("path"),
              "concurrent_bases": bool(stack_trainer.CONCURRENT_BASES and dev.type == "cuda"),
@@ -345,8 +348,12 @@ def bench_gbdt(a):
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1000 * elapsed / a.steps, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": round(value / base, 2),
-            "dtype": "fp8" if (deep and fp8 is not None) else "fp32",
+            # dtype = the precision of the TIMED work (training); the fp8 leaf-value inference runs
+            # after the clock and reports its own dtype in fp8_leaf_inference
+            "dtype": "fp32",
             "train_dtype": "fp32 gradients, int64 fixed-point histograms, f64 leaf values",
+            "infer_dtype": "fp32 folded stump tables" + (" (+ fp8 e4m3 leaf GEMV, see fp8_leaf_inference)"
+                                                         if fp8 is not None else ""),
             "data": "synthetic Table S1-shaped cohort (device generator), no NaN",
             "auroc": round(float(auc), 4),
             "infer_rows_x_models_per_sec": round(n_hold * seeds / max(t_inf, 1e-12), 1) if t_inf == t_inf else None,

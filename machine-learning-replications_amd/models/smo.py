@@ -582,6 +582,8 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
 
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
 WS_INNER_PER_Q = int(os.environ.get("HFENS_SVM_WS_INNER", "4"))        # inner pair cap = this × q
+WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
+_WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None):
@@ -603,6 +605,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     wsn = torch.zeros(P * Q, dtype=torch.float32, device=device)
     wdc = torch.zeros(P * Q, dtype=torch.float32, device=device)
     wsprev = torch.zeros(P * (Q // 2), dtype=torch.int32, device=device)
+    wsidx = torch.zeros(P * Q, dtype=torch.int32, device=device)
+    wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
     max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
     max_inner = WS_INNER_PER_Q * Q
     keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
@@ -611,38 +615,81 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     E.ws_init(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
               states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
     done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
-    outer = 0
-    # ~35 outer rounds on the bench's 10k problem (scripts/ws_sim.py): one host check after the
-    # first 24, then every 8 (finished problems return at once from the launches in between)
-    chunk = steps_per_check or 24
-    while outer < max_outer:
+    err = None
+    if not _WS_SYNC[0]:
+        # no host synchronisation: WS_ROUNDS_AHEAD rounds are enqueued at once (finished problems
+        # return from each launch at once), so the caller's other streams are launched meanwhile;
+        # a batch still unconverged after them reports err and is re-solved synchronously by
+        # finish_svc_batch
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
-                   keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC, chunk, s)
-        outer += chunk
-        chunk = steps_per_check or 8
-        if bool((done_view != 0).all()):
-            break
+                   wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
+                   min(WS_ROUNDS_AHEAD, max_outer), wprof.data_ptr() if wprof is not None else 0, s)
+        err = (done_view == 0).any().to(torch.int32).reshape(1)
+    else:
+        outer = 0
+        # one host check after the first 24 rounds, then every 8
+        chunk = steps_per_check or 24
+        while outer < max_outer:
+            E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
+                       states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
+                       wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
+                       chunk, wprof.data_ptr() if wprof is not None else 0, s)
+            outer += chunk
+            chunk = steps_per_check or 8
+            if bool((done_view != 0).all()):
+                break
     rho = torch.empty(P, dtype=torch.float64, device=device)
     iters = torch.empty(P, dtype=torch.int32, device=device)
     inner = torch.empty(P, dtype=torch.int64, device=device)
     gap = torch.empty(P, dtype=torch.float64, device=device)
     E.ws_finalize(pdev.data_ptr(), P, states.data_ptr(), alpha.data_ptr(), G.data_ptr(), rho.data_ptr(),
                   iters.data_ptr(), inner.data_ptr(), gap.data_ptr(), s)
-    cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 10:22].cpu().contiguous().view(torch.int64).numpy()
-    LAST_WS_STATS.update(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
-                         cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
-                         cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5], q=Q)
+
+    def stats():   # read back only when someone looks (tests, bench diagnostics): no sync here
+        cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 10:22].cpu().contiguous().view(torch.int64).numpy()
+        return dict(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
+                    cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
+                    cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5], q=Q,
+                    phases=wprof.view(P, 6).cpu().numpy() if wprof is not None else None)
+    LAST_WS_STATS.set_thunk(stats)
     LAST_SMO_INFO.clear()
-    LAST_SMO_INFO.update(problems=P, max_l=max_l, solver="ws", q=Q, outer_max=int(iters.max().item()))
-    return alpha, rho, iters, None
+    LAST_SMO_INFO.update(problems=P, max_l=max_l, solver="ws", q=Q)
+    return alpha, rho, iters, err
 
 
-LAST_WS_STATS: dict = {}
+class _LazyStats(dict):
+    """A dict filled on first read from a thunk (device statistics read back only if used)."""
+
+    def set_thunk(self, f):
+        self.clear()
+        self._f = f
+
+    def _fill(self):
+        f = getattr(self, "_f", None)
+        if f is not None:
+            self._f = None
+            super().update(f())
+
+    def __getitem__(self, k):
+        self._fill()
+        return super().__getitem__(k)
+
+    def get(self, k, d=None):
+        self._fill()
+        return super().get(k, d)
+
+    def __contains__(self, k):
+        self._fill()
+        return super().__contains__(k)
+
+
+LAST_WS_STATS = _LazyStats()
 LAST_SMO_PROF: dict = {}
 LAST_SMO_INFO: dict = {}
 PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
 PROFILE_COOP = os.environ.get("HFENS_PROFILE_COOP", "0") == "1"   # in-kernel phase counters of the cooperative SMO
+PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # in-kernel phase counters of the working-set solver
 
 
 def assign_problems(sizes, world: int) -> List[int]:
@@ -968,20 +1015,25 @@ def finish_svc_batch(st: dict):
                                                    st["sol"], st["AB"], st["device"])
     err = sol.get("smo_err")
     if err is not None and float(err.max()) != 0.0:
-        # a member exchange timed out (members not co-resident beside concurrent work): re-solve
-        # the whole batch with the one-workgroup kernel.  Under a process group err is part of
-        # the all-reduced solution vector, so every rank takes this branch together.
+        # cooperative SMO: a member exchange timed out (members not co-resident beside concurrent
+        # work) → re-solve with the one-workgroup kernel; working-set SMO: a problem needed more
+        # than WS_ROUNDS_AHEAD rounds → re-solve with host-checked rounds.  Under a process group
+        # err is part of the all-reduced solution vector, so every rank takes this branch together.
         if st.get("retried"):
-            raise RuntimeError("SMO: member exchange timed out again on the one-workgroup re-solve")
+            raise RuntimeError("SMO: the synchronous re-solve failed again")
         import warnings
-        warnings.warn("cooperative SMO timed out waiting for a member; re-solving with one workgroup per problem")
-        _FORCE_SINGLE[0] = True
+        ws = LAST_SMO_INFO.get("solver") == "ws"
+        warnings.warn("working-set SMO needed more than %d rounds; re-solving with host-checked rounds"
+                      % WS_ROUNDS_AHEAD if ws else
+                      "cooperative SMO timed out waiting for a member; re-solving with one workgroup per problem")
+        flag = _WS_SYNC if ws else _FORCE_SINGLE
+        flag[0] = True
         try:
             st2 = launch_svc_batch(*st["args"])
         finally:
-            _FORCE_SINGLE[0] = False
+            flag[0] = False
         st2["retried"] = True
-        LAST_SMO_INFO["coop_fallback"] = True
+        LAST_SMO_INFO["ws_resolve" if ws else "coop_fallback"] = True
         return finish_svc_batch(st2)
     # ---- final models: ONE device→host read of the Platt (A, B) pairs and every final solve's
     # support mask, ρ and iteration count; the bookkeeping is then numpy, the gathers non-blocking

@@ -231,6 +231,9 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         lr_budget = logreg_solver.BLOCK_BUDGET[0]
         if _smo.LAST_SMO_INFO.get("solver") in ("coop", "coop-otf"):
             logreg_solver.BLOCK_BUDGET[0] = max(1, _smo.COOP_RESERVE_CUS // 2)
+        elif _smo.LAST_SMO_INFO.get("solver") == "ws" and X.is_cuda:
+            # the working-set solver holds one CU per problem (its gradient updates come and go)
+            logreg_solver.BLOCK_BUDGET[0] = max(1, _smo._num_cus(X.device) - int(_smo.LAST_SMO_INFO["problems"]) - 8)
         try:
             with torch.cuda.stream(other):
                 for i, (name, est) in enumerate(clf.estimators):

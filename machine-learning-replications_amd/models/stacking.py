@@ -133,16 +133,25 @@ class StackingClassifier(Estimator):
             from .scaler import StandardScaler
             from .svc import SVC
             e = self.estimators_
+            # the same shape/flag contract as ops.packing.pack_stack (the fused GPU kernel):
+            # no passthrough, an RBF SVC with Platt probabilities, and the scaler's with_mean /
+            # with_std flags honoured (identity centre / scale when off)
             if (ops.has_ext() and len(e) == 3 and isinstance(e[0], Pipeline) and len(e[0].steps) == 2
                     and isinstance(e[0].steps[0][1], StandardScaler) and isinstance(e[0].steps[1][1], SVC)
                     and isinstance(e[1], GradientBoostingClassifier) and isinstance(e[2], LogisticRegression)
-                    and isinstance(self.final_estimator_, LogisticRegression)):
+                    and isinstance(self.final_estimator_, LogisticRegression)
+                    and not getattr(self, "passthrough", False)
+                    and e[0].steps[1][1].kernel == "rbf" and e[0].steps[1][1].probability
+                    and e[0].steps[1][1]._dual_coef_.shape[0] == 1):
                 import numpy as np
                 sc, svc = e[0].steps[0][1], e[0].steps[1][1]
                 g, lr, mt = e[1], e[2], self.final_estimator_
                 c = lambda t, dt=np.float64: np.ascontiguousarray(t.detach().cpu().numpy(), dtype=dt)  # noqa: E731
                 K = int(g.tree_feature_.shape[1])
-                pk = dict(mean=c(sc.mean_), scale=c(sc.scale_), sv=c(svc.support_vectors_),
+                Fs = int(svc.support_vectors_.shape[1])
+                mean = c(sc.mean_) if sc.with_mean else np.zeros(Fs)
+                scale = c(sc.scale_) if sc.with_std else np.ones(Fs)
+                pk = dict(mean=mean, scale=scale, sv=c(svc.support_vectors_),
                           coef=c(svc._dual_coef_[0]), gamma=float(svc._gamma), icpt=float(svc._intercept_[0]),
                           A=float(svc._probA[0]), B=float(svc._probB[0]), T=int(g.tree_feature_.shape[0]), K=K,
                           feat=c(g.tree_feature_, np.int64), thr=c(g.tree_threshold_),
@@ -150,8 +159,8 @@ class StackingClassifier(Estimator):
                           value=c(g.tree_value_.reshape(g.tree_value_.shape[0], -1)[:, :K]),
                           init=float(g.init_raw_), lr=float(g.learning_rate), lrc=c(lr.coef_[0]),
                           lri=float(lr.intercept_[0]), meta=c(mt.coef_[0]), metai=float(mt.intercept_[0]),
-                          F=int(sc.mean_.numel()))
-                if pk["meta"].size != 3 or pk["lrc"].size != pk["F"] or pk["sv"].shape[1] != pk["F"]:
+                          F=Fs)
+                if pk["mean"].size != Fs or pk["scale"].size != Fs or pk["meta"].size != 3 or pk["lrc"].size != pk["F"] or pk["sv"].shape[1] != pk["F"]:
                     pk = None
                 else:   # raw pointers resolved once (each .ctypes access costs ~1 µs)
                     pk["args"] = (pk["mean"].ctypes.data, pk["scale"].ctypes.data, pk["sv"].shape[0],

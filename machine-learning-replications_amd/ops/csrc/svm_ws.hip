@@ -218,29 +218,18 @@ __global__ __launch_bounds__(256) void ws_init_kernel(const WsProb* __restrict__
   ws_publish_keys(P, b, t, valid, 0.0, -1.0, X);
 }
 
-// LDS carve of ws_select_solve (dynamic region only, every block a multiple of 16 bytes):
-//   [small]  256 ints: scan scratch (16), bin info (8), reduction slots (4 × 2 parities × 16 u32)
-//   [A]      selection: hist [2][2048] int + membership bitmap [1024] u32; then z_B [q][FP] f32
-//   [snB]    γ'·‖z‖² of B [q]      [widx] point index of each slot [q]
-//   [mirror] g, α, K(x_i,·) of every slot, 2 parities each: [3][2][q] f32
-__host__ __device__ constexpr size_t ws_lds_bytes(int Q, int FP) {
-  return 256 * 4 + ((size_t)Q * FP * 4 > 20480 ? (size_t)Q * FP * 4 : 20480) + (size_t)Q * 4 * 2 +
-         (size_t)6 * Q * 4;
-}
+// ---- ws_select: the next working set (one 1024-thread workgroup per problem) -------------------
+// LDS (dynamic region only, every block a multiple of 16 bytes): scan scratch (16 ints), bin info
+// (8), histograms [2][2048] int, membership bitmap [1024] u32 (points picked this round), widx [Q].
+constexpr size_t ws_sel_lds_bytes(int Q) { return 32 * 4 + 4096 * 4 + 1024 * 4 + (size_t)Q * 4; }
 
-// M = points per lane (selection).  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L
-// its points w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots
-// give index-ordered ranks.  FP = features padded to a multiple of 4; Q = working-set size (one
-// slot per thread).  FP: F rounded up to 4 (Q = 1024) or to 8 (Q = 512).
-template <int M, int FP, int Q>
-__global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
-    const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
-    const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
-    float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc, int Fp2,
-    int* __restrict__ wsprev, double eps, int max_outer, int max_inner, double inner_frac, WsAux X) {
-  static_assert(Q <= kWsThreads && (Q & (Q - 1)) == 0, "one slot per thread, power of two");
-  static_assert(FP % 4 == 0, "z rows are read as float4");
-  constexpr unsigned kIdx = Q - 1;   // slot bits packed under the selection keys
+// M = points per lane.  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L its points
+// w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots give
+// index-ordered ranks.  Writes B (point indices, new picks first) to wsidx[b][0, nws).
+template <int M, int Q>
+__global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
+    const WsProb* __restrict__ probs, WsState* __restrict__ states, int* __restrict__ wsidx,
+    int* __restrict__ wsprev, double eps, int max_outer, WsAux X) {
   const int b = blockIdx.x;
   WsState* S = states + b;
   if (S->done) return;
@@ -251,22 +240,11 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
   const int l = P.l;
   extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
   int* shi = reinterpret_cast<int*>(ws_lds);                     // [16]
-  int* binfo = shi + 16;                                         // [8]
-  unsigned* red = reinterpret_cast<unsigned*>(binfo + 8);        // [4][2][16]
-  unsigned char* regA = ws_lds + 256 * 4;
-  int* hist = reinterpret_cast<int*>(regA);                      // [2][2048]
-  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);       // [1024]: points picked this round
-  float* zB = reinterpret_cast<float*>(regA);                    // [Q][FP] (after the selection)
-  const size_t szA = (size_t)Q * FP * 4 > 20480 ? (size_t)Q * FP * 4 : 20480;
-  float* snB = reinterpret_cast<float*>(regA + szA);             // [Q]
-  int* widx = reinterpret_cast<int*>(snB + Q);                   // [Q]
-  float* gl = reinterpret_cast<float*>(widx + Q);                // [2][Q]
-  float* al = gl + 2 * Q;                                        // [2][Q]
-  float* kil = al + 2 * Q;                                       // [2][Q]
+  int* binfo = shi + 16;                                         // [8] (+8 pad)
+  int* hist = shi + 32;                                          // [2][2048]
+  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);       // [1024]
+  int* widx = reinterpret_cast<int*>(bm + 1024);                 // [Q]
   const int t0 = wave * 64 * M + lane;
-
-  const double* Gp = G_all + P.aoff;
-  double* ap = alpha_all + P.aoff;
   const long long c0 = __builtin_amdgcn_s_memtime();
   // ---- global gap from the maxima published by the gradient kernel
   const unsigned long long gku = X.gkey[2 * b], gkl = X.gkey[2 * b + 1];
@@ -294,7 +272,7 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
   const int n_low = n_up >> 16;
   n_up &= 0xFFFF;
   if (!(gap >= eps) || S->outer >= max_outer || n_up == 0 || n_low == 0) {
-    if (tid == 0) { S->done = 1; S->gap = gap; S->nc = 0; }
+    if (tid == 0) { S->done = 1; S->gap = gap; S->nc = 0; S->nws = 0; }
     return;
   }
   if (tid == 0) { X.gkey[2 * b] = 0ull; X.gkey[2 * b + 1] = 0ull; }   // consumed (all read it above)
@@ -371,89 +349,179 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
   }
   const int nnew = base;
   __syncthreads();
-  // ---- the previous round's new picks that were not picked again (index-ordered by their old slot)
-  {
-    const int pv = tid < nprev ? wsprev[(size_t)b * (Q / 2) + tid] : -1;
-    const bool keep = pv >= 0 && !((bm[pv >> 5] >> (pv & 31)) & 1u);
-    const unsigned long long kb = __ballot(keep);
-    int ktot;
-    const int kpos = nnew + wave_base(__popcll(kb), shi, &ktot) + __popcll(kb & lanes_below());
-    if (keep) widx[kpos] = pv;
-    __syncthreads();   // every old entry was read before the new picks overwrite the list
-    for (int w = tid; w < nnew; w += kWsThreads) wsprev[(size_t)b * (Q / 2) + w] = widx[w];
-    base = nnew + ktot;
-  }
-  const int nws = base;
+  // ---- the previous round's new picks that were not picked again (in their old order)
+  const int pv = tid < nprev ? wsprev[(size_t)b * (Q / 2) + tid] : -1;
+  const bool keep = pv >= 0 && !((bm[pv >> 5] >> (pv & 31)) & 1u);
+  const unsigned long long kb = __ballot(keep);
+  int ktot;
+  const int kpos = nnew + wave_base(__popcll(kb), shi, &ktot) + __popcll(kb & lanes_below());
+  if (keep) widx[kpos] = pv;
+  __syncthreads();   // every old entry was read before the new picks overwrite the list
+  const int nws = nnew + ktot;
+  for (int w = tid; w < nnew; w += kWsThreads) wsprev[(size_t)b * (Q / 2) + w] = widx[w];
+  for (int w = tid; w < nws; w += kWsThreads) wsidx[(size_t)b * Q + w] = widx[w];
   const long long c1 = __builtin_amdgcn_s_memtime();
-  // ---- features of B into LDS (zero-padded to FP: the padded terms of the dot are exact no-ops)
-  for (int e = tid; e < nws * FP; e += kWsThreads) {
+  if (tid == 0) {
+    S->cyc_select += c1 - c0;
+    S->cyc_p0 += c0a - c0;
+    S->cyc_p1 += c0b - c0a;
+    S->cyc_p2 += c0c - c0b;
+    S->nws = nws;
+    S->nprev = nnew;
+    S->gap = gap;
+  }
+}
+
+// ---- ws_solve: the inner SMO on B (one 256-thread workgroup per problem) -----------------------
+// Four waves, SL = Q/256 slots per thread (slot s = tid + 256·m), each slot's features in
+// registers.  LDS: reduction slots (4 keys × 2 parities × 4 waves), z_B [Q][FP] f32, γ'‖z‖² [Q],
+// widx [Q], and per-slot mirrors of g, α and K(x_i,·), 2 parities each (a slot is read by every
+// thread after the barrier that follows its write, and rewritten only two barriers later).
+constexpr int kWsInner = 256;
+constexpr size_t ws_solve_lds_bytes(int Q, int FP) {
+  return 32 * 4 * 2 + (size_t)Q * FP * 4 + (size_t)Q * 4 * 2 + (size_t)6 * Q * 4;
+}
+
+template <int FP, int Q>
+__global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
+    const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
+    const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
+    const int* __restrict__ wsidx, float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc,
+    int Fp2, double eps, int max_inner, double inner_frac, long long* __restrict__ prof) {
+  static_assert(Q % kWsInner == 0 && (Q & (Q - 1)) == 0, "whole slots per thread, power of two");
+  static_assert(FP % 4 == 0, "z rows are read as float4");
+  constexpr int SL = Q / kWsInner;
+  constexpr unsigned kIdx = Q - 1;   // slot bits packed under the selection keys
+  const int b = blockIdx.x;
+  WsState* S = states + b;
+  if (S->done) return;
+  const WsProb P = probs[b];
+  const int nws = S->nws;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
+  unsigned* red = reinterpret_cast<unsigned*>(ws_lds);            // [4 keys][2 parities][4 waves]
+  float* zB = reinterpret_cast<float*>(ws_lds + 32 * 4 * 2);       // [Q][FP]
+  float* snB = zB + (size_t)Q * FP;                                 // [Q]
+  int* widx = reinterpret_cast<int*>(snB + Q);                      // [Q]
+  float* gl = reinterpret_cast<float*>(widx + Q);                   // [2][Q]
+  float* al = gl + 2 * Q;                                           // [2][Q]
+  float* kil = al + 2 * Q;                                          // [2][Q]
+  const double* Gp = G_all + P.aoff;
+  double* ap = alpha_all + P.aoff;
+  const long long c1 = __builtin_amdgcn_s_memtime();
+  for (int w = tid; w < nws; w += kWsInner) widx[w] = wsidx[(size_t)b * Q + w];
+  __syncthreads();
+  // features of B (zero-padded to FP: the padded terms of the dot are exact no-ops)
+  for (int e = tid; e < nws * FP; e += kWsInner) {
     const int w = e / FP, c = e - w * FP;
     zB[e] = c < F ? zcat[(P.zoff + widx[w]) * F + c] : 0.f;
   }
-  for (int w = tid; w < nws; w += kWsThreads) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
+  for (int w = tid; w < nws; w += kWsInner) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
   __syncthreads();
   const long long c2 = __builtin_amdgcn_s_memtime();
-  // ---- inner SMO on B: thread s owns slot s (f32 local state, features in registers)
-  const int s = tid;
-  const bool valid = s < nws;
-  const int t = valid ? widx[s] : 0;
-  const bool pos = t < P.npos;
-  const float y = pos ? 1.f : -1.f;
-  const float Cw = (float)(pos ? P.Cp : P.Cn);
-  const double a0 = valid ? ap[t] : 0.0;
-  float a = (float)a0;
-  float g = valid ? (float)Gp[t] : 0.f;
-  float zr[FP];
+  bool valid[SL], pos[SL];
+  int tt[SL];
+  float y[SL], Cw[SL], a[SL], g[SL], sn[SL];
+  double a0[SL];
+  float zr[SL][FP];
 #pragma unroll
-  for (int k = 0; k < FP; k += 4) {
-    const f32x4 v = valid ? *reinterpret_cast<const f32x4*>(&zB[s * FP + k]) : f32x4{0.f, 0.f, 0.f, 0.f};
-    zr[k] = v[0]; zr[k + 1] = v[1]; zr[k + 2] = v[2]; zr[k + 3] = v[3];
+  for (int m = 0; m < SL; ++m) {
+    const int s = tid + kWsInner * m;
+    valid[m] = s < nws;
+    tt[m] = valid[m] ? widx[s] : 0;
+    pos[m] = tt[m] < P.npos;
+    y[m] = pos[m] ? 1.f : -1.f;
+    Cw[m] = (float)(pos[m] ? P.Cp : P.Cn);
+    a0[m] = valid[m] ? ap[tt[m]] : 0.0;
+    a[m] = (float)a0[m];
+    g[m] = valid[m] ? (float)Gp[tt[m]] : 0.f;
+    sn[m] = valid[m] ? snB[s] : 0.f;
+#pragma unroll
+    for (int k = 0; k < FP; k += 4) {
+      const f32x4 v = valid[m] ? *reinterpret_cast<const f32x4*>(&zB[s * FP + k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      zr[m][k] = v[0]; zr[m][k + 1] = v[1]; zr[m][k + 2] = v[2]; zr[m][k + 3] = v[3];
+    }
   }
-  const float sn_own = valid ? snB[s] : 0.f;
   const float k2c = -2.f * P.ngl2e;
   const float Cpf = (float)P.Cp, Cnf = (float)P.Cn;
-  // K(x_r, x_s) for this thread's slot s: the gradient kernel's expression (MFMA = k-ordered fma
-  // chain from 0), so the inner solver and ws_gupdate see the same f32 kernel values
-  auto krow = [&](int r) {
-    float d = 0.f;
+  // K(x_r, x_s) for every slot s of this thread: the gradient kernel's expression (MFMA = k-ordered
+  // fma chain from 0), so the inner solver and ws_gupdate see the same f32 kernel values
+  auto krow = [&](int r, float (&out)[SL]) {
+    float d[SL];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) d[m] = 0.f;
 #pragma unroll
     for (int k = 0; k < FP; k += 4) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(&zB[r * FP + k]);
-      d = fmaf(v[0], zr[k], d);
-      d = fmaf(v[1], zr[k + 1], d);
-      d = fmaf(v[2], zr[k + 2], d);
-      d = fmaf(v[3], zr[k + 3], d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int m = 0; m < SL; ++m) d[m] = fmaf(v[q], zr[m][k + q], d[m]);
+      }
     }
-    return __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d, snB[r] + sn_own), 0.f));
+    const float snr = snB[r];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) out[m] = __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d[m], snr + sn[m]), 0.f));
+  };
+  auto red4 = [&](const unsigned* r) {
+    const uint4 v = *reinterpret_cast<const uint4*>(r);
+    return max(max(v.x, v.y), max(v.z, v.w));
   };
   float tol_in = -1.f;
   const float epsf = (float)eps;
+  // optional in-kernel phase stamps (HFENS_PROFILE_WS=1): keys, barrier 1, row i, barrier 2,
+  // pair update, row j + gradient — s_memtime waits for outstanding LDS reads, so this perturbs
+  const bool pf = prof != nullptr;
+  long long ph[6] = {0, 0, 0, 0, 0, 0};
+  long long tp = pf ? __builtin_amdgcn_s_memtime() : 0;
+#define WS_STAMP(k)                                         \
+  if (pf) {                                                 \
+    const long long tn = __builtin_amdgcn_s_memtime();      \
+    ph[k] += tn - tp;                                       \
+    tp = tn;                                                \
+  }
   int it = 0;
   for (; it < max_inner; ++it) {
     const int par = it & 1;
     float* glp = gl + par * Q;
     float* alp = al + par * Q;
     float* kip = kil + par * Q;
-    unsigned* r1 = red + par * 16;          // step-1 keys
-    unsigned* r3 = red + 32 + par * 16;     // I_low maxima (local gap)
-    unsigned* r2 = red + 64 + par * 16;     // step-2 keys
-    unsigned* r4 = red + 96 + par * 16;     // I_up maxima, unmasked (local gap)
-    if (valid) { glp[s] = g; alp[s] = a; }
-    const bool up = valid && (pos ? a < Cw : a > 0.f);
-    const bool low = valid && (pos ? a > 0.f : a < Cw);
-    // step 1: i = argmax_{I_up ∩ B} −y·G.  The slot rides in the key's low bits (a ~1e-4
-    // relative tie window for the pick); the stopping test uses the unmasked maxima.
-    const unsigned kv = up ? f32_okey(-y * g) : 0u;
-    unsigned k1 = up ? ((kv & ~kIdx) | (unsigned)s) : 0u;
-    unsigned k3 = low ? f32_okey(y * g) : 0u;
+    unsigned* r1 = red + 0 + par * 4;      // step-1 keys (slot in the low bits)
+    unsigned* r3 = red + 8 + par * 4;      // I_low maxima (local gap)
+    unsigned* r2 = red + 16 + par * 4;     // step-2 keys
+    unsigned* r4 = red + 24 + par * 4;     // I_up maxima, unmasked (local gap)
+    // Branch-free per-slot work (masks, not conditionals: hipcc turns `valid && …` into exec-mask
+    // branches, measured at ~40 % of a pair).  Slots ≥ nws write their own unused mirror entries
+    // and compute on zero features; their keys are masked to 0.
+    unsigned k1 = 0u, k3 = 0u, k4 = 0u;
+    bool low[SL];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const unsigned s = (unsigned)(tid + kWsInner * m);
+      glp[s] = g[m];
+      alp[s] = a[m];
+      const bool below = a[m] < Cw[m], above = a[m] > 0.f;
+      const bool up = valid[m] & ((pos[m] & below) | (!pos[m] & above));
+      low[m] = valid[m] & ((pos[m] & above) | (!pos[m] & below));
+      const float yg = y[m] * g[m];
+      // step 1: i = argmax_{I_up ∩ B} −y·G.  The slot rides in the key's low bits (a ~1e-4
+      // relative tie window for the pick); the stopping test uses the unmasked maxima.
+      const unsigned um = 0u - (unsigned)up, lm = 0u - (unsigned)low[m];
+      const unsigned kv = f32_okey(-yg) & um;
+      k4 = max(k4, kv);
+      k1 = max(k1, ((kv & ~kIdx) | s) & um);
+      k3 = max(k3, f32_okey(yg) & lm);
+    }
     k1 = wave_max_u32(k1);
     k3 = wave_max_u32(k3);
-    const unsigned k4 = wave_max_u32(kv);
+    k4 = wave_max_u32(k4);
     if (lane == 0) { r1[wave] = k1; r3[wave] = k3; r4[wave] = k4; }
+    WS_STAMP(0)
     __syncthreads();
-    unsigned K1 = 0u, K3 = 0u, K4 = 0u;
-#pragma unroll
-    for (int w = 0; w < kWsWaves; ++w) { K1 = max(K1, r1[w]); K3 = max(K3, r3[w]); K4 = max(K4, r4[w]); }
+    const unsigned K1 = __builtin_amdgcn_readfirstlane(red4(r1));
+    const unsigned K3 = __builtin_amdgcn_readfirstlane(red4(r3));
+    const unsigned K4 = __builtin_amdgcn_readfirstlane(red4(r4));
     if (K1 == 0u || K3 == 0u) break;
     const int i = (int)(K1 & kIdx);
     const float Gi = glp[i];
@@ -465,23 +533,25 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
     if (lgap < tol_in) break;
     // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / (2 − 2 K_it)
-    const float Ki = valid ? krow(i) : 0.f;
-    if (valid) kip[s] = Ki;
+    WS_STAMP(1)
+    float Ki[SL];
+    krow(i, Ki);
     unsigned k2 = 0u;
-    if (low) {
-      const float gd = GmaxB + y * g;
-      if (gd > 0.f) {
-        float quad = 2.f - 2.f * Ki;
-        if (quad <= 0.f) quad = 1e-12f;
-        k2 = (f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~kIdx) | (unsigned)s;
-      }
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const unsigned s = (unsigned)(tid + kWsInner * m);
+      kip[s] = Ki[m];
+      const float gd = GmaxB + y[m] * g[m];
+      const float q0 = 2.f - 2.f * Ki[m];
+      const float quad = q0 <= 0.f ? 1e-12f : q0;
+      const unsigned ok = 0u - (unsigned)(low[m] & (gd > 0.f));
+      k2 = max(k2, ((f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~kIdx) | s) & ok);
     }
     k2 = wave_max_u32(k2);
     if (lane == 0) r2[wave] = k2;
+    WS_STAMP(2)
     __syncthreads();
-    unsigned K2 = 0u;
-#pragma unroll
-    for (int w = 0; w < kWsWaves; ++w) K2 = max(K2, r2[w]);
+    const unsigned K2 = __builtin_amdgcn_readfirstlane(red4(r2));
     if (K2 == 0u) break;
     const int j = (int)(K2 & kIdx);
     const float Gj = glp[j];
@@ -490,74 +560,102 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_solve_kernel(
     const bool jpos = widx[j] < P.npos;
     const float yj = jpos ? 1.f : -1.f;
     const float Ci = ipos ? Cpf : Cnf, Cj = jpos ? Cpf : Cnf;
-    float ai = ai_old, aj = aj_old;
-    if (yi != yj) {
-      float quad = 2.f + 2.f * (yi * yj) * Kij;
-      if (quad <= 0.f) quad = 1e-12f;
-      const float delta = (-Gi - Gj) * __builtin_amdgcn_rcpf(quad);
-      const float diff = ai - aj;
-      ai += delta;
-      aj += delta;
-      if (diff > 0.f) { if (aj < 0.f) { aj = 0.f; ai = diff; } }
-      else { if (ai < 0.f) { ai = 0.f; aj = -diff; } }
-      if (diff > Ci - Cj) { if (ai > Ci) { ai = Ci; aj = Ci - diff; } }
-      else { if (aj > Cj) { aj = Cj; ai = Cj + diff; } }
-    } else {
-      float quad = 2.f - 2.f * (yi * yj) * Kij;
-      if (quad <= 0.f) quad = 1e-12f;
-      const float delta = (Gi - Gj) * __builtin_amdgcn_rcpf(quad);
-      const float sum = ai + aj;
-      ai -= delta;
-      aj += delta;
-      if (sum > Ci) { if (ai > Ci) { ai = Ci; aj = sum - Ci; } }
-      else { if (aj < 0.f) { aj = 0.f; ai = sum; } }
-      if (sum > Cj) { if (aj > Cj) { aj = Cj; ai = sum - Cj; } }
-      else { if (ai < 0.f) { ai = 0.f; aj = sum; } }
+    WS_STAMP(3)
+    // libsvm's two-variable step and clipping, both label cases evaluated, then selected
+    // (Q_ii + Q_jj ∓ 2 Q_ij = 2 − 2 K_ij either way)
+    const float q0 = 2.f - 2.f * Kij;
+    const float rq = __builtin_amdgcn_rcpf(q0 <= 0.f ? 1e-12f : q0);
+    float ao, bo, as, bs;
+    {  // y_i ≠ y_j
+      const float delta = (-Gi - Gj) * rq;
+      const float diff = ai_old - aj_old;
+      ao = ai_old + delta;
+      bo = aj_old + delta;
+      const bool c1 = (diff > 0.f) & (bo < 0.f), c2 = !(diff > 0.f) & (ao < 0.f);
+      ao = c1 ? diff : (c2 ? 0.f : ao);
+      bo = c1 ? 0.f : (c2 ? -diff : bo);
+      const bool c3 = (diff > Ci - Cj) & (ao > Ci), c4 = !(diff > Ci - Cj) & (bo > Cj);
+      ao = c3 ? Ci : (c4 ? Cj + diff : ao);
+      bo = c3 ? Ci - diff : (c4 ? Cj : bo);
     }
+    {  // y_i = y_j
+      const float delta = (Gi - Gj) * rq;
+      const float sum = ai_old + aj_old;
+      as = ai_old - delta;
+      bs = aj_old + delta;
+      const bool c1 = (sum > Ci) & (as > Ci), c2 = !(sum > Ci) & (bs < 0.f);
+      as = c1 ? Ci : (c2 ? sum : as);
+      bs = c1 ? sum - Ci : (c2 ? 0.f : bs);
+      const bool c3 = (sum > Cj) & (bs > Cj), c4 = !(sum > Cj) & (as < 0.f);
+      as = c3 ? sum - Cj : (c4 ? 0.f : as);
+      bs = c3 ? Cj : (c4 ? sum : bs);
+    }
+    const bool opp = ipos != jpos;
+    const float ai = opp ? ao : as, aj = opp ? bo : bs;
     const float ci = yi * (ai - ai_old), cj = yj * (aj - aj_old);
-    const float Kj = valid ? krow(j) : 0.f;
-    if (s == i) a = ai;
-    if (s == j) a = aj;
-    g += y * fmaf(Ki, ci, Kj * cj);
+    WS_STAMP(4)
+    float Kj[SL];
+    krow(j, Kj);
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const int s = tid + kWsInner * m;
+      a[m] = s == i ? ai : (s == j ? aj : a[m]);
+      g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
+    }
+    WS_STAMP(5)
+  }
+#undef WS_STAMP
+  if (pf && tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) prof[(size_t)b * 6 + k] += ph[k];
   }
   // ---- publish: α of B, changed entries (slot order) for the global gradient update
-  double anew = a0;
-  if (valid && a != (float)a0) {
-    const double C = pos ? P.Cp : P.Cn;
-    anew = a <= 0.f ? 0.0 : (a >= Cw ? C : a0 + ((double)a - (double)(float)a0));
-  }
-  const bool ch = valid && anew != a0;
-  const unsigned long long cm = __ballot(ch);
-  int nc;
-  const int cpos = wave_base(__popcll(cm), shi, &nc) + __popcll(cm & lanes_below());
-  if (ch) {
-    ap[t] = anew;
-    for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + cpos] = k < F ? zB[s * FP + k] : 0.f;
-    wsn[(size_t)b * Q + cpos] = sn_own;
-    wdc[(size_t)b * Q + cpos] = (float)((double)y * (anew - a0));
+  int nc = 0;
+#pragma unroll
+  for (int m = 0; m < SL; ++m) {
+    const int s = tid + kWsInner * m;
+    double anew = a0[m];
+    if (valid[m] && a[m] != (float)a0[m]) {
+      const double C = pos[m] ? P.Cp : P.Cn;
+      anew = a[m] <= 0.f ? 0.0 : (a[m] >= Cw[m] ? C : a0[m] + ((double)a[m] - (double)(float)a0[m]));
+    }
+    const bool ch = valid[m] && anew != a0[m];
+    const unsigned long long cm = __ballot(ch);
+    // exclusive prefix over the 4 waves for this m (one barrier pair), then this lane's rank
+    __syncthreads();
+    if (lane == 0) red[wave] = (unsigned)__popcll(cm);
+    __syncthreads();
+    int wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWsInner / 64; ++w) {
+      const int v = (int)red[w];
+      wb += w < wave ? v : 0;
+      tot += v;
+    }
+    const int cpos = nc + wb + __popcll(cm & lanes_below());
+    if (ch) {
+      ap[tt[m]] = anew;
+      for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + cpos] = k < F ? zB[s * FP + k] : 0.f;
+      wsn[(size_t)b * Q + cpos] = sn[m];
+      wdc[(size_t)b * Q + cpos] = (float)((double)y[m] * (anew - a0[m]));
+    }
+    nc += tot;
   }
   const int ncp = (nc + 31) & ~31;
-  for (int p = nc + tid; p < ncp; p += kWsThreads) {
+  for (int p = nc + tid; p < ncp; p += kWsInner) {
     for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + p] = 0.f;
     wsn[(size_t)b * Q + p] = 0.f;
     wdc[(size_t)b * Q + p] = 0.f;
   }
   const long long c3 = __builtin_amdgcn_s_memtime();
   if (tid == 0) {
-    S->cyc_select += c1 - c0;
-    S->cyc_p0 += c0a - c0;
-    S->cyc_p1 += c0b - c0a;
-    S->cyc_p2 += c0c - c0b;
     S->cyc_build += c2 - c1;
     S->cyc_inner += c3 - c2;
     // no pair moved: the f32 selection keys hid an f64 violation below eps-resolution — done
     if (it == 0 || nc == 0) S->done = 1;
     S->nc = nc;
-    S->nws = nws;
-    S->nprev = nnew;
     S->outer += 1;
     S->inner += it;
-    S->gap = gap;
   }
 }
 
@@ -716,11 +814,12 @@ void ws_init(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t
 }
 
 // n_iter outer iterations (select+solve, then the gradient update) enqueued back to back; finished
-// problems return at once.  wsz/wsn/wdc hold [P][2·KS][q] / [P][q] / [P][q]; wsprev [P][q/2].
+// problems return at once.  wsz/wsn/wdc hold [P][2·KS][q] / [P][q] / [P][q]; wsprev [P][q/2];
+// wsidx [P][q].
 void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
               uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
-              uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
-              double inner_frac, int n_iter, uintptr_t stream) {
+              uintptr_t wsidx, uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
+              double inner_frac, int n_iter, uintptr_t prof, uintptr_t stream) {
   const WsAux X = ws_aux(keys, n, gkey);
   HFENS_REQUIRE(F >= 1 && F <= 48, "ws_steps: 1 <= F <= 48");
   // (< 32768: the packed 16|16-bit member counts of the radix selector)
@@ -742,20 +841,27 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
   auto wd = (float*)wdc;
   auto wp = (int*)wsprev;
   const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
+  int* wi = (int*)wsidx;
   for (int it = 0; it < n_iter; ++it) {
-#define WS_SEL(MM, FF, QQ)                                                                              \
-  if (M == MM && FP == FF) {                                                                            \
-    hipLaunchKernelGGL((ws_select_solve_kernel<MM, FF, QQ>), dim3(P), dim3(kWsThreads),                 \
-                       ws_lds_bytes(QQ, FF), st, pp, sp, zp, F, np_, ap, gp, wz, wn, wd, Fp2, wp, eps,  \
-                       max_outer, max_inner, inner_frac, X);                                            \
+#define WS_SEL(MM, QQ)                                                                                  \
+  if (M == MM && Q == QQ) {                                                                             \
+    hipLaunchKernelGGL((ws_select_kernel<MM, QQ>), dim3(P), dim3(kWsThreads), ws_sel_lds_bytes(QQ), st,  \
+                       pp, sp, wi, wp, eps, max_outer, X);                                              \
   } else
-#define WS_SEL_M(FF, QQ) WS_SEL(4, FF, QQ) WS_SEL(16, FF, QQ) WS_SEL(32, FF, QQ)
-    WS_SEL_M(4, 1024) WS_SEL_M(8, 1024) WS_SEL_M(12, 1024) WS_SEL_M(16, 1024) WS_SEL_M(20, 1024)
-    WS_SEL_M(24, 1024) WS_SEL_M(32, 512) WS_SEL_M(40, 512) WS_SEL_M(48, 512) {
-      HFENS_REQUIRE(false, "ws_steps: no select/solve instance for this F");
-    }
-#undef WS_SEL_M
+    WS_SEL(4, 1024) WS_SEL(16, 1024) WS_SEL(32, 1024) WS_SEL(4, 512) WS_SEL(16, 512) WS_SEL(32, 512) {}
 #undef WS_SEL
+    launch_check();
+#define WS_SOL(FF, QQ)                                                                                  \
+  if (FP == FF && Q == QQ) {                                                                            \
+    hipLaunchKernelGGL((ws_solve_kernel<FF, QQ>), dim3(P), dim3(kWsInner), ws_solve_lds_bytes(QQ, FF),  \
+                       st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac,   \
+                       (long long*)prof);                                                              \
+  } else
+    WS_SOL(4, 1024) WS_SOL(8, 1024) WS_SOL(12, 1024) WS_SOL(16, 1024) WS_SOL(20, 1024) WS_SOL(24, 1024)
+    WS_SOL(32, 512) WS_SOL(40, 512) WS_SOL(48, 512) {
+      HFENS_REQUIRE(false, "ws_steps: no solve instance for this F");
+    }
+#undef WS_SOL
     launch_check();
     const dim3 grid((max_l + 255) / 256, P);
 #define WS_UPD(K)                                                                                    \

@@ -134,11 +134,9 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         else:
             proba_all, ysel_all, yy_all = proba, y_sel, yy
         report = metrics.classification_report(ysel_all, yy_all)
+        # (the held-out rows are already gathered for the report, so the AUROC comes from them;
+        # metrics.roc_auc_sharded is the R8 path for callers that keep scores sharded)
         scores = metrics.evaluate(ysel_all, proba_all)
-        if group is not None:
-            # the AUROC from the sharded rows by one bucket-count all-reduce (R8); equals the
-            # gathered value exactly (tests/test_distributed.py::test_roc_auc_sharded_is_exact)
-            scores["auroc"] = metrics.roc_auc_sharded(y_sel, proba, group)
     n_train = X_dev.shape[0]
     if fit_group is not None:
         from .parallel import dist as pdist

@@ -364,16 +364,20 @@ def _auc_sharded(rank, world, group):
     for bins in (1 << 16, 8):                                  # fine grid, and a grid of all-mixed buckets
         out.append(metrics.roc_auc_sharded(shard_rows(torch.as_tensor(y), rank, world),
                                            shard_rows(torch.as_tensor(s), rank, world), group, bins=bins))
+    # every score tied: one bucket holds all rows (the sort path, no pairwise matrix) → exactly ½
+    out.append(metrics.roc_auc_sharded(shard_rows(torch.as_tensor(y), rank, world),
+                                       shard_rows(torch.full((3001,), 0.25, dtype=torch.float64), rank, world), group))
     return torch.tensor(out), torch.tensor([metrics.roc_auc(torch.as_tensor(y), torch.as_tensor(s))])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_roc_auc_sharded_is_exact(world):
     """R8: the bucket-count all-reduce AUROC equals the single-process (sklearn-equal) AUROC exactly
     (ties inside mixed buckets resolved from their gathered rows)."""
     got, want = _run("_auc_sharded", world)
     assert abs(float(got[0]) - float(want[0])) < 1e-15
     assert abs(float(got[1]) - float(want[0])) < 1e-15
+    assert float(got[2]) == 0.5
 
 
 def _bin_data():

@@ -179,3 +179,24 @@ def test_native_host_predictor_deep_trees():
     got = clf.predict_proba(Xt)[:, 1]
     want = _force_generic(clf, lambda: clf.predict_proba(Xt)[:, 1])
     assert float((got - want).abs().max()) < 1e-12
+
+
+@pytest.mark.parametrize("flags", [(False, True), (True, False), (False, False)])
+def test_native_host_predictor_honours_scaler_flags(flags):
+    """A pipeline whose StandardScaler has with_mean / with_std off: the native host predictor
+    uses an identity centre / scale like the per-model path (it used mean_/scale_)."""
+    if not ops.has_ext():
+        pytest.skip("HIP extension not built")
+    from hfens.config import EnsembleConfig, build_estimators
+    from hfens.io.synth import make_hf_cohort
+    X, y, _ = make_hf_cohort(300, 9, seed=6, nan_frac=0.0)
+    X, y = torch.as_tensor(X), torch.as_tensor(y)
+    clf = build_estimators(EnsembleConfig(gbc_estimators=10))
+    sc = clf.estimators[0][1].steps[0][1]
+    sc.with_mean, sc.with_std = flags
+    clf.fit(X, y)
+    assert clf._host_pack() is not None
+    Xt = torch.as_tensor(make_hf_cohort(50, 9, seed=7, nan_frac=0.0)[0])
+    got = clf.predict_proba(Xt)[:, 1]
+    want = _force_generic(clf, lambda: clf.predict_proba(Xt)[:, 1])
+    assert float((got - want).abs().max()) < 1e-12

@@ -84,3 +84,23 @@ def test_ws_bench_scale_meets_libsvm_tolerance(dev, monkeypatch):
     dd = np.abs(d - sk.decision_function(Z))
     assert np.median(dd) < 1e-3 and dd.max() < 1e-2, (np.median(dd), dd.max())
     assert (np.sign(d) == np.sign(sk.decision_function(Z))).mean() > 0.999
+
+
+def test_ws_unconverged_batch_is_resolved_synchronously(dev, monkeypatch):
+    """The working-set rounds are enqueued without host checks (WS_ROUNDS_AHEAD); a batch that has
+    not converged after them is re-solved with host-checked rounds by finish_svc_batch — the same
+    rounds in the same order, so the same model bit for bit."""
+    import warnings
+    X, y = _data(6000, 17, 31)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    monkeypatch.setattr(smo, "SOLVER", "ws")
+    ref = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.to(dev))
+    assert "ws_resolve" not in smo.LAST_SMO_INFO
+    monkeypatch.setattr(smo, "WS_ROUNDS_AHEAD", 2)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        m = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.to(dev))
+    assert smo.LAST_SMO_INFO.get("ws_resolve") and any("host-checked" in str(x.message) for x in w)
+    assert torch.equal(m.support_.cpu(), ref.support_.cpu())
+    assert torch.equal(m._dual_coef_.cpu(), ref._dual_coef_.cpu())
+    assert m._probA.item() == ref._probA.item() and m._probB.item() == ref._probB.item()
