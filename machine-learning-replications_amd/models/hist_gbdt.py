@@ -246,6 +246,7 @@ class _State:
     bagw: Optional[torch.Tensor] = None    # [T, B] Σ in-bag weight per stage (train_score_ norm.)
     frank: Optional[torch.Tensor] = None   # [T, B, F] int32 tie-break rank (sklearn visit order)
     reduced: bool = False                  # r2 / dev / bagw already global (stage path)
+    peer: Optional[object] = None          # parallel.xgmi.PeerComm used by the stage loop
 
     @property
     def wcur(self) -> torch.Tensor:
@@ -354,6 +355,8 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         _run_host(st, group)
     hmark("gbc_enqueued")
     check_finite(st.value, "GBDT leaf values")
+    if getattr(st, "peer", None) is not None:
+        st.peer.check()     # (after the guard's host read: no extra synchronisation point)
     _finish(models, st, sw, p1, group)
     return models
 
@@ -527,13 +530,13 @@ GRAPH_INFO: dict = {}
 _GRAPH_KEEP: list = []
 
 
-def _graph_units(st, group, prof) -> int:
+def _graph_units(st, group, prof, peer=None) -> int:
     if STAGE_GRAPH == "0" or prof is not None or st.T + 2 < GRAPH_MIN_STAGES:
         return 0
     if group is not None:
         import torch.distributed as dist
-        if dist.get_backend(group) != "nccl":
-            return 0
+        if peer is None and dist.get_backend(group) != "nccl":
+            return 0     # gloo collectives cannot be captured; peer kernels and RCCL can
     elif STAGE_GRAPH != "1":
         return 0     # single process: the eager loop is GPU-bound already (measured), keep it
     # units of 3 stages t ≡ 0, 1, 2 (mod 3) while every stage of the unit still all-reduces (t ≤ T)
@@ -580,7 +583,14 @@ def _run_stage(st: _State, group):
     plen = st.B * groups * (3 * hist_len + 8)
     partials = runtime.workspace(dev, "gbdt_stage_partials", plen, torch.int64)
     prof = torch.zeros(st.B * groups * 6, dtype=torch.int64, device=dev) if PROFILE_STAGE_T >= 0 else None
-    n_coll = [0]
+    n_coll, n_xg = [0], [0]
+    # data parallel: the per-stage int64 sum goes through IPC-mapped peer buffers (one kernel, no
+    # RCCL call, no host round trip: parallel/xgmi.py) when the ranks share a node, else RCCL
+    peer = None
+    if group is not None and dev.type == "cuda":
+        from ..parallel import xgmi
+        peer = xgmi.peer_comm(group, dev, slot)
+    base = peer.epoch if peer is not None else 0
 
     def stage(t, host_t, t_dev=None):
         E.gbdt_stump_stage(host_t, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
@@ -598,12 +608,18 @@ def _run_stage(st: _State, group):
             # stage t's histogram + root Σw r² + previous tree's leaf Σw r² + deviance + bag count:
             # ONE exact int64 SUM per stage (SURVEY.md §5.8 R1/R2 merged)
             k = host_t % 3
-            import torch.distributed as dist
-            dist.all_reduce(comm[k * slot:(k + 1) * slot], op=dist.ReduceOp.SUM, group=group)
-            n_coll[0] += 1
+            if peer is not None:
+                peer.allreduce_(comm[k * slot:(k + 1) * slot], k, t, t_dev, epoch_base=base, stream=s)
+                n_xg[0] += 1
+            else:
+                import torch.distributed as dist
+                dist.all_reduce(comm[k * slot:(k + 1) * slot], op=dist.ReduceOp.SUM, group=group)
+                n_coll[0] += 1
 
     t0 = time.perf_counter()
-    units = _graph_units(st, group, prof)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    units = _graph_units(st, group, prof, peer)
     if units:
         # HIP graph of one 3-stage unit (stage kernel [+ partial reduce] + counter tick [+ the
         # stage's all-reduce], × 3 — the comm slots rotate with period 3), captured once per fit
@@ -626,7 +642,8 @@ def _run_stage(st: _State, group):
         s = ops.stream_ptr(dev)
         for _ in range(units):
             g.replay()
-        n_coll[0] = 3 * units if group is not None else 0   # the capture issued one unit's worth
+        if group is not None:   # the capture issued one unit's worth
+            (n_xg if peer is not None else n_coll)[0] = 3 * units
         GRAPH_INFO.update(units=units, nodes_per_unit=3, stages_eager=st.T + 2 - 3 * units)
         start = 3 * units
         keep_graph = g
@@ -637,6 +654,9 @@ def _run_stage(st: _State, group):
     for t in range(start, st.T + 2):
         stage(t, t)
     GRAPH_INFO["host_s"] = time.perf_counter() - t0
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev1.record()
+    GRAPH_INFO["loop_events"] = (ev0, ev1)   # device time of the stage loop (read after a sync)
     if keep_graph is not None:
         # the graph's launches must not outlive it: keep it referenced until the work is done
         _GRAPH_KEEP.append((keep_graph, torch.cuda.Event()))
@@ -644,6 +664,10 @@ def _run_stage(st: _State, group):
         _prune_graphs()
     n_coll = n_coll[0]
     COLLECTIVES["per_stage"] = n_coll / (st.T + 1) if group is not None else 0.0
+    COLLECTIVES["xgmi_per_stage"] = n_xg[0] / (st.T + 1) if group is not None else 0.0
+    if peer is not None:
+        peer.advance(st.T + 2)
+        st.peer = peer
     if prof is not None:
         LAST_STAGE_PROF["stamps"] = prof.view(-1, 6).cpu().numpy()
     st.reduced = True      # r2 / dev / bagw were booked from the all-reduced slots

@@ -583,6 +583,7 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
 WS_INNER_PER_Q = int(os.environ.get("HFENS_SVM_WS_INNER", "4"))        # inner pair cap = this × q
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
+WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
@@ -624,7 +625,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
                    wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
-                   min(WS_ROUNDS_AHEAD, max_outer), wprof.data_ptr() if wprof is not None else 0, s)
+                   min(WS_ROUNDS_AHEAD, max_outer), wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
         err = (done_view == 0).any().to(torch.int32).reshape(1)
     else:
         outer = 0
@@ -634,7 +635,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                        states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
                        wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
-                       chunk, wprof.data_ptr() if wprof is not None else 0, s)
+                       chunk, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
             outer += chunk
             chunk = steps_per_check or 8
             if bool((done_view != 0).all()):

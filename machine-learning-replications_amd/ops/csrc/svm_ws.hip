@@ -372,25 +372,25 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
   }
 }
 
-// ---- ws_solve: the inner SMO on B (one 256-thread workgroup per problem) -----------------------
-// Four waves, SL = Q/256 slots per thread (slot s = tid + 256·m), each slot's features in
+// ---- ws_solve: the inner SMO on B (one TH-thread workgroup per problem) ------------------------
+// TH/64 waves, SL = Q/TH slots per thread (slot s = tid + TH·m), each slot's features in
 // registers.  LDS: reduction slots (4 keys × 2 parities × 4 waves), z_B [Q][FP] f32, γ'‖z‖² [Q],
 // widx [Q], and per-slot mirrors of g, α and K(x_i,·), 2 parities each (a slot is read by every
 // thread after the barrier that follows its write, and rewritten only two barriers later).
-constexpr int kWsInner = 256;
 constexpr size_t ws_solve_lds_bytes(int Q, int FP) {
-  return 32 * 4 * 2 + (size_t)Q * FP * 4 + (size_t)Q * 4 * 2 + (size_t)6 * Q * 4;
+  return 64 * 4 + (size_t)Q * FP * 4 + (size_t)Q * 4 * 2 + (size_t)6 * Q * 4;
 }
 
-template <int FP, int Q>
-__global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
+template <int FP, int Q, int TH>
+__global__ __launch_bounds__(TH) void ws_solve_kernel(
     const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
     const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
     const int* __restrict__ wsidx, float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc,
     int Fp2, double eps, int max_inner, double inner_frac, long long* __restrict__ prof) {
-  static_assert(Q % kWsInner == 0 && (Q & (Q - 1)) == 0, "whole slots per thread, power of two");
+  static_assert(Q % TH == 0 && (Q & (Q - 1)) == 0 && TH % 64 == 0 && TH <= 512, "whole slots per thread");
   static_assert(FP % 4 == 0, "z rows are read as float4");
-  constexpr int SL = Q / kWsInner;
+  constexpr int SL = Q / TH;
+  constexpr int NW = TH / 64;        // waves
   constexpr unsigned kIdx = Q - 1;   // slot bits packed under the selection keys
   const int b = blockIdx.x;
   WsState* S = states + b;
@@ -400,8 +400,8 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
-  unsigned* red = reinterpret_cast<unsigned*>(ws_lds);            // [4 keys][2 parities][4 waves]
-  float* zB = reinterpret_cast<float*>(ws_lds + 32 * 4 * 2);       // [Q][FP]
+  unsigned* red = reinterpret_cast<unsigned*>(ws_lds);            // [4 keys][2 parities][NW ≤ 8 waves]
+  float* zB = reinterpret_cast<float*>(ws_lds + 64 * 4);       // [Q][FP]
   float* snB = zB + (size_t)Q * FP;                                 // [Q]
   int* widx = reinterpret_cast<int*>(snB + Q);                      // [Q]
   float* gl = reinterpret_cast<float*>(widx + Q);                   // [2][Q]
@@ -410,14 +410,14 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
   const double* Gp = G_all + P.aoff;
   double* ap = alpha_all + P.aoff;
   const long long c1 = __builtin_amdgcn_s_memtime();
-  for (int w = tid; w < nws; w += kWsInner) widx[w] = wsidx[(size_t)b * Q + w];
+  for (int w = tid; w < nws; w += TH) widx[w] = wsidx[(size_t)b * Q + w];
   __syncthreads();
   // features of B (zero-padded to FP: the padded terms of the dot are exact no-ops)
-  for (int e = tid; e < nws * FP; e += kWsInner) {
+  for (int e = tid; e < nws * FP; e += TH) {
     const int w = e / FP, c = e - w * FP;
     zB[e] = c < F ? zcat[(P.zoff + widx[w]) * F + c] : 0.f;
   }
-  for (int w = tid; w < nws; w += kWsInner) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
+  for (int w = tid; w < nws; w += TH) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
   __syncthreads();
   const long long c2 = __builtin_amdgcn_s_memtime();
   bool valid[SL], pos[SL];
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
   float zr[SL][FP];
 #pragma unroll
   for (int m = 0; m < SL; ++m) {
-    const int s = tid + kWsInner * m;
+    const int s = tid + TH * m;
     valid[m] = s < nws;
     tt[m] = valid[m] ? widx[s] : 0;
     pos[m] = tt[m] < P.npos;
@@ -464,9 +464,14 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
 #pragma unroll
     for (int m = 0; m < SL; ++m) out[m] = __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d[m], snr + sn[m]), 0.f));
   };
-  auto red4 = [&](const unsigned* r) {
-    const uint4 v = *reinterpret_cast<const uint4*>(r);
-    return max(max(v.x, v.y), max(v.z, v.w));
+  auto red4 = [&](const unsigned* r) {   // max over the NW waves' slots (uint4 reads)
+    unsigned x = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; w += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(r + w);
+      x = max(max(x, max(v.x, v.y)), max(v.z, v.w));
+    }
+    return x;
   };
   float tol_in = -1.f;
   const float epsf = (float)eps;
@@ -487,10 +492,10 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     float* glp = gl + par * Q;
     float* alp = al + par * Q;
     float* kip = kil + par * Q;
-    unsigned* r1 = red + 0 + par * 4;      // step-1 keys (slot in the low bits)
-    unsigned* r3 = red + 8 + par * 4;      // I_low maxima (local gap)
-    unsigned* r2 = red + 16 + par * 4;     // step-2 keys
-    unsigned* r4 = red + 24 + par * 4;     // I_up maxima, unmasked (local gap)
+    unsigned* r1 = red + (0 * 2 + par) * NW;   // step-1 keys (slot in the low bits)
+    unsigned* r3 = red + (1 * 2 + par) * NW;   // I_low maxima (local gap)
+    unsigned* r2 = red + (2 * 2 + par) * NW;   // step-2 keys
+    unsigned* r4 = red + (3 * 2 + par) * NW;   // I_up maxima, unmasked (local gap)
     // Branch-free per-slot work (masks, not conditionals: hipcc turns `valid && …` into exec-mask
     // branches, measured at ~40 % of a pair).  Slots ≥ nws write their own unused mirror entries
     // and compute on zero features; their keys are masked to 0.
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     bool low[SL];
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
-      const unsigned s = (unsigned)(tid + kWsInner * m);
+      const unsigned s = (unsigned)(tid + TH * m);
       glp[s] = g[m];
       alp[s] = a[m];
       const bool below = a[m] < Cw[m], above = a[m] > 0.f;
@@ -539,7 +544,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     unsigned k2 = 0u;
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
-      const unsigned s = (unsigned)(tid + kWsInner * m);
+      const unsigned s = (unsigned)(tid + TH * m);
       kip[s] = Ki[m];
       const float gd = GmaxB + y[m] * g[m];
       const float q0 = 2.f - 2.f * Ki[m];
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     krow(j, Kj);
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
-      const int s = tid + kWsInner * m;
+      const int s = tid + TH * m;
       a[m] = s == i ? ai : (s == j ? aj : a[m]);
       g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
     }
@@ -613,7 +618,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
   int nc = 0;
 #pragma unroll
   for (int m = 0; m < SL; ++m) {
-    const int s = tid + kWsInner * m;
+    const int s = tid + TH * m;
     double anew = a0[m];
     if (valid[m] && a[m] != (float)a0[m]) {
       const double C = pos[m] ? P.Cp : P.Cn;
@@ -627,7 +632,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     __syncthreads();
     int wb = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kWsInner / 64; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const int v = (int)red[w];
       wb += w < wave ? v : 0;
       tot += v;
@@ -642,7 +647,7 @@ __global__ __launch_bounds__(kWsInner) void ws_solve_kernel(
     nc += tot;
   }
   const int ncp = (nc + 31) & ~31;
-  for (int p = nc + tid; p < ncp; p += kWsInner) {
+  for (int p = nc + tid; p < ncp; p += TH) {
     for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + p] = 0.f;
     wsn[(size_t)b * Q + p] = 0.f;
     wdc[(size_t)b * Q + p] = 0.f;
@@ -819,7 +824,7 @@ void ws_init(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t
 void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
               uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
               uintptr_t wsidx, uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
-              double inner_frac, int n_iter, uintptr_t prof, uintptr_t stream) {
+              double inner_frac, int n_iter, uintptr_t prof, int inner_threads, uintptr_t stream) {
   const WsAux X = ws_aux(keys, n, gkey);
   HFENS_REQUIRE(F >= 1 && F <= 48, "ws_steps: 1 <= F <= 48");
   // (< 32768: the packed 16|16-bit member counts of the radix selector)
@@ -842,6 +847,7 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
   auto wp = (int*)wsprev;
   const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
   int* wi = (int*)wsidx;
+  const int TH = inner_threads == 512 ? 512 : 256;
   for (int it = 0; it < n_iter; ++it) {
 #define WS_SEL(MM, QQ)                                                                                  \
   if (M == MM && Q == QQ) {                                                                             \
@@ -853,9 +859,14 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
     launch_check();
 #define WS_SOL(FF, QQ)                                                                                  \
   if (FP == FF && Q == QQ) {                                                                            \
-    hipLaunchKernelGGL((ws_solve_kernel<FF, QQ>), dim3(P), dim3(kWsInner), ws_solve_lds_bytes(QQ, FF),  \
-                       st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac,   \
-                       (long long*)prof);                                                              \
+    if (TH == 512)                                                                                      \
+      hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, 512>), dim3(P), dim3(512), ws_solve_lds_bytes(QQ, FF), \
+                         st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, \
+                         (long long*)prof);                                                            \
+    else                                                                                                \
+      hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, 256>), dim3(P), dim3(256), ws_solve_lds_bytes(QQ, FF), \
+                         st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, \
+                         (long long*)prof);                                                            \
   } else
     WS_SOL(4, 1024) WS_SOL(8, 1024) WS_SOL(12, 1024) WS_SOL(16, 1024) WS_SOL(20, 1024) WS_SOL(24, 1024)
     WS_SOL(32, 512) WS_SOL(40, 512) WS_SOL(48, 512) {

@@ -58,6 +58,8 @@ def rank_device() -> torch.device:
 
 def shutdown():
     if dist.is_initialized():
+        from . import xgmi
+        xgmi.release_all()
         dist.destroy_process_group()
 
 

@@ -1,0 +1,162 @@
+"""Peer-memory ("one-shot xGMI") all-reduce of int64 payloads between the ranks of one node
+(the per-stage GBDT histograms are ~50 KB per model — latency-bound, where an
+RCCL ring pays ≈130 µs per call even at world 1, profiles/r2_runs/stage_graph_overhead_125k.log).
+
+Each rank allocates one uncached device buffer (``ops/csrc/xgmi.hip`` layout: recv[W][3][cap]
+int64 + flags) and exchanges its IPC handle once over the process group; every rank maps every
+other rank's buffer (``hipIpcOpenMemHandle``, lazy peer access over xGMI).  A reduction is then ONE
+kernel on the caller's stream — push the local payload into every peer, flag it, wait for the
+peers' flags, sum — so it can sit inside a captured HIP graph and costs no host round trip and no
+RCCL call.  Integer sums make it bit-identical to ``torch.distributed.all_reduce``.
+
+The same code serves ranks on different GPUs (peer access over xGMI) and several ranks sharing
+one GPU (tests: IPC mappings of the same device).  Handles are exchanged with
+``all_gather_object`` (gloo or nccl); ranks on different hosts cannot map each other, so
+:func:`peer_comm` returns None there and callers keep RCCL.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+CHUNK = 2048          # int64 per block of xgmi_allreduce_kernel (ops/csrc/xgmi.hip kXgChunk)
+MAX_RANKS = 16
+MODE = os.environ.get("HFENS_XGMI", "auto")    # "auto" | "0" (RCCL only) | "1" (require)
+TIMEOUT_S = float(os.environ.get("HFENS_XGMI_TIMEOUT", "5"))
+UNCACHED = os.environ.get("HFENS_XGMI_UNCACHED", "1") != "0"
+
+
+def buffer_bytes(W: int, cap: int) -> int:
+    nchunk = -(-cap // CHUNK)
+    return W * 3 * cap * 8 + (-(-(3 * W * nchunk * 4) // 256)) * 256
+
+
+class PeerComm:
+    """IPC-mapped peer buffers of a process group; ``allreduce_`` sums int64 slots in place."""
+
+    def __init__(self, group, device, cap: int):
+        import torch.distributed as dist
+        from .. import ops
+        self.E = E = ops.ext()
+        self.group = group
+        self.W, self.me = dist.get_world_size(group), dist.get_rank(group)
+        self.device = torch.device(device)
+        self.cap = int(cap) + (int(cap) & 1)
+        self.epoch = 0            # stage sequence number (identical on every rank)
+        out = np.zeros(1, dtype=np.uint64)
+        with torch.cuda.device(self.device):
+            h = np.zeros(64, dtype=np.uint8)
+            self.uncached = UNCACHED
+            E.xgmi_alloc(buffer_bytes(self.W, self.cap), int(self.uncached), out.ctypes.data)
+            self.own = int(out[0])
+            try:
+                E.xgmi_ipc_handle(self.own, h.ctypes.data)
+            except RuntimeError:
+                if not self.uncached:
+                    raise
+                # no IPC handle for uncached memory on this driver: plain device memory (the
+                # kernel's system-scope fences then order the hand-off through the caches)
+                E.xgmi_free(self.own)
+                self.uncached = False
+                E.xgmi_alloc(buffer_bytes(self.W, self.cap), 0, out.ctypes.data)
+                self.own = int(out[0])
+                E.xgmi_ipc_handle(self.own, h.ctypes.data)
+            handles = [None] * self.W
+            dist.all_gather_object(handles, h.tobytes(), group=group)
+            ptrs, self.opened = [], []
+            for r, hb in enumerate(handles):
+                if r == self.me:
+                    ptrs.append(self.own)
+                    continue
+                hh = np.frombuffer(hb, dtype=np.uint8).copy()
+                E.xgmi_ipc_open(hh.ctypes.data, out.ctypes.data)
+                ptrs.append(int(out[0]))
+                self.opened.append(int(out[0]))
+        self.peers = torch.tensor(np.array(ptrs, dtype=np.uint64).view(np.int64), device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        dist.barrier(group=group)   # every mapping exists before anyone writes into it
+
+    def allreduce_(self, t: torch.Tensor, k: int, t_host: int, t_dev: Optional[torch.Tensor] = None,
+                   epoch_base: Optional[int] = None, stream: Optional[int] = None):
+        """Sum the int64 tensor ``t`` (≤ cap elements) over the ranks, in place, on the current
+        stream; ``k`` = stage % 3 (slot), epoch = base + stage + 1 (from ``t_dev`` when given)."""
+        from .. import ops
+        assert t.dtype == torch.int64 and t.is_contiguous() and t.numel() <= self.cap
+        self.E.xgmi_allreduce_i64(t.data_ptr(), t.numel(), self.peers.data_ptr(), self.W, self.me, k, self.cap,
+                                  self.epoch if epoch_base is None else epoch_base, int(t_host),
+                                  t_dev.data_ptr() if t_dev is not None else 0, self.err.data_ptr(), TIMEOUT_S,
+                                  stream if stream is not None else ops.stream_ptr(self.device))
+
+    def advance(self, stages: int):
+        """Reserve ``stages`` epochs after a loop that used epochs base+1 … base+stages."""
+        self.epoch += int(stages)
+
+    def check(self):
+        if int(self.err.item()) != 0:
+            raise RuntimeError("xGMI peer all-reduce timed out waiting for a peer rank "
+                               f"(HFENS_XGMI_TIMEOUT={TIMEOUT_S} s); set HFENS_XGMI=0 to use RCCL")
+
+
+_CACHE: Dict[tuple, PeerComm] = {}
+_OK: Dict[int, bool] = {}
+
+
+def _same_host(group) -> bool:
+    import torch.distributed as dist
+    names = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, socket.gethostname(), group=group)
+    return len(set(names)) == 1
+
+
+def peer_comm(group, device, cap: int) -> Optional[PeerComm]:
+    """The group's peer buffers (created once, grown when ``cap`` grows) or None when the ranks
+    cannot map each other (different hosts, > 16 ranks, HFENS_XGMI=0, no GPU)."""
+    import torch.distributed as dist
+    if group is None or MODE == "0" or torch.device(device).type != "cuda":
+        return None
+    gid = id(group)
+    if gid not in _OK:
+        W = dist.get_world_size(group)
+        _OK[gid] = W <= MAX_RANKS and _same_host(group)
+        if not _OK[gid] and MODE == "1":
+            raise RuntimeError("HFENS_XGMI=1 but the ranks cannot map each other's memory")
+    if not _OK[gid]:
+        return None
+    key = (gid, str(torch.device(device)))
+    pc = _CACHE.get(key)
+    if pc is None or pc.cap < cap:
+        epoch = pc.epoch if pc is not None else 0
+        if pc is not None:
+            pc.close()
+        pc = PeerComm(group, device, cap)
+        pc.epoch = epoch
+        _CACHE[key] = pc
+    return pc
+
+
+def _close(self: PeerComm):
+    import torch.distributed as dist
+    torch.cuda.synchronize(self.device)
+    if dist.is_initialized():
+        dist.barrier(group=self.group)   # no peer still writes into a buffer being unmapped
+    for p in self.opened:
+        self.E.xgmi_ipc_close(p)
+    self.opened = []
+    if self.own:
+        self.E.xgmi_free(self.own)
+        self.own = 0
+
+
+PeerComm.close = _close
+
+
+def release_all():
+    """Unmap and free every peer buffer (before destroying the process group)."""
+    for pc in list(_CACHE.values()):
+        pc.close()
+    _CACHE.clear()
+    _OK.clear()

@@ -232,31 +232,32 @@ def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
         assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-12)
 
 
-def _dp_stage_worker(rank, world, port, q):
+def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0):
     import os
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HFENS_XGMI=xgmi)
     import torch.distributed as dist
     from hfens.models import hist_gbdt
+    from hfens.parallel import dist as pdist
     from hfens.parallel.dist import shard_rows
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda:0")
         X, y = _data(9000, 17, 53)
-        ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
-        fit_gbdt_batch(ms, shard_rows(X, rank, world).to(dev), shard_rows(y, rank, world).to(dev),
-                       group=dist.group.WORLD)
+        for _ in range(2):   # twice: the second fit reuses the peer buffers (epochs continue)
+            ms = [GradientBoostingClassifier(n_estimators=T, max_depth=1, subsample=subsample, random_state=s)
+                  for s in (1, 2)]
+            fit_gbdt_batch(ms, shard_rows(X, rank, world).to(dev), shard_rows(y, rank, world).to(dev),
+                           group=dist.group.WORLD)
         if rank == 0:
             q.put((hist_gbdt.LAST_PATH["path"], hist_gbdt.COLLECTIVES["per_stage"],
+                   hist_gbdt.COLLECTIVES.get("xgmi_per_stage", 0.0), hist_gbdt.GRAPH_INFO.get("units", 0),
                    [(m.tree_feature_.cpu().numpy(), m.tree_threshold_.cpu().numpy(), m.tree_value_.cpu().numpy(),
                      m.tree_impurity_.cpu().numpy(), m.train_score_.cpu().numpy()) for m in ms]))
     finally:
-        dist.destroy_process_group()
+        pdist.shutdown()
 
 
-def test_gbdt_stage_data_parallel_bit_identical(dev):
-    """Two ranks on the card (gloo carries the int64 all-reduce of device tensors): the sharded
-    stage path issues exactly ONE collective per boosting stage and reproduces the single-process
-    fit bit for bit, impurities included."""
+def _run_dp_stage(world, xgmi, T=30, subsample=1.0):
     import socket
     import torch.multiprocessing as mp
     sk = socket.socket()
@@ -265,16 +266,19 @@ def test_gbdt_stage_data_parallel_bit_identical(dev):
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_stage_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_stage_worker, args=(r, world, port, q, xgmi, T, subsample)) for r in range(world)]
     for p in procs:
         p.start()
-    path, per_stage, got = q.get(timeout=100)
+    out = q.get(timeout=150)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert path == "stage" and per_stage == 1.0
+    return out
+
+
+def _check_dp_stage_equal(dev, got, T=30, subsample=1.0):
     X, y = _data(9000, 17, 53)
-    ms = [GradientBoostingClassifier(n_estimators=30, max_depth=1, random_state=s) for s in (1, 2)]
+    ms = [GradientBoostingClassifier(n_estimators=T, max_depth=1, subsample=subsample, random_state=s) for s in (1, 2)]
     fit_gbdt_batch(ms, X.to(dev), y.to(dev))
     for (f, t, v, imp, ts), m in zip(got, ms):
         assert np.array_equal(f, m.tree_feature_.cpu().numpy())
@@ -282,6 +286,27 @@ def test_gbdt_stage_data_parallel_bit_identical(dev):
         assert np.array_equal(v, m.tree_value_.cpu().numpy())
         assert np.array_equal(imp, m.tree_impurity_.cpu().numpy())
         assert np.array_equal(ts, m.train_score_.cpu().numpy())
+
+
+def test_gbdt_stage_data_parallel_bit_identical(dev):
+    """Two ranks on the card, RCCL-free gloo group with the peer path off (HFENS_XGMI=0): the
+    sharded stage path issues exactly ONE collective per boosting stage and reproduces the
+    single-process fit bit for bit, impurities included."""
+    path, per_stage, xg, units, got = _run_dp_stage(2, "0")
+    assert path == "stage" and per_stage == 1.0 and xg == 0.0
+    _check_dp_stage_equal(dev, got)
+
+
+@pytest.mark.parametrize("world,subsample", [(2, 1.0), (4, 1.0), (4, 0.8)])
+def test_gbdt_stage_xgmi_bit_identical(dev, world, subsample):
+    """the per-stage sum through IPC-mapped peer buffers (parallel/xgmi.py, one
+    kernel per stage, captured in the stage graph) — 2 and 4 processes on one card, each mapping
+    the others' buffers — gives the single-process fit bit for bit with ZERO collectives per
+    stage (the process group only exchanged the IPC handles)."""
+    path, per_stage, xg, units, got = _run_dp_stage(world, "1", subsample=subsample)
+    assert path == "stage" and per_stage == 0.0 and xg == 1.0
+    assert units == 31 // 3          # the stage loop ran as replayed HIP graphs
+    _check_dp_stage_equal(dev, got, subsample=subsample)
 
 
 def _gbdt_outputs(ms):
