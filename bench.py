@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--seeds", type=int, default=None, help="gbdt/deep: models (seeds) trained together")
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--subsample", type=float, default=1.0)
+    ap.add_argument("--dp-policy", default="auto",
+                    help="gbdt/deep multi-GPU layout: auto | seeds | rows | <ranks per seed group>")
     a = ap.parse_args()
     if a.config == "infer":
         return bench_infer(a)
@@ -266,17 +268,25 @@ def bench_gbdt(a):
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
         ops.ext()
-    lo, hi = pdist.shard_bounds(rows, rank, world)
-    X, y = make_hf_cohort_device(rows, a.features, seed=a.seed, rows=(lo, hi), device=dev)
+    # multi-GPU layout (parallel/ensemble.py): S ranks per seed group — S = 1 trains whole seeds
+    # per rank with no collective, S = N shards the rows of every seed (per-stage peer-memory
+    # sum), in between a hybrid; every seed's trees are bit-identical to the one-GPU fit
+    from hfens.parallel import ensemble
+    S = ensemble.seed_layout(world, seeds, rows, a.dp_policy) if group is not None else 1
+    G = world // S
+    mine = ensemble.my_seeds(rank, world, seeds, S)
+    glo, ghi = pdist.shard_bounds(rows, rank % S, S)     # this rank's rows within its group
+    X, y = make_hf_cohort_device(rows, a.features, seed=a.seed, rows=(glo, ghi), device=dev)
+    sub = ensemble.group_of(rank, world, S, group) if group is not None else None
     n_hold = max(1, rows // 5)
-    hlo, hhi = pdist.shard_bounds(n_hold, rank, world)
-    Xh, yh = make_hf_cohort_device(n_hold, a.features, seed=a.seed + 1, rows=(hlo, hhi), device=dev)
+    Xh, yh = make_hf_cohort_device(n_hold, a.features, seed=a.seed + 1, rows=(0, n_hold), device=dev)
 
     def fit():
         ms = [GradientBoostingClassifier(n_estimators=trees, max_depth=a.depth, subsample=a.subsample,
                                          random_state=a.seed + k) for k in range(seeds)]
-        fit_gbdt_batch(ms, X, y, group=group)
-        return ms
+        if mine:
+            fit_gbdt_batch([ms[k] for k in mine], X, y, group=sub)
+        return [ms[k] for k in mine]
 
     def barrier():
         if group is not None:
@@ -296,27 +306,35 @@ def bench_gbdt(a):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
         elapsed = float(t)
-    # untimed: held-out AUROC of the seed-averaged ensemble (folded stump tables) and its speed
-    bins_h = ms[0]._bin_mapper.transform(Xh)
-    if a.depth == 1:
-        T, init = stump_bin_tables(ms)
-        raw = ensemble_raw_binned(T, init, bins_h)
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(5):
+    # untimed: held-out AUROC of the seed-averaged ensemble (folded stump tables) and its speed;
+    # every rank scores its own seeds on all held-out rows, one SUM over the seed groups' leaders
+    lead = rank % S == 0
+    t_inf = float("nan")
+    ssum = torch.zeros(n_hold, dtype=torch.float64, device=dev)
+    if ms and lead:
+        bins_h = ms[0]._bin_mapper.transform(Xh)
+        if a.depth == 1:
+            T, init = stump_bin_tables(ms)
             raw = ensemble_raw_binned(T, init, bins_h)
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        t_inf = (time.perf_counter() - t1) / 5
-    else:
-        raw = torch.stack([m.decision_function(Xh) for m in ms])
-        t_inf = float("nan")
-    score = torch.sigmoid(raw.double()).mean(0)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(5):
+                raw = ensemble_raw_binned(T, init, bins_h)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t_inf = (time.perf_counter() - t1) / 5
+        else:
+            raw = torch.stack([m.decision_function(Xh) for m in ms])
+        ssum = torch.sigmoid(raw.double()).sum(0)
+    if group is not None:
+        pdist.all_reduce_sum_(ssum, group)
+    score = ssum / seeds
     # fp8 leaf values on the matrix cores (BASELINE config 5): the same ensemble as a leaf one-hot ×
     # two-term e4m3 leaf-value GEMV (ops/csrc/forest_fp8.hip), timed, with its AUROC delta
+    # (one-process runs: it needs every seed's trees on one device)
     fp8 = None
-    if dev.type == "cuda" and seeds <= 8:
+    if dev.type == "cuda" and seeds <= 8 and group is None:
         from hfens.models.forest_infer import Fp8Forest
         f8 = Fp8Forest(ms)
         raw8 = f8.raw(bins_h)
@@ -328,17 +346,9 @@ def bench_gbdt(a):
         t_f8 = (time.perf_counter() - t2) / 5
         score8 = torch.sigmoid(raw8.double()).mean(0)
         fp8 = dict(score=score8, t=t_f8, max_raw_err=float((raw8.double() - raw.double()).abs().max()))
-    yh_local = yh
-    if group is not None:
-        score = pdist.all_gather_rows(score[:, None], group)[:, 0]
-        yh = pdist.all_gather_rows(yh[:, None].to(score.dtype), group)[:, 0]
     auc = metrics.roc_auc(yh.double(), score)
     if fp8 is not None:
-        s8 = fp8["score"]
-        if group is not None:
-            s8 = pdist.all_gather_rows(s8[:, None], group)[:, 0]
-        fp8["auroc"] = metrics.roc_auc(yh.double(), s8)
-    del yh_local
+        fp8["auroc"] = metrics.roc_auc(yh.double(), fp8["score"])
     value = rows * seeds * a.steps / elapsed
     if rank == 0:
         base = CPU_BASELINE_DEEP_ROWS_SEEDS_PER_S if deep else CPU_BASELINE_GBDT_ROWS_PER_S
@@ -364,7 +374,10 @@ def bench_gbdt(a):
                 "auroc_delta": round(float(fp8["auroc"] - auc), 6), "max_abs_raw_err": fp8["max_raw_err"],
                 "rows_x_models_per_sec": round(n_hold * seeds / max(fp8["t"], 1e-12), 1)},
             "config": {"model": f"hist GBDT {trees} trees depth {a.depth} x {seeds} seeds, subsample {a.subsample}",
-                       "global_batch": rows, "seq_len": a.features, "parallelism": f"dp{world}"},
+                       "global_batch": rows, "seq_len": a.features,
+                       "parallelism": f"dp{world}" if S == world else
+                       (f"seeds{G}" if S == 1 else f"seeds{G}xdp{S}"),
+                       "seed_groups": G, "ranks_per_group": S},
         }), flush=True)
     pdist.shutdown()
 

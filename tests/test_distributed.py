@@ -418,3 +418,65 @@ def test_fit_bins_dp_equals_single_process(world):
         assert torch.equal(lo, bm.lo_val)
         assert torch.equal(hi, bm.hi_val)
         assert torch.equal(e, bm.edges)
+
+
+def _seed_ens(rank, world, group):
+    """Every seed-group layout S (ranks per group) of 5 seeds: each rank trains its seeds (on its
+    row shard of the group) and the trees of every seed are all-gathered as int64/f64 rows."""
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.parallel import ensemble
+    X, y, _ = _data(1500, 12, 9)
+    out = {}
+    for S in [s for s in (1, 2, 4) if world % s == 0]:
+        ms = [GradientBoostingClassifier(n_estimators=8, max_depth=1, subsample=0.7, random_state=10 + k)
+              for k in range(5)]
+        mine = ensemble.fit_seed_ensemble(ms, X, y, rank, world, S, group)
+        # one row per (seed, tree): [seed, feature, threshold, value0..2, train_score]; group
+        # leaders contribute, everyone else sends nothing
+        rows = []
+        if rank % S == 0:
+            for k in mine:
+                m = ms[k]
+                for t in range(8):
+                    rows.append([k, float(m.tree_feature_[t, 0]), float(m.tree_threshold_[t, 0])]
+                                + [float(v) for v in m.tree_value_[t].reshape(-1)[:3]] + [float(m.train_score_[t])])
+        loc = torch.tensor(rows, dtype=torch.float64).reshape(-1, 7)
+        from hfens.parallel.dist import all_gather_rows
+        allr = all_gather_rows(loc, group)
+        out[S] = allr[torch.argsort(allr[:, 0] * 100 + torch.arange(allr.shape[0]) % 8, stable=True)]
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_seed_parallel_bit_identical(world):
+    """Seed / hybrid / row layouts of a 5-seed bagged ensemble (parallel/ensemble.py, BASELINE
+    config 5): every seed's trees, leaf values and train scores equal the single-process batched
+    fit bit for bit (S = 1: whole seeds per rank, no collective; S = world: rows sharded)."""
+    from hfens.models.gbdt import GradientBoostingClassifier
+    from hfens.models.hist_gbdt import fit_gbdt_batch
+    got = _run("_seed_ens", world)
+    X, y, _ = _data(1500, 12, 9)
+    ms = [GradientBoostingClassifier(n_estimators=8, max_depth=1, subsample=0.7, random_state=10 + k)
+          for k in range(5)]
+    fit_gbdt_batch(ms, X, y)
+    want = torch.tensor([[k, float(m.tree_feature_[t, 0]), float(m.tree_threshold_[t, 0])]
+                         + [float(v) for v in m.tree_value_[t].reshape(-1)[:3]] + [float(m.train_score_[t])]
+                         for k, m in enumerate(ms) for t in range(8)], dtype=torch.float64)
+    assert set(got) == {s for s in (1, 2, 4) if world % s == 0}
+    for S, rows in got.items():
+        assert rows.shape == want.shape, (S, rows.shape)
+        assert torch.equal(rows, want), S
+
+
+def test_seed_layout_cost_model():
+    from hfens.parallel import ensemble
+    assert ensemble.seed_layout(8, 1, 1_000_000) == 8          # one seed: shard its rows
+    assert ensemble.seed_layout(8, 5, 1_000_000, "seeds") == 1
+    assert ensemble.seed_layout(8, 5, 1_000_000, "rows") == 8
+    assert ensemble.seed_layout(8, 5, 1_000_000, "4") == 4
+    S = ensemble.seed_layout(8, 5, 1_000_000)
+    assert 8 % S == 0
+    assert ensemble.my_seeds(0, 8, 5, 1) == [0] and ensemble.my_seeds(5, 8, 5, 1) == []
+    assert ensemble.my_seeds(4, 8, 5, 4) == [1, 3] and ensemble.my_seeds(3, 8, 5, 4) == [0, 2, 4]
+    with pytest.raises(ValueError):
+        ensemble.seed_layout(8, 5, 1000, "3")
