@@ -234,7 +234,9 @@ def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
 
 def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0):
     import os
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HFENS_XGMI=xgmi)
+    # ranks sharing ONE card: one hardware queue each, so 4 processes' queues are all resident
+    # (a spinning peer kernel must not keep another rank's queue from being scheduled)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HFENS_XGMI=xgmi, GPU_MAX_HW_QUEUES="1")
     import torch.distributed as dist
     from hfens.models import hist_gbdt
     from hfens.parallel import dist as pdist
@@ -334,12 +336,15 @@ def test_gbdt_stage_graph_bit_identical(dev, monkeypatch, T, subsample):
             assert np.array_equal(u, v)
 
 
-def test_gbdt_stage_graph_rccl_world1(dev):
-    """The RCCL branch (backend "nccl") on a one-rank group: its per-stage all-reduces are captured
-    in the stage graph, one collective per stage, and the model equals the single-process fit."""
+def test_gbdt_stage_graph_rccl_world1(dev, monkeypatch):
+    """The RCCL branch (backend "nccl", peer-memory path off) on a one-rank group: its per-stage
+    all-reduces are captured in the stage graph, one collective per stage, and the model equals the
+    single-process fit."""
     import tempfile
     import torch.distributed as dist
     from hfens.models import hist_gbdt
+    from hfens.parallel import xgmi
+    monkeypatch.setattr(xgmi, "MODE", "0")
     store = tempfile.mktemp(prefix="hfens_pg_")   # file store: no TCP port to race for
     dist.init_process_group("nccl", init_method=f"file://{store}", rank=0, world_size=1,
                             device_id=torch.device(dev))
