@@ -285,6 +285,10 @@ def _threshold_edges(lo: torch.Tensor, hi: torch.Tensor, up: torch.Tensor) -> to
         t = a / 2.0 + c / 2.0
         t = torch.where((t == c) | torch.isinf(t), a, t)
         t32 = t.to(torch.float32)
+        # round toward a: a float32 x == t32 > t must bin right (the threshold walk: x <= t is
+        # false), so an edge that rounded up steps back to the float below it (still ≥ a)
+        down = torch.nextafter(t32, torch.full_like(t32, -float("inf")))
+        t32 = torch.where(t32.double() > t, down, t32)
         t32 = torch.where(t32.double() >= c, a.to(torch.float32), t32)
         e[:-1] = t32
     return e

@@ -355,9 +355,11 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
         _run_host(st, group)
     hmark("gbc_enqueued")
     check_finite(st.value, "GBDT leaf values")
+    hmark("gbc_guarded")
     if getattr(st, "peer", None) is not None:
         st.peer.check()     # (after the guard's host read: no extra synchronisation point)
     _finish(models, st, sw, p1, group)
+    hmark("gbc_finished")
     return models
 
 
@@ -550,6 +552,15 @@ PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage w
 LAST_STAGE_PROF: dict = {}
 
 
+def stage_plan(n: int, B: int, hist_len: int, ncu: int) -> np.ndarray:
+    """gbdt_stump_stage's launch geometry: [rows per workgroup, workgroups per model, partial
+    slots used (0/1), partial buffer length in int64] (ops/csrc/gbdt.hip sg_plan)."""
+    from .. import ops
+    out = np.zeros(4, dtype=np.int64)
+    ops.ext().gbdt_stage_plan(int(n), int(B), int(hist_len), int(ncu), out.ctypes.data)
+    return out
+
+
 def _stage_ok(st: _State) -> bool:
     nbh = st.bm.nb_host
     return (STUMP_PATH == "stage" and st.D == 1 and st.F <= 128 and nbh is not None
@@ -577,10 +588,10 @@ def _run_stage(st: _State, group):
         binsp[:, st.n:].zero_()
         binsp[:, :st.n].copy_(st.bins)
     # per-workgroup partial slots (the kernel reduces them in a second small launch when a model
-    # spans more than 16 workgroups; sized for ≤ 2 workgroups per CU per model)
+    # spans more than 16 workgroups), sized from the kernel's own launch plan (one source of truth)
     from .smo import _num_cus
-    groups = min(-(-st.n // 1024), 2 * _num_cus(dev))
-    plen = st.B * groups * (3 * hist_len + 8)
+    plan = stage_plan(st.n, st.B, hist_len, _num_cus(dev))
+    groups, plen = int(plan[1]), max(1, int(plan[3]))
     partials = runtime.workspace(dev, "gbdt_stage_partials", plen, torch.int64)
     prof = torch.zeros(st.B * groups * 6, dtype=torch.int64, device=dev) if PROFILE_STAGE_T >= 0 else None
     n_coll, n_xg = [0], [0]

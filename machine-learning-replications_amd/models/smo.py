@@ -690,7 +690,7 @@ LAST_SMO_PROF: dict = {}
 LAST_SMO_INFO: dict = {}
 PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
 PROFILE_COOP = os.environ.get("HFENS_PROFILE_COOP", "0") == "1"   # in-kernel phase counters of the cooperative SMO
-PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # in-kernel phase counters of the working-set solver
+PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # phase counters (svm_ws.hip built with -DHFENS_WS_STAMPS)
 
 
 def assign_problems(sizes, world: int) -> List[int]:

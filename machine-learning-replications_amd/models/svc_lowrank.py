@@ -77,12 +77,12 @@ def _native(Phi: torch.Tensor) -> bool:
     return Phi.is_cuda and Phi.dtype == torch.float64 and Phi.is_contiguous() and ops.has_ext()
 
 
-def _wsyrk_part_len(n: int, r: int, ncu: int) -> int:
-    """Partial-tile buffer of ops/csrc/lowrank.hip wsyrk_f64 (same rule as wsyrk_groups)."""
-    nt = -(-r // 128)
-    T = nt * (nt + 1) // 2
-    G = max(1, min(-(-2 * ncu // T), -(-n // 64)))
-    return G * T * 128 * 128
+def _part_len(fn: str, *args) -> int:
+    """Partial buffer length of a split-K kernel of ops/csrc/lowrank.hip, from the kernel's own rule."""
+    import numpy as np
+    out = np.zeros(1, dtype=np.int64)
+    getattr(ops.ext(), fn)(*[int(a) for a in args], out.ctypes.data)
+    return int(out[0])
 
 
 # The native f64-MFMA weighted SYRK (ops/csrc/lowrank.hip) computes only the upper tiles and never
@@ -107,8 +107,7 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     l, r = Phi.shape
     if NATIVE_SYRK and _native(Phi) and r <= 2048:
         from .. import runtime
-        from .smo import _num_cus
-        plen = _wsyrk_part_len(l, r, _num_cus(Phi.device))
+        plen = _part_len("wsyrk_part_len", l, r)
         part = runtime.workspace(Phi.device, _ws_name("wsyrk_part"), plen, torch.float64)
         S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
         ops.ext().wsyrk_f64(Phi.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
@@ -134,11 +133,11 @@ def _phit(Phi: torch.Tensor, V: torch.Tensor, P32: torch.Tensor = None) -> torch
     if P32 is not None and r <= 512 and r % 4 == 0 and V.shape[1] <= 4 and P32.data_ptr() % 16 == 0:
         from .. import runtime
         k = V.shape[1]
-        G = (l + 63) // 64 if l < 1024 * 64 else 1024
-        part = runtime.workspace(Phi.device, _ws_name("phit_part"), G * r * k, torch.float64)
+        plen = _part_len("phit_part_len", l, r, k)
+        part = runtime.workspace(Phi.device, _ws_name("phit_part"), plen, torch.float64)
         Vc = V.to(torch.float64).contiguous()
         out = torch.empty(r, k, dtype=torch.float64, device=Phi.device)
-        ops.ext().phit_f32(P32.data_ptr(), Vc.data_ptr(), l, r, k, part.data_ptr(), G * r * k, out.data_ptr(),
+        ops.ext().phit_f32(P32.data_ptr(), Vc.data_ptr(), l, r, k, part.data_ptr(), plen, out.data_ptr(),
                            ops.stream_ptr(Phi.device))
         return out
     k = l // _SYRK_CHUNK

@@ -10,6 +10,7 @@ namespace hfens {
 
 constexpr int kWave = 64;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 

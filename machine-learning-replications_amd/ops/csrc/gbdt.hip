@@ -1564,6 +1564,31 @@ size_t gbdt_stump_stage_lds(int hist_len, bool mf) {
          (mf ? kSgMaxInd * 32 * sizeof(int) : 0);
 }
 
+// Launch geometry of gbdt_stump_stage — the ONE place it is computed (the Python side sizes the
+// partial-slot buffer from gbdt_stage_plan).  Rows per workgroup: 1024-row sub-tiles, as many per
+// workgroup as keeps the whole grid within k workgroups per CU (HFENS_SG_WGS_PER_CU, default 1: the
+// kernel holds one workgroup per CU, so a grid one workgroup over the CU count runs a second full
+// round; the redundant split and the histogram flush are per workgroup, so fewer, longer
+// workgroups also do less of both).  out = {rows_per_wg, groups, uses_partials, partials_len}.
+static void sg_plan(long long n, int B, int hist_len, int ncu, long long* out) {
+  const char* e = std::getenv("HFENS_SG_WGS_PER_CU");   // read per call: tests sweep it
+  const int wgs_per_cu = e ? std::min(4, std::max(1, std::atoi(e))) : 1;
+  const long long tiles = (n + kSgTile - 1) / kSgTile;
+  const long long want = std::max(1LL, (long long)wgs_per_cu * ncu / B);   // workgroups per model
+  const long long per = (tiles + want - 1) / want;                          // sub-tiles per workgroup
+  const long long rows = per * kSgTile;
+  const long long groups = (n + rows - 1) / rows;
+  const long long slot_m = 3LL * hist_len + kSgExtra;
+  out[0] = rows;
+  out[1] = groups;
+  out[2] = groups > kRdSplit ? 1 : 0;
+  out[3] = out[2] ? (long long)B * groups * slot_m : 0;
+}
+
+void gbdt_stage_plan(long long n, int B, int hist_len, int ncu, uintptr_t out) {
+  sg_plan(n, B, hist_len, ncu, reinterpret_cast<long long*>(out));
+}
+
 void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long long ldb, uintptr_t nbins, int hist_len,
                       uintptr_t lo_val, uintptr_t hi_val, uintptr_t y, uintptr_t w, uintptr_t raw, uintptr_t wt,
                       uintptr_t seeds, long long row_off, double subsample, uintptr_t comm, uintptr_t feat,
@@ -1592,28 +1617,19 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   // t_dev (graph replay): the kernel takes the stage index from device memory; the host t still
   // selects the comm slot of the reduce launch, so a captured unit must start at t ≡ 0 (mod 3)
   HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");
-  // rows per workgroup: 1024-row sub-tiles, as many per workgroup as keeps the whole grid within
-  // k workgroups per CU (default 1: the kernel holds one workgroup per CU, so a grid one workgroup
-  // over the CU count runs a second full round; the redundant split and the histogram flush are
-  // per workgroup, so fewer, longer workgroups also do less of both)
   int dev_id = 0, ncu = 256;
   HFENS_CHECK(hipGetDevice(&dev_id));
   HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id));
-  static const int wgs_per_cu = [] {
-    const char* e = std::getenv("HFENS_SG_WGS_PER_CU");
-    return e ? std::min(2, std::max(1, std::atoi(e))) : 1;
-  }();
-  const long long tiles = (n + kSgTile - 1) / kSgTile;
-  const long long want = std::max(1LL, (long long)wgs_per_cu * ncu / B);   // workgroups per model
-  const long long per = (tiles + want - 1) / want;                          // sub-tiles per workgroup
-  J.rows_per_wg = (int)(per * kSgTile);
-  const int groups = (int)((n + J.rows_per_wg - 1) / J.rows_per_wg);
+  long long plan[4];
+  sg_plan(n, B, hist_len, ncu, plan);
+  J.rows_per_wg = (int)plan[0];
+  const int groups = (int)plan[1];
   // exact int32 slice sums: |slice| ≤ 127 per row
   if ((long long)J.rows_per_wg * 127 >= (1LL << 31)) mf = false;
   const size_t lds = gbdt_stump_stage_lds(hist_len, mf);
   const long long slot_m = 3LL * hist_len + kSgExtra;
-  if (groups <= kRdSplit || partials == 0) J.partials = nullptr;
-  else HFENS_REQUIRE(partials_len >= (long long)B * groups * slot_m, "gbdt_stump_stage: partials buffer too small");
+  if (plan[2] == 0 || partials == 0) J.partials = nullptr;
+  else HFENS_REQUIRE(partials_len >= plan[3], "gbdt_stump_stage: partials buffer too small (size it with gbdt_stage_plan)");
   if (mf && nt == 1024) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, 1024>), dim3(groups, B), dim3(1024), lds, as_stream(stream), J);
   else if (mf) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   else hipLaunchKernelGGL((gbdt_stump_stage_kernel<false, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void wsyrk_reduce_kernel(const double* __restr
   }
 }
 
-// row groups of the split-K (models/svc_lowrank.py sizes the partial buffer with the same rule)
+// row groups of the split-K (the partial buffer is sized from wsyrk_part_len below)
 static int wsyrk_groups(long long n, int T) {
   int dev = 0, ncu = 256;
   HFENS_CHECK(hipGetDevice(&dev));
@@ -150,6 +150,19 @@ static int wsyrk_groups(long long n, int T) {
   const long long max_g = (n + 4 * kSyKC - 1) / (4 * kSyKC);    // ≥ 4 slabs per group
   if (G > max_g) G = max_g;
   return (int)(G < 1 ? 1 : G);
+}
+
+// partial-buffer lengths (f64 elements) of wsyrk_f64 / phit_f32: the Python side sizes its
+// workspaces from these, never from a copy of the rules
+void wsyrk_part_len(long long n, int r, uintptr_t out) {
+  const int nt = (r + kSyT - 1) / kSyT, T = nt * (nt + 1) / 2;
+  *reinterpret_cast<long long*>(out) = (long long)wsyrk_groups(n, T) * T * kSyT * kSyT;
+}
+
+static long long phit_groups(long long n) { return n < 1024 * 64 ? (n + 63) / 64 : 1024; }
+
+void phit_part_len(long long n, int r, int k, uintptr_t out) {
+  *reinterpret_cast<long long*>(out) = phit_groups(n) * r * k;
 }
 
 void wsyrk_f64(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, long long part_len, uintptr_t S,
@@ -358,8 +371,8 @@ void phit_f32(uintptr_t Phi, uintptr_t V, long long n, int r, int k, uintptr_t p
               uintptr_t stream) {
   HFENS_REQUIRE(n >= 1 && r >= 1 && r <= 512 && r % 4 == 0 && k >= 1 && k <= kGvMaxK && (Phi & 15) == 0,
                 "phit_f32: r <= 512, r % 4 == 0, 16-byte aligned Φ, 1 <= k <= 4");
-  const long long G = n < 1024 * 64 ? (n + 63) / 64 : 1024;
-  HFENS_REQUIRE(part_len >= G * r * k, "phit_f32: partial buffer too small");
+  const long long G = phit_groups(n);
+  HFENS_REQUIRE(part_len >= G * r * k, "phit_f32: partial buffer too small (size it with phit_part_len)");
   const long long per = (n + G - 1) / G;
   hipStream_t st = as_stream(stream);
   auto go = [&](auto kk) {

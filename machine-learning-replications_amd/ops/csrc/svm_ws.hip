@@ -29,6 +29,8 @@
 // Results meet libsvm's KKT tolerance but follow a different pair sequence, so α agrees with
 // libsvm to O(eps), not bit for bit (the exact-sequence solvers stay in svm.hip / svm_coop.hip for
 // small problems and parity tests).  Deterministic: no order-dependent atomics.
+#include <type_traits>
+
 #include "common.h"
 
 namespace hfens {
@@ -390,6 +392,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   static_assert(Q % TH == 0 && (Q & (Q - 1)) == 0 && TH % 64 == 0 && TH <= 512, "whole slots per thread");
   static_assert(FP % 4 == 0, "z rows are read as float4");
   constexpr int SL = Q / TH;
+  static_assert(SL % 2 == 0, "slots go in pairs (packed f32 fma)");
   constexpr int NW = TH / 64;        // waves
   constexpr unsigned kIdx = Q - 1;   // slot bits packed under the selection keys
   const int b = blockIdx.x;
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   int tt[SL];
   float y[SL], Cw[SL], a[SL], g[SL], sn[SL];
   double a0[SL];
-  float zr[SL][FP];
+  f32x2 zp[SL / 2][FP];   // features of slots (2h, 2h+1) side by side: one v_pk_fma_f32 per k
 #pragma unroll
   for (int m = 0; m < SL; ++m) {
     const int s = tid + TH * m;
@@ -440,29 +443,32 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
 #pragma unroll
     for (int k = 0; k < FP; k += 4) {
       const f32x4 v = valid[m] ? *reinterpret_cast<const f32x4*>(&zB[s * FP + k]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      zr[m][k] = v[0]; zr[m][k + 1] = v[1]; zr[m][k + 2] = v[2]; zr[m][k + 3] = v[3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zp[m / 2][k + q][m & 1] = v[q];
     }
   }
   const float k2c = -2.f * P.ngl2e;
   const float Cpf = (float)P.Cp, Cnf = (float)P.Cn;
   // K(x_r, x_s) for every slot s of this thread: the gradient kernel's expression (MFMA = k-ordered
   // fma chain from 0), so the inner solver and ws_gupdate see the same f32 kernel values
+  // (packed: each lane of the pair is the same k-ordered fma chain, bit for bit)
   auto krow = [&](int r, float (&out)[SL]) {
-    float d[SL];
+    f32x2 d[SL / 2];
 #pragma unroll
-    for (int m = 0; m < SL; ++m) d[m] = 0.f;
+    for (int h = 0; h < SL / 2; ++h) d[h] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < FP; k += 4) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(&zB[r * FP + k]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
-        for (int m = 0; m < SL; ++m) d[m] = fmaf(v[q], zr[m][k + q], d[m]);
+        for (int h = 0; h < SL / 2; ++h) d[h] = __builtin_elementwise_fma(f32x2{v[q], v[q]}, zp[h][k + q], d[h]);
       }
     }
     const float snr = snB[r];
 #pragma unroll
-    for (int m = 0; m < SL; ++m) out[m] = __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d[m], snr + sn[m]), 0.f));
+    for (int m = 0; m < SL; ++m)
+      out[m] = __builtin_amdgcn_exp2f(fminf(fmaf(k2c, d[m / 2][m & 1], snr + sn[m]), 0.f));
   };
   auto red4 = [&](const unsigned* r) {   // max over the NW waves' slots (uint4 reads)
     unsigned x = 0u;
@@ -477,6 +483,8 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   const float epsf = (float)eps;
   // optional in-kernel phase stamps (HFENS_PROFILE_WS=1): keys, barrier 1, row i, barrier 2,
   // pair update, row j + gradient — s_memtime waits for outstanding LDS reads, so this perturbs
+  // (compiled in only with -DHFENS_WS_STAMPS: even an untaken stamp costs scalar work per pair)
+#ifdef HFENS_WS_STAMPS
   const bool pf = prof != nullptr;
   long long ph[6] = {0, 0, 0, 0, 0, 0};
   long long tp = pf ? __builtin_amdgcn_s_memtime() : 0;
@@ -486,9 +494,15 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     ph[k] += tn - tp;                                       \
     tp = tn;                                                \
   }
+#else
+  const bool pf = false;
+  long long ph[6] = {0, 0, 0, 0, 0, 0};
+#define WS_STAMP(k)
+#endif
   int it = 0;
-  for (; it < max_inner; ++it) {
-    const int par = it & 1;
+  // one pair; false = stop.  Unrolled by parity (compile-time mirror / reduction-slot offsets)
+  auto pair = [&](auto parc) -> bool {
+    constexpr int par = decltype(parc)::value;
     float* glp = gl + par * Q;
     float* alp = al + par * Q;
     float* kip = kil + par * Q;
@@ -527,7 +541,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     const unsigned K1 = __builtin_amdgcn_readfirstlane(red4(r1));
     const unsigned K3 = __builtin_amdgcn_readfirstlane(red4(r3));
     const unsigned K4 = __builtin_amdgcn_readfirstlane(red4(r4));
-    if (K1 == 0u || K3 == 0u) break;
+    if (K1 == 0u || K3 == 0u) return false;
     const int i = (int)(K1 & kIdx);
     const float Gi = glp[i];
     const bool ipos = widx[i] < P.npos;
@@ -536,7 +550,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     const float lgap = f32_from_okey(K4) + f32_from_okey(K3);
     // (0.9999: the f32 local gap of a problem whose f64 gap is still ≥ eps always takes a pair)
     if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
-    if (lgap < tol_in) break;
+    if (lgap < tol_in) return false;
     // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / (2 − 2 K_it)
     WS_STAMP(1)
     float Ki[SL];
@@ -557,7 +571,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     WS_STAMP(2)
     __syncthreads();
     const unsigned K2 = __builtin_amdgcn_readfirstlane(red4(r2));
-    if (K2 == 0u) break;
+    if (K2 == 0u) return false;
     const int j = (int)(K2 & kIdx);
     const float Gj = glp[j];
     const float ai_old = alp[i], aj_old = alp[j];
@@ -608,6 +622,11 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
       g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
     }
     WS_STAMP(5)
+    ++it;
+    return true;
+  };
+  while (it < max_inner && pair(std::integral_constant<int, 0>{}) && it < max_inner &&
+         pair(std::integral_constant<int, 1>{})) {
   }
 #undef WS_STAMP
   if (pf && tid == 0) {
@@ -857,21 +876,24 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
     WS_SEL(4, 1024) WS_SEL(16, 1024) WS_SEL(32, 1024) WS_SEL(4, 512) WS_SEL(16, 512) WS_SEL(32, 512) {}
 #undef WS_SEL
     launch_check();
-#define WS_SOL(FF, QQ)                                                                                  \
-  if (FP == FF && Q == QQ) {                                                                            \
-    if (TH == 512)                                                                                      \
-      hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, 512>), dim3(P), dim3(512), ws_solve_lds_bytes(QQ, FF), \
-                         st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, \
-                         (long long*)prof);                                                            \
-    else                                                                                                \
-      hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, 256>), dim3(P), dim3(256), ws_solve_lds_bytes(QQ, FF), \
-                         st, pp, sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, \
-                         (long long*)prof);                                                            \
+#define WS_SOL_TH(FF, QQ, TT)                                                                           \
+  hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, TT>), dim3(P), dim3(TT), ws_solve_lds_bytes(QQ, FF), st, pp, sp, \
+                     zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, (long long*)prof)
+#define WS_SOL(FF)                                                                                      \
+  if (FP == FF && Q == 1024) {                                                                          \
+    if (TH == 512) WS_SOL_TH(FF, 1024, 512);                                                            \
+    else WS_SOL_TH(FF, 1024, 256);                                                                      \
   } else
-    WS_SOL(4, 1024) WS_SOL(8, 1024) WS_SOL(12, 1024) WS_SOL(16, 1024) WS_SOL(20, 1024) WS_SOL(24, 1024)
-    WS_SOL(32, 512) WS_SOL(40, 512) WS_SOL(48, 512) {
+#define WS_SOL512(FF)                                                                                   \
+  if (FP == FF && Q == 512) {                                                                           \
+    WS_SOL_TH(FF, 512, 256);                                                                            \
+  } else
+    WS_SOL(4) WS_SOL(8) WS_SOL(12) WS_SOL(16) WS_SOL(20) WS_SOL(24)
+    WS_SOL512(32) WS_SOL512(40) WS_SOL512(48) {
       HFENS_REQUIRE(false, "ws_steps: no solve instance for this F");
     }
+#undef WS_SOL512
+#undef WS_SOL_TH
 #undef WS_SOL
     launch_check();
     const dim3 grid((max_l + 255) / 256, P);

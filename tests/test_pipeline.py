@@ -181,3 +181,26 @@ def test_cooperative_solver_member_policies(monkeypatch):
     assert hist_gbdt._graph_units(St, None, object()) == 0        # stamps requested: eager
     St.T = 5
     assert hist_gbdt._graph_units(St, None, None) == 0            # too short to pay for a capture
+
+
+def test_bin_edges_round_toward_the_lower_value():
+    """a split threshold t = (a + c)/2 in f64 that rounds UP to a float32 t32 must not
+    put x == t32 in the left bin — the threshold walk (x <= t, f64, as sklearn) sends it right."""
+    import numpy as np
+    from hfens.models.binning import _threshold_edges
+    rng = np.random.default_rng(5)
+    hits = 0
+    for _ in range(2000):
+        a, c = np.sort(rng.normal(size=2).astype(np.float32))
+        if a == c:
+            continue
+        lo = torch.tensor([a, c], dtype=torch.float64)
+        e = _threshold_edges(lo, lo, lo.to(torch.float32))
+        t = float(a) / 2.0 + float(c) / 2.0
+        t32 = np.float32(t)
+        hits += float(t32) > t
+        for x in (t32, np.nextafter(t32, np.float32(-np.inf)), np.nextafter(t32, np.float32(np.inf)), a, c):
+            left_bin = float(x) <= float(e[0])
+            left_walk = float(x) <= t
+            assert left_bin == left_walk, (a, c, x)
+    assert hits > 100      # the rounding-up case was exercised

@@ -513,3 +513,24 @@ def test_develop_plan_ahead_identical(dev, monkeypatch):
     assert torch.equal(out[False].proba_sel, out[True].proba_sel)
     m0, m1 = out[False].model, out[True].model
     assert torch.equal(m0.oof_meta_, m1.oof_meta_)
+
+
+@pytest.mark.parametrize("wgs", ["1", "2", "4"])
+def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs):
+    """the partial-slot buffer is sized from the kernel's own launch plan
+    (gbdt_stage_plan), so every workgroups-per-CU setting and model count runs (no 'partials
+    buffer too small'), and the trees do not depend on the grid."""
+    from hfens.models import hist_gbdt
+    X, y = _data(120_000, 12, 7)
+    ref = None
+    monkeypatch.setenv("HFENS_SG_WGS_PER_CU", wgs)
+    for B in (1, 5, 6):
+        ms = [GradientBoostingClassifier(n_estimators=4, max_depth=1, random_state=s) for s in range(B)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev))
+        assert hist_gbdt.LAST_PATH["path"] == "stage"
+        plan = hist_gbdt.stage_plan(X.shape[0], B, int(ms[0]._bin_mapper.nb_host.sum()),
+                                    torch.cuda.get_device_properties(dev).multi_processor_count)
+        assert plan[1] * plan[0] >= X.shape[0] and (plan[2] == 0) == (plan[3] == 0)
+        if B == 1:
+            ref = ms[0].tree_feature_.cpu()
+        assert torch.equal(ms[0].tree_feature_.cpu(), ref)
