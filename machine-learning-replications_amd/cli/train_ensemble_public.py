@@ -1,12 +1,14 @@
 """Model development entry point (reference ``train_ensemble_public.py``).
 
 No-argument behaviour follows the reference: load ``develop_data.mat`` and
-``model_select_data.mat`` next to the script (``T:34-40``), print the selected
-feature names and count (``T:56-59``), fit the stack, print the held-out
-``classification_report`` at ``> 0.5`` (``T:62-64``) and draw ROC/PR with Wald
-bands (``T:66-90``; saved as PNGs instead of ``plt.show()``).  Those ``.mat``
-files are private, so when they are absent a Table-S1-shaped synthetic cohort is
-generated (``--rows``, ``--features``).  Extras: ``--device cuda``, ``--save-model``
+``model_select_data.mat`` from the directory of the script that was run
+(``T:33-39``: ``os.path.dirname(__file__)``), print the selected feature names and
+count (``T:56-59``), fit the stack, print the held-out ``classification_report`` at
+``> 0.5`` (``T:62-64``) and ALWAYS draw the ROC/PR curves with Wald bands
+(``T:66-90``; written as ``hf_roc.png`` / ``hf_pr.png`` in the working directory
+instead of ``plt.show()`` on a headless node, ``--no-plots`` to skip).  Those
+``.mat`` files are private, so when they are absent a Table-S1-shaped synthetic
+cohort is generated (``--rows``, ``--features``).  Extras: ``--device cuda``, ``--save-model``
 (writes the sklearn-0.23.2 ``.pkl`` layout that ``predict_hf.py`` reads),
 ``--timings``; under ``torchrun`` the development rows are sharded over ranks.
 """
@@ -20,18 +22,22 @@ import sys
 import numpy as np
 
 
-def main(argv=None) -> int:
+def main(argv=None, script_dir=None) -> int:
     ap = argparse.ArgumentParser(description="train the HF-progression stacking ensemble")
-    ap.add_argument("--data-dir", default=None, help="directory with develop_data.mat / model_select_data.mat")
+    ap.add_argument("--data-dir", default=None,
+                    help="directory with develop_data.mat / model_select_data.mat (default: the script's)")
     ap.add_argument("--rows", type=int, default=713, help="synthetic rows per set (when no .mat files)")
     ap.add_argument("--features", type=int, default=64, help="synthetic candidate features")
     ap.add_argument("--seed", type=int, default=2020)
     ap.add_argument("--device", default=None, help="cpu | cuda (default: cuda if available)")
     ap.add_argument("--save-model", default=None, help="write a 0.23.2-layout hf_predict_model.pkl")
-    ap.add_argument("--plots", default=None, help="PNG prefix for ROC/PR plots")
+    ap.add_argument("--plots", default="hf", help="PNG prefix for the ROC/PR plots (default 'hf')")
+    ap.add_argument("--no-plots", action="store_true", help="skip the ROC/PR figures")
     ap.add_argument("--timings", action="store_true")
     ap.add_argument("--json", default=None, help="append a JSON result line to this file")
     a = ap.parse_args(argv)
+    if a.no_plots:
+        a.plots = None
 
     import torch
     from ..io.mat import load_data, names_list
@@ -45,7 +51,8 @@ def main(argv=None) -> int:
     if device == "cuda":
         device = str(pdist.rank_device())
         torch.cuda.set_device(torch.device(device))
-    data_dir = a.data_dir or os.getcwd()
+    # T:33-34: the .mat files sit next to the script that was run (not the working directory)
+    data_dir = a.data_dir or script_dir or os.path.dirname(os.path.abspath(sys.argv[0] or "."))
     dev_path = os.path.join(data_dir, "develop_data.mat")
     sel_path = os.path.join(data_dir, "model_select_data.mat")
     if os.path.exists(dev_path) and os.path.exists(sel_path):

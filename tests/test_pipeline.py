@@ -204,3 +204,26 @@ def test_bin_edges_round_toward_the_lower_value():
             left_walk = float(x) <= t
             assert left_bin == left_walk, (a, c, x)
     assert hits > 100      # the rounding-up case was exercised
+
+
+def test_train_cli_reads_mat_next_to_script_and_plots(tmp_path, monkeypatch, capsys):
+    """Reference no-arg behaviour (T:33-39, 66-90): the .mat files are read from the directory of
+    the script that was run, not the working directory, and the ROC/PR figures are always drawn."""
+    from hfens.cli.train_ensemble_public import main
+    from hfens.io.mat import save_data
+    from hfens.io.synth import make_dev_select
+    Xd, yd, Xs, ys, names = make_dev_select(300, 24, seed=3)
+    script_dir = tmp_path / "scriptdir"
+    script_dir.mkdir()
+    save_data(str(script_dir / "develop_data.mat"), Xd, yd, names)
+    save_data(str(script_dir / "model_select_data.mat"), Xs, ys, names)
+    work = tmp_path / "work"
+    work.mkdir()
+    monkeypatch.chdir(work)
+    assert main(["--device", "cpu", "--json", str(work / "r.json")], script_dir=str(script_dir)) == 0
+    out = capsys.readouterr().out
+    assert "number of features =  17" in out and "not found" not in out
+    import json
+    assert json.loads(open(work / "r.json").read().splitlines()[-1])["source"] == "mat"
+    made = sorted(p.name for p in work.iterdir())
+    assert any(n.startswith("hf") and n.endswith((".png", ".svg")) for n in made), made
