@@ -9,10 +9,21 @@ the global layout.
 
 The collectives are few and small (the workload is latency-bound, not
 bandwidth-bound): int64 histogram all-reduces (R1, ≤ 0.7 MB per tree level for
-6 models × 40 features × 256 bins × 3), moment / Gram / gradient all-reduces
-(R3-R5, ≤ 40 KB), and one-shot all-gathers of rows for the task-parallel SVM
-fits and the KNN donor set (R6, R9).  Integer (fixed-point) payloads make the
-reductions exact, so results are identical for 1, 2, 4 or 8 ranks.
+6 models × 40 features × 256 bins × 3; on one node through IPC peer memory,
+parallel/xgmi.py), moment / Gram / gradient all-reduces (R3-R5, ≤ 40 KB), and
+one-shot all-gathers of rows for the task-parallel SVM fits and the KNN donor set
+(R6, R9).
+
+What is exact across rank counts (tests/test_distributed.py, world 2/4/8):
+* the integer reductions — GBDT fixed-point histograms (bit-identical trees), KNN
+  donor arg-mins, sharded AUROC bucket counts — and every task-parallel result
+  ('task' policy: all ranks fit on the full rows, bit-identical to one process);
+* NOT the f64 sums of the 'dp' policy (LassoCV Grams, scaler moments, LR Newton
+  moments/line-search losses): each rank sums its rows, then the ranks' partials are
+  added, so the summation order depends on the rank count and a sum moves by a few
+  ulp (≤ (N−1)·ε relative to Σ|terms|).  Pinned by test_develop_dp_matches_single:
+  same selected features, held-out probabilities within 1e-12 (measured ≤ 4.4e-16).
+  A discrete decision that sits on an exact tie of such a sum could still flip.
 """
 from __future__ import annotations
 

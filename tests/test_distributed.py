@@ -165,12 +165,13 @@ def _develop(rank, world, group, policy="dp"):
     Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
     r = develop(shard_rows(Xd, rank, world), shard_rows(yd, rank, world), shard_rows(Xs, rank, world),
                 shard_rows(ys, rank, world), names, device="cpu", group=group)
-    return r.selected.copy(), r.scores
+    from hfens.parallel.dist import all_gather_rows
+    p = all_gather_rows(r.proba_sel.double()[:, None], group)[:, 0]
+    return r.selected.copy(), r.scores, p
 
 
 def _develop_task(rank, world, group):
-    sel, scores = _develop(rank, world, group, policy="task")
-    return sel, scores
+    return _develop(rank, world, group, policy="task")
 
 
 def _svc_task(rank, world, group):
@@ -249,7 +250,7 @@ def test_assign_problems_lpt():
     assert max(loads) - min(loads) <= 4
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_svc_task_parallel_matches_single(world):
     from hfens.models.smo import fit_svc_batch
     from hfens.models.svc import SVC
@@ -263,26 +264,39 @@ def test_svc_task_parallel_matches_single(world):
         assert ic == float(s._intercept_[0]) and a == s._probA.item() and b == s._probB.item()
 
 
-@pytest.mark.slow
-def test_develop_task_matches_single():
+@pytest.mark.parametrize("world", [2, 8])
+def test_develop_task_matches_single(world):
+    """'task' policy (rows gathered once, the SMO problems spread over ranks): every rank fits on
+    the full rows, so the model equals the single-process one bit for bit.  The held-out rows are
+    scored per shard: ≤ 256 rows go through the native f64 host predictor, more through the
+    per-model torch path — the same f64 formula, equal to 1e-12 (at world 8: 75-row shards)."""
     from hfens.io.synth import make_dev_select
     from hfens.pipeline import develop
-    sel, scores = _run("_develop_task")
+    sel, scores, p = _run("_develop_task", world)
     Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
     r = develop(Xd, yd, Xs, ys, names, device="cpu")
     assert np.array_equal(sel, r.selected)
-    assert abs(scores["auroc"] - r.scores["auroc"]) < 1e-12   # replicated fits: same model
+    assert float((p - r.proba_sel.double()).abs().max()) <= 1e-12
+    if world == 2:   # 300-row shards: the same predict path as the single process
+        assert torch.equal(p, r.proba_sel.double())
+    assert abs(scores["auroc"] - r.scores["auroc"]) <= 1e-12
 
 
-@pytest.mark.slow
-def test_develop_dp_matches_single():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_develop_dp_matches_single(world):
+    """'dp' policy (rows stay sharded): the integer reductions (GBDT histograms, KNN donors,
+    AUROC) are exact; the f64 sums (LassoCV Grams, scaler moments, LR Newton moments) are summed
+    in a rank-count-dependent order, which moves them by a few ulp.  Pinned here: the same
+    selected features and held-out probabilities within 1e-12 of the single-process fit
+    (measured: ≤ 4.4e-16) at 2, 4 and 8 ranks (VERDICT r2 #5; parallel/dist.py states the bound)."""
     from hfens.io.synth import make_dev_select
     from hfens.pipeline import develop
-    sel, scores = _run("_develop")
+    sel, scores, p = _run("_develop", world)
     Xd, yd, Xs, ys, names = make_dev_select(600, 30, seed=5)
     r = develop(Xd, yd, Xs, ys, names, device="cpu")
     assert np.array_equal(sel, r.selected)
-    assert abs(scores["auroc"] - r.scores["auroc"]) < 1e-3  # f64 reduction order differs per rank
+    assert float((p - r.proba_sel.double()).abs().max()) <= 1e-12
+    assert abs(scores["auroc"] - r.scores["auroc"]) <= 1e-12
 
 
 def _stack_dp(rank, world, group, lowrank=False):
@@ -321,7 +335,7 @@ def _stack_single(lowrank=False):
     return sc, svc, clf
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_stack_dp_scaler_and_svc_match_single(world):
     """the DP stack's StandardScaler moments are reduced over ALL ranks, so the
     scaled rows, the SVC solution and the meta-learner equal the single-process fit."""
