@@ -40,7 +40,28 @@ def _check_same(models, attrs):
             raise ValueError(f"batched logistic fit needs identical '{a}' across models")
 
 
-def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
+def _newton_finish(Hb, gb, wb, pn, lam, d, eps_diag):
+    """Exact minimiser of the L1-QP on the current sign pattern of w + d, or None when it is not
+    optimal (mirror of ops/csrc/l1qp.h: the same reduced system, the same acceptance test)."""
+    F1 = gb.shape[0]
+    Hp = Hb + eps_diag * np.eye(F1)
+    u = wb + d
+    S = (~pn) | (u != 0)
+    sig = np.where(pn, np.sign(u), 0.0)
+    A = np.where(S[:, None] & S[None, :], Hp, 0.0) + np.diag((~S).astype(float))
+    rhs = np.where(S, Hp @ wb - gb - lam * sig, 0.0)
+    try:
+        L = np.linalg.cholesky(A)
+    except np.linalg.LinAlgError:
+        return None
+    un = np.linalg.solve(L.T, np.linalg.solve(L, rhs))
+    ok = np.all(np.where(S & pn, ((sig > 0) & (un > 0)) | ((sig < 0) & (un < 0)), True))
+    r = gb + Hp @ (un - wb)
+    ok = ok and np.all(np.where(~S, np.abs(r) <= lam * (1 + 1e-12), True))
+    return un - wb if ok else None
+
+
+def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12, eps_diag=0.0):
     Hn, gn, wn = H.cpu().numpy(), g.cpu().numpy(), w.cpu().numpy()
     pn = penal.cpu().numpy().astype(bool)
     B, F1 = gn.shape
@@ -49,7 +70,7 @@ def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
         Hb, gb, wb = Hn[b], gn[b], wn[b]
         d = np.zeros(F1)
         Hd = np.zeros(F1)
-        for _ in range(max_sweeps):
+        for sweep in range(max_sweeps):
             mx = 0.0
             for k in range(F1):
                 a = max(Hb[k, k], 1e-300)
@@ -68,6 +89,11 @@ def _host_l1_qp(H, g, w, penal, lam, max_sweeps=200, tol=1e-12):
                     mx = max(mx, abs(step))
             if mx <= tol:
                 break
+            if sweep % 4 == 3:   # ops/csrc/l1qp.h: exact finish on the sign pattern, if optimal
+                dn = _newton_finish(Hb, gb, wb, pn, lam, d, eps_diag)
+                if dn is not None:
+                    d = dn
+                    break
         out[b] = d
     return torch.as_tensor(out, dtype=g.dtype, device=g.device)
 

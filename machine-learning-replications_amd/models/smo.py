@@ -581,7 +581,10 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
 
 
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
-WS_INNER_PER_Q = int(os.environ.get("HFENS_SVM_WS_INNER", "4"))        # inner pair cap = this × q
+# inner pairs per round: the 36 problems advance in lock-step rounds, so one long inner solve holds
+# up every other problem's next round; a cap bounds that wait (the capped problem simply continues
+# in its next working set)
+WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
@@ -609,7 +612,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     wsidx = torch.zeros(P * Q, dtype=torch.int32, device=device)
     wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
     max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
-    max_inner = WS_INNER_PER_Q * Q
+    max_inner = WS_MAX_INNER
     keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
     hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
     gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)

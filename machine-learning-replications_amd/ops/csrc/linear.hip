@@ -10,6 +10,7 @@
 //                  ½‖y−Xw‖²/n + α‖w‖₁ with centred X, y; duality-gap stop), one wave per
 //                  problem (CV fold), warm-started along the path, recording the path.
 #include "common.h"
+#include "l1qp.h"
 
 namespace hfens {
 
@@ -23,8 +24,12 @@ __global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __re
   const int b = blockIdx.x;
   const int j = threadIdx.x;
   double* Hs = sm;                 // [F1][F1]
+  double* ws = Hs + F1 * F1;       // [F1] w
+  double* A = ws + F1;             // [F1][F1] Newton scratch (l1qp.h)
+  double* v = A + F1 * F1;         // [F1]
   const double* Hb = H + (size_t)b * F1 * F1;
   for (int k = j; k < F1 * F1; k += 64) Hs[k] = Hb[k];
+  if (j < F1) ws[j] = w[b * F1 + j];
   __syncthreads();
   const double gj = j < F1 ? g[b * F1 + j] : 0.0;
   const double wj = j < F1 ? w[b * F1 + j] : 0.0;
@@ -56,6 +61,8 @@ __global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __re
       }
     }
     if (maxstep <= tol) break;
+    // every 4 sweeps: the exact minimiser on the current sign pattern, if it is optimal
+    if ((sweep & 3) == 3 && l1qp_newton_finish(F1, Hs, ws, 0.0, gj, wj, j < F1 && penal[j], lam, dj, A, v)) break;
   }
   if (j < F1) d_out[b * F1 + j] = dj;
 }
@@ -63,7 +70,7 @@ __global__ __launch_bounds__(64) void l1_qp_cd_kernel(int F1, const double* __re
 void l1_qp_cd(int B, int F1, uintptr_t H, uintptr_t g, uintptr_t w, uintptr_t penal, double lam,
               int max_sweeps, double tol, uintptr_t d_out, uintptr_t stream) {
   HFENS_REQUIRE(F1 >= 1 && F1 <= 64, "l1_qp_cd: 1 <= F+1 <= 64");
-  const size_t lds = (size_t)F1 * F1 * sizeof(double);
+  const size_t lds = (2 * (size_t)F1 * F1 + 2 * (size_t)F1) * sizeof(double);
   hipLaunchKernelGGL(l1_qp_cd_kernel, dim3(B), dim3(64), lds, as_stream(stream), F1,
                      (const double*)H, (const double*)g, (const double*)w,
                      (const unsigned char*)penal, lam, max_sweeps, tol, (double*)d_out);

@@ -16,6 +16,7 @@
 // Stopping rules, step rule and constants are logreg_solver.py's, applied per model (a model
 // stops when IT has converged, not when the whole batch has).
 #include "common.h"
+#include "l1qp.h"
 
 namespace hfens {
 
@@ -295,6 +296,11 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
               hk = hnext;
             }
             if (maxstep <= 1e-12) break;
+            // every 4 sweeps: the exact minimiser on the current sign pattern (l1qp.h), if optimal;
+            // the row-chunk LDS is free during this phase and holds its scratch
+            if ((sweep & 3) == 3 &&
+                l1qp_newton_finish(F1, H, Wl, 1e-12, gj, wj, j < F1 && J.penal[j], 1.0, dj, xs, xs + F1 * F1))
+              break;
           }
         }
         const double delta = wave_sum(j < F1 ? gj * dj + fabs(wj + dj) - fabs(wj) : 0.0);
@@ -423,6 +429,7 @@ static size_t logreg_lds_plan(int F1, int* CR_out) {
   int CR = (32 * 1024) / (F1 * (int)sizeof(double));
   CR = CR > 1024 ? 1024 : CR / 64 * 64;
   if (CR < 64) CR = 64;
+  if ((long long)CR * F1 < (long long)F1 * F1 + F1) CR = (F1 + 1 + 63) / 64 * 64;   // l1qp.h scratch
   *CR_out = CR;
   const size_t lds = ((size_t)CR * F1 + 2 * CR + F1 * F1 + 3 * F1 + kLrThreads + kLrWaves * kLrSteps + 16 +
                       (T + 1)) * sizeof(double) + 2 * (size_t)npairs;

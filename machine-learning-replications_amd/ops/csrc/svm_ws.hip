@@ -413,14 +413,34 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   const double* Gp = G_all + P.aoff;
   double* ap = alpha_all + P.aoff;
   const long long c1 = __builtin_amdgcn_s_memtime();
-  for (int w = tid; w < nws; w += TH) widx[w] = wsidx[(size_t)b * Q + w];
-  __syncthreads();
-  // features of B (zero-padded to FP: the padded terms of the dot are exact no-ops)
-  for (int e = tid; e < nws * FP; e += TH) {
-    const int w = e / FP, c = e - w * FP;
-    zB[e] = c < F ? zcat[(P.zoff + widx[w]) * F + c] : 0.f;
+  // features of B: thread s loads the rows of its own slots (all loads in flight at once) into
+  // LDS, zero-padded to FP (the padded terms of the dot are exact no-ops)
+  {
+    int wi[SL];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const int s = tid + TH * m;
+      wi[m] = s < nws ? wsidx[(size_t)b * Q + s] : -1;
+    }
+    float zv[SL][FP];
+    float znv[SL];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const float* zrow = zcat + (P.zoff + (wi[m] < 0 ? 0 : wi[m])) * F;
+#pragma unroll
+      for (int k = 0; k < FP; ++k) zv[m][k] = (wi[m] >= 0 && k < F) ? zrow[k] : 0.f;
+      znv[m] = wi[m] >= 0 ? zn_all[P.aoff + wi[m]] : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const int s = tid + TH * m;
+      widx[s] = wi[m] < 0 ? 0 : wi[m];
+      snB[s] = P.ngl2e * znv[m];
+#pragma unroll
+      for (int k = 0; k < FP; k += 4)
+        *reinterpret_cast<f32x4*>(&zB[s * FP + k]) = f32x4{zv[m][k], zv[m][k + 1], zv[m][k + 2], zv[m][k + 3]};
+    }
   }
-  for (int w = tid; w < nws; w += TH) snB[w] = P.ngl2e * zn_all[P.aoff + widx[w]];
   __syncthreads();
   const long long c2 = __builtin_amdgcn_s_memtime();
   bool valid[SL], pos[SL];
