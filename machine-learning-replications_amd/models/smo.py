@@ -18,6 +18,7 @@ path mirrors every step in numpy (used on CPU and by the kernel tests).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass
 from typing import List, Optional
@@ -590,76 +591,174 @@ WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-sol
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
+# Lock-step decoupling: one round kernel ends when its SLOWEST problem's inner solve does, so the
+# largest problems (the final fits, l = n) wait every round on the CV folds' solves and vice versa
+# (measured on the bench: 22 ms of rounds for a 17.5 ms critical problem).  Problems are grouped by
+# size class (a class: l within WS_SPLIT_FRAC of its largest member), at most WS_GROUPS groups (the
+# smallest classes share the last); every group runs its rounds on a stream of its own and is
+# lock-step only within itself.  WS_GROUPS = 1: one group.
+WS_SPLIT_FRAC = float(os.environ.get("HFENS_SVM_WS_SPLIT", "0.95"))
+WS_GROUPS = int(os.environ.get("HFENS_SVM_WS_GROUPS", "3"))
+_WS_ENQ_CHUNK = 4   # rounds per group per host enqueue turn
+
+
+def _ws_groups(live, device) -> List[List[int]]:
+    P = len(live)
+    if (WS_GROUPS <= 1 or P < 2 or torch.device(device).type != "cuda"
+            or not torch.cuda.is_available()):
+        return [list(range(P))]
+    order = sorted(range(P), key=lambda k: (-live[k].l, k))
+    groups: List[List[int]] = []
+    for k in order:
+        if groups and (live[k].l >= WS_SPLIT_FRAC * live[groups[-1][0]].l or len(groups) == WS_GROUPS):
+            groups[-1].append(k)
+        else:
+            groups.append([k])
+    return [sorted(g) for g in groups]
+
+
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None):
     P = len(live)
-    arr = np.zeros(P, _WS_DT)
-    for k, p in enumerate(live):
-        arr[k] = (zoffs[k], aoffs[k], p.l, p.npos, p.Cp, p.Cn,
-                  -p.gamma * 1.4426950408889634, 0)
-    max_l = int(arr["l"].max())
     n = aoffs[-1]
     Q = ws_q(F)
     Fp2 = 2 * _ws_ks(F)
-    pdev = _dev_struct(arr, device)
+    # per-point arrays (indexed by each problem's absolute offset) are shared by the groups
     zn = torch.empty(n, dtype=torch.float32, device=device)
     alpha = torch.empty(n, dtype=torch.float64, device=device)
     G = torch.empty(n, dtype=torch.float64, device=device)
-    states = torch.zeros(P * _WS_STATE_BYTES // 4, dtype=torch.int32, device=device)
-    wsz = torch.zeros(P * Fp2 * Q, dtype=torch.float32, device=device)
-    wsn = torch.zeros(P * Q, dtype=torch.float32, device=device)
-    wdc = torch.zeros(P * Q, dtype=torch.float32, device=device)
-    wsprev = torch.zeros(P * (Q // 2), dtype=torch.int32, device=device)
-    wsidx = torch.zeros(P * Q, dtype=torch.int32, device=device)
-    wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
-    max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
-    max_inner = WS_MAX_INNER
     keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
     hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
-    gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)
-    E.ws_init(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
-              states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
-    done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
-    err = None
-    if not _WS_SYNC[0]:
+    max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
+    max_inner = WS_MAX_INNER
+    groups = _ws_groups(live, device) if not _WS_SYNC[0] else [list(range(P))]
+    cuda = torch.device(device).type == "cuda"
+    caller = torch.cuda.current_stream(device) if cuda else None
+    runs = []
+    for gi, idx in enumerate(groups):
+        # the last (smallest) group on the caller's stream, the others on process-lifetime side streams
+        side = None
+        if gi == len(groups) - 1:
+            st = s
+        else:
+            from .. import runtime
+            side = runtime.stream(device, f"svc_ws_{gi}", priority=-1)
+            side.wait_stream(caller)
+            st = side.cuda_stream
+        runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
+                              side, zn, alpha, G, keys, hist, n, Q, Fp2))
+    if _WS_SYNC[0]:
+        runs[0]["sync_rounds"](steps_per_check)
+    else:
         # no host synchronisation: WS_ROUNDS_AHEAD rounds are enqueued at once (finished problems
         # return from each launch at once), so the caller's other streams are launched meanwhile;
         # a batch still unconverged after them reports err and is re-solved synchronously by
-        # finish_svc_batch
+        # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
+        # group's stream starts within one chunk of host launch time.
+        left = min(WS_ROUNDS_AHEAD, max_outer)
+        while left > 0:
+            k = min(_WS_ENQ_CHUNK, left)
+            for r in runs:
+                r["steps"](k)
+            left -= k
+    for r in runs:
+        r["finish"]()
+    for r in runs:
+        if r["side"] is not None:
+            caller.wait_stream(r["side"])
+            for t in (alpha, G, zn, keys, r["rho"], r["iters"], r["idx_dev"]):
+                t.record_stream(r["side"])
+    if len(runs) == 1:
+        rho, iters, err = runs[0]["rho"], runs[0]["iters"], runs[0]["err"]
+    else:
+        rho = torch.empty(P, dtype=torch.float64, device=device)
+        iters = torch.empty(P, dtype=torch.int32, device=device)
+        for r in runs:
+            rho.index_copy_(0, r["idx_dev"], r["rho"])
+            iters.index_copy_(0, r["idx_dev"], r["iters"])
+        err = None if _WS_SYNC[0] else torch.stack([r["err"] for r in runs]).amax().reshape(1)
+
+    def stats():   # read back only when someone looks (tests, bench diagnostics): no sync here
+        order = np.concatenate([r["idx"] for r in runs])
+        inv = np.empty_like(order)
+        inv[order] = np.arange(order.shape[0])
+        parts = [r["stats"]() for r in runs]
+        out = {k: np.concatenate([p[k] for p in parts])[inv]
+               for k in ("outer", "inner", "gap", "cyc_select", "cyc_build", "cyc_inner", "cyc_p0", "cyc_p1", "cyc_p2")}
+        ph = [p["phases"] for p in parts]
+        out.update(q=Q, groups=[list(map(int, r["idx"])) for r in runs],
+                   phases=np.concatenate(ph)[inv] if all(x is not None for x in ph) else None)
+        return out
+    LAST_WS_STATS.set_thunk(stats)
+    LAST_SMO_INFO.clear()
+    LAST_SMO_INFO.update(problems=P, max_l=int(max(p.l for p in live)), solver="ws", q=Q, ws_groups=len(runs))
+    return alpha, rho, iters, err
+
+
+def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, s, side,
+              zn, alpha, G, keys, hist, n, Q, Fp2):
+    """State of the problems ``live[idx]``, whose rounds go on stream ``s`` (per-problem state is
+    group-local; the per-point arrays are the shared ones, addressed by each problem's absolute
+    offset).  Returns closures: ``steps(k)`` enqueues k rounds, ``sync_rounds(chunk)`` runs
+    host-checked rounds until every problem is done, ``finish()`` enqueues the ρ / statistics pass."""
+    P = len(idx)
+    arr = np.zeros(P, _WS_DT)
+    for k, j in enumerate(idx):
+        p = live[j]
+        arr[k] = (zoffs[j], aoffs[j], p.l, p.npos, p.Cp, p.Cn, -p.gamma * 1.4426950408889634, 0)
+    max_l = int(arr["l"].max())
+    ctx = (lambda: torch.cuda.stream(side)) if side is not None else contextlib.nullcontext
+    out = dict(side=side, idx=np.asarray(idx, dtype=np.int64), err=None)
+    with ctx():
+        pdev = _dev_struct(arr, device)
+        states = torch.zeros(P * _WS_STATE_BYTES // 4, dtype=torch.int32, device=device)
+        wsz = torch.zeros(P * Fp2 * Q, dtype=torch.float32, device=device)
+        wsn = torch.zeros(P * Q, dtype=torch.float32, device=device)
+        wdc = torch.zeros(P * Q, dtype=torch.float32, device=device)
+        wsprev = torch.zeros(P * (Q // 2), dtype=torch.int32, device=device)
+        wsidx = torch.zeros(P * Q, dtype=torch.int32, device=device)
+        wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
+        gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)
+        rho = torch.empty(P, dtype=torch.float64, device=device)
+        iters = torch.empty(P, dtype=torch.int32, device=device)
+        inner = torch.empty(P, dtype=torch.int64, device=device)
+        gap = torch.empty(P, dtype=torch.float64, device=device)
+        E.ws_init(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
+                  states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
+        out["idx_dev"] = _to_dev(out["idx"], device)
+    done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
+
+    def steps(k):
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
                    wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
-                   min(WS_ROUNDS_AHEAD, max_outer), wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
-        err = (done_view == 0).any().to(torch.int32).reshape(1)
-    else:
+                   k, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
+
+    def sync_rounds(steps_per_check):
         outer = 0
-        # one host check after the first 24 rounds, then every 8
-        chunk = steps_per_check or 24
+        chunk = steps_per_check or 24   # one host check after the first 24 rounds, then every 8
         while outer < max_outer:
-            E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
-                       states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
-                       wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
-                       chunk, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
+            steps(chunk)
             outer += chunk
             chunk = steps_per_check or 8
             if bool((done_view != 0).all()):
                 break
-    rho = torch.empty(P, dtype=torch.float64, device=device)
-    iters = torch.empty(P, dtype=torch.int32, device=device)
-    inner = torch.empty(P, dtype=torch.int64, device=device)
-    gap = torch.empty(P, dtype=torch.float64, device=device)
-    E.ws_finalize(pdev.data_ptr(), P, states.data_ptr(), alpha.data_ptr(), G.data_ptr(), rho.data_ptr(),
-                  iters.data_ptr(), inner.data_ptr(), gap.data_ptr(), s)
 
-    def stats():   # read back only when someone looks (tests, bench diagnostics): no sync here
+    def finish():
+        with ctx():
+            if not _WS_SYNC[0]:
+                out["err"] = (done_view == 0).any().to(torch.int32).reshape(1)
+            E.ws_finalize(pdev.data_ptr(), P, states.data_ptr(), alpha.data_ptr(), G.data_ptr(), rho.data_ptr(),
+                          iters.data_ptr(), inner.data_ptr(), gap.data_ptr(), s)
+
+    def stats():
         cyc = states.view(P, _WS_STATE_BYTES // 4)[:, 10:22].cpu().contiguous().view(torch.int64).numpy()
         return dict(outer=iters.cpu().numpy(), inner=inner.cpu().numpy(), gap=gap.cpu().numpy(),
                     cyc_select=cyc[:, 0], cyc_build=cyc[:, 1], cyc_inner=cyc[:, 2],
-                    cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5], q=Q,
+                    cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5],
                     phases=wprof.view(P, 6).cpu().numpy() if wprof is not None else None)
-    LAST_WS_STATS.set_thunk(stats)
-    LAST_SMO_INFO.clear()
-    LAST_SMO_INFO.update(problems=P, max_l=max_l, solver="ws", q=Q)
-    return alpha, rho, iters, err
+    out.update(rho=rho, iters=iters, steps=steps, sync_rounds=sync_rounds, finish=finish, stats=stats,
+               keep=(pdev, states, wsz, wsn, wdc, wsprev, wsidx, gkey, wprof, inner, gap))
+    return out
 
 
 class _LazyStats(dict):
