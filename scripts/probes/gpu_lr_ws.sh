@@ -5,7 +5,7 @@ D=gpurun_out/lrws
 mkdir -p $D
 timeout -k 10 500 python -u -m pytest tests/test_train_gpu.py tests/test_svm_ws_gpu.py -x -q -k "logreg or ws" --timeout 200 --timeout-method thread -p no:cacheprovider > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $D/pytest.log; exit 1; }
 tail -1 $D/pytest.log
-HFENS_CONCURRENT_BASES=0 timeout -k 10 300 python scripts/lr_probe.py > $D/lr.log 2>&1 || { echo "lr failed"; tail -30 $D/lr.log; exit 1; }
+HFENS_CONCURRENT_BASES=0 timeout -k 10 300 python scripts/probes/lr_probe.py > $D/lr.log 2>&1 || { echo "lr failed"; tail -30 $D/lr.log; exit 1; }
 grep members $D/lr.log
 HFENS_CONCURRENT_BASES=0 timeout -k 10 300 python scripts/ws_stats.py > $D/ws.log 2>&1 || { echo "ws_stats failed"; tail -30 $D/ws.log; exit 1; }
 grep "problem 35\|fit_svc" $D/ws.log

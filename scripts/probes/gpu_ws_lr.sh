@@ -10,6 +10,6 @@ for th in 256 512; do
   echo "== threads $th"; grep "problem 35\|fit_svc" $D/ws_$th.log
 done
 for m in 0 1 4 8; do
-  HFENS_LOGREG_MEMBERS=$m HFENS_CONCURRENT_BASES=0 timeout -k 10 300 python scripts/lr_probe.py > $D/lr_$m.log 2>&1 || { echo "lr $m failed"; tail -30 $D/lr_$m.log; exit 1; }
+  HFENS_LOGREG_MEMBERS=$m HFENS_CONCURRENT_BASES=0 timeout -k 10 300 python scripts/probes/lr_probe.py > $D/lr_$m.log 2>&1 || { echo "lr $m failed"; tail -30 $D/lr_$m.log; exit 1; }
   grep members $D/lr_$m.log
 done

@@ -7,5 +7,5 @@ rm -rf $D; mkdir -p $D
 export TMPDIR=/tmp
 HFENS_CONCURRENT_BASES=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $D/raw -o tr -- python scripts/ws_stats.py > $D/run.log 2>&1 || { echo "trace failed"; tail -20 $D/run.log; exit 1; }
 f=$(find $D/raw -name "*kernel_trace.csv" | head -1)
-python scripts/ws_trace_report.py "$f" > $D/report.txt && cat $D/report.txt
+python scripts/probes/ws_trace_report.py "$f" > $D/report.txt && cat $D/report.txt
 rm -rf $D/raw
