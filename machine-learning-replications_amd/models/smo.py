@@ -456,11 +456,36 @@ def _num_cus(device) -> int:
     return _NCU[d]
 
 
-def coop_members(P: int, max_l: int, ncu: int) -> int:
-    """Workgroups per problem for the cooperative SMO (1 = the one-workgroup kernel)."""
+def coop_members(P: int, max_l: int, ncu: int, resident: int = None) -> int:
+    """Workgroups per problem for the cooperative SMO (1 = the one-workgroup kernel).
+
+    Co-residency by construction: P·W members must all be resident at once,
+    so W is bounded by what the device co-schedules of the kernel (``resident``: occupancy per CU
+    × CUs, :func:`coop_resident`; one member per CU at most) minus the COOP_RESERVE_CUS left to
+    the concurrent GBC/LR stream.  A member that still arrives late (other work holding its CU)
+    costs at most one exchange deadline (HFENS_SMO_WAIT_MS, 20 ms; svm_coop.hip) before the
+    whole launch gives up and the batch is re-solved by the one-workgroup kernel."""
     if not COOP or PROFILE_SMO or P <= 0 or _FORCE_SINGLE[0]:
         return 1
-    return max(1, min(_COOP_MAX_W, max(ncu - COOP_RESERVE_CUS, P) // P, -(-max_l // COOP_MIN_SLICE)))
+    cap = min(ncu, resident if resident is not None else ncu) - COOP_RESERVE_CUS
+    if cap < 2 * P:
+        return 1
+    return max(1, min(_COOP_MAX_W, cap // P, -(-max_l // COOP_MIN_SLICE)))
+
+
+_RESIDENT: dict = {}
+
+
+def coop_resident(device) -> int:
+    """Blocks of the cooperative kernel the device co-schedules (hipOccupancy… × CUs)."""
+    d = torch.device(device)
+    if d not in _RESIDENT:
+        from .. import ops
+        out = np.zeros(2, dtype=np.int64)
+        with torch.cuda.device(d):
+            ops.ext().coop_resident_blocks(out.ctypes.data)
+        _RESIDENT[d] = int(out[0])
+    return _RESIDENT[d]
 
 
 def _gram_parents(live) -> List[int]:
@@ -494,7 +519,7 @@ def _column_map(par: _Prob, sub: _Prob, inv: Optional[np.ndarray] = None) -> np.
 def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     max_l = max(p.l for p in live)
     max_iter = max(10_000_000, 100 * max_l) if max_iter_cap is None else max_iter_cap
-    W = coop_members(len(live), max_l, _num_cus(device))
+    W = coop_members(len(live), max_l, _num_cus(device), coop_resident(device))
     if W > 1 and COOP_OTF and not PROFILE_COOP and F <= _OTF_MAX_F and -(-max_l // W) <= _OTF_MAX_S:
         op = np.zeros(len(live), _OTF_DT)
         for k, p in enumerate(live):
@@ -511,7 +536,7 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
                              gap.data_ptr(), err.data_ptr(), s)
         LAST_SMO_INFO.update(members=W, problems=len(live), max_l=max_l, solver="coop-otf")
         return alpha, rho, iters, err
-    W = coop_members(len(live), max_l, _num_cus(device))
+    W = coop_members(len(live), max_l, _num_cus(device), coop_resident(device))
     parent = _gram_parents(live) if (W > 1 and SHARE_GRAM) else [-1] * len(live)
     own = [k for k in range(len(live)) if parent[k] < 0]
     g = np.zeros(len(own), _GRAM_DT)
@@ -841,6 +866,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     s = ops.stream_ptr(device)
     live = [p for p in probs if p.rows is not None]
     F = Zs[0].shape[1]
+    LAST_SMO_INFO.clear()
     zcat = _gather_rows(Zs, live, "rows", device)
     from ..utils.timing import hmark
     hmark("svc_gather")

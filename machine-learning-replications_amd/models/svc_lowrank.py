@@ -41,6 +41,7 @@ import threading
 
 import numpy as np
 import torch
+import torch.distributed
 
 from .. import ops
 
@@ -57,9 +58,11 @@ def _rbf(A: torch.Tensor, B: torch.Tensor, gamma: float) -> torch.Tensor:
     return torch.exp(-gamma * d2.clamp_(min=0.0))
 
 
-def nystrom_map(Z: torch.Tensor, idx: torch.Tensor, gamma: float):
-    """(Φ [l, r], T [m, r]) with Φ = K(Z, L) T and T = U Λ^{-1/2} (dropped tiny eigenvalues)."""
-    L = Z[idx]
+def nystrom_map(Z: torch.Tensor, idx: torch.Tensor, gamma: float, L: torch.Tensor = None):
+    """(Φ [l, r], T [m, r]) with Φ = K(Z, L) T and T = U Λ^{-1/2} (dropped tiny eigenvalues).
+    ``L``: the landmark rows when they are not all rows of ``Z`` (a row shard, data parallel)."""
+    if L is None:
+        L = Z[idx]
     W = _rbf(L, L, gamma)
     # the m × m (m ≤ 1024) eigendecomposition on the host: the device solver took ≈ 350 ms of a 1M-row
     # map's 384 ms (rocSOLVER syevd on one small matrix); LAPACK on the host takes tens of ms
@@ -90,6 +93,7 @@ def _part_len(fn: str, *args) -> int:
 # against 8.1 + 1.4 ms for the split-K library bmm plus the scaled copy (profiles/r2_ipm_native.md),
 # so the library path stays the default until the kernel is tuned.
 NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
+SYRK_BLOCK = int(os.environ.get("HFENS_SYRK_BLOCK", "128"))   # library path: block-upper product (0: full)
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
 F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
@@ -105,6 +109,8 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     into 8192-row slabs (one batched GEMM, ~100 slabs × tiles in flight) and the slab products
     summed.  ``HFENS_WSYRK=1``: the native upper-tile f64-MFMA kernel (deterministic split-K)."""
     l, r = Phi.shape
+    if l == 0:
+        return torch.zeros(r, r, dtype=Phi.dtype, device=Phi.device)
     if NATIVE_SYRK and _native(Phi) and r <= 2048:
         from .. import runtime
         plen = _part_len("wsyrk_part_len", l, r)
@@ -118,11 +124,28 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     if k > 0:
         P = Phi[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, r)
         Pd = P * d[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, 1)
-        S += torch.bmm(P.transpose(1, 2), Pd).sum(0)
+        _upper_bmm(S, P, Pd)
     if k * _SYRK_CHUNK < l:
         T = Phi[k * _SYRK_CHUNK:]
-        S += T.T @ (T * d[k * _SYRK_CHUNK:, None])
+        _upper_bmm(S, T[None], (T * d[k * _SYRK_CHUNK:, None])[None])
+    if 0 < SYRK_BLOCK < r:
+        S = torch.triu(S) + torch.triu(S, 1).T
     return S
+
+
+def _upper_bmm(S: torch.Tensor, P: torch.Tensor, Pd: torch.Tensor) -> None:
+    """S += Σ_slabs Pᵀ Pd over the block-upper triangle only: block row i (SYRK_BLOCK columns of
+    Φ) times columns i·bs … r — 64 % of the full product's flops at r = 428, bs = 128; the lower
+    triangle is mirrored by the caller.  Each block row is one strided batched GEMM (column slices
+    of the slab views, no copies)."""
+    r = S.shape[0]
+    bs = SYRK_BLOCK
+    if bs <= 0 or bs >= r:
+        S += torch.bmm(P.transpose(1, 2), Pd).sum(0)
+        return
+    for i0 in range(0, r, bs):
+        i1 = min(r, i0 + bs)
+        S[i0:i1, i0:] += torch.bmm(P[:, :, i0:i1].transpose(1, 2), Pd[:, :, i0:]).sum(0)
 
 
 def _phit(Phi: torch.Tensor, V: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
@@ -130,6 +153,8 @@ def _phit(Phi: torch.Tensor, V: torch.Tensor, P32: torch.Tensor = None) -> torch
     a 10⁶-long reduction ran 50× below HBM rate: one output tile, no K split).  ``P32``: the same
     Φ stored in f32 (Φ = f64(P32) exactly): the native split-K pass reads half the bytes."""
     l, r = Phi.shape
+    if l == 0:
+        return torch.zeros(r, V.shape[1], dtype=torch.float64, device=Phi.device)
     if P32 is not None and r <= 512 and r % 4 == 0 and V.shape[1] <= 4 and P32.data_ptr() % 16 == 0:
         from .. import runtime
         k = V.shape[1]
@@ -155,6 +180,8 @@ def _phi_mv(Phi: torch.Tensor, W: torch.Tensor, P32: torch.Tensor = None) -> tor
     """Φ W for a skinny W [r, k] (k ≤ 4): GPU one native pass over Φ (ops/csrc/lowrank.hip
     phi_gemv; over the f32 copy ``P32`` when given), else the library product."""
     l, r = Phi.shape
+    if l == 0:
+        return torch.zeros(0, W.shape[1], dtype=torch.float64, device=Phi.device)
     if _native(Phi) and r <= 512 and W.shape[1] <= 4:
         Wc = W.to(torch.float64).contiguous()
         Y = torch.empty(l, W.shape[1], dtype=torch.float64, device=Phi.device)
@@ -178,7 +205,7 @@ def _bc(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
     vectorised same-shape kernel (measured: 63 vs 6 µs; its expand-copy 193 µs), so the IPM's
     scalar-times-vector updates fill a dense copy natively (ops/csrc/lowrank.hip fill_dev)."""
     n = like.shape[0]
-    if like.is_cuda and ops.has_ext():
+    if like.is_cuda and ops.has_ext() and n > 0:
         src = t.to(torch.float64).reshape(1).contiguous()
         out = torch.empty(n, dtype=torch.float64, device=like.device)
         ops.ext().fill_dev(out.data_ptr(), n, src.data_ptr(), ops.stream_ptr(like.device))
@@ -188,18 +215,58 @@ def _bc(t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
 
 def _max_step(v, dv):
     """Largest t ≤ 1 with v + t·dv ≥ 0 (device scalar, no host sync)."""
+    if v.numel() == 0:
+        return torch.ones((), dtype=v.dtype, device=v.device)
     ratio = torch.where(dv < 0, -v / torch.where(dv < 0, dv, -torch.ones_like(dv)), torch.full_like(v, 1.0))
     return ratio.min().clamp(max=1.0)
 
 
+class _Red:
+    """Cross-rank reductions of the row-sharded interior point: every
+    quantity the IPM reduces over rows — Φᵀ D⁻¹ Φ, Φᵀ v, the dot products, the step-length
+    minima, the residual maxima — is a sum / min / max over rows, so with the rows of Φ split
+    over the ranks of ``group`` each one becomes a local reduction plus ONE all-reduce; every
+    row-indexed vector (α, ν, μ, D, the directions) stays on its rank.  The all-reduced results
+    are the same bits on every rank, so the r × r factor and every step length agree exactly.
+    ``group=None``: the identity (one process)."""
+
+    def __init__(self, group):
+        self.g = group
+
+    def _ar(self, t, op):
+        if self.g is None:
+            return t
+        import torch.distributed as dist
+        shape = t.shape
+        buf = t.reshape(-1).contiguous().clone()
+        dist.all_reduce(buf, op=op, group=self.g)
+        return buf.reshape(shape)
+
+    def sum(self, t):
+        import torch.distributed as dist
+        return self._ar(t, dist.ReduceOp.SUM)
+
+    def min(self, t):
+        import torch.distributed as dist
+        return self._ar(t, dist.ReduceOp.MIN)
+
+    def max(self, t):
+        import torch.distributed as dist
+        return self._ar(t, dist.ReduceOp.MAX)
+
+
 def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int = IPM_MAX_ITER,
-                 tol: float = IPM_TOL):
+                 tol: float = IPM_TOL, group=None):
     """Solve min ½αᵀQα − 1ᵀα, yᵀα = 0, 0 ≤ α ≤ c, Q = diag(y) Φ Φᵀ diag(y), to high accuracy.
 
     Mehrotra predictor–corrector on (α, ν ≥ 0 for α ≥ 0, μ ≥ 0 for α ≤ c, b). Returns
     (α, ρ, iterations), ρ in libsvm's convention (decision = Σ y_i α_i K(x_i, ·) − ρ).
     Per iteration: one split-K weighted Gram (:func:`_weighted_gram`), one r × r Cholesky, six
-    skinny GEMMs over Φ, and ONE host synchronisation (the convergence test)."""
+    skinny GEMMs over Φ, and ONE host synchronisation (the convergence test).
+
+    ``group``: the rows of (Φ, y, c) are this rank's shard of the problem; the reductions over
+    rows are all-reduced (:class:`_Red`) and the returned α is this rank's shard."""
+    red = _Red(group)
     l, r = Phi.shape
     dt = torch.float64
     Phi = Phi.to(dt)
@@ -208,7 +275,8 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     P32 = None
     if F32_PHI and _native(Phi) and r <= 512:
         p32 = Phi.to(torch.float32)
-        if bool((p32.to(dt) == Phi).all()):
+        exact = (p32.to(dt) == Phi).all().to(dt).reshape(1)
+        if bool(red.min(exact)[0] > 0):   # every rank's shard exact: one path on every rank
             P32 = p32
     y = y.to(dt)
     c = c.to(dt)
@@ -217,7 +285,8 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     mu = torch.full((l,), IPM_NU0, dtype=dt, device=Phi.device)
     b = torch.zeros((), dtype=dt, device=Phi.device)
     eye = torch.eye(r, dtype=dt, device=Phi.device)
-    csum = float(c.sum())
+    csum = float(red.sum(c.sum()))
+    lg = float(red.sum(torch.tensor([float(l)], dtype=dt, device=Phi.device))[0])   # global rows
     # on the GPU the r × r factor / solves are the native single-workgroup kernels (ops/csrc/
     # linalg.hip: equilibration and jitter retries on the device, no library workspace, no host
     # read of `info`); the host path keeps torch.linalg
@@ -231,12 +300,14 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     it = 0
     for it in range(1, max_iter + 1):
         s = c - a
-        w = _phit(Phi, (y * a)[:, None], P32)[:, 0]       # Φᵀ Y α
+        w = red.sum(_phit(Phi, (y * a)[:, None], P32)[:, 0])   # Φᵀ Y α
         g = y * _phi_mv(Phi, w[:, None], P32)[:, 0] - 1.0   # Qα − 1
         rd = g + _bc(b, y) * y - nu + mu
-        re = torch.dot(y, a)
-        gap = (torch.dot(a, nu) + torch.dot(s, mu)) / (2 * l)
-        parts = [gap, rd.abs().max(), re.abs()] + ([info[0].to(dt)] if native else [])
+        sums = red.sum(torch.stack([torch.dot(y, a), torch.dot(a, nu) + torch.dot(s, mu)]))
+        re = sums[0]
+        gap = sums[1] / (2 * lg)
+        rdmax = red.max(rd.abs().max() if l else torch.zeros((), dtype=dt, device=Phi.device))
+        parts = [gap, rdmax, re.abs()] + ([info[0].to(dt)] if native else [])
         chk = torch.stack(parts).cpu()
         if native and float(chk[3]) < 0:
             fin = lambda t: bool(torch.isfinite(t).all())   # noqa: E731
@@ -262,7 +333,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         # S = I + Vᵀ D⁻¹ V  (V = YΦ, so Vᵀ D⁻¹ V = Φᵀ D⁻¹ Φ).  Free points drive D → 0, so S spans
         # many decades: equilibrate symmetrically before the Cholesky (exact); a relative jitter on
         # the unit diagonal is added only if it still fails.
-        S = eye + _weighted_gram(Phi, Dinv)
+        S = eye + red.sum(_weighted_gram(Phi, Dinv))
         S_prev, Dinv_prev = S, Dinv
         if DEBUG:
             dS = torch.diagonal(S)
@@ -291,7 +362,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
             Dinv_k = Dk[kk] if kk in Dk else Dinv[:, None]
             y_k = yk[kk] if kk in yk else y[:, None]
             du = Dinv_k * u
-            rhs = _phit(Phi, y_k * du, P32)
+            rhs = red.sum(_phit(Phi, y_k * du, P32))
             if native:
                 rhs = rhs.contiguous()
                 E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, rhs.shape[1], rhs.data_ptr(),
@@ -301,27 +372,30 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                 t = sc[:, None] * torch.cholesky_solve(sc[:, None] * rhs, Lc)
             return du - Dinv_k * (y_k * _phi_mv(Phi, t, P32))
 
-        def dirs(Mh, My, yMy, rnu, rmu):
-            db = (torch.dot(y, Mh) + re) / yMy
+        def dirs(Mh, My, yMy, rnu, rmu, yMh=None):
+            if yMh is None:
+                yMh = red.sum(torch.dot(y, Mh))
+            db = (yMh + re) / yMy
             da = Mh - _bc(db, My) * My
             dnu = (-rnu - nu * da) / a
             dmu = (-rmu + mu * da) / s
             return da, db, dnu, dmu
 
         def step_len(da, dnu, dmu):
-            return torch.minimum(torch.minimum(_max_step(a, da), _max_step(s, -da)),
-                                 torch.minimum(_max_step(nu, dnu), _max_step(mu, dmu)))
+            return red.min(torch.minimum(torch.minimum(_max_step(a, da), _max_step(s, -da)),
+                                         torch.minimum(_max_step(nu, dnu), _max_step(mu, dmu))))
 
         # predictor (affine scaling): its right-hand side and y share one pass over Φ
         rnu, rmu = a * nu, s * mu
         h = -rd - rnu / a + rmu / s
         M2 = Minv(torch.stack([h, y], 1))
         Mh, My = M2[:, 0], M2[:, 1]
-        yMy = torch.dot(y, My)
-        da, db, dnu, dmu = dirs(Mh, My, yMy, rnu, rmu)
+        yd2 = red.sum(torch.stack([torch.dot(y, My), torch.dot(y, Mh)]))
+        yMy = yd2[0]
+        da, db, dnu, dmu = dirs(Mh, My, yMy, rnu, rmu, yd2[1])
         ta = step_len(da, dnu, dmu)
         tav = _bc(ta, a)
-        gap_aff = (torch.dot(a + tav * da, nu + tav * dnu) + torch.dot(s - tav * da, mu + tav * dmu)) / (2 * l)
+        gap_aff = red.sum(torch.dot(a + tav * da, nu + tav * dnu) + torch.dot(s - tav * da, mu + tav * dmu)) / (2 * lg)
         sigma = (gap_aff / gap) ** 3
         # corrector (centring + second-order terms)
         tau = sigma * gap
@@ -353,7 +427,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
             ta_c = torch.maximum(torch.minimum(torch.maximum(va, lo), hi) - va, -hi)
             ts_c = torch.maximum(torch.minimum(torch.maximum(vs, lo), hi) - vs, -hi)
             Mh = Minv((ta_c / a - ts_c / s)[:, None])[:, 0]
-            dbc = torch.dot(y, Mh) / yMy
+            dbc = red.sum(torch.dot(y, Mh)) / yMy
             dac = Mh - _bc(dbc, My) * My
             nda, ndb = da + dac, db + dbc
             ndnu = dnu + (ta_c - nu * dac) / a
@@ -379,28 +453,73 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     return a, float(rho), it
 
 
-def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
+def _solve_groups(group, n: int):
+    """``n`` process groups over the ranks of ``group`` for concurrent row-sharded solves: each
+    host thread of a fit issues its all-reduces on its own communicator, so the ranks' collective
+    orders agree per communicator however the threads interleave (created once, collectively)."""
+    key = (id(group), n)
+    if key not in _GROUPS:
+        import torch.distributed as dist
+        ranks = list(range(dist.get_world_size(group)))
+        _GROUPS[key] = [dist.new_group(ranks) for _ in range(n)]
+    return _GROUPS[key]
+
+
+_GROUPS: dict = {}
+
+
+def _gamma(svc, Z: torch.Tensor, group) -> float:
+    """``svc.resolve_gamma`` over the rows of every rank ('scale': the global two-pass variance)."""
+    if group is None or svc.gamma != "scale":
+        return svc.resolve_gamma(Z)
+    red = _Red(group)
+    Zd = Z.to(torch.float64)
+    n = red.sum(torch.tensor([float(Zd.numel())], dtype=torch.float64, device=Z.device))
+    mean = red.sum(Zd.sum().reshape(1)) / n
+    v = float(red.sum(((Zd - mean) ** 2).sum().reshape(1)) / n)
+    return 1.0 / (Z.shape[1] * v) if v != 0 else 1.0
+
+
+def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
     """Fit every ``svcs[f]`` on (already scaled) ``Zs[f]`` with labels ``ys[f]`` ∈ {0, 1}:
-    Platt CV problems + final problem per fit, as libsvm, on the fit's Nyström map."""
+    Platt CV problems + final problem per fit, as libsvm, on the fit's Nyström map.
+
+    ``group`` (data parallel): ``Zs[f]`` / ``ys[f]`` are this rank's
+    contiguous block of fit ``f``'s rows (rank order = row order).  Every rank then works on
+    every problem: the labels are all-gathered once (the libsvm CV split is a function of them),
+    the 512 landmark rows are assembled by one all-reduce, each rank maps only its own rows
+    (Φ_local = K(Z_local, L) T) and the interior point runs row-sharded (:class:`_Red`: one
+    all-reduce per row reduction).  Held-out decision values meet in one all-reduce before the
+    Platt fit.  Every rank ends with the same model; it equals the one-process fit up to the
+    summation order of the row sums (tests/test_distributed.py, world 2/4/8)."""
     from .smo import _expand, _sigmoid_train_host
     from ..utils.guards import check_binary, check_finite
     m = int(n_landmarks or N_LANDMARKS)
+    red = _Red(group)
 
     def fit_one(f, svc, Z, y, slot):
         check_finite(Z, f"SVC.fit X (fit {f})")
-        check_binary(y, f"SVC.fit y (fit {f})")
         dev = Z.device
         Zd = Z.to(torch.float64)
-        y_np = y.reshape(-1).to(torch.float64).cpu().numpy()
+        n_loc = int(Z.shape[0])
+        if group is None:
+            check_binary(y, f"SVC.fit y (fit {f})")
+            y_np = y.reshape(-1).to(torch.float64).cpu().numpy()
+            off = 0
+        else:
+            from ..parallel import dist as pdist
+            y_all = pdist.all_gather_rows(y.reshape(-1, 1).to(torch.float64), group)[:, 0]
+            check_binary(y_all, f"SVC.fit y (fit {f})")
+            y_np = y_all.cpu().numpy()
+            off, _ = pdist.row_offset(n_loc, group, dev)
         l = y_np.shape[0]
-        gamma = svc.resolve_gamma(Zd)
+        gamma = _gamma(svc, Zd, group)
         if svc.class_weight == "balanced":
             cnt = np.bincount((y_np > 0.5).astype(np.int64), minlength=2).astype(np.float64)
             cw = l / (2 * cnt)
         else:
             cw = svc.class_weights(torch.as_tensor(y_np)).cpu().numpy()
         probs, mt = _expand(f, y_np, gamma, cw, svc)
-        grouped = mt["grouped"]
         n0 = mt["n0"]
         # landmarks: a seeded draw of the fit's rows, grouped class 0 first (libsvm SV order)
         g = torch.Generator().manual_seed(int(svc.random_state or 0) * 1000003 + l)
@@ -409,47 +528,72 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
         cls1 = y_np[pick] > 0.5
         pick = np.concatenate([np.sort(pick[~cls1]), np.sort(pick[cls1])])
         idx = torch.as_tensor(pick, device=dev)
-        Phi, T = nystrom_map(Zd, idx, gamma)
+        if group is None:
+            Lm = None
+        else:
+            # the landmark rows from their owner ranks: zero elsewhere, one exact all-reduce
+            own = (pick >= off) & (pick < off + n_loc)
+            Lm = torch.zeros(k, Zd.shape[1], dtype=torch.float64, device=dev)
+            if own.any():
+                Lm[torch.as_tensor(np.nonzero(own)[0], device=dev)] = Zd[torch.as_tensor(pick[own] - off, device=dev)]
+            Lm = red.sum(Lm)
+        Phi, T = nystrom_map(Zd, idx, gamma, L=Lm)
         if F32_PHI and _native(Phi) and Phi.shape[1] <= 512:
             # Φ rounded to f32 once (≈ 6e-8 relative, far inside the Nyström approximation's own
             # error): the IPM's HBM-bound skinny passes then read an f32 copy, half the bytes
             Phi = Phi.to(torch.float32).to(torch.float64)
         # libsvm-internal labels: class 0 = +1 (grouped order); per-point C
-        yint = torch.as_tensor(np.where(y_np > 0.5, -1.0, 1.0), dtype=torch.float64, device=dev)
+        y_loc = y_np[off:off + n_loc]
+        yint = torch.as_tensor(np.where(y_loc > 0.5, -1.0, 1.0), dtype=torch.float64, device=dev)
         cvec = torch.where(yint > 0, torch.full_like(yint, mt["C0"]), torch.full_like(yint, mt["C1"]))
-        dec_cv = np.zeros(l)
         lab = np.where(np.arange(l) < n0, 1.0, -1.0)          # grouped-position labels
-        iters = []
 
-        def solve_cv(p):
-            rows = torch.as_tensor(p.rows, device=dev)
-            a, rho, it = ipm_svc_dual(Phi[rows], yint[rows], cvec[rows])
-            wv = _phit(Phi[rows], (yint[rows] * a)[:, None])[:, 0]
-            held = torch.as_tensor(p.held_rows, device=dev)
-            return (Phi[held] @ wv - rho).cpu().numpy(), it
+        def local(rows_global):
+            """This rank's rows of a problem (problem order kept), as local indices."""
+            if group is None:
+                return rows_global
+            keep = (rows_global >= off) & (rows_global < off + n_loc)
+            return rows_global[keep] - off
+
+        def solve_cv(p, sg):
+            rows = torch.as_tensor(local(p.rows), device=dev)
+            a, rho, it = ipm_svc_dual(Phi[rows], yint[rows], cvec[rows], group=sg)
+            wv = _Red(sg).sum(_phit(Phi[rows], (yint[rows] * a)[:, None])[:, 0])
+            keep = (p.held_rows >= off) & (p.held_rows < off + n_loc)
+            held = torch.as_tensor(p.held_rows[keep] - off, device=dev)
+            return p.held[keep], (Phi[held] @ wv - rho).cpu().numpy(), it
+
+        def solve_final(sg):
+            a_f, rho_f, it_f = ipm_svc_dual(Phi, yint, cvec, group=sg)
+            wv_f = _Red(sg).sum(_phit(Phi, (yint * a_f)[:, None])[:, 0])
+            return rho_f, it_f, T @ wv_f
 
         cv = [p for p in probs if p.fold >= 0 and p.rows is not None]
+        dec_cv = np.zeros(l)
+        first = group is None or torch.distributed.get_rank(group) == 0
         for p in probs:
-            if p.fold >= 0 and p.rows is None:
-                dec_cv[p.held] = p.const
+            if p.fold >= 0 and p.rows is None and first:
+                dec_cv[p.held] = p.const      # constant folds: set once (rank 0), summed below
         nthr = min(IPM_THREADS, len(cv)) if Z.is_cuda else 1
         if nthr > 1:
-            # the Platt CV solves are independent: two host threads, each on its own stream and
-            # scratch buffers, so one solve's latency-bound steps (the single-workgroup factor and
-            # triangular solves, the per-iteration convergence read) overlap the other's
-            # bandwidth-bound passes; the same kernels on the same inputs: identical results
+            # the Platt CV solves are independent: host threads, each on its own stream and scratch
+            # buffers (and, data parallel, its own communicator), so one solve's latency-bound steps
+            # (the single-workgroup factor and triangular solves, the per-iteration convergence
+            # read) overlap the others' bandwidth-bound passes.  Problem j always runs on thread
+            # j mod nthr, in order: a fixed schedule (the same on every rank), and no two solves
+            # ever share a thread's scratch; the same kernels on the same inputs: identical results
             from concurrent.futures import ThreadPoolExecutor
             from .. import runtime
             main = torch.cuda.current_stream(dev)
+            sgs = _solve_groups(group, nthr + 1) if group is not None else [None] * (nthr + 1)
 
-            def worker(jp):
-                j, p = jp
-                _TL.tag = f"#s{slot}t{j % nthr}"
+            def worker(t):
+                _TL.tag = f"#s{slot}t{t}"
                 with torch.cuda.device(dev):
-                    st = runtime.stream(dev, f"ipm{slot}_{j % nthr}")
+                    st = runtime.stream(dev, f"ipm{slot}_{t}")
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
-                        return solve_cv(p)
+                        return [(j, solve_cv(p, sgs[t])) for j, p in enumerate(cv) if j % nthr == t]
 
             def final_worker():
                 # the final problem (the largest) is independent of the CV solves: it runs on its
@@ -459,41 +603,41 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None):
                     st = runtime.stream(dev, f"ipm_final{slot}")
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
-                        a_f, rho_f, it_f = ipm_svc_dual(Phi, yint, cvec)
-                        wv_f = _phit(Phi, (yint * a_f)[:, None])[:, 0]
-                        return rho_f, it_f, (T @ wv_f).cpu()
+                        rho_f, it_f, beta_f = solve_final(sgs[nthr])
+                        return rho_f, it_f, beta_f.cpu()
 
             with ThreadPoolExecutor(nthr + 1) as ex:
                 fin = ex.submit(final_worker)
-                outs = list(ex.map(worker, enumerate(cv)))
+                parts = [ex.submit(worker, t) for t in range(nthr)]
+                outs = sorted(sum((q.result() for q in parts), []), key=lambda jo: jo[0])
+                outs = [o for _, o in outs]
                 rho, it_final, beta_h = fin.result()
+            beta = beta_h.to(dev)
         else:
-            outs = [solve_cv(p) for p in cv]
+            outs = [solve_cv(p, group) for p in cv]
             rho = None
-        for p, (dec, it) in zip(cv, outs):
-            dec_cv[p.held] = dec
+        iters = []
+        for held, dec, it in outs:
+            dec_cv[held] = dec
             iters.append(it)
+        if group is not None:
+            dec_cv = red.sum(torch.as_tensor(dec_cv, device=dev)).cpu().numpy()
         A, B = _sigmoid_train_host(dec_cv, lab) if svc.probability else (0.0, 0.0)
         if rho is None:
-            a, rho, it = ipm_svc_dual(Phi, yint, cvec)
-            iters.append(it)
-            wv = _phit(Phi, (yint * a)[:, None])[:, 0]
-            beta = T @ wv                                      # coefficients on the landmarks
-        else:
-            it = it_final
-            iters.append(it)
-            beta = beta_h.to(dev)
+            rho, it_final, beta = solve_final(group)
+        iters.append(it_final)
         n_sv0 = int((~cls1).sum())
-        svc.set_fitted(support=idx, support_vectors=Zd[idx], n_support=[n_sv0, k - n_sv0],
-                       dual_coef_libsvm=beta, rho=rho, probA=A, probB=B, gamma=gamma,
-                       class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
-                       shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=dev)
-        svc.n_iter_ = int(it)
+        svc.set_fitted(support=idx, support_vectors=Lm if Lm is not None else Zd[idx],
+                       n_support=[n_sv0, k - n_sv0], dual_coef_libsvm=beta, rho=rho, probA=A, probB=B,
+                       gamma=gamma, class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
+                       shape_fit=(l, Z.shape[1]), n_features=Z.shape[1], device=dev)
+        svc.n_iter_ = int(it_final)
         svc.solver_ = "nystrom-ipm"
-        LAST_INFO.update(solver="nystrom-ipm", landmarks=k, rank=int(T.shape[1]), ipm_iters=iters)
+        LAST_INFO.update(solver="nystrom-ipm", landmarks=k, rank=int(T.shape[1]), ipm_iters=iters,
+                         row_sharded=group is not None)
 
     cuda = bool(Zs) and Zs[0].is_cuda
-    nfit = min(FIT_THREADS, len(svcs)) if cuda else 1
+    nfit = min(FIT_THREADS, len(svcs)) if (cuda and group is None) else 1
     if nfit > 1:
         # fits are independent too: FIT_THREADS of them at a time, each on its own stream with its
         # own slot of per-thread streams and scratch buffers (a slot is held for a whole fit), so

@@ -51,6 +51,11 @@ struct SmoCoopOut {
   long long* prof;  // [P][7] s_memtime phase totals of member 0 (nullptr = off): step2, red2,
                     // xchg2, pair, update, red1, xchg1
   int prefetch;     // 1: pull the member's candidate Gram row into L2 while the exchange runs
+  int pad_;
+  long long wait_ticks;    // one exchange waits at most this long (100 MHz real-time counter), then
+                           // flags err: a member that is not resident costs a bounded delay, and the
+                           // host re-solves with the one-workgroup kernel (models/smo.py)
+  long long inject_ticks;  // test hook: member 1 of problem 0 starts this late (0 = off)
 };
 
 constexpr int kCoopThreads = 512;
@@ -61,7 +66,17 @@ constexpr int kPkMask = (1 << kPkBits) - 1;
 constexpr int kMaxMembers = 16;
 constexpr double kCTau = 1e-12;
 constexpr double kCInf = 1.0e300;
-constexpr unsigned kSpinLimit = 1u << 22;
+constexpr long long kWaitMsDefault = 20;   // HFENS_SMO_WAIT_MS: per-exchange deadline
+
+// 100 MHz constant-rate counter (independent of the shader clock)
+__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+
+// the test hook of SmoCoopOut::inject_ticks: one member arrives late (never in production runs)
+__device__ __forceinline__ void coop_inject_delay(long long ticks, int p, int w) {
+  if (ticks <= 0 || p != 0 || w != 1) return;
+  const long long until = rt_now() + ticks;
+  while (rt_now() < until) __builtin_amdgcn_s_sleep(127);
+}
 
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoch, unsigned v) {
   __hip_atomic_store((gu64_t*)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
@@ -121,7 +136,7 @@ __device__ __forceinline__ CoopPart coop_block_red(double a, double b, int idx, 
 // false = timed out.
 template <int GS>
 __device__ __forceinline__ bool coop_gather_t(unsigned long long* slot, int W, int ng, unsigned epoch,
-                                              unsigned (*vals)[GS], unsigned* err, int* sh_fail) {
+                                              unsigned (*vals)[GS], const SmoCoopOut& out, int* sh_fail) {
   constexpr int R = (kMaxMembers * GS + 63) / 64;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -129,6 +144,7 @@ __device__ __forceinline__ bool coop_gather_t(unsigned long long* slot, int W, i
     unsigned v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = 0u;
+    const long long deadline = rt_now() + out.wait_ticks;
     unsigned spins = 0;
     bool fail = false;
     for (;;) {
@@ -145,9 +161,14 @@ __device__ __forceinline__ bool coop_gather_t(unsigned long long* slot, int W, i
         }
       }
       if (__all(ok)) break;
-      if (++spins > kSpinLimit) {
+      // the real-time counter is read every 64th poll only (a scalar memory read of its own)
+      // every 64th poll: the deadline (real-time counter) and the error flag — once any member
+      // of the launch has given up, the others leave at their next check instead of waiting out
+      // their own deadlines
+      if ((++spins & 63u) == 0 &&
+          (rt_now() > deadline || __hip_atomic_load(out.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
         fail = true;
-        if (lane == 0) atomicOr(err, 1u);
+        if (lane == 0) atomicOr(out.err, 1u);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -167,8 +188,8 @@ __device__ __forceinline__ bool coop_gather_t(unsigned long long* slot, int W, i
 }
 
 __device__ __forceinline__ bool coop_gather(unsigned long long* slot, int W, int ng, unsigned epoch,
-                                            unsigned (*vals)[kGran], unsigned* err, int* sh_fail) {
-  return coop_gather_t<kGran>(slot, W, ng, epoch, vals, err, sh_fail);
+                                            unsigned (*vals)[kGran], const SmoCoopOut& out, int* sh_fail) {
+  return coop_gather_t<kGran>(slot, W, ng, epoch, vals, out, sh_fail);
 }
 
 // Point ownership inside member w: thread tid, group g < K4, lane-of-vector e < 4 owns column
@@ -196,6 +217,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
   const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int p = xcd + 8 * (q / W), w = q % W;
   if (p >= P) return;
+  coop_inject_delay(out.inject_ticks, p, w);
   const SmoCoopProb Pr = probs[p];
   const float* Kp = K + Pr.koff;
   const int tid = threadIdx.x;
@@ -297,7 +319,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       put_u64(mine + 3, epoch, bits_of(av));
     }
     const Pf pf = prefetch_issue(loc.idx);
-    if (!coop_gather(s, W, 5, epoch, vals[epoch & 1], out.err, &sh_fail)) return false;
+    if (!coop_gather(s, W, 5, epoch, vals[epoch & 1], out, &sh_fail)) return false;
     prefetch_retire(pf);
     const unsigned(*v)[kGran] = vals[epoch & 1];
     kb = u64_of(&v[0][0]);
@@ -399,7 +421,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
       }
     }
     const Pf pf2 = prefetch_issue(loc.idx);
-    if (!coop_gather(s2, W, 10, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    if (!coop_gather(s2, W, 10, epoch, vals[epoch & 1], out, &sh_fail)) return;
     prefetch_retire(pf2);
     tick(2);
     unsigned long long ka2, kb2;
@@ -567,7 +589,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
     put_u64(mine + 4, epoch, bits_of(Sm));
     put_u64(mine + 6, epoch, bits_of(Cm));
   }
-  if (!coop_gather(s3, W, 8, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+  if (!coop_gather(s3, W, 8, epoch, vals[epoch & 1], out, &sh_fail)) return;
   if (w == 0 && tid == 0) {
     const unsigned(*v)[kGran] = vals[epoch & 1];
     unsigned long long kru = u64_of(&v[0][0]), krl = u64_of(&v[0][2]);
@@ -584,6 +606,28 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_kernel(const SmoCoopPro
     out.iters[p] = (int)iter;
     out.gap[p] = last_gap;
   }
+}
+
+// Exchange deadline and the late-member test hook, from the environment (read per launch).
+static void coop_timing(SmoCoopOut& o) {
+  const char* w = std::getenv("HFENS_SMO_WAIT_MS");
+  const char* d = std::getenv("HFENS_SMO_INJECT_DELAY_MS");
+  const double wait_ms = (w && w[0]) ? std::atof(w) : (double)kWaitMsDefault;
+  o.wait_ticks = (long long)(wait_ms * 1e5);               // 100 MHz counter
+  o.inject_ticks = (d && d[0]) ? (long long)(std::atof(d) * 1e5) : 0;
+}
+
+// Members of one problem spin on each other, so all of them must be resident together: the
+// launchers bound P·W by the CU count (one member per CU), and the Python side subtracts the CUs
+// it leaves to concurrent kernels.  This returns what the hardware would co-schedule of the
+// kernel on an idle device (occupancy per CU × CUs): the upper bound models/smo.py clamps W with.
+void coop_resident_blocks(uintptr_t out) {
+  int dev = 0, ncu = 256, per_cu = 0;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  HFENS_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smo_coop_kernel<8, true>, kCoopThreads, 0));
+  ((long long*)out)[0] = (long long)per_cu * ncu;
+  ((long long*)out)[1] = ncu;
 }
 
 void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintptr_t maps, uintptr_t alpha,
@@ -604,6 +648,7 @@ void smo_coop_batch(uintptr_t probs, int P, int W, int max_S, uintptr_t K, uintp
   const char* pfe = std::getenv("HFENS_SMO_PREFETCH");
   SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, (long long*)prof,
                (pfe && pfe[0] == '0') ? 0 : 1};
+  coop_timing(o);
   hipStream_t st = as_stream(stream);
   // every polled granule starts at epoch 0 (epochs count from 1 within the call)
   HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kGran * sizeof(unsigned long long), st));
@@ -672,6 +717,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
   const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int p = xcd + 8 * (q / W), w = q % W;
   if (p >= P) return;
+  coop_inject_delay(out.inject_ticks, p, w);
   const SmoOtfProb Pr = probs[p];
   const int tid = threadIdx.x;
   const int base = w * Pr.S;
@@ -773,7 +819,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
       if (has) publish_row(mine + 5, loc.idx);
       else publish_zero_row(mine + 5);
     }
-    if (!coop_gather_t<kOtfGran>(s, W, 6 + F, epoch, vals[epoch & 1], out.err, &sh_fail)) return false;
+    if (!coop_gather_t<kOtfGran>(s, W, 6 + F, epoch, vals[epoch & 1], out, &sh_fail)) return false;
     const unsigned(*v)[kOtfGran] = vals[epoch & 1];
     kb = u64_of(&v[0][0]);
     idx = (int)v[0][2];
@@ -851,7 +897,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
         else publish_zero_row(mine + 10);
       }
     }
-    if (!coop_gather_t<kOtfGran>(s2, W, 11 + F, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+    if (!coop_gather_t<kOtfGran>(s2, W, 11 + F, epoch, vals[epoch & 1], out, &sh_fail)) return;
     unsigned long long ka2, kb2;
     int j, mj;
     double aj_old, Gj, Kij;
@@ -1001,7 +1047,7 @@ __global__ __launch_bounds__(kCoopThreads) void smo_coop_otf_kernel(const SmoOtf
     put_u64(mine + 4, epoch, bits_of(Sm));
     put_u64(mine + 6, epoch, bits_of(Cm));
   }
-  if (!coop_gather_t<kOtfGran>(s3, W, 8, epoch, vals[epoch & 1], out.err, &sh_fail)) return;
+  if (!coop_gather_t<kOtfGran>(s3, W, 8, epoch, vals[epoch & 1], out, &sh_fail)) return;
   if (w == 0 && tid == 0) {
     const unsigned(*v)[kOtfGran] = vals[epoch & 1];
     unsigned long long kru = u64_of(&v[0][0]), krl = u64_of(&v[0][2]);
@@ -1033,6 +1079,7 @@ void smo_coop_otf_batch(uintptr_t probs, int P, int W, int F, int max_S, uintptr
   HFENS_REQUIRE((long long)P * W <= ncu, "smo_coop_otf_batch: P·W exceeds the CU count (choose a smaller W)");
   const long long blocks = 8LL * ((P + 7) / 8) * W;
   SmoCoopOut o{(double*)rho, (int*)iters, (double*)gap, (unsigned*)err, nullptr};
+  coop_timing(o);
   hipStream_t st = as_stream(stream);
   HFENS_CHECK(hipMemsetAsync((void*)xchg, 0, (size_t)P * 2 * kMaxMembers * kOtfGran * sizeof(unsigned long long), st));
   auto pp = (const SmoOtfProb*)probs;

@@ -2,7 +2,9 @@
 call site R9).
 
 An SVM dual QP is not row-separable, so the six SVC fits of a stacking fit (5 OOF
-folds + refit, each = 6 SMO problems) are distributed over ranks instead:
+folds + refit, each = 6 SMO problems) are distributed over ranks instead (the large fits of the
+Nyström + interior-point path ARE row-separable and stay row-sharded, see
+``fit_svc_batch_distributed``):
 every fit's (scaled) training rows are all-gathered once, fit ``f`` is solved by
 rank ``f mod world`` with the batched SMO, and the fitted parameters are
 broadcast back so every rank holds the full model.
@@ -11,11 +13,23 @@ from __future__ import annotations
 
 import torch
 
-from ..models.smo import finish_svc_batch, launch_svc_batch
+from ..models.smo import finish_svc_batch, launch_svc_batch, use_lowrank
 from . import dist as pdist
 
 
 def fit_svc_batch_distributed(svcs, Zs, ys, group):
+    """``Zs[f]`` / ``ys[f]``: this rank's rows of fit ``f``.  Exact-solver fits are all-gathered and
+    solved task-parallel (below); large fits (:func:`use_lowrank` on the GLOBAL sizes) stay
+    row-sharded and every rank works on every interior-point solve (svc_lowrank, data parallel)."""
+    sizes = pdist.all_reduce_sum_f64([torch.tensor([float(y.numel()) for y in ys], dtype=torch.float64,
+                                                   device=pdist._default_device(group))], group)[0]
+    if use_lowrank([int(v) for v in sizes.tolist()]):
+        from ..models import smo
+        from ..models.svc_lowrank import fit_svc_lowrank_batch
+        smo.LAST_SMO_INFO.clear()
+        smo.LAST_SMO_INFO.update(solver="nystrom-ipm", problems=6 * len(svcs), max_l=int(sizes.max()),
+                                 row_sharded=True)
+        return fit_svc_lowrank_batch(svcs, Zs, ys, group=group)
     return finish_svc_batch_distributed(launch_svc_batch_distributed(svcs, Zs, ys, group), group)
 
 

@@ -534,3 +534,105 @@ def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs):
         if B == 1:
             ref = ms[0].tree_feature_.cpu()
         assert torch.equal(ms[0].tree_feature_.cpu(), ref)
+
+
+def _lowrank_dp_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GPU_MAX_HW_QUEUES="1")
+    import torch.distributed as dist
+    from hfens.models import svc_lowrank
+    from hfens.parallel import dist as pdist
+    from hfens.parallel.dist import shard_rows
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        Z, y = _data(6000, 8, 71)
+        svc = SVC(class_weight="balanced", probability=True, random_state=2020)
+        svc_lowrank.fit_svc_lowrank_batch([svc], [shard_rows(Z, rank, world).to(dev)],
+                                          [shard_rows(y, rank, world).to(dev)], n_landmarks=256,
+                                          group=dist.group.WORLD)
+        if rank == 0:
+            q.put((svc._dual_coef_.cpu(), float(svc._intercept_[0]), svc._probA.item(), svc._probB.item(),
+                   svc.support_.cpu(), svc_lowrank.LAST_INFO["row_sharded"]))
+    finally:
+        pdist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_lowrank_svc_row_sharded_threads(dev, world):
+    """the row-sharded interior point with its concurrent Platt-CV solves (3
+    host threads + the final solve, each on its own stream AND its own communicator) — 2 / 4
+    processes on one card over gloo — equals the one-process GPU fit to 1e-8."""
+    import socket
+    import torch.multiprocessing as mp
+    from hfens.models import svc_lowrank
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_lowrank_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    coef, ic, pa, pb, sup, sharded = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Z, y = _data(6000, 8, 71)
+    ref = SVC(class_weight="balanced", probability=True, random_state=2020)
+    svc_lowrank.fit_svc_lowrank_batch([ref], [Z.to(dev)], [y.to(dev)], n_landmarks=256)
+    assert sharded is True
+    assert torch.equal(sup, ref.support_.cpu())
+    assert torch.allclose(coef, ref._dual_coef_.cpu(), rtol=0, atol=1e-8)
+    assert abs(ic - float(ref._intercept_[0])) < 1e-8
+    assert abs(pa - ref._probA.item()) < 1e-8 and abs(pb - ref._probB.item()) < 1e-8
+
+
+@pytest.mark.parametrize("otf", [False, True])
+def test_smo_coop_late_member_falls_back(dev, monkeypatch, otf):
+    """a member that arrives late (HFENS_SMO_INJECT_DELAY_MS holds member 1 of
+    problem 0 back) makes the others give up at the exchange deadline (HFENS_SMO_WAIT_MS) instead
+    of spinning for seconds; the launch reports smo_err, the batch is re-solved by the
+    one-workgroup kernel, and the model equals the one-workgroup fit.  The timeout's own cost —
+    the faulted fit minus the one-workgroup fit minus the injected delay — stays ≤ 50 ms."""
+    import time
+    import warnings
+    from hfens.models import smo
+    rows = 3000
+    X, y = _data(rows, 17, 23)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    yd = y.to(dev)
+    Zs, ys = [Z[: rows * 4 // 5], Z], [yd[: rows * 4 // 5], yd]
+    monkeypatch.setattr(smo, "SOLVER", "exact")
+    monkeypatch.setattr(smo, "COOP_OTF", otf)
+    monkeypatch.setenv("HFENS_SMO_WAIT_MS", "20")
+    assert smo.coop_resident(dev) >= torch.cuda.get_device_properties(dev).multi_processor_count
+
+    def fit(coop, delay_ms=None):
+        monkeypatch.setattr(smo, "COOP", coop)
+        if delay_ms is None:
+            monkeypatch.delenv("HFENS_SMO_INJECT_DELAY_MS", raising=False)
+        else:
+            monkeypatch.setenv("HFENS_SMO_INJECT_DELAY_MS", str(delay_ms))
+        svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        with warnings.catch_warnings(record=True) as wl:
+            warnings.simplefilter("always")
+            smo.fit_svc_batch(svcs, Zs, ys)
+        torch.cuda.synchronize()
+        return svcs, dict(smo.LAST_SMO_INFO), 1e3 * (time.perf_counter() - t), wl
+
+    fit(False)                                             # warm-up (kernels loaded)
+    one, info1, t_one, _ = fit(False)
+    fb, info2, t_fb, wl = fit(True, delay_ms=60)
+    assert info1["members"] == 1
+    assert info2.get("coop_fallback") is True and any("timed out" in str(w.message) for w in wl)
+    for a, b in zip(one, fb):
+        assert a.n_iter_ == b.n_iter_
+        assert torch.equal(a.support_, b.support_)
+        assert torch.equal(a._dual_coef_, b._dual_coef_)
+    assert t_fb - t_one - 60.0 <= 50.0, (t_fb, t_one)
+    ok, info3, _, wl3 = fit(True)                          # no injection: no fallback
+    assert not info3.get("coop_fallback") and info3["members"] > 1 and not wl3
