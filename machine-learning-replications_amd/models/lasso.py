@@ -13,6 +13,8 @@ per-fold Gram / Xᵀy / yᵀy / row counts are all-reduced (rows sharded).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -59,6 +61,9 @@ def _cd_path_host(G, q, yy, n, alphas, max_iter, tol):
                     break
         out[a] = w
     return out
+
+
+SPECULATIVE_REFIT = os.environ.get("HFENS_LASSO_SPEC_REFIT", "1") != "0"
 
 
 class LassoCV(Estimator):
@@ -137,6 +142,24 @@ class LassoCV(Estimator):
         else:
             grid = torch.as_tensor(np.sort(np.asarray(self.alphas, dtype=np.float64))[::-1].copy())
         grid = grid.to(dev)
+        A = int(grid.numel())
+        refit_all = None
+        if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT:
+            # the refit at the CV-chosen alpha is a cold-start solve on all rows (sklearn's
+            # Lasso(alpha=best).fit); which alpha wins is known only after the CV paths, so solve the
+            # cold start for EVERY alpha on a side stream while the CV paths run (one wave each, the
+            # device is otherwise idle) and pick the winner afterwards: the same kernel on the same
+            # inputs as the one-problem refit, bit-identical, and no second dependent launch on the
+            # critical path
+            from .. import runtime
+            main = torch.cuda.current_stream(dev)
+            side = runtime.stream(dev, "lasso_refit")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                refit_all = self._solve(G[k:].expand(A, F, F), q[k:].expand(A, F), yy[k:].expand(A),
+                                        cnt[k:].expand(A), grid[:, None])          # [A, 1, F]
+                ev = torch.cuda.Event()
+                ev.record(side)
         coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
         if overlap is not None:
             overlap()
@@ -156,8 +179,12 @@ class LassoCV(Estimator):
         self.alpha_ = float(grid[best])
         self.alphas_ = grid
         self.mse_path_ = mse.t()
-        final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
-        w = final[0, 0]
+        if refit_all is not None:
+            torch.cuda.current_stream(dev).wait_event(ev)
+            w = refit_all[best, 0]
+        else:
+            final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
+            w = final[0, 0]
         self.coef_ = w
         self.intercept_ = my[k] - mx[k] @ w
         self.n_features_in_ = F

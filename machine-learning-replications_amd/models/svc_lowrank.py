@@ -43,7 +43,7 @@ import numpy as np
 import torch
 import torch.distributed
 
-from .. import ops
+from .. import ops, runtime
 
 N_LANDMARKS = int(os.environ.get("HFENS_SVC_LANDMARKS", "512"))
 IPM_MAX_ITER = 80
@@ -308,7 +308,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         gap = sums[1] / (2 * lg)
         rdmax = red.max(rd.abs().max() if l else torch.zeros((), dtype=dt, device=Phi.device))
         parts = [gap, rdmax, re.abs()] + ([info[0].to(dt)] if native else [])
-        chk = torch.stack(parts).cpu()
+        chk = runtime.host_read(torch.stack(parts))   # sleeps, does not spin (runtime.host_read)
         if native and float(chk[3]) < 0:
             fin = lambda t: bool(torch.isfinite(t).all())   # noqa: E731
             raise FloatingPointError(

@@ -10,7 +10,7 @@ for mf in ${MFS:-1 0}; do
   export HFENS_SG_THREADS=${NT:-512}
   HFENS_GBDT_MFMA=$mf timeout -k 10 200 python3 -u bench.py --config gbdt --steps 10 --warmup 2 > $D/gbdt_$mf.json 2> $D/gbdt_$mf.err || { echo "gbdt $mf failed"; tail -20 $D/gbdt_$mf.err; exit 1; }
   HFENS_GBDT_MFMA=$mf timeout -k 10 300 python3 -u bench.py --config deep --steps 2 --warmup 1 --subsample 0.8 > $D/deep_$mf.json 2> $D/deep_$mf.err || { echo "deep $mf failed"; tail -20 $D/deep_$mf.err; exit 1; }
-  HFENS_GBDT_MFMA=$mf timeout -k 10 200 python3 -u scripts/stage_prof.py > $D/prof_$mf.txt 2>&1 || { echo "prof $mf failed"; tail -20 $D/prof_$mf.txt; exit 1; }
+  HFENS_GBDT_MFMA=$mf timeout -k 10 200 python3 -u scripts/probes/stage_prof.py > $D/prof_$mf.txt 2>&1 || { echo "prof $mf failed"; tail -20 $D/prof_$mf.txt; exit 1; }
   python3 -c "
 import json
 for c in ('gbdt','deep'):

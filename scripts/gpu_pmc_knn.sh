@@ -6,7 +6,7 @@ mkdir -p $D
 export TMPDIR=/tmp
 pass() {  # pass TAG COUNTERS...
   local tag=$1; shift
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $D/$tag -o p --output-format csv -- python3 scripts/knn_probe.py 300000 > $D/$tag.log 2>&1 || { echo "$tag failed"; tail -5 $D/$tag.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $D/$tag -o p --output-format csv -- python3 scripts/probes/knn_probe.py 300000 > $D/$tag.log 2>&1 || { echo "$tag failed"; tail -5 $D/$tag.log; exit 1; }
   f=$(find $D/$tag -name "*counter_collection.csv" | head -1)
   python3 scripts/pmc_summary.py $f $D/$tag.csv knn_donor && rm -rf $D/$tag && cat $D/$tag.csv | cut -c1-400
 }

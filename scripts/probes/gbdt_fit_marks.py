@@ -10,7 +10,7 @@ os.environ["HFENS_TRACE_HOST"] = "1"
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models.gbdt import GradientBoostingClassifier  # noqa: E402
 from hfens.models.hist_gbdt import fit_gbdt_batch  # noqa: E402

@@ -11,7 +11,7 @@ import time
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.io.synth import make_hf_cohort_device  # noqa: E402
 from hfens.models import hist_gbdt  # noqa: E402
 from hfens.models.gbdt import GradientBoostingClassifier  # noqa: E402

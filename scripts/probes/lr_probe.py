@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hfens.io.synth import make_hf_cohort  # noqa: E402
 from hfens.models import logreg_solver  # noqa: E402
 from hfens.pipeline import develop  # noqa: E402

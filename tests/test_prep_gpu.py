@@ -50,3 +50,19 @@ def test_weighted_moments(dev):
     assert torch.allclose(G.cpu(), Gr, rtol=1e-12, atol=1e-9)
     assert torch.allclose(a.cpu(), ar, rtol=1e-12, atol=1e-9)
     assert torch.allclose(v.cpu(), vr, rtol=1e-12, atol=1e-9)
+
+
+def test_lasso_speculative_refit_bit_identical(dev, monkeypatch):
+    """The all-alpha cold-start refits solved on a side stream beside the CV paths (the winner picked
+    afterwards) give exactly the one-problem refit at the chosen alpha."""
+    from hfens.models import lasso
+    X, y, _ = make_hf_cohort(5000, 40, seed=9, nan_frac=0.0)
+    Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    out = {}
+    for spec in (False, True):
+        monkeypatch.setattr(lasso, "SPECULATIVE_REFIT", spec)
+        m = LassoCV(cv=10).fit(Xt, yt)
+        out[spec] = (m.alpha_, m.coef_.cpu(), float(m.intercept_))
+    assert out[False][0] == out[True][0]
+    assert torch.equal(out[False][1], out[True][1])
+    assert out[False][2] == out[True][2]
