@@ -146,3 +146,29 @@ def test_knn_imputer_matches():
             dd = np.where(ok, D[r], np.inf)
             tied = np.abs(dd - dd.min()) <= 1e-9 * max(1.0, dd.min())
             assert ours[r, c] in X[tied, c] and sk[r, c] in X[tied, c]
+
+
+@pytest.mark.parametrize("seed", [2020, 7])
+def test_gbc_duplicate_column_ties_match_sklearn_partitions(seed):
+    """ADVICE r2 (low), pinned against scikit-learn itself.  With every column present three times
+    each stump has a 3-way tie that is exact in real arithmetic.  sklearn does NOT see it as an exact
+    tie: its splitter re-sorts the samples per feature with an unstable introsort, so duplicate
+    columns sum their equal-valued rows in different orders and the winner is decided by f64
+    rounding (measured: the same column index in 24 of 60 trees).  What IS reproducible, and pinned
+    here: every tree splits the training rows into exactly sklearn's partition (an equivalent column
+    and threshold), and train_score_ / probabilities agree to 1e-7."""
+    from sklearn.ensemble import GradientBoostingClassifier as SkGBC
+    from hfens.models.gbdt import GradientBoostingClassifier
+    X, y = _cohort(600, 8, 31)
+    X = np.round(X * 2) / 2
+    Xd = np.concatenate([X, X, X], axis=1)
+    ours = GradientBoostingClassifier(n_estimators=60, max_depth=1, random_state=seed).fit(
+        torch.as_tensor(Xd), torch.as_tensor(y))
+    ref = SkGBC(n_estimators=60, max_depth=1, random_state=seed).fit(Xd, y)
+    of, ot = ours.tree_feature_[:, 0].numpy(), ours.tree_threshold_[:, 0].numpy()
+    for t, est in enumerate(ref.estimators_):
+        f, th = est[0].tree_.feature[0], est[0].tree_.threshold[0]
+        assert np.array_equal(Xd[:, f].astype(np.float32) <= th, Xd[:, of[t]].astype(np.float32) <= ot[t]), t
+    assert np.abs(ours.train_score_.numpy() - ref.train_score_).max() < 1e-7
+    p = ours.predict_proba(torch.as_tensor(Xd)).numpy()[:, 1]
+    assert np.abs(p - ref.predict_proba(Xd)[:, 1]).max() < 1e-7
