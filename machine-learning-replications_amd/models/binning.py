@@ -176,7 +176,28 @@ def _fit_bins_dp(X32: torch.Tensor, max_bins: int, group) -> BinMapper:
     n_loc, F = X32.shape
     dev = X32.device
     inf = float("inf")
-    srt = torch.sort((X32 + 0.0).t().contiguous(), dim=1)[0]            # +0.0: −0 → +0 (one value)
+    Xt = (X32 + 0.0).t().contiguous()                                    # +0.0: −0 → +0 (one value)
+    # small non-negative integer features (binary flags, ordinals: most of a Table-S1 cohort): their
+    # distinct values over ALL ranks are the occupied cells of a [F, 256] bincount (one MAX
+    # all-reduce) — no sort and no value-table gather for them
+    si = ((Xt == torch.round(Xt)) & (Xt >= 0) & (Xt <= 255)).all(1).to(torch.int64)
+    dist.all_reduce(si, op=dist.ReduceOp.MIN, group=group)
+    occ = torch.zeros(F, 256, dtype=torch.int64, device=dev)
+    si_d = si.bool()
+    if n_loc > 0 and bool(si_d.any()):
+        ii = torch.nonzero(si_d)[:, 0]
+        codes = Xt.index_select(0, ii).to(torch.int64) + 256 * torch.arange(ii.numel(), device=dev)[:, None]
+        occ[ii] = (torch.bincount(codes.reshape(-1), minlength=256 * ii.numel()).view(-1, 256) > 0).to(torch.int64)
+    dist.all_reduce(occ, op=dist.ReduceOp.MAX, group=group)
+    occ_h = occ.cpu().numpy() > 0
+    si_h = si.cpu().numpy() > 0
+    int_f = [f for f in range(F) if si_h[f] and int(occ_h[f].sum()) <= max_bins]
+    rest = [f for f in range(F) if f not in set(int_f)]
+    ri = torch.as_tensor(rest, dtype=torch.int64, device=dev)
+    srt_r = torch.sort(Xt.index_select(0, ri), dim=1)[0] if rest else Xt[:0]
+    srt = torch.zeros(F, n_loc, dtype=Xt.dtype, device=dev)
+    if rest:
+        srt[ri] = srt_r
     new = torch.ones_like(srt, dtype=torch.bool)
     new[:, 1:] = srt[:, 1:] != srt[:, :-1]
     k_loc = new.sum(1).to(torch.int64)
@@ -188,7 +209,13 @@ def _fit_bins_dp(X32: torch.Tensor, max_bins: int, group) -> BinMapper:
     kmax_h = kmax.cpu()
     k_h = torch.full((F,), max_bins + 1, dtype=torch.int64)
     small_h = torch.full((F, max_bins), float("nan"), dtype=torch.float32)
-    cand = [f for f in range(F) if int(kmax_h[f]) <= max_bins]
+    mn_int = {}
+    for f in int_f:
+        vals = np.nonzero(occ_h[f])[0].astype(np.float32)
+        k_h[f] = int(vals.shape[0])
+        small_h[f, :vals.shape[0]] = torch.from_numpy(vals)
+        mn_int[f] = float(vals[0]) if vals.shape[0] else inf
+    cand = [f for f in rest if int(kmax_h[f]) <= max_bins]
     if cand:
         tab = torch.full((len(cand), max_bins), float("nan"), dtype=torch.float32, device=dev)
         for i_, f in enumerate(cand):
@@ -203,12 +230,14 @@ def _fit_bins_dp(X32: torch.Tensor, max_bins: int, group) -> BinMapper:
             if u.numel() <= max_bins:
                 k_h[f] = u.numel()
                 small_h[f, :u.numel()] = u
-    big_f = [f for f in range(F) if int(k_h[f]) > max_bins]
+    big_f = [f for f in rest if int(k_h[f]) > max_bins]
     hi_h = torch.zeros(F, max_bins, dtype=torch.float32)
     lo_h = torch.zeros(F, max_bins, dtype=torch.float32)
     mn = srt[:, 0].clone() if n_loc > 0 else torch.full((F,), inf, dtype=torch.float32, device=dev)
     dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
     mn_h = mn.cpu()
+    for f, v in mn_int.items():
+        mn_h[f] = v
     if big_f:
         bi = torch.as_tensor(big_f, device=dev)
         sb = srt.index_select(0, bi).contiguous()

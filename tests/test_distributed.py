@@ -416,13 +416,14 @@ def test_roc_auc_sharded_is_exact(world):
 def _bin_data():
     g = np.random.default_rng(11)
     n = 1003
-    X = np.empty((n, 6), dtype=np.float64)
+    X = np.empty((n, 7), dtype=np.float64)
     X[:, 0] = g.normal(size=n) * 1e3                          # continuous, negatives
     X[:, 1] = g.integers(0, 2, n)                             # binary
     X[:, 2] = np.where(np.arange(n) < n // 2, g.integers(0, 200, n), g.integers(200, 400, n))  # ≤ 256 per shard, 400 total
     X[:, 3] = np.round(g.normal(size=n), 1)                   # heavy ties across shards
     X[:, 4] = np.where(g.random(n) < 0.5, 0.0, -0.0)          # ±0: one value
     X[:, 5] = np.sort(g.exponential(size=n))                  # sorted: each shard holds a value range
+    X[:, 6] = g.integers(0, 100, n)                           # small integers: bincount path (> 16 values: quantiles at mb 16)
     return torch.as_tensor(X)
 
 
