@@ -23,7 +23,10 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-HOST_BIN_MAX_ROWS = int(os.environ.get("HFENS_HOST_BIN_ROWS", str(1 << 17)))
+# single-process GPU fits bin on the host below this many rows (numpy unique beats the device sorts
+# and their syncs on small inputs); measured on the MI355X box: 125k rows took 13.8 ms on the host
+# path against ~4 ms for the device path at 1M rows (profiles/r3_gbdt_dp.md)
+HOST_BIN_MAX_ROWS = int(os.environ.get("HFENS_HOST_BIN_ROWS", str(1 << 15)))
 # per-feature distinct-value all-gathers under DP (round-1 path, kept for A/B)
 LEGACY_DP_BINS = os.environ.get("HFENS_DP_BINS", "") == "legacy"
 
@@ -247,13 +250,25 @@ def _fit_bins_dp(X32: torch.Tensor, max_bins: int, group) -> BinMapper:
         need = (r + 1).to(dev).expand(len(big_f), max_bins).contiguous()
         lo_k = torch.zeros_like(need)
         hi_k = torch.full_like(need, 0xFFFFFFFF)
-        for _ in range(32):   # smallest key K with #(key ≤ K) ≥ rank + 1, over all ranks
-            mid = (lo_k + hi_k) // 2
-            cnt = torch.searchsorted(kb, mid, right=True) if n_loc > 0 else torch.zeros_like(mid)
+        # smallest key K with #(key ≤ K) ≥ rank + 1 over all ranks: a 16-way search, 4 key bits per
+        # round — 9 rounds (the span shrinks ≥ 16× per round, ≤ 1 after 8; no host sync in the loop)
+        # instead of 32 bisections;
+        # the same K (each round keeps the sub-interval holding the first pivot that reaches it)
+        m = torch.arange(1, 16, dtype=torch.int64, device=dev)
+        for _ in range(9):
+            span = hi_k - lo_k                                           # [Fb, G] (≥ 0)
+            piv = lo_k[..., None] + (span[..., None] * m) // 16          # [Fb, G, 15] ascending
+            if n_loc > 0:
+                cnt = torch.searchsorted(kb, piv.reshape(len(big_f), -1), right=True).view_as(piv)
+            else:
+                cnt = torch.zeros_like(piv)
             dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-            ge = cnt >= need
-            hi_k = torch.where(ge, mid, hi_k)
-            lo_k = torch.where(ge, lo_k, mid + 1)
+            ge = cnt >= need[..., None]
+            first = torch.where(ge.any(-1), ge.to(torch.int64).argmax(-1), torch.full_like(lo_k, 15))
+            # answer in (piv[first-1], piv[first]] (piv[-1] = lo_k - 1, piv[15] = hi_k)
+            prev = torch.where(first > 0, piv.gather(-1, (first - 1).clamp(min=0)[..., None])[..., 0] + 1, lo_k)
+            nxt_hi = torch.where(first < 15, piv.gather(-1, first.clamp(max=14)[..., None])[..., 0], hi_k)
+            lo_k, hi_k = prev, nxt_hi
         hq = _unkey(lo_k)                                                 # quantile group ends
         if n_loc > 0:
             pos = torch.searchsorted(sb, hq, right=True)
