@@ -11,8 +11,6 @@
 //                  problem (CV fold), warm-started along the path, recording the path.
 #include "common.h"
 #include "l1qp.h"
-#include <cstdlib>
-#include <type_traits>
 
 namespace hfens {
 
@@ -170,112 +168,12 @@ __global__ __launch_bounds__(64) void lasso_cd_path_kernel(int F, int A, const d
   }
 }
 
-// The same path with lane j's row of G held in REGISTERS and the coordinate loop unrolled at
-// compile time (FM ≥ F): coordinate k's column entry is a static register, its broadcast a
-// constant-lane readlane, so the per-coordinate dependent chain is the owner's soft-threshold,
-// one readlane and one fma — no ballot, no ctz and no data-dependent LDS read on it.  Every
-// coordinate is visited (the ballot kernel skips the provably-zero ones; on the 10-fold bench
-// path most coordinates move, profiles/r3_headline.md).  Same arithmetic in the same order as
-// lasso_cd_path_kernel: bit-identical coefficients, gaps and iteration counts (tested).
-template <int FM>
-__global__ __launch_bounds__(64) void lasso_cd_path_reg_kernel(int F, int A, const double* __restrict__ G,
-                                                               const double* __restrict__ q,
-                                                               const double* __restrict__ yy,
-                                                               const double* __restrict__ nrows,
-                                                               const double* __restrict__ alphas,
-                                                               int max_iter, double tol,
-                                                               double* __restrict__ coefs,
-                                                               double* __restrict__ gaps,
-                                                               int* __restrict__ iters) {
-  const int p = blockIdx.x;
-  const int j = threadIdx.x;
-  const double* Gp = G + (size_t)p * F * F;
-  double grow[FM];   // G[j][k]
-#pragma unroll
-  for (int k = 0; k < FM; ++k) grow[k] = (j < F && k < F) ? Gp[(size_t)j * F + k] : 0.0;
-  const double n = nrows[p];
-  const double qj = j < F ? q[p * F + j] : 0.0;
-  const double gjj = j < F ? Gp[(size_t)j * F + j] : 0.0;
-  const double inv_gjj = gjj != 0.0 ? 1.0 / gjj : 0.0;
-  const unsigned long long live = __ballot(j < F && gjj != 0.0);
-  const double yyp = yy[p];
-  double wj = 0.0;
-  double Hw = 0.0;
-  const double tol_s = tol * yyp;
-  for (int a = 0; a < A; ++a) {
-    const double l1 = alphas[p * A + a] * n;
-    int it = 0;
-    double gap = 0.0;
-    for (it = 0; it < max_iter; ++it) {
-      double d_w_max = 0.0;
-#pragma unroll
-      for (int k = 0; k < FM; ++k) {
-        if (k < F && ((live >> k) & 1ull)) {
-          double dw_l = 0.0;
-          if (j == k) {
-            const double tmp = qj - Hw + gjj * wj;
-            const double nw = fabs(tmp) > l1 ? copysign(fabs(tmp) - l1, tmp) * inv_gjj : 0.0;
-            dw_l = nw - wj;
-            wj = nw;
-          }
-          const double dw = readlane_f64(dw_l, k);
-          if (dw != 0.0) {
-            Hw += grow[k] * dw;
-            d_w_max = fmax(d_w_max, fabs(dw));
-          }
-        }
-      }
-      // w_max over the sweep = max |w| after it (each coordinate is visited once, zeros add nothing)
-      double w_max = j < F ? fabs(wj) : 0.0;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) w_max = fmax(w_max, __shfl_xor(w_max, o, kWave));
-      if (w_max == 0.0 || d_w_max / w_max < tol || it == max_iter - 1) {
-        const double wq = wave_sum(j < F ? wj * qj : 0.0);
-        const double wHw = wave_sum(j < F ? wj * Hw : 0.0);
-        const double l1n = wave_sum(j < F ? fabs(wj) : 0.0);
-        double dual_norm = j < F ? fabs(qj - Hw) : 0.0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) dual_norm = fmax(dual_norm, __shfl_xor(dual_norm, o, kWave));
-        const double R_norm2 = yyp - 2.0 * wq + wHw;
-        double const_ = 1.0;
-        double gp = R_norm2;
-        if (dual_norm > l1) {
-          const_ = l1 / dual_norm;
-          const double A_norm2 = R_norm2 * const_ * const_;
-          gp = 0.5 * (R_norm2 + A_norm2);
-        }
-        gap = gp + l1 * l1n - const_ * (yyp - wq);
-        if (gap < tol_s) break;
-      }
-    }
-    if (j < F) coefs[((size_t)p * A + a) * F + j] = wj;
-    if (j == 0) { gaps[p * A + a] = gap; iters[p * A + a] = it + 1; }
-  }
-}
-
 void lasso_cd_path(int P, int F, int A, uintptr_t G, uintptr_t q, uintptr_t yy, uintptr_t nrows,
                    uintptr_t alphas, int max_iter, double tol, uintptr_t coefs, uintptr_t gaps,
                    uintptr_t iters, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "lasso_cd_path: 1 <= F <= 64");
-  const char* env = std::getenv("HFENS_LASSO_KERNEL");
-  const bool reg = !(env && env[0] == 'b');   // "ballot": the LDS / ballot-skip kernel
-  hipStream_t st = as_stream(stream);
-  if (reg) {
-    auto go = [&](auto fm) {
-      constexpr int FM = decltype(fm)::value;
-      hipLaunchKernelGGL(lasso_cd_path_reg_kernel<FM>, dim3(P), dim3(64), 0, st, F, A, (const double*)G,
-                         (const double*)q, (const double*)yy, (const double*)nrows, (const double*)alphas,
-                         max_iter, tol, (double*)coefs, (double*)gaps, (int*)iters);
-    };
-    if (F <= 16) go(std::integral_constant<int, 16>{});
-    else if (F <= 32) go(std::integral_constant<int, 32>{});
-    else if (F <= 48) go(std::integral_constant<int, 48>{});
-    else go(std::integral_constant<int, 64>{});
-    launch_check();
-    return;
-  }
   const size_t lds = (size_t)F * F * sizeof(double);
-  hipLaunchKernelGGL(lasso_cd_path_kernel, dim3(P), dim3(64), lds, st, F, A,
+  hipLaunchKernelGGL(lasso_cd_path_kernel, dim3(P), dim3(64), lds, as_stream(stream), F, A,
                      (const double*)G, (const double*)q, (const double*)yy, (const double*)nrows,
                      (const double*)alphas, max_iter, tol, (double*)coefs, (double*)gaps,
                      (int*)iters);

@@ -66,19 +66,3 @@ def test_lasso_speculative_refit_bit_identical(dev, monkeypatch):
     assert out[False][0] == out[True][0]
     assert torch.equal(out[False][1], out[True][1])
     assert out[False][2] == out[True][2]
-
-
-@pytest.mark.parametrize("F", [12, 40, 61])
-def test_lasso_register_kernel_bit_identical(dev, monkeypatch, F):
-    """The register-resident unrolled LassoCV path kernel (default) against the LDS / ballot-skip
-    kernel (HFENS_LASSO_KERNEL=ballot): identical coefficients, alpha and mse path, bit for bit."""
-    X, y, _ = make_hf_cohort(6000, F, seed=17, nan_frac=0.0)
-    Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
-    out = {}
-    for k in ("ballot", "reg"):
-        monkeypatch.setenv("HFENS_LASSO_KERNEL", k)
-        m = LassoCV(cv=10).fit(Xt, yt)
-        out[k] = (m.alpha_, m.coef_.cpu(), m.mse_path_.cpu())
-    assert out["ballot"][0] == out["reg"][0]
-    assert torch.equal(out["ballot"][1], out["reg"][1])
-    assert torch.equal(out["ballot"][2], out["reg"][2])
