@@ -78,6 +78,14 @@ def main():
     from hfens.utils import metrics
     from hfens import ops
 
+    # long device-bound fits (config 3: ≥ 2^18 rows) let host waits sleep instead of spin
+    # (runtime.blocking_sync; HFENS_BLOCKING_SYNC=0/1 overrides)
+    bs = os.environ.get("HFENS_BLOCKING_SYNC", "1" if a.rows >= (1 << 18) else "0") == "1"
+    blocking = False
+    if bs and torch.cuda.device_count() > 0:
+        from hfens import runtime
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+        blocking = runtime.blocking_sync()
     group, rank, world = pdist.init_from_env()
     if world != a.gpus:
         if rank == 0:
@@ -172,7 +180,7 @@ def main():
                        "global_batch": n_total, "seq_len": a.features, "rows_per_gpu": a.rows // max(1, world),
                        "features": a.features, "parallelism": f"dp{world}",
                        "stage_seconds": stage_med},
-            "diag": dict(run_facts(dev, a.steps, elapsed, cpu, host_med, step_ends, t0),
+            "diag": dict(run_facts(dev, a.steps, elapsed, cpu, host_med, step_ends, t0), blocking_sync=blocking,
                          busiest_threads_cpu_s=_thread_delta(threads0, threads1)),
         }
         print(json.dumps(out), flush=True)

@@ -95,3 +95,21 @@ def host_read(t: torch.Tensor) -> torch.Tensor:
     ev.record(torch.cuda.current_stream(t.device))
     ev.synchronize()
     return out.reshape(t.shape).clone()
+
+
+def blocking_sync(enable: bool = True) -> bool:
+    """hipSetDeviceFlags(hipDeviceScheduleBlockingSync) on the current device BEFORE torch creates
+    its context: every host wait (stream / event synchronisation, blocking copies) then sleeps on
+    the completion signal instead of spinning a core.  For long device-bound runs (config 3: four
+    interior-point threads that each wait once per iteration); latency-bound fits keep the default
+    spin (a sleeping waiter wakes tens of µs late).  Returns whether the flag was set."""
+    if not enable:
+        return False
+    import ctypes
+    import os
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    try:
+        hip = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
+        return hip.hipSetDeviceFlags(ctypes.c_uint(0x4)) == 0   # hipDeviceScheduleBlockingSync
+    except OSError:
+        return False
