@@ -15,17 +15,19 @@ Every model is trained on exactly the rows and with exactly the reductions of a 
 (int64 histograms), so each seed's trees are bit-identical to the single-GPU fit whatever the
 layout (tests/test_distributed.py::test_seed_parallel_bit_identical).
 
-``auto`` picks S from a per-stage cost model of the stage kernel measured on one MI355X
-(profiles/r3_gbdt_dp.md): t(B, n) ≈ F0 + C·B·n (F0 ≈ 20 µs fixed, C ≈ 65 µs per model per 1M rows),
-plus ≈ X µs for the peer reduction when S > 1 — the layout with the smallest bottleneck group.
+``auto`` picks S from a per-stage cost model of the stage loop measured on one MI355X
+(profiles/r3_gbdt_dp.md, ``scripts/probes/gbdt_shard_probe.py``: 45.3 / 90.1 µs per stage for one
+model at 125k / 1M rows, 72.9 / 297.8 µs for five): t(B, n) ≈ F0 + C·B·n with F0 ≈ 40 µs fixed and
+C ≈ 51 µs per model per 1M rows, plus ≈ X = 10 µs for the peer reduction when S > 1 (measured at
+world 1) — the layout with the smallest bottleneck group.
 """
 from __future__ import annotations
 
 import os
 from typing import Dict, List, Tuple
 
-STAGE_FIXED_US = float(os.environ.get("HFENS_SEED_COST_F0", "20"))
-STAGE_ROW_US = float(os.environ.get("HFENS_SEED_COST_C", "65"))      # per model per 1M rows
+STAGE_FIXED_US = float(os.environ.get("HFENS_SEED_COST_F0", "40"))
+STAGE_ROW_US = float(os.environ.get("HFENS_SEED_COST_C", "51"))      # per model per 1M rows
 STAGE_XGMI_US = float(os.environ.get("HFENS_SEED_COST_X", "10"))
 
 
