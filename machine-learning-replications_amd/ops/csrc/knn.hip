@@ -12,6 +12,7 @@
 // 64-bit atomicMin on (float bits of d², donor index): smallest distance, then lowest donor index
 // — deterministic regardless of split count or arrival order.
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace hfens {
@@ -118,6 +119,163 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
   }
 }
 
+// The same search with a packed-FMA fast pass in front of the exact distance.
+// Receiver and donor rows are zero-filled at missing cells (as staged above); with m_r the
+// receiver's 0/1 present mask, the fast pass accumulates Σ_f fma(−m_r, x_d, x_r)² over all
+// features with v_pk_fma_f32 (two features per instruction, the same even/odd accumulator split):
+//   * a COMPLETE donor (md = 0): every term is the exact kernel's term bit for bit (x_r − x_d with
+//     one rounding when both are present, +0 when the receiver is missing), so the sum IS the exact
+//     distance;
+//   * a donor with missing cells: the terms of its missing features that the receiver has
+//     contribute x_r² instead of 0.  corr = Σ of those x_r² (a uniform loop over the donor's few
+//     missing features) gives a lower bound lb = (fast − corr) − 2⁻¹⁶·(fast + corr) of the exact
+//     sum (≤ ~100 roundings of ≤ 2⁻²⁴ each); a donor whose bound cannot beat the receiver's current
+//     worst slot is skipped — exactly, since the slot test is strict — and only the others run
+//     the exact masked direct-difference pass of knn_donor_kernel.
+// The exact pass decides every update, so the donors equal knn_donor_kernel's bit for bit (tested).
+template <int FMAX>
+__global__ __launch_bounds__(256) void knn_donor_fast_kernel(
+    const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
+    const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
+    int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best) {
+  constexpr int LD = (FMAX + 3) / 4 * 4;
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* ds = sm;
+  unsigned long long* dm = (unsigned long long*)(ds + kKnnTile * LD);
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  const bool active = r < nr;
+  const int d_begin = blockIdx.y * per_split;
+  const int d_end = min(nd, d_begin + per_split);
+  float xr[LD];
+#pragma unroll
+  for (int f = 0; f < LD; ++f) xr[f] = (active && f < F) ? R[(size_t)r * F + f] : 0.f;
+  const unsigned long long mr = active ? rmask[r] : 0ull;
+  f32x2v xr2[LD / 2], nm2[LD / 2];   // receiver values and −(present) as feature pairs
+#pragma unroll
+  for (int h = 0; h < LD / 2; ++h) {
+    xr2[h] = f32x2v{xr[2 * h], xr[2 * h + 1]};
+    const float m0 = (2 * h < F && !((mr >> (2 * h)) & 1ull)) ? -1.f : -0.f;
+    const float m1 = (2 * h + 1 < F && !((mr >> (2 * h + 1)) & 1ull)) ? -1.f : -0.f;
+    nm2[h] = f32x2v{m0, m1};
+  }
+  int col[kKnnSlots];
+  float bd[kKnnSlots];
+  int bi[kKnnSlots];
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k) {
+    col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
+    bd[k] = INFINITY;
+    bi[k] = -1;
+    any |= col[k] >= 0;
+  }
+  unsigned long long need = 0ull;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k)
+    if (col[k] >= 0) need |= 1ull << col[k];
+  float bmax = INFINITY;
+  const float fF = (float)F;
+  for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
+    __syncthreads();
+    const int nt = min(kKnnTile, d_end - d0);
+    for (int e = threadIdx.x; e < nt * LD; e += 256) {
+      const int rr = e / LD, c = e % LD;
+      ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
+    }
+    if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
+    __syncthreads();
+    if (!any) continue;
+    for (int t = 0; t < nt; ++t) {
+      const unsigned long long md = dm[t];
+      if ((need & ~md) == 0ull) continue;
+      const int present = F - __builtin_popcountll(mr | md);
+      if (present <= 0) continue;
+      const float scale = fF / (float)present;
+      const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
+      // ---- fast pass: packed fma over feature pairs, even features into .x, odd into .y
+      f32x2v acc = f32x2v{0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < LD / 4; ++q) {
+        if (4 * q < F) {
+          const float4 v = xd4[q];
+          const f32x2v u0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{v.x, v.y}, xr2[2 * q]);
+          const f32x2v u1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{v.z, v.w}, xr2[2 * q + 1]);
+          acc = __builtin_elementwise_fma(u0, u0, acc);
+          acc = __builtin_elementwise_fma(u1, u1, acc);
+        }
+      }
+      const float sf = acc.x + acc.y;
+      bool exact = md == 0ull;
+      if (!exact) {
+        // the receiver-present features the donor lacks added x_r² each: a uniform loop (the
+        // donor's missing cells, usually one), register index from a scalar
+        float corr = 0.f;
+        unsigned long long mm = md & ~mr & ((F >= 64) ? ~0ull : ((1ull << F) - 1ull));
+        while (mm) {
+          const int f = __builtin_ctzll(mm);
+          mm &= mm - 1ull;
+          float xv = 0.f;
+#pragma unroll
+          for (int g = 0; g < LD; ++g) xv = g == f ? xr[g] : xv;
+          corr = fmaf(xv, xv, corr);
+        }
+        // ≤ 32 fma roundings per accumulator in either pass, ≤ 64 in corr, one subtraction: ≤ ~100
+        // units of 2^-24 of (fast + corr); 2^-16 = 256 units
+        const float lb = (sf - corr) - 1.52587890625e-05f * (sf + corr);
+        // a donor whose lower bound (scaled, rounded down a further 2^-20) reaches the worst
+        // active slot can improve no slot: skipped, exactly as the exact pass would skip it
+        if (!(fmaxf(lb, 0.f) * scale * 0.99999905f < bmax)) continue;
+      } else if (!(fmaxf(sf, 0.f) * scale < bmax)) {
+        continue;
+      }
+      float s = sf;
+      if (!exact) {
+        // ---- exact pass (knn_donor_kernel's masked direct differences, same order and roundings)
+        const unsigned long long both = ~(mr | md);
+        const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < LD / 4; ++q) {
+          if (4 * q < F) {
+            const float4 v = xd4[q];
+            const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+            const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
+            const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
+            const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
+            const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
+            s0 = fmaf(a, a, s0);
+            s1 = fmaf(b, b, s1);
+            s0 = fmaf(c, c, s0);
+            s1 = fmaf(d, d, s1);
+          }
+        }
+        s = s0 + s1;
+      }
+      const float dist = fmaxf(s, 0.f) * scale;
+      if (!(dist < bmax)) continue;
+      const int di = d0 + t;
+      float m = 0.f;
+#pragma unroll
+      for (int k = 0; k < kKnnSlots; ++k) {
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < bd[k]) { bd[k] = dist; bi[k] = di; }
+        if (col[k] >= 0) m = fmaxf(m, bd[k]);
+      }
+      bmax = m;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < kKnnSlots; ++k) {
+      if (bi[k] >= 0) {
+        const unsigned long long key =
+            ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned long long)(unsigned)bi[k];
+        atomicMin(&best[(size_t)r * kKnnSlots + k], key);
+      }
+    }
+  }
+}
+
 void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
                 uintptr_t slot_col, uintptr_t best, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_donors: 1 <= F <= 64 (64-bit missing masks)");
@@ -139,14 +297,22 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   int per = (nd + splits - 1) / splits;
   per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
   splits = (nd + per - 1) / per;
+  const char* kenv = std::getenv("HFENS_KNN_KERNEL");
+  const bool direct = kenv && kenv[0] == 'd';   // "direct": the exact pass for every donor
   auto go = [&](auto fm) {
     constexpr int FM = decltype(fm)::value;
     constexpr int LD = (FM + 3) / 4 * 4;
     const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
-    hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
-                       (const unsigned long long*)rmask, nr, (const float*)D,
-                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                       (unsigned long long*)best);
+    if (direct)
+      hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
+                         (const unsigned long long*)rmask, nr, (const float*)D,
+                         (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
+                         (unsigned long long*)best);
+    else
+      hipLaunchKernelGGL(knn_donor_fast_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
+                         (const unsigned long long*)rmask, nr, (const float*)D,
+                         (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
+                         (unsigned long long*)best);
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});

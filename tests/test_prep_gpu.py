@@ -66,3 +66,22 @@ def test_lasso_speculative_refit_bit_identical(dev, monkeypatch):
     assert out[False][0] == out[True][0]
     assert torch.equal(out[False][1], out[True][1])
     assert out[False][2] == out[True][2]
+
+
+@pytest.mark.parametrize("n,F,nan", [(20000, 40, 0.02), (6000, 17, 0.1), (3000, 64, 0.3), (4000, 33, 0.0)])
+def test_knn_fast_pass_same_donors(dev, monkeypatch, n, F, nan):
+    """the packed-FMA fast pass with its exact lower-bound skip
+    (knn_donor_fast_kernel, default) picks the SAME donors as the exact masked direct-difference
+    kernel for every missing cell (HFENS_KNN_KERNEL=direct): identical imputed matrices, exact ties
+    (binary features, duplicated rows) included."""
+    X, _, _ = make_hf_cohort(n, F, seed=3 * n + F, nan_frac=nan)
+    X = np.concatenate([X, X[: n // 10]], axis=0)            # duplicated rows: exact distance ties
+    if nan == 0.0:
+        X[::7, 3] = np.nan                                   # a few receivers still
+    Xt = torch.as_tensor(X, device=dev)
+    out = {}
+    for k in ("direct", "fast"):
+        monkeypatch.setenv("HFENS_KNN_KERNEL", k)
+        imp = KNNImputer(n_neighbors=1).fit(Xt)
+        out[k] = imp.transform(Xt).cpu()
+    assert torch.equal(out["direct"], out["fast"])
