@@ -88,6 +88,8 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             from .models.stack_trainer import plan_stacking
             y_ev.synchronize()
             plan_box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
+    from .utils.timing import hmark
+    hmark("develop")
     with timer.stage("impute"):
         if group is None:
             imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(X_dev)
@@ -101,17 +103,21 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         if dev.type == "cuda" and AUX_STREAM:
             from . import runtime
             aux = runtime.stream(dev, "aux")
+        hmark("imputer_fit")
         X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
+        hmark("impute_enqueued")
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
     fit_group = None if task else group
     with timer.stage("select"):
         sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=overlap)
+        hmark("lasso_fit")
         mask = sfm.get_support()
         mt = torch.as_tensor(mask, device=dev)
         X_dev_optm = X_dev[:, mt]
         fn_new = [n for n, m in zip(names, mask) if m]
+        hmark("selected")
     clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None,
             plan=plan_box.get("plan"))
     if aux is not None:
