@@ -377,7 +377,7 @@ def bench_gbdt(a):
             "infer_rows_x_models_per_sec": round(n_hold * seeds / max(t_inf, 1e-12), 1) if t_inf == t_inf else None,
             "fp8_leaf_inference": None if fp8 is None else {
                 "leaf_dtype": "fp8 e4m3 two-term (hi + lo), per-model power-of-two scale",
-                "kernel": "forest_fp8: leaf one-hot x fp8 leaf values, v_mfma_f32_16x16x32_fp8_fp8",
+                "kernel": "forest_fp8: leaf one-hot x fp8 leaf values, v_mfma_scale_f32_16x16x128_f8f6f4",
                 "auroc": round(float(fp8["auroc"]), 5), "auroc_fp32_tables": round(float(auc), 5),
                 "auroc_delta": round(float(fp8["auroc"] - auc), 6), "max_abs_raw_err": fp8["max_raw_err"],
                 "rows_x_models_per_sec": round(n_hold * seeds / max(fp8["t"], 1e-12), 1)},

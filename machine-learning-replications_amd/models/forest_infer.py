@@ -115,13 +115,15 @@ class Fp8Forest:
         self.inv_scale = (1.0 / sigma).to(torch.float32)
         self.init = torch.tensor([float(m.init_raw_) for m in models], dtype=torch.float64)
         Kall = S * K
-        self.Q = Q = -(-Kall // 32)
-        Bm = torch.zeros(Q * 32, 16, dtype=torch.uint8)
+        # K steps of 128 slots (gfx950 v_mfma_scale_f32_16x16x128_f8f6f4): lane ℓ = 16·g + column
+        # holds slots 128q + 32g + j, j < 32, of its column — the A side's order (forest_fp8.hip)
+        self.Q = Q = -(-Kall // 128)
+        Bm = torch.zeros(Q * 128, 16, dtype=torch.uint8)
         for s_ in range(S):
             Bm[s_ * K:(s_ + 1) * K, s_] = hi[s_].view(torch.uint8)
             Bm[s_ * K:(s_ + 1) * K, S + s_] = lo[s_].view(torch.uint8)
-        frag = Bm.view(Q, 4, 8, 16).permute(0, 1, 3, 2).reshape(Q, 64, 8).contiguous()   # [q][lane][j]
-        self.bfrag = frag.view(torch.int64).reshape(Q * 64)
+        frag = Bm.view(Q, 4, 32, 16).permute(0, 1, 3, 2).reshape(Q, 64, 32).contiguous()   # [q][lane][j]
+        self.bfrag = frag.view(torch.int64).reshape(Q * 64 * 4)
         self.nodes_all = nodes.reshape(S * T, NI).to(torch.int16)   # (blo << 8 | feat) ≤ 0xFFFF as i16 bits
         self.device = dev
         self._dev_cache = None

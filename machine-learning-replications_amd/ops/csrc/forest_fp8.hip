@@ -10,23 +10,27 @@
 // and the split costs nothing: the MFMA's N = 16 is there anyway.  Products 1·fp8 are exact and
 // accumulate in f32; the end result is ≈ 2^-8-relative per leaf value (fp8 alone: 2^-4).
 //
-// One wave computes 16 rows × all K with v_mfma_f32_16x16x32_fp8_fp8: per 32-slot K step, lane ℓ
-// builds its A fragment — rows ℓ mod 16, slots 8⌊ℓ/16⌋ … +7 — by walking the (≤ 4 for stumps)
-// trees those slots belong to on the row's bins (LDS), and reads its B fragment (one 8-byte word,
-// pre-swizzled on the host into the MFMA's lane order) from LDS.  Workgroups are persistent over
+// One wave computes 16 rows × all K with gfx950's block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+// (e4m3 operands, unit E8M0 scales): per 128-slot K step, lane ℓ builds its A fragment — row ℓ mod
+// 16, slots 32⌊ℓ/16⌋ … +31 (32 bytes) — by walking the (≤ 16 for stumps) trees those slots belong
+// to on the row's bins (LDS), and reads its B fragment (32 bytes, pre-swizzled on the host into the
+// same lane / byte → slot order) from LDS.  A and B use one (lane group, byte) → k assignment, so
+// the product sums every slot once whatever the hardware's internal k order.  4× fewer MFMAs than
+// the gfx940-era 16x16x32 fp8 form; the tree walks that build the one-hot dominate either way.  Workgroups are persistent over
 // 64-row tiles, so V, the tree table and the fragment layout are staged in LDS once per workgroup.
 #include "common.h"
 
 namespace hfens {
 
 typedef float f8x4_acc __attribute__((ext_vector_type(4)));
+typedef int f8x8i __attribute__((ext_vector_type(8)));
 
 struct F8Job {
   const unsigned char* bins;          // [F][ldb] u8 feature-major bins
   long long ldb, n;
-  int F, T, d, Q, S;                  // features, trees, depth, K steps (K_pad / 32), models
+  int F, T, d, Q, S;                  // features, trees, depth, K steps (K_pad / 128), models
   const unsigned short* nodes;        // [T][2^d − 1] internal heap nodes: (blo << 8) | feat, feat 255 = leaf
-  const unsigned long long* bfrag;    // [Q][64] B fragments (8 × fp8 each, MFMA lane order)
+  const unsigned long long* bfrag;    // [Q][64][4] B fragments (32 × fp8 per lane, MFMA lane order)
   const float* inv_scale;             // [S]
   const double* init;                 // [S]
   float* out;                         // [S][n]
@@ -39,13 +43,13 @@ constexpr unsigned kF8One = 0x38u;    // e4m3: 1.0
 __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int stage_b, int stage_nodes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char f8_lds[];
   const int NI = (1 << J.d) - 1;
-  unsigned long long* sb = reinterpret_cast<unsigned long long*>(f8_lds);                 // [Q][64]
-  unsigned short* sn = reinterpret_cast<unsigned short*>(f8_lds + (stage_b ? (size_t)J.Q * 64 * 8 : 0));
-  unsigned char* rb = f8_lds + (stage_b ? (size_t)J.Q * 64 * 8 : 0) +
+  unsigned long long* sb = reinterpret_cast<unsigned long long*>(f8_lds);                 // [Q][64][4]
+  unsigned short* sn = reinterpret_cast<unsigned short*>(f8_lds + (stage_b ? (size_t)J.Q * 64 * 32 : 0));
+  unsigned char* rb = f8_lds + (stage_b ? (size_t)J.Q * 64 * 32 : 0) +
                       (stage_nodes ? (((size_t)J.T * NI * 2 + 15) & ~(size_t)15) : 0);    // [waves][16][F]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (stage_b)
-    for (int i = tid; i < J.Q * 64; i += blockDim.x) sb[i] = J.bfrag[i];
+    for (int i = tid; i < J.Q * 64 * 4; i += blockDim.x) sb[i] = J.bfrag[i];
   if (stage_nodes)
     for (int i = tid; i < J.T * NI; i += blockDim.x) sn[i] = J.nodes[i];
   __syncthreads();
@@ -68,11 +72,11 @@ __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int 
     const unsigned char* rowb = myb + r * J.F;
     f8x4_acc acc = {0.f, 0.f, 0.f, 0.f};
     for (int q = 0; q < J.Q; ++q) {
-      const int k0 = 32 * q + 8 * kb;
-      unsigned lo = 0u, hi = 0u;
+      const int k0 = 128 * q + 32 * kb;
+      unsigned w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       int tprev = -1, leaf = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 32; ++j) {
         const int k = k0 + j;
         const int t = k >> J.d;
         if (t != tprev) {
@@ -90,12 +94,15 @@ __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int 
           leaf = h - (L - 1);
         }
         const unsigned byte = (t < J.T && (k & (L - 1)) == leaf) ? kF8One : 0u;
-        if (j < 4) lo |= byte << (8 * j);
-        else hi |= byte << (8 * (j - 4));
+        w[j >> 2] |= byte << (8 * (j & 3));
       }
-      const long a = (long)(((unsigned long long)hi << 32) | lo);
-      const long b = (long)Bf[(size_t)q * 64 + lane];
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, acc, 0, 0, 0);
+      const f8x8i a = {(int)w[0], (int)w[1], (int)w[2], (int)w[3], (int)w[4], (int)w[5], (int)w[6], (int)w[7]};
+      const unsigned long long* bq = Bf + ((size_t)q * 64 + lane) * 4;
+      const f8x8i b = {(int)(unsigned)bq[0], (int)(unsigned)(bq[0] >> 32), (int)(unsigned)bq[1],
+                       (int)(unsigned)(bq[1] >> 32), (int)(unsigned)bq[2], (int)(unsigned)(bq[2] >> 32),
+                       (int)(unsigned)bq[3], (int)(unsigned)(bq[3] >> 32)};
+      // fmt 0/0 = e4m3 A and B; scales 127 = 2^0 (E8M0) for both
+      acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, 127, 0, 127);
     }
     // C: lane ℓ holds rows 4⌊ℓ/16⌋ + i (i < 4) of column ℓ mod 16; model s = hi column s + lo column S + s
     const int col = lane & 15;
@@ -120,9 +127,9 @@ void forest_fp8(uintptr_t bins, long long ldb, long long n, int F, int T, int d,
   HFENS_REQUIRE(F >= 1 && F <= kF8MaxF, "forest_fp8: 1 <= F <= 128");
   HFENS_REQUIRE(d >= 1 && d <= 5 && T >= 1, "forest_fp8: depth 1..5");
   HFENS_REQUIRE(S >= 1 && 2 * S <= 16, "forest_fp8: 1..8 models per launch (hi/lo columns of one 16-wide tile)");
-  HFENS_REQUIRE((long long)Q * 32 >= (long long)T << d, "forest_fp8: K steps do not cover the leaf slots");
+  HFENS_REQUIRE((long long)Q * 128 >= (long long)T << d, "forest_fp8: K steps do not cover the leaf slots");
   if (n == 0) return;
-  const size_t bsz = (size_t)Q * 64 * 8;
+  const size_t bsz = (size_t)Q * 64 * 32;
   const size_t nsz = (((size_t)T * ((1 << d) - 1) * 2) + 15) & ~(size_t)15;
   const size_t rsz = (size_t)kF8Waves * 16 * F;
   int stage_b = 1, stage_n = 1;

@@ -175,7 +175,10 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   for (int k = 0; k < kKnnSlots; ++k)
     if (col[k] >= 0) need |= 1ull << col[k];
   float bmax = INFINITY;
-  const float fF = (float)F;
+  // F / present for every present count, the same IEEE division as the exact kernel, looked up
+  // instead of recomputed per donor (a full-precision f32 divide is ~10 VALU instructions)
+  __shared__ float s_scale[65];
+  if (threadIdx.x <= 64) s_scale[threadIdx.x] = threadIdx.x > 0 ? (float)F / (float)threadIdx.x : 0.f;
   for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
     __syncthreads();
     const int nt = min(kKnnTile, d_end - d0);
@@ -191,19 +194,19 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
       if ((need & ~md) == 0ull) continue;
       const int present = F - __builtin_popcountll(mr | md);
       if (present <= 0) continue;
-      const float scale = fF / (float)present;
+      const float scale = s_scale[present];
       const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
       // ---- fast pass: packed fma over feature pairs, even features into .x, odd into .y
       f32x2v acc = f32x2v{0.f, 0.f};
+      // every quad, F or not: features ≥ F are zero on both sides (fma(0, 0, acc) = acc), and a
+      // runtime `4q < F` guard would put a branch and an LDS wait between the quads' reads
 #pragma unroll
       for (int q = 0; q < LD / 4; ++q) {
-        if (4 * q < F) {
-          const float4 v = xd4[q];
-          const f32x2v u0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{v.x, v.y}, xr2[2 * q]);
-          const f32x2v u1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{v.z, v.w}, xr2[2 * q + 1]);
-          acc = __builtin_elementwise_fma(u0, u0, acc);
-          acc = __builtin_elementwise_fma(u1, u1, acc);
-        }
+        const float4 v = xd4[q];
+        const f32x2v u0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{v.x, v.y}, xr2[2 * q]);
+        const f32x2v u1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{v.z, v.w}, xr2[2 * q + 1]);
+        acc = __builtin_elementwise_fma(u0, u0, acc);
+        acc = __builtin_elementwise_fma(u1, u1, acc);
       }
       const float sf = acc.x + acc.y;
       bool exact = md == 0ull;
@@ -236,19 +239,17 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
         const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-        for (int q = 0; q < LD / 4; ++q) {
-          if (4 * q < F) {
-            const float4 v = xd4[q];
-            const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
-            const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
-            const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
-            const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
-            const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
-            s0 = fmaf(a, a, s0);
-            s1 = fmaf(b, b, s1);
-            s0 = fmaf(c, c, s0);
-            s1 = fmaf(d, d, s1);
-          }
+        for (int q = 0; q < LD / 4; ++q) {   // (features ≥ F: 0 − 0 on both sides, adds 0)
+          const float4 v = xd4[q];
+          const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+          const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
+          const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
+          const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
+          const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
+          s0 = fmaf(a, a, s0);
+          s1 = fmaf(b, b, s1);
+          s0 = fmaf(c, c, s0);
+          s1 = fmaf(d, d, s1);
         }
         s = s0 + s1;
       }

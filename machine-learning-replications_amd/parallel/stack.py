@@ -18,9 +18,16 @@ from . import dist as pdist
 
 
 def fit_svc_batch_distributed(svcs, Zs, ys, group):
-    """``Zs[f]`` / ``ys[f]``: this rank's rows of fit ``f``.  Exact-solver fits are all-gathered and
-    solved task-parallel (below); large fits (:func:`use_lowrank` on the GLOBAL sizes) stay
-    row-sharded and every rank works on every interior-point solve (svc_lowrank, data parallel)."""
+    """``Zs[f]`` / ``ys[f]``: this rank's rows of fit ``f``."""
+    return finish_svc_batch_distributed(launch_svc_batch_distributed(svcs, Zs, ys, group), group)
+
+
+def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
+    """Exact-solver fits: all-gather every fit's rows (collective), then enqueue this rank's fits on
+    the current stream (no host sync after the SMO launch).  Large fits (:func:`use_lowrank` on the
+    GLOBAL sizes) stay row-sharded instead: every rank works on every interior-point solve
+    (svc_lowrank, data parallel), synchronously.  Collectives stay on the calling thread, so all
+    ranks issue them in one order on one communicator."""
     sizes = pdist.all_reduce_sum_f64([torch.tensor([float(y.numel()) for y in ys], dtype=torch.float64,
                                                    device=pdist._default_device(group))], group)[0]
     if use_lowrank([int(v) for v in sizes.tolist()]):
@@ -29,14 +36,8 @@ def fit_svc_batch_distributed(svcs, Zs, ys, group):
         smo.LAST_SMO_INFO.clear()
         smo.LAST_SMO_INFO.update(solver="nystrom-ipm", problems=6 * len(svcs), max_l=int(sizes.max()),
                                  row_sharded=True)
-        return fit_svc_lowrank_batch(svcs, Zs, ys, group=group)
-    return finish_svc_batch_distributed(launch_svc_batch_distributed(svcs, Zs, ys, group), group)
-
-
-def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
-    """All-gather every fit's rows (collective), then enqueue this rank's fits on the current
-    stream (no host sync after the SMO launch).  Collectives stay on the calling thread, so all
-    ranks issue them in one order on one communicator."""
+        fit_svc_lowrank_batch(svcs, Zs, ys, group=group)
+        return dict(svcs=svcs, Zs=Zs, st=None, done=True)
     world, rank = pdist.dist.get_world_size(group), pdist.dist.get_rank(group)
     full_Z = [pdist.all_gather_rows(Z, group) for Z in Zs]
     full_y = [pdist.all_gather_rows(y[:, None].to(torch.float64), group)[:, 0] for y in ys]
@@ -50,6 +51,8 @@ def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
 def finish_svc_batch_distributed(pre: dict, group):
     """Complete this rank's fits, then broadcast every fit from its owner (collectives)."""
     svcs, Zs = pre["svcs"], pre["Zs"]
+    if pre.get("done"):
+        return svcs
     if pre["st"] is not None:
         finish_svc_batch(pre["st"])
     return broadcast_svc_fits(svcs, Zs, group)
