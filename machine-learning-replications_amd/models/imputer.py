@@ -87,7 +87,9 @@ class KNNImputer(Estimator):
         F = Xs[0].shape[1]
         if F > 64:
             raise ValueError("KNNImputer device path supports at most 64 features")
+        from ..utils.timing import hmark
         host = torch.cat([_masks_u64(torch.isnan(X)) for X in Xs] + [self._valid.to(torch.int64)]).cpu().numpy()
+        hmark("imp_masks_read")
         bits_all = host[:-F].view(np.uint64)
         from .smo import _to_dev
         dev = Xs[0].device
@@ -102,6 +104,7 @@ class KNNImputer(Estimator):
             if st is None:
                 self._impute_device(X, bits, D32, dm)
                 out.append(X.index_select(1, keep))
+                hmark("imp_main_enqueued")
             else:
                 # everything that touches X — the imputation AND the column selection — is queued
                 # on st; the caller joins st before reading the result
@@ -127,6 +130,8 @@ class KNNImputer(Estimator):
         center = self._col_mean
         Rm_np = ((bits[rows_np, None] >> np.arange(F, dtype=np.uint64)) & np.uint64(1)).astype(bool)
         rl, cc = np.nonzero(Rm_np)                       # missing cells, row-major, columns ascending
+        from ..utils.timing import hmark
+        hmark("imp_plan")
         nm = Rm_np.sum(1)
         start = np.concatenate([[0], np.cumsum(nm)[:-1]])
         kk = np.arange(rl.shape[0]) - start[rl]          # slot of each cell within its row
@@ -142,6 +147,7 @@ class KNNImputer(Estimator):
         buf = _to_dev(np.concatenate([a.astype(np.int64, copy=False) for a in parts]), dev)
         o = np.concatenate([[0], np.cumsum(sizes)])
         rows, Rm, rm, slot_dev, flat, r_idx, c_idx = (buf[o[i]:o[i + 1]] for i in range(7))
+        hmark("imp_h2d")
         Rm = (Rm != 0).view(nr, F)
         slot_dev = slot_dev.view(nr, nslot).to(torch.int32)
         Xr = X.index_select(0, rows)
@@ -155,6 +161,7 @@ class KNNImputer(Estimator):
                          D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), ops.stream_ptr(dev))
             if nslot != SLOTS:
                 best[:, s0:s0 + SLOTS] = blk
+        hmark("imp_knn_launched")
         # packed (d² float bits << 32 | donor); all-ones = no donor with a defined distance
         b = best.view(-1).index_select(0, flat)
         donor = torch.where(b == -1, torch.full_like(b, -1), b & 0xFFFFFFFF)
