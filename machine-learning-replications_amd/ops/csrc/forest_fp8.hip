@@ -40,7 +40,12 @@ constexpr int kF8Waves = 4;
 constexpr int kF8MaxF = 128;
 constexpr unsigned kF8One = 0x38u;    // e4m3: 1.0
 
+// DEPTH = tree depth: the 32 slots a lane owns per K step hold NT = 32 / 2^DEPTH whole trees, walked
+// level-synchronously (all NT node reads, then all NT bin reads, per level) so their LDS latencies
+// overlap instead of chaining tree after tree.
+template <int DEPTH>
 __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int stage_b, int stage_nodes) {
+  constexpr int LT = 1 << DEPTH, NT = 32 / LT, NIT = LT - 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char f8_lds[];
   const int NI = (1 << J.d) - 1;
   unsigned long long* sb = reinterpret_cast<unsigned long long*>(f8_lds);                 // [Q][64][4]
@@ -56,7 +61,6 @@ __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int 
   const unsigned long long* Bf = stage_b ? sb : J.bfrag;
   const unsigned short* Nd = stage_nodes ? sn : J.nodes;
   unsigned char* myb = rb + (size_t)wave * 16 * J.F;
-  const int L = 1 << J.d;
   const int r = lane & 15, kb = lane >> 4;
   const long long tiles = (J.n + 15) / 16;
   for (long long tile = (long long)blockIdx.x * kF8Waves + wave; tile < tiles; tile += (long long)gridDim.x * kF8Waves) {
@@ -74,27 +78,34 @@ __global__ __launch_bounds__(kF8Waves * 64) void forest_fp8_kernel(F8Job J, int 
     for (int q = 0; q < J.Q; ++q) {
       const int k0 = 128 * q + 32 * kb;
       unsigned w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-      int tprev = -1, leaf = 0;
+      const int t0 = k0 >> DEPTH;          // the lane's first tree (k0 is a multiple of 32 ≥ LT)
+      int h[NT];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int k = k0 + j;
-        const int t = k >> J.d;
-        if (t != tprev) {
-          tprev = t;
-          int h = 0;
-          if (t < J.T) {
-            const unsigned short* tn = Nd + (size_t)t * NI;
-            for (int lev = 0; lev < J.d; ++lev) {
-              const unsigned nd = tn[h];
-              const unsigned f = nd & 0xFFu;
-              const int right = (f != 0xFFu) && (rowb[f < (unsigned)J.F ? f : 0u] > (nd >> 8));
-              h = 2 * h + 1 + right;
-            }
-          }
-          leaf = h - (L - 1);
+      for (int i = 0; i < NT; ++i) h[i] = 0;
+#pragma unroll
+      for (int lev = 0; lev < DEPTH; ++lev) {
+        unsigned nd[NT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) nd[i] = t0 + i < J.T ? Nd[(size_t)(t0 + i) * NIT + h[i]] : 0xFFu;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const unsigned f = nd[i] & 0xFFu;
+          const int right = (f != 0xFFu) && (rowb[f < (unsigned)J.F ? f : 0u] > (nd[i] >> 8));
+          h[i] = 2 * h[i] + 1 + right;
         }
-        const unsigned byte = (t < J.T && (k & (L - 1)) == leaf) ? kF8One : 0u;
-        w[j >> 2] |= byte << (8 * (j & 3));
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (t0 + i >= J.T) continue;
+        const int leaf = h[i] - (LT - 1);            // slot i·LT + leaf of the lane's 32
+        if constexpr (LT <= 4) {
+          const int dw = (i * LT) >> 2;              // the tree's slots lie in one dword
+          w[dw] |= kF8One << (8 * (((i * LT) & 3) + leaf));
+        } else {
+#pragma unroll
+          for (int c = 0; c < LT / 4; ++c)
+            w[(i * LT >> 2) + c] |= (leaf >> 2) == c ? kF8One << (8 * (leaf & 3)) : 0u;
+        }
       }
       const f8x8i a = {(int)w[0], (int)w[1], (int)w[2], (int)w[3], (int)w[4], (int)w[5], (int)w[6], (int)w[7]};
       const unsigned long long* bq = Bf + ((size_t)q * 64 + lane) * 4;
@@ -145,8 +156,15 @@ void forest_fp8(uintptr_t bins, long long ldb, long long n, int F, int T, int d,
   if (g > cap) g = cap;
   F8Job J{(const unsigned char*)bins, ldb, n, F, T, d, Q, S, (const unsigned short*)nodes,
           (const unsigned long long*)bfrag, (const float*)inv_scale, (const double*)init, (float*)out};
-  hipLaunchKernelGGL(forest_fp8_kernel, dim3((unsigned)g), dim3(kF8Waves * 64), lds, as_stream(stream), J, stage_b,
-                     stage_n);
+  switch (d) {
+#define F8_CASE(D)                                                                                            \
+  case D:                                                                                                    \
+    hipLaunchKernelGGL(forest_fp8_kernel<D>, dim3((unsigned)g), dim3(kF8Waves * 64), lds, as_stream(stream), J, \
+                       stage_b, stage_n);                                                                    \
+    break;
+    F8_CASE(1) F8_CASE(2) F8_CASE(3) F8_CASE(4) F8_CASE(5)
+#undef F8_CASE
+  }
   launch_check();
 }
 
