@@ -53,13 +53,20 @@ class KNNImputer(Estimator):
     def transform(self, X):
         return self.transform_many([X])[0]
 
-    def transform_many(self, Xs, streams=None):
+    def transform_many(self, Xs, streams=None, defer=False):
         """Impute several matrices with ONE device→host read for all of them (the per-row
         missing-column bitmasks).  ``streams[i]`` (device path): the stream matrix i's donor
-        search is queued on (it waits for the current stream first)."""
+        search is queued on (it waits for the current stream first).  ``defer`` (device path):
+        the side-stream matrices are NOT planned and launched here; the call returns
+        ``(outs, run)`` and ``run()`` does it later — their host-side planning (≈ 1 ms at 10k
+        rows) then runs where the caller's thread would otherwise wait on the device — and
+        returns the finished list (those matrices only ever waited for this transform's inputs)."""
         Xs = [as_tensor(X, device=self._fit_X.device).clone() for X in Xs]
         if Xs and Xs[0].is_cuda and self.n_neighbors == 1:
-            return self._impute_device_many(Xs, streams)
+            return self._impute_device_many(Xs, streams, defer)
+        if defer:
+            done = self.transform_many(Xs)
+            return done, (lambda: done)
         for X in Xs:
             miss = torch.isnan(X)
             rows = torch.nonzero(miss.any(1)).squeeze(1)
@@ -80,7 +87,7 @@ class KNNImputer(Estimator):
             pr = self._prep = (self._fit_X, D32, dm)
         return pr[1], pr[2]
 
-    def _impute_device_many(self, Xs, streams):
+    def _impute_device_many(self, Xs, streams, defer=False):
         """The (row, column) work lists are built with numpy from the bitmasks and uploaded
         non-blocking, so the donor launches and the scatters queue without further host
         synchronisation."""
@@ -96,7 +103,9 @@ class KNNImputer(Estimator):
         keep = _to_dev(np.nonzero(host[-F:])[0].astype(np.int64), dev)   # columns with a fit value
         D32, dm = self._fit_prep()
         main = torch.cuda.current_stream(dev)
-        off, out = 0, []
+        ready = torch.cuda.Event()
+        ready.record(main)          # the inputs of every matrix: masks, fit operands, X itself
+        off, out, jobs = 0, [], []
         for i, X in enumerate(Xs):
             bits = bits_all[off:off + X.shape[0]]
             off += X.shape[0]
@@ -106,18 +115,33 @@ class KNNImputer(Estimator):
                 out.append(X.index_select(1, keep))
                 hmark("imp_main_enqueued")
             else:
-                # everything that touches X — the imputation AND the column selection — is queued
-                # on st; the caller joins st before reading the result
-                st.wait_stream(main)
-                # X, keep and the fit operands were allocated on the current stream: without
-                # record_stream their blocks could be handed to new current-stream tensors while st
-                # still reads / writes them
-                for t in (X, keep, D32, dm, self._fit_X, self._col_mean):
-                    t.record_stream(st)
-                with torch.cuda.stream(st):
-                    self._impute_device(X, bits, D32, dm)
-                    out.append(X.index_select(1, keep))
-        return out
+                def job(i=i, X=X, bits=bits, st=st):
+                    # everything that touches X — the imputation AND the column selection — is
+                    # queued on st; the caller joins st before reading the result
+                    st.wait_event(ready)
+                    # X, keep and the fit operands were allocated on the current stream: without
+                    # record_stream their blocks could be handed to new current-stream tensors while
+                    # st still reads / writes them
+                    for t in (X, keep, D32, dm, self._fit_X, self._col_mean):
+                        t.record_stream(st)
+                    with torch.cuda.device(dev), torch.cuda.stream(st):
+                        self._impute_device(X, bits, D32, dm)
+                        out[i] = X.index_select(1, keep)
+                out.append(None)
+                jobs.append(job)
+        if not defer:
+            for job in jobs:
+                job()
+            return out
+        state = {"done": False}
+
+        def run():
+            if not state["done"]:
+                for job in jobs:
+                    job()
+                state["done"] = True
+            return out
+        return out, run
 
     def _impute_device(self, X, bits, D32, dm):
         from .. import ops

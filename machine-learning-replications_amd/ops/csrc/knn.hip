@@ -189,27 +189,16 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
     __syncthreads();
     if (!any) continue;
-    for (int t = 0; t < nt; ++t) {
+    // donors two at a time: their fast sums are independent fma chains (each 2 × ≤ 32 dependent
+    // steps: the accumulation order must stay the exact kernel's), interleaved to hide the latency;
+    // the bookkeeping then runs donor t before donor t + 1, exactly as one at a time
+    auto donor = [&](int t, float sf) {
       const unsigned long long md = dm[t];
-      if ((need & ~md) == 0ull) continue;
+      if ((need & ~md) == 0ull) return;
       const int present = F - __builtin_popcountll(mr | md);
-      if (present <= 0) continue;
+      if (present <= 0) return;
       const float scale = s_scale[present];
-      const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
-      // ---- fast pass: packed fma over feature pairs, even features into .x, odd into .y
-      f32x2v acc = f32x2v{0.f, 0.f};
-      // every quad, F or not: features ≥ F are zero on both sides (fma(0, 0, acc) = acc), and a
-      // runtime `4q < F` guard would put a branch and an LDS wait between the quads' reads
-#pragma unroll
-      for (int q = 0; q < LD / 4; ++q) {
-        const float4 v = xd4[q];
-        const f32x2v u0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{v.x, v.y}, xr2[2 * q]);
-        const f32x2v u1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{v.z, v.w}, xr2[2 * q + 1]);
-        acc = __builtin_elementwise_fma(u0, u0, acc);
-        acc = __builtin_elementwise_fma(u1, u1, acc);
-      }
-      const float sf = acc.x + acc.y;
-      bool exact = md == 0ull;
+      const bool exact = md == 0ull;
       if (!exact) {
         // the receiver-present features the donor lacks added x_r² each: a uniform loop (the
         // donor's missing cells, usually one), register index from a scalar
@@ -228,13 +217,14 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
         const float lb = (sf - corr) - 1.52587890625e-05f * (sf + corr);
         // a donor whose lower bound (scaled, rounded down a further 2^-20) reaches the worst
         // active slot can improve no slot: skipped, exactly as the exact pass would skip it
-        if (!(fmaxf(lb, 0.f) * scale * 0.99999905f < bmax)) continue;
+        if (!(fmaxf(lb, 0.f) * scale * 0.99999905f < bmax)) return;
       } else if (!(fmaxf(sf, 0.f) * scale < bmax)) {
-        continue;
+        return;
       }
       float s = sf;
       if (!exact) {
         // ---- exact pass (knn_donor_kernel's masked direct differences, same order and roundings)
+        const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
         const unsigned long long both = ~(mr | md);
         const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
         float s0 = 0.f, s1 = 0.f;
@@ -254,7 +244,7 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
         s = s0 + s1;
       }
       const float dist = fmaxf(s, 0.f) * scale;
-      if (!(dist < bmax)) continue;
+      if (!(dist < bmax)) return;
       const int di = d0 + t;
       float m = 0.f;
 #pragma unroll
@@ -263,6 +253,29 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
         if (col[k] >= 0) m = fmaxf(m, bd[k]);
       }
       bmax = m;
+    };
+    for (int t = 0; t < nt; t += 2) {
+      const int t1 = t + 1 < nt ? t + 1 : t;
+      const float4* xa = reinterpret_cast<const float4*>(ds + t * LD);
+      const float4* xb = reinterpret_cast<const float4*>(ds + t1 * LD);
+      // ---- fast pass: packed fma over feature pairs, even features into .x, odd into .y — every
+      // quad, F or not (features ≥ F are zero on both sides: fma(0, 0, acc) = acc; a runtime
+      // `4q < F` guard would put a branch and an LDS wait between the quads' reads)
+      f32x2v accA = f32x2v{0.f, 0.f}, accB = f32x2v{0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < LD / 4; ++q) {
+        const float4 va = xa[q], vb = xb[q];
+        const f32x2v a0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{va.x, va.y}, xr2[2 * q]);
+        const f32x2v a1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{va.z, va.w}, xr2[2 * q + 1]);
+        const f32x2v b0 = __builtin_elementwise_fma(nm2[2 * q], f32x2v{vb.x, vb.y}, xr2[2 * q]);
+        const f32x2v b1 = __builtin_elementwise_fma(nm2[2 * q + 1], f32x2v{vb.z, vb.w}, xr2[2 * q + 1]);
+        accA = __builtin_elementwise_fma(a0, a0, accA);
+        accB = __builtin_elementwise_fma(b0, b0, accB);
+        accA = __builtin_elementwise_fma(a1, a1, accA);
+        accB = __builtin_elementwise_fma(b1, b1, accB);
+      }
+      donor(t, accA.x + accA.y);
+      if (t1 != t) donor(t1, accB.x + accB.y);
     }
   }
   if (active) {

@@ -104,14 +104,29 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             from . import runtime
             aux = runtime.stream(dev, "aux")
         hmark("imputer_fit")
-        X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
+        run_sel = None
+        if aux is not None and group is None:
+            # the held-out rows' planning and launch (host numpy, ≈ 1 ms at 10k rows) are deferred
+            # into the LassoCV path's device time below, off the host's critical path
+            (X_dev, _), run_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux], defer=True)
+        else:
+            X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
         hmark("impute_enqueued")
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
     fit_group = None if task else group
     with timer.stage("select"):
-        sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=overlap)
+        lasso_overlap = overlap
+        if run_sel is not None:
+            def lasso_overlap():
+                run_sel()
+                hmark("heldout_impute_enqueued")
+                if overlap is not None:
+                    overlap()
+        sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=lasso_overlap)
+        if run_sel is not None:
+            X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
         hmark("lasso_fit")
         mask = sfm.get_support()
         mt = torch.as_tensor(mask, device=dev)
