@@ -71,6 +71,11 @@ def shutdown():
     if dist.is_initialized():
         from . import xgmi
         xgmi.release_all()
+        # communicators cached per process group (keyed by the group object's id) die with it
+        from ..models import svc_lowrank
+        from . import ensemble
+        svc_lowrank._GROUPS.clear()
+        ensemble._GROUPS.clear()
         dist.destroy_process_group()
 
 
