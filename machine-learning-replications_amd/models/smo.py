@@ -606,7 +606,10 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
     return alpha, rho, iters, err
 
 
-WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.1"))   # inner stop: local gap < frac·gap0
+# inner stop: local gap < frac·gap0.  Swept on the headline (profiles/r3_runs/ws_sweep, 10 steps each):
+# 0.05 39.1, 0.1 34.3, 0.15 33.7, 0.2 31.4-31.8, 0.25 32.2, 0.3 32.8 ms/fit — 0.2 moves 13 % fewer pairs
+# (8.6k vs 9.9k on the critical problem) in about as many rounds (35 vs 34)
+WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.2"))
 # inner pairs per round: the 36 problems advance in lock-step rounds, so one long inner solve holds
 # up every other problem's next round; a cap bounds that wait (the capped problem simply continues
 # in its next working set)
