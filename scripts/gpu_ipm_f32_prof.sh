@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 D=gpurun_out/ipmf32prof
 rm -rf $D && mkdir -p $D
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/raw -o ipm -- python3 scripts/probes/ipm_probe.py 1000000 512 ipm-only > $D/probe.log 2>&1 \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/raw -o ipm -- python3 scripts/probes/ipm_probe.py 1000000 512 ipm-only ${IPM_MAPS:-both} > $D/probe.log 2>&1 \
   || { tail -20 $D/probe.log; exit 1; }
 grep "ipm solve" $D/probe.log
 f=$(find $D/raw -name "*kernel_stats.csv" | head -1)

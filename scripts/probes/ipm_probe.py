@@ -37,7 +37,10 @@ def main():
     if only_ipm:
         c = torch.where(y > 0, 0.625, 2.5).to(torch.float64)
         # f64 Φ (skinny passes over f64) and Φ rounded to f32 (skinny passes over the f32 copy)
-        for tag, P in (("f64 map", Phi), ("f32-rounded map", Phi.to(torch.float32).to(torch.float64))):
+        maps = (("f64 map", Phi), ("f32-rounded map", Phi.to(torch.float32).to(torch.float64)))
+        if len(sys.argv) > 4 and sys.argv[4] == "f32-only":
+            maps = maps[1:]
+        for tag, P in maps:
             ipm_svc_dual(P, y, c, max_iter=3)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
