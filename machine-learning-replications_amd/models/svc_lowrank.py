@@ -103,7 +103,19 @@ FIT_THREADS = int(os.environ.get("HFENS_IPM_FITS", "1"))      # fits solved at a
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 
 
-def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+def _scaled_rows(Phi: torch.Tensor, d: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
+    """diag(d)·Φ: from the exact f32 copy in one native pass when there is one (half the read
+    bytes of torch's non-vectorised broadcast multiply, the same f64 products), else torch."""
+    l, r = Phi.shape
+    if P32 is not None and Phi.is_cuda and r % 4 == 0 and P32.is_contiguous() and P32.data_ptr() % 16 == 0:
+        out = torch.empty(l, r, dtype=torch.float64, device=Phi.device)
+        ops.ext().scale_rows_f32(P32.data_ptr(), d.contiguous().data_ptr(), l, r, out.data_ptr(),
+                                 ops.stream_ptr(Phi.device))
+        return out
+    return Phi * d[:, None]
+
+
+def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
     """Φᵀ diag(d) Φ as a split-K batched GEMM: a plain [r × r] GEMM over a 10⁵–10⁶-long K has
     only (r/128)² output tiles — a few dozen workgroups on a 256-CU part — so the rows are cut
     into 8192-row slabs (one batched GEMM, ~100 slabs × tiles in flight) and the slab products
@@ -121,13 +133,14 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
         return S
     k = l // _SYRK_CHUNK
     S = torch.zeros(r, r, dtype=Phi.dtype, device=Phi.device)
+    m = k * _SYRK_CHUNK
     if k > 0:
-        P = Phi[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, r)
-        Pd = P * d[: k * _SYRK_CHUNK].view(k, _SYRK_CHUNK, 1)
+        P = Phi[:m].view(k, _SYRK_CHUNK, r)
+        Pd = _scaled_rows(Phi[:m], d[:m], P32[:m] if P32 is not None else None).view(k, _SYRK_CHUNK, r)
         _upper_bmm(S, P, Pd)
-    if k * _SYRK_CHUNK < l:
-        T = Phi[k * _SYRK_CHUNK:]
-        _upper_bmm(S, T[None], (T * d[k * _SYRK_CHUNK:, None])[None])
+    if m < l:
+        T = Phi[m:]
+        _upper_bmm(S, T[None], _scaled_rows(T, d[m:], P32[m:] if P32 is not None else None)[None])
     if 0 < SYRK_BLOCK < r:
         S = torch.triu(S) + torch.triu(S, 1).T
     return S
@@ -333,7 +346,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         # S = I + Vᵀ D⁻¹ V  (V = YΦ, so Vᵀ D⁻¹ V = Φᵀ D⁻¹ Φ).  Free points drive D → 0, so S spans
         # many decades: equilibrate symmetrically before the Cholesky (exact); a relative jitter on
         # the unit diagonal is added only if it still fails.
-        S = eye + red.sum(_weighted_gram(Phi, Dinv))
+        S = eye + red.sum(_weighted_gram(Phi, Dinv, P32))
         S_prev, Dinv_prev = S, Dinv
         if DEBUG:
             dS = torch.diagonal(S)
@@ -382,6 +395,14 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
             return da, db, dnu, dmu
 
         def step_len(da, dnu, dmu):
+            if native and l > 0:
+                # one fused pass (lowrank.hip ipm_max_step): the same quotients and minimum as below
+                out = torch.ones((), dtype=dt, device=Phi.device)
+                v4 = [t.contiguous() for t in (a, da, s, nu, dnu, mu, dmu)]
+                E.ipm_max_step(v4[0].data_ptr(), v4[1].data_ptr(), v4[2].data_ptr(), v4[1].data_ptr(),
+                               v4[3].data_ptr(), v4[4].data_ptr(), v4[5].data_ptr(), v4[6].data_ptr(),
+                               1.0, -1.0, 1.0, 1.0, l, out.data_ptr(), ops.stream_ptr(Phi.device))
+                return red.min(out)
             return red.min(torch.minimum(torch.minimum(_max_step(a, da), _max_step(s, -da)),
                                          torch.minimum(_max_step(nu, dnu), _max_step(mu, dmu))))
 

@@ -408,4 +408,80 @@ void fill_dev(uintptr_t out, long long n, uintptr_t src, uintptr_t stream) {
   launch_check();
 }
 
+// ---- the interior point's step-length bound in ONE pass (models/svc_lowrank.py step_len):
+// min over the 4 (v, dv) pairs and all rows of −v_i / dv_i where dv_i < 0 (the pair's dv scaled by
+// sign[k] = ±1: the slack pair uses −Δα), capped at 1.  The same IEEE quotient as the torch
+// expression it replaces (and min is exact), so the step lengths are bit-identical; ~45 small torch
+// launches per call become two.  Ratios are ≥ 0, so their f64 bit patterns order as unsigned ints:
+// the block minima merge with a 64-bit atomicMin into *out (pre-set to 1.0).
+__global__ __launch_bounds__(256) void ipm_max_step_kernel(const double* __restrict__ v0, const double* __restrict__ d0,
+                                                           const double* __restrict__ v1, const double* __restrict__ d1,
+                                                           const double* __restrict__ v2, const double* __restrict__ d2,
+                                                           const double* __restrict__ v3, const double* __restrict__ d3,
+                                                           double s0, double s1, double s2, double s3, long long n,
+                                                           unsigned long long* __restrict__ out) {
+  double m = 1.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double a0 = s0 * d0[i], a1 = s1 * d1[i], a2 = s2 * d2[i], a3 = s3 * d3[i];
+    if (a0 < 0.0) m = fmin(m, -v0[i] / a0);
+    if (a1 < 0.0) m = fmin(m, -v1[i] / a1);
+    if (a2 < 0.0) m = fmin(m, -v2[i] / a2);
+    if (a3 < 0.0) m = fmin(m, -v3[i] / a3);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
+  __shared__ double wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmin(fmin(wm[0], wm[1]), fmin(wm[2], wm[3]));
+    atomicMin(out, (unsigned long long)__double_as_longlong(m));
+  }
+}
+
+void ipm_max_step(uintptr_t v0, uintptr_t d0, uintptr_t v1, uintptr_t d1, uintptr_t v2, uintptr_t d2, uintptr_t v3,
+                  uintptr_t d3, double s0, double s1, double s2, double s3, long long n, uintptr_t out,
+                  uintptr_t stream) {
+  if (n <= 0) return;
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4LL * ncu) blocks = 4LL * ncu;
+  hipLaunchKernelGGL(ipm_max_step_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), (const double*)v0,
+                     (const double*)d0, (const double*)v1, (const double*)d1, (const double*)v2, (const double*)d2,
+                     (const double*)v3, (const double*)d3, s0, s1, s2, s3, n, (unsigned long long*)out);
+  launch_check();
+}
+
+// ---- diag(d)·Φ for the weighted Gram, from the exact f32 copy of Φ (half the bytes of the f64 read;
+// the product is the same f64 multiply of the same values as torch's broadcast P * d).
+__global__ __launch_bounds__(256) void scale_rows_f32_kernel(const float* __restrict__ P, const double* __restrict__ d,
+                                                             long long n, int r, double* __restrict__ out) {
+  const int r4 = r >> 2;   // r % 4 == 0 (checked)
+  const long long tot = n * r4;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < tot; e += (long long)gridDim.x * 256) {
+    const long long i = e / r4;
+    const int c = (int)(e - i * r4) * 4;
+    const float4 p = *reinterpret_cast<const float4*>(P + i * r + c);
+    const double di = d[i];
+    double2* o = reinterpret_cast<double2*>(out + i * r + c);
+    o[0] = double2{(double)p.x * di, (double)p.y * di};
+    o[1] = double2{(double)p.z * di, (double)p.w * di};
+  }
+}
+
+void scale_rows_f32(uintptr_t P, uintptr_t d, long long n, int r, uintptr_t out, uintptr_t stream) {
+  HFENS_REQUIRE(r % 4 == 0 && r >= 4, "scale_rows_f32: r must be a positive multiple of 4");
+  if (n <= 0) return;
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  long long blocks = (n * (r / 4) + 255) / 256;
+  if (blocks > 16LL * ncu) blocks = 16LL * ncu;
+  hipLaunchKernelGGL(scale_rows_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), (const float*)P,
+                     (const double*)d, n, r, (double*)out);
+  launch_check();
+}
+
 }  // namespace hfens

@@ -129,3 +129,26 @@ def test_lowrank_svc_threaded_platt_cv_identical(dev, monkeypatch):
         for a, b in zip(out[(1, 1)], out[key]):
             assert a._hs == b._hs, key                      # (intercept, Platt A, Platt B)
             assert torch.equal(a.dual_coef_, b.dual_coef_), key
+
+
+def test_ipm_fused_step_and_scaled_rows_match_torch(dev):
+    """The interior point's fused kernels (lowrank.hip ipm_max_step, scale_rows_f32) give the torch
+    expressions they replace bit for bit: the step-length bound over the four (v, dv) pairs and
+    diag(d)·Φ from the exact f32 copy."""
+    from hfens import ops
+    from hfens.models import svc_lowrank as sl
+    g = torch.Generator(device=dev).manual_seed(5)
+    n = 300_001
+    vs = [torch.rand(n, generator=g, device=dev, dtype=torch.float64) + 1e-3 for _ in range(4)]
+    ds = [torch.randn(n, generator=g, device=dev, dtype=torch.float64) for _ in range(4)]
+    ref = torch.minimum(torch.minimum(sl._max_step(vs[0], ds[0]), sl._max_step(vs[1], -ds[1])),
+                        torch.minimum(sl._max_step(vs[2], ds[2]), sl._max_step(vs[3], ds[3])))
+    out = torch.ones((), dtype=torch.float64, device=dev)
+    ops.ext().ipm_max_step(vs[0].data_ptr(), ds[0].data_ptr(), vs[1].data_ptr(), ds[1].data_ptr(), vs[2].data_ptr(),
+                           ds[2].data_ptr(), vs[3].data_ptr(), ds[3].data_ptr(), 1.0, -1.0, 1.0, 1.0, n,
+                           out.data_ptr(), ops.stream_ptr(dev))
+    assert float(out) == float(ref)
+    P32 = torch.randn(n, 428, generator=g, device=dev, dtype=torch.float32)
+    d = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 1e6
+    got = sl._scaled_rows(P32.double(), d, P32)
+    assert torch.equal(got, P32.double() * d[:, None])
