@@ -32,7 +32,6 @@
 #include <type_traits>
 
 #include "common.h"
-#include <cstdlib>
 
 namespace hfens {
 
@@ -384,7 +383,7 @@ constexpr size_t ws_solve_lds_bytes(int Q, int FP) {
   return 64 * 4 + (size_t)Q * FP * 4 + (size_t)Q * 4 * 2 + (size_t)6 * Q * 4;
 }
 
-template <int FP, int Q, int TH, bool ILP = false>
+template <int FP, int Q, int TH>
 __global__ __launch_bounds__(TH) void ws_solve_kernel(
     const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
     const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
@@ -473,29 +472,18 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   // K(x_r, x_s) for every slot s of this thread: the gradient kernel's expression (MFMA = k-ordered
   // fma chain from 0), so the inner solver and ws_gupdate see the same f32 kernel values
   // (packed: each lane of the pair is the same k-ordered fma chain, bit for bit)
-  // ILP: even and odd features in two chains of half the depth, summed at the end — a different
-  // rounding than ws_gupdate's k-ordered chain (the inner solver's kernel values then differ from
-  // the gradient kernel's by an ulp; the outer rounds recompute G from ws_gupdate's, and the stop
-  // test is on that G), for half the dependent fma latency per row
   auto krow = [&](int r, float (&out)[SL]) {
-    f32x2 d[SL / 2], e[SL / 2];
+    f32x2 d[SL / 2];
 #pragma unroll
-    for (int h = 0; h < SL / 2; ++h) { d[h] = f32x2{0.f, 0.f}; e[h] = f32x2{0.f, 0.f}; }
+    for (int h = 0; h < SL / 2; ++h) d[h] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < FP; k += 4) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(&zB[r * FP + k]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
-        for (int h = 0; h < SL / 2; ++h) {
-          if (ILP && (q & 1)) e[h] = __builtin_elementwise_fma(f32x2{v[q], v[q]}, zp[h][k + q], e[h]);
-          else d[h] = __builtin_elementwise_fma(f32x2{v[q], v[q]}, zp[h][k + q], d[h]);
-        }
+        for (int h = 0; h < SL / 2; ++h) d[h] = __builtin_elementwise_fma(f32x2{v[q], v[q]}, zp[h][k + q], d[h]);
       }
-    }
-    if (ILP) {
-#pragma unroll
-      for (int h = 0; h < SL / 2; ++h) d[h] = d[h] + e[h];
     }
     const float snr = snB[r];
 #pragma unroll
@@ -899,8 +887,6 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
   const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
   int* wi = (int*)wsidx;
   const int TH = inner_threads == 512 ? 512 : 256;
-  const char* ilp_env = std::getenv("HFENS_WS_KROW_ILP");
-  const bool krow_ilp = ilp_env && ilp_env[0] == '1';
   for (int it = 0; it < n_iter; ++it) {
 #define WS_SEL(MM, QQ)                                                                                  \
   if (M == MM && Q == QQ) {                                                                             \
@@ -911,12 +897,8 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
 #undef WS_SEL
     launch_check();
 #define WS_SOL_TH(FF, QQ, TT)                                                                           \
-  if (krow_ilp)                                                                                         \
-    hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, TT, true>), dim3(P), dim3(TT), ws_solve_lds_bytes(QQ, FF), st, pp, \
-                       sp, zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, (long long*)prof); \
-  else                                                                                                  \
-    hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, TT>), dim3(P), dim3(TT), ws_solve_lds_bytes(QQ, FF), st, pp, sp, \
-                       zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, (long long*)prof)
+  hipLaunchKernelGGL((ws_solve_kernel<FF, QQ, TT>), dim3(P), dim3(TT), ws_solve_lds_bytes(QQ, FF), st, pp, sp, \
+                     zp, F, np_, ap, gp, wi, wz, wn, wd, Fp2, eps, max_inner, inner_frac, (long long*)prof)
 #define WS_SOL(FF)                                                                                      \
   if (FP == FF && Q == 1024) {                                                                          \
     if (TH == 512) WS_SOL_TH(FF, 1024, 512);                                                            \
