@@ -385,17 +385,31 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                 t = sc[:, None] * torch.cholesky_solve(sc[:, None] * rhs, Lc)
             return du - Dinv_k * (y_k * _phi_mv(Phi, t, P32))
 
+        fused = native and l > 0 and not _FUSED_OFF   # the elementwise tails as single passes (lowrank.hip ipm_*)
+
+        def col(v):
+            """(pointer, element stride) of a 1-D view (a column of a [l, k] solve result)."""
+            return v.data_ptr(), int(v.stride(0))
+
         def dirs(Mh, My, yMy, rnu, rmu, yMh=None):
             if yMh is None:
                 yMh = red.sum(torch.dot(y, Mh))
             db = (yMh + re) / yMy
+            if fused:
+                da, dnu, dmu = (torch.empty_like(a) for _ in range(3))
+                (pm, sm), (py, sy) = col(Mh), col(My)
+                dbc = db.contiguous()
+                E.ipm_dirs(pm, sm, py, sy, dbc.data_ptr(), rnu.data_ptr(), rmu.data_ptr(), nu.data_ptr(),
+                           mu.data_ptr(), a.data_ptr(), s.data_ptr(), l, da.data_ptr(), dnu.data_ptr(),
+                           dmu.data_ptr(), ops.stream_ptr(Phi.device))
+                return da, db, dnu, dmu
             da = Mh - _bc(db, My) * My
             dnu = (-rnu - nu * da) / a
             dmu = (-rmu + mu * da) / s
             return da, db, dnu, dmu
 
         def step_len(da, dnu, dmu):
-            if native and l > 0:
+            if native and l > 0 and not _FUSED_OFF:
                 # one fused pass (lowrank.hip ipm_max_step): the same quotients and minimum as below
                 out = torch.ones((), dtype=dt, device=Phi.device)
                 v4 = [t.contiguous() for t in (a, da, s, nu, dnu, mu, dmu)]
@@ -441,6 +455,32 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         # large SVM duals otherwise crawl at step lengths of 0.25–0.5 (profiles/r2_ipm_native.md).
         # Accept / reject stays on the device (no host synchronisation).
         for _ in range(N_CORRECTORS):
+            if fused:
+                ta_c, ts_c, rhs_c = (torch.empty_like(a) for _ in range(3))
+                alc, tauc = alpha.reshape(()).contiguous(), tau.reshape(()).contiguous()
+                E.ipm_gondzio_rhs(a.data_ptr(), s.data_ptr(), nu.data_ptr(), mu.data_ptr(), da.data_ptr(),
+                                  dnu.data_ptr(), dmu.data_ptr(), alc.data_ptr(), tauc.data_ptr(), l,
+                                  ta_c.data_ptr(), ts_c.data_ptr(), rhs_c.data_ptr(), ops.stream_ptr(Phi.device))
+                Mh = Minv(rhs_c[:, None])[:, 0]
+                dbc = red.sum(torch.dot(y, Mh)) / yMy
+                nda, ndnu, ndmu = (torch.empty_like(a) for _ in range(3))
+                (pm, sm), (py, sy) = col(Mh), col(My)
+                dbcc = dbc.contiguous()
+                E.ipm_gondzio_apply(pm, sm, py, sy, dbcc.data_ptr(), da.data_ptr(), dnu.data_ptr(), dmu.data_ptr(),
+                                    ta_c.data_ptr(), ts_c.data_ptr(), nu.data_ptr(), mu.data_ptr(), a.data_ptr(),
+                                    s.data_ptr(), l, nda.data_ptr(), ndnu.data_ptr(), ndmu.data_ptr(),
+                                    ops.stream_ptr(Phi.device))
+                ndb = db + dbc
+                nalpha = step_len(nda, ndnu, ndmu)
+                ok = nalpha >= 1.01 * alpha
+                # keep the corrected direction where ok, in place (stream order: every queued read
+                # of the old direction precedes this write)
+                okc = ok.reshape(()).contiguous()
+                E.ipm_select3(okc.data_ptr(), nda.data_ptr(), ndnu.data_ptr(), ndmu.data_ptr(), l, da.data_ptr(),
+                              dnu.data_ptr(), dmu.data_ptr(), ops.stream_ptr(Phi.device))
+                db = torch.where(ok, ndb, db)
+                alpha = torch.where(ok, nalpha, alpha)
+                continue
             atv = _bc(torch.clamp(1.5 * alpha + 0.1, max=1.0), a)
             va = (a + atv * da) * (nu + atv * dnu)
             vs = (s - atv * da) * (mu + atv * dmu)
@@ -697,3 +737,4 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
 
 
 LAST_INFO: dict = {}
+_FUSED_OFF = os.environ.get("HFENS_IPM_FUSED", "1") == "0"   # the torch-expression tails (tests / A/B)

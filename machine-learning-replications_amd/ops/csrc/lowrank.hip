@@ -454,6 +454,135 @@ void ipm_max_step(uintptr_t v0, uintptr_t d0, uintptr_t v1, uintptr_t d1, uintpt
   launch_check();
 }
 
+// ---- the interior point's per-row direction algebra, fused (models/svc_lowrank.py ipm_svc_dual):
+// each kernel is the elementwise tail of one step in ONE pass over the rows, the same IEEE
+// operations in the same order as the torch expressions it replaces (contraction off), so the
+// iterates are bit-identical; ~50 small launches per iteration become 5.  Device scalars are read
+// on the device (no host round trip).  Mh / My may be strided columns of a [l, k] solve result.
+__global__ __launch_bounds__(256) void ipm_dirs_kernel(const double* __restrict__ Mh, int smh, const double* __restrict__ My,
+                                                       int smy, const double* __restrict__ dbp,
+                                                       const double* __restrict__ rnu, const double* __restrict__ rmu,
+                                                       const double* __restrict__ nu, const double* __restrict__ mu,
+                                                       const double* __restrict__ a, const double* __restrict__ s,
+                                                       long long n, double* __restrict__ da, double* __restrict__ dnu,
+                                                       double* __restrict__ dmu) {
+#pragma clang fp contract(off)
+  const double db = *dbp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double d = Mh[i * smh] - db * My[i * smy];
+    da[i] = d;
+    dnu[i] = (-rnu[i] - nu[i] * d) / a[i];
+    dmu[i] = (-rmu[i] + mu[i] * d) / s[i];
+  }
+}
+
+// Gondzio corrector target: the trial point's complementarity products pushed into [0.1τ, 10τ]
+__global__ __launch_bounds__(256) void ipm_gondzio_rhs_kernel(const double* __restrict__ a, const double* __restrict__ s,
+                                                              const double* __restrict__ nu, const double* __restrict__ mu,
+                                                              const double* __restrict__ da, const double* __restrict__ dnu,
+                                                              const double* __restrict__ dmu, const double* __restrict__ alphap,
+                                                              const double* __restrict__ taup, long long n,
+                                                              double* __restrict__ ta, double* __restrict__ ts,
+                                                              double* __restrict__ rhs) {
+#pragma clang fp contract(off)
+  const double at = fmin(1.5 * *alphap + 0.1, 1.0);
+  const double tau = *taup;
+  const double lo = 0.1 * tau, hi = 10.0 * tau;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double va = (a[i] + at * da[i]) * (nu[i] + at * dnu[i]);
+    const double vs = (s[i] - at * da[i]) * (mu[i] + at * dmu[i]);
+    const double tca = fmax(fmin(fmax(va, lo), hi) - va, -hi);
+    const double tcs = fmax(fmin(fmax(vs, lo), hi) - vs, -hi);
+    ta[i] = tca;
+    ts[i] = tcs;
+    rhs[i] = tca / a[i] - tcs / s[i];
+  }
+}
+
+// Gondzio corrector applied to the direction: the corrected (Δα, Δν, Δμ)
+__global__ __launch_bounds__(256) void ipm_gondzio_apply_kernel(const double* __restrict__ Mh, int smh,
+                                                                const double* __restrict__ My, int smy,
+                                                                const double* __restrict__ dbcp,
+                                                                const double* __restrict__ da, const double* __restrict__ dnu,
+                                                                const double* __restrict__ dmu, const double* __restrict__ ta,
+                                                                const double* __restrict__ ts, const double* __restrict__ nu,
+                                                                const double* __restrict__ mu, const double* __restrict__ a,
+                                                                const double* __restrict__ s, long long n,
+                                                                double* __restrict__ nda, double* __restrict__ ndnu,
+                                                                double* __restrict__ ndmu) {
+#pragma clang fp contract(off)
+  const double dbc = *dbcp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double dac = Mh[i * smh] - dbc * My[i * smy];
+    nda[i] = da[i] + dac;
+    ndnu[i] = dnu[i] + (ta[i] - nu[i] * dac) / a[i];
+    ndmu[i] = dmu[i] + (ts[i] + mu[i] * dac) / s[i];
+  }
+}
+
+// keep the corrected direction where *ok (a device bool as 0/1 byte), in place
+__global__ __launch_bounds__(256) void ipm_select3_kernel(const bool* __restrict__ okp, const double* __restrict__ x0,
+                                                          const double* __restrict__ x1, const double* __restrict__ x2,
+                                                          long long n, double* __restrict__ y0, double* __restrict__ y1,
+                                                          double* __restrict__ y2) {
+  if (!*okp) return;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    y0[i] = x0[i];
+    y1[i] = x1[i];
+    y2[i] = x2[i];
+  }
+}
+
+static unsigned ipm_blocks(long long n) {
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  long long b = (n + 255) / 256;
+  if (b > 8LL * ncu) b = 8LL * ncu;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+void ipm_dirs(uintptr_t Mh, int smh, uintptr_t My, int smy, uintptr_t db, uintptr_t rnu, uintptr_t rmu, uintptr_t nu,
+              uintptr_t mu, uintptr_t a, uintptr_t s, long long n, uintptr_t da, uintptr_t dnu, uintptr_t dmu,
+              uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_dirs_kernel, dim3(ipm_blocks(n)), dim3(256), 0, as_stream(stream), (const double*)Mh, smh,
+                     (const double*)My, smy, (const double*)db, (const double*)rnu, (const double*)rmu,
+                     (const double*)nu, (const double*)mu, (const double*)a, (const double*)s, n, (double*)da,
+                     (double*)dnu, (double*)dmu);
+  launch_check();
+}
+
+void ipm_gondzio_rhs(uintptr_t a, uintptr_t s, uintptr_t nu, uintptr_t mu, uintptr_t da, uintptr_t dnu, uintptr_t dmu,
+                     uintptr_t alpha, uintptr_t tau, long long n, uintptr_t ta, uintptr_t ts, uintptr_t rhs,
+                     uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_gondzio_rhs_kernel, dim3(ipm_blocks(n)), dim3(256), 0, as_stream(stream), (const double*)a,
+                     (const double*)s, (const double*)nu, (const double*)mu, (const double*)da, (const double*)dnu,
+                     (const double*)dmu, (const double*)alpha, (const double*)tau, n, (double*)ta, (double*)ts,
+                     (double*)rhs);
+  launch_check();
+}
+
+void ipm_gondzio_apply(uintptr_t Mh, int smh, uintptr_t My, int smy, uintptr_t dbc, uintptr_t da, uintptr_t dnu,
+                       uintptr_t dmu, uintptr_t ta, uintptr_t ts, uintptr_t nu, uintptr_t mu, uintptr_t a, uintptr_t s,
+                       long long n, uintptr_t nda, uintptr_t ndnu, uintptr_t ndmu, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_gondzio_apply_kernel, dim3(ipm_blocks(n)), dim3(256), 0, as_stream(stream), (const double*)Mh,
+                     smh, (const double*)My, smy, (const double*)dbc, (const double*)da, (const double*)dnu,
+                     (const double*)dmu, (const double*)ta, (const double*)ts, (const double*)nu, (const double*)mu,
+                     (const double*)a, (const double*)s, n, (double*)nda, (double*)ndnu, (double*)ndmu);
+  launch_check();
+}
+
+void ipm_select3(uintptr_t ok, uintptr_t x0, uintptr_t x1, uintptr_t x2, long long n, uintptr_t y0, uintptr_t y1,
+                 uintptr_t y2, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_select3_kernel, dim3(ipm_blocks(n)), dim3(256), 0, as_stream(stream), (const bool*)ok,
+                     (const double*)x0, (const double*)x1, (const double*)x2, n, (double*)y0, (double*)y1, (double*)y2);
+  launch_check();
+}
+
 // ---- diag(d)·Φ for the weighted Gram, from the exact f32 copy of Φ (half the bytes of the f64 read;
 // the product is the same f64 multiply of the same values as torch's broadcast P * d).
 __global__ __launch_bounds__(256) void scale_rows_f32_kernel(const float* __restrict__ P, const double* __restrict__ d,

@@ -152,3 +152,23 @@ def test_ipm_fused_step_and_scaled_rows_match_torch(dev):
     d = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 1e6
     got = sl._scaled_rows(P32.double(), d, P32)
     assert torch.equal(got, P32.double() * d[:, None])
+
+
+def test_ipm_fused_direction_kernels_bit_identical(dev, monkeypatch):
+    """The interior point with its fused direction / Gondzio kernels (lowrank.hip ipm_dirs,
+    ipm_gondzio_rhs, ipm_gondzio_apply, ipm_select3: the same IEEE operations in the same order,
+    contraction off) reproduces the torch-expression iterates bit for bit."""
+    from hfens.models import svc_lowrank as sl
+    g = torch.Generator(device=dev).manual_seed(11)
+    n, r = 60_000, 96
+    Phi = torch.randn(n, r, generator=g, device=dev, dtype=torch.float64).to(torch.float32).to(torch.float64)
+    y = torch.where(torch.rand(n, generator=g, device=dev) < 0.3, -1.0, 1.0).to(torch.float64)
+    c = torch.where(y > 0, 0.7, 2.1).to(torch.float64)
+    out = {}
+    for fused in (False, True):
+        monkeypatch.setattr(sl, "_FUSED_OFF", not fused)
+        a, rho, it = sl.ipm_svc_dual(Phi, y, c)
+        out[fused] = (a.cpu(), rho, it)
+    assert out[False][2] == out[True][2]
+    assert out[False][1] == out[True][1]
+    assert torch.equal(out[False][0], out[True][0])
