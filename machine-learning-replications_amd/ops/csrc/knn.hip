@@ -147,14 +147,13 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   const bool active = r < nr;
   const int d_begin = blockIdx.y * per_split;
   const int d_end = min(nd, d_begin + per_split);
-  float xr[LD];
-#pragma unroll
-  for (int f = 0; f < LD; ++f) xr[f] = (active && f < F) ? R[(size_t)r * F + f] : 0.f;
   const unsigned long long mr = active ? rmask[r] : 0ull;
-  f32x2v xr2[LD / 2], nm2[LD / 2];   // receiver values and −(present) as feature pairs
+  // receiver values and −(present) as feature pairs (the only copy of the row: 2 waves → 3 per SIMD)
+  f32x2v xr2[LD / 2], nm2[LD / 2];
 #pragma unroll
   for (int h = 0; h < LD / 2; ++h) {
-    xr2[h] = f32x2v{xr[2 * h], xr[2 * h + 1]};
+    xr2[h] = f32x2v{(active && 2 * h < F) ? R[(size_t)r * F + 2 * h] : 0.f,
+                    (active && 2 * h + 1 < F) ? R[(size_t)r * F + 2 * h + 1] : 0.f};
     const float m0 = (2 * h < F && !((mr >> (2 * h)) & 1ull)) ? -1.f : -0.f;
     const float m1 = (2 * h + 1 < F && !((mr >> (2 * h + 1)) & 1ull)) ? -1.f : -0.f;
     nm2[h] = f32x2v{m0, m1};
@@ -209,7 +208,7 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
           mm &= mm - 1ull;
           float xv = 0.f;
 #pragma unroll
-          for (int g = 0; g < LD; ++g) xv = g == f ? xr[g] : xv;
+          for (int g = 0; g < LD; ++g) xv = g == f ? xr2[g >> 1][g & 1] : xv;
           corr = fmaf(xv, xv, corr);
         }
         // ≤ 32 fma roundings per accumulator in either pass, ≤ 64 in corr, one subtraction: ≤ ~100
@@ -232,10 +231,10 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
         for (int q = 0; q < LD / 4; ++q) {   // (features ≥ F: 0 − 0 on both sides, adds 0)
           const float4 v = xd4[q];
           const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
-          const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
-          const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
-          const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
-          const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
+          const float a = (bq & 1u) ? xr2[2 * q][0] - v.x : 0.f;
+          const float b = (bq & 2u) ? xr2[2 * q][1] - v.y : 0.f;
+          const float c = (bq & 4u) ? xr2[2 * q + 1][0] - v.z : 0.f;
+          const float d = (bq & 8u) ? xr2[2 * q + 1][1] - v.w : 0.f;
           s0 = fmaf(a, a, s0);
           s1 = fmaf(b, b, s1);
           s0 = fmaf(c, c, s0);
