@@ -24,8 +24,11 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# fast contraction everywhere except where a kernel says `#pragma clang fp contract(off)` (the
+# libsvm-arithmetic SMO kernels, the interior point's bit-identical tails): plain `fast` ignores
+# the pragma
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-            "-Wno-unused-result", "-ffp-contract=fast"]
+            "-Wno-unused-result", "-ffp-contract=fast-honor-pragmas"]
 
 
 def _torch_lib() -> str:
