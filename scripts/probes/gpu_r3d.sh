@@ -2,7 +2,7 @@
 # Round 3: the fast KNN pass (same donors + rates), the driver's headline command with host marks,
 # then the multi-rank rehearsals on one card.
 set -o pipefail
-bash scripts/gpu_knn_fast.sh || exit 1
+bash scripts/probes/gpu_knn_fast.sh || exit 1
 D=gpurun_out/r3d
 mkdir -p $D
 HFENS_TRACE_HOST=1 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $D/headline.json 2> $D/headline.err || { echo "headline failed"; tail -30 $D/headline.err; exit 1; }

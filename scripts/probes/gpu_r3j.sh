@@ -5,4 +5,4 @@ timeout -k 10 400 python -u -m pytest tests/test_linalg_gpu.py tests/test_svc_lo
 tail -2 gpurun_out/r3j_pytest.log
 timeout -k 10 300 python3 scripts/probes/knn_probe.py 300000 > gpurun_out/r3j_knn.log 2>&1 || { echo "knn failed"; tail -20 gpurun_out/r3j_knn.log; exit 1; }
 grep rows gpurun_out/r3j_knn.log
-bash scripts/gpu_r3h.sh
+bash scripts/probes/gpu_r3h.sh

@@ -9,4 +9,4 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --timings > gpurun_out/r
 python3 -c "import json; d=json.loads(open('gpurun_out/r3k_head.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['value'], d['auroc'], d['diag'].get('step_ms_min_med_max'))"
 timeout -k 10 300 python3 scripts/probes/knn_probe.py 300000 > gpurun_out/r3k_knn.log 2>&1 || { echo "knn failed"; tail -20 gpurun_out/r3k_knn.log; exit 1; }
 grep rows gpurun_out/r3k_knn.log
-bash scripts/gpu_r3h.sh
+bash scripts/probes/gpu_r3h.sh
