@@ -13,6 +13,9 @@
 //
 // f64 MFMA 16x16x4 operand maps (gfx950): A[i = l&15][k = l>>4], B[k = l>>4][j = l&15];
 // C/D col = l&15, row = (l>>4) + 4·reg (the f64 exception to the common C map).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -159,10 +162,62 @@ void wsyrk_part_len(long long n, int r, uintptr_t out) {
   *reinterpret_cast<long long*>(out) = (long long)wsyrk_groups(n, T) * T * kSyT * kSyT;
 }
 
-static long long phit_groups(long long n) { return n < 1024 * 64 ? (n + 63) / 64 : 1024; }
+// launch shape of the skinny passes: rows in flight per thread / wave, and the grid (sweep knobs
+// of scripts/probes/skinny_probe.py: HFENS_PHIT_CFG / HFENS_GEMV_CFG = "rows,grid")
+struct SkinnyCfg { int rows, grid; };
+static SkinnyCfg skinny_cfg(const char* env, int rows, int grid) {
+  SkinnyCfg c{rows, grid};
+  if (const char* e = std::getenv(env)) {
+    int a = 0, b = 0;
+    if (std::sscanf(e, "%d,%d", &a, &b) == 2) { c.rows = a; c.grid = b; }
+  }
+  return c;
+}
+
+template <int K, int R>
+__global__ void phit_flat_kernel(const float* __restrict__, const double* __restrict__, long long, int, long long,
+                                 double* __restrict__);
+
+// phit launch: the flat kernel (HFENS_PHIT_CFG "R,0", the default: R rows in flight per thread,
+// the grid exactly the resident workgroups) or the row-slab kernel ("R,w": w workgroups per CU).
+// The partial buffer is sized from phit_groups through phit_part_len, so both sides agree.
+static int phit_flat_rows() {
+  const SkinnyCfg c = skinny_cfg("HFENS_PHIT_CFG", 4, 0);
+  return c.grid == 0 ? (c.rows == 8 ? 8 : (c.rows == 2 ? 2 : 4)) : 0;
+}
+
+template <int K, int R>
+static long long phit_flat_groups(long long n, int r, int ncu) {
+  int per_cu = 1;
+  HFENS_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, phit_flat_kernel<K, R>, 256, 0));
+  const long long need = std::max(1LL, ((long long)n * (r / 4) + 256LL * 4 * R - 1) / (256LL * 4 * R));
+  return std::min((long long)ncu * std::max(1, per_cu), need);
+}
+
+static long long phit_groups(long long n, int r, int k) {
+  int dev = 0, ncu = 256;
+  HFENS_CHECK(hipGetDevice(&dev));
+  HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int R = phit_flat_rows();
+  if (R > 0 && r % 4 == 0) {
+    auto byk = [&](auto rr) -> long long {
+      constexpr int RR = decltype(rr)::value;
+      if (k == 1) return phit_flat_groups<1, RR>(n, r, ncu);
+      if (k == 2) return phit_flat_groups<2, RR>(n, r, ncu);
+      if (k == 3) return phit_flat_groups<3, RR>(n, r, ncu);
+      return phit_flat_groups<4, RR>(n, r, ncu);
+    };
+    if (R == 8) return byk(std::integral_constant<int, 8>{});
+    if (R == 2) return byk(std::integral_constant<int, 2>{});
+    return byk(std::integral_constant<int, 4>{});
+  }
+  if (n < 1024 * 64) return (n + 63) / 64;
+  const int wpc = skinny_cfg("HFENS_PHIT_CFG", 4, 0).grid;
+  return (long long)ncu * std::min(16, std::max(1, wpc));
+}
 
 void phit_part_len(long long n, int r, int k, uintptr_t out) {
-  *reinterpret_cast<long long*>(out) = phit_groups(n) * r * k;
+  *reinterpret_cast<long long*>(out) = phit_groups(n, r, k) * r * k;
 }
 
 void wsyrk_f64(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, long long part_len, uintptr_t S,
@@ -186,9 +241,10 @@ void wsyrk_f64(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, l
 // Y[i][q] = Σ_c Φ[i][c]·W[c][q], q < k ≤ 4.  Waves stride over rows (one 4 KB row per wave step:
 // lane l owns columns 8l … 8l+7, r ≤ 512, with its W slice in registers); wave-sum per (row, q).
 constexpr int kGvMaxK = 4;
-constexpr int kGvRows = 4;
 
-template <int K, typename TP>
+// CONTIG: lane l owns columns 4l … 4l+3 and 256 + 4l … (each float4 load instruction reads one
+// contiguous 1 KB run of the row) instead of 8l … 8l+7 (two half-used runs)
+template <int K, typename TP, int kGvRows, bool CONTIG = false>
 __global__ __launch_bounds__(256) void phi_gemv_kernel(const TP* __restrict__ Phi, const double* __restrict__ W,
                                                        long long n, int r, double* __restrict__ Y) {
   const int lane = threadIdx.x & 63;
@@ -200,7 +256,7 @@ __global__ __launch_bounds__(256) void phi_gemv_kernel(const TP* __restrict__ Ph
   for (int e = 0; e < 8; ++e)
 #pragma unroll
     for (int q = 0; q < K; ++q) {
-      const int c = 8 * lane + e;
+      const int c = CONTIG ? 4 * lane + 256 * (e >> 2) + (e & 3) : 8 * lane + e;
       w[e][q] = c < r ? W[(size_t)c * K + q] : 0.0;
     }
   // kGvRows rows per wave step: their loads are issued together (the pass is bound by bytes in
@@ -215,7 +271,7 @@ __global__ __launch_bounds__(256) void phi_gemv_kernel(const TP* __restrict__ Ph
         if (vec4) {   // two 16-byte loads per lane (8 columns): the pass is load-instruction bound
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const int c = 8 * lane + 4 * h;
+            const int c = CONTIG ? 4 * lane + 256 * h : 8 * lane + 4 * h;
             const float4 v = (i < n && c < r) ? *reinterpret_cast<const float4*>(pr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
             x[u][4 * h] = v.x; x[u][4 * h + 1] = v.y; x[u][4 * h + 2] = v.z; x[u][4 * h + 3] = v.w;
           }
@@ -224,7 +280,7 @@ __global__ __launch_bounds__(256) void phi_gemv_kernel(const TP* __restrict__ Ph
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int c = 8 * lane + e;
+        const int c = CONTIG ? 4 * lane + 256 * (e >> 2) + (e & 3) : 8 * lane + e;
         x[u][e] = (i < n && c < r) ? (double)pr[c] : 0.0;
       }
     }
@@ -256,19 +312,40 @@ static void phi_gemv_any(const void* Phi, bool f32, uintptr_t W, long long n, in
   int dev = 0, ncu = 256;
   HFENS_CHECK(hipGetDevice(&dev));
   HFENS_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  long long blocks = (long long)ncu * 8;
-  const long long need = (n + 4 * kGvRows - 1) / (4 * kGvRows);
-  if (blocks > need) blocks = need;
+  const SkinnyCfg cfg = skinny_cfg("HFENS_GEMV_CFG", 2, 3);   // 2 rows per wave, contiguous, resident grid
   hipStream_t st = as_stream(stream);
+  auto launch = [&](auto kern, int rows) {
+    long long blocks = (long long)ncu * 8;
+    if (cfg.grid == 1 || cfg.grid == 3) {   // exactly the resident workgroups: no second, partial round of waves
+      int per_cu = 1;
+      HFENS_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+      blocks = (long long)ncu * std::max(1, per_cu);
+    }
+    const long long need = (n + 4 * rows - 1) / (4 * rows);
+    if (blocks > need) blocks = need;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)Phi, (const double*)W, n, r,
+                       (double*)Y);
+    launch_check();
+  };
   auto go = [&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    if (f32)
-      hipLaunchKernelGGL((phi_gemv_kernel<K, float>), dim3((unsigned)blocks), dim3(256), 0, st, (const float*)Phi,
+    if (!f32) {
+      long long blocks = (long long)ncu * 8;
+      const long long need = (n + 15) / 16;
+      if (blocks > need) blocks = need;
+      hipLaunchKernelGGL((phi_gemv_kernel<K, double, 4>), dim3((unsigned)blocks), dim3(256), 0, st, (const double*)Phi,
                          (const double*)W, n, r, (double*)Y);
-    else
-      hipLaunchKernelGGL((phi_gemv_kernel<K, double>), dim3((unsigned)blocks), dim3(256), 0, st, (const double*)Phi,
-                         (const double*)W, n, r, (double*)Y);
-    launch_check();
+      launch_check();
+      return;
+    }
+    if (cfg.grid == 3) {   // contiguous lane → column map, resident grid
+      if (cfg.rows == 4) launch(phi_gemv_kernel<K, float, 4, true>, 4);
+      else launch(phi_gemv_kernel<K, float, 2, true>, 2);
+      return;
+    }
+    if (cfg.rows == 8) launch(phi_gemv_kernel<K, float, 8>, 8);
+    else if (cfg.rows == 2) launch(phi_gemv_kernel<K, float, 2>, 2);
+    else launch(phi_gemv_kernel<K, float, 4>, 4);
   };
   if (k == 1) go(std::integral_constant<int, 1>{});
   else if (k == 2) go(std::integral_constant<int, 2>{});
@@ -288,9 +365,7 @@ void phi_gemv_f32(uintptr_t Phi, uintptr_t W, long long n, int r, int k, uintptr
 // out[c][q] = Σ_i Φ[i][c]·V[i][q] (Φᵀ V, V [n][k], k ≤ 4) with Φ in f32, f64 arithmetic: workgroup g
 // sums its row slab (thread t owns columns t and t + 256; 4 rows in flight; V rows are uniform loads)
 // into a partial [r][k] slot, and a second launch adds the G slots in slot order (deterministic).
-constexpr int kPtRows = 4;
-
-template <int K>
+template <int K, int kPtRows>
 __global__ __launch_bounds__(256) void phit_f32_kernel(const float* __restrict__ Phi, const double* __restrict__ V,
                                                        long long n, int r, long long per, double* __restrict__ part) {
   // thread t: columns 4·(t % 128) … +3 (one 16-byte load per row), row stream t / 128 (rows of the
@@ -354,6 +429,79 @@ __global__ __launch_bounds__(256) void phit_f32_kernel(const float* __restrict__
   }
 }
 
+// Φᵀ V over Φ as one flat stream of float4s (r % 4 == 0): grid thread g takes elements g, g + S,
+// g + 2S, … with S a multiple of r/4, so its column group (g mod r/4) never changes and its rows
+// advance by S/(r/4); every lane of every load is active and a wave's load is 1 KB contiguous.
+// A workgroup's threads of one column group meet in LDS in thread order (deterministic), one
+// partial [r][k] slot per workgroup as in phit_f32_kernel.
+template <int K, int R>
+__global__ __launch_bounds__(256) void phit_flat_kernel(const float* __restrict__ Phi, const double* __restrict__ V,
+                                                        long long n, int r4, long long S, double* __restrict__ part) {
+  const int t = threadIdx.x;
+  const long long g = (long long)blockIdx.x * 256 + t;
+  const long long Sq = S / r4;
+  double acc[4][K];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int q = 0; q < K; ++q) acc[e][q] = 0.0;
+  if (g < S) {
+    const float4* P4 = reinterpret_cast<const float4*>(Phi);
+    const long long c4 = g % r4;
+    long long i = g / r4;
+    for (; i + (R - 1) * Sq < n; i += R * Sq) {
+      float4 x[R];
+      double v[R][K];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const long long iu = i + u * Sq;
+        x[u] = P4[iu * r4 + c4];
+#pragma unroll
+        for (int q = 0; q < K; ++q) v[u][q] = V[iu * K + q];
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          acc[0][q] = fma((double)x[u].x, v[u][q], acc[0][q]);
+          acc[1][q] = fma((double)x[u].y, v[u][q], acc[1][q]);
+          acc[2][q] = fma((double)x[u].z, v[u][q], acc[2][q]);
+          acc[3][q] = fma((double)x[u].w, v[u][q], acc[3][q]);
+        }
+    }
+    for (; i < n; i += Sq) {
+      const float4 x = P4[i * r4 + c4];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const double vq = V[i * K + q];
+        acc[0][q] = fma((double)x.x, vq, acc[0][q]);
+        acc[1][q] = fma((double)x.y, vq, acc[1][q]);
+        acc[2][q] = fma((double)x.z, vq, acc[2][q]);
+        acc[3][q] = fma((double)x.w, vq, acc[3][q]);
+      }
+    }
+  }
+  __shared__ double sh[256][4 * K];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int q = 0; q < K; ++q) sh[t][e * K + q] = acc[e][q];
+  __syncthreads();
+  if (t < r4) {
+    const long long g0 = (long long)blockIdx.x * 256;
+    const int cg = (int)((g0 + t) % r4);
+    double* slot = part + (size_t)blockIdx.x * 4 * r4 * K;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        double sum = 0.0;
+        for (int tt = t; tt < 256; tt += r4) sum += sh[tt][e * K + q];
+        slot[(size_t)(4 * cg + e) * K + q] = sum;
+      }
+  }
+}
+
 // one wave per output element: lanes take every 64th partial, then a wave sum (fixed order:
 // deterministic)
 __global__ __launch_bounds__(256) void phit_reduce_kernel(const double* __restrict__ part, int G, long long m,
@@ -371,14 +519,31 @@ void phit_f32(uintptr_t Phi, uintptr_t V, long long n, int r, int k, uintptr_t p
               uintptr_t stream) {
   HFENS_REQUIRE(n >= 1 && r >= 1 && r <= 512 && r % 4 == 0 && k >= 1 && k <= kGvMaxK && (Phi & 15) == 0,
                 "phit_f32: r <= 512, r % 4 == 0, 16-byte aligned Φ, 1 <= k <= 4");
-  const long long G = phit_groups(n);
+  const long long G = phit_groups(n, r, k);
   HFENS_REQUIRE(part_len >= G * r * k, "phit_f32: partial buffer too small (size it with phit_part_len)");
   const long long per = (n + G - 1) / G;
   hipStream_t st = as_stream(stream);
+  const int R = phit_flat_rows();
+  const int rows = skinny_cfg("HFENS_PHIT_CFG", 4, 0).rows;
+  const int r4 = r / 4;
+  const long long S = G * 256 - (G * 256) % r4;   // a multiple of r/4: each thread keeps its column group
   auto go = [&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    hipLaunchKernelGGL(phit_f32_kernel<K>, dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi, (const double*)V,
-                       n, r, per, (double*)part);
+    if (R == 8)
+      hipLaunchKernelGGL((phit_flat_kernel<K, 8>), dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)V, n, r4, S, (double*)part);
+    else if (R == 2)
+      hipLaunchKernelGGL((phit_flat_kernel<K, 2>), dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)V, n, r4, S, (double*)part);
+    else if (R == 4)
+      hipLaunchKernelGGL((phit_flat_kernel<K, 4>), dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)V, n, r4, S, (double*)part);
+    else if (rows == 8)
+      hipLaunchKernelGGL((phit_f32_kernel<K, 8>), dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)V, n, r, per, (double*)part);
+    else
+      hipLaunchKernelGGL((phit_f32_kernel<K, 4>), dim3((unsigned)G), dim3(256), 0, st, (const float*)Phi,
+                         (const double*)V, n, r, per, (double*)part);
     launch_check();
   };
   if (k == 1) go(std::integral_constant<int, 1>{});
