@@ -28,6 +28,7 @@ constexpr int kChThreads = 1024;
 constexpr int kChWaves = kChThreads / 64;
 constexpr int kChNB = 64;   // solve block (wave 0 substitution chains)
 constexpr int kChMaxK = 4;
+constexpr int kChTU = 4;    // trailing-update blocks per load round (chol_spd)
 
 __device__ __forceinline__ double ch_readlane(double v, int lane) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -122,22 +123,42 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
       __syncthreads();
       const int nbk = m16 / 16;
       const int nblocks = nbk * (nbk + 1) / 2;
-      for (int blk = wave; blk < nblocks; blk += kChWaves) {
-        int bi = 0, rem = blk;
-        while (rem > bi) { rem -= bi + 1; ++bi; }
-        const int bj = rem;                               // 0 ≤ bj ≤ bi
-        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      // kChTU blocks per round: their L tiles are loaded before any of them is written back (a
+      // store into L between a block's load and the next one's would serialise one L2 round trip
+      // per block), then the MFMAs, then the stores — the same L − acc per element as before
+      for (int blk0 = wave; blk0 < nblocks; blk0 += kChWaves * kChTU) {
+        double old[kChTU][4];
+        int bis[kChTU], bjs[kChTU];
 #pragma unroll
-        for (int ks = 0; ks < NB / 4; ++ks) {
-          const int kb = 4 * ks + (lane >> 4);
-          const double a = PT[(size_t)kb * r + 16 * bi + (lane & 15)];
-          const double b = PT[(size_t)kb * r + 16 * bj + (lane & 15)];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        for (int c = 0; c < kChTU; ++c) {
+          const int blk = blk0 + c * kChWaves;
+          int bi = 0, rem = blk;
+          while (rem > bi) { rem -= bi + 1; ++bi; }
+          bis[c] = blk < nblocks ? bi : -1;
+          bjs[c] = rem;                                    // 0 ≤ bj ≤ bi
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * rem + (lane & 15);
+            old[c][reg] = (blk < nblocks && i < m && j <= i) ? L[(size_t)(m0 + i) * r + m0 + j] : 0.0;
+          }
         }
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * bj + (lane & 15);
-          if (i < m && j <= i) L[(size_t)(m0 + i) * r + m0 + j] -= acc[reg];
+        for (int c = 0; c < kChTU; ++c) {
+          const int bi = bis[c], bj = bjs[c];
+          if (bi < 0) continue;
+          f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ks = 0; ks < NB / 4; ++ks) {
+            const int kb = 4 * ks + (lane >> 4);
+            const double a = PT[(size_t)kb * r + 16 * bi + (lane & 15)];
+            const double b = PT[(size_t)kb * r + 16 * bj + (lane & 15)];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * bj + (lane & 15);
+            if (i < m && j <= i) L[(size_t)(m0 + i) * r + m0 + j] = old[c][reg] - acc[reg];
+          }
         }
       }
       __syncthreads();
@@ -156,37 +177,45 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
   if (tid == 0) out_info[0] = tries;
 }
 
-// x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.  Each
-// 64-row step stages its diagonal block of L in LDS (the substitution chain of wave 0 then waits on
-// LDS, not on a global load per column) and the solved block of x in LDS for the row updates.
-// K = right-hand sides (compile time: the per-lane vectors stay in registers).  The diagonal blocks'
-// pivots are inverted in parallel first (the substitution chain then multiplies), and the
-// off-diagonal updates issue their row loads 16 at a time (one load round per 16 columns instead
-// of one per column: the runtime-bound loop had serialised 64 L2 round trips per block).
+// x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.  Per
+// 64-row block: wave 0 runs the substitution chain on the block's diagonal block of L (staged in
+// LDS; the pivots inverted in parallel first, the chain then multiplies) while waves 1… stage the
+// NEXT diagonal block (double-buffered), so the staging round trip overlaps the chain; then every
+// thread loads its row's 64-column slice of L in one round (512 threads: the 64 values fit in
+// registers; the 1024-thread version needed four rounds of 16) and updates its right-hand sides.
+// The arithmetic and its order are unchanged.  K = right-hand sides (compile time: the per-lane
+// vectors stay in registers).
+constexpr int kCsThreads = 512;
+
 template <int K>
-__global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __restrict__ L, const double* __restrict__ sc,
+__global__ __launch_bounds__(kCsThreads) void chol_solve_kernel(const double* __restrict__ L, const double* __restrict__ sc,
                                                                 int r, double* __restrict__ B) {
-  __shared__ double Db[kChNB][kChNB + 1];
+  __shared__ double Db[2][kChNB][kChNB + 1];
   __shared__ double Xb[kChNB][kChMaxK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < r * K; e += kChThreads) B[e] *= sc[e / K];
+  const int nblk = (r + kChNB - 1) / kChNB;
+  auto stage = [&](int buf, int k0, int t0, int nt) {   // Db[buf] ← diagonal block at k0
+    const int nb = min(kChNB, r - k0);
+    for (int e = t0; e < nb * nb; e += nt) {
+      const int a = e / nb, c = e % nb;
+      Db[buf][a][c] = c <= a ? L[(size_t)(k0 + a) * r + k0 + c] : 0.0;
+    }
+  };
+  for (int e = tid; e < r * K; e += kCsThreads) B[e] *= sc[e / K];
+  stage(0, 0, tid, kCsThreads);
   __syncthreads();
   // forward: L y = b
-  for (int k0 = 0; k0 < r; k0 += kChNB) {
-    const int nb = min(kChNB, r - k0);
-    for (int e = tid; e < nb * nb; e += kChThreads) {
-      const int a = e / nb, c = e % nb;
-      Db[a][c] = c <= a ? L[(size_t)(k0 + a) * r + k0 + c] : 0.0;
-    }
-    __syncthreads();
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int k0 = kb * kChNB, nb = min(kChNB, r - k0), cur = kb & 1;
+    if (wave != 0 && kb + 1 < nblk) stage(cur ^ 1, k0 + kChNB, tid - 64, kCsThreads - 64);
     if (wave == 0) {
       double y[K];
 #pragma unroll
       for (int q = 0; q < K; ++q) y[q] = lane < nb ? B[(size_t)(k0 + lane) * K + q] : 0.0;
-      const double dinv = lane < nb ? 1.0 / Db[lane][lane] : 0.0;
+      const double dinv = lane < nb ? 1.0 / Db[cur][lane][lane] : 0.0;
       for (int j = 0; j < nb; ++j) {
         const double dj = ch_readlane(dinv, j);
-        const double lij = (lane > j && lane < nb) ? Db[lane][j] : 0.0;
+        const double lij = (lane > j && lane < nb) ? Db[cur][lane][j] : 0.0;
 #pragma unroll
         for (int q = 0; q < K; ++q) {
           if (lane == j) y[q] *= dj;
@@ -202,43 +231,43 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
         }
     }
     __syncthreads();
-    for (int i = k0 + nb + tid; i < r; i += kChThreads) {
+    for (int i = k0 + nb + tid; i < r; i += kCsThreads) {
+      double l[kChNB];   // the row's whole slice in one round of loads
       const double* li = L + (size_t)i * r + k0;
+#pragma unroll
+      for (int u = 0; u < kChNB; ++u) l[u] = u < nb ? li[u] : 0.0;
       double acc[K];
 #pragma unroll
       for (int q = 0; q < K; ++q) acc[q] = 0.0;
-      for (int b0 = 0; b0 < nb; b0 += 16) {
-        double l[16];
+      // 16 columns at a time: the scheduler would otherwise hoist all 64·K LDS reads of Xb next to
+      // the 64 loaded L values (spills)
 #pragma unroll
-        for (int u = 0; u < 16; ++u) l[u] = b0 + u < nb ? li[b0 + u] : 0.0;
+      for (int b0 = 0; b0 < kChNB; b0 += 16) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
+        for (int u = b0; u < b0 + 16; ++u)
 #pragma unroll
-          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], b0 + u < nb ? Xb[b0 + u][q] : 0.0, acc[q]);
+          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], u < nb ? Xb[u][q] : 0.0, acc[q]);
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int q = 0; q < K; ++q) B[(size_t)i * K + q] -= acc[q];
     }
     __syncthreads();
   }
-  // backward: Lᵀ x = y (blocks from the bottom)
-  const int nblk = (r + kChNB - 1) / kChNB;
+  // backward: Lᵀ x = y (blocks from the bottom); the last forward block is staged in Db[(nblk-1)&1]
   for (int bi = nblk - 1; bi >= 0; --bi) {
-    const int k0 = bi * kChNB, nb = min(kChNB, r - k0);
-    for (int e = tid; e < nb * nb; e += kChThreads) {
-      const int a = e / nb, c = e % nb;
-      Db[a][c] = c <= a ? L[(size_t)(k0 + a) * r + k0 + c] : 0.0;
-    }
-    __syncthreads();
+    const int k0 = bi * kChNB, nb = min(kChNB, r - k0), cur = (nblk - 1 - bi + (nblk - 1)) & 1;
+    const double* Lb = L + (size_t)k0 * r;
+    if (wave != 0 && bi > 0) stage(cur ^ 1, k0 - kChNB, tid - 64, kCsThreads - 64);
     if (wave == 0) {
       double x[K];
 #pragma unroll
       for (int q = 0; q < K; ++q) x[q] = lane < nb ? B[(size_t)(k0 + lane) * K + q] : 0.0;
-      const double dinv = lane < nb ? 1.0 / Db[lane][lane] : 0.0;
+      const double dinv = lane < nb ? 1.0 / Db[cur][lane][lane] : 0.0;
       for (int j = nb - 1; j >= 0; --j) {
         const double dj = ch_readlane(dinv, j);
         // Lᵀ[lane][j] = L[j][lane] for lane < j
-        const double lji = lane < j ? Db[j][lane] : 0.0;
+        const double lji = lane < j ? Db[cur][j][lane] : 0.0;
 #pragma unroll
         for (int q = 0; q < K; ++q) {
           if (lane == j) x[q] *= dj;
@@ -254,26 +283,30 @@ __global__ __launch_bounds__(kChThreads) void chol_solve_kernel(const double* __
         }
     }
     __syncthreads();
-    // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j  (lanes read consecutive i: coalesced)
-    for (int i = tid; i < k0; i += kChThreads) {
+    // rows above the block: b_i −= Σ_{j in block} L[j][i]·x_j (lanes read consecutive i: coalesced)
+    for (int i = tid; i < k0; i += kCsThreads) {
+      double l[kChNB];
+#pragma unroll
+      for (int u = 0; u < kChNB; ++u) l[u] = u < nb ? Lb[(unsigned)(u * r + i)] : 0.0;
       double acc[K];
 #pragma unroll
       for (int q = 0; q < K; ++q) acc[q] = 0.0;
-      for (int b0 = 0; b0 < nb; b0 += 16) {
-        double l[16];
+      // 16 columns at a time: the scheduler would otherwise hoist all 64·K LDS reads of Xb next to
+      // the 64 loaded L values (spills)
 #pragma unroll
-        for (int u = 0; u < 16; ++u) l[u] = b0 + u < nb ? L[(size_t)(k0 + b0 + u) * r + i] : 0.0;
+      for (int b0 = 0; b0 < kChNB; b0 += 16) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
+        for (int u = b0; u < b0 + 16; ++u)
 #pragma unroll
-          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], b0 + u < nb ? Xb[b0 + u][q] : 0.0, acc[q]);
+          for (int q = 0; q < K; ++q) acc[q] = fma(l[u], u < nb ? Xb[u][q] : 0.0, acc[q]);
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int q = 0; q < K; ++q) B[(size_t)i * K + q] -= acc[q];
     }
     __syncthreads();
   }
-  for (int e = tid; e < r * K; e += kChThreads) B[e] *= sc[e / K];
+  for (int e = tid; e < r * K; e += kCsThreads) B[e] *= sc[e / K];
 }
 
 void chol_spd(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uintptr_t stream) {
@@ -292,7 +325,7 @@ void chol_solve(uintptr_t L, uintptr_t sc, int r, int k, uintptr_t B, uintptr_t 
   HFENS_REQUIRE(r >= 1 && r <= 1024 && k >= 1 && k <= kChMaxK, "chol_solve: 1 <= r <= 1024, 1 <= k <= 4");
   auto go = [&](auto kk) {
     constexpr int K = decltype(kk)::value;
-    hipLaunchKernelGGL(chol_solve_kernel<K>, dim3(1), dim3(kChThreads), 0, as_stream(stream), (const double*)L,
+    hipLaunchKernelGGL(chol_solve_kernel<K>, dim3(1), dim3(kCsThreads), 0, as_stream(stream), (const double*)L,
                        (const double*)sc, r, (double*)B);
     launch_check();
   };

@@ -69,3 +69,20 @@ Pd = torch.empty(n, r, dtype=torch.float64, device=dev)
 d = torch.rand(n, generator=g, device=dev, dtype=torch.float64)
 us = timeit(lambda: E.scale_rows_f32(P.data_ptr(), d.data_ptr(), n, r, Pd.data_ptr(), st))
 print(f"scale_rows  : {us:8.1f} us  {3 * GB / us * 1e6 / 1e3:5.2f} TB/s (read f32 + write f64)", flush=True)
+
+# the r × r factor and solves of the same iteration (linalg.hip chol_spd / chol_solve, one workgroup)
+A = torch.randn(4 * r, r, generator=g, device=dev, dtype=torch.float64)
+S = A.T @ A + torch.eye(r, device=dev, dtype=torch.float64)
+Lc = torch.empty(r, r, dtype=torch.float64, device=dev)
+scv = torch.empty(r, dtype=torch.float64, device=dev)
+info = torch.zeros(1, dtype=torch.int32, device=dev)
+us = timeit(lambda: E.chol_spd(S.data_ptr(), r, Lc.data_ptr(), scv.data_ptr(), info.data_ptr(), st))
+print(f"chol_spd r={r}: {us:8.1f} us", flush=True)
+for k in (1, 2):
+    B0 = torch.randn(r, k, generator=g, device=dev, dtype=torch.float64)
+    Bk = B0.clone()
+    us = timeit(lambda: E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, k, Bk.data_ptr(), st))
+    Bk.copy_(B0)
+    E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, k, Bk.data_ptr(), st)
+    res = float((S @ Bk - B0).abs().max() / B0.abs().max())
+    print(f"chol_solve r={r} k={k}: {us:8.1f} us  residual {res:.1e}", flush=True)
