@@ -133,16 +133,33 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
 //     worst slot is skipped — exactly, since the slot test is strict — and only the others run
 //     the exact masked direct-difference pass of knn_donor_kernel.
 // The exact pass decides every update, so the donors equal knn_donor_kernel's bit for bit (tested).
+// XS (LD ≤ 40): the receiver rows also sit in LDS, column-major per thread, for the correction's
+// uniform-index reads; the donor tile is then kKnnFastTile rows so two workgroups still fit per CU.
+constexpr int kKnnFastTile = 224;
+template <int FMAX>
+constexpr bool knn_fast_xs() { return (FMAX + 3) / 4 * 4 <= 40; }
+template <int FMAX>
+constexpr int knn_fast_tile() { return knn_fast_xs<FMAX>() ? kKnnFastTile : kKnnTile; }
+template <int FMAX>
+constexpr size_t knn_fast_lds() {
+  constexpr int LD = (FMAX + 3) / 4 * 4;
+  return (size_t)knn_fast_tile<FMAX>() * LD * sizeof(float) + knn_fast_tile<FMAX>() * sizeof(unsigned long long) +
+         (knn_fast_xs<FMAX>() ? (size_t)LD * 256 * sizeof(float) : 0);
+}
+
 template <int FMAX>
 __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
     int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
+  constexpr bool XS = knn_fast_xs<FMAX>();
+  constexpr int TILE = knn_fast_tile<FMAX>();
   typedef float f32x2v __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ds = sm;
-  unsigned long long* dm = (unsigned long long*)(ds + kKnnTile * LD);
+  unsigned long long* dm = (unsigned long long*)(ds + TILE * LD);
+  float* xs = reinterpret_cast<float*>(dm + TILE);   // XS: [LD][256] receiver values
   const int r = blockIdx.x * 256 + threadIdx.x;
   const bool active = r < nr;
   const int d_begin = blockIdx.y * per_split;
@@ -157,6 +174,10 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     const float m0 = (2 * h < F && !((mr >> (2 * h)) & 1ull)) ? -1.f : -0.f;
     const float m1 = (2 * h + 1 < F && !((mr >> (2 * h + 1)) & 1ull)) ? -1.f : -0.f;
     nm2[h] = f32x2v{m0, m1};
+    if constexpr (XS) {
+      xs[(2 * h) * 256 + threadIdx.x] = xr2[h][0];
+      xs[(2 * h + 1) * 256 + threadIdx.x] = xr2[h][1];
+    }
   }
   int col[kKnnSlots];
   float bd[kKnnSlots];
@@ -178,9 +199,9 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   // instead of recomputed per donor (a full-precision f32 divide is ~10 VALU instructions)
   __shared__ float s_scale[65];
   if (threadIdx.x <= 64) s_scale[threadIdx.x] = threadIdx.x > 0 ? (float)F / (float)threadIdx.x : 0.f;
-  for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
+  for (int d0 = d_begin; d0 < d_end; d0 += TILE) {
     __syncthreads();
-    const int nt = min(kKnnTile, d_end - d0);
+    const int nt = min(TILE, d_end - d0);
     for (int e = threadIdx.x; e < nt * LD; e += 256) {
       const int rr = e / LD, c = e % LD;
       ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
@@ -201,14 +222,20 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
       if (!exact) {
         // the receiver-present features the donor lacks added x_r² each: a uniform loop (the
         // donor's missing cells, usually one), register index from a scalar
+        // XS: each cell's x_r from this thread's column of the LDS copy of the receiver rows (one
+        // conflict-free read); otherwise an LD-way register select
         float corr = 0.f;
         unsigned long long mm = md & ~mr & ((F >= 64) ? ~0ull : ((1ull << F) - 1ull));
         while (mm) {
           const int f = __builtin_ctzll(mm);
           mm &= mm - 1ull;
           float xv = 0.f;
+          if constexpr (XS) {
+            xv = xs[f * 256 + threadIdx.x];
+          } else {
 #pragma unroll
-          for (int g = 0; g < LD; ++g) xv = g == f ? xr2[g >> 1][g & 1] : xv;
+            for (int g = 0; g < LD; ++g) xv = g == f ? xr2[g >> 1][g & 1] : xv;
+          }
           corr = fmaf(xv, xv, corr);
         }
         // ≤ 32 fma roundings per accumulator in either pass, ≤ 64 in corr, one subtraction: ≤ ~100
@@ -307,22 +334,24 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   const int max_splits = (nd + kKnnTile - 1) / kKnnTile;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
-  int per = (nd + splits - 1) / splits;
-  per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
-  splits = (nd + per - 1) / per;
   const char* kenv = std::getenv("HFENS_KNN_KERNEL");
   const bool direct = kenv && kenv[0] == 'd';   // "direct": the exact pass for every donor
   auto go = [&](auto fm) {
     constexpr int FM = decltype(fm)::value;
     constexpr int LD = (FM + 3) / 4 * 4;
-    const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
+    const int tile = direct ? kKnnTile : knn_fast_tile<FM>();
+    int per = (nd + splits - 1) / splits;
+    per = (per + tile - 1) / tile * tile;
+    const int nsp = (nd + per - 1) / per;
+    const size_t lds = direct ? (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long)
+                              : knn_fast_lds<FM>();
     if (direct)
-      hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
+      hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
                          (unsigned long long*)best);
     else
-      hipLaunchKernelGGL(knn_donor_fast_kernel<FM>, dim3(rb, splits), dim3(256), lds, st, (const float*)R,
+      hipLaunchKernelGGL(knn_donor_fast_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
                          (unsigned long long*)best);
@@ -330,6 +359,7 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
   else if (F <= 32) go(std::integral_constant<int, 32>{});
+  else if (F <= 40) go(std::integral_constant<int, 40>{});
   else if (F <= 48) go(std::integral_constant<int, 48>{});
   else go(std::integral_constant<int, 64>{});
 }
