@@ -202,9 +202,32 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   for (int d0 = d_begin; d0 < d_end; d0 += TILE) {
     __syncthreads();
     const int nt = min(TILE, d_end - d0);
-    for (int e = threadIdx.x; e < nt * LD; e += 256) {
-      const int rr = e / LD, c = e % LD;
-      ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
+    if (XS && F == LD) {   // (XS widths only: at LD ≥ 48 the copy's registers cost occupancy)
+      // the tile is one contiguous run of D: float4 copies, all of a thread's loads in flight
+      // before its first LDS write (a scalar loop waited out one global round trip per element)
+      const float4* src = reinterpret_cast<const float4*>(D + (size_t)d0 * F);
+      float4* dst = reinterpret_cast<float4*>(ds);
+      const int n4 = nt * LD / 4;
+      constexpr int U = XS ? (TILE * LD / 4 + 255) / 256 : 0, UC = 4;   // rounds of UC loads
+#pragma unroll
+      for (int u0 = 0; u0 < U; u0 += UC) {
+        float4 v[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int e = threadIdx.x + 256 * (u0 + u);
+          v[u] = (u0 + u < U && e < n4) ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int e = threadIdx.x + 256 * (u0 + u);
+          if (u0 + u < U && e < n4) dst[e] = v[u];
+        }
+      }
+    } else {
+      for (int e = threadIdx.x; e < nt * LD; e += 256) {
+        const int rr = e / LD, c = e % LD;
+        ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
+      }
     }
     if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
     __syncthreads();
