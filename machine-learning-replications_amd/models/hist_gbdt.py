@@ -591,7 +591,7 @@ def _run_stage(st: _State, group):
     # spans more than 16 workgroups), sized from the kernel's own launch plan (one source of truth)
     from .smo import _num_cus
     plan = stage_plan(st.n, st.B, hist_len, _num_cus(dev))
-    groups, plen = int(plan[1]), max(1, int(plan[3]))
+    groups, plen, uses_partials = int(plan[1]), max(1, int(plan[3])), bool(plan[2])
     partials = runtime.workspace(dev, "gbdt_stage_partials", plen, torch.int64)
     prof = torch.zeros(st.B * groups * 6, dtype=torch.int64, device=dev) if PROFILE_STAGE_T >= 0 else None
     n_coll, n_xg = [0], [0]
@@ -604,6 +604,9 @@ def _run_stage(st: _State, group):
     base = peer.epoch if peer is not None else 0
 
     def stage(t, host_t, t_dev=None):
+        # a graph-replayed stage with a partial reduce advances the device counter inside that
+        # reduce launch (one launch less per stage)
+        tick_in_reduce = t_dev is not None and uses_partials and host_t <= st.T
         E.gbdt_stump_stage(host_t, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
                            bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
                            st.raw.data_ptr(), ptr(st.wt), ptr(st.seeds), st.row_off, st.subsample,
@@ -612,8 +615,8 @@ def _run_stage(st: _State, group):
                            ptr(st.bagw), ptr(st.frank), partials.data_ptr(), plen, st.lr, st.qscale,
                            st.dscale, st.min_leaf_q,
                            st.min_split_q, ptr(prof) if (prof is not None and t == PROFILE_STAGE_T) else 0,
-                           ptr(t_dev), s)
-        if t_dev is not None:
+                           ptr(t_dev), int(tick_in_reduce), s)
+        if t_dev is not None and not tick_in_reduce:
             E.gbdt_stage_tick(t_dev.data_ptr(), s)
         if group is not None and (t_dev is not None or t <= st.T):
             # stage t's histogram + root Σw r² + previous tree's leaf Σw r² + deviance + bag count:

@@ -1548,7 +1548,10 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
 constexpr int kRdSplit = 16;
 __global__ __launch_bounds__(256) void gbdt_stage_reduce_kernel(const long long* __restrict__ partials,
                                                                 long long* __restrict__ slot, int G,
-                                                                long long slot_m) {
+                                                                long long slot_m, int* __restrict__ tick) {
+  // graph replay: the device stage counter advances here (nothing in this launch reads it; the
+  // next stage launch does, after it) instead of in a separate gbdt_stage_tick launch
+  if (tick != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) tick[0] = tick[0] + 1;
   const int b = blockIdx.z;
   const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
   if (k >= slot_m) return;
@@ -1595,7 +1598,7 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
                       uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t dev,
                       uintptr_t bagw, uintptr_t frank, uintptr_t partials, long long partials_len, double lr,
                       double qscale, double dscale, double min_leaf_q, double min_split_q, uintptr_t prof,
-                      uintptr_t t_dev, uintptr_t stream) {
+                      uintptr_t t_dev, int tick_in_reduce, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stump_stage: 1 <= F <= 128");
   HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
   const bool active = subsample < 1.0;
@@ -1634,10 +1637,15 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   else if (mf) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   else hipLaunchKernelGGL((gbdt_stump_stage_kernel<false, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   launch_check();
+  // tick_in_reduce (graph replay with a partial reduce): the caller skips gbdt_stage_tick, so the
+  // reduce launch must exist — the caller derives that from gbdt_stage_plan (uses_partials) and t ≤ T
+  HFENS_REQUIRE(!tick_in_reduce || (t_dev != 0 && J.partials != nullptr && t <= T),
+                "gbdt_stump_stage: tick_in_reduce needs t_dev and a partial-reduce launch");
   if (J.partials != nullptr && t <= T) {
     long long* slot = (long long*)comm + (size_t)(t % 3) * B * slot_m;
     hipLaunchKernelGGL(gbdt_stage_reduce_kernel, dim3((unsigned)((slot_m + 255) / 256), kRdSplit, B), dim3(256), 0,
-                       as_stream(stream), (const long long*)J.partials, slot, groups, slot_m);
+                       as_stream(stream), (const long long*)J.partials, slot, groups, slot_m,
+                       tick_in_reduce ? (int*)t_dev : nullptr);
     launch_check();
   }
 }
