@@ -35,6 +35,10 @@ def buffer_bytes(W: int, cap: int) -> int:
     return W * 3 * cap * 8 + (-(-(3 * W * nchunk * 4) // 256)) * 256
 
 
+class PeerUnavailable(RuntimeError):
+    """Some rank of the group could not map a peer's buffer (every rank raises it together)."""
+
+
 class PeerComm:
     """IPC-mapped peer buffers of a process group; ``allreduce_`` sums int64 slots in place."""
 
@@ -68,14 +72,31 @@ class PeerComm:
             handles = [None] * self.W
             dist.all_gather_object(handles, h.tobytes(), group=group)
             ptrs, self.opened = [], []
+            err = ""
             for r, hb in enumerate(handles):
                 if r == self.me:
                     ptrs.append(self.own)
                     continue
                 hh = np.frombuffer(hb, dtype=np.uint8).copy()
-                E.xgmi_ipc_open(hh.ctypes.data, out.ctypes.data)
+                try:
+                    E.xgmi_ipc_open(hh.ctypes.data, out.ctypes.data)
+                except RuntimeError as e:   # this rank cannot map that peer's buffer
+                    err = f"rank {self.me} cannot map rank {r}'s buffer: {e}"
+                    break
                 ptrs.append(int(out[0]))
                 self.opened.append(int(out[0]))
+            # every rank takes the same path: the peer kernel only if ALL mappings exist
+            errs = [None] * self.W
+            dist.all_gather_object(errs, err, group=group)
+            bad = [e for e in errs if e]
+            if bad:
+                for p in self.opened:
+                    E.xgmi_ipc_close(p)
+                self.opened = []
+                dist.barrier(group=group)   # every mapping of this buffer is closed before it is freed
+                E.xgmi_free(self.own)
+                self.own = 0
+                raise PeerUnavailable("; ".join(bad))
         self.peers = torch.tensor(np.array(ptrs, dtype=np.uint64).view(np.int64), device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         dist.barrier(group=group)   # every mapping exists before anyone writes into it
@@ -132,7 +153,14 @@ def peer_comm(group, device, cap: int) -> Optional[PeerComm]:
         epoch = pc.epoch if pc is not None else 0
         if pc is not None:
             pc.close()
-        pc = PeerComm(group, device, cap)
+        try:
+            pc = PeerComm(group, device, cap)
+        except PeerUnavailable:
+            if MODE == "1":
+                raise
+            _OK[gid] = False   # auto: the group keeps RCCL (all ranks decided together)
+            _CACHE.pop(key, None)
+            return None
         pc.epoch = epoch
         _CACHE[key] = pc
     return pc

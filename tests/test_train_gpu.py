@@ -232,7 +232,7 @@ def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
         assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-12)
 
 
-def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0):
+def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0, fail_open_rank=-1):
     import os
     # ranks sharing ONE card: one hardware queue each, so 4 processes' queues are all resident
     # (a spinning peer kernel must not keep another rank's queue from being scheduled)
@@ -244,6 +244,12 @@ def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda:0")
+        if rank == fail_open_rank:   # this rank cannot map its peers' buffers
+            from hfens import ops
+
+            def _no_map(*a):
+                raise RuntimeError("injected: hipIpcOpenMemHandle failed")
+            setattr(ops.ext(), "xgmi_ipc_open", _no_map)
         X, y = _data(9000, 17, 53)
         for _ in range(2):   # twice: the second fit reuses the peer buffers (epochs continue)
             ms = [GradientBoostingClassifier(n_estimators=T, max_depth=1, subsample=subsample, random_state=s)
@@ -259,7 +265,7 @@ def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0):
         pdist.shutdown()
 
 
-def _run_dp_stage(world, xgmi, T=30, subsample=1.0):
+def _run_dp_stage(world, xgmi, T=30, subsample=1.0, fail_open_rank=-1):
     import socket
     import torch.multiprocessing as mp
     sk = socket.socket()
@@ -268,7 +274,8 @@ def _run_dp_stage(world, xgmi, T=30, subsample=1.0):
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_stage_worker, args=(r, world, port, q, xgmi, T, subsample)) for r in range(world)]
+    procs = [ctx.Process(target=_dp_stage_worker, args=(r, world, port, q, xgmi, T, subsample, fail_open_rank))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=150)
@@ -309,6 +316,15 @@ def test_gbdt_stage_xgmi_bit_identical(dev, world, subsample):
     assert path == "stage" and per_stage == 0.0 and xg == 1.0
     assert units == 31 // 3          # the stage loop ran as replayed HIP graphs
     _check_dp_stage_equal(dev, got, subsample=subsample)
+
+
+def test_gbdt_stage_xgmi_mapping_failure_falls_back(dev):
+    """HFENS_XGMI=auto and ONE rank cannot map a peer's buffer: every rank drops the peer path
+    together (the mapping errors are gathered before anyone uses the kernel) and the group keeps the
+    collective path — one all-reduce per stage, the single-process fit bit for bit, no hang."""
+    path, per_stage, xg, units, got = _run_dp_stage(3, "auto", fail_open_rank=1)
+    assert path == "stage" and per_stage == 1.0 and xg == 0.0
+    _check_dp_stage_equal(dev, got)
 
 
 def _gbdt_outputs(ms):
