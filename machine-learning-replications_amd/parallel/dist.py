@@ -51,7 +51,35 @@ def init_from_env(backend: str = None):
         # fail fast instead of hanging on a dead peer
         timeout = datetime.timedelta(seconds=float(os.environ.get("HFENS_DIST_TIMEOUT", "600")))
         dist.init_process_group(backend=backend, timeout=timeout)
+        if os.environ.get("HFENS_DIST_REQUIRE_DEVICE", "0") == "1" and torch.cuda.is_available():
+            require_device_tensors()
     return dist.group.WORLD, dist.get_rank(), dist.get_world_size()
+
+
+_TENSOR_COLLECTIVES = ("all_reduce", "all_gather", "broadcast", "reduce_scatter_tensor",
+                       "all_gather_into_tensor", "all_to_all_single", "reduce", "gather", "scatter")
+
+
+def require_device_tensors():
+    """Make every tensor collective called through ``torch.distributed`` raise on a host tensor.
+    RCCL (backend "nccl") only takes device tensors, while the gloo rehearsals on one card
+    (scripts/dp_rehearsal.sh) accept both; with HFENS_DIST_REQUIRE_DEVICE=1 a rehearsal fails where
+    an RCCL run would.  (Object collectives are not wrapped: torch stages them itself.)"""
+    def wrap(name, fn):
+        def checked(*args, **kw):
+            for a in list(args) + list(kw.values()):
+                ts = a if isinstance(a, (list, tuple)) else [a]
+                for t in ts:
+                    if isinstance(t, torch.Tensor) and not t.is_cuda:
+                        raise RuntimeError(f"torch.distributed.{name} on a host tensor {tuple(t.shape)} "
+                                           f"{t.dtype}: RCCL takes device tensors only")
+            return fn(*args, **kw)
+        checked.__wrapped__ = fn
+        return checked
+    for name in _TENSOR_COLLECTIVES:
+        fn = getattr(dist, name, None)
+        if fn is not None and not hasattr(fn, "__wrapped__"):
+            setattr(dist, name, wrap(name, fn))
 
 
 def local_rank() -> int:

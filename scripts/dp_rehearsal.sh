@@ -3,7 +3,8 @@
 # The cooperative kernels assume they own the CUs they were sized for, which is false when N
 # processes share one card, so the rehearsal runs the one-workgroup SMO / LR (same results).
 set -o pipefail
-export HFENS_DIST_BACKEND=gloo HFENS_SMO_COOP=0 HFENS_LOGREG_MEMBERS=1
+# HFENS_DIST_REQUIRE_DEVICE: every tensor collective must get device tensors, as under RCCL
+export HFENS_DIST_BACKEND=gloo HFENS_SMO_COOP=0 HFENS_LOGREG_MEMBERS=1 HFENS_DIST_REQUIRE_DEVICE=1
 mkdir -p gpurun_out/dp
 for N in ${RANKS:-2 4}; do
   timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \

@@ -2,7 +2,7 @@
 # Rehearse the 'dp' policy (>= 2^18 rows: row-sharded KNN / LassoCV / GBDT with the peer-memory stage
 # sum / row-sharded interior-point SVC) with 2 ranks sharing one card over gloo, against one process.
 set -o pipefail
-export HFENS_SMO_COOP=0 HFENS_LOGREG_MEMBERS=1
+export HFENS_SMO_COOP=0 HFENS_LOGREG_MEMBERS=1 HFENS_DIST_REQUIRE_DEVICE=1   # collectives on device tensors only, as under RCCL
 mkdir -p gpurun_out/dpl
 ROWS=${ROWS:-300000}
 HFENS_DIST_BACKEND=gloo timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
