@@ -461,7 +461,7 @@ def _seed_ens(rank, world, group):
     from hfens.parallel import ensemble
     X, y, _ = _data(1500, 12, 9)
     out = {}
-    for S in [s for s in (1, 2, 4) if world % s == 0]:
+    for S in [s for s in (1, 2, 4, 8) if world % s == 0]:
         ms = [GradientBoostingClassifier(n_estimators=8, max_depth=1, subsample=0.7, random_state=10 + k)
               for k in range(5)]
         mine = ensemble.fit_seed_ensemble(ms, X, y, rank, world, S, group)
@@ -481,7 +481,7 @@ def _seed_ens(rank, world, group):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_seed_parallel_bit_identical(world):
     """Seed / hybrid / row layouts of a 5-seed bagged ensemble (parallel/ensemble.py, BASELINE
     config 5): every seed's trees, leaf values and train scores equal the single-process batched
@@ -496,7 +496,7 @@ def test_seed_parallel_bit_identical(world):
     want = torch.tensor([[k, float(m.tree_feature_[t, 0]), float(m.tree_threshold_[t, 0])]
                          + [float(v) for v in m.tree_value_[t].reshape(-1)[:3]] + [float(m.train_score_[t])]
                          for k, m in enumerate(ms) for t in range(8)], dtype=torch.float64)
-    assert set(got) == {s for s in (1, 2, 4) if world % s == 0}
+    assert set(got) == {s for s in (1, 2, 4, 8) if world % s == 0}
     for S, rows in got.items():
         assert rows.shape == want.shape, (S, rows.shape)
         assert torch.equal(rows, want), S
