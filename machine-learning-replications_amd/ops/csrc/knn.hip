@@ -140,14 +140,23 @@ template <int FMAX>
 constexpr bool knn_fast_xs() { return (FMAX + 3) / 4 * 4 <= 40; }
 template <int FMAX>
 constexpr int knn_fast_tile() { return knn_fast_xs<FMAX>() ? kKnnFastTile : kKnnTile; }
+
 template <int FMAX>
 constexpr size_t knn_fast_lds() {
   constexpr int LD = (FMAX + 3) / 4 * 4;
   return (size_t)knn_fast_tile<FMAX>() * LD * sizeof(float) + knn_fast_tile<FMAX>() * sizeof(unsigned long long) +
          (knn_fast_xs<FMAX>() ? (size_t)LD * 256 * sizeof(float) : 0);
 }
-
 template <int FMAX>
+constexpr size_t knn_fast_lds_sm() {   // SM: only the receiver-value table
+  return knn_fast_xs<FMAX>() ? (size_t)((FMAX + 3) / 4 * 4) * 256 * sizeof(float) : 0;
+}
+
+// SM (F == LD): the donor rows are read straight from global memory at wave-uniform addresses —
+// scalar loads into SGPRs, the VALU reading them as operands — instead of broadcast LDS reads of a
+// staged tile.  A broadcast ds_read_b128 still moves 1 KB per wave through the CU's LDS port, so
+// with 8 waves per CU the staged kernel was bound by LDS bandwidth (≈ 20 b128 reads per donor pair).
+template <int FMAX, bool SM>
 __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
@@ -157,9 +166,9 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   constexpr int TILE = knn_fast_tile<FMAX>();
   typedef float f32x2v __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* ds = sm;
-  unsigned long long* dm = (unsigned long long*)(ds + TILE * LD);
-  float* xs = reinterpret_cast<float*>(dm + TILE);   // XS: [LD][256] receiver values
+  float* ds = sm;                                                           // !SM: [TILE][LD]
+  unsigned long long* dm = (unsigned long long*)(ds + (SM ? 0 : TILE * LD));  // !SM: [TILE]
+  float* xs = SM ? sm : reinterpret_cast<float*>(dm + TILE);   // XS: [LD][256] receiver values
   const int r = blockIdx.x * 256 + threadIdx.x;
   const bool active = r < nr;
   const int d_begin = blockIdx.y * per_split;
@@ -200,8 +209,11 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   __shared__ float s_scale[65];
   if (threadIdx.x <= 64) s_scale[threadIdx.x] = threadIdx.x > 0 ? (float)F / (float)threadIdx.x : 0.f;
   for (int d0 = d_begin; d0 < d_end; d0 += TILE) {
-    __syncthreads();
     const int nt = min(TILE, d_end - d0);
+    if constexpr (SM) {
+      __syncthreads();   // (s_scale / xs written before the first tile)
+    } else {
+    __syncthreads();
     if (XS && F == LD) {   // (XS widths only: at LD ≥ 48 the copy's registers cost occupancy)
       // the tile is one contiguous run of D: float4 copies, all of a thread's loads in flight
       // before its first LDS write (a scalar loop waited out one global round trip per element)
@@ -231,12 +243,13 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     }
     if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
     __syncthreads();
+    }
     if (!any) continue;
     // donors two at a time: their fast sums are independent fma chains (each 2 × ≤ 32 dependent
     // steps: the accumulation order must stay the exact kernel's), interleaved to hide the latency;
     // the bookkeeping then runs donor t before donor t + 1, exactly as one at a time
     auto donor = [&](int t, float sf) {
-      const unsigned long long md = dm[t];
+      const unsigned long long md = SM ? dmask[d0 + t] : dm[t];
       if ((need & ~md) == 0ull) return;
       const int present = F - __builtin_popcountll(mr | md);
       if (present <= 0) return;
@@ -273,7 +286,8 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
       float s = sf;
       if (!exact) {
         // ---- exact pass (knn_donor_kernel's masked direct differences, same order and roundings)
-        const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
+        const float4* xd4 = SM ? reinterpret_cast<const float4*>(D + (size_t)(d0 + t) * LD)
+                               : reinterpret_cast<const float4*>(ds + t * LD);
         const unsigned long long both = ~(mr | md);
         const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
         float s0 = 0.f, s1 = 0.f;
@@ -305,8 +319,10 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     };
     for (int t = 0; t < nt; t += 2) {
       const int t1 = t + 1 < nt ? t + 1 : t;
-      const float4* xa = reinterpret_cast<const float4*>(ds + t * LD);
-      const float4* xb = reinterpret_cast<const float4*>(ds + t1 * LD);
+      const float4* xa = SM ? reinterpret_cast<const float4*>(D + (size_t)(d0 + t) * LD)
+                            : reinterpret_cast<const float4*>(ds + t * LD);
+      const float4* xb = SM ? reinterpret_cast<const float4*>(D + (size_t)(d0 + t1) * LD)
+                            : reinterpret_cast<const float4*>(ds + t1 * LD);
       // ---- fast pass: packed fma over feature pairs, even features into .x, odd into .y — every
       // quad, F or not (features ≥ F are zero on both sides: fma(0, 0, acc) = acc; a runtime
       // `4q < F` guard would put a branch and an LDS wait between the quads' reads)
@@ -359,6 +375,7 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   if (splits < 1) splits = 1;
   const char* kenv = std::getenv("HFENS_KNN_KERNEL");
   const bool direct = kenv && kenv[0] == 'd';   // "direct": the exact pass for every donor
+  const bool lds_tiles = kenv && kenv[0] == 'l';  // "lds": the fast pass on staged LDS tiles
   auto go = [&](auto fm) {
     constexpr int FM = decltype(fm)::value;
     constexpr int LD = (FM + 3) / 4 * 4;
@@ -373,8 +390,13 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
                          (unsigned long long*)best);
+    else if (F == LD && !lds_tiles && (D & 15) == 0)
+      hipLaunchKernelGGL((knn_donor_fast_kernel<FM, true>), dim3(rb, nsp), dim3(256), knn_fast_lds_sm<FM>(), st,
+                         (const float*)R, (const unsigned long long*)rmask, nr, (const float*)D,
+                         (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
+                         (unsigned long long*)best);
     else
-      hipLaunchKernelGGL(knn_donor_fast_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
+      hipLaunchKernelGGL((knn_donor_fast_kernel<FM, false>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
                          (unsigned long long*)best);
