@@ -1524,9 +1524,9 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   }
   if (pst && tid == 0) pst[2] = (long long)__builtin_amdgcn_s_memtime() - t_0;
   sg_block_sum<6, kW>(acc6, red, ext);
-  // publish: with many workgroups per model, plain stores of the whole partial slot (reduced by
-  // gbdt_stage_reduce_kernel — hundreds of workgroups' int64 atomics on the same ~50 KB of
-  // histogram serialise at the memory side); with few, atomics straight into the slot
+  // publish: int64 atomics straight into the slot (the default at every grid size: measured faster
+  // than the partial slots + reduce launch up to 245 workgroups per model, sg_plan), or plain stores
+  // of the whole partial slot for gbdt_stage_reduce_kernel (HFENS_SG_ATOMIC_GROUPS)
   long long* part = J.partials ? J.partials + ((size_t)b * gridDim.x + blockIdx.x) * slot_m : nullptr;
   if (tid < kSgExtra) {
     // extras layout: [0] root Σw r² (t), [1..3] leaf Σw r² (t−1), [4] deviance (t−1), [5] bag (t)
@@ -1584,7 +1584,14 @@ static void sg_plan(long long n, int B, int hist_len, int ncu, long long* out) {
   const long long slot_m = 3LL * hist_len + kSgExtra;
   out[0] = rows;
   out[1] = groups;
-  out[2] = groups > kRdSplit ? 1 : 0;
+  // every workgroup adds its histogram straight into the slot with int64 atomics (integer sums:
+  // the same bits in any order); HFENS_SG_ATOMIC_GROUPS = g publishes partial slots for
+  // gbdt_stage_reduce_kernel above g workgroups per model instead.  Measured (gbdt_shard_probe,
+  // profiles/r3_gbdt_dp.md): atomics at 123 / 245 workgroups were 2–4 % faster per stage than
+  // partials + the reduce launch (43.5 vs 45.5 µs at 125k rows, 87.7 vs 89.2 µs at 1M).
+  const char* ae = std::getenv("HFENS_SG_ATOMIC_GROUPS");   // read per call: tests and probes sweep it
+  const long long amax = ae ? std::max(1, std::atoi(ae)) : (1LL << 40);
+  out[2] = groups > amax ? 1 : 0;
   out[3] = out[2] ? (long long)B * groups * slot_m : 0;
 }
 

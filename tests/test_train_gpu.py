@@ -531,15 +531,20 @@ def test_develop_plan_ahead_identical(dev, monkeypatch):
     assert torch.equal(m0.oof_meta_, m1.oof_meta_)
 
 
-@pytest.mark.parametrize("wgs", ["1", "2", "4"])
-def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs):
+@pytest.mark.parametrize("wgs,atomic", [("1", None), ("2", None), ("4", None), ("1", "16"), ("2", "16"),
+                                         ("4", "16")])
+def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs, atomic):
     """the partial-slot buffer is sized from the kernel's own launch plan
     (gbdt_stage_plan), so every workgroups-per-CU setting and model count runs (no 'partials
-    buffer too small'), and the trees do not depend on the grid."""
+    buffer too small'), and the trees do not depend on the grid.  atomic = None: every workgroup
+    adds into the slot with int64 atomics (the default); "16": above 16 workgroups per model the
+    partial slots + reduce launch — the same integers either way."""
     from hfens.models import hist_gbdt
     X, y = _data(120_000, 12, 7)
     ref = None
     monkeypatch.setenv("HFENS_SG_WGS_PER_CU", wgs)
+    if atomic is not None:
+        monkeypatch.setenv("HFENS_SG_ATOMIC_GROUPS", atomic)
     for B in (1, 5, 6):
         ms = [GradientBoostingClassifier(n_estimators=4, max_depth=1, random_state=s) for s in range(B)]
         fit_gbdt_batch(ms, X.to(dev), y.to(dev))
@@ -547,9 +552,12 @@ def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs):
         plan = hist_gbdt.stage_plan(X.shape[0], B, int(ms[0]._bin_mapper.nb_host.sum()),
                                     torch.cuda.get_device_properties(dev).multi_processor_count)
         assert plan[1] * plan[0] >= X.shape[0] and (plan[2] == 0) == (plan[3] == 0)
+        assert plan[2] == (1 if atomic is not None and plan[1] > int(atomic) else 0)
         if B == 1:
-            ref = ms[0].tree_feature_.cpu()
-        assert torch.equal(ms[0].tree_feature_.cpu(), ref)
+            ref = (ms[0].tree_feature_.cpu(), ms[0].tree_value_.cpu(), ms[0].train_score_.cpu())
+        assert torch.equal(ms[0].tree_feature_.cpu(), ref[0])
+        assert torch.equal(ms[0].tree_value_.cpu(), ref[1])
+        assert torch.equal(ms[0].train_score_.cpu(), ref[2])
 
 
 def _lowrank_dp_worker(rank, world, port, q):
