@@ -74,9 +74,36 @@ __device__ __forceinline__ double couple_p1(double dec, double A, double B) {
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
 
+// X3: the sv·z products on the bf16 matrix cores, exactly split.  Every f32 operand v is cut into
+// three bf16 pieces v = v0 + v1 + v2 (truncation: 8 + 8 + 8 significant bits, no rounding), and
+// sv·z = Σ_f Σ_{i+j ≤ 2} sv_f,i · z_f,j (the 6 largest piece products; the dropped ones are
+// ≤ 3·2⁻²⁴ of |sv_f||z_f|, f32-level).  The 6·2KS (product, feature) items are packed along K in two
+// lane-half lists — half 0: (0,0), (0,1), (1,0); half 1: (0,2), (1,1), (2,0) as (sv piece, z
+// piece) — so one v_mfma_f32_32x32x16_bf16 takes 16 items: ⌈3KS/4⌉ MFMAs per 32 × 32 tile against
+// KS of v_mfma_f32_32x32x2f32 (7 vs 9 for the 17-feature model, at 16× the rate per instruction).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int KS>
+constexpr int x3_blocks() { return (3 * 2 * KS + 7) / 8; }   // MFMA k-blocks of 8 items per half
+
+__device__ __forceinline__ void x3_split(float v, unsigned (&b)[3]) {   // bf16 bits of the 3 pieces
+  const unsigned u0 = __float_as_uint(v) & 0xFFFF0000u;
+  const float r1 = v - __uint_as_float(u0);
+  const unsigned u1 = __float_as_uint(r1) & 0xFFFF0000u;
+  const float r2 = r1 - __uint_as_float(u1);
+  b[0] = u0 >> 16;
+  b[1] = u1 >> 16;
+  b[2] = __float_as_uint(r2) >> 16;   // r2 has ≤ 8 significant bits: exact in bf16
+}
+
+// piece of the SV (js) and of the row (iz) for item-list position p (0..2) of lane half h
+__host__ __device__ constexpr int x3_sv_piece(int h, int p) { return h ? 2 - p : (p == 1 ? 1 : 0); }
+__host__ __device__ constexpr int x3_z_piece(int h, int p) { return h ? p : (p == 2 ? 1 : 0); }
+
 // KS = MFMA k-steps (2 features each); the row tile holds 64·F ≤ 64·2KS values, so each lane
 // prefetches at most 2KS of them.
-template <int KS, int W, typename TX>
+template <int KS, int W, typename TX, bool X3 = false>
 __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restrict__ X,
                                                                        long long n, StackModel M,
                                                                        int CH, int nodes_in_lds,
@@ -85,8 +112,10 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
   const int F = M.F, mp = M.mp;
   const int ldx = F | 1;
   const int nch = (mp + CH - 1) / CH;
-  float* sv_l = lds;                              // [2KS][CH]
-  float* sn_l = sv_l + 2 * KS * CH;               // [CH]
+  constexpr int NB3 = x3_blocks<KS>();
+  float* sv_l = lds;                              // [2KS][CH] f32, or X3: [NB3][CH][16] bf16
+  unsigned short* sv3 = reinterpret_cast<unsigned short*>(lds);
+  float* sn_l = sv_l + (X3 ? NB3 * CH * 8 : 2 * KS * CH);   // [CH]
   float* cf_l = sn_l + CH;                        // [CH]
   float* mu_l = cf_l + CH;                        // [2KS] mean, then [2KS] 1/scale
   float* is_l = mu_l + 2 * KS;
@@ -96,6 +125,29 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
   float* nv_l = reinterpret_cast<float*>(nd_l + (nodes_in_lds ? M.T * M.K : 0));
   auto stage = [&](int c) {  // SV chunk c → LDS (block-wide; caller synchronises)
     const int c0 = c * CH, cl = min(CH, mp - c0);
+    if constexpr (X3) {
+      // item (m, j, 8h + e): list position q = 8m + e of half h → (piece, feature) of SV j
+      for (int i = threadIdx.x; i < NB3 * CH * 16; i += blockDim.x) {
+        const int m = i / (CH * 16), rem = i - m * CH * 16, j = rem >> 4, he = rem & 15;
+        const int h = he >> 3, q = 8 * m + (he & 7);
+        unsigned v = 0;
+        if (j < cl && q < 3 * 2 * KS) {
+          const int pl = q / (2 * KS), f = q - pl * (2 * KS);
+          if (f < F) {
+            unsigned b[3];
+            x3_split(M.svt[(size_t)f * mp + c0 + j], b);
+            const int js = x3_sv_piece(h, pl);
+            v = js == 0 ? b[0] : (js == 1 ? b[1] : b[2]);
+          }
+        }
+        sv3[i] = (unsigned short)v;
+      }
+      for (int i = threadIdx.x; i < 2 * CH; i += blockDim.x) {
+        const int k = i / CH, j = i - k * CH;
+        sn_l[i] = j < cl ? (k == 0 ? M.ngl2e * M.sn[c0 + j] : M.coef[c0 + j]) : 0.f;
+      }
+      return;
+    }
     for (int i = threadIdx.x; i < (2 * KS + 2) * CH; i += blockDim.x) {
       const int k = i / CH, j = i - k * CH;
       float v = 0.f;
@@ -175,6 +227,46 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
     }
     zna += __shfl_xor(zna, 32, kWave);
     znb += __shfl_xor(znb, 32, kWave);
+    // X3: this lane's row pieces for its lane half's item list (rows r32 and 32 + r32)
+    bf16x8_t z3a[X3 ? NB3 : 1], z3b[X3 ? NB3 : 1];
+    if constexpr (X3) {
+      unsigned pa3[2 * KS][3], pb3[2 * KS][3];
+#pragma unroll
+      for (int f = 0; f < 2 * KS; ++f) {
+        float a = 0.f, b = 0.f;
+        if (f < F) {
+          const float mu = mu_l[f], is = is_l[f];
+          a = (xw[r32 * ldx + f] - mu) * is;
+          b = (xw[(32 + r32) * ldx + f] - mu) * is;
+        }
+        x3_split(a, pa3[f]);
+        x3_split(b, pb3[f]);
+      }
+#pragma unroll
+      for (int m = 0; m < NB3; ++m) {
+        unsigned wa[4], wb[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          unsigned lo_a = 0, hi_a = 0, lo_b = 0, hi_b = 0;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const int q = 8 * m + 2 * e2 + d;
+            unsigned va = 0, vb = 0;
+            if (q < 3 * 2 * KS) {
+              const int pl = q / (2 * KS), f = q - pl * (2 * KS);
+              const int i0 = x3_z_piece(0, pl), i1 = x3_z_piece(1, pl);
+              va = hi ? pa3[f][i1] : pa3[f][i0];
+              vb = hi ? pb3[f][i1] : pb3[f][i0];
+            }
+            if (d == 0) { lo_a = va; lo_b = vb; } else { hi_a = va; hi_b = vb; }
+          }
+          wa[e2] = lo_a | (hi_a << 16);
+          wb[e2] = lo_b | (hi_b << 16);
+        }
+        z3a[m] = __builtin_bit_cast(bf16x8_t, (u32x4_t){wa[0], wa[1], wa[2], wa[3]});
+        z3b[m] = __builtin_bit_cast(bf16x8_t, (u32x4_t){wb[0], wb[1], wb[2], wb[3]});
+      }
+    }
     // exponent of exp(−γ‖sv−z‖²) in base 2: (γ'·‖sv‖²) + (γ'·‖z‖²) + (−2γ')·(sv·z), γ' = −γ·log2 e;
     // ‖sv‖² is staged pre-scaled.  No clamp at 0: a rounding-negative distance only turns
     // exp2 into 1+ε, exactly like the double-precision kernel evaluation it mirrors.
@@ -183,6 +275,16 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
     auto mma = [&](int t, f32x16& A, f32x16& B) {
       A = f32x16{0.f};
       B = f32x16{0.f};
+      if constexpr (X3) {
+#pragma unroll
+        for (int m = 0; m < NB3; ++m) {
+          const u32x4_t raw = *reinterpret_cast<const u32x4_t*>(&sv3[((size_t)m * CH + t + r32) * 16 + 8 * hi]);
+          const bf16x8_t sv = __builtin_bit_cast(bf16x8_t, raw);
+          A = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sv, z3a[m], A, 0, 0, 0);
+          B = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sv, z3b[m], B, 0, 0, 0);
+        }
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const float sv = sv_l[(2 * s + hi) * CH + t + r32];
@@ -267,19 +369,22 @@ __global__ __launch_bounds__(64 * W) void stack_infer_kernel(const TX* __restric
   }
 }
 
-static size_t stack_lds_bytes(int W, int F, int CH, int ks, size_t node_bytes) {
+// floats of LDS per staged SV: f32 k-major features, or X3's bf16 item blocks; + ‖sv‖², coef
+static int stack_sv_floats(int ks, bool x3) { return x3 ? ((3 * 2 * ks + 7) / 8) * 8 + 2 : 2 * ks + 2; }
+
+static size_t stack_lds_bytes(int W, int F, int CH, int ks, size_t node_bytes, bool x3 = false) {
   size_t xs = (size_t)W * 64 * (F | 1);
   xs = (xs + 3) & ~(size_t)3;
-  return ((size_t)(2 * ks + 2) * CH + 4 * ks + xs) * 4 + node_bytes;
+  return ((size_t)stack_sv_floats(ks, x3) * CH + 4 * ks + xs) * 4 + node_bytes;
 }
 
 constexpr size_t kStackLdsCap = 160 * 1024;
 
 // SV chunk (multiple of 32): all SVs resident when they fit, else the largest chunk that does.
-static int stack_chunk(int W, int F, int mp, int ks, size_t node_bytes) {
-  const size_t fixed = stack_lds_bytes(W, F, 0, ks, node_bytes);
+static int stack_chunk(int W, int F, int mp, int ks, size_t node_bytes, bool x3 = false) {
+  const size_t fixed = stack_lds_bytes(W, F, 0, ks, node_bytes, x3);
   if (fixed >= kStackLdsCap) return 0;
-  long long ch = (long long)((kStackLdsCap - fixed) / ((size_t)(2 * ks + 2) * 4)) / 32 * 32;
+  long long ch = (long long)((kStackLdsCap - fixed) / ((size_t)stack_sv_floats(ks, x3) * 4)) / 32 * 32;
   if (ch > mp) ch = mp;
   return (int)ch;
 }
@@ -296,26 +401,26 @@ struct StackPlan {
 
 // LDS plan for W waves/workgroup: SVs resident if at all possible (trees only when they fit too);
 // occupancy from the runtime for the kernel's real register count.
-template <int KS, int W, typename TX>
+template <int KS, int W, typename TX, bool X3 = false>
 static StackPlan stack_plan(const StackModel& M) {
   StackPlan p;
   const size_t node_bytes = M.st_off ? 0 : (size_t)M.T * M.K * 20;
   bool in_lds = node_bytes > 0 && node_bytes <= 24 * 1024;
-  int CH = stack_chunk(W, M.F, M.mp, KS, in_lds ? node_bytes : 0);
+  int CH = stack_chunk(W, M.F, M.mp, KS, in_lds ? node_bytes : 0, X3);
   if (in_lds && CH < M.mp) {
-    const int ch2 = stack_chunk(W, M.F, M.mp, KS, 0);
+    const int ch2 = stack_chunk(W, M.F, M.mp, KS, 0, X3);
     if (ch2 > CH) { in_lds = false; CH = ch2; }
   }
   if (CH < 32) return p;
   p.CH = CH;
   p.in_lds = in_lds;
-  p.lds = stack_lds_bytes(W, M.F, CH, KS, in_lds ? node_bytes : 0);
-  HFENS_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p.blocks_per_cu, stack_infer_kernel<KS, W, TX>,
+  p.lds = stack_lds_bytes(W, M.F, CH, KS, in_lds ? node_bytes : 0, X3);
+  HFENS_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p.blocks_per_cu, stack_infer_kernel<KS, W, TX, X3>,
                                                            64 * W, p.lds));
   return p;
 }
 
-template <int KS, int W, typename TX>
+template <int KS, int W, typename TX, bool X3 = false>
 static void stack_go(const TX* X, long long n, const StackModel& M, const StackPlan& p, int grid,
                      float* out, hipStream_t st) {
   if (grid <= 0) {
@@ -327,7 +432,7 @@ static void stack_go(const TX* X, long long n, const StackModel& M, const StackP
     const long long cap = (long long)(p.blocks_per_cu > 0 ? p.blocks_per_cu : 1) * ncu;
     grid = (int)(need < cap ? need : cap);
   }
-  hipLaunchKernelGGL((stack_infer_kernel<KS, W, TX>), dim3(grid), dim3(64 * W), p.lds, st, X, n, M, p.CH,
+  hipLaunchKernelGGL((stack_infer_kernel<KS, W, TX, X3>), dim3(grid), dim3(64 * W), p.lds, st, X, n, M, p.CH,
                      p.in_lds, out);
   launch_check();
 }
@@ -346,6 +451,20 @@ static void stack_pick(const TX* X, long long n, const StackModel& M, int grid, 
                        hipStream_t st) {
   static const int forced = env_int("HFENS_STACK_WAVES", 0);
   constexpr bool narrow = KS <= 9;
+  if constexpr (narrow) {
+    // X3 (bf16x3 products on the bf16 matrix cores) when every SV stays resident in LDS;
+    // HFENS_STACK_X3=0 keeps the f32 MFMA path
+    if (env_int("HFENS_STACK_X3", 1) != 0) {
+      const int xw = forced == 12 || forced == 8 ? forced : env_int("HFENS_STACK_X3_WAVES", 8);
+      if (xw == 12) {
+        const StackPlan q = stack_plan<KS, 12, TX, true>(M);
+        if (q.CH >= M.mp && q.blocks_per_cu > 0) return stack_go<KS, 12, TX, true>(X, n, M, q, grid, out, st);
+      } else {
+        const StackPlan q = stack_plan<KS, 8, TX, true>(M);
+        if (q.CH >= M.mp && q.blocks_per_cu > 0) return stack_go<KS, 8, TX, true>(X, n, M, q, grid, out, st);
+      }
+    }
+  }
   const StackPlan p8 = stack_plan<KS, 8, TX>(M);
   StackPlan p12, p16;
   if constexpr (narrow) {
