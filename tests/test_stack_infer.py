@@ -116,6 +116,24 @@ def test_stack_infer_random(dev, F, m, T, depth, grid, stumps):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("F,m,T,depth,stumps", [(17, 434, 100, 1, True), (5, 64, 10, 2, False), (11, 250, 30, 1, True)])
+def test_stack_infer_x3_matches_f32_mfma(dev, monkeypatch, F, m, T, depth, stumps):
+    """The RBF products as an exact three-way bf16 split on the bf16 matrix cores (stack.hip X3,
+    the default when the SVs fit LDS) against the f32-MFMA kernel (HFENS_STACK_X3=0) and the fp64
+    host reference: the decision values differ only by the dropped ≤ 3·2⁻²⁴ piece products."""
+    pk_h = _random_pstack(F, m, T, depth, "cpu", seed=F * m, stumps=stumps)
+    pk_d = _random_pstack(F, m, T, depth, dev, seed=F * m, stumps=stumps)
+    x = torch.randn(20000, F, dtype=torch.float64)
+    want = ref.stack_infer(x.to(torch.float32), pk_h)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HFENS_STACK_X3", mode)
+        out[mode] = ops.stack_infer(x.to(dev), pk_d).cpu().double()
+    assert torch.allclose(out["1"], out["0"], atol=1e-6)
+    assert torch.allclose(out["1"], want, atol=5e-6)
+
+
+@pytest.mark.gpu
 def test_stack_infer_out_buffer(dev, ckpt_path):
     gpu = load_checkpoint(ckpt_path, device=dev)
     pk = gpu._packed_stack(torch.device(dev))
