@@ -267,7 +267,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     n = X.shape[0]
     y_np = None
     svc_pre = None
-    if plan is not None and group is None and svc_group is None and int(plan["y_np"].shape[0]) == n:
+    if plan is not None and group is None and int(plan["y_np"].shape[0]) == n:
         # folds, row sets and SVC problem expansions computed ahead from the same labels (plan_stacking)
         y_np, folds_np, svc_pre = plan["y_np"], plan["folds_np"], plan["svc_pre"]
     elif group is None:

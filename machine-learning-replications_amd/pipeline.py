@@ -78,16 +78,22 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
     # the labels come over in a non-blocking copy issued now, long finished by then
     plan_box = {}
     overlap = None
-    if group is None and dev.type == "cuda" and PLAN_AHEAD:
-        y_pin = torch.empty(y_dev.shape[0], dtype=torch.float64, pin_memory=True)
-        y_pin.copy_(y_dev, non_blocking=True)
+
+    def plan_ahead(y_full):
+        # (task policy: called after the all-gather, so every rank plans from the same full labels)
+        y_pin = torch.empty(y_full.shape[0], dtype=torch.float64, pin_memory=True)
+        y_pin.copy_(y_full, non_blocking=True)
         y_ev = torch.cuda.Event()
         y_ev.record()
 
-        def overlap():
+        def run():
             from .models.stack_trainer import plan_stacking
             y_ev.synchronize()
             plan_box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
+        return run
+
+    if group is None and dev.type == "cuda" and PLAN_AHEAD:
+        overlap = plan_ahead(y_dev)
     from .utils.timing import hmark
     hmark("develop")
     with timer.stage("impute"):
@@ -105,7 +111,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             aux = runtime.stream(dev, "aux")
         hmark("imputer_fit")
         run_sel = None
-        if aux is not None and group is None:
+        if aux is not None and (group is None or task):
             # the held-out rows' planning and launch (host numpy, ≈ 1 ms at 10k rows) are deferred
             # into the LassoCV path's device time below, off the host's critical path
             (X_dev, _), run_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux], defer=True)
@@ -115,6 +121,8 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
+            if dev.type == "cuda" and PLAN_AHEAD:
+                overlap = plan_ahead(y_dev)
     fit_group = None if task else group
     with timer.stage("select"):
         lasso_overlap = overlap
