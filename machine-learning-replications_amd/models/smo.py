@@ -383,8 +383,22 @@ _WS_STATE_BYTES = 88     # sizeof(WsState) in svm_ws.hip
 WS_MAX_F = 48            # features the working-set kernel's register/LDS budget admits
 
 
+# K-cached rounds (svm_ws.hip ws_kc_round_kernel): q = 256 with the working set's kernel matrix in
+# LDS and a one-wave pair loop; for F ≤ WS_KC_MAX_F.  HFENS_SVM_WS_KC=0 keeps the q = 1024 solver.
+WS_KC = os.environ.get("HFENS_SVM_WS_KC", "1") != "0"
+WS_KC_MAX_F = 24
+WS_KC_Q = 256
+
+
+def ws_kc(F: int) -> bool:
+    return WS_KC and F <= WS_KC_MAX_F
+
+
 def ws_q(F: int) -> int:
-    """Working-set size of svm_ws.hip for F features (one slot per thread; z_B must fit LDS)."""
+    """Working-set size of svm_ws.hip for F features (K-cached: 256; else one slot per thread with
+    z_B in LDS: 1024 / 512)."""
+    if ws_kc(F):
+        return WS_KC_Q
     return 1024 if F <= 24 else 512
 
 
@@ -615,6 +629,8 @@ WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.2"))
 # in its next working set)
 WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
+# the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
+WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
@@ -682,7 +698,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         # a batch still unconverged after them reports err and is re-solved synchronously by
         # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
         # group's stream starts within one chunk of host launch time.
-        left = min(WS_ROUNDS_AHEAD, max_outer)
+        left = min(WS_KC_ROUNDS_AHEAD if ws_kc(F) else WS_ROUNDS_AHEAD, max_outer)
         while left > 0:
             k = min(_WS_ENQ_CHUNK, left)
             for r in runs:
@@ -718,7 +734,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         return out
     LAST_WS_STATS.set_thunk(stats)
     LAST_SMO_INFO.clear()
-    LAST_SMO_INFO.update(problems=P, max_l=int(max(p.l for p in live)), solver="ws", q=Q, ws_groups=len(runs))
+    LAST_SMO_INFO.update(problems=P, max_l=int(max(p.l for p in live)), solver="ws", q=Q, ws_groups=len(runs),
+                         ws_kc=ws_kc(F))
     return alpha, rho, iters, err
 
 
@@ -755,7 +772,15 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
         out["idx_dev"] = _to_dev(out["idx"], device)
     done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
 
+    kc = ws_kc(F)
+
     def steps(k):
+        if kc:
+            E.ws_steps_kc(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(),
+                          G.data_ptr(), states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(),
+                          wsprev.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner,
+                          WS_INNER_FRAC, k, s)
+            return
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
                    wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
@@ -1084,6 +1109,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
            else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
     hmark("svc_solve_enqueued")
+    solver = LAST_SMO_INFO.get("solver")   # this batch's solver (the global is overwritten by later batches)
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
     AB = [None] * len(svcs)
     decs, labs, pl = [], [], []
@@ -1132,11 +1158,11 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             E.platt_batch(pdev.data_ptr(), len(pl), dcat.data_ptr(), lcat.data_ptr(), ABt.data_ptr(),
                           ops.stream_ptr(device))
             return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
-                        keep=(pdev, dcat, lcat), device=device, args=args)
+                        keep=(pdev, dcat, lcat), device=device, args=args, solver=solver)
         for k, f in enumerate(pl):
             AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
     return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=None,
-                device=device, args=args)
+                device=device, args=args, solver=solver)
 
 
 def finish_svc_batch(st: dict):
@@ -1154,9 +1180,9 @@ def finish_svc_batch(st: dict):
         if st.get("retried"):
             raise RuntimeError("SMO: the synchronous re-solve failed again")
         import warnings
-        ws = LAST_SMO_INFO.get("solver") == "ws"
-        warnings.warn("working-set SMO needed more than %d rounds; re-solving with host-checked rounds"
-                      % WS_ROUNDS_AHEAD if ws else
+        ws = st.get("solver") == "ws"
+        warnings.warn("working-set SMO needed more than the rounds enqueued ahead; re-solving with host-checked rounds"
+                      if ws else
                       "cooperative SMO timed out waiting for a member; re-solving with one workgroup per problem")
         flag = _WS_SYNC if ws else _FORCE_SINGLE
         flag[0] = True

@@ -521,9 +521,22 @@ def _solve_groups(group, n: int):
     key = (id(group), n)
     if key not in _GROUPS:
         import torch.distributed as dist
-        ranks = list(range(dist.get_world_size(group)))
+        # new_group takes GLOBAL ranks: the members of `group` as the default group numbers them
+        ranks = dist.get_process_group_ranks(group)
         _GROUPS[key] = [dist.new_group(ranks) for _ in range(n)]
     return _GROUPS[key]
+
+
+def _threads_safe(group) -> bool:
+    """Concurrent host threads may each drive a communicator only where the backend tolerates
+    interleaved blocking collectives: gloo does (CPU threads), RCCL does not promise it — its
+    kernels block until every peer arrives, and the process's few hardware queues and the caching
+    allocator's synchronisations couple the threads' streams — so an RCCL-backed fit runs its
+    solves from ONE thread, in one fixed collective order on every rank."""
+    if group is None:
+        return True
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
 
 
 _GROUPS: dict = {}
@@ -635,7 +648,7 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
         for p in probs:
             if p.fold >= 0 and p.rows is None and first:
                 dec_cv[p.held] = p.const      # constant folds: set once (rank 0), summed below
-        nthr = min(IPM_THREADS, len(cv)) if Z.is_cuda else 1
+        nthr = min(IPM_THREADS, len(cv)) if (Z.is_cuda and _threads_safe(group)) else 1
         if nthr > 1:
             # the Platt CV solves are independent: host threads, each on its own stream and scratch
             # buffers (and, data parallel, its own communicator), so one solve's latency-bound steps

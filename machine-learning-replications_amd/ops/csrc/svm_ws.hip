@@ -228,24 +228,18 @@ constexpr size_t ws_sel_lds_bytes(int Q) { return 32 * 4 + 4096 * 4 + 1024 * 4 +
 // M = points per lane.  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L its points
 // w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots give
 // index-ordered ranks.  Writes B (point indices, new picks first) to wsidx[b][0, nws).
-template <int M, int Q>
-__global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
-    const WsProb* __restrict__ probs, WsState* __restrict__ states, int* __restrict__ wsidx,
-    int* __restrict__ wsprev, double eps, int max_outer, WsAux X) {
-  const int b = blockIdx.x;
-  WsState* S = states + b;
-  if (S->done) return;
-  const WsProb P = probs[b];
+// The selection body, shared by ws_select_kernel and the fused K-cached round (ws_kc_round_kernel):
+// every thread of the 1024-thread workgroup calls it; returns the working-set size (B in widx[0, nws),
+// LDS, visible to every thread on return) or −1 when problem b is done.  LDS: shi [16], binfo [16],
+// hist [2][2048], bm [1024] (both dead on return), widx [Q].
+template <int M, int Q, bool kWriteIdx>
+__device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S, int* __restrict__ wsidx,
+                                              int* __restrict__ wsprev, double eps, int max_outer, const WsAux& X,
+                                              int* shi, int* binfo, int* hist, unsigned* bm, int* widx) {
   const int nprev = S->nprev;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l = P.l;
-  extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
-  int* shi = reinterpret_cast<int*>(ws_lds);                     // [16]
-  int* binfo = shi + 16;                                         // [8] (+8 pad)
-  int* hist = shi + 32;                                          // [2][2048]
-  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);       // [1024]
-  int* widx = reinterpret_cast<int*>(bm + 1024);                 // [Q]
   const int t0 = wave * 64 * M + lane;
   const long long c0 = __builtin_amdgcn_s_memtime();
   // ---- global gap from the maxima published by the gradient kernel
@@ -275,7 +269,7 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
   n_up &= 0xFFFF;
   if (!(gap >= eps) || S->outer >= max_outer || n_up == 0 || n_low == 0) {
     if (tid == 0) { S->done = 1; S->gap = gap; S->nc = 0; S->nws = 0; }
-    return;
+    return -1;
   }
   if (tid == 0) { X.gkey[2 * b] = 0ull; X.gkey[2 * b + 1] = 0ull; }   // consumed (all read it above)
   // ---- level-1 histograms (top 11 key bits)
@@ -361,7 +355,8 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
   __syncthreads();   // every old entry was read before the new picks overwrite the list
   const int nws = nnew + ktot;
   for (int w = tid; w < nnew; w += kWsThreads) wsprev[(size_t)b * (Q / 2) + w] = widx[w];
-  for (int w = tid; w < nws; w += kWsThreads) wsidx[(size_t)b * Q + w] = widx[w];
+  if (kWriteIdx)
+    for (int w = tid; w < nws; w += kWsThreads) wsidx[(size_t)b * Q + w] = widx[w];
   const long long c1 = __builtin_amdgcn_s_memtime();
   if (tid == 0) {
     S->cyc_select += c1 - c0;
@@ -372,6 +367,24 @@ __global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
     S->nprev = nnew;
     S->gap = gap;
   }
+  return nws;
+}
+
+template <int M, int Q>
+__global__ __launch_bounds__(kWsThreads) void ws_select_kernel(
+    const WsProb* __restrict__ probs, WsState* __restrict__ states, int* __restrict__ wsidx,
+    int* __restrict__ wsprev, double eps, int max_outer, WsAux X) {
+  const int b = blockIdx.x;
+  WsState* S = states + b;
+  if (S->done) return;
+  const WsProb P = probs[b];
+  extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
+  int* shi = reinterpret_cast<int*>(ws_lds);                     // [16]
+  int* binfo = shi + 16;                                         // [8] (+8 pad)
+  int* hist = shi + 32;                                          // [2][2048]
+  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);       // [1024]
+  int* widx = reinterpret_cast<int*>(bm + 1024);                 // [Q]
+  ws_select_body<M, Q, true>(P, b, S, wsidx, wsprev, eps, max_outer, X, shi, binfo, hist, bm, widx);
 }
 
 // ---- ws_solve: the inner SMO on B (one TH-thread workgroup per problem) ------------------------
@@ -703,6 +716,263 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   }
 }
 
+// ---- ws_kc_round: one whole round with the working set's kernel matrix cached in LDS -------------
+// The q = 1024 solver above pays ≈ 4.3k cycles per pair: four waves, two barriers and two dependent
+// LDS round trips per pair, and an F-term RBF row recomputed per pick (profiles/r3_headline.md).
+// On the bench's problems the pair count barely depends on q (10k points: 8.5k pairs at q = 1024,
+// 10.5k at q = 256; scripts/probes/ws_qsim.py), only the round count does (41 → 193).  So this
+// variant shrinks the working set to q = 256, whose kernel matrix fits the CU's LDS as an f32 upper
+// triangle (256·257/2 words = 128.5 KB), and makes the pair loop ONE wave:
+//   1. selection (ws_select_body, all 16 waves; no separate launch, B stays in LDS);
+//   2. z_B gathered into LDS ([2·KS][QP] f32, the MFMA operand layout), then K_BB on the f32-input
+//      MFMA (36 upper 32×32 tiles over 16 waves) with ws_gupdate's exact expression, so the inner
+//      solver and the gradient kernel see the same f32 kernel values bit for bit;
+//   3. wave 0 alone runs libsvm's WSS3 pairs: 4 slots per lane in registers, the i / j picks are DPP
+//      wave maxima (no barrier, no LDS round trip), a kernel row is 4 LDS reads, no exp;
+//   4. wave 0 publishes α of B and the changed coefficients (slot order) for ws_gupdate.
+// Same dual, same pair rule, same global f64 stopping rule as ws_solve_kernel.
+constexpr int kKcQ = 256;
+constexpr int kKcQP = kKcQ + 1;                       // zbuf row stride (conflict-free gather stores)
+constexpr int kKcTri = kKcQ * (kKcQ + 1) / 2;         // f32 words of the upper triangle
+constexpr size_t kc_zbuf_bytes(int KS) {
+  return (size_t)2 * KS * kKcQP * 4 > (4096 + 1024) * 4 ? (size_t)2 * KS * kKcQP * 4 : (4096 + 1024) * 4;
+}
+// LDS: shi [16] + binfo [16] | widx [Q] | snB [Q] | zbuf (aliases the selector's hist + bm) | tri
+constexpr size_t kc_lds_bytes(int KS) { return 128 + 2 * kKcQ * 4 + (kc_zbuf_bytes(KS) + 15) / 16 * 16 + (size_t)kKcTri * 4; }
+static_assert(kc_lds_bytes(12) <= 163840, "the K-cached round must fit the CU's 160 KiB of LDS");
+
+__device__ __forceinline__ int kc_rowstart(int r) { return r * kKcQ - ((r * (r - 1)) >> 1); }
+
+template <typename T>
+__device__ __forceinline__ T sel4(const T (&v)[4], int m) {   // v[m] for a wave-uniform m
+  return m == 0 ? v[0] : (m == 1 ? v[1] : (m == 2 ? v[2] : v[3]));
+}
+__device__ __forceinline__ float rdlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+
+template <int M, int KS>
+__global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
+    const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
+    const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
+    int* __restrict__ wsprev, float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc,
+    int Fp2, double eps, int max_outer, int max_inner, double inner_frac, WsAux X) {
+  constexpr int Q = kKcQ;
+  constexpr int SL = Q / 64;            // slots per lane of the solving wave (slot s = 64·m + lane)
+  constexpr unsigned kIdx = Q - 1;      // slot bits packed under the selection keys
+  static_assert(SL == 4, "sel4 assumes four slots per lane");
+  const int b = blockIdx.x;
+  WsState* S = states + b;
+  if (S->done) return;
+  const WsProb P = probs[b];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
+  int* shi = reinterpret_cast<int*>(ws_lds);
+  int* binfo = shi + 16;
+  int* widx = shi + 32;                                                  // [Q]
+  float* snB = reinterpret_cast<float*>(widx + Q);                       // [Q]
+  float* zbuf = snB + Q;                                                 // [2·KS][QP]
+  int* hist = reinterpret_cast<int*>(zbuf);                              // (selector only) [2][2048]
+  unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);               // (selector only) [1024]
+  float* tri = zbuf + (kc_zbuf_bytes(KS) + 15) / 16 * 4;                 // [Q(Q+1)/2]
+  const int nws = ws_select_body<M, Q, false>(P, b, S, nullptr, wsprev, eps, max_outer, X, shi, binfo, hist,
+                                              bm, widx);
+  if (nws < 0) return;
+  const long long c1 = __builtin_amdgcn_s_memtime();
+  // ---- z_B and γ'‖z‖² into LDS (zero rows past nws / features past F: exact no-ops in the dots)
+  for (int e = tid; e < 2 * KS * Q; e += kWsThreads) {
+    const int k = e / Q, s = e - k * Q;
+    zbuf[k * kKcQP + s] = (s < nws && k < F) ? zcat[(P.zoff + widx[s]) * F + k] : 0.f;
+  }
+  if (tid < Q) snB[tid] = tid < nws ? P.ngl2e * zn_all[P.aoff + widx[tid]] : 0.f;
+  __syncthreads();
+  // ---- K_BB upper triangle: tile (ta ≤ tb) of 32×32, ws_gupdate's MFMA chain and epilogue
+  {
+    const int r32 = lane & 31, hi = lane >> 5;
+    const float k2 = -2.f * P.ngl2e;
+    for (int t = wave; t < 36; t += kWsWaves) {
+      int ta = 0, rem = t;
+      while (rem >= 8 - ta) { rem -= 8 - ta; ++ta; }
+      const int tb = ta + rem;
+      f32x16 A = {0.f};
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        const float* zr = zbuf + (2 * q + hi) * kKcQP;
+        A = __builtin_amdgcn_mfma_f32_32x32x2f32(zr[ta * 32 + r32], zr[tb * 32 + r32], A, 0, 0, 0);
+      }
+      const int col = tb * 32 + r32;
+      const float snc = snB[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ta * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        const float kv = __builtin_amdgcn_exp2f(fminf(fmaf(k2, A[r], snB[row] + snc), 0.f));
+        if (row <= col) tri[kc_rowstart(row) + col - row] = kv;
+      }
+    }
+  }
+  __syncthreads();
+  const long long c2 = __builtin_amdgcn_s_memtime();
+  if (wave != 0) return;
+  // ---- the pair loop: wave 0 alone
+  const double* Gp = G_all + P.aoff;
+  double* ap = alpha_all + P.aoff;
+  bool valid[SL], pos[SL];
+  int tt[SL], rb[SL];
+  float y[SL], Cw[SL], a[SL], g[SL];
+  double a0[SL];
+#pragma unroll
+  for (int m = 0; m < SL; ++m) {
+    const int s = 64 * m + lane;
+    valid[m] = s < nws;
+    tt[m] = valid[m] ? widx[s] : 0;
+    pos[m] = tt[m] < P.npos;
+    y[m] = pos[m] ? 1.f : -1.f;
+    Cw[m] = (float)(pos[m] ? P.Cp : P.Cn);
+    a0[m] = valid[m] ? ap[tt[m]] : 0.0;
+    a[m] = (float)a0[m];
+    g[m] = valid[m] ? (float)Gp[tt[m]] : 0.f;
+    rb[m] = kc_rowstart(s) - s;   // K(r, s) for r > s lives at rowstart(s) + r − s
+  }
+  // K(r, ·) for this lane's slots (r wave-uniform): upper-triangle address of (min, max)
+  auto krow = [&](int r, float (&out)[SL]) {
+    const int ra = kc_rowstart(r) - r;
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const int s = 64 * m + lane;
+      out[m] = tri[s >= r ? ra + s : rb[m] + r];
+    }
+  };
+  const float Cpf = (float)P.Cp, Cnf = (float)P.Cn;
+  const float epsf = (float)eps;
+  float tol_in = -1.f;
+  int it = 0;
+  while (it < max_inner) {
+    // step 1: i = argmax_{I_up ∩ B} −y·G (slot in the key's low bits); I_low maximum for the gap
+    unsigned k1 = 0u, k3 = 0u;
+    bool low[SL];
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const unsigned s = (unsigned)(64 * m + lane);
+      const bool below = a[m] < Cw[m], above = a[m] > 0.f;
+      const bool up = valid[m] & ((pos[m] & below) | (!pos[m] & above));
+      low[m] = valid[m] & ((pos[m] & above) | (!pos[m] & below));
+      const float yg = y[m] * g[m];
+      const unsigned um = 0u - (unsigned)up, lm = 0u - (unsigned)low[m];
+      k1 = max(k1, ((f32_okey(-yg) & ~kIdx) | s) & um);
+      k3 = max(k3, f32_okey(yg) & lm);
+    }
+    const unsigned K1 = __builtin_amdgcn_readfirstlane(wave_max_u32(k1));
+    const unsigned K3 = __builtin_amdgcn_readfirstlane(wave_max_u32(k3));
+    if (K1 == 0u || K3 == 0u) break;
+    const int i = (int)(K1 & kIdx), mi = i >> 6, li = i & 63;
+    const float Gi = rdlane_f(sel4(g, mi), li);
+    const float ai_old = rdlane_f(sel4(a, mi), li);
+    const bool ipos = __builtin_amdgcn_readlane(sel4(tt, mi), li) < P.npos;
+    const float yi = ipos ? 1.f : -1.f;
+    const float GmaxB = -yi * Gi;
+    const float lgap = GmaxB + f32_from_okey(K3);
+    if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
+    if (lgap < tol_in) break;
+    // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / (2 − 2 K_it)
+    float Ki[SL];
+    krow(i, Ki);
+    unsigned k2 = 0u;
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const unsigned s = (unsigned)(64 * m + lane);
+      const float gd = GmaxB + y[m] * g[m];
+      const float q0 = 2.f - 2.f * Ki[m];
+      const float quad = q0 <= 0.f ? 1e-12f : q0;
+      const unsigned ok = 0u - (unsigned)(low[m] & (gd > 0.f));
+      k2 = max(k2, ((f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~kIdx) | s) & ok);
+    }
+    const unsigned K2 = __builtin_amdgcn_readfirstlane(wave_max_u32(k2));
+    if (K2 == 0u) break;
+    const int j = (int)(K2 & kIdx), mj = j >> 6, lj = j & 63;
+    float Kj[SL];
+    krow(j, Kj);   // issued before the scalar step below: its LDS latency hides under it
+    const float Gj = rdlane_f(sel4(g, mj), lj);
+    const float aj_old = rdlane_f(sel4(a, mj), lj);
+    const float Kij = rdlane_f(sel4(Ki, mj), lj);
+    const bool jpos = __builtin_amdgcn_readlane(sel4(tt, mj), lj) < P.npos;
+    const float yj = jpos ? 1.f : -1.f;
+    const float Ci = ipos ? Cpf : Cnf, Cj = jpos ? Cpf : Cnf;
+    // libsvm's two-variable step and clipping (ws_solve_kernel's branch-free form)
+    const float q0 = 2.f - 2.f * Kij;
+    const float rq = __builtin_amdgcn_rcpf(q0 <= 0.f ? 1e-12f : q0);
+    float ao, bo, as, bs;
+    {  // y_i ≠ y_j
+      const float delta = (-Gi - Gj) * rq;
+      const float diff = ai_old - aj_old;
+      ao = ai_old + delta;
+      bo = aj_old + delta;
+      const bool c1 = (diff > 0.f) & (bo < 0.f), c2 = !(diff > 0.f) & (ao < 0.f);
+      ao = c1 ? diff : (c2 ? 0.f : ao);
+      bo = c1 ? 0.f : (c2 ? -diff : bo);
+      const bool c3 = (diff > Ci - Cj) & (ao > Ci), c4 = !(diff > Ci - Cj) & (bo > Cj);
+      ao = c3 ? Ci : (c4 ? Cj + diff : ao);
+      bo = c3 ? Ci - diff : (c4 ? Cj : bo);
+    }
+    {  // y_i = y_j
+      const float delta = (Gi - Gj) * rq;
+      const float sum = ai_old + aj_old;
+      as = ai_old - delta;
+      bs = aj_old + delta;
+      const bool c1 = (sum > Ci) & (as > Ci), c2 = !(sum > Ci) & (bs < 0.f);
+      as = c1 ? Ci : (c2 ? sum : as);
+      bs = c1 ? sum - Ci : (c2 ? 0.f : bs);
+      const bool c3 = (sum > Cj) & (bs > Cj), c4 = !(sum > Cj) & (as < 0.f);
+      as = c3 ? sum - Cj : (c4 ? 0.f : as);
+      bs = c3 ? Cj : (c4 ? sum : bs);
+    }
+    const bool opp = ipos != jpos;
+    const float ai = opp ? ao : as, aj = opp ? bo : bs;
+    const float ci = yi * (ai - ai_old), cj = yj * (aj - aj_old);
+#pragma unroll
+    for (int m = 0; m < SL; ++m) {
+      const int s = 64 * m + lane;
+      a[m] = s == i ? ai : (s == j ? aj : a[m]);
+      g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
+    }
+    ++it;
+  }
+  // ---- publish: α of B, changed entries (slot order) for the global gradient update
+  int nc = 0;
+#pragma unroll
+  for (int m = 0; m < SL; ++m) {
+    const int s = 64 * m + lane;
+    double anew = a0[m];
+    if (valid[m] && a[m] != (float)a0[m]) {
+      const double C = pos[m] ? P.Cp : P.Cn;
+      anew = a[m] <= 0.f ? 0.0 : (a[m] >= Cw[m] ? C : a0[m] + ((double)a[m] - (double)(float)a0[m]));
+    }
+    const bool ch = valid[m] && anew != a0[m];
+    const unsigned long long cm = __ballot(ch);
+    const int cpos = nc + __popcll(cm & lanes_below());
+    if (ch) {
+      ap[tt[m]] = anew;
+      for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + cpos] = zbuf[k * kKcQP + s];
+      wsn[(size_t)b * Q + cpos] = snB[s];
+      wdc[(size_t)b * Q + cpos] = (float)((double)y[m] * (anew - a0[m]));
+    }
+    nc += __popcll(cm);
+  }
+  const int ncp = (nc + 31) & ~31;
+  for (int p = nc + lane; p < ncp; p += 64) {
+    for (int k = 0; k < Fp2; ++k) wsz[((size_t)b * Fp2 + k) * Q + p] = 0.f;
+    wsn[(size_t)b * Q + p] = 0.f;
+    wdc[(size_t)b * Q + p] = 0.f;
+  }
+  const long long c3 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    S->cyc_build += c2 - c1;
+    S->cyc_inner += c3 - c2;
+    if (it == 0 || nc == 0) S->done = 1;
+    S->nc = nc;
+    S->outer += 1;
+    S->inner += it;
+  }
+}
+
 // G_t += y_t · Σ_c dc_c · exp2(γ'‖x_t − x_c‖²) for every point t of every active problem, then t's
 // selection keys for the next working set.  The changed coefficients are staged through LDS in
 // chunks of kWsChunk; every wave takes part in every barrier (waves past the end compute nothing).
@@ -923,6 +1193,54 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
                        wn, wd, Fp2, Q, X);                                                          \
     break;
     switch (KS) { WS_UPD(4) WS_UPD(9) WS_UPD(12) WS_UPD(24) }
+#undef WS_UPD
+    launch_check();
+  }
+}
+
+// n_iter K-cached rounds (ws_kc_round + ws_gupdate) enqueued back to back; q = kKcQ, F ≤ 24.
+// wsz/wsn/wdc hold [P][2·KS][256] / [P][256] / [P][256]; wsprev [P][128].
+void ws_steps_kc(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
+                 uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
+                 uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
+                 double inner_frac, int n_iter, uintptr_t stream) {
+  const WsAux X = ws_aux(keys, n, gkey);
+  HFENS_REQUIRE(F >= 1 && F <= 24, "ws_steps_kc: 1 <= F <= 24");
+  HFENS_REQUIRE(max_l < 32 * kWsThreads, "ws_steps_kc: problems of 32768+ points need the multi-workgroup selector");
+  if (P == 0 || max_l == 0) return;
+  hipStream_t st = as_stream(stream);
+  const int KS = ws_ks(F);
+  const int Fp2 = 2 * KS;
+  const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
+  auto pp = (const WsProb*)probs;
+  auto sp = (WsState*)states;
+  auto zp = (const float*)zcat;
+  auto np_ = (const float*)zn;
+  auto ap = (double*)alpha;
+  auto gp = (double*)G;
+  auto wz = (float*)wsz;
+  auto wn = (float*)wsn;
+  auto wd = (float*)wdc;
+  auto wp = (int*)wsprev;
+  const dim3 grid((max_l + 255) / 256, P);
+  for (int it = 0; it < n_iter; ++it) {
+#define KC_ROUND(MM, KK)                                                                                     \
+  if (M == MM && KS == KK) {                                                                                 \
+    hipLaunchKernelGGL((ws_kc_round_kernel<MM, KK>), dim3(P), dim3(kWsThreads), kc_lds_bytes(KK), st, pp, sp, \
+                       zp, F, np_, ap, gp, wp, wz, wn, wd, Fp2, eps, max_outer, max_inner, inner_frac, X);   \
+  } else
+    KC_ROUND(4, 4) KC_ROUND(4, 9) KC_ROUND(4, 12) KC_ROUND(16, 4) KC_ROUND(16, 9) KC_ROUND(16, 12)
+    KC_ROUND(32, 4) KC_ROUND(32, 9) KC_ROUND(32, 12) {
+      HFENS_REQUIRE(false, "ws_steps_kc: no round instance for this F");
+    }
+#undef KC_ROUND
+    launch_check();
+#define WS_UPD(K)                                                                                    \
+  case K:                                                                                           \
+    hipLaunchKernelGGL(ws_gupdate_kernel<K>, grid, dim3(256), 0, st, pp, sp, zp, F, np_, ap, gp, wz, \
+                       wn, wd, Fp2, kKcQ, X);                                                       \
+    break;
+    switch (KS) { WS_UPD(4) WS_UPD(9) WS_UPD(12) }
 #undef WS_UPD
     launch_check();
   }

@@ -11,7 +11,8 @@
 //   2. drains its stores (system-scope release) and stores its epoch into flag[k][me][c] of every
 //      rank (one lane per destination),
 //   3. polls its own flag[k][r][c] for r = 0..W−1 (one lane per source, relaxed system-scope loads,
-//      s_sleep between polls, bounded by an s_memtime deadline that sets *err),
+//      s_sleep between polls, bounded by an s_memrealtime deadline — the fixed 100 MHz clock, not
+//      the DVFS-scaled shader clock — that sets *err),
 //   4. after a system-scope acquire sums recv[r][k][chunk] over r and writes the total back into
 //      the local slot.
 // int64 sums are exact, so the result is bit-identical to RCCL's all-reduce and to one process.
@@ -83,9 +84,9 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* _
   __syncthreads();
   if (tid < W) {
     const unsigned* f = flags_of(peers[me]) + ((size_t)k * W + tid) * nchunk + c;
-    const long long t0 = __builtin_amdgcn_s_memtime();
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
     while (xg_load_sys(f) != epoch) {
-      if (__builtin_amdgcn_s_memtime() - t0 > spin_ticks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > spin_ticks) {
         atomicOr(err, 1u);
         s_fail = 1;
         break;
@@ -111,8 +112,8 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* _
 
 // ---- host side ------------------------------------------------------------------------------
 // out[0] = device pointer of a zeroed allocation of `bytes` bytes (IPC-shareable): uncached
-// (every access bypasses the caches) or, uncached = 0, plain device memory (the kernel's
-// system-scope release/acquire fences then write back / invalidate the L2 around the hand-off)
+// (every access bypasses the caches: the only form the peer path uses across GPUs) or, uncached =
+// 0, plain device memory (tests only)
 void xgmi_alloc(long long bytes, int uncached, uintptr_t out) {
   void* p = nullptr;
   if (uncached) HFENS_CHECK(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached));
@@ -152,7 +153,7 @@ void xgmi_allreduce_i64(uintptr_t local, long long count, uintptr_t peers, int W
   if (count == 0) return;
   const int nchunk = (int)((cap + kXgChunk - 1) / kXgChunk);
   const int grid = (int)((count + kXgChunk - 1) / kXgChunk);
-  const long long ticks = (long long)(timeout_s * 2.5e9);   // s_memtime: shader clock (≤ 2.5 GHz)
+  const long long ticks = (long long)(timeout_s * 1.0e8);   // s_memrealtime: fixed 100 MHz
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(grid), dim3(kXgThreads), 0, as_stream(stream),
                      reinterpret_cast<long long*>(local), count, reinterpret_cast<long long* const*>(peers), W, me,
                      k, cap, nchunk, (unsigned)epoch_base, t_host, reinterpret_cast<const int*>(t_dev),

@@ -72,11 +72,17 @@ def group_of(rank: int, world: int, S: int, parent=None):
         return None
     if S == world:
         return parent if parent is not None else dist.group.WORLD
-    key = (world, S)
+    # members as GLOBAL ranks (new_group's numbering): position r of the parent is members[r]
+    members = dist.get_process_group_ranks(parent) if parent is not None else list(range(world))
+    if len(members) != world:
+        raise ValueError(f"group_of: world {world} but the parent group has {len(members)} ranks")
+    key = (world, S, tuple(members))
     if key not in _GROUPS:
         mine = None
         for g0 in range(0, world, S):
-            pg = dist.new_group(list(range(g0, g0 + S)))
+            # every rank of the DEFAULT group must call new_group for every subgroup, in order;
+            # a parent that is not the whole world would need its non-members to call it too
+            pg = dist.new_group(members[g0:g0 + S])
             if g0 <= rank < g0 + S:
                 mine = pg
         _GROUPS[key] = mine

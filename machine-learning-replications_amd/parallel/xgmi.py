@@ -13,6 +13,15 @@ The same code serves ranks on different GPUs (peer access over xGMI) and several
 one GPU (tests: IPC mappings of the same device).  Handles are exchanged with
 ``all_gather_object`` (gloo or nccl); ranks on different hosts cannot map each other, so
 :func:`peer_comm` returns None there and callers keep RCCL.
+
+Policy (``HFENS_XGMI``): ``auto`` (default) keeps RCCL — the peer kernel has only been validated
+with ranks sharing one GPU, where every rank reads through the same L2, and cross-GPU visibility of
+the remote stores and flags has not been checked bit for bit against RCCL on a multi-GPU node yet;
+``try`` attempts the peer path and drops to RCCL on every rank together when any rank cannot map a
+peer; ``1`` requires it; ``0`` never uses it.  Only uncached (fine-grained) buffers are mapped: if
+the driver cannot share one, the group keeps RCCL (no coarse-grained fallback, whose L2 lines an
+acquire would not invalidate).  A peer wait that times out sets an error flag that
+:meth:`PeerComm.check` all-reduces over the group, so every rank raises together.
 """
 from __future__ import annotations
 
@@ -25,9 +34,9 @@ import torch
 
 CHUNK = 2048          # int64 per block of xgmi_allreduce_kernel (ops/csrc/xgmi.hip kXgChunk)
 MAX_RANKS = 16
-MODE = os.environ.get("HFENS_XGMI", "auto")    # "auto" | "0" (RCCL only) | "1" (require)
-TIMEOUT_S = float(os.environ.get("HFENS_XGMI_TIMEOUT", "5"))
-UNCACHED = os.environ.get("HFENS_XGMI_UNCACHED", "1") != "0"
+MODE = os.environ.get("HFENS_XGMI", "auto")    # "auto" (= RCCL) | "try" | "0" (RCCL only) | "1" (require)
+TIMEOUT_S = float(os.environ.get("HFENS_XGMI_TIMEOUT", "60"))
+UNCACHED = os.environ.get("HFENS_XGMI_UNCACHED", "1") != "0"   # "0": plain device memory (one-GPU tests only)
 
 
 def buffer_bytes(W: int, cap: int) -> int:
@@ -57,23 +66,21 @@ class PeerComm:
             self.uncached = UNCACHED
             E.xgmi_alloc(buffer_bytes(self.W, self.cap), int(self.uncached), out.ctypes.data)
             self.own = int(out[0])
+            err = ""
             try:
                 E.xgmi_ipc_handle(self.own, h.ctypes.data)
-            except RuntimeError:
-                if not self.uncached:
-                    raise
-                # no IPC handle for uncached memory on this driver: plain device memory (the
-                # kernel's system-scope fences then order the hand-off through the caches)
-                E.xgmi_free(self.own)
-                self.uncached = False
-                E.xgmi_alloc(buffer_bytes(self.W, self.cap), 0, out.ctypes.data)
-                self.own = int(out[0])
-                E.xgmi_ipc_handle(self.own, h.ctypes.data)
+            except RuntimeError as e:
+                # no IPC handle for this (uncached) buffer: the whole group keeps RCCL — a plain
+                # coarse-grained buffer is not a safe substitute across GPUs
+                err = f"rank {self.me} cannot share its peer buffer: {e}"
             handles = [None] * self.W
-            dist.all_gather_object(handles, h.tobytes(), group=group)
+            dist.all_gather_object(handles, (h.tobytes(), err), group=group)
             ptrs, self.opened = [], []
-            err = ""
-            for r, hb in enumerate(handles):
+            if any(e for _, e in handles):
+                err = err or "a peer rank cannot share its buffer"
+            for r, (hb, _) in enumerate(handles):
+                if err:
+                    break
                 if r == self.me:
                     ptrs.append(self.own)
                     continue
@@ -117,7 +124,16 @@ class PeerComm:
         self.epoch += int(stages)
 
     def check(self):
-        if int(self.err.item()) != 0:
+        """Collective: every rank of the group learns whether ANY rank's peer wait timed out (a
+        late rank's own sums are fine, its peers' are not), and all raise together; the flag is
+        reset so a later fit starts clean."""
+        import torch.distributed as dist
+        e = self.err.to(torch.int64)
+        if dist.get_backend(self.group) == "gloo":
+            e = e.cpu()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)
+        self.err.zero_()
+        if int(e.item()) != 0:
             raise RuntimeError("xGMI peer all-reduce timed out waiting for a peer rank "
                                f"(HFENS_XGMI_TIMEOUT={TIMEOUT_S} s); set HFENS_XGMI=0 to use RCCL")
 
@@ -137,7 +153,7 @@ def peer_comm(group, device, cap: int) -> Optional[PeerComm]:
     """The group's peer buffers (created once, grown when ``cap`` grows) or None when the ranks
     cannot map each other (different hosts, > 16 ranks, HFENS_XGMI=0, no GPU)."""
     import torch.distributed as dist
-    if group is None or MODE == "0" or torch.device(device).type != "cuda":
+    if group is None or MODE in ("0", "auto") or torch.device(device).type != "cuda":
         return None
     gid = id(group)
     if gid not in _OK:

@@ -319,10 +319,10 @@ def test_gbdt_stage_xgmi_bit_identical(dev, world, subsample):
 
 
 def test_gbdt_stage_xgmi_mapping_failure_falls_back(dev):
-    """HFENS_XGMI=auto and ONE rank cannot map a peer's buffer: every rank drops the peer path
+    """HFENS_XGMI=try and ONE rank cannot map a peer's buffer: every rank drops the peer path
     together (the mapping errors are gathered before anyone uses the kernel) and the group keeps the
     collective path — one all-reduce per stage, the single-process fit bit for bit, no hang."""
-    path, per_stage, xg, units, got = _run_dp_stage(3, "auto", fail_open_rank=1)
+    path, per_stage, xg, units, got = _run_dp_stage(3, "try", fail_open_rank=1)
     assert path == "stage" and per_stage == 1.0 and xg == 0.0
     _check_dp_stage_equal(dev, got)
 
