@@ -35,6 +35,9 @@ def main(argv=None, script_dir=None) -> int:
     ap.add_argument("--no-plots", action="store_true", help="skip the ROC/PR figures")
     ap.add_argument("--timings", action="store_true")
     ap.add_argument("--json", default=None, help="append a JSON result line to this file")
+    ap.add_argument("--lr-optimum", action="store_true",
+                    help="solve 'lg' to its exact optimum on the device instead of reproducing liblinear's "
+                         "default-tolerance iterate and seed draw (the reference's T:31/T:46 behaviour)")
     a = ap.parse_args(argv)
     if a.no_plots:
         a.plots = None
@@ -69,7 +72,12 @@ def main(argv=None, script_dir=None) -> int:
     if group is not None:
         X_dev, y_dev = pdist.shard_rows(X_dev, rank, world), pdist.shard_rows(y_dev, rank, world)
         X_sel, y_sel = pdist.shard_rows(X_sel, rank, world), pdist.shard_rows(y_sel, rank, world)
-    res = develop(X_dev, y_dev, X_sel, y_sel, names, device=device, group=group)
+    from ..config import EnsembleConfig
+    cfg = EnsembleConfig(liblinear_exact=not a.lr_optimum)
+    # T:31: numpy's GLOBAL generator seeded with init_rs — liblinear's seeds ('lg', random_state=None)
+    # are drawn from it, six times, in the stacking fit's order
+    np.random.seed(cfg.seed)
+    res = develop(X_dev, y_dev, X_sel, y_sel, names, device=device, group=group, cfg=cfg)
     if a.plots:
         # collectives on EVERY rank (before the rank-0 block); only rank 0 draws
         p_all = res.proba_sel

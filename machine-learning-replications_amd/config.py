@@ -22,6 +22,10 @@ class EnsembleConfig:
     lr_C: float = 1.0
     meta_C: float = 1.0
     stack_folds: int = 5             # StackingClassifier cv=None → StratifiedKFold(5)
+    # 'lg' as the reference gets it: liblinear's default-tolerance iterate, its coordinate order
+    # seeded from numpy's global RNG (T:31, T:46; host emulation, models/logreg_solver.py).  False:
+    # the device solver's exact optimum (the benchmark's default; the two differ by liblinear's tol)
+    liblinear_exact: bool = False
 
     def to_dict(self):
         return asdict(self)
@@ -42,6 +46,7 @@ def build_estimators(cfg: Optional[EnsembleConfig] = None):
                                            learning_rate=cfg.gbc_learning_rate, random_state=cfg.seed)),
         ("lg", LogisticRegression(C=cfg.lr_C, class_weight="balanced", penalty="l1", solver="liblinear")),
     ]
+    estimators[2][1].emulate_liblinear = bool(cfg.liblinear_exact)
     return StackingClassifier(estimators=estimators,
                               final_estimator=LogisticRegression(C=cfg.meta_C, class_weight="balanced"))
 

@@ -41,6 +41,15 @@ class LogisticRegression(Estimator):
         self.warm_start = warm_start
         self.n_jobs = n_jobs
         self.l1_ratio = l1_ratio
+        # (framework option, not a scikit-learn parameter: never pickled) penalty='l1' +
+        # solver='liblinear': reproduce liblinear's default-tolerance iterate and its seed draw
+        # (logreg_solver._fit_liblinear_exact) instead of solving to the optimum on the device
+        self.emulate_liblinear = False
+
+    def clone(self):
+        c = super().clone()
+        c.emulate_liblinear = self.emulate_liblinear
+        return c
 
     def sample_weights(self, y: torch.Tensor) -> torch.Tensor:
         if self.class_weight == "balanced":

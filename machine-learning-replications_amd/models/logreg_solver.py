@@ -155,8 +155,64 @@ def _allreduce(ts, group):
     return pdist.all_reduce_sum_f64(ts, group)
 
 
+def _check_random_state(rs):
+    """scikit-learn's check_random_state: None → numpy's global RandomState (the one
+    ``train_ensemble_public.py:31`` seeds), an int → a fresh RandomState, an instance → itself."""
+    if rs is None:
+        return np.random.mtrand._rand
+    if isinstance(rs, (int, np.integer)):
+        return np.random.RandomState(int(rs))
+    return rs
+
+
+def _fit_liblinear_exact(models, X: torch.Tensor, yv: torch.Tensor, masks: torch.Tensor, max_iter: int,
+                         seed_order=None):
+    """liblinear's own default-tolerance iterate (ops/csrc/liblinear_host.hip), one host solve per
+    model.  The seeds are drawn exactly as scikit-learn's ``_fit_liblinear`` draws them —
+    ``check_random_state(random_state).randint(INT_MAX)`` — in model order, so a stacking fit
+    that lists the refit first and then the CV folds consumes numpy's global stream in the
+    reference's order (StackingClassifier refits every estimator, then cross_val_predict fold by
+    fold: the six 'lg' fits are the only draws after ``seed(2020)``).
+    ``seed_order``: the model indices in draw order (default: list order)."""
+    from concurrent.futures import ThreadPoolExecutor
+    m0 = models[0]
+    E = ops.ext()
+    Xh = np.ascontiguousarray(X.detach().to("cpu", torch.float64).numpy())
+    yh = np.ascontiguousarray(yv.detach().to("cpu", torch.float64).numpy())
+    mh = masks.detach().cpu().numpy().astype(bool)
+    seeds = [0] * len(models)
+    for b in (seed_order if seed_order is not None else range(len(models))):
+        seeds[b] = int(_check_random_state(models[b].random_state).randint(np.iinfo("i").max))
+    F = Xh.shape[1]
+    bias = float(m0.intercept_scaling) if m0.fit_intercept else -1.0
+
+    def solve(b):
+        rows = np.flatnonzero(mh[b])
+        Xb = np.ascontiguousarray(Xh[rows])
+        yb = np.ascontiguousarray(yh[rows])
+        n1 = float((yb > 0.5).sum())
+        n0 = float(yb.shape[0]) - n1
+        cw = (yb.shape[0] / (2.0 * np.array([n0, n1]))) if m0.class_weight == "balanced" else np.ones(2)
+        sw = np.ones(yb.shape[0])
+        w = np.zeros(F + (1 if bias > 0 else 0))
+        it = E.liblinear_l1r_lr(Xb.ctypes.data, yb.ctypes.data, sw.ctypes.data, int(yb.shape[0]), F, bias,
+                                float(m0.C) * cw[0], float(m0.C) * cw[1], float(m0.tol), int(max_iter), seeds[b],
+                                w.ctypes.data)
+        return w, it
+
+    with ThreadPoolExecutor(min(8, len(models))) as ex:
+        outs = list(ex.map(solve, range(len(models))))
+    dev = X.device
+    for m, (w, it) in zip(models, outs):
+        icpt = w[F] * bias if bias > 0 else 0.0
+        m.set_fitted(torch.as_tensor(w[:F]), torch.tensor([icpt], dtype=torch.float64),
+                     torch.tensor([it], dtype=torch.int32), F, device=dev)
+    LAST_PATH["path"] = "liblinear-host"
+    return models
+
+
 def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
-                     group=None, max_outer: int = 100):
+                     group=None, max_outer: int = 100, seed_order=None):
     m0 = models[0]
     _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
     if m0.penalty not in ("l1", "l2"):
@@ -171,6 +227,9 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
     if masks is None:
         masks = torch.ones(B, n, dtype=torch.bool, device=dev)
     yv = y.to(device=dev, dtype=torch.float64)
+    if (m0.penalty == "l1" and m0.solver == "liblinear" and group is None
+            and all(getattr(m, "emulate_liblinear", False) for m in models)):
+        return _fit_liblinear_exact(models, X, yv, masks, int(m0.max_iter), seed_order)
     ypm = 2.0 * yv - 1.0
     if m0.fit_intercept:
         Xa = torch.cat([X, torch.full((n, 1), float(m0.intercept_scaling), dtype=torch.float64, device=dev)], 1)

@@ -156,7 +156,10 @@ def fit_base_batch(est, X, y, masks, group=None, timer=None, svc_group=None, row
         fit_gbdt_batch(clones, X, y, masks, group=group)
     else:
         clones = [est.clone() for _ in range(masks.shape[0])]
-        fit_logreg_batch(clones, X, y, masks, group=group)
+        # masks are [fold 0 … fold K−1, refit]; scikit-learn fits the refit first (its seed draw
+        # from the global RNG comes first, the liblinear emulation's draw order)
+        nb = masks.shape[0]
+        fit_logreg_batch(clones, X, y, masks, group=group, seed_order=[nb - 1] + list(range(nb - 1)))
     return clones
 
 

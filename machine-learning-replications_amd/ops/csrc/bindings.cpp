@@ -13,6 +13,9 @@ void forest_raw(uintptr_t X, int n, int F, uintptr_t nodes, uintptr_t values, in
                 double init, double lr, uintptr_t out, uintptr_t stream);
 // stack.hip
 long long stack_infer_lds(int F, int mp, int nodes_total);
+// liblinear_host.hip
+int liblinear_l1r_lr(uintptr_t X, uintptr_t y, uintptr_t sw, int l, int n, double bias, double C0, double C1,
+                     double eps, int max_newton_iter, long long seed, uintptr_t w);
 #define HFENS_DECLS
 #include "decls.inc"
 #undef HFENS_DECLS
@@ -26,6 +29,8 @@ PYBIND11_MODULE(_hfens_hip, m) {
   m.def("svc_proba1", &hfens::svc_proba1);
   m.def("forest_raw", &hfens::forest_raw);
   m.def("stack_infer_lds", &hfens::stack_infer_lds);
+  // (host-only and sequential: release the GIL so the stacking fit's six solves run in parallel threads)
+  m.def("liblinear_l1r_lr", &hfens::liblinear_l1r_lr, py::call_guard<py::gil_scoped_release>());
 #define HFENS_DEFS
 #include "decls.inc"
 #undef HFENS_DEFS

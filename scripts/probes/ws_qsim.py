@@ -7,6 +7,7 @@ solver (q/4 most violating I_up + q/4 I_low points, previous round's new picks k
 pairs inside B until the local gap < frac · the round's starting local gap, f64 global gap
 < 1e-3 to stop).  Usage: python scripts/probes/ws_qsim.py [rows] [q ...]
 """
+import os
 import sys
 import time
 
@@ -34,9 +35,20 @@ def build_problem(rows=10000, seed=2020):
     Z = Z[order]
     yv = np.where(np.arange(len(y)) < n0, 1.0, -1.0)
     C = np.where(yv > 0, cw[0], cw[1])
-    sq = (Z * Z).sum(1)
-    K = np.exp(-gamma * np.maximum(sq[:, None] + sq[None, :] - 2.0 * Z @ Z.T, 0.0)).astype(np.float32)
-    return K, yv, C
+    return KernelCols(Z.astype(np.float32), gamma), yv, C
+
+
+class KernelCols:
+    """K[:, cols] / K[np.ix_(B, B)] of the RBF kernel computed on demand (no l² matrix)."""
+
+    def __init__(self, Z, gamma):
+        self.Z, self.gamma = Z, gamma
+        self.sq = (Z.astype(np.float64) ** 2).sum(1)
+
+    def block(self, rows, cols):
+        Zr, Zc = self.Z[rows].astype(np.float64), self.Z[cols].astype(np.float64)
+        d = self.sq[rows][:, None] + self.sq[cols][None, :] - 2.0 * Zr @ Zc.T
+        return np.exp(-self.gamma * np.maximum(d, 0.0)).astype(np.float32)
 
 
 def smo_sub(KB, GB, aB, CB, yB, tol, max_inner):
@@ -125,7 +137,7 @@ def ws(K, yv, C, q, frac, eps=1e-3, max_inner=None, reuse=True):
         keep = prev[~np.isin(prev, new)] if reuse else np.array([], dtype=int)
         B = np.concatenate([new, keep])[:q]
         prev = new
-        KB = K[np.ix_(B, B)].astype(np.float64)
+        KB = K.block(B, B).astype(np.float64)
         aB = a[B].copy()
         GB = G[B].copy()
         yB = yv[B]
@@ -138,15 +150,16 @@ def ws(K, yv, C, q, frac, eps=1e-3, max_inner=None, reuse=True):
         da = aB - a[B]
         ch = np.flatnonzero(da != 0)
         nchanged.append(len(ch))
-        G += yv * (K[:, B[ch]].astype(np.float64) @ (yB[ch] * da[ch]))
+        G += yv * (K.block(np.arange(l), B[ch]).astype(np.float64) @ (yB[ch] * da[ch]))
         a[B] = aB
         outer += 1
         if n_in == 0:
             break
     nsv = int((a > 0).sum())
+    sv = np.flatnonzero(a > 0)
+    obj = 0.5 * (a[sv] * yv[sv]) @ (K.block(sv, sv).astype(np.float64) @ (a[sv] * yv[sv])) - a.sum() if len(sv) <= 20000 else float("nan")
     return dict(q=q, frac=frac, rounds=outer, pairs=inner, gap=float(gap), nsv=nsv,
-                changed_mean=float(np.mean(nchanged)) if nchanged else 0.0,
-                obj=float(0.5 * (a * yv) @ (K.astype(np.float64) @ (a * yv)) - a.sum()))
+                changed_mean=float(np.mean(nchanged)) if nchanged else 0.0, obj=float(obj))
 
 
 if __name__ == "__main__":
@@ -155,8 +168,9 @@ if __name__ == "__main__":
     t = time.time()
     K, yv, C = build_problem(rows)
     print(f"problem: l={len(yv)} npos={(yv > 0).sum()} C={C[0]:.4f}/{C[-1]:.4f} ({time.time() - t:.1f}s)", flush=True)
+    fracs = [float(v) for v in os.environ.get("FRACS", "0.1,0.2,0.4").split(",")]
     for q in qs:
-        for frac in (0.1, 0.2, 0.4):
+        for frac in fracs:
             t = time.time()
             r = ws(K, yv, C, q, frac)
             print(r, f"{time.time() - t:.1f}s", flush=True)

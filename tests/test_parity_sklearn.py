@@ -176,3 +176,53 @@ def test_gbc_duplicate_column_ties_match_sklearn_partitions(seed):
     assert np.abs(ours.train_score_.numpy() - ref.train_score_).max() < 1e-7
     p = ours.predict_proba(torch.as_tensor(Xd)).numpy()[:, 1]
     assert np.abs(p - ref.predict_proba(Xd)[:, 1]).max() < 1e-7
+
+
+def test_l1_logreg_liblinear_emulation_is_bit_exact():
+    """E15: with the global RNG seeded as the reference seeds it
+    (train_ensemble_public.py:31), the host liblinear emulation reproduces scikit-learn's
+    DEFAULT-tolerance iterate — same seed draw, same coordinate permutations, same early stop."""
+    from sklearn.linear_model import LogisticRegression as SkLR
+    from hfens.models.linear import LogisticRegression
+    X, y = _cohort(700, 17, 22)
+    for gs in (2020, 7):
+        np.random.seed(gs)
+        ref = SkLR(penalty="l1", solver="liblinear", class_weight="balanced").fit(X, y)
+        np.random.seed(gs)
+        m = LogisticRegression(penalty="l1", solver="liblinear", class_weight="balanced")
+        m.emulate_liblinear = True
+        m.fit(torch.as_tensor(X), torch.as_tensor(y))
+        assert np.abs(m.coef_.numpy() - ref.coef_).max() <= 1e-8
+        assert abs(float(m.intercept_[0]) - float(ref.intercept_[0])) <= 1e-8
+        assert int(m.n_iter_[0]) == int(ref.n_iter_[0])
+
+
+def test_stacking_lg_draws_follow_sklearn_order():
+    """The stacking fit draws the six 'lg' seeds from the global RNG in scikit-learn's order
+    (refit first, then the 5 CV folds): the refit's coefficients equal sklearn's stack's to 1e-8,
+    and the meta-learner (fit on the OOF probabilities, lg's among them) agrees closely."""
+    from sklearn.ensemble import GradientBoostingClassifier as SkGBC, StackingClassifier as SkStack
+    from sklearn.linear_model import LogisticRegression as SkLR
+    from sklearn.pipeline import make_pipeline as sk_pipe
+    from sklearn.preprocessing import StandardScaler as SkScaler
+    from sklearn.svm import SVC as SkSVC
+    from hfens.config import EnsembleConfig, build_estimators
+    X, y = _cohort(500, 12, 41)
+    np.random.seed(2020)
+    sk = SkStack(estimators=[("svc", sk_pipe(SkScaler(), SkSVC(class_weight="balanced", probability=True,
+                                                               random_state=2020))),
+                             ("gbc", SkGBC(n_estimators=100, max_depth=1, random_state=2020)),
+                             ("lg", SkLR(penalty="l1", solver="liblinear", class_weight="balanced"))],
+                 final_estimator=SkLR(class_weight="balanced")).fit(X, y)
+    np.random.seed(2020)
+    ours = build_estimators(EnsembleConfig(liblinear_exact=True)).fit(torch.as_tensor(X), torch.as_tensor(y))
+    lg = ours.estimators_[2]
+    assert np.abs(lg.coef_.numpy() - sk.estimators_[2].coef_).max() <= 1e-8
+    assert abs(float(lg.intercept_[0]) - float(sk.estimators_[2].intercept_[0])) <= 1e-8
+    # the five fold fits: the same draws continued (refit, then cross_val_predict fold by fold)
+    from sklearn.model_selection import StratifiedKFold, cross_val_predict
+    np.random.seed(2020)
+    SkLR(penalty="l1", solver="liblinear", class_weight="balanced").fit(X, y)
+    oof = cross_val_predict(SkLR(penalty="l1", solver="liblinear", class_weight="balanced"), X, y,
+                            cv=StratifiedKFold(5), method="predict_proba")[:, 1]
+    assert np.abs(ours.oof_meta_[:, 2].numpy() - oof).max() <= 1e-8
