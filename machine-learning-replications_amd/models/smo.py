@@ -631,6 +631,11 @@ WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
+WS_KC_DIRECT_MAX = 16 * 1024      # svm_ws.hip kWsDirectMax: larger problems select from candidate lists
+WS_GRAPH = os.environ.get("HFENS_SVM_WS_GRAPH", "1") != "0"
+WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # rounds per captured graph
+_WS_GRAPHS: dict = {}
+WS_BIG_CHUNK = int(os.environ.get("HFENS_SVM_WS_BIG_CHUNK", "64"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
@@ -666,17 +671,41 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     n = aoffs[-1]
     Q = ws_q(F)
     Fp2 = 2 * _ws_ks(F)
-    # per-point arrays (indexed by each problem's absolute offset) are shared by the groups
-    zn = torch.empty(n, dtype=torch.float32, device=device)
-    alpha = torch.empty(n, dtype=torch.float64, device=device)
-    G = torch.empty(n, dtype=torch.float64, device=device)
-    keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
-    hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
-    max_outer = 5_000 if max_iter_cap is None else int(max_iter_cap)
+    max_outer = (max(5_000, max(p.l for p in live) // 4) if max_iter_cap is None else int(max_iter_cap))
     max_inner = WS_MAX_INNER
-    groups = _ws_groups(live, device) if not _WS_SYNC[0] else [list(range(P))]
+    # large problems (candidate-list selection, hundreds to thousands of rounds): host-checked rounds
+    # in chunks of WS_BIG_CHUNK from the start, one group (the rounds-ahead guess would be far off)
+    big = ws_kc(F) and max(p.l for p in live) > WS_KC_DIRECT_MAX
+    sync = _WS_SYNC[0] or big
+    if big and steps_per_check is None:
+        steps_per_check = WS_BIG_CHUNK
+    groups = _ws_groups(live, device) if not sync else [list(range(P))]
     cuda = torch.device(device).type == "cuda"
     caller = torch.cuda.current_stream(device) if cuda else None
+    # HIP graphs of the rounds (K-cached, rounds enqueued ahead): ~290 rounds × 2 launches × 3 groups
+    # per fit cost as much host time as the device spends on them, so each group's rounds are
+    # captured once (WS_GRAPH_CHUNK rounds per graph) and replayed.  Every argument of a captured
+    # launch must be the same buffer at every replay: the per-point arrays, the features and every
+    # per-group buffer are process-lifetime workspaces (runtime.workspace), re-filled per fit.
+    use_graph = (WS_GRAPH and cuda and ws_kc(F) and not sync
+                 and caller.cuda_stream != torch.cuda.default_stream(device).cuda_stream)
+    # per-point arrays (indexed by each problem's absolute offset) are shared by the groups
+    if use_graph:
+        from .. import runtime
+        zc = runtime.workspace(device, "ws_zcat", zcat.numel(), torch.float32)
+        zc.copy_(zcat.reshape(-1))
+        zcat = zc
+        zn = runtime.workspace(device, "ws_zn", n, torch.float32)
+        alpha = runtime.workspace(device, "ws_alpha", n, torch.float64)
+        G = runtime.workspace(device, "ws_G", n, torch.float64)
+        keys = runtime.workspace(device, "ws_keys", 2 * n, torch.int32)
+        hist = runtime.workspace(device, "ws_hist", 1, torch.int32)
+    else:
+        zn = torch.empty(n, dtype=torch.float32, device=device)
+        alpha = torch.empty(n, dtype=torch.float64, device=device)
+        G = torch.empty(n, dtype=torch.float64, device=device)
+        keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
+        hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
     runs = []
     for gi, idx in enumerate(groups):
         # the last (smallest) group on the caller's stream, the others on process-lifetime side streams
@@ -689,8 +718,9 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             side.wait_stream(caller)
             st = side.cuda_stream
         runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
-                              side, zn, alpha, G, keys, hist, n, Q, Fp2))
-    if _WS_SYNC[0]:
+                              side, zn, alpha, G, keys, hist, n, Q, Fp2, gi=gi if use_graph else None,
+                              cap_stream=(side if side is not None else caller) if use_graph else None))
+    if sync:
         runs[0]["sync_rounds"](steps_per_check)
     else:
         # no host synchronisation: WS_ROUNDS_AHEAD rounds are enqueued at once (finished problems
@@ -699,8 +729,9 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
         # group's stream starts within one chunk of host launch time.
         left = min(WS_KC_ROUNDS_AHEAD if ws_kc(F) else WS_ROUNDS_AHEAD, max_outer)
+        chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
         while left > 0:
-            k = min(_WS_ENQ_CHUNK, left)
+            k = min(chunk, left)
             for r in runs:
                 r["steps"](k)
             left -= k
@@ -711,6 +742,10 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             caller.wait_stream(r["side"])
             for t in (alpha, G, zn, keys, r["rho"], r["iters"], r["idx_dev"]):
                 t.record_stream(r["side"])
+    if use_graph:
+        # the solution leaves the workspace: the next fit's rounds may overwrite it while this
+        # fit's models are still being extracted on another stream
+        alpha = alpha.clone()
     if len(runs) == 1:
         rho, iters, err = runs[0]["rho"], runs[0]["iters"], runs[0]["err"]
     else:
@@ -719,7 +754,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         for r in runs:
             rho.index_copy_(0, r["idx_dev"], r["rho"])
             iters.index_copy_(0, r["idx_dev"], r["iters"])
-        err = None if _WS_SYNC[0] else torch.stack([r["err"] for r in runs]).amax().reshape(1)
+        err = None if sync else torch.stack([r["err"] for r in runs]).amax().reshape(1)
 
     def stats():   # read back only when someone looks (tests, bench diagnostics): no sync here
         order = np.concatenate([r["idx"] for r in runs])
@@ -740,7 +775,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
 
 
 def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, s, side,
-              zn, alpha, G, keys, hist, n, Q, Fp2):
+              zn, alpha, G, keys, hist, n, Q, Fp2, gi=None, cap_stream=None):
     """State of the problems ``live[idx]``, whose rounds go on stream ``s`` (per-problem state is
     group-local; the per-point arrays are the shared ones, addressed by each problem's absolute
     offset).  Returns closures: ``steps(k)`` enqueues k rounds, ``sync_rounds(chunk)`` runs
@@ -753,16 +788,37 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
     max_l = int(arr["l"].max())
     ctx = (lambda: torch.cuda.stream(side)) if side is not None else contextlib.nullcontext
     out = dict(side=side, idx=np.asarray(idx, dtype=np.int64), err=None)
+    graph = gi is not None
     with ctx():
-        pdev = _dev_struct(arr, device)
-        states = torch.zeros(P * _WS_STATE_BYTES // 4, dtype=torch.int32, device=device)
-        wsz = torch.zeros(P * Fp2 * Q, dtype=torch.float32, device=device)
-        wsn = torch.zeros(P * Q, dtype=torch.float32, device=device)
-        wdc = torch.zeros(P * Q, dtype=torch.float32, device=device)
-        wsprev = torch.zeros(P * (Q // 2), dtype=torch.int32, device=device)
-        wsidx = torch.zeros(P * Q, dtype=torch.int32, device=device)
+        if graph:
+            from .. import runtime
+
+            def buf(name, numel, dtype):
+                t = runtime.workspace(device, f"ws_g{gi}_{name}", numel, dtype)
+                t.zero_()
+                return t
+            host = torch.from_numpy(arr.view(np.uint8).copy()).pin_memory()
+            pdev = runtime.workspace(device, f"ws_g{gi}_pdev", host.numel(), torch.uint8)
+            pdev.copy_(host, non_blocking=True)
+        else:
+            def buf(name, numel, dtype):
+                return torch.zeros(numel, dtype=dtype, device=device)
+            pdev = _dev_struct(arr, device)
+            host = None
+        states = buf("states", P * _WS_STATE_BYTES // 4, torch.int32)
+        wsz = buf("wsz", P * Fp2 * Q, torch.float32)
+        wsn = buf("wsn", P * Q, torch.float32)
+        wdc = buf("wdc", P * Q, torch.float32)
+        wsprev = buf("wsprev", P * (Q // 2), torch.int32)
+        wsidx = buf("wsidx", P * Q, torch.int32)
         wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
-        gkey = torch.zeros(2 * P, dtype=torch.int64, device=device)
+        gkey = buf("gkey", 2 * P, torch.int64)
+        cand = None
+        if ws_kc(F):
+            nc_out = np.zeros(1, dtype=np.int64)
+            E.ws_kc_cand_len(max_l, nc_out.ctypes.data)
+            if int(nc_out[0]) > 0:   # large problems: per-block candidate lists (svm_ws.hip ws_cand_kernel)
+                cand = buf("cand", 3 * P * int(nc_out[0]), torch.int32)
         rho = torch.empty(P, dtype=torch.float64, device=device)
         iters = torch.empty(P, dtype=torch.int32, device=device)
         inner = torch.empty(P, dtype=torch.int64, device=device)
@@ -775,10 +831,34 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
     kc = ws_kc(F)
 
     def steps(k):
+        if graph:
+            # one captured graph per (group, shape, buffers, round count); replayed on the group's stream
+            key = (gi, P, max_l, F, n, k, eps, max_outer, max_inner, WS_INNER_FRAC,
+                   tuple(int(t.data_ptr()) for t in (pdev, zcat, zn, alpha, G, states, wsz, wsn, wdc, wsprev,
+                                                        keys, gkey)), int(cand.data_ptr()) if cand is not None else 0)
+            g = _WS_GRAPHS.get(key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(cap_stream):
+                    g.capture_begin(capture_error_mode="thread_local")
+                    try:
+                        launch(k)
+                    finally:
+                        g.capture_end()
+                _WS_GRAPHS[key] = g
+                while len(_WS_GRAPHS) > 24:
+                    _WS_GRAPHS.pop(next(iter(_WS_GRAPHS)))
+            with torch.cuda.stream(cap_stream):
+                g.replay()
+            return
+        launch(k)
+
+    def launch(k):
         if kc:
             E.ws_steps_kc(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(),
                           G.data_ptr(), states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(),
-                          wsprev.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner,
+                          wsprev.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(),
+                          cand.data_ptr() if cand is not None else 0, eps, max_outer, max_inner,
                           WS_INNER_FRAC, k, s)
             return
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
@@ -810,7 +890,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
                     cyc_p0=cyc[:, 3], cyc_p1=cyc[:, 4], cyc_p2=cyc[:, 5],
                     phases=wprof.view(P, 6).cpu().numpy() if wprof is not None else None)
     out.update(rho=rho, iters=iters, steps=steps, sync_rounds=sync_rounds, finish=finish, stats=stats,
-               keep=(pdev, states, wsz, wsn, wdc, wsprev, wsidx, gkey, wprof, inner, gap))
+               keep=(pdev, states, wsz, wsn, wdc, wsprev, wsidx, gkey, wprof, inner, gap, cand, host))
     return out
 
 

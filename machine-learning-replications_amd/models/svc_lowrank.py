@@ -93,6 +93,12 @@ def _part_len(fn: str, *args) -> int:
 # against 8.1 + 1.4 ms for the split-K library bmm plus the scaled copy (profiles/r2_ipm_native.md),
 # so the library path stays the default until the kernel is tuned.
 NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
+# The weighted Gram on the f32-input MFMA (lowrank.hip wsyrk_f32: Φ exact in f32, d ⊙ Φ rounded to
+# f32, f32 accumulation over ≤ 256 rows, f64 beyond): the interior point's Newton systems then use
+# an S accurate to ~1e-7 relative while every residual, step and stopping test stays f64 (an
+# inexact-Newton interior point; the directions' accuracy only affects the iteration count).
+# "f64": the library block-upper f64 path.
+GRAM = os.environ.get("HFENS_IPM_GRAM", "f32")
 SYRK_BLOCK = int(os.environ.get("HFENS_SYRK_BLOCK", "128"))   # library path: block-upper product (0: full)
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
@@ -123,6 +129,14 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor, P32: torch.Tensor = None)
     l, r = Phi.shape
     if l == 0:
         return torch.zeros(r, r, dtype=Phi.dtype, device=Phi.device)
+    if GRAM == "f32" and P32 is not None and _native(Phi) and r <= 2048 and r % 4 == 0 and P32.data_ptr() % 16 == 0:
+        from .. import runtime
+        plen = _part_len("wsyrk_part_len", l, r)
+        part = runtime.workspace(Phi.device, _ws_name("wsyrk_part"), plen, torch.float64)
+        S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
+        ops.ext().wsyrk_f32(P32.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
+                            ops.stream_ptr(Phi.device))
+        return S
     if NATIVE_SYRK and _native(Phi) and r <= 2048:
         from .. import runtime
         plen = _part_len("wsyrk_part_len", l, r)

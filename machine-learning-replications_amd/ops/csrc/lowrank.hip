@@ -144,6 +144,136 @@ __global__ __launch_bounds__(256) void wsyrk_reduce_kernel(const double* __restr
   }
 }
 
+// ---- wsyrk_f32: the same product on the f32-input MFMA -------------------------
+// Φ is exactly f32 (svc_lowrank rounds the Nyström map once), so the left operand A = Φ is exact;
+// the right operand B = d ⊙ Φ is formed in f64 while staging and rounded to f32 (2⁻²⁴ relative per
+// element).  v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation, 2× the f64 MFMA rate)
+// accumulates kWfFlush rows at a time; those partial sums are then added into f64 registers, so the
+// f32 rounding never spans more than 256 rows and the split-K partials and their reduction are f64
+// (the same deterministic wsyrk_reduce as the f64 kernel).  Tile 128×128 per workgroup (4 waves,
+// 2×2 of 64×64, each 2×2 MFMA blocks); a wave whose 64-column (or 64-row) half lies entirely past r
+// skips its MFMAs, so the padding of r = 428 costs (448/428)², not (512/428)².
+constexpr int kWfKC = 32;                 // rows per LDS slab
+constexpr int kWfLd = kSyT + 4;           // padded LDS row (f32)
+constexpr int kWfFlush = 256;             // rows per f32 accumulation before the f64 fold
+
+__global__ __launch_bounds__(kSyThreads) void wsyrk_f32_kernel(const float* __restrict__ Phi, const double* __restrict__ d,
+                                                                long long n, int r, int nt, int T, int G,
+                                                                long long rows_per_group, double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[2][kWfKC][kWfLd];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWfKC][kWfLd];
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;   // (XCD-aware map: see wsyrk_f64_kernel)
+  const int gi = xcd + 8 * (q / T), tile = q % T;
+  if (gi >= G) return;
+  int t = tile, I = 0;
+  while (t >= nt - I) { t -= nt - I; ++I; }
+  const int J = I + t;
+  const int c0a = I * kSyT, c0b = J * kSyT;
+  const long long r0 = (long long)gi * rows_per_group, r1 = min(n, r0 + rows_per_group);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+  const bool active = c0a + wr < r && c0b + wc < r;   // wave-uniform
+  f32x16 acc[2][2];
+  double accd[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      acc[a][b] = f32x16{0.f};
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accd[a][b][e] = 0.0;
+    }
+  // staging: 32 rows × 128 columns per operand = 1024 float4, 4 per thread per operand; the next
+  // slab's loads are issued before this slab's MFMAs and stored to LDS after them
+  f32x4 va[4], vb[4];
+  double vd[4];
+  long long lrow0 = r0;
+  auto load = [&](long long row0) {
+    lrow0 = row0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * kSyThreads;
+      const int rr = e >> 5, c4 = (e & 31) * 4;
+      const long long row = min(row0 + rr, r1 - 1);
+      const float* pr = Phi + row * r;
+      va[u] = *reinterpret_cast<const f32x4*>(pr + min(c0a + c4, r - 4));
+      vb[u] = *reinterpret_cast<const f32x4*>(pr + min(c0b + c4, r - 4));
+      vd[u] = d[row];
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * kSyThreads;
+      const int rr = e >> 5, c4 = (e & 31) * 4;
+      const bool ok = lrow0 + rr < r1;
+      const bool oka = ok && c0a + c4 < r, okb = ok && c0b + c4 < r;
+      f32x4 a, b;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] = oka ? va[u][k] : 0.f;
+        b[k] = okb ? (float)(vd[u] * (double)vb[u][k]) : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(&As[buf][rr][c4]) = a;
+      *reinterpret_cast<f32x4*>(&Bs[buf][rr][c4]) = b;
+    }
+  };
+  int buf = 0;
+  if (r0 < r1) {
+    load(r0);
+    store(0);
+  }
+  __syncthreads();
+  int since = 0;
+  for (long long row0 = r0; row0 < r1; row0 += kWfKC) {
+    const bool more = row0 + kWfKC < r1;
+    if (more) load(row0 + kWfKC);
+    if (active) {
+#pragma unroll
+      for (int ks = 0; ks < kWfKC / 2; ++ks) {
+        const int kr = 2 * ks + (lane >> 5);
+        float a[2], b[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          a[p] = As[buf][kr][wr + 32 * p + (lane & 31)];
+          b[p] = Bs[buf][kr][wc + 32 * p + (lane & 31)];
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) acc[p][qq] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[p], b[qq], acc[p][qq], 0, 0, 0);
+      }
+      since += kWfKC;
+      if (since >= kWfFlush || !more) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accd[p][qq][e] += (double)acc[p][qq][e];
+            acc[p][qq] = f32x16{0.f};
+          }
+        since = 0;
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partial tile [128][128] of this (group, tile): the f32x16 C map, row = 8(e>>2) + 4(lane>>5) + (e&3)
+  double* out = part + ((size_t)gi * T + tile) * kSyT * kSyT;
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wr + 32 * p + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+        const int col = wc + 32 * qq + (lane & 31);
+        out[row * kSyT + col] = active ? accd[p][qq][e] : 0.0;
+      }
+}
+
 // row groups of the split-K (the partial buffer is sized from wsyrk_part_len below)
 static int wsyrk_groups(long long n, int T) {
   int dev = 0, ncu = 256;
@@ -231,6 +361,27 @@ void wsyrk_f64(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, l
   hipStream_t st = as_stream(stream);
   const long long blocks = 8LL * ((G + 7) / 8) * T;
   hipLaunchKernelGGL(wsyrk_f64_kernel, dim3((unsigned)blocks), dim3(kSyThreads), 0, st, (const double*)Phi,
+                     (const double*)d, n, r, nt, T, G, per, (double*)part);
+  launch_check();
+  hipLaunchKernelGGL(wsyrk_reduce_kernel, dim3(T, 16), dim3(256), 0, st, (const double*)part, G, T, nt, r,
+                     (double*)S);
+  launch_check();
+}
+
+// S = Φᵀ diag(d) Φ from the f32 copy of Φ (wsyrk_f32_kernel); the same partial layout, row
+// groups and reduction as wsyrk_f64 (part_len from wsyrk_part_len).
+void wsyrk_f32(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, long long part_len, uintptr_t S,
+               uintptr_t stream) {
+  HFENS_REQUIRE(n >= 1 && r >= 4 && r <= 2048 && r % 4 == 0, "wsyrk_f32: n >= 1, 4 <= r <= 2048, r % 4 == 0");
+  HFENS_REQUIRE((Phi & 15) == 0, "wsyrk_f32: Φ must be 16-byte aligned");
+  const int nt = (r + kSyT - 1) / kSyT, T = nt * (nt + 1) / 2;
+  const int G = wsyrk_groups(n, T);
+  HFENS_REQUIRE(part_len >= (long long)G * T * kSyT * kSyT, "wsyrk_f32: partial buffer too small");
+  long long per = (n + G - 1) / G;
+  per = (per + kWfKC - 1) / kWfKC * kWfKC;
+  hipStream_t st = as_stream(stream);
+  const long long blocks = 8LL * ((G + 7) / 8) * T;
+  hipLaunchKernelGGL(wsyrk_f32_kernel, dim3((unsigned)blocks), dim3(kSyThreads), 0, st, (const float*)Phi,
                      (const double*)d, n, r, nt, T, G, per, (double*)part);
   launch_check();
   hipLaunchKernelGGL(wsyrk_reduce_kernel, dim3(T, 16), dim3(256), 0, st, (const double*)part, G, T, nt, r,

@@ -227,51 +227,19 @@ constexpr size_t ws_sel_lds_bytes(int Q) { return 32 * 4 + 4096 * 4 + 1024 * 4 +
 
 // M = points per lane.  Wave w owns the contiguous chunk [w·64M, (w+1)·64M) and lane L its points
 // w·64M + m·64 + L: loads are coalesced and index order = (wave, m, lane), so ballots give
-// index-ordered ranks.  Writes B (point indices, new picks first) to wsidx[b][0, nws).
-// The selection body, shared by ws_select_kernel and the fused K-cached round (ws_kc_round_kernel):
-// every thread of the 1024-thread workgroup calls it; returns the working-set size (B in widx[0, nws),
-// LDS, visible to every thread on return) or −1 when problem b is done.  LDS: shi [16], binfo [16],
-// hist [2][2048], bm [1024] (both dead on return), widx [Q].
-template <int M, int Q, bool kWriteIdx>
-__device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S, int* __restrict__ wsidx,
-                                              int* __restrict__ wsprev, double eps, int max_outer, const WsAux& X,
-                                              int* shi, int* binfo, int* hist, unsigned* bm, int* widx) {
-  const int nprev = S->nprev;
+// index-ordered ranks.
+//
+// ws_pick_lists: the k_up largest non-zero I_up keys, then the k_low largest I_low keys among the
+// positions not picked for I_up (two-level 11-bit radix histograms in LDS, ties taken in position
+// order: deterministic).  emit(i, p) is called for every pick (i = output slot, new picks of the up
+// list first, each list in position order); returns the pick count.  Every thread calls it.
+template <int M, typename Emit>
+__device__ __forceinline__ int ws_pick_lists(const unsigned (&ku)[M], const unsigned (&kl)[M], int t0, int k_up,
+                                             int k_low, int* shi, int* binfo, int* hist, Emit emit) {
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int l = P.l;
-  const int t0 = wave * 64 * M + lane;
-  const long long c0 = __builtin_amdgcn_s_memtime();
-  // ---- global gap from the maxima published by the gradient kernel
-  const unsigned long long gku = X.gkey[2 * b], gkl = X.gkey[2 * b + 1];
-  const double Gmax = gku ? f64_from_okey(gku) : -kWsInf;
-  const double Gmax2 = gkl ? f64_from_okey(gkl) : -kWsInf;
-  const double gap = Gmax + Gmax2;
-  // keys of this lane's points + member counts; all loads issued before any use
-  unsigned ku[M], kl[M];
-  int nu = 0, nl = 0;
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int t = t0 + 64 * m;
-    ku[m] = t < l ? __builtin_nontemporal_load(X.keys + P.aoff + t) : 0u;
-    kl[m] = t < l ? __builtin_nontemporal_load(X.keys + X.n + P.aoff + t) : 0u;
-  }
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    nu += __popcll(__ballot(ku[m] != 0u));
-    nl += __popcll(__ballot(kl[m] != 0u));
-  }
-  for (int i = tid; i < 4096 + 1024; i += kWsThreads) hist[i] = 0;   // hist + bitmap
+  for (int i = tid; i < 4096; i += kWsThreads) hist[i] = 0;
   if (tid < 8) binfo[tid] = 0;
-  int n_up;
-  wave_base(nu | (nl << 16), shi, &n_up);
-  const int n_low = n_up >> 16;
-  n_up &= 0xFFFF;
-  if (!(gap >= eps) || S->outer >= max_outer || n_up == 0 || n_low == 0) {
-    if (tid == 0) { S->done = 1; S->gap = gap; S->nc = 0; S->nws = 0; }
-    return -1;
-  }
-  if (tid == 0) { X.gkey[2 * b] = 0ull; X.gkey[2 * b + 1] = 0ull; }   // consumed (all read it above)
+  __syncthreads();
   // ---- level-1 histograms (top 11 key bits)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -279,11 +247,8 @@ __device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S
     hist_add(hist, kl[m] != 0u, 2048 + (int)(kl[m] >> 21));
   }
   __syncthreads();
-  const int k_up = min(Q / 4, n_up), k_low = min(Q / 4, n_low);
-  const long long c0a = __builtin_amdgcn_s_memtime();
   ws_find_bin(hist, k_up, k_low, shi, binfo);
   __syncthreads();
-  const long long c0b = __builtin_amdgcn_s_memtime();
   const unsigned bu1 = binfo[0], bl1 = binfo[2];
   const int au1 = binfo[1], al1 = binfo[3];
   for (int i = tid; i < 4096; i += kWsThreads) hist[i] = 0;
@@ -296,10 +261,9 @@ __device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S
   __syncthreads();
   ws_find_bin(hist, k_up - au1, k_low - al1, shi, binfo + 4);
   __syncthreads();
-  const long long c0c = __builtin_amdgcn_s_memtime();
   const unsigned Tu = (bu1 << 11) | (unsigned)binfo[4], Tl = (bl1 << 11) | (unsigned)binfo[6];
   const int need_u = k_up - au1 - binfo[5], need_l = k_low - al1 - binfo[7];
-  // ---- index-ordered compaction of the new picks (up list, then low list without the up picks)
+  // ---- position-ordered compaction (up list, then low list without the up picks)
   unsigned selm = 0u;
   int base = 0;
 #pragma unroll
@@ -333,21 +297,104 @@ __device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S
     for (int m = 0; m < M; ++m) {
       const bool take = (pick >> m) & 1u;
       const unsigned long long tb = __ballot(take);
-      if (take) {
-        const int t = t0 + 64 * m;
-        widx[pos + __popcll(tb & lanes_below())] = t;
-        atomicOr(&bm[t >> 5], 1u << (t & 31));
-      }
+      if (take) emit(pos + __popcll(tb & lanes_below()), t0 + 64 * m);
       pos += __popcll(tb);
     }
     selm |= pick;
     base += stot;
   }
-  const int nnew = base;
+  return base;
+}
+
+// Candidate lists for problems too large for one workgroup's selector (ws_cand_kernel): per block
+// of kWsCandBlk points the union of its top-(Q/4) I_up and top-(Q/4) I_low points, as (index, up key,
+// low key) in ncand = blocks · kWsCandPer slots per problem (unused slots: key 0).  The global top
+// of each list is the top of the union of the blocks' tops, so the selector then only reads the
+// candidates.
+struct WsCand {
+  int* idx;          // [P][ncand] point index (−1: empty)
+  unsigned* ku;      // [P][ncand]
+  unsigned* kl;      // [P][ncand]
+  int ncand;         // 0: the selector reads every point's keys
+};
+constexpr int kWsCandM = 8;
+constexpr int kWsCandBlk = kWsCandM * kWsThreads;   // 8192 points per candidate block
+
+// The selection body, shared by ws_select_kernel and the fused K-cached round (ws_kc_round_kernel):
+// every thread of the 1024-thread workgroup calls it; returns the working-set size (B in widx[0, nws),
+// LDS, visible to every thread on return) or −1 when problem b is done.  LDS: shi [16], binfo [16],
+// hist [2][2048], bm [1024] (both dead on return), widx [Q].  kCand: the keys come from the
+// candidate lists C (positions → point indices) instead of every point.
+template <int M, int Q, bool kWriteIdx, bool kCand = false>
+__device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S, int* __restrict__ wsidx,
+                                              int* __restrict__ wsprev, double eps, int max_outer, const WsAux& X,
+                                              int* shi, int* binfo, int* hist, unsigned* bm, int* widx,
+                                              const WsCand& C = WsCand{nullptr, nullptr, nullptr, 0}) {
+  const int nprev = S->nprev;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int L = kCand ? C.ncand : P.l;
+  const int t0 = wave * 64 * M + lane;
+  const long long c0 = __builtin_amdgcn_s_memtime();
+  // ---- global gap from the maxima published by the gradient kernel
+  const unsigned long long gku = X.gkey[2 * b], gkl = X.gkey[2 * b + 1];
+  const double Gmax = gku ? f64_from_okey(gku) : -kWsInf;
+  const double Gmax2 = gkl ? f64_from_okey(gkl) : -kWsInf;
+  const double gap = Gmax + Gmax2;
+  // keys of this lane's points (candidates) + member counts; all loads issued before any use
+  unsigned ku[M], kl[M];
+  int nu = 0, nl = 0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int t = t0 + 64 * m;
+    if (kCand) {
+      ku[m] = t < L ? C.ku[(size_t)b * C.ncand + t] : 0u;
+      kl[m] = t < L ? C.kl[(size_t)b * C.ncand + t] : 0u;
+    } else {
+      ku[m] = t < L ? __builtin_nontemporal_load(X.keys + P.aoff + t) : 0u;
+      kl[m] = t < L ? __builtin_nontemporal_load(X.keys + X.n + P.aoff + t) : 0u;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    nu += __popcll(__ballot(ku[m] != 0u));
+    nl += __popcll(__ballot(kl[m] != 0u));
+  }
+  if (!kCand)
+    for (int i = tid; i < 1024; i += kWsThreads) bm[i] = 0;
+  int n_up;
+  wave_base(nu | (nl << 16), shi, &n_up);
+  const int n_low = n_up >> 16;
+  n_up &= 0xFFFF;
+  if (!(gap >= eps) || S->outer >= max_outer || n_up == 0 || n_low == 0) {
+    if (tid == 0) { S->done = 1; S->gap = gap; S->nc = 0; S->nws = 0; }
+    return -1;
+  }
+  if (tid == 0) { X.gkey[2 * b] = 0ull; X.gkey[2 * b + 1] = 0ull; }   // consumed (all read it above)
+  const int k_up = min(Q / 4, n_up), k_low = min(Q / 4, n_low);
+  const long long c0a = __builtin_amdgcn_s_memtime();
+  const int nnew = ws_pick_lists<M>(ku, kl, t0, k_up, k_low, shi, binfo, hist, [&](int i, int p) {
+    if (kCand) {
+      widx[i] = C.idx[(size_t)b * C.ncand + p];
+    } else {
+      widx[i] = p;
+      atomicOr(&bm[p >> 5], 1u << (p & 31));
+    }
+  });
+  const long long c0b = __builtin_amdgcn_s_memtime();
+  const long long c0c = c0b;
   __syncthreads();
   // ---- the previous round's new picks that were not picked again (in their old order)
   const int pv = tid < nprev ? wsprev[(size_t)b * (Q / 2) + tid] : -1;
-  const bool keep = pv >= 0 && !((bm[pv >> 5] >> (pv & 31)) & 1u);
+  bool again = false;
+  if (pv >= 0) {
+    if (kCand) {
+      for (int w = 0; w < nnew; ++w) again |= widx[w] == pv;
+    } else {
+      again = (bm[pv >> 5] >> (pv & 31)) & 1u;
+    }
+  }
+  const bool keep = pv >= 0 && !again;
   const unsigned long long kb = __ballot(keep);
   int ktot;
   const int kpos = nnew + wave_base(__popcll(kb), shi, &ktot) + __popcll(kb & lanes_below());
@@ -368,6 +415,55 @@ __device__ __forceinline__ int ws_select_body(const WsProb& P, int b, WsState* S
     S->gap = gap;
   }
   return nws;
+}
+
+// Stage 1 of the selection for large problems: grid = (blocks of kWsCandBlk points, P).  Each block
+// writes the union of its top-(Q/4) I_up and I_low points to its kWsCandPer(Q) candidate slots.
+template <int Q>
+__global__ __launch_bounds__(kWsThreads) void ws_cand_kernel(const WsProb* __restrict__ probs,
+                                                             const WsState* __restrict__ states, WsAux X, WsCand C) {
+  constexpr int M = kWsCandM;
+  constexpr int per = Q / 2;   // candidate slots per block
+  const int b = blockIdx.y, blk = blockIdx.x;
+  if (states[b].done) return;
+  const WsProb P = probs[b];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int beg = blk * kWsCandBlk;
+  int* out_idx = C.idx + (size_t)b * C.ncand + (size_t)blk * per;
+  unsigned* out_ku = C.ku + (size_t)b * C.ncand + (size_t)blk * per;
+  unsigned* out_kl = C.kl + (size_t)b * C.ncand + (size_t)blk * per;
+  __shared__ int shi[16], binfo[16];
+  __shared__ int hist[4096];
+  __shared__ int pick[per];
+  const int t0 = wave * 64 * M + lane;
+  unsigned ku[M], kl[M];
+  int nu = 0, nl = 0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int t = beg + t0 + 64 * m;
+    ku[m] = t < P.l ? __builtin_nontemporal_load(X.keys + P.aoff + t) : 0u;
+    kl[m] = t < P.l ? __builtin_nontemporal_load(X.keys + X.n + P.aoff + t) : 0u;
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    nu += __popcll(__ballot(ku[m] != 0u));
+    nl += __popcll(__ballot(kl[m] != 0u));
+  }
+  int n_up;
+  wave_base(nu | (nl << 16), shi, &n_up);
+  const int n_low = n_up >> 16;
+  n_up &= 0xFFFF;
+  const int np = (n_up == 0 && n_low == 0) ? 0
+                 : ws_pick_lists<M>(ku, kl, t0, min(Q / 4, n_up), min(Q / 4, n_low), shi, binfo, hist,
+                                    [&](int i, int p) { pick[i] = beg + p; });
+  __syncthreads();
+  if (tid < per) {
+    const int t = tid < np ? pick[tid] : -1;
+    out_idx[tid] = t;
+    out_ku[tid] = t >= 0 ? X.keys[P.aoff + t] : 0u;
+    out_kl[tid] = t >= 0 ? X.keys[X.n + P.aoff + t] : 0u;
+  }
 }
 
 template <int M, int Q>
@@ -749,12 +845,12 @@ __device__ __forceinline__ T sel4(const T (&v)[4], int m) {   // v[m] for a wave
 }
 __device__ __forceinline__ float rdlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 
-template <int M, int KS>
+template <int M, int KS, bool kCand>
 __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
     const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
     const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
     int* __restrict__ wsprev, float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc,
-    int Fp2, double eps, int max_outer, int max_inner, double inner_frac, WsAux X) {
+    int Fp2, double eps, int max_outer, int max_inner, double inner_frac, WsAux X, WsCand C) {
   constexpr int Q = kKcQ;
   constexpr int SL = Q / 64;            // slots per lane of the solving wave (slot s = 64·m + lane)
   constexpr unsigned kIdx = Q - 1;      // slot bits packed under the selection keys
@@ -774,8 +870,8 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
   int* hist = reinterpret_cast<int*>(zbuf);                              // (selector only) [2][2048]
   unsigned* bm = reinterpret_cast<unsigned*>(hist + 4096);               // (selector only) [1024]
   float* tri = zbuf + (kc_zbuf_bytes(KS) + 15) / 16 * 4;                 // [Q(Q+1)/2]
-  const int nws = ws_select_body<M, Q, false>(P, b, S, nullptr, wsprev, eps, max_outer, X, shi, binfo, hist,
-                                              bm, widx);
+  const int nws = ws_select_body<M, Q, false, kCand>(P, b, S, nullptr, wsprev, eps, max_outer, X, shi, binfo,
+                                                     hist, bm, widx, C);
   if (nws < 0) return;
   const long long c1 = __builtin_amdgcn_s_memtime();
   // ---- z_B and γ'‖z‖² into LDS (zero rows past nws / features past F: exact no-ops in the dots)
@@ -1200,18 +1296,39 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
 
 // n_iter K-cached rounds (ws_kc_round + ws_gupdate) enqueued back to back; q = kKcQ, F ≤ 24.
 // wsz/wsn/wdc hold [P][2·KS][256] / [P][256] / [P][256]; wsprev [P][128].
+// Selection mode: problems of ≤ kWsDirectMax points are selected from every point's keys by the
+// round kernel itself; larger ones first get per-block candidate lists (ws_cand_kernel, one more
+// launch per round) and the round kernel selects among those.  cand: [3][P][ncand] u32 workspace,
+// ncand = ws_kc_ncand(max_l) (0 below the threshold).
+constexpr int kWsDirectMax = 16 * kWsThreads;
+long long ws_kc_ncand(long long max_l) {
+  return max_l <= kWsDirectMax ? 0 : (max_l + kWsCandBlk - 1) / kWsCandBlk * (kKcQ / 2);
+}
+
+void ws_kc_cand_len(long long max_l, uintptr_t out) { *reinterpret_cast<long long*>(out) = ws_kc_ncand(max_l); }
+
 void ws_steps_kc(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
                  uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
-                 uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
-                 double inner_frac, int n_iter, uintptr_t stream) {
+                 uintptr_t keys, long long n, uintptr_t gkey, uintptr_t cand, double eps, int max_outer,
+                 int max_inner, double inner_frac, int n_iter, uintptr_t stream) {
   const WsAux X = ws_aux(keys, n, gkey);
   HFENS_REQUIRE(F >= 1 && F <= 24, "ws_steps_kc: 1 <= F <= 24");
-  HFENS_REQUIRE(max_l < 32 * kWsThreads, "ws_steps_kc: problems of 32768+ points need the multi-workgroup selector");
+  const long long ncand = ws_kc_ncand(max_l);
+  HFENS_REQUIRE(ncand <= 32LL * kWsThreads, "ws_steps_kc: at most 2^21 points per problem");
+  HFENS_REQUIRE(ncand == 0 || cand != 0, "ws_steps_kc: the candidate workspace is missing");
   if (P == 0 || max_l == 0) return;
   hipStream_t st = as_stream(stream);
   const int KS = ws_ks(F);
   const int Fp2 = 2 * KS;
-  const int M = max_l <= 4 * kWsThreads ? 4 : max_l <= 16 * kWsThreads ? 16 : 32;
+  const long long L = ncand ? ncand : max_l;   // keys the round kernel's selector reads per problem
+  const int M = L <= 4 * kWsThreads ? 4 : L <= 16 * kWsThreads ? 16 : 32;
+  WsCand C{nullptr, nullptr, nullptr, (int)ncand};
+  if (ncand) {
+    C.idx = reinterpret_cast<int*>(cand);
+    C.ku = reinterpret_cast<unsigned*>(cand) + (size_t)P * ncand;
+    C.kl = reinterpret_cast<unsigned*>(cand) + 2 * (size_t)P * ncand;
+  }
+  const dim3 cgrid((max_l + kWsCandBlk - 1) / kWsCandBlk, P);
   auto pp = (const WsProb*)probs;
   auto sp = (WsState*)states;
   auto zp = (const float*)zcat;
@@ -1224,14 +1341,20 @@ void ws_steps_kc(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintp
   auto wp = (int*)wsprev;
   const dim3 grid((max_l + 255) / 256, P);
   for (int it = 0; it < n_iter; ++it) {
-#define KC_ROUND(MM, KK)                                                                                     \
-  if (M == MM && KS == KK) {                                                                                 \
-    hipLaunchKernelGGL((ws_kc_round_kernel<MM, KK>), dim3(P), dim3(kWsThreads), kc_lds_bytes(KK), st, pp, sp, \
-                       zp, F, np_, ap, gp, wp, wz, wn, wd, Fp2, eps, max_outer, max_inner, inner_frac, X);   \
+    if (ncand) {
+      hipLaunchKernelGGL((ws_cand_kernel<kKcQ>), cgrid, dim3(kWsThreads), 0, st, pp, sp, X, C);
+      launch_check();
+    }
+#define KC_ROUND(MM, KK, CC)                                                                                     \
+  if (M == MM && KS == KK && (ncand != 0) == CC) {                                                               \
+    hipLaunchKernelGGL((ws_kc_round_kernel<MM, KK, CC>), dim3(P), dim3(kWsThreads), kc_lds_bytes(KK), st, pp, sp, \
+                       zp, F, np_, ap, gp, wp, wz, wn, wd, Fp2, eps, max_outer, max_inner, inner_frac, X, C);    \
   } else
-    KC_ROUND(4, 4) KC_ROUND(4, 9) KC_ROUND(4, 12) KC_ROUND(16, 4) KC_ROUND(16, 9) KC_ROUND(16, 12)
-    KC_ROUND(32, 4) KC_ROUND(32, 9) KC_ROUND(32, 12) {
-      HFENS_REQUIRE(false, "ws_steps_kc: no round instance for this F");
+    KC_ROUND(4, 4, false) KC_ROUND(4, 9, false) KC_ROUND(4, 12, false) KC_ROUND(16, 4, false)
+    KC_ROUND(16, 9, false) KC_ROUND(16, 12, false)
+    KC_ROUND(4, 9, true) KC_ROUND(16, 9, true) KC_ROUND(32, 9, true) KC_ROUND(4, 4, true) KC_ROUND(16, 4, true)
+    KC_ROUND(32, 4, true) KC_ROUND(4, 12, true) KC_ROUND(16, 12, true) KC_ROUND(32, 12, true) {
+      HFENS_REQUIRE(false, "ws_steps_kc: no round instance for this F / size");
     }
 #undef KC_ROUND
     launch_check();

@@ -1,5 +1,6 @@
 """Native single-workgroup SPD factor / solve (ops/csrc/linalg.hip) vs torch.linalg in f64: the
 interior-point SVC's r × r Woodbury systems (equilibrated, jitter retries on the device)."""
+import numpy as np
 import pytest
 import torch
 
@@ -172,3 +173,50 @@ def test_ipm_fused_direction_kernels_bit_identical(dev, monkeypatch):
     assert out[False][2] == out[True][2]
     assert out[False][1] == out[True][1]
     assert torch.equal(out[False][0], out[True][0])
+
+
+@pytest.mark.parametrize("n,r", [(37, 16), (20011, 428), (70000, 512), (5000, 132)])
+def test_wsyrk_f32_matches_f64(dev, monkeypatch, n, r):
+    """The f32-input-MFMA weighted SYRK (lowrank.hip wsyrk_f32: Φ exact in f32, d ⊙ Φ rounded to f32,
+    f32 sums over ≤ 256 rows folded into f64) against the f64 product of the same Φ: every entry
+    within 1e-6 of the magnitude of its terms, symmetric, deterministic."""
+    from hfens.models import svc_lowrank
+    from hfens.models.svc_lowrank import _weighted_gram
+    monkeypatch.setattr(svc_lowrank, "GRAM", "f32")
+    g = torch.Generator(device=dev).manual_seed(3 * n + r)
+    P32 = torch.randn(n, r, generator=g, device=dev, dtype=torch.float32)
+    Phi = P32.double()
+    d = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 10 ** torch.randint(-6, 6, (n,), generator=g, device=dev)
+    S = _weighted_gram(Phi, d, P32)
+    want = Phi.T @ (d[:, None] * Phi)
+    mag = Phi.abs().T @ (d[:, None] * Phi.abs())
+    assert torch.equal(S, S.T)
+    err = float(((S - want).abs() / mag).max())
+    assert err < 1e-6, err
+    assert torch.equal(S, _weighted_gram(Phi, d, P32))      # deterministic
+
+
+def test_ipm_f32_gram_matches_f64_path(dev, monkeypatch):
+    """The interior point with the f32-MFMA Gram in its Newton systems (the default) converges to the
+    f64 path's optimum: same stopping test (f64 residuals), dual coefficients and ρ within 1e-6."""
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import svc_lowrank
+    X, y, _ = make_hf_cohort(30000, 17, seed=5, nan_frac=0.0)
+    Z = torch.as_tensor(X, device=dev)
+    Z = (Z - Z.mean(0)) / Z.std(0).clamp(min=1e-12)
+    g = torch.Generator().manual_seed(1)
+    idx = torch.randperm(Z.shape[0], generator=g)[:256].to(dev)
+    Phi, _ = svc_lowrank.nystrom_map(Z, idx, 1.0 / 17)
+    Phi = Phi.to(torch.float32).to(torch.float64)          # exactly f32, as fit_svc_lowrank_batch
+    yv = torch.as_tensor(np.where(y > 0.5, -1.0, 1.0), device=dev)
+    c = torch.where(yv > 0, 0.62, 2.5).to(torch.float64)
+    out = {}
+    for mode in ("f64", "f32"):
+        monkeypatch.setattr(svc_lowrank, "GRAM", mode)
+        a, rho, it = svc_lowrank.ipm_svc_dual(Phi, yv, c)
+        out[mode] = (a, rho, it)
+    a64, rho64, it64 = out["f64"]
+    a32, rho32, it32 = out["f32"]
+    assert it32 <= it64 + 5, (it32, it64)
+    assert float((a32 - a64).abs().max()) <= 1e-6 * float(c.max()), float((a32 - a64).abs().max())
+    assert abs(rho32 - rho64) <= 1e-6, (rho32, rho64)

@@ -1,0 +1,40 @@
+"""Large-problem SVC on the MI355X: the exact working-set SMO past the
+one-workgroup selector's range (candidate-list selection, svm_ws.hip ws_cand_kernel) against the
+Nyström + interior-point approximation (svc_lowrank) on the same 40k-row draw."""
+import numpy as np
+import pytest
+import torch
+
+from hfens.io.synth import make_hf_cohort
+from hfens.models import smo
+from hfens.models.svc import SVC
+from hfens.utils import metrics
+
+pytestmark = pytest.mark.gpu
+
+
+def _draw(n, seed):
+    X, y, _ = make_hf_cohort(n, 17, seed=seed, nan_frac=0.0)
+    return X, y
+
+
+def test_exact_ws_vs_lowrank_40k(dev, monkeypatch):
+    X, y = _draw(40000, 40)
+    Xt, yt = _draw(20000, 41)
+    mu, sd = X.mean(0), X.std(0)
+    sd = np.where(sd > 0, sd, 1.0)
+    Z = torch.as_tensor((X - mu) / sd, device=dev)
+    Zt = torch.as_tensor((Xt - mu) / sd, device=dev)
+    out = {}
+    for solver in ("ws", "lowrank"):
+        monkeypatch.setattr(smo, "SOLVER", solver)
+        m = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, torch.as_tensor(y, device=dev))
+        if solver == "ws":
+            st = smo.LAST_WS_STATS
+            assert (st["gap"] < 1e-3).all(), st["gap"]          # libsvm's stopping rule, every problem
+            assert smo.LAST_SMO_INFO.get("ws_kc")
+        d = m.decision_function(Zt).double().cpu().numpy()
+        p = m.predict_proba(Zt)[:, 1].double().cpu()
+        out[solver] = (d, metrics.evaluate(torch.as_tensor(yt), p)["auroc"])
+    assert abs(out["ws"][1] - out["lowrank"][1]) <= 0.002, (out["ws"][1], out["lowrank"][1])
+    assert np.corrcoef(out["ws"][0], out["lowrank"][0])[0, 1] >= 0.999
