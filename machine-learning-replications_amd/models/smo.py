@@ -385,19 +385,26 @@ WS_MAX_F = 48            # features the working-set kernel's register/LDS budget
 
 # K-cached rounds (svm_ws.hip ws_kc_round_kernel): q = 256 with the working set's kernel matrix in
 # LDS and a one-wave pair loop; for F ≤ WS_KC_MAX_F.  HFENS_SVM_WS_KC=0 keeps the q = 1024 solver.
-WS_KC = os.environ.get("HFENS_SVM_WS_KC", "1") != "0"
+# "auto": K-cached rounds for problems past the one-workgroup selector (> WS_KC_DIRECT_MAX points,
+# candidate-list selection), the q = 1024 solver below that: on the bench's 10k problem the K-cached
+# rounds measured 44 vs 33 ms per fit (226 rounds of ≈ 45 µs selection + build against 35 of the
+# q = 1024 solver, profiles/r4_headline.md).  "1": always (F ≤ 24); "0": never.
+WS_KC = os.environ.get("HFENS_SVM_WS_KC", "auto")
 WS_KC_MAX_F = 24
 WS_KC_Q = 256
+WS_KC_DIRECT_MAX = 16 * 1024      # svm_ws.hip kWsDirectMax: larger problems select from candidate lists
 
 
-def ws_kc(F: int) -> bool:
-    return WS_KC and F <= WS_KC_MAX_F
+def ws_kc(F: int, max_l: int = 0) -> bool:
+    if WS_KC == "0" or F > WS_KC_MAX_F:
+        return False
+    return WS_KC == "1" or max_l > WS_KC_DIRECT_MAX
 
 
-def ws_q(F: int) -> int:
+def ws_q(F: int, max_l: int = 0) -> int:
     """Working-set size of svm_ws.hip for F features (K-cached: 256; else one slot per thread with
     z_B in LDS: 1024 / 512)."""
-    if ws_kc(F):
+    if ws_kc(F, max_l):
         return WS_KC_Q
     return 1024 if F <= 24 else 512
 
@@ -631,7 +638,6 @@ WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
-WS_KC_DIRECT_MAX = 16 * 1024      # svm_ws.hip kWsDirectMax: larger problems select from candidate lists
 WS_GRAPH = os.environ.get("HFENS_SVM_WS_GRAPH", "1") != "0"
 WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # rounds per captured graph
 _WS_GRAPHS: dict = {}
@@ -669,13 +675,15 @@ def _ws_groups(live, device) -> List[List[int]]:
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None):
     P = len(live)
     n = aoffs[-1]
-    Q = ws_q(F)
+    ml = max(p.l for p in live)
+    kc_all = ws_kc(F, ml)          # one solver kind for the whole batch (every group)
+    Q = ws_q(F, ml)
     Fp2 = 2 * _ws_ks(F)
     max_outer = (max(5_000, max(p.l for p in live) // 4) if max_iter_cap is None else int(max_iter_cap))
     max_inner = WS_MAX_INNER
     # large problems (candidate-list selection, hundreds to thousands of rounds): host-checked rounds
     # in chunks of WS_BIG_CHUNK from the start, one group (the rounds-ahead guess would be far off)
-    big = ws_kc(F) and max(p.l for p in live) > WS_KC_DIRECT_MAX
+    big = kc_all and ml > WS_KC_DIRECT_MAX
     sync = _WS_SYNC[0] or big
     if big and steps_per_check is None:
         steps_per_check = WS_BIG_CHUNK
@@ -687,7 +695,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     # captured once (WS_GRAPH_CHUNK rounds per graph) and replayed.  Every argument of a captured
     # launch must be the same buffer at every replay: the per-point arrays, the features and every
     # per-group buffer are process-lifetime workspaces (runtime.workspace), re-filled per fit.
-    use_graph = (WS_GRAPH and cuda and ws_kc(F) and not sync
+    use_graph = (WS_GRAPH and cuda and kc_all and not sync and not PROFILE_WS
                  and caller.cuda_stream != torch.cuda.default_stream(device).cuda_stream)
     # per-point arrays (indexed by each problem's absolute offset) are shared by the groups
     if use_graph:
@@ -718,7 +726,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             side.wait_stream(caller)
             st = side.cuda_stream
         runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
-                              side, zn, alpha, G, keys, hist, n, Q, Fp2, gi=gi if use_graph else None,
+                              side, zn, alpha, G, keys, hist, n, Q, Fp2, kc_all, gi=gi if use_graph else None,
                               cap_stream=(side if side is not None else caller) if use_graph else None))
     if sync:
         runs[0]["sync_rounds"](steps_per_check)
@@ -728,7 +736,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         # a batch still unconverged after them reports err and is re-solved synchronously by
         # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
         # group's stream starts within one chunk of host launch time.
-        left = min(WS_KC_ROUNDS_AHEAD if ws_kc(F) else WS_ROUNDS_AHEAD, max_outer)
+        left = min(WS_KC_ROUNDS_AHEAD if kc_all else WS_ROUNDS_AHEAD, max_outer)
         chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
         while left > 0:
             k = min(chunk, left)
@@ -770,12 +778,12 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     LAST_WS_STATS.set_thunk(stats)
     LAST_SMO_INFO.clear()
     LAST_SMO_INFO.update(problems=P, max_l=int(max(p.l for p in live)), solver="ws", q=Q, ws_groups=len(runs),
-                         ws_kc=ws_kc(F))
+                         ws_kc=kc_all)
     return alpha, rho, iters, err
 
 
 def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, s, side,
-              zn, alpha, G, keys, hist, n, Q, Fp2, gi=None, cap_stream=None):
+              zn, alpha, G, keys, hist, n, Q, Fp2, kc=False, gi=None, cap_stream=None):
     """State of the problems ``live[idx]``, whose rounds go on stream ``s`` (per-problem state is
     group-local; the per-point arrays are the shared ones, addressed by each problem's absolute
     offset).  Returns closures: ``steps(k)`` enqueues k rounds, ``sync_rounds(chunk)`` runs
@@ -814,7 +822,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
         wprof = torch.zeros(P * 6, dtype=torch.int64, device=device) if PROFILE_WS else None
         gkey = buf("gkey", 2 * P, torch.int64)
         cand = None
-        if ws_kc(F):
+        if kc:
             nc_out = np.zeros(1, dtype=np.int64)
             E.ws_kc_cand_len(max_l, nc_out.ctypes.data)
             if int(nc_out[0]) > 0:   # large problems: per-block candidate lists (svm_ws.hip ws_cand_kernel)
@@ -827,8 +835,6 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
                   states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
         out["idx_dev"] = _to_dev(out["idx"], device)
     done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
-
-    kc = ws_kc(F)
 
     def steps(k):
         if graph:
@@ -859,7 +865,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
                           G.data_ptr(), states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(),
                           wsprev.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(),
                           cand.data_ptr() if cand is not None else 0, eps, max_outer, max_inner,
-                          WS_INNER_FRAC, k, s)
+                          WS_INNER_FRAC, k, wprof.data_ptr() if wprof is not None else 0, s)
             return
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
@@ -925,7 +931,7 @@ LAST_SMO_PROF: dict = {}
 LAST_SMO_INFO: dict = {}
 PROFILE_SMO = os.environ.get("HFENS_PROFILE_SMO", "0") == "1"
 PROFILE_COOP = os.environ.get("HFENS_PROFILE_COOP", "0") == "1"   # in-kernel phase counters of the cooperative SMO
-PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # phase counters (svm_ws.hip built with -DHFENS_WS_STAMPS)
+PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # phase counters (q=1024: svm_ws.hip built with -DHFENS_WS_STAMPS; K-cached: a stamped instance)
 
 
 def assign_problems(sizes, world: int) -> List[int]:
@@ -1071,22 +1077,29 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
     return finish_svc_batch(launch_svc_batch(svcs, Zs, ys, max_iter_cap, group=group))
 
 
-# Exact (libsvm pair sequence) vs large-problem path (``svc_lowrank``: Nyström reduced-set SVC,
-# interior-point dual).  "auto": exact while every problem has ≤ EXACT_MAX_POINTS points and the
-# batch's stored Grams (Σ l² f32) fit GRAM_BUDGET bytes; otherwise low-rank.  The bench's 10k-row
-# configuration (max l = 10,000, 7 GB of Grams) stays exact.
-EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "32768"))
+# Exact vs large-problem path (``svc_lowrank``: Nyström reduced-set SVC, interior-point dual).
+# GPU: the working-set SMO needs O(n) memory (no Gram), and its candidate-list selection handles any
+# size, so "auto" keeps every problem exact up to EXACT_MAX_POINTS — the measured crossover
+# (scripts/probes/svc_crossover.py, profiles/r4_svc_crossover.md: one probability fit, exact vs
+# Nyström 0.17 vs 1.56 s at 40k rows, 0.81 vs 1.55 s at 100k); features past the K-cached kernel's
+# range (F > 24) keep the one-workgroup selector's 32,768-point limit.  Host (CPU): the exact solver
+# stores every problem's Gram, so it stays below EXACT_HOST_MAX points and GRAM_BUDGET bytes.
+EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "200000"))
+EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 
 
-def use_lowrank(sizes) -> bool:
+def use_lowrank(sizes, F: int = 17, device_type: str = "cpu") -> bool:
     if SOLVER == "lowrank":
         return True
     if SOLVER in ("exact", "ws"):
         return False
+    m = max(sizes)
+    if device_type == "cuda":
+        return m > EXACT_MAX_POINTS or (F > WS_KC_MAX_F and m >= 32768)
     # problem sizes ≈ 0.8·l (Platt folds) and l (final) per fit
     gram = sum(4.0 * (5 * (0.8 * l) ** 2 + l * l) for l in sizes)
-    return max(sizes) > EXACT_MAX_POINTS or gram > GRAM_BUDGET
+    return m > EXACT_HOST_MAX or gram > GRAM_BUDGET
 
 
 def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None,
@@ -1105,7 +1118,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     expansion then runs on the host while the device computes the guards and γ statistics, and
     only those are read back."""
     from .. import ops
-    if use_lowrank([int(y.numel()) for y in ys]):
+    if use_lowrank([int(y.numel()) for y in ys], int(Zs[0].shape[1]), Zs[0].device.type):
         from .svc_lowrank import fit_svc_lowrank_batch
         LAST_SMO_INFO.clear()
         LAST_SMO_INFO.update(solver="nystrom-ipm", problems=6 * len(svcs), max_l=max(int(y.numel()) for y in ys))

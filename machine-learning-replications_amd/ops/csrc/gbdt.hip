@@ -1113,6 +1113,41 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
     }
   }
   if (t > T) return;   // the closing launch only books the last slot
+  // a sub-tile's row inputs (this thread's two rows: kSgTile = 2 × threads) are loaded one sub-tile
+  // ahead — issued before the previous sub-tile's histogram, consumed by the next apply — so their
+  // global latencies overlap the histogram instead of stalling the apply.  The first sub-tile's
+  // weights, raw scores and labels do not depend on tree t−1's split: they are issued before it, so
+  // their latency hides under the split (a third of a small-shard stage, profiles/r3_gbdt_dp.md);
+  // only the split feature's bin column waits for it.
+  const int w0r = blockIdx.x * J.rows_per_wg;
+  const int w1r = min(n, w0r + J.rows_per_wg);
+  float w0v[RPT];
+  double rwv[RPT], yv[RPT];
+  int bnv[RPT];
+  auto load_vals = [&](int rs) {
+    const int ms = min(kSgTile, w1r - rs);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int k = tid + u * kT;
+      const bool ok = k < ms;
+      const int i = rs + (ok ? k : 0);
+      const size_t bi = (size_t)b * n + i;
+      w0v[u] = ok ? J.w[bi] : 0.f;
+      rwv[u] = ok ? J.raw[bi] : 0.0;
+      yv[u] = ok ? (double)J.y[i] : 0.0;
+    }
+  };
+  auto load_bins = [&](int rs, int pfeat) {
+    const int ms = min(kSgTile, w1r - rs);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int k = tid + u * kT;
+      const bool ok = k < ms;
+      const int i = rs + (ok ? k : 0);
+      bnv[u] = (ok && t >= 1 && pfeat >= 0) ? (int)J.bins[(size_t)pfeat * J.ldb + i] : 0;
+    }
+  };
+  if (w0r < w1r) load_vals(w0r);
   // ---- 1: split of tree t−1 from the reduced stage-(t−1) histogram
   if (t >= 1) {
     // stage the reduced histogram in LDS first (one bulk round of loads, 8 in flight per thread):
@@ -1239,29 +1274,7 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
     if constexpr (MF)
       for (int k = tid; k < n_mb * 32 * 32; k += kT) Tsl[k] = 0;
   }
-  const int w0r = blockIdx.x * J.rows_per_wg;
-  const int w1r = min(n, w0r + J.rows_per_wg);
-  // a sub-tile's row inputs (this thread's two rows: kSgTile = 2 × threads) are loaded one sub-tile
-  // ahead — issued before the previous sub-tile's histogram, consumed by the next apply — so their
-  // global latencies overlap the histogram instead of stalling the apply
-  float w0v[RPT];
-  double rwv[RPT], yv[RPT];
-  int bnv[RPT];
-  auto load_rows = [&](int rs) {
-    const int ms = min(kSgTile, w1r - rs);
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-      const int k = tid + u * kT;
-      const bool ok = k < ms;
-      const int i = rs + (ok ? k : 0);
-      const size_t bi = (size_t)b * n + i;
-      w0v[u] = ok ? J.w[bi] : 0.f;
-      rwv[u] = ok ? J.raw[bi] : 0.0;
-      yv[u] = ok ? (double)J.y[i] : 0.0;
-      bnv[u] = (ok && has_prev && pf >= 0) ? (int)J.bins[(size_t)pf * J.ldb + i] : 0;
-    }
-  };
-  if (w0r < w1r) load_rows(w0r);
+  if (w0r < w1r) load_bins(w0r, pf);   // (its weights / raw / labels were issued before the split)
   for (int r0 = w0r; r0 < w1r; r0 += kSgTile) {
     const int m = min(kSgTile, w1r - r0);
     __syncthreads();   // the previous sub-tile's histogram passes are done with the row cache
@@ -1311,7 +1324,10 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
         if (J.active) acc6[5] += in ? q_of(wi, J.qscale) : 0;
       }
     }
-    if (r0 + kSgTile < w1r) load_rows(r0 + kSgTile);
+    if (r0 + kSgTile < w1r) {
+      load_vals(r0 + kSgTile);
+      load_bins(r0 + kSgTile, pf);
+    }
     if (!has_cur) continue;
     for (int k = m + tid; k < kSgTile; k += kT) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
     __syncthreads();

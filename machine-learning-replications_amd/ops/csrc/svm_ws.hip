@@ -151,7 +151,8 @@ __device__ __forceinline__ int wave_base(int wave_total, int* sh, int* total) {
 }
 
 // LDS histogram add: when every active lane of the wave hits one bin (massive ties, e.g. all
-// G = −1 at the start) one lane adds the popcount instead of 64 serialized atomics.
+// G = −1 at the start) one lane adds the popcount instead of 64 serialized atomics.  (Folding up to
+// three clusters per instruction was measured slower: 23 → 35 µs per selection, r4d.)
 __device__ __forceinline__ void hist_add(int* hist, bool on, int bin) {
   const unsigned long long act = __ballot(on);
   if (!act) return;
@@ -554,7 +555,10 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   const long long c2 = __builtin_amdgcn_s_memtime();
   bool valid[SL], pos[SL];
   int tt[SL];
-  float y[SL], Cw[SL], a[SL], g[SL], sn[SL];
+  // yg = y·G (the solver's natural variable: keys −yG / yG, gd = GmaxB + yG, and the update
+  // yG += K_i c_i + K_j c_j with y² = 1 — bit for bit y·(G + y·Δ) since ×(±1) is exact); the
+  // I_up / I_low tests as y·α < tu and −y·α < tl with per-slot bounds (−∞ for empty slots)
+  float y[SL], Cw[SL], a[SL], yg[SL], sn[SL], tu[SL], tl[SL];
   double a0[SL];
   f32x2 zp[SL / 2][FP];   // features of slots (2h, 2h+1) side by side: one v_pk_fma_f32 per k
 #pragma unroll
@@ -565,9 +569,11 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     pos[m] = tt[m] < P.npos;
     y[m] = pos[m] ? 1.f : -1.f;
     Cw[m] = (float)(pos[m] ? P.Cp : P.Cn);
+    tu[m] = valid[m] ? (pos[m] ? Cw[m] : 0.f) : -INFINITY;
+    tl[m] = valid[m] ? (pos[m] ? 0.f : Cw[m]) : -INFINITY;
     a0[m] = valid[m] ? ap[tt[m]] : 0.0;
     a[m] = (float)a0[m];
-    g[m] = valid[m] ? (float)Gp[tt[m]] : 0.f;
+    yg[m] = valid[m] ? y[m] * (float)Gp[tt[m]] : 0.f;
     sn[m] = valid[m] ? snB[s] : 0.f;
 #pragma unroll
     for (int k = 0; k < FP; k += 4) {
@@ -647,19 +653,18 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
       const unsigned s = (unsigned)(tid + TH * m);
-      glp[s] = g[m];
+      glp[s] = yg[m];
       alp[s] = a[m];
-      const bool below = a[m] < Cw[m], above = a[m] > 0.f;
-      const bool up = valid[m] & ((pos[m] & below) | (!pos[m] & above));
-      low[m] = valid[m] & ((pos[m] & above) | (!pos[m] & below));
-      const float yg = y[m] * g[m];
+      const float ya = y[m] * a[m];
+      const bool up = ya < tu[m];
+      low[m] = -ya < tl[m];
       // step 1: i = argmax_{I_up ∩ B} −y·G.  The slot rides in the key's low bits (a ~1e-4
       // relative tie window for the pick); the stopping test uses the unmasked maxima.
       const unsigned um = 0u - (unsigned)up, lm = 0u - (unsigned)low[m];
-      const unsigned kv = f32_okey(-yg) & um;
+      const unsigned kv = f32_okey(-yg[m]) & um;
       k4 = max(k4, kv);
       k1 = max(k1, ((kv & ~kIdx) | s) & um);
-      k3 = max(k3, f32_okey(yg) & lm);
+      k3 = max(k3, f32_okey(yg[m]) & lm);
     }
     k1 = wave_max_u32(k1);
     k3 = wave_max_u32(k3);
@@ -672,10 +677,11 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     const unsigned K4 = __builtin_amdgcn_readfirstlane(red4(r4));
     if (K1 == 0u || K3 == 0u) return false;
     const int i = (int)(K1 & kIdx);
-    const float Gi = glp[i];
+    const float ygi = glp[i];
     const bool ipos = widx[i] < P.npos;
     const float yi = ipos ? 1.f : -1.f;
-    const float GmaxB = -yi * Gi;
+    const float Gi = yi * ygi;
+    const float GmaxB = -ygi;
     const float lgap = f32_from_okey(K4) + f32_from_okey(K3);
     // (0.9999: the f32 local gap of a problem whose f64 gap is still ≥ eps always takes a pair)
     if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
@@ -689,7 +695,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     for (int m = 0; m < SL; ++m) {
       const unsigned s = (unsigned)(tid + TH * m);
       kip[s] = Ki[m];
-      const float gd = GmaxB + y[m] * g[m];
+      const float gd = GmaxB + yg[m];
       const float q0 = 2.f - 2.f * Ki[m];
       const float quad = q0 <= 0.f ? 1e-12f : q0;
       const unsigned ok = 0u - (unsigned)(low[m] & (gd > 0.f));
@@ -702,11 +708,11 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     const unsigned K2 = __builtin_amdgcn_readfirstlane(red4(r2));
     if (K2 == 0u) return false;
     const int j = (int)(K2 & kIdx);
-    const float Gj = glp[j];
     const float ai_old = alp[i], aj_old = alp[j];
     const float Kij = kip[j];
     const bool jpos = widx[j] < P.npos;
     const float yj = jpos ? 1.f : -1.f;
+    const float Gj = yj * glp[j];
     const float Ci = ipos ? Cpf : Cnf, Cj = jpos ? Cpf : Cnf;
     WS_STAMP(3)
     // libsvm's two-variable step and clipping, both label cases evaluated, then selected
@@ -748,7 +754,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     for (int m = 0; m < SL; ++m) {
       const int s = tid + TH * m;
       a[m] = s == i ? ai : (s == j ? aj : a[m]);
-      g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
+      yg[m] += fmaf(Ki[m], ci, Kj[m] * cj);
     }
     WS_STAMP(5)
     ++it;
@@ -839,18 +845,32 @@ static_assert(kc_lds_bytes(12) <= 163840, "the K-cached round must fit the CU's 
 
 __device__ __forceinline__ int kc_rowstart(int r) { return r * kKcQ - ((r * (r - 1)) >> 1); }
 
-template <typename T>
-__device__ __forceinline__ T sel4(const T (&v)[4], int m) {   // v[m] for a wave-uniform m
-  return m == 0 ? v[0] : (m == 1 ? v[1] : (m == 2 ? v[2] : v[3]));
+// v[m] for a wave-uniform m, branch-free: the masks are scalar values (the compiler turned the
+// ternary form into scalar branches, a fetch bubble each inside the pair loop)
+__device__ __forceinline__ unsigned sel4u(const unsigned (&v)[4], int m) {
+  const unsigned m0 = 0u - (unsigned)(m == 0), m1 = 0u - (unsigned)(m == 1);
+  const unsigned m2 = 0u - (unsigned)(m == 2), m3 = 0u - (unsigned)(m == 3);
+  return (v[0] & m0) | (v[1] & m1) | (v[2] & m2) | (v[3] & m3);
+}
+__device__ __forceinline__ float sel4(const float (&v)[4], int m) {
+  const unsigned u[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  return __uint_as_float(sel4u(u, m));
+}
+__device__ __forceinline__ int sel4(const int (&v)[4], int m) {
+  const unsigned u[4] = {(unsigned)v[0], (unsigned)v[1], (unsigned)v[2], (unsigned)v[3]};
+  return (int)sel4u(u, m);
 }
 __device__ __forceinline__ float rdlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 
-template <int M, int KS, bool kCand>
+// kStamp: in-kernel s_memtime phase totals of the pair loop into prof[b][5] (diagnostic instance,
+// HFENS_PROFILE_WS=1; the stamps wait for outstanding LDS reads, so they perturb what they measure)
+template <int M, int KS, bool kCand, bool kStamp = false>
 __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
     const WsProb* __restrict__ probs, WsState* __restrict__ states, const float* __restrict__ zcat, int F,
     const float* __restrict__ zn_all, double* __restrict__ alpha_all, const double* __restrict__ G_all,
     int* __restrict__ wsprev, float* __restrict__ wsz, float* __restrict__ wsn, float* __restrict__ wdc,
-    int Fp2, double eps, int max_outer, int max_inner, double inner_frac, WsAux X, WsCand C) {
+    int Fp2, double eps, int max_outer, int max_inner, double inner_frac, WsAux X, WsCand C,
+    long long* __restrict__ prof = nullptr) {
   constexpr int Q = kKcQ;
   constexpr int SL = Q / 64;            // slots per lane of the solving wave (slot s = 64·m + lane)
   constexpr unsigned kIdx = Q - 1;      // slot bits packed under the selection keys
@@ -913,7 +933,8 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
   double* ap = alpha_all + P.aoff;
   bool valid[SL], pos[SL];
   int tt[SL], rb[SL];
-  float y[SL], Cw[SL], a[SL], g[SL];
+  // yg = y·G and the y·α < tu / −y·α < tl membership tests: see ws_solve_kernel
+  float y[SL], Cw[SL], a[SL], yg[SL], tu[SL], tl[SL];
   double a0[SL];
 #pragma unroll
   for (int m = 0; m < SL; ++m) {
@@ -923,9 +944,11 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
     pos[m] = tt[m] < P.npos;
     y[m] = pos[m] ? 1.f : -1.f;
     Cw[m] = (float)(pos[m] ? P.Cp : P.Cn);
+    tu[m] = valid[m] ? (pos[m] ? Cw[m] : 0.f) : -INFINITY;
+    tl[m] = valid[m] ? (pos[m] ? 0.f : Cw[m]) : -INFINITY;
     a0[m] = valid[m] ? ap[tt[m]] : 0.0;
     a[m] = (float)a0[m];
-    g[m] = valid[m] ? (float)Gp[tt[m]] : 0.f;
+    yg[m] = valid[m] ? y[m] * (float)Gp[tt[m]] : 0.f;
     rb[m] = kc_rowstart(s) - s;   // K(r, s) for r > s lives at rowstart(s) + r − s
   }
   // K(r, ·) for this lane's slots (r wave-uniform): upper-triangle address of (min, max)
@@ -941,6 +964,15 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
   const float epsf = (float)eps;
   float tol_in = -1.f;
   int it = 0;
+  long long ph[5] = {0, 0, 0, 0, 0};
+  long long tp = kStamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](int k) {
+    if constexpr (kStamp) {
+      const long long tn = __builtin_amdgcn_s_memtime();
+      ph[k] += tn - tp;
+      tp = tn;
+    }
+  };
   while (it < max_inner) {
     // step 1: i = argmax_{I_up ∩ B} −y·G (slot in the key's low bits); I_low maximum for the gap
     unsigned k1 = 0u, k3 = 0u;
@@ -948,49 +980,53 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
       const unsigned s = (unsigned)(64 * m + lane);
-      const bool below = a[m] < Cw[m], above = a[m] > 0.f;
-      const bool up = valid[m] & ((pos[m] & below) | (!pos[m] & above));
-      low[m] = valid[m] & ((pos[m] & above) | (!pos[m] & below));
-      const float yg = y[m] * g[m];
+      const float ya = y[m] * a[m];
+      const bool up = ya < tu[m];
+      low[m] = -ya < tl[m];
       const unsigned um = 0u - (unsigned)up, lm = 0u - (unsigned)low[m];
-      k1 = max(k1, ((f32_okey(-yg) & ~kIdx) | s) & um);
-      k3 = max(k3, f32_okey(yg) & lm);
+      k1 = max(k1, ((f32_okey(-yg[m]) & ~kIdx) | s) & um);
+      k3 = max(k3, f32_okey(yg[m]) & lm);
     }
     const unsigned K1 = __builtin_amdgcn_readfirstlane(wave_max_u32(k1));
     const unsigned K3 = __builtin_amdgcn_readfirstlane(wave_max_u32(k3));
+    stamp(0);
     if (K1 == 0u || K3 == 0u) break;
     const int i = (int)(K1 & kIdx), mi = i >> 6, li = i & 63;
-    const float Gi = rdlane_f(sel4(g, mi), li);
+    const float ygi = rdlane_f(sel4(yg, mi), li);
     const float ai_old = rdlane_f(sel4(a, mi), li);
     const bool ipos = __builtin_amdgcn_readlane(sel4(tt, mi), li) < P.npos;
     const float yi = ipos ? 1.f : -1.f;
-    const float GmaxB = -yi * Gi;
+    const float Gi = yi * ygi;
+    const float GmaxB = -ygi;
     const float lgap = GmaxB + f32_from_okey(K3);
     if (tol_in < 0.f) tol_in = fmaxf(0.9999f * epsf, (float)inner_frac * lgap);
     if (lgap < tol_in) break;
     // step 2: j = argmax over I_low ∩ B of (GmaxB + yG)² / (2 − 2 K_it)
     float Ki[SL];
     krow(i, Ki);
+    stamp(1);
     unsigned k2 = 0u;
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
       const unsigned s = (unsigned)(64 * m + lane);
-      const float gd = GmaxB + y[m] * g[m];
+      const float gd = GmaxB + yg[m];
       const float q0 = 2.f - 2.f * Ki[m];
       const float quad = q0 <= 0.f ? 1e-12f : q0;
       const unsigned ok = 0u - (unsigned)(low[m] & (gd > 0.f));
       k2 = max(k2, ((f32_okey(gd * gd * __builtin_amdgcn_rcpf(quad)) & ~kIdx) | s) & ok);
     }
     const unsigned K2 = __builtin_amdgcn_readfirstlane(wave_max_u32(k2));
+    stamp(2);
     if (K2 == 0u) break;
     const int j = (int)(K2 & kIdx), mj = j >> 6, lj = j & 63;
     float Kj[SL];
     krow(j, Kj);   // issued before the scalar step below: its LDS latency hides under it
-    const float Gj = rdlane_f(sel4(g, mj), lj);
+    const float ygj = rdlane_f(sel4(yg, mj), lj);
     const float aj_old = rdlane_f(sel4(a, mj), lj);
     const float Kij = rdlane_f(sel4(Ki, mj), lj);
     const bool jpos = __builtin_amdgcn_readlane(sel4(tt, mj), lj) < P.npos;
     const float yj = jpos ? 1.f : -1.f;
+    const float Gj = yj * ygj;
     const float Ci = ipos ? Cpf : Cnf, Cj = jpos ? Cpf : Cnf;
     // libsvm's two-variable step and clipping (ws_solve_kernel's branch-free form)
     const float q0 = 2.f - 2.f * Kij;
@@ -1023,13 +1059,19 @@ __global__ __launch_bounds__(kWsThreads) void ws_kc_round_kernel(
     const bool opp = ipos != jpos;
     const float ai = opp ? ao : as, aj = opp ? bo : bs;
     const float ci = yi * (ai - ai_old), cj = yj * (aj - aj_old);
+    stamp(3);
 #pragma unroll
     for (int m = 0; m < SL; ++m) {
       const int s = 64 * m + lane;
       a[m] = s == i ? ai : (s == j ? aj : a[m]);
-      g[m] += y[m] * fmaf(Ki[m], ci, Kj[m] * cj);
+      yg[m] += fmaf(Ki[m], ci, Kj[m] * cj);
     }
+    stamp(4);
     ++it;
+  }
+  if constexpr (kStamp) {
+    if (lane == 0)
+      for (int k = 0; k < 5; ++k) prof[(size_t)b * 6 + k] += ph[k];
   }
   // ---- publish: α of B, changed entries (slot order) for the global gradient update
   int nc = 0;
@@ -1310,7 +1352,7 @@ void ws_kc_cand_len(long long max_l, uintptr_t out) { *reinterpret_cast<long lon
 void ws_steps_kc(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
                  uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
                  uintptr_t keys, long long n, uintptr_t gkey, uintptr_t cand, double eps, int max_outer,
-                 int max_inner, double inner_frac, int n_iter, uintptr_t stream) {
+                 int max_inner, double inner_frac, int n_iter, uintptr_t prof, uintptr_t stream) {
   const WsAux X = ws_aux(keys, n, gkey);
   HFENS_REQUIRE(F >= 1 && F <= 24, "ws_steps_kc: 1 <= F <= 24");
   const long long ncand = ws_kc_ncand(max_l);
@@ -1345,6 +1387,11 @@ void ws_steps_kc(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintp
       hipLaunchKernelGGL((ws_cand_kernel<kKcQ>), cgrid, dim3(kWsThreads), 0, st, pp, sp, X, C);
       launch_check();
     }
+    if (prof && M == 16 && KS == 9 && ncand == 0) {   // diagnostic instance (the bench's shape)
+      hipLaunchKernelGGL((ws_kc_round_kernel<16, 9, false, true>), dim3(P), dim3(kWsThreads), kc_lds_bytes(9), st,
+                         pp, sp, zp, F, np_, ap, gp, wp, wz, wn, wd, Fp2, eps, max_outer, max_inner, inner_frac, X, C,
+                         (long long*)prof);
+    } else
 #define KC_ROUND(MM, KK, CC)                                                                                     \
   if (M == MM && KS == KK && (ncand != 0) == CC) {                                                               \
     hipLaunchKernelGGL((ws_kc_round_kernel<MM, KK, CC>), dim3(P), dim3(kWsThreads), kc_lds_bytes(KK), st, pp, sp, \

@@ -30,7 +30,7 @@ def launch_svc_batch_distributed(svcs, Zs, ys, group) -> dict:
     ranks issue them in one order on one communicator."""
     sizes = pdist.all_reduce_sum_f64([torch.tensor([float(y.numel()) for y in ys], dtype=torch.float64,
                                                    device=pdist._default_device(group))], group)[0]
-    if use_lowrank([int(v) for v in sizes.tolist()]):
+    if use_lowrank([int(v) for v in sizes.tolist()], int(Zs[0].shape[1]), Zs[0].device.type):
         from ..models import smo
         from ..models.svc_lowrank import fit_svc_lowrank_batch
         smo.LAST_SMO_INFO.clear()

@@ -33,7 +33,8 @@ for k in np.argsort(-st["inner"])[:4]:
           f"({st['cyc_inner'][k] / clk / 1e3:.2f} ms)")
 ph = st.get("phases")
 if ph is not None:
-    names = ["keys", "barrier1+i", "row_i", "barrier2+j", "pair", "row_j+grad"]
+    names = (["keys+i max", "fetch i+row_i", "j keys+max", "fetch j+row_j+step", "update", "-"]
+             if st.get("q") == 256 else ["keys", "barrier1+i", "row_i", "barrier2+j", "pair", "row_j+grad"])
     k = int(np.argmax(st["inner"]))
     tot = ph[k].sum()
     print("phases of problem", k, "(cycles/pair):",

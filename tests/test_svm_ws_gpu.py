@@ -27,10 +27,14 @@ def _dual(Z, y_pm, coef_sv, sv_idx, gamma):
     return 0.5 * coef_sv @ K @ coef_sv - a.sum()
 
 
-@pytest.mark.parametrize("n,F", [(1500, 17), (6000, 17), (4000, 40)])
-def test_ws_solver_matches_libsvm(dev, monkeypatch, n, F):
+@pytest.mark.parametrize("n,F,kc", [(1500, 17, "auto"), (6000, 17, "auto"), (4000, 40, "auto"), (6000, 17, "1"),
+                                    (3000, 24, "1")])
+def test_ws_solver_matches_libsvm(dev, monkeypatch, n, F, kc):
+    """kc = "1": the K-cached q = 256 rounds (svm_ws.hip ws_kc_round_kernel) forced on a problem the
+    q = 1024 solver would take."""
     from sklearn.svm import SVC as SK
     monkeypatch.setattr(smo, "SOLVER", "ws")
+    monkeypatch.setattr(smo, "WS_KC", kc)
     X, y = _data(n, F, n + F)
     Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).numpy()
     sk = SK(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.numpy())
@@ -72,9 +76,9 @@ def test_ws_bench_scale_meets_libsvm_tolerance(dev, monkeypatch):
     m = SVC(class_weight="balanced", random_state=2020)
     m.fit(torch.as_tensor(Z).to(dev), y.to(dev))
     st = smo.LAST_WS_STATS
-    assert smo.LAST_SMO_INFO["solver"] == "ws" and st["q"] == smo.ws_q(17)
+    assert smo.LAST_SMO_INFO["solver"] == "ws" and st["q"] == smo.ws_q(17, 10000)
     assert (st["gap"] < 1e-3).all(), st["gap"]
-    assert int(st["outer"].max()) <= (400 if smo.ws_kc(17) else 120), st["outer"]
+    assert int(st["outer"].max()) <= (400 if smo.ws_kc(17, 10000) else 120), st["outer"]
     sk = SK(class_weight="balanced", random_state=2020).fit(Z, y.numpy())
     gamma = 1.0 / (17 * Z.var())
     ours = _dual(Z, None, m._dual_coef_[0].cpu().numpy(), m.support_.cpu().numpy(), gamma)
