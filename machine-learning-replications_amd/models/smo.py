@@ -1081,10 +1081,11 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
 # GPU: the working-set SMO needs O(n) memory (no Gram), and its candidate-list selection handles any
 # size, so "auto" keeps every problem exact up to EXACT_MAX_POINTS — the measured crossover
 # (scripts/probes/svc_crossover.py, profiles/r4_svc_crossover.md: one probability fit, exact vs
-# Nyström 0.17 vs 1.56 s at 40k rows, 0.81 vs 1.55 s at 100k); features past the K-cached kernel's
+# Nyström 0.17 vs 1.56 s at 40k rows, 0.81 vs 1.55 s at 100k, 3.05 vs 1.94 s at 200k, 6.98 vs
+# 2.04 s at 300k: exact time grows as l^1.9, so the two cross near 150k); features past the K-cached kernel's
 # range (F > 24) keep the one-workgroup selector's 32,768-point limit.  Host (CPU): the exact solver
 # stores every problem's Gram, so it stays below EXACT_HOST_MAX points and GRAM_BUDGET bytes.
-EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "200000"))
+EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "150000"))
 EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 

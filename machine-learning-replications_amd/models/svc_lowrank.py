@@ -101,8 +101,11 @@ NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
 # f32, f32 accumulation over ≤ 256 rows, f64 beyond): the interior point's Newton systems then use
 # an S accurate to ~1e-7 relative while every residual, step and stopping test stays f64 (an
 # inexact-Newton interior point; the directions' accuracy only affects the iteration count).
-# "f64": the library block-upper f64 path.
-GRAM = os.environ.get("HFENS_IPM_GRAM", "f32")
+# Measured at 1M × 512 (profiles/r4_svc_crossover.md): 80 iterations at 15.8 ms against the f64
+# path's 36 at 13.6 ms — late in the solve D⁻¹ spans many decades and the ~1e-7 error in S costs
+# more Newton steps than the cheaper product saves (the Gram is not the per-iteration bottleneck)
+# — so "f64", the library block-upper f64 path, is the default and "f32" is opt-in.
+GRAM = os.environ.get("HFENS_IPM_GRAM", "f64")
 SYRK_BLOCK = int(os.environ.get("HFENS_SYRK_BLOCK", "128"))   # library path: block-upper product (0: full)
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
