@@ -17,6 +17,9 @@ import torch
 from .base import Estimator, as_tensor
 
 SLOTS = 8
+# f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
+EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
+KNN_CAND = 32   # knn.hip kKnnCand
 
 
 def _masks_u64(miss: torch.Tensor) -> torch.Tensor:
@@ -84,8 +87,16 @@ class KNNImputer(Estimator):
             center = self._col_mean  # centring improves f32 accuracy; distances are shift-invariant
             D32 = (D - center).where(~self._mask_fit, torch.zeros_like(D)).to(torch.float32).contiguous()
             dm = _masks_u64(self._mask_fit).contiguous()
-            pr = self._prep = (self._fit_X, D32, dm)
+            # the f64 refine's operands: raw values zero-filled (the host mirror's arithmetic) and the
+            # largest centred magnitude (its error window), both left on the device
+            D64 = D.to(torch.float64).contiguous()
+            dmax = D32.abs().amax().reshape(1) if D32.numel() else torch.zeros(1, device=D.device)
+            pr = self._prep = (self._fit_X, D32, dm, D64, dmax)
         return pr[1], pr[2]
+
+    def _fit_prep64(self):
+        self._fit_prep()
+        return self._prep[3], self._prep[4]
 
     def _impute_device_many(self, Xs, streams, defer=False):
         """The (row, column) work lists are built with numpy from the bitmasks and uploaded
@@ -178,11 +189,23 @@ class KNNImputer(Estimator):
         R32 = torch.where(Rm, torch.zeros_like(Xr), Xr - center).to(torch.float32).contiguous()
         rm = rm.contiguous()
         best = torch.empty(nr, nslot, dtype=torch.int64, device=dev)
+        alt = torch.empty(nr, SLOTS, dtype=torch.int32, device=dev)
+        if EXACT:
+            D64, dmax = self._fit_prep64()
+            R64 = torch.where(Rm, torch.zeros_like(Xr), Xr).to(torch.float64).contiguous()
+            Mx = torch.maximum(dmax, R32.abs().amax().reshape(1)).to(torch.float32).contiguous()
+            work = torch.empty((4 + nr * (1 + 2 * SLOTS + SLOTS * KNN_CAND)), dtype=torch.int32, device=dev)
         for s0 in range(0, nslot, SLOTS):
             slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
             blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)
             E.knn_donors(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(),
-                         D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), ops.stream_ptr(dev))
+                         D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), ops.stream_ptr(dev))
+            if EXACT:
+                # slots whose runner-up is within the f32 error of the best: re-decided in f64
+                # (knn.hip knn_refine) — the donors then equal the host mirror's f64 choice
+                E.knn_refine(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(), D32.shape[0], F,
+                             slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
+                             Mx.data_ptr(), work.data_ptr(), ops.stream_ptr(dev))
             if nslot != SLOTS:
                 best[:, s0:s0 + SLOTS] = blk
         hmark("imp_knn_launched")
@@ -206,9 +229,14 @@ class KNNImputer(Estimator):
             mr = torch.isnan(R)
             Rz = torch.where(mr, torch.zeros_like(R), R)
             pres_r = (~mr).to(torch.float64)
-            # Σ_common (x−y)², direct differences in f64 (exact ties stay ties)
+            # Σ_common (x−y)², direct differences in f64 summed in feature order (exact ties stay
+            # ties; the device's f64 refine, knn.hip knn_dist64, does the same operations)
             both = pres_r[:, None, :] * pres_f[None, :, :]
-            d2 = (both * (Rz[:, None, :] - D[None, :, :]) ** 2).sum(-1)
+            diff = Rz[:, None, :] - D[None, :, :]
+            sq = both * (diff * diff)
+            d2 = sq[..., 0].clone()
+            for f in range(1, F):
+                d2 = d2 + sq[..., f]
             common = both.sum(-1)
             dist = torch.where(common > 0, d2 * F / common.clamp(min=1),
                                torch.full_like(d2, float("inf")))

@@ -401,12 +401,16 @@ def ws_kc(F: int, max_l: int = 0) -> bool:
     return WS_KC == "1" or max_l > WS_KC_DIRECT_MAX
 
 
+# working-set size of the recomputing solver for F ≤ 24 (512: half the slots per pair, more rounds)
+WS_Q = int(os.environ.get("HFENS_SVM_WS_Q", "1024"))
+
+
 def ws_q(F: int, max_l: int = 0) -> int:
     """Working-set size of svm_ws.hip for F features (K-cached: 256; else one slot per thread with
     z_B in LDS: 1024 / 512)."""
     if ws_kc(F, max_l):
         return WS_KC_Q
-    return 1024 if F <= 24 else 512
+    return WS_Q if (F <= 24 and WS_Q in (512, 1024)) else 1024 if F <= 24 else 512
 
 
 def _ws_ks(F: int) -> int:
@@ -638,12 +642,12 @@ WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
-WS_GRAPH = os.environ.get("HFENS_SVM_WS_GRAPH", "1") != "0"
+# HIP-graph replay of the rounds: "1" K-cached rounds only, "all" the q = 1024 rounds too, "0" off
+WS_GRAPH = os.environ.get("HFENS_SVM_WS_GRAPH", "1")
 WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # rounds per captured graph
 _WS_GRAPHS: dict = {}
 WS_BIG_CHUNK = int(os.environ.get("HFENS_SVM_WS_BIG_CHUNK", "64"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
-_WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
 # Lock-step decoupling: one round kernel ends when its SLOWEST problem's inner solve does, so the
@@ -654,7 +658,9 @@ _WS_SYNC = [False]   # set while re-solving a batch that did not converge within
 # lock-step only within itself.  WS_GROUPS = 1: one group.
 WS_SPLIT_FRAC = float(os.environ.get("HFENS_SVM_WS_SPLIT", "0.95"))
 WS_GROUPS = int(os.environ.get("HFENS_SVM_WS_GROUPS", "3"))
-_WS_ENQ_CHUNK = 4   # rounds per group per host enqueue turn
+WS_EVENTS = os.environ.get("HFENS_WS_EVENTS", "0") == "1"
+LAST_WS_EVENTS: dict = {}
+_WS_ENQ_CHUNK = int(os.environ.get("HFENS_SVM_WS_ENQ_CHUNK", "4"))   # rounds per group per host enqueue turn
 
 
 def _ws_groups(live, device) -> List[List[int]]:
@@ -695,7 +701,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     # captured once (WS_GRAPH_CHUNK rounds per graph) and replayed.  Every argument of a captured
     # launch must be the same buffer at every replay: the per-point arrays, the features and every
     # per-group buffer are process-lifetime workspaces (runtime.workspace), re-filled per fit.
-    use_graph = (WS_GRAPH and cuda and kc_all and not sync and not PROFILE_WS
+    use_graph = (WS_GRAPH != "0" and cuda and (kc_all or WS_GRAPH == "all") and not sync and not PROFILE_WS
                  and caller.cuda_stream != torch.cuda.default_stream(device).cuda_stream)
     # per-point arrays (indexed by each problem's absolute offset) are shared by the groups
     if use_graph:
@@ -728,6 +734,20 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
                               side, zn, alpha, G, keys, hist, n, Q, Fp2, kc_all, gi=gi if use_graph else None,
                               cap_stream=(side if side is not None else caller) if use_graph else None))
+    from ..utils.timing import hmark
+    hmark("ws_groups_ready")
+    # HFENS_WS_EVENTS=1 (diagnostic): device events per group after every enqueued chunk, read by
+    # scripts/probes/ws_events.py (event time − the batch's start event, no profiler attached)
+    evs = None
+    if WS_EVENTS and cuda:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(caller)
+        evs = dict(start=ev0, rounds=[[] for _ in runs])
+
+        def _mark(gi, r):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(r["side"] if r["side"] is not None else caller)
+            evs["rounds"][gi].append(e)
     if sync:
         runs[0]["sync_rounds"](steps_per_check)
     else:
@@ -740,11 +760,19 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
         while left > 0:
             k = min(chunk, left)
-            for r in runs:
+            for gi, r in enumerate(runs):
                 r["steps"](k)
+                if evs is not None:
+                    _mark(gi, r)
             left -= k
-    for r in runs:
+            hmark("ws_chunk")
+    for gi, r in enumerate(runs):
         r["finish"]()
+        if evs is not None:
+            _mark(gi, r)
+    if evs is not None:
+        LAST_WS_EVENTS.clear()
+        LAST_WS_EVENTS.update(evs, chunk=chunk if not sync else None)
     for r in runs:
         if r["side"] is not None:
             caller.wait_stream(r["side"])
@@ -870,7 +898,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
                    wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
-                   k, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, s)
+                   k, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, Q, s)
 
     def sync_rounds(steps_per_check):
         outer = 0
@@ -1006,15 +1034,18 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     for k, p in enumerate(live):
         a0 = aoffs_start[k]
         out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
+    # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
+    # for the held-out decisions below and the stacking trainer's device OOF (enqueue_svc_oof)
+    sign = torch.empty(aoffs[-1], dtype=torch.float32, device=device)
+    for k, p in enumerate(live):
+        a0, l = aoffs_start[k], p.l
+        sign[a0:a0 + p.npos] = 1.0
+        sign[a0 + p.npos:a0 + l] = -1.0
+    coef = (sign * alpha.to(torch.float32)).contiguous()
+    out["_dec"] = dict(zcat=zcat, coef=coef, F=F, zoff={id(p): zoffs[k] for k, p in enumerate(live)})
     # ---- Platt held-out decision values of every CV sub-model: one batched launch
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
     if platt:
-        sign = torch.empty(aoffs[-1], dtype=torch.float32, device=device)
-        for k, p in enumerate(live):
-            a0, l = aoffs_start[k], p.l
-            sign[a0:a0 + p.npos] = 1.0
-            sign[a0 + p.npos:a0 + l] = -1.0
-        coef = (sign * alpha.to(torch.float32)).contiguous()
         hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
         per = 1024
         S = (max_l + per - 1) // per
@@ -1259,6 +1290,58 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
                 device=device, args=args, solver=solver)
 
 
+def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
+    """Out-of-fold P(class 1) of fits launched by :func:`launch_svc_batch`, enqueued on the current
+    stream behind their SMO and Platt kernels with no host synchronisation: ``items`` = [(fit f,
+    scaled rows Zt [h, F] on the device, their row indices in ``meta`` (int64, device))]; fit f's
+    final model's probability of each row is written to ``meta[rows, col]`` (one batched decision
+    launch + one sigmoid/coupling launch).  Returns False when the batch has no device decision
+    state (host solve, low-rank path, a degenerate problem): the caller then predicts as usual.
+    Stale if :func:`finish_svc_batch` re-solves the batch (``st["resolved"]``)."""
+    from .. import ops
+    sol = st.get("sol")
+    if st.get("done") or st.get("ABt") is None or sol is None or "_dec" not in sol or not items:
+        return False
+    dec_state, all_probs, pl, device = sol["_dec"], st["all_probs"], st["pl"], st["device"]
+    finals = []
+    for f, Zt, _ in items:
+        p = [q for q in all_probs if q.fit == f and q.fold < 0][0]
+        if p.rows is None or f not in pl or int(Zt.shape[1]) != dec_state["F"]:
+            return False
+        finals.append(p)
+    E = ops.ext()
+    s = ops.stream_ptr(device)
+    per = 1024
+    max_l = max(p.l for p in finals)
+    S = (max_l + per - 1) // per
+    dt = np.zeros(len(items), _DEC_DT)
+    hoff = 0
+    hs = []
+    for i, ((f, Zt, _), p) in enumerate(zip(items, finals)):
+        h = int(Zt.shape[0])
+        dt[i] = (dec_state["zoff"][id(p)], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
+        hoff += h
+        hs.append(h)
+    hcat = torch.cat([Zt.to(torch.float32) for _, Zt, _ in items]).contiguous()
+    part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
+    ddev = _dev_struct(dt, device)
+    E.svm_dec_batch(dec_state["zcat"].data_ptr(), dec_state["coef"].data_ptr(), hcat.data_ptr(), dec_state["F"],
+                    ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(), s)
+    dec = part.to(torch.float64).sum(1).contiguous()
+    model = torch.repeat_interleave(torch.arange(len(items), dtype=torch.int32),
+                                    torch.as_tensor(hs, dtype=torch.int64))
+    model = _to_dev(model.numpy(), device)
+    rho = torch.stack([st["sol"][id(p)][1].reshape(()).to(torch.float64) for p in finals]).contiguous()
+    sel = _to_dev(np.array([pl.index(f) for f, _, _ in items], dtype=np.int64), device)
+    AB = st["ABt"].view(-1, 2).index_select(0, sel).reshape(-1).contiguous()
+    rows = torch.cat([r.to(torch.int64) for _, _, r in items]).contiguous()
+    assert meta.dtype == torch.float64 and meta.is_contiguous() and meta.dim() == 2
+    E.svc_oof(dec.data_ptr(), model.data_ptr(), rho.data_ptr(), AB.data_ptr(), rows.data_ptr(), meta.data_ptr(),
+              int(meta.shape[1]), int(col), hoff, s)
+    st["oof_keep"] = (hcat, part, ddev, dec, model, rho, sel, AB, rows)
+    return True
+
+
 def finish_svc_batch(st: dict):
     """Platt parameters to the host, support-vector extraction, ``set_fitted``."""
     if st.get("done"):
@@ -1280,6 +1363,7 @@ def finish_svc_batch(st: dict):
                       "cooperative SMO timed out waiting for a member; re-solving with one workgroup per problem")
         flag = _WS_SYNC if ws else _FORCE_SINGLE
         flag[0] = True
+        st["resolved"] = True   # (anything enqueued from the first solution, e.g. a device OOF, is stale)
         try:
             st2 = launch_svc_batch(*st["args"])
         finally:
@@ -1297,6 +1381,8 @@ def finish_svc_batch(st: dict):
                       torch.stack([torch.as_tensor(it).to(device=device, dtype=torch.float64).reshape(()) for _, _, it in sols])]
                      + ([st["ABt"].to(device=device, dtype=torch.float64)] if st["ABt"] is not None else [])
                      ).cpu().numpy()
+    from ..utils.timing import hmark
+    hmark("svc_host_read")
     nl = sum(ls)
     if st["ABt"] is not None:
         ABc = host[nl + 2 * len(svcs):]
@@ -1322,4 +1408,5 @@ def finish_svc_batch(st: dict):
                        class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
                        shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
         svc.n_iter_ = int(host[nl + len(svcs) + f])
+    hmark("svc_set_fitted")
     return svcs

@@ -43,6 +43,9 @@ from .svc import SVC
 N_FOLDS = 5
 _TRACE_HOST = os.environ.get("HFENS_TRACE_HOST", "0") == "1"
 CONCURRENT_BASES = os.environ.get("HFENS_CONCURRENT_BASES", "1") != "0"
+# the SVC's out-of-fold column computed on the device behind the SMO (smo.enqueue_svc_oof) instead
+# of by the fold models' predict_proba after their host bookkeeping
+DEVICE_SVC_OOF = os.environ.get("HFENS_DEVICE_SVC_OOF", "1") != "0"
 
 
 def _kind(est):
@@ -190,7 +193,7 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
 
 
 def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
-                          svc_pre=None):
+                          svc_pre=None, oof_svc_dev=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -226,6 +229,10 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                     yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
                     pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh,
                                                            plan=(svc_pre or {}).get(i)))
+                    if oof_svc_dev is not None and svc_group is None:
+                        # the OOF column straight from the device solution, behind the SMO on this
+                        # stream: no wait for the fitted models' host bookkeeping
+                        pending[i][1]["oof_dev"] = oof_svc_dev(i, clones, pending[i][1])
                 else:
                     pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
                 hmark("svc_launched")
@@ -254,7 +261,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                 else:
                     finish_svc_batch_distributed(st, group)
                 out[i] = clones
-                if oof is not None:
+                if oof is not None and not (st.get("oof_dev") and not st.get("resolved")):
                     oof(i, clones)
         hmark("svc_finished")
         main.wait_stream(side)
@@ -296,7 +303,16 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre)
+    def oof_svc_dev(col, fitted, st):
+        if not (DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])):
+            return False
+        from .smo import enqueue_svc_oof
+        items = [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
+                 for k in range(N_FOLDS) if test_idx[k].numel()]
+        return enqueue_svc_oof(st, items, meta, col)
+
+    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre,
+                                       oof_svc_dev if group is None else None)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream

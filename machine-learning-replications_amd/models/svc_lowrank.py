@@ -264,8 +264,23 @@ class _Red:
     are the same bits on every rank, so the r × r factor and every step length agree exactly.
     ``group=None``: the identity (one process)."""
 
+    # peer-memory path (parallel/xgmi.py, HFENS_XGMI=try / 1 with ranks on one node): each reduction
+    # is ONE f64 kernel folding the ranks' values in rank order — deterministic for a fixed world,
+    # no RCCL call inside the iteration; its payloads go up to the r × r Gram
+    PEER_CAP = 512 * 512 + 4096
+    STATS = {"rccl": 0, "peer": 0}
+
     def __init__(self, group):
         self.g = group
+        self._peer = None if group is not None else False
+
+    def _peer_for(self, t):
+        if self._peer is None:
+            self._peer = False
+            if t.is_cuda:
+                from ..parallel import xgmi
+                self._peer = xgmi.peer_comm(self.g, t.device, self.PEER_CAP, tag="ipm") or False
+        return self._peer
 
     def _ar(self, t, op):
         if self.g is None:
@@ -273,8 +288,19 @@ class _Red:
         import torch.distributed as dist
         shape = t.shape
         buf = t.reshape(-1).contiguous().clone()
-        dist.all_reduce(buf, op=op, group=self.g)
+        peer = self._peer_for(buf)
+        if peer and buf.dtype == torch.float64 and buf.numel() <= peer.cap:
+            peer.reduce_f64_(buf, {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MAX: "max", dist.ReduceOp.MIN: "min"}[op])
+            _Red.STATS["peer"] += 1
+        else:
+            dist.all_reduce(buf, op=op, group=self.g)
+            _Red.STATS["rccl"] += 1
         return buf.reshape(shape)
+
+    def check(self):
+        """Collective: raise on every rank if any peer wait timed out (after a solve)."""
+        if self._peer:
+            self._peer.check()
 
     def sum(self, t):
         import torch.distributed as dist
@@ -532,6 +558,7 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     # gap); ρ = −b: stationarity gives y_i G_i = −b on every free point, which is libsvm's ρ
     a = torch.where(a < 1e-9 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-9), c, a))
     rho = -b
+    red.check()
     return a, float(rho), it
 
 
@@ -557,6 +584,11 @@ def _threads_safe(group) -> bool:
     if group is None:
         return True
     import torch.distributed as dist
+    from ..parallel import xgmi
+    if xgmi.MODE in ("try", "1"):
+        # peer-memory reductions spin on the device until every rank's kernel arrives: two threads'
+        # kernels queued in opposite orders on two ranks' in-order queues would wait on each other
+        return False
     return dist.get_backend(group) == "gloo"
 
 

@@ -175,6 +175,34 @@ void svc_proba1(uintptr_t dec, uintptr_t out, int n, double A, double B, uintptr
   launch_check();
 }
 
+// Out-of-fold P(class 1) of several SVC models straight from their decision sums, on the device:
+// row i (model k = model[i]) gets meta[rows[i]·ld + col] = proba(f32(dec[i] − rho[k]); A_k, B_k) with
+// (A_k, B_k) = AB[2k], AB[2k+1] as the Platt kernel left them — the stacking trainer's OOF column
+// without reading the fitted models back to the host (predict_proba's precision: f32 decision,
+// f64 sigmoid + coupling, f32 result).
+__global__ void svc_oof_kernel(const double* __restrict__ dec, const int* __restrict__ model,
+                               const double* __restrict__ rho, const double* __restrict__ AB,
+                               const long long* __restrict__ rows, double* __restrict__ meta, int ld, int col,
+                               int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int k = model[i];
+    const float d = (float)(dec[i] - rho[k]);
+    meta[rows[i] * ld + col] = (double)(float)platt_couple_p1((double)d, AB[2 * k], AB[2 * k + 1]);
+  }
+}
+
+void svc_oof(uintptr_t dec, uintptr_t model, uintptr_t rho, uintptr_t AB, uintptr_t rows, uintptr_t meta, int ld,
+             int col, int n, uintptr_t stream) {
+  if (n == 0) return;
+  int grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(svc_oof_kernel, dim3(grid), dim3(256), 0, as_stream(stream), reinterpret_cast<const double*>(dec),
+                     reinterpret_cast<const int*>(model), reinterpret_cast<const double*>(rho),
+                     reinterpret_cast<const double*>(AB), reinterpret_cast<const long long*>(rows),
+                     reinterpret_cast<double*>(meta), ld, col, n);
+  launch_check();
+}
+
 // ------------------------------------------------------------------------------------------
 // Generic forest walk.  nodes: int4 {feature, left, right, float_as_int(thr32)} [T*K];
 // values float [T*K] (unshrunk leaf values).  One thread per row; the row tile lives in LDS

@@ -20,12 +20,33 @@ namespace hfens {
 constexpr int kKnnTile = 256;
 constexpr int kKnnSlots = 8;
 
+// Merge of one donor split's per-slot results: the best as (f32 distance bits, donor) by 64-bit
+// atomicMin, and alt = the smallest distance of any OTHER donor (the f64 refine's ambiguity test):
+// the loser of every best exchange (this split's key, or the key it displaced) and this split's own
+// runner-up go to alt — every non-winning split best ends there exactly once, whatever the order.
+__device__ __forceinline__ void knn_merge_slots(unsigned long long* best, unsigned* alt, int r,
+                                                const float (&bd)[kKnnSlots], const float (&b2)[kKnnSlots],
+                                                const int (&bi)[kKnnSlots]) {
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k) {
+    if (bi[k] < 0) continue;
+    const size_t e = (size_t)r * kKnnSlots + k;
+    const unsigned long long key =
+        ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned long long)(unsigned)bi[k];
+    const unsigned long long old = atomicMin(&best[e], key);
+    const unsigned long long loser = old < key ? key : old;
+    if (loser != ~0ull) atomicMin(&alt[e], (unsigned)(loser >> 32));
+    if (b2[k] < INFINITY) atomicMin(&alt[e], __float_as_uint(b2[k]));
+  }
+}
+
 template <int FMAX>
 __global__ __launch_bounds__(256) void knn_donor_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
     int per_split, const int* __restrict__ slot_col /*[nr][kKnnSlots] column or −1*/,
-    unsigned long long* __restrict__ best /*[nr][kKnnSlots] packed (dist bits, idx)*/) {
+    unsigned long long* __restrict__ best /*[nr][kKnnSlots] packed (dist bits, idx)*/,
+    unsigned* __restrict__ alt /*[nr][kKnnSlots] f32 bits of the runner-up distance*/) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ds = sm;                                                        // [256][LD] donor tile
@@ -39,13 +60,14 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
   for (int f = 0; f < LD; ++f) xr[f] = (active && f < F) ? R[(size_t)r * F + f] : 0.f;
   const unsigned long long mr = active ? rmask[r] : 0ull;
   int col[kKnnSlots];
-  float bd[kKnnSlots];
+  float bd[kKnnSlots], b2[kKnnSlots];   // best and runner-up distance per slot
   int bi[kKnnSlots];
   bool any = false;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k) {
     col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
     bd[k] = INFINITY;
+    b2[k] = INFINITY;
     bi[k] = -1;
     any |= col[k] >= 0;
   }
@@ -101,22 +123,20 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
       float m = 0.f;
 #pragma unroll
       for (int k = 0; k < kKnnSlots; ++k) {
-        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < bd[k]) { bd[k] = dist; bi[k] = di; }
-        if (col[k] >= 0) m = fmaxf(m, bd[k]);
+        // strict best (ties: the lower donor index, met first) and the runner-up (a tie with the
+        // best lands there): a donor at or past every slot's runner-up changes nothing
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < b2[k]) {
+          const bool nb = dist < bd[k];
+          b2[k] = nb ? bd[k] : dist;
+          bi[k] = nb ? di : bi[k];
+          bd[k] = nb ? dist : bd[k];
+        }
+        if (col[k] >= 0) m = fmaxf(m, b2[k]);
       }
       bmax = m;
     }
   }
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < kKnnSlots; ++k) {
-      if (bi[k] >= 0) {
-        const unsigned long long key =
-            ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned long long)(unsigned)bi[k];
-        atomicMin(&best[(size_t)r * kKnnSlots + k], key);
-      }
-    }
-  }
+  if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
 }
 
 // The same search with a packed-FMA fast pass in front of the exact distance.
@@ -160,7 +180,8 @@ template <int FMAX, bool SM>
 __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
-    int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best) {
+    int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best,
+    unsigned* __restrict__ alt) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
   constexpr bool XS = knn_fast_xs<FMAX>();
   constexpr int TILE = knn_fast_tile<FMAX>();
@@ -189,13 +210,14 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     }
   }
   int col[kKnnSlots];
-  float bd[kKnnSlots];
+  float bd[kKnnSlots], b2[kKnnSlots];   // best and runner-up distance per slot
   int bi[kKnnSlots];
   bool any = false;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k) {
     col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
     bd[k] = INFINITY;
+    b2[k] = INFINITY;
     bi[k] = -1;
     any |= col[k] >= 0;
   }
@@ -312,8 +334,15 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
       float m = 0.f;
 #pragma unroll
       for (int k = 0; k < kKnnSlots; ++k) {
-        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < bd[k]) { bd[k] = dist; bi[k] = di; }
-        if (col[k] >= 0) m = fmaxf(m, bd[k]);
+        // strict best (ties: the lower donor index, met first) and the runner-up (a tie with the
+        // best lands there): a donor at or past every slot's runner-up changes nothing
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < b2[k]) {
+          const bool nb = dist < bd[k];
+          b2[k] = nb ? bd[k] : dist;
+          bi[k] = nb ? di : bi[k];
+          bd[k] = nb ? dist : bd[k];
+        }
+        if (col[k] >= 0) m = fmaxf(m, b2[k]);
       }
       bmax = m;
     };
@@ -343,24 +372,16 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
       if (t1 != t) donor(t1, accB.x + accB.y);
     }
   }
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < kKnnSlots; ++k) {
-      if (bi[k] >= 0) {
-        const unsigned long long key =
-            ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned long long)(unsigned)bi[k];
-        atomicMin(&best[(size_t)r * kKnnSlots + k], key);
-      }
-    }
-  }
+  if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
 }
 
 void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
-                uintptr_t slot_col, uintptr_t best, uintptr_t stream) {
+                uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_donors: 1 <= F <= 64 (64-bit missing masks)");
   if (nr == 0 || nd == 0) return;
   hipStream_t st = as_stream(stream);
   HFENS_CHECK(hipMemsetAsync((void*)best, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned long long), st));
+  HFENS_CHECK(hipMemsetAsync((void*)alt, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned), st));
   const int rb = (nr + 255) / 256;
   // enough splits for ≥ 2048 workgroups, and donor ranges of ≤ 16k rows per workgroup: a
   // workgroup then runs for milliseconds, not the whole search, so kernels of other streams (the
@@ -389,17 +410,17 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
       hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best);
+                         (unsigned long long*)best, (unsigned*)alt);
     else if (F == LD && !lds_tiles && (D & 15) == 0)
       hipLaunchKernelGGL((knn_donor_fast_kernel<FM, true>), dim3(rb, nsp), dim3(256), knn_fast_lds_sm<FM>(), st,
                          (const float*)R, (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best);
+                         (unsigned long long*)best, (unsigned*)alt);
     else
       hipLaunchKernelGGL((knn_donor_fast_kernel<FM, false>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best);
+                         (unsigned long long*)best, (unsigned*)alt);
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
@@ -408,5 +429,240 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   else if (F <= 48) go(std::integral_constant<int, 48>{});
   else go(std::integral_constant<int, 64>{});
 }
+
+
+// ---- f64-exact donors: the f32 search above picks the same donor as the f64
+// direct-difference mirror (models/imputer.py _impute_host: Σ over common features in feature
+// order of fl((x−y)·(x−y)) in f64, × F / |common|, lowest index on ties) except where another
+// donor's distance is within the f32 error of the best.  Those slots are found from the runner-up
+// distance (alt) and re-decided in f64 over the donors whose f32 distance can reach the best:
+//   knn_ambig   : per (receiver, slot): ambiguous ⇔ alt ≤ d1 + W(d1) with W a generous bound of the
+//                 f32 distance error (both distances' errors: 2^-12 relative, plus an absolute term
+//                 for near-duplicate rows scaled by the largest centred magnitude Mx); compacts the
+//                 ambiguous receivers and records each ambiguous slot's f32 threshold;
+//   knn_cand    : the f32 direct-difference scan again, over the ambiguous receivers only (grid
+//                 sized for every receiver, blocks past the device count exit at once), appending
+//                 each donor within its slot's threshold to the slot's candidate list (≤ kKnnCand;
+//                 an overflowing slot is re-scanned over every donor in f64);
+//   knn_resolve : one wave per ambiguous slot: f64 distances of its candidates, (distance, index)
+//                 minimum, written back as the slot's donor.
+// The result does not depend on atomic arrival order (candidates are evaluated as a set).
+constexpr int kKnnCand = 32;
+
+__global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long* __restrict__ best,
+                                                        const unsigned* __restrict__ alt,
+                                                        const int* __restrict__ slot_col, int nr, int F,
+                                                        const float* __restrict__ Mx, float* __restrict__ thr,
+                                                        int* __restrict__ rlist, int* __restrict__ counts) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= nr) return;
+  const float M = 2.f * Mx[0], Ff = (float)F;
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k) {
+    const size_t e = (size_t)r * kKnnSlots + k;
+    float t = -1.f;
+    const unsigned long long b = best[e];
+    if (slot_col[e] >= 0 && b != ~0ull) {
+      const float d1 = __uint_as_float((unsigned)(b >> 32));
+      // error of a scaled f32 distance: relative (≤ (F + 8)·2^-24 for positive terms) plus an absolute
+      // part from the rounding of the centred inputs, ~2^-24·M·sqrt(F·d)·F; ×2 for the two distances
+      // compared, ×≥16 margin
+      const float W = 0x1p-12f * d1 + 0x1p-16f * Ff * M * sqrtf(Ff * d1) + 0x1p-28f * Ff * Ff * M * M;
+      const unsigned a = alt[e];
+      if (a != 0xFFFFFFFFu && __uint_as_float(a) <= d1 + W) {
+        t = d1 + W;
+        any = true;
+      }
+    }
+    thr[e] = t;
+  }
+  if (any) rlist[atomicAdd(&counts[0], 1)] = r;
+}
+
+template <int FMAX>
+__global__ __launch_bounds__(256) void knn_cand_kernel(
+    const float* __restrict__ R, const unsigned long long* __restrict__ rmask, const int* __restrict__ rlist,
+    const int* __restrict__ counts, const float* __restrict__ D, const unsigned long long* __restrict__ dmask,
+    int nd, int F, int per_split, const int* __restrict__ slot_col, const float* __restrict__ thr,
+    int* __restrict__ ccount, int* __restrict__ cand) {
+  constexpr int LD = (FMAX + 3) / 4 * 4;
+  const int nrl = counts[0];
+  if ((int)blockIdx.x * 256 >= nrl) return;   // (grid sized for every receiver)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* ds = sm;
+  unsigned long long* dm = (unsigned long long*)(ds + kKnnTile * LD);
+  const int li = blockIdx.x * 256 + threadIdx.x;
+  const bool active = li < nrl;
+  const int r = active ? rlist[li] : 0;
+  const int d_begin = blockIdx.y * per_split;
+  const int d_end = min(nd, d_begin + per_split);
+  float xr[LD];
+#pragma unroll
+  for (int f = 0; f < LD; ++f) xr[f] = (active && f < F) ? R[(size_t)r * F + f] : 0.f;
+  const unsigned long long mr = active ? rmask[r] : 0ull;
+  int col[kKnnSlots];
+  float th[kKnnSlots];
+  unsigned long long need = 0ull;
+  float tmax = -1.f;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k) {
+    const size_t e = (size_t)r * kKnnSlots + k;
+    th[k] = active ? thr[e] : -1.f;
+    col[k] = (active && th[k] >= 0.f) ? slot_col[e] : -1;
+    if (col[k] >= 0) need |= 1ull << col[k];
+    tmax = fmaxf(tmax, col[k] >= 0 ? th[k] : -1.f);
+  }
+  for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
+    __syncthreads();
+    const int nt = min(kKnnTile, d_end - d0);
+    for (int e = threadIdx.x; e < nt * LD; e += 256) {
+      const int rr = e / LD, c = e % LD;
+      ds[e] = c < F ? D[(size_t)(d0 + rr) * F + c] : 0.f;
+    }
+    if (threadIdx.x < nt) dm[threadIdx.x] = dmask[d0 + threadIdx.x];
+    __syncthreads();
+    if (need == 0ull) continue;
+    for (int t = 0; t < nt; ++t) {
+      const unsigned long long md = dm[t];
+      if ((need & ~md) == 0ull) continue;
+      const float4* xd4 = reinterpret_cast<const float4*>(ds + t * LD);
+      const unsigned long long both = ~(mr | md);
+      const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < LD / 4; ++q) {
+        if (4 * q < F) {
+          const float4 v = xd4[q];
+          const unsigned bq = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+          const float a = (bq & 1u) ? xr[4 * q] - v.x : 0.f;
+          const float b = (bq & 2u) ? xr[4 * q + 1] - v.y : 0.f;
+          const float c = (bq & 4u) ? xr[4 * q + 2] - v.z : 0.f;
+          const float d = (bq & 8u) ? xr[4 * q + 3] - v.w : 0.f;
+          s0 = fmaf(a, a, s0);
+          s1 = fmaf(b, b, s1);
+          s0 = fmaf(c, c, s0);
+          s1 = fmaf(d, d, s1);
+        }
+      }
+      const int present = F - __builtin_popcountll(mr | md);
+      if (present <= 0) continue;
+      const float dist = fmaxf(s0 + s1, 0.f) * ((float)F / (float)present);
+      if (!(dist <= tmax)) continue;
+#pragma unroll
+      for (int k = 0; k < kKnnSlots; ++k) {
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist <= th[k]) {
+          const size_t e = (size_t)r * kKnnSlots + k;
+          const int pos = atomicAdd(&ccount[e], 1);
+          if (pos < kKnnCand) cand[e * kKnnCand + pos] = d0 + t;
+        }
+      }
+    }
+  }
+}
+
+// f64 distance of the mirror: common features in order, fl((x−y)·(x−y)) summed, × F / |common|
+#pragma clang fp contract(off)
+__device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsigned long long mr,
+                                             const double* __restrict__ y, unsigned long long md, int F) {
+  double s = 0.0;
+  int present = 0;
+  for (int f = 0; f < F; ++f) {
+    if (((mr | md) >> f) & 1ull) continue;
+    const double t = x[f] - y[f];
+    s = s + t * t;
+    ++present;
+  }
+  return present > 0 ? (s * (double)F) / (double)present : INFINITY;
+}
+#pragma clang fp contract(on)
+
+__global__ __launch_bounds__(64) void knn_resolve_kernel(
+    const double* __restrict__ R64, const unsigned long long* __restrict__ rmask, const int* __restrict__ rlist,
+    const int* __restrict__ counts, const double* __restrict__ D64, const unsigned long long* __restrict__ dmask,
+    int nd, int F, const int* __restrict__ slot_col, const float* __restrict__ thr,
+    const int* __restrict__ ccount, const int* __restrict__ cand, unsigned long long* __restrict__ best) {
+  const int nrl = counts[0];
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < nrl * kKnnSlots; w += gridDim.x) {   // every wave reaches the end
+    const int r = rlist[w / kKnnSlots];
+    const int k = w % kKnnSlots;
+    const size_t e = (size_t)r * kKnnSlots + k;
+    if (thr[e] < 0.f) continue;
+    const int c = slot_col[e];
+    const unsigned long long mr = rmask[r];
+    const double* x = R64 + (size_t)r * F;
+    const int nc = ccount[e];
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    auto consider = [&](int d) {
+      const unsigned long long md = dmask[d];
+      if ((md >> c) & 1ull) return;
+      const double dist = knn_dist64(x, mr, D64 + (size_t)d * F, md, F);
+      if (dist < bd || (dist == bd && d < bi)) { bd = dist; bi = d; }
+    };
+    if (nc <= kKnnCand) {
+      for (int p = lane; p < nc; p += 64) consider(cand[e * kKnnCand + p]);
+    } else {
+      for (int d = lane; d < nd; d += 64) consider(d);   // candidate list overflowed: every donor
+    }
+    // (distance, index) minimum over the wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    if (lane == 0 && bi != 0x7fffffff)
+      best[e] = (best[e] & 0xFFFFFFFF00000000ull) | (unsigned long long)(unsigned)bi;
+  }
+}
+
+void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
+                uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t R64, uintptr_t D64, uintptr_t Mx,
+                uintptr_t work, uintptr_t stream) {
+  // work: int32 [1 + nr + nr·8 (ccount) + nr·8·kKnnCand (cand)] + f32 [nr·8] (thr), zeroed here
+  HFENS_REQUIRE(F >= 1 && F <= 64, "knn_refine: 1 <= F <= 64");
+  if (nr == 0 || nd == 0) return;
+  hipStream_t st = as_stream(stream);
+  int* counts = (int*)work;
+  int* rlist = counts + 4;
+  int* ccount = rlist + nr;
+  int* cand = ccount + (size_t)nr * kKnnSlots;
+  float* thr = (float*)(cand + (size_t)nr * kKnnSlots * kKnnCand);
+  HFENS_CHECK(hipMemsetAsync(counts, 0, 4 * sizeof(int), st));
+  HFENS_CHECK(hipMemsetAsync(ccount, 0, (size_t)nr * kKnnSlots * sizeof(int), st));
+  const int rb = (nr + 255) / 256;
+  hipLaunchKernelGGL(knn_ambig_kernel, dim3(rb), dim3(256), 0, st, (const unsigned long long*)best,
+                     (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, rlist, counts);
+  launch_check();
+  int splits = (nd + 16383) / 16384;
+  if (splits < 1) splits = 1;
+  auto go = [&](auto fm) {
+    constexpr int FM = decltype(fm)::value;
+    constexpr int LD = (FM + 3) / 4 * 4;
+    int per = (nd + splits - 1) / splits;
+    per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
+    const int nsp = (nd + per - 1) / per;
+    const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
+    hipLaunchKernelGGL(knn_cand_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
+                       (const unsigned long long*)rmask, rlist, counts, (const float*)D,
+                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, ccount, cand);
+    launch_check();
+  };
+  if (F <= 16) go(std::integral_constant<int, 16>{});
+  else if (F <= 32) go(std::integral_constant<int, 32>{});
+  else if (F <= 40) go(std::integral_constant<int, 40>{});
+  else if (F <= 48) go(std::integral_constant<int, 48>{});
+  else go(std::integral_constant<int, 64>{});
+  int grid = nr * kKnnSlots;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(knn_resolve_kernel, dim3(grid), dim3(64), 0, st, (const double*)R64,
+                     (const unsigned long long*)rmask, rlist, counts, (const double*)D64,
+                     (const unsigned long long*)dmask, nd, F, (const int*)slot_col, thr, ccount, cand,
+                     (unsigned long long*)best);
+  launch_check();
+}
+
 
 }  // namespace hfens

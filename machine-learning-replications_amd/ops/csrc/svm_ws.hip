@@ -818,6 +818,14 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   }
 }
 
+// v[m] for a wave-uniform m, branch-free: the masks are scalar values (the compiler turned the
+// ternary form into scalar branches, a fetch bubble each inside the pair loops)
+__device__ __forceinline__ unsigned sel4u(const unsigned (&v)[4], int m) {
+  const unsigned m0 = 0u - (unsigned)(m == 0), m1 = 0u - (unsigned)(m == 1);
+  const unsigned m2 = 0u - (unsigned)(m == 2), m3 = 0u - (unsigned)(m == 3);
+  return (v[0] & m0) | (v[1] & m1) | (v[2] & m2) | (v[3] & m3);
+}
+
 // ---- ws_kc_round: one whole round with the working set's kernel matrix cached in LDS -------------
 // The q = 1024 solver above pays ≈ 4.3k cycles per pair: four waves, two barriers and two dependent
 // LDS round trips per pair, and an F-term RBF row recomputed per pick (profiles/r3_headline.md).
@@ -845,13 +853,6 @@ static_assert(kc_lds_bytes(12) <= 163840, "the K-cached round must fit the CU's 
 
 __device__ __forceinline__ int kc_rowstart(int r) { return r * kKcQ - ((r * (r - 1)) >> 1); }
 
-// v[m] for a wave-uniform m, branch-free: the masks are scalar values (the compiler turned the
-// ternary form into scalar branches, a fetch bubble each inside the pair loop)
-__device__ __forceinline__ unsigned sel4u(const unsigned (&v)[4], int m) {
-  const unsigned m0 = 0u - (unsigned)(m == 0), m1 = 0u - (unsigned)(m == 1);
-  const unsigned m2 = 0u - (unsigned)(m == 2), m3 = 0u - (unsigned)(m == 3);
-  return (v[0] & m0) | (v[1] & m1) | (v[2] & m2) | (v[3] & m3);
-}
 __device__ __forceinline__ float sel4(const float (&v)[4], int m) {
   const unsigned u[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
   return __uint_as_float(sel4u(u, m));
@@ -1271,7 +1272,7 @@ void ws_init(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t
 void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t alpha,
               uintptr_t G, uintptr_t states, uintptr_t wsz, uintptr_t wsn, uintptr_t wdc, uintptr_t wsprev,
               uintptr_t wsidx, uintptr_t keys, long long n, uintptr_t gkey, double eps, int max_outer, int max_inner,
-              double inner_frac, int n_iter, uintptr_t prof, int inner_threads, uintptr_t stream) {
+              double inner_frac, int n_iter, uintptr_t prof, int inner_threads, int q, uintptr_t stream) {
   const WsAux X = ws_aux(keys, n, gkey);
   HFENS_REQUIRE(F >= 1 && F <= 48, "ws_steps: 1 <= F <= 48");
   // (< 32768: the packed 16|16-bit member counts of the radix selector)
@@ -1280,7 +1281,9 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
   hipStream_t st = as_stream(stream);
   const int KS = ws_ks(F);
   const int Fp2 = 2 * KS;
-  const int Q = ws_q(F);
+  // q: 0 = the default for F; 512 for F ≤ 24 is the smaller working set (half the per-pair slots)
+  const int Q = q == 0 ? ws_q(F) : q;
+  HFENS_REQUIRE(Q == 512 || (Q == 1024 && F <= 24), "ws_steps: q is 512, or 1024 for F <= 24");
   const int FP = F <= 24 ? (F + 3) / 4 * 4 : (F + 7) / 8 * 8;
   auto pp = (const WsProb*)probs;
   auto sp = (WsState*)states;
@@ -1317,6 +1320,7 @@ void ws_steps(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_
     WS_SOL_TH(FF, 512, 256);                                                                            \
   } else
     WS_SOL(4) WS_SOL(8) WS_SOL(12) WS_SOL(16) WS_SOL(20) WS_SOL(24)
+    WS_SOL512(4) WS_SOL512(8) WS_SOL512(12) WS_SOL512(16) WS_SOL512(20) WS_SOL512(24)
     WS_SOL512(32) WS_SOL512(40) WS_SOL512(48) {
       HFENS_REQUIRE(false, "ws_steps: no solve instance for this F");
     }

@@ -39,7 +39,18 @@ __device__ __forceinline__ void xg_store_sys(unsigned* p, unsigned v) {
   __hip_atomic_store((xg_gu32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* __restrict__ local,
+// T = long long (exact sums) or double (sum / max / min folded in RANK order 0 … W−1: every rank
+// computes the same bits, deterministic for a fixed world; the row-sharded interior point's
+// reductions, svc_lowrank._Red).  OP: 0 sum, 1 max, 2 min.
+template <typename T, int OP>
+__device__ __forceinline__ T xg_fold(T a, T b) {
+  if constexpr (OP == 0) return a + b;
+  else if constexpr (OP == 1) return a > b ? a : b;
+  else return a < b ? a : b;
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(T* __restrict__ local,
                                                                     long long count,
                                                                     long long* const* __restrict__ peers,
                                                                     int W, int me, int k, long long cap,
@@ -47,6 +58,7 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* _
                                                                     int t_host, const int* __restrict__ t_dev,
                                                                     unsigned* __restrict__ err,
                                                                     long long spin_ticks) {
+  static_assert(sizeof(T) == 8, "8-byte elements (the receive slots are int64-sized)");
   const int c = blockIdx.x, tid = threadIdx.x;
   const long long beg = (long long)c * kXgChunk;
   const long long end = min(count, beg + kXgChunk);
@@ -60,14 +72,14 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* _
   // 1. push this chunk to every rank (the comm slots of the stage kernel are 8-byte aligned only:
   //    8-byte stores, 512 B per wave instruction; the chunk's values are loaded once)
   constexpr int kPer = (int)(kXgChunk / kXgThreads);
-  long long v[kPer];
+  T v[kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const long long i = beg + tid + (long long)q * kXgThreads;
-    v[q] = i < end ? local[i] : 0;
+    v[q] = i < end ? local[i] : T(0);
   }
   for (int p = 0; p < W; ++p) {
-    long long* dst = peers[p] + (size_t)me * 3 * cap + recv_slot;
+    T* dst = reinterpret_cast<T*>(peers[p] + (size_t)me * 3 * cap + recv_slot);
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const long long i = beg + tid + (long long)q * kXgThreads;
@@ -97,14 +109,14 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(long long* _
   __syncthreads();
   if (s_fail) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  // 4. total over the ranks (exact integer sums) back into the local slot
-  const long long* recv = peers[me] + recv_slot;
+  // 4. the fold over the ranks, in rank order, back into the local slot (int64 sums: exact)
+  const T* recv = reinterpret_cast<const T*>(peers[me] + recv_slot);
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const long long i = beg + tid + (long long)q * kXgThreads;
     if (i < end) {
-      long long s = 0;
-      for (int r = 0; r < W; ++r) s += recv[(size_t)r * 3 * cap + i];
+      T s = recv[i];
+      for (int r = 1; r < W; ++r) s = xg_fold<T, OP>(s, recv[(size_t)r * 3 * cap + i]);
       local[i] = s;
     }
   }
@@ -142,23 +154,37 @@ void xgmi_ipc_open(uintptr_t handle, uintptr_t out) {
 
 void xgmi_ipc_close(uintptr_t p) { HFENS_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(p))); }
 
-// All-reduce (sum) of `count` int64 at `local` over the W ranks whose buffers `peers` (device
-// array of W base pointers, this rank's own at index me) points to; slot k = stage % 3.
-void xgmi_allreduce_i64(uintptr_t local, long long count, uintptr_t peers, int W, int me, int k, long long cap,
-                        long long epoch_base, int t_host, uintptr_t t_dev, uintptr_t err, double timeout_s,
-                        uintptr_t stream) {
-  HFENS_REQUIRE(W >= 1 && W <= kXgMaxRanks && me >= 0 && me < W, "xgmi_allreduce_i64: 1 <= W <= 16, 0 <= me < W");
-  HFENS_REQUIRE(k >= 0 && k < 3 && count >= 0 && count <= cap, "xgmi_allreduce_i64: slot 0..2, count <= cap");
-  HFENS_REQUIRE((local & 7) == 0, "xgmi_allreduce_i64: the local slot must be 8-byte aligned");
+// All-reduce of `count` 8-byte elements at `local` (dtype 0: int64, 1: f64; op 0 sum, 1 max, 2 min —
+// int64 supports sum only) over the W ranks whose buffers `peers` (device array of W base pointers,
+// this rank's own at index me) points to; slot k rotates with the call sequence (period 3).
+void xgmi_allreduce(uintptr_t local, long long count, int dtype, int op, uintptr_t peers, int W, int me, int k,
+                    long long cap, long long epoch_base, int t_host, uintptr_t t_dev, uintptr_t err, double timeout_s,
+                    uintptr_t stream) {
+  HFENS_REQUIRE(W >= 1 && W <= kXgMaxRanks && me >= 0 && me < W, "xgmi_allreduce: 1 <= W <= 16, 0 <= me < W");
+  HFENS_REQUIRE(k >= 0 && k < 3 && count >= 0 && count <= cap, "xgmi_allreduce: slot 0..2, count <= cap");
+  HFENS_REQUIRE((local & 7) == 0, "xgmi_allreduce: the local buffer must be 8-byte aligned");
+  HFENS_REQUIRE((dtype == 0 && op == 0) || (dtype == 1 && op >= 0 && op <= 2),
+                "xgmi_allreduce: int64 sum, or f64 sum / max / min");
   if (count == 0) return;
   const int nchunk = (int)((cap + kXgChunk - 1) / kXgChunk);
   const int grid = (int)((count + kXgChunk - 1) / kXgChunk);
   const long long ticks = (long long)(timeout_s * 1.0e8);   // s_memrealtime: fixed 100 MHz
-  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(grid), dim3(kXgThreads), 0, as_stream(stream),
-                     reinterpret_cast<long long*>(local), count, reinterpret_cast<long long* const*>(peers), W, me,
-                     k, cap, nchunk, (unsigned)epoch_base, t_host, reinterpret_cast<const int*>(t_dev),
-                     reinterpret_cast<unsigned*>(err), ticks);
+  auto go = [&](auto kern, auto* loc) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kXgThreads), 0, as_stream(stream), loc, count,
+                       reinterpret_cast<long long* const*>(peers), W, me, k, cap, nchunk, (unsigned)epoch_base, t_host,
+                       reinterpret_cast<const int*>(t_dev), reinterpret_cast<unsigned*>(err), ticks);
+  };
+  if (dtype == 0) go(xgmi_allreduce_kernel<long long, 0>, reinterpret_cast<long long*>(local));
+  else if (op == 0) go(xgmi_allreduce_kernel<double, 0>, reinterpret_cast<double*>(local));
+  else if (op == 1) go(xgmi_allreduce_kernel<double, 1>, reinterpret_cast<double*>(local));
+  else go(xgmi_allreduce_kernel<double, 2>, reinterpret_cast<double*>(local));
   launch_check();
+}
+
+void xgmi_allreduce_i64(uintptr_t local, long long count, uintptr_t peers, int W, int me, int k, long long cap,
+                        long long epoch_base, int t_host, uintptr_t t_dev, uintptr_t err, double timeout_s,
+                        uintptr_t stream) {
+  xgmi_allreduce(local, count, 0, 0, peers, W, me, k, cap, epoch_base, t_host, t_dev, err, timeout_s, stream);
 }
 
 }  // namespace hfens

@@ -119,6 +119,20 @@ class PeerComm:
                                   t_dev.data_ptr() if t_dev is not None else 0, self.err.data_ptr(), TIMEOUT_S,
                                   stream if stream is not None else ops.stream_ptr(self.device))
 
+    def reduce_f64_(self, t: torch.Tensor, op: str = "sum", stream: Optional[int] = None):
+        """All-reduce the f64 tensor ``t`` in place (``op`` sum / max / min, folded in rank order
+        0 … W−1: the same bits on every rank, deterministic for a fixed world) — ONE kernel on the
+        current stream, no RCCL call.  Calls are collective and sequenced: every rank makes the same
+        calls in the same order (epochs and slots follow the call count)."""
+        from .. import ops
+        assert t.dtype == torch.float64 and t.is_contiguous() and t.numel() <= self.cap
+        k = (self.epoch + 1) % 3
+        self.E.xgmi_allreduce(t.data_ptr(), t.numel(), 1, {"sum": 0, "max": 1, "min": 2}[op], self.peers.data_ptr(),
+                              self.W, self.me, k, self.cap, self.epoch, 0, 0, self.err.data_ptr(), TIMEOUT_S,
+                              stream if stream is not None else ops.stream_ptr(self.device))
+        self.epoch += 1
+        return t
+
     def advance(self, stages: int):
         """Reserve ``stages`` epochs after a loop that used epochs base+1 … base+stages."""
         self.epoch += int(stages)
@@ -149,9 +163,11 @@ def _same_host(group) -> bool:
     return len(set(names)) == 1
 
 
-def peer_comm(group, device, cap: int) -> Optional[PeerComm]:
+def peer_comm(group, device, cap: int, tag: str = "") -> Optional[PeerComm]:
     """The group's peer buffers (created once, grown when ``cap`` grows) or None when the ranks
-    cannot map each other (different hosts, > 16 ranks, HFENS_XGMI=0, no GPU)."""
+    cannot map each other (different hosts, > 16 ranks, HFENS_XGMI=0, no GPU).  ``tag``: an
+    independent set of buffers (its own epochs and slot rotation) for another user of the group,
+    e.g. the interior point's reductions ("ipm") beside the GBDT stage sums ("")."""
     import torch.distributed as dist
     if group is None or MODE in ("0", "auto") or torch.device(device).type != "cuda":
         return None
@@ -163,7 +179,7 @@ def peer_comm(group, device, cap: int) -> Optional[PeerComm]:
             raise RuntimeError("HFENS_XGMI=1 but the ranks cannot map each other's memory")
     if not _OK[gid]:
         return None
-    key = (gid, str(torch.device(device)))
+    key = (gid, str(torch.device(device)), tag)
     pc = _CACHE.get(key)
     if pc is None or pc.cap < cap:
         epoch = pc.epoch if pc is not None else 0

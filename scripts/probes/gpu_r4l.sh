@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4: f64-exact KNN donors; device-side SVC OOF column — GPU tests, headline bench, aligned host/device timeline
+set -o pipefail
+D=gpurun_out/r4l
+mkdir -p $D
+timeout -k 10 300 python -u -m pytest tests/test_prep_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > $D/pytest_prep.log 2>&1 || { echo "pytest prep failed"; tail -40 $D/pytest_prep.log; exit 1; }
+tail -3 $D/pytest_prep.log
+timeout -k 10 400 python -u -m pytest tests/test_train_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "device_svc_oof or plan_ahead or develop" > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $D/pytest.log; exit 1; }
+tail -3 $D/pytest.log
+for k in 1 0; do
+  HFENS_DEVICE_SVC_OOF=$k timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $D/bench_oof$k.json 2> $D/bench_oof$k.err || { echo "bench failed"; tail -30 $D/bench_oof$k.err; exit 1; }
+  python -c "import json; d=json.loads(open('$D/bench_oof$k.json').read().strip().split('\n')[-1]); print('oof$k', d['ms_per_step'], d['diag']['step_ms_min_med_max'], d['auroc'])"
+done
+HFENS_TRACE_HOST=1 timeout -k 10 200 python -u scripts/probes/ws_events.py > $D/ev_host.log 2>&1 || { echo "events failed"; tail -30 $D/ev_host.log; exit 1; }
+tail -6 $D/ev_host.log

@@ -560,9 +560,9 @@ def test_gbdt_stage_plan_sizes_partials(dev, monkeypatch, wgs, atomic):
         assert torch.equal(ms[0].train_score_.cpu(), ref[2])
 
 
-def _lowrank_dp_worker(rank, world, port, q):
+def _lowrank_dp_worker(rank, world, port, q, xgmi="0"):
     import os
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GPU_MAX_HW_QUEUES="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GPU_MAX_HW_QUEUES="1", HFENS_XGMI=xgmi)
     import torch.distributed as dist
     from hfens.models import svc_lowrank
     from hfens.parallel import dist as pdist
@@ -577,16 +577,21 @@ def _lowrank_dp_worker(rank, world, port, q):
                                           group=dist.group.WORLD)
         if rank == 0:
             q.put((svc._dual_coef_.cpu(), float(svc._intercept_[0]), svc._probA.item(), svc._probB.item(),
-                   svc.support_.cpu(), svc_lowrank.LAST_INFO["row_sharded"]))
+                   svc.support_.cpu(), svc_lowrank.LAST_INFO["row_sharded"], dict(svc_lowrank._Red.STATS)))
     finally:
+        from hfens.parallel import xgmi as _xg
+        _xg.release_all()
         pdist.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_lowrank_svc_row_sharded_threads(dev, world):
+@pytest.mark.parametrize("world,xgmi", [(2, "0"), (4, "0"), (2, "1"), (4, "1")])
+def test_lowrank_svc_row_sharded_threads(dev, world, xgmi):
     """the row-sharded interior point with its concurrent Platt-CV solves (3
     host threads + the final solve, each on its own stream AND its own communicator) — 2 / 4
-    processes on one card over gloo — equals the one-process GPU fit to 1e-8."""
+    processes on one card over gloo — equals the one-process GPU fit to 1e-8.  xgmi = "1" (VERDICT
+    r3 next #5): every reduction of the solves is one peer-memory f64 kernel folding the ranks in
+    rank order (parallel/xgmi.py reduce_f64_) — ZERO collectives inside the interior point — with
+    the solves run from one thread (svc_lowrank._threads_safe)."""
     import socket
     import torch.multiprocessing as mp
     from hfens.models import svc_lowrank
@@ -596,10 +601,10 @@ def test_lowrank_svc_row_sharded_threads(dev, world):
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_lowrank_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_lowrank_dp_worker, args=(r, world, port, q, xgmi)) for r in range(world)]
     for p in procs:
         p.start()
-    coef, ic, pa, pb, sup, sharded = q.get(timeout=100)
+    coef, ic, pa, pb, sup, sharded, red = q.get(timeout=100)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -607,6 +612,10 @@ def test_lowrank_svc_row_sharded_threads(dev, world):
     ref = SVC(class_weight="balanced", probability=True, random_state=2020)
     svc_lowrank.fit_svc_lowrank_batch([ref], [Z.to(dev)], [y.to(dev)], n_landmarks=256)
     assert sharded is True
+    if xgmi == "1":
+        assert red["rccl"] == 0 and red["peer"] > 0, red
+    else:
+        assert red["peer"] == 0 and red["rccl"] > 0, red
     assert torch.equal(sup, ref.support_.cpu())
     assert torch.allclose(coef, ref._dual_coef_.cpu(), rtol=0, atol=1e-8)
     assert abs(ic - float(ref._intercept_[0])) < 1e-8
@@ -661,3 +670,25 @@ def test_smo_coop_late_member_falls_back(dev, monkeypatch, otf):
     assert t_fb - t_one - 60.0 <= 50.0, (t_fb, t_one)
     ok, info3, _, wl3 = fit(True)                          # no injection: no fallback
     assert not info3.get("coop_fallback") and info3["members"] > 1 and not wl3
+
+
+def test_device_svc_oof_matches_fold_models(dev, monkeypatch):
+    """The stacking trainer's SVC out-of-fold column computed on the device behind the SMO
+    (smo.enqueue_svc_oof: decision sums over the final problems' rows, Platt sigmoid + coupling from
+    the device (A, B)) equals the fold models' predict_proba to f32 rounding, and the meta model
+    fitted on it is the same model."""
+    from hfens import pipeline
+    from hfens.models import stack_trainer
+    from hfens.io.synth import make_hf_cohort
+    Xd, yd, names = make_hf_cohort(3000, 40, seed=91, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(1000, 40, seed=92, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(stack_trainer, "DEVICE_SVC_OOF", flag)
+        out[flag] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+    m0, m1 = out[False].model, out[True].model
+    d = (m0.oof_meta_ - m1.oof_meta_).abs()
+    assert float(d[:, 1:].max()) == 0.0            # the other columns are untouched
+    assert float(d[:, 0].max()) <= 2e-6, float(d[:, 0].max())
+    assert float((out[False].proba_sel - out[True].proba_sel).abs().max()) <= 1e-5
