@@ -156,34 +156,29 @@ class KNNImputer(Estimator):
 
     def _impute_device(self, X, bits, D32, dm):
         from .. import ops
-        from .smo import _to_dev
         E = ops.ext()
         n, F = X.shape
-        rows_np = np.nonzero(bits)[0]
-        if rows_np.size == 0:
+        # the work lists from the rows' missing-column bitmasks, planned natively (host.hip
+        # knn_plan_host) into ONE pinned buffer → one H2D copy, sliced on the device
+        dev = X.device
+        nslot_max = -(-F // SLOTS) * SLOTS
+        cap = 2 * n + n * nslot_max + 3 * n * F
+        hb = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+        dims = np.zeros(3, dtype=np.int64)
+        bits = np.ascontiguousarray(bits, dtype=np.uint64)
+        E.knn_plan_host(bits.ctypes.data, n, F, SLOTS, hb.data_ptr(), cap, dims.ctypes.data)
+        nr, nc, nslot = (int(v) for v in dims)
+        if nr <= 0:
             return
         center = self._col_mean
-        Rm_np = ((bits[rows_np, None] >> np.arange(F, dtype=np.uint64)) & np.uint64(1)).astype(bool)
-        rl, cc = np.nonzero(Rm_np)                       # missing cells, row-major, columns ascending
         from ..utils.timing import hmark
         hmark("imp_plan")
-        nm = Rm_np.sum(1)
-        start = np.concatenate([[0], np.cumsum(nm)[:-1]])
-        kk = np.arange(rl.shape[0]) - start[rl]          # slot of each cell within its row
-        nslot = -(-int(nm.max()) // SLOTS) * SLOTS
-        slot_all = np.full((rows_np.shape[0], nslot), -1, dtype=np.int32)
-        slot_all[rl, kk] = cc
-        dev = X.device
-        # every index array in ONE pinned host buffer → one H2D copy, sliced on the device
-        nr, nc = rows_np.shape[0], rl.shape[0]
-        parts = [rows_np, Rm_np.reshape(-1), bits[rows_np].view(np.int64), slot_all.reshape(-1),
-                 rl * nslot + kk, rows_np[rl], cc]
-        sizes = [a.shape[0] for a in parts]
-        buf = _to_dev(np.concatenate([a.astype(np.int64, copy=False) for a in parts]), dev)
+        sizes = [nr, nr, nr * nslot, nc, nc, nc]
+        buf = hb[:sum(sizes)].to(dev, non_blocking=True)
         o = np.concatenate([[0], np.cumsum(sizes)])
-        rows, Rm, rm, slot_dev, flat, r_idx, c_idx = (buf[o[i]:o[i + 1]] for i in range(7))
+        rows, rm, slot_dev, flat, r_idx, c_idx = (buf[o[i]:o[i + 1]] for i in range(6))
         hmark("imp_h2d")
-        Rm = (Rm != 0).view(nr, F)
+        Rm = ((rm[:, None] >> torch.arange(F, device=dev)) & 1) != 0
         slot_dev = slot_dev.view(nr, nslot).to(torch.int32)
         Xr = X.index_select(0, rows)
         R32 = torch.where(Rm, torch.zeros_like(Xr), Xr - center).to(torch.float32).contiguous()

@@ -114,6 +114,7 @@ IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
 IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "3"))   # concurrent Platt-CV solves per fit (+ the final)
 FIT_THREADS = int(os.environ.get("HFENS_IPM_FITS", "1"))      # fits solved at a time (2: no gain measured, GPU saturated)
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
+CHOL_MW = os.environ.get("HFENS_CHOL_MW", "1") != "0"      # multi-workgroup r × r Cholesky (r ≤ 512)
 
 
 def _scaled_rows(Phi: torch.Tensor, d: torch.Tensor, P32: torch.Tensor = None) -> torch.Tensor:
@@ -356,6 +357,8 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
         Lc = torch.empty(r, r, dtype=dt, device=Phi.device)
         scv = torch.empty(r, dtype=dt, device=Phi.device)
         info = torch.zeros(1, dtype=torch.int32, device=Phi.device)
+        chw = torch.zeros(4, dtype=torch.int32, device=Phi.device)         # chol_spd_mw failure flag
+        chpt = torch.empty(32 * r, dtype=dt, device=Phi.device)            # chol_spd_mw transposed panel
     yk = {1: y[:, None], 2: torch.stack([y, y], 1)}
     it = 0
     for it in range(1, max_iter + 1):
@@ -401,7 +404,11 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
                   f"{float(D.max()):.3e}] a_min {float(a.min()):.3e} s_min {float(s.min()):.3e} "
                   f"diagS [{float(dS.min()):.3e}, {float(dS.max()):.3e}] finite {bool(torch.isfinite(S).all())}",
                   flush=True)
-        if native:
+        if native and CHOL_MW and r <= 512:
+            # multi-workgroup blocked factor (linalg.hip chol_spd_mw; bit-identical to chol_spd)
+            E.chol_spd_mw(S.contiguous().data_ptr(), r, Lc.data_ptr(), scv.data_ptr(), info.data_ptr(),
+                          chw.data_ptr(), chpt.data_ptr(), ops.stream_ptr(Phi.device))
+        elif native:
             E.chol_spd(S.contiguous().data_ptr(), r, Lc.data_ptr(), scv.data_ptr(), info.data_ptr(),
                        ops.stream_ptr(Phi.device))
         else:

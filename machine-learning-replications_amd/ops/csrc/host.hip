@@ -176,4 +176,62 @@ void stack_predict_host(int n, int F, uintptr_t X_, uintptr_t mean_, uintptr_t s
   }
 }
 
+// KNN imputation work lists from the rows' missing-column bitmasks (models/imputer.py
+// _impute_device; the numpy version cost ≈ 1 ms of host time at 10k rows before the donor search
+// could launch).  bits [n] u64 (bit f = column f missing); out: int64 buffer of capacity `cap`
+// filled as [rows (nr) | bits of those rows (nr) | slot columns (nr × nslot, −1 padded) | flat slot
+// index of every missing cell (nc) | its row (nc) | its column (nc)], cells row-major with columns
+// ascending (the numpy order); dims[0..2] = nr, nc, nslot (nslot = max missing per row rounded up
+// to `slots`).  dims[0] = −1 when `cap` is too small (nothing written past it).
+void knn_plan_host(uintptr_t bits_, long long n, int F, int slots, uintptr_t out_, long long cap, uintptr_t dims_) {
+  const uint64_t* bits = reinterpret_cast<const uint64_t*>(bits_);
+  long long* out = reinterpret_cast<long long*>(out_);
+  long long* dims = reinterpret_cast<long long*>(dims_);
+  const uint64_t fmask = F >= 64 ? ~0ull : ((1ull << F) - 1ull);
+  long long nr = 0, nc = 0;
+  int mx = 0;
+  for (long long i = 0; i < n; ++i) {
+    const uint64_t b = bits[i] & fmask;
+    if (!b) continue;
+    ++nr;
+    const int c = __builtin_popcountll(b);
+    nc += c;
+    mx = c > mx ? c : mx;
+  }
+  const int nslot = nr ? (mx + slots - 1) / slots * slots : 0;
+  dims[0] = nr;
+  dims[1] = nc;
+  dims[2] = nslot;
+  if (2 * nr + nr * nslot + 3 * nc > cap) {
+    dims[0] = -1;
+    return;
+  }
+  long long* rows = out;
+  long long* rb = rows + nr;
+  long long* slot = rb + nr;
+  long long* flat = slot + nr * nslot;
+  long long* ri = flat + nc;
+  long long* ci = ri + nc;
+  long long k = 0, e = 0;
+  for (long long i = 0; i < n; ++i) {
+    uint64_t b = bits[i] & fmask;
+    if (!b) continue;
+    rows[k] = i;
+    rb[k] = (long long)b;
+    int s = 0;
+    while (b) {
+      const int f = __builtin_ctzll(b);
+      b &= b - 1ull;
+      slot[k * nslot + s] = f;
+      flat[e] = k * nslot + s;
+      ri[e] = i;
+      ci[e] = f;
+      ++s;
+      ++e;
+    }
+    for (; s < nslot; ++s) slot[k * nslot + s] = -1;
+    ++k;
+  }
+}
+
 }  // namespace hfens

@@ -44,7 +44,10 @@ size_t chol_spd_lds(int r, int NB) { return ((size_t)NB * (NB + 1) + (size_t)NB 
 template <int NB>
 __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __restrict__ S, int r,
                                                               double* __restrict__ L, double* __restrict__ sc,
-                                                              int* __restrict__ out_info) {
+                                                              int* __restrict__ out_info,
+                                                              const int* __restrict__ skip_if_ok = nullptr) {
+  // (the multi-workgroup factorisation ran first and succeeded: nothing to do)
+  if (skip_if_ok != nullptr && skip_if_ok[0] == 0) return;
   extern __shared__ __attribute__((aligned(16))) double chsm[];
   double* Dg = chsm;
   double* PT = Dg + NB * (NB + 1);
@@ -175,6 +178,142 @@ __global__ __launch_bounds__(kChThreads) void chol_spd_kernel(const double* __re
     __syncthreads();
   }
   if (tid == 0) out_info[0] = tries;
+}
+
+// ---- chol_spd_mw: the same blocked factorisation spread over the GPU -------
+// chol_spd_kernel runs every phase inside ONE workgroup (≈ 1.2 ms at r = 512, the largest single item
+// of the interior point after the Gram and the skinny passes).  Here each NB-column step is three
+// launches — the NB × NB diagonal block (one workgroup, the same loops), the panel rows (one thread
+// per row over ⌈m/256⌉ workgroups, the transposed panel PT in global memory instead of LDS), the
+// trailing lower triangle (one wave per 16 × 16 block on v_mfma_f64_16x16x4_f64 over ⌈blocks/8⌉
+// workgroups) — with every element computed by the same operations in the same order as the
+// one-workgroup kernel, so L is bit-identical to it.  Only the unjittered attempt runs here: a
+// failed pivot sets work[0] and the remaining launches exit at once; chol_spd_kernel then runs with
+// skip_if_ok = work and does its full jitter ladder from S.
+template <int NB>
+__global__ __launch_bounds__(256) void chol_mw_init_kernel(const double* __restrict__ S, int r,
+                                                           double* __restrict__ L, double* __restrict__ sc,
+                                                           int* __restrict__ work) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e == 0) work[0] = 0;
+  if (e >= (size_t)r * r) return;
+  const int i = (int)(e / r), j = (int)(e % r);
+  const double di = S[(size_t)i * r + i], dj = S[(size_t)j * r + j];
+  const double si = di > 0.0 ? 1.0 / sqrt(di) : 1.0, sj = dj > 0.0 ? 1.0 / sqrt(dj) : 1.0;
+  if (j == 0) sc[i] = si;
+  L[e] = j <= i ? S[e] * si * sj + (i == j ? 0.0 : 0.0) : 0.0;
+}
+
+template <int NB>
+__global__ __launch_bounds__(kChThreads) void chol_mw_diag_kernel(double* __restrict__ L, int r, int k0,
+                                                                  int* __restrict__ work) {
+  if (work[0] != 0) return;
+  __shared__ double Dg[NB * (NB + 1)];
+  __shared__ double dgl[NB];
+  __shared__ int s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = min(NB, r - k0);
+  if (tid == 0) s_bad = 0;
+  for (int e = tid; e < nb * nb; e += kChThreads) {
+    const int a = e / nb, b = e % nb;
+    Dg[a * (NB + 1) + b] = b <= a ? L[(size_t)(k0 + a) * r + k0 + b] : 0.0;
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    const double pj = Dg[j * (NB + 1) + j];
+    if (!(pj > 0.0) || !isfinite(pj)) {
+      if (tid == 0) work[0] = 1;
+      return;
+    }
+    const double dj = sqrt(pj);
+    for (int a = j + 1 + tid; a < nb; a += kChThreads) Dg[a * (NB + 1) + j] /= dj;
+    if (tid == 0) dgl[j] = dj;
+    __syncthreads();
+    for (int a = j + 1 + wave; a < nb; a += kChWaves)
+      for (int b = j + 1 + lane; b <= a; b += 64)
+        Dg[a * (NB + 1) + b] -= Dg[a * (NB + 1) + j] * Dg[b * (NB + 1) + j];
+    __syncthreads();
+  }
+  for (int j = tid; j < nb; j += kChThreads) Dg[j * (NB + 1) + j] = dgl[j];
+  __syncthreads();
+  for (int e = tid; e < nb * nb; e += kChThreads) {
+    const int a = e / nb, b = e % nb;
+    if (b <= a) L[(size_t)(k0 + a) * r + k0 + b] = Dg[a * (NB + 1) + b];
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void chol_mw_panel_kernel(double* __restrict__ L, int r, int k0,
+                                                            double* __restrict__ PT, const int* __restrict__ work) {
+  if (work[0] != 0) return;
+  __shared__ double Dg[NB * (NB + 1)];
+  const int nb = min(NB, r - k0), m0 = k0 + nb, m = r - m0;
+  for (int e = threadIdx.x; e < nb * nb; e += 256) {
+    const int a = e / nb, b = e % nb;
+    Dg[a * (NB + 1) + b] = b <= a ? L[(size_t)(k0 + a) * r + k0 + b] : 0.0;
+  }
+  __syncthreads();
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int m16 = (m + 15) & ~15;
+  if (t >= m && t < m16) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) PT[(size_t)b * r + t] = 0.0;
+  }
+  if (t >= m) return;
+  double x[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) x[b] = b < nb ? L[(size_t)(m0 + t) * r + k0 + b] : 0.0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+      double v = x[b];
+#pragma unroll
+      for (int p = 0; p < b; ++p) v -= x[p] * Dg[b * (NB + 1) + p];
+      x[b] = v / Dg[b * (NB + 1) + b];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    if (b < nb) {
+      L[(size_t)(m0 + t) * r + k0 + b] = x[b];
+      PT[(size_t)b * r + t] = x[b];
+    }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void chol_mw_trail_kernel(double* __restrict__ L, int r, int k0,
+                                                            const double* __restrict__ PT,
+                                                            const int* __restrict__ work) {
+  if (work[0] != 0) return;
+  const int nb = min(NB, r - k0), m0 = k0 + nb, m = r - m0;
+  const int m16 = (m + 15) & ~15;
+  const int nbk = m16 / 16;
+  const int nblocks = nbk * (nbk + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per 16 × 16 block
+  if (blk >= nblocks) return;
+  int bi = 0, rem = blk;
+  while (rem > bi) { rem -= bi + 1; ++bi; }
+  const int bj = rem;
+  double old[4];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * bj + (lane & 15);
+    old[reg] = (i < m && j <= i) ? L[(size_t)(m0 + i) * r + m0 + j] : 0.0;
+  }
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < NB / 4; ++ks) {
+    const int kb = 4 * ks + (lane >> 4);
+    const double a = PT[(size_t)kb * r + 16 * bi + (lane & 15)];
+    const double b = PT[(size_t)kb * r + 16 * bj + (lane & 15)];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int i = 16 * bi + (lane >> 4) + 4 * reg, j = 16 * bj + (lane & 15);
+    if (i < m && j <= i) L[(size_t)(m0 + i) * r + m0 + j] = old[reg] - acc[reg];
+  }
 }
 
 // x ← sc ∘ (L Lᵀ)⁻¹ (sc ∘ B): B [r][k] row-major (k ≤ 4), overwritten with the solution.  Per
@@ -318,6 +457,40 @@ void chol_spd(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uin
     hipLaunchKernelGGL(chol_spd_kernel<16>, dim3(1), dim3(kChThreads), chol_spd_lds(r, 16), as_stream(stream),
                        (const double*)S, r, (double*)L, (double*)sc, (int*)info);
   }
+  launch_check();
+}
+
+__global__ void chol_mw_info_kernel(const int* __restrict__ work, int* __restrict__ info) {
+  if (threadIdx.x == 0 && work[0] == 0) info[0] = 0;
+}
+
+// work: int32 [≥ 2] scratch (failure flag), PT: f64 [32 · r] scratch (the transposed panel)
+void chol_spd_mw(uintptr_t S, int r, uintptr_t L, uintptr_t sc, uintptr_t info, uintptr_t work, uintptr_t PT,
+                 uintptr_t stream) {
+  HFENS_REQUIRE(r >= 1 && r <= 512, "chol_spd_mw: 1 <= r <= 512");
+  constexpr int NB = 32;
+  hipStream_t st = as_stream(stream);
+  double* Lp = (double*)L;
+  int* wk = (int*)work;
+  const size_t rr = (size_t)r * r;
+  hipLaunchKernelGGL(chol_mw_init_kernel<NB>, dim3((unsigned)((rr + 255) / 256)), dim3(256), 0, st, (const double*)S, r,
+                     Lp, (double*)sc, wk);
+  for (int k0 = 0; k0 < r; k0 += NB) {
+    hipLaunchKernelGGL(chol_mw_diag_kernel<NB>, dim3(1), dim3(kChThreads), 0, st, Lp, r, k0, wk);
+    const int m = r - min(NB, r - k0) - k0;
+    if (m <= 0) break;
+    hipLaunchKernelGGL(chol_mw_panel_kernel<NB>, dim3((m + 15 + 255) / 256), dim3(256), 0, st, Lp, r, k0,
+                       (double*)PT, (const int*)wk);
+    const int nbk = ((m + 15) & ~15) / 16;
+    const int nblocks = nbk * (nbk + 1) / 2;
+    hipLaunchKernelGGL(chol_mw_trail_kernel<NB>, dim3((nblocks + 3) / 4), dim3(256), 0, st, Lp, r, k0,
+                       (const double*)PT, (const int*)wk);
+  }
+  launch_check();
+  // the one-workgroup kernel with its jitter ladder, only if the plain attempt failed; else info = 0
+  hipLaunchKernelGGL(chol_spd_kernel<32>, dim3(1), dim3(kChThreads), chol_spd_lds(r, 32), st, (const double*)S, r, Lp,
+                     (double*)sc, (int*)info, (const int*)wk);
+  hipLaunchKernelGGL(chol_mw_info_kernel, dim3(1), dim3(64), 0, st, (const int*)wk, (int*)info);
   launch_check();
 }
 

@@ -227,3 +227,52 @@ def test_ipm_f32_gram_matches_f64_path(dev, monkeypatch):
     assert abs(rho32 - rho64) <= 1e-6, (rho32, rho64)
     obj = lambda a, w: float(0.5 * (w @ w) - a.sum())   # noqa: E731
     assert abs(obj(a32, w32) - obj(a64, w64)) <= 1e-8 * abs(obj(a64, w64))
+
+
+@pytest.mark.parametrize("r", [1, 31, 96, 300, 509, 512])
+def test_chol_spd_mw_bit_identical(dev, r):
+    """The multi-workgroup blocked Cholesky (diagonal block / panel rows / MFMA trailing update as
+    separate launches) computes every element with the one-workgroup kernel's operations in its
+    order: L, the equilibration and info are bit-identical."""
+    E = ops.ext()
+    S = _spd(r, 8, r + 1).to(dev)
+    out = []
+    for mw in (False, True):
+        L = torch.full((r, r), float("nan"), dtype=torch.float64, device=dev)
+        sc = torch.empty(r, dtype=torch.float64, device=dev)
+        info = torch.full((1,), 99, dtype=torch.int32, device=dev)
+        if mw:
+            work = torch.zeros(4, dtype=torch.int32, device=dev)
+            PT = torch.empty(32 * r, dtype=torch.float64, device=dev)
+            E.chol_spd_mw(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), work.data_ptr(),
+                          PT.data_ptr(), ops.stream_ptr(dev))
+        else:
+            E.chol_spd(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), ops.stream_ptr(dev))
+        out.append((L.cpu(), sc.cpu(), int(info)))
+    assert out[0][2] == out[1][2] == 0
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][0], out[1][0])
+
+
+def test_chol_spd_mw_falls_back_on_semidefinite(dev):
+    """A failed plain attempt hands over to the one-workgroup kernel's jitter ladder: the same factor
+    and retry count as chol_spd."""
+    E = ops.ext()
+    r = 200
+    A = torch.randn(r, 60, dtype=torch.float64, generator=torch.Generator().manual_seed(5))
+    S = (A @ A.T).to(dev)
+    res = []
+    for mw in (False, True):
+        L = torch.empty(r, r, dtype=torch.float64, device=dev)
+        sc = torch.empty(r, dtype=torch.float64, device=dev)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        if mw:
+            work = torch.zeros(4, dtype=torch.int32, device=dev)
+            PT = torch.empty(32 * r, dtype=torch.float64, device=dev)
+            E.chol_spd_mw(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), work.data_ptr(),
+                          PT.data_ptr(), ops.stream_ptr(dev))
+        else:
+            E.chol_spd(S.data_ptr(), r, L.data_ptr(), sc.data_ptr(), info.data_ptr(), ops.stream_ptr(dev))
+        res.append((L.cpu(), int(info)))
+    assert res[0][1] >= 1 and res[0][1] == res[1][1]
+    assert torch.equal(res[0][0], res[1][0])
