@@ -19,7 +19,6 @@ from .base import Estimator, as_tensor
 SLOTS = 8
 # f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
 EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
-KNN_CAND = 32   # knn.hip kKnnCand
 
 
 def _masks_u64(miss: torch.Tensor) -> torch.Tensor:
@@ -189,7 +188,8 @@ class KNNImputer(Estimator):
             D64, dmax = self._fit_prep64()
             R64 = torch.where(Rm, torch.zeros_like(Xr), Xr).to(torch.float64).contiguous()
             Mx = torch.maximum(dmax, R32.abs().amax().reshape(1)).to(torch.float32).contiguous()
-            work = torch.empty((4 + nr * (1 + 2 * SLOTS + SLOTS * KNN_CAND)), dtype=torch.int32, device=dev)
+            # knn.hip knn_refine scratch: dmin u64 | didx i32 | thr f32 per slot, receiver list, counts
+            work = torch.empty(nr * SLOTS * 2 + nr * SLOTS * 2 + nr + 8, dtype=torch.int32, device=dev)
         for s0 in range(0, nslot, SLOTS):
             slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
             blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)

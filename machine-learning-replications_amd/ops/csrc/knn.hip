@@ -436,24 +436,26 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 // order of fl((x−y)·(x−y)) in f64, × F / |common|, lowest index on ties) except where another
 // donor's distance is within the f32 error of the best.  Those slots are found from the runner-up
 // distance (alt) and re-decided in f64 over the donors whose f32 distance can reach the best:
-//   knn_ambig   : per (receiver, slot): ambiguous ⇔ alt ≤ d1 + W(d1) with W a generous bound of the
-//                 f32 distance error (both distances' errors: 2^-12 relative, plus an absolute term
-//                 for near-duplicate rows scaled by the largest centred magnitude Mx); compacts the
-//                 ambiguous receivers and records each ambiguous slot's f32 threshold;
-//   knn_cand    : the f32 direct-difference scan again, over the ambiguous receivers only (grid
-//                 sized for every receiver, blocks past the device count exit at once), appending
-//                 each donor within its slot's threshold to the slot's candidate list (≤ kKnnCand;
-//                 an overflowing slot is re-scanned over every donor in f64);
-//   knn_resolve : one wave per ambiguous slot: f64 distances of its candidates, (distance, index)
-//                 minimum, written back as the slot's donor.
-// The result does not depend on atomic arrival order (candidates are evaluated as a set).
-constexpr int kKnnCand = 32;
+//   knn_ambig : per (receiver, slot): ambiguous ⇔ alt ≤ d1 + W(d1), W a generous bound of the f32
+//               distance error (both distances' errors: 2^-12 relative plus an absolute term for
+//               near-duplicate rows scaled by the largest centred magnitude Mx); compacts the
+//               ambiguous receivers, records each ambiguous slot's f32 threshold d1 + W;
+//   knn_cand  : the f32 direct-difference scan again, over the ambiguous receivers only (grid
+//               sized for every receiver, blocks past the device count exit at once): every donor
+//               within a slot's threshold gets its f64 distance, and
+//               pass 0 — atomicMin of the slot's f64 minimum (as order-preserving u64 bits),
+//               pass 1 — among the donors whose f64 distance equals it, atomicMin of the index;
+//   knn_commit: the slot's donor ← that index.
+// Cost ≤ two f32 scans of the ambiguous receivers (f64 only for the few donors in a window);
+// the result does not depend on atomic arrival order.
 
 __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long* __restrict__ best,
                                                         const unsigned* __restrict__ alt,
                                                         const int* __restrict__ slot_col, int nr, int F,
                                                         const float* __restrict__ Mx, float* __restrict__ thr,
-                                                        int* __restrict__ rlist, int* __restrict__ counts) {
+                                                        unsigned long long* __restrict__ dmin,
+                                                        int* __restrict__ didx, int* __restrict__ rlist,
+                                                        int* __restrict__ counts) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= nr) return;
   const float M = 2.f * Mx[0], Ff = (float)F;
@@ -465,9 +467,9 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
     const unsigned long long b = best[e];
     if (slot_col[e] >= 0 && b != ~0ull) {
       const float d1 = __uint_as_float((unsigned)(b >> 32));
-      // error of a scaled f32 distance: relative (≤ (F + 8)·2^-24 for positive terms) plus an absolute
-      // part from the rounding of the centred inputs, ~2^-24·M·sqrt(F·d)·F; ×2 for the two distances
-      // compared, ×≥16 margin
+      // error of a scaled f32 distance: relative ≤ (F + 8)·2^-24 for positive terms, plus an
+      // absolute part from the rounding of the centred inputs, ~2^-24·M·sqrt(F·d)·F; ×2 for the two
+      // distances compared, ≥ 16× margin
       const float W = 0x1p-12f * d1 + 0x1p-16f * Ff * M * sqrtf(Ff * d1) + 0x1p-28f * Ff * Ff * M * M;
       const unsigned a = alt[e];
       if (a != 0xFFFFFFFFu && __uint_as_float(a) <= d1 + W) {
@@ -476,16 +478,35 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
       }
     }
     thr[e] = t;
+    dmin[e] = ~0ull;
+    didx[e] = 0x7fffffff;
   }
   if (any) rlist[atomicAdd(&counts[0], 1)] = r;
 }
 
-template <int FMAX>
+// f64 distance of the mirror: common features in order, fl((x−y)·(x−y)) summed, × F / |common|
+#pragma clang fp contract(off)
+__device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsigned long long mr,
+                                             const double* __restrict__ y, unsigned long long md, int F) {
+  double s = 0.0;
+  int present = 0;
+  for (int f = 0; f < F; ++f) {
+    if (((mr | md) >> f) & 1ull) continue;
+    const double t = x[f] - y[f];
+    s = s + t * t;
+    ++present;
+  }
+  return present > 0 ? (s * (double)F) / (double)present : INFINITY;
+}
+#pragma clang fp contract(on)
+
+template <int FMAX, int PASS>
 __global__ __launch_bounds__(256) void knn_cand_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, const int* __restrict__ rlist,
     const int* __restrict__ counts, const float* __restrict__ D, const unsigned long long* __restrict__ dmask,
     int nd, int F, int per_split, const int* __restrict__ slot_col, const float* __restrict__ thr,
-    int* __restrict__ ccount, int* __restrict__ cand) {
+    const double* __restrict__ R64, const double* __restrict__ D64, unsigned long long* __restrict__ dmin,
+    int* __restrict__ didx) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
   const int nrl = counts[0];
   if ((int)blockIdx.x * 256 >= nrl) return;   // (grid sized for every receiver)
@@ -513,6 +534,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(
     if (col[k] >= 0) need |= 1ull << col[k];
     tmax = fmaxf(tmax, col[k] >= 0 ? th[k] : -1.f);
   }
+  const double* x64 = R64 + (size_t)r * F;
   for (int d0 = d_begin; d0 < d_end; d0 += kKnnTile) {
     __syncthreads();
     const int nt = min(kKnnTile, d_end - d0);
@@ -549,92 +571,53 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(
       if (present <= 0) continue;
       const float dist = fmaxf(s0 + s1, 0.f) * ((float)F / (float)present);
       if (!(dist <= tmax)) continue;
+      const int di = d0 + t;
+      double d64 = -1.0;   // computed once for the donor, only if some slot's window holds it
 #pragma unroll
       for (int k = 0; k < kKnnSlots; ++k) {
         if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist <= th[k]) {
+          if (d64 < 0.0) d64 = knn_dist64(x64, mr, D64 + (size_t)di * F, md, F);
           const size_t e = (size_t)r * kKnnSlots + k;
-          const int pos = atomicAdd(&ccount[e], 1);
-          if (pos < kKnnCand) cand[e * kKnnCand + pos] = d0 + t;
+          const unsigned long long key = (unsigned long long)__double_as_longlong(d64);   // d64 ≥ 0
+          if constexpr (PASS == 0) atomicMin(&dmin[e], key);
+          else if (key == dmin[e]) atomicMin(&didx[e], di);
         }
       }
     }
   }
 }
 
-// f64 distance of the mirror: common features in order, fl((x−y)·(x−y)) summed, × F / |common|
-#pragma clang fp contract(off)
-__device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsigned long long mr,
-                                             const double* __restrict__ y, unsigned long long md, int F) {
-  double s = 0.0;
-  int present = 0;
-  for (int f = 0; f < F; ++f) {
-    if (((mr | md) >> f) & 1ull) continue;
-    const double t = x[f] - y[f];
-    s = s + t * t;
-    ++present;
-  }
-  return present > 0 ? (s * (double)F) / (double)present : INFINITY;
-}
-#pragma clang fp contract(on)
-
-__global__ __launch_bounds__(64) void knn_resolve_kernel(
-    const double* __restrict__ R64, const unsigned long long* __restrict__ rmask, const int* __restrict__ rlist,
-    const int* __restrict__ counts, const double* __restrict__ D64, const unsigned long long* __restrict__ dmask,
-    int nd, int F, const int* __restrict__ slot_col, const float* __restrict__ thr,
-    const int* __restrict__ ccount, const int* __restrict__ cand, unsigned long long* __restrict__ best) {
+__global__ __launch_bounds__(256) void knn_commit_kernel(const int* __restrict__ rlist, const int* __restrict__ counts,
+                                                         const float* __restrict__ thr,
+                                                         const int* __restrict__ didx,
+                                                         unsigned long long* __restrict__ best) {
   const int nrl = counts[0];
-  const int lane = threadIdx.x;
-  for (int w = blockIdx.x; w < nrl * kKnnSlots; w += gridDim.x) {   // every wave reaches the end
-    const int r = rlist[w / kKnnSlots];
-    const int k = w % kKnnSlots;
-    const size_t e = (size_t)r * kKnnSlots + k;
-    if (thr[e] < 0.f) continue;
-    const int c = slot_col[e];
-    const unsigned long long mr = rmask[r];
-    const double* x = R64 + (size_t)r * F;
-    const int nc = ccount[e];
-    double bd = INFINITY;
-    int bi = 0x7fffffff;
-    auto consider = [&](int d) {
-      const unsigned long long md = dmask[d];
-      if ((md >> c) & 1ull) return;
-      const double dist = knn_dist64(x, mr, D64 + (size_t)d * F, md, F);
-      if (dist < bd || (dist == bd && d < bi)) { bd = dist; bi = d; }
-    };
-    if (nc <= kKnnCand) {
-      for (int p = lane; p < nc; p += 64) consider(cand[e * kKnnCand + p]);
-    } else {
-      for (int d = lane; d < nd; d += 64) consider(d);   // candidate list overflowed: every donor
-    }
-    // (distance, index) minimum over the wave
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double od = __shfl_xor(bd, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
-    }
-    if (lane == 0 && bi != 0x7fffffff)
-      best[e] = (best[e] & 0xFFFFFFFF00000000ull) | (unsigned long long)(unsigned)bi;
+  for (int w = blockIdx.x * 256 + threadIdx.x; w < nrl * kKnnSlots; w += gridDim.x * 256) {
+    const size_t e = (size_t)rlist[w / kKnnSlots] * kKnnSlots + w % kKnnSlots;
+    if (thr[e] >= 0.f && didx[e] != 0x7fffffff)
+      best[e] = (best[e] & 0xFFFFFFFF00000000ull) | (unsigned long long)(unsigned)didx[e];
   }
 }
 
+// work: 8-byte aligned scratch of knn_refine_work_words(nr) int32 words
 void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
                 uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t R64, uintptr_t D64, uintptr_t Mx,
                 uintptr_t work, uintptr_t stream) {
-  // work: int32 [1 + nr + nr·8 (ccount) + nr·8·kKnnCand (cand)] + f32 [nr·8] (thr), zeroed here
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_refine: 1 <= F <= 64");
+  HFENS_REQUIRE((work & 7) == 0, "knn_refine: work must be 8-byte aligned");
   if (nr == 0 || nd == 0) return;
   hipStream_t st = as_stream(stream);
-  int* counts = (int*)work;
-  int* rlist = counts + 4;
-  int* ccount = rlist + nr;
-  int* cand = ccount + (size_t)nr * kKnnSlots;
-  float* thr = (float*)(cand + (size_t)nr * kKnnSlots * kKnnCand);
+  // layout: dmin u64 [nr·8] | didx i32 [nr·8] | thr f32 [nr·8] | rlist i32 [nr] | counts i32 [4]
+  unsigned long long* dmin = (unsigned long long*)work;
+  int* didx = (int*)(dmin + (size_t)nr * kKnnSlots);
+  float* thr = (float*)(didx + (size_t)nr * kKnnSlots);
+  int* rlist = (int*)(thr + (size_t)nr * kKnnSlots);
+  int* counts = rlist + nr;
   HFENS_CHECK(hipMemsetAsync(counts, 0, 4 * sizeof(int), st));
-  HFENS_CHECK(hipMemsetAsync(ccount, 0, (size_t)nr * kKnnSlots * sizeof(int), st));
   const int rb = (nr + 255) / 256;
   hipLaunchKernelGGL(knn_ambig_kernel, dim3(rb), dim3(256), 0, st, (const unsigned long long*)best,
-                     (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, rlist, counts);
+                     (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, dmin, didx, rlist,
+                     counts);
   launch_check();
   int splits = (nd + 16383) / 16384;
   if (splits < 1) splits = 1;
@@ -645,9 +628,14 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
     per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
     const int nsp = (nd + per - 1) / per;
     const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
-    hipLaunchKernelGGL(knn_cand_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
+    hipLaunchKernelGGL((knn_cand_kernel<FM, 0>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                        (const unsigned long long*)rmask, rlist, counts, (const float*)D,
-                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, ccount, cand);
+                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, (const double*)R64,
+                       (const double*)D64, dmin, didx);
+    hipLaunchKernelGGL((knn_cand_kernel<FM, 1>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
+                       (const unsigned long long*)rmask, rlist, counts, (const float*)D,
+                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, (const double*)R64,
+                       (const double*)D64, dmin, didx);
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
@@ -655,14 +643,11 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   else if (F <= 40) go(std::integral_constant<int, 40>{});
   else if (F <= 48) go(std::integral_constant<int, 48>{});
   else go(std::integral_constant<int, 64>{});
-  int grid = nr * kKnnSlots;
+  int grid = (nr * kKnnSlots + 255) / 256;
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(knn_resolve_kernel, dim3(grid), dim3(64), 0, st, (const double*)R64,
-                     (const unsigned long long*)rmask, rlist, counts, (const double*)D64,
-                     (const unsigned long long*)dmask, nd, F, (const int*)slot_col, thr, ccount, cand,
+  hipLaunchKernelGGL(knn_commit_kernel, dim3(grid), dim3(256), 0, st, rlist, counts, thr, didx,
                      (unsigned long long*)best);
   launch_check();
 }
-
 
 }  // namespace hfens
