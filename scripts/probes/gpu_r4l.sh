@@ -3,11 +3,11 @@
 set -o pipefail
 D=gpurun_out/r4l
 mkdir -p $D
-timeout -k 10 300 python -u -m pytest tests/test_prep_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > $D/pytest_prep.log 2>&1 || { echo "pytest prep failed"; tail -40 $D/pytest_prep.log; exit 1; }
-tail -3 $D/pytest_prep.log
-timeout -k 10 200 python -u -m pytest tests/test_linalg_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "chol" > $D/pytest_chol.log 2>&1 || { echo "pytest chol failed"; tail -40 $D/pytest_chol.log; exit 1; }
-tail -3 $D/pytest_chol.log
-timeout -k 10 560 python -u -m pytest tests/test_train_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "device_svc_oof or plan_ahead or develop or lowrank_svc_row_sharded or gbdt_stage_xgmi" > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $D/pytest.log; exit 1; }
+echo skip-prep
+
+echo skip-chol
+
+timeout -k 10 560 python -u -m pytest tests/test_train_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "device_svc_oof" > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $D/pytest.log; exit 1; }
 tail -3 $D/pytest.log
 for k in 1 0; do
   HFENS_DEVICE_SVC_OOF=$k timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $D/bench_oof$k.json 2> $D/bench_oof$k.err || { echo "bench failed"; tail -30 $D/bench_oof$k.err; exit 1; }
