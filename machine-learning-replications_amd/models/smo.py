@@ -635,6 +635,10 @@ def _solve_exact(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s):
 # 0.05 39.1, 0.1 34.3, 0.15 33.7, 0.2 31.4-31.8, 0.25 32.2, 0.3 32.8 ms/fit — 0.2 moves 13 % fewer pairs
 # (8.6k vs 9.9k on the critical problem) in about as many rounds (35 vs 34)
 WS_INNER_FRAC = float(os.environ.get("HFENS_SVM_WS_FRAC", "0.2"))
+# the same for the group holding the largest problem (the fit's critical path when groups run
+# side by side); host simulation of the bench's 10k problem (scripts/probes/ws_qsim.py, q = 1024):
+# 0.2 → 37 rounds / 8.4k pairs, 0.3 → 39 / 8.0k, 0.4 → 46 / 7.9k
+WS_INNER_FRAC_BIG = float(os.environ.get("HFENS_SVM_WS_FRAC_BIG", str(WS_INNER_FRAC)))
 # inner pairs per round: the 36 problems advance in lock-step rounds, so one long inner solve holds
 # up every other problem's next round; a cap bounds that wait (the capped problem simply continues
 # in its next working set)
@@ -733,7 +737,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             st = side.cuda_stream
         runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
                               side, zn, alpha, G, keys, hist, n, Q, Fp2, kc_all, gi=gi if use_graph else None,
-                              cap_stream=(side if side is not None else caller) if use_graph else None))
+                              cap_stream=(side if side is not None else caller) if use_graph else None,
+                              frac=WS_INNER_FRAC_BIG if (gi == 0 and len(groups) > 1) else WS_INNER_FRAC))
     from ..utils.timing import hmark
     hmark("ws_groups_ready")
     # HFENS_WS_EVENTS=1 (diagnostic): device events per group after every enqueued chunk, read by
@@ -811,12 +816,13 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
 
 
 def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, s, side,
-              zn, alpha, G, keys, hist, n, Q, Fp2, kc=False, gi=None, cap_stream=None):
+              zn, alpha, G, keys, hist, n, Q, Fp2, kc=False, gi=None, cap_stream=None, frac=None):
     """State of the problems ``live[idx]``, whose rounds go on stream ``s`` (per-problem state is
     group-local; the per-point arrays are the shared ones, addressed by each problem's absolute
     offset).  Returns closures: ``steps(k)`` enqueues k rounds, ``sync_rounds(chunk)`` runs
     host-checked rounds until every problem is done, ``finish()`` enqueues the ρ / statistics pass."""
     P = len(idx)
+    frac = WS_INNER_FRAC if frac is None else frac
     arr = np.zeros(P, _WS_DT)
     for k, j in enumerate(idx):
         p = live[j]
@@ -867,7 +873,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
     def steps(k):
         if graph:
             # one captured graph per (group, shape, buffers, round count); replayed on the group's stream
-            key = (gi, P, max_l, F, n, k, eps, max_outer, max_inner, WS_INNER_FRAC,
+            key = (gi, P, max_l, F, n, k, eps, max_outer, max_inner, frac,
                    tuple(int(t.data_ptr()) for t in (pdev, zcat, zn, alpha, G, states, wsz, wsn, wdc, wsprev,
                                                         keys, gkey)), int(cand.data_ptr()) if cand is not None else 0)
             g = _WS_GRAPHS.get(key)
@@ -893,11 +899,11 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
                           G.data_ptr(), states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(),
                           wsprev.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(),
                           cand.data_ptr() if cand is not None else 0, eps, max_outer, max_inner,
-                          WS_INNER_FRAC, k, wprof.data_ptr() if wprof is not None else 0, s)
+                          frac, k, wprof.data_ptr() if wprof is not None else 0, s)
             return
         E.ws_steps(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                    states.data_ptr(), wsz.data_ptr(), wsn.data_ptr(), wdc.data_ptr(), wsprev.data_ptr(),
-                   wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, WS_INNER_FRAC,
+                   wsidx.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), eps, max_outer, max_inner, frac,
                    k, wprof.data_ptr() if wprof is not None else 0, WS_THREADS, Q, s)
 
     def sync_rounds(steps_per_check):
