@@ -652,6 +652,7 @@ WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # round
 _WS_GRAPHS: dict = {}
 WS_BIG_CHUNK = int(os.environ.get("HFENS_SVM_WS_BIG_CHUNK", "64"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
+_WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
 # Lock-step decoupling: one round kernel ends when its SLOWEST problem's inner solve does, so the
