@@ -619,7 +619,14 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
                      (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, dmin, didx, rlist,
                      counts);
   launch_check();
-  int splits = (nd + 16383) / 16384;
+  // donor splits as in knn_donors (≥ 2048 workgroups, ≤ 16k donors each): the ambiguous receivers
+  // are often a large share at 10k rows (binary features tie exactly), and ⌈nr/256⌉ workgroups alone
+  // would leave most CUs idle; blocks past the device receiver count exit at once
+  int splits = 2048 / rb;
+  const int by_range = (nd + 16383) / 16384;
+  if (splits < by_range) splits = by_range;
+  const int max_splits = (nd + kKnnTile - 1) / kKnnTile;
+  if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   auto go = [&](auto fm) {
     constexpr int FM = decltype(fm)::value;
