@@ -89,7 +89,7 @@ class KNNImputer(Estimator):
             # the f64 refine's operands: raw values zero-filled (the host mirror's arithmetic) and the
             # largest centred magnitude (its error window), both left on the device
             D64 = D.to(torch.float64).contiguous()
-            dmax = D32.abs().amax().reshape(1) if D32.numel() else torch.zeros(1, device=D.device)
+            dmax = D32.abs().amax(0) if D32.numel() else torch.zeros(D32.shape[1], device=D.device)
             pr = self._prep = (self._fit_X, D32, dm, D64, dmax)
         return pr[1], pr[2]
 
@@ -187,7 +187,10 @@ class KNNImputer(Estimator):
         if EXACT:
             D64, dmax = self._fit_prep64()
             R64 = torch.where(Rm, torch.zeros_like(Xr), Xr).to(torch.float64).contiguous()
-            Mx = torch.maximum(dmax, R32.abs().amax().reshape(1)).to(torch.float32).contiguous()
+            # ‖m‖, m_f = the largest centred magnitude of column f over donors and receivers (the
+            # f32 error bound of knn.hip knn_ambig)
+            Mx = torch.linalg.vector_norm(torch.maximum(dmax, R32.abs().amax(0)).to(torch.float64)).reshape(1)
+            Mx = Mx.to(torch.float32).contiguous()
             # knn.hip knn_refine scratch: dmin u64 | didx i32 | thr f32 per slot, receiver list, counts
             work = torch.empty(nr * SLOTS * 2 + nr * SLOTS * 2 + nr + 8, dtype=torch.int32, device=dev)
         for s0 in range(0, nslot, SLOTS):

@@ -436,9 +436,9 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 // order of fl((x−y)·(x−y)) in f64, × F / |common|, lowest index on ties) except where another
 // donor's distance is within the f32 error of the best.  Those slots are found from the runner-up
 // distance (alt) and re-decided in f64 over the donors whose f32 distance can reach the best:
-//   knn_ambig : per (receiver, slot): ambiguous ⇔ alt ≤ d1 + W(d1), W a generous bound of the f32
-//               distance error (both distances' errors: 2^-12 relative plus an absolute term for
-//               near-duplicate rows scaled by the largest centred magnitude Mx); compacts the
+//   knn_ambig : per (receiver, slot): ambiguous ⇔ alt ≤ d1 + W(d1), W a bound of the f32 distance
+//               error (both distances, ×8 margin; a relative term and one in sqrt(d) scaled by the
+//               per-column largest centred magnitudes, for near-duplicate rows); compacts the
 //               ambiguous receivers, records each ambiguous slot's f32 threshold d1 + W;
 //   knn_cand  : the f32 direct-difference scan again, over the ambiguous receivers only (grid
 //               sized for every receiver, blocks past the device count exit at once): every donor
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
                                                         int* __restrict__ counts) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= nr) return;
-  const float M = 2.f * Mx[0], Ff = (float)F;
+  const float mn = Mx[0], Ff = (float)F;   // ‖m‖: norm over columns of the largest centred magnitude
   bool any = false;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k) {
@@ -467,10 +467,12 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
     const unsigned long long b = best[e];
     if (slot_col[e] >= 0 && b != ~0ull) {
       const float d1 = __uint_as_float((unsigned)(b >> 32));
-      // error of a scaled f32 distance: relative ≤ (F + 8)·2^-24 for positive terms, plus an
-      // absolute part from the rounding of the centred inputs, ~2^-24·M·sqrt(F·d)·F; ×2 for the two
-      // distances compared, ≥ 16× margin
-      const float W = 0x1p-12f * d1 + 0x1p-16f * Ff * M * sqrtf(Ff * d1) + 0x1p-28f * Ff * Ff * M * M;
+      // error of a scaled f32 distance d = (F/p)·Σ δ_f² with δ_f the difference of two f32-rounded
+      // centred values: each δ_f is off by ≤ u(|x_f−c_f| + |y_f−c_f| + |δ_f|), u = 2^-24, so
+      //   |Δd| ≤ 8u·‖m‖·sqrt(F·d) + (F+2)u·d + 4F²u²‖m‖²      (Cauchy–Schwarz, F/p ≤ F)
+      // with m_f the largest centred magnitude of column f; ×2 for the two distances compared and
+      // ×8 margin
+      const float W = 0x1p-20f * (8.f * mn * sqrtf(Ff * d1) + (Ff + 2.f) * d1) + 0x1p-42f * Ff * Ff * mn * mn;
       const unsigned a = alt[e];
       if (a != 0xFFFFFFFFu && __uint_as_float(a) <= d1 + W) {
         t = d1 + W;

@@ -12,7 +12,7 @@ run() {
   python -c "import json; d=json.loads(open('$D/$name.json').read().strip().split('\n')[-1]); print('$name', d['ms_per_step'], d['diag']['step_ms_min_med_max'], d['auroc'], d['diag']['svm'].get('ws_rounds_max'), d['diag']['svm'].get('ws_pairs_max'))"
 }
 run base HFENS_X=0 &&
-run fracbig3 HFENS_SVM_WS_FRAC_BIG=0.3 &&
+
 run knn_f32 HFENS_KNN_EXACT=0 &&
 HFENS_TRACE_HOST=1 timeout -k 10 200 python -u scripts/probes/ws_events.py > $D/ev_host.log 2>&1 || { echo "events failed"; tail -30 $D/ev_host.log; exit 1; }
 tail -5 $D/ev_host.log
