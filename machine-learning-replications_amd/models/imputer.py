@@ -191,8 +191,9 @@ class KNNImputer(Estimator):
             # f32 error bound of knn.hip knn_ambig)
             Mx = torch.linalg.vector_norm(torch.maximum(dmax, R32.abs().amax(0)).to(torch.float64)).reshape(1)
             Mx = Mx.to(torch.float32).contiguous()
-            # knn.hip knn_refine scratch: dmin u64 | didx i32 | thr f32 per slot, receiver list, counts
-            work = torch.empty(nr * SLOTS * 2 + nr * SLOTS * 2 + nr + 8, dtype=torch.int32, device=dev)
+            # knn.hip knn_refine scratch: dmin, dwin u64 | didx, didx2 i32 | thr, thr2 f32 per slot;
+            # two receiver lists; counts
+            work = torch.empty(nr * SLOTS * 8 + 2 * nr + 8, dtype=torch.int32, device=dev)
         for s0 in range(0, nslot, SLOTS):
             slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
             blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)

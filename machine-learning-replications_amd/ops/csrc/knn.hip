@@ -442,12 +442,17 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 //               ambiguous receivers, records each ambiguous slot's f32 threshold d1 + W;
 //   knn_cand  : the f32 direct-difference scan again, over the ambiguous receivers only (grid
 //               sized for every receiver, blocks past the device count exit at once): every donor
-//               within a slot's threshold gets its f64 distance, and
-//               pass 0 — atomicMin of the slot's f64 minimum (as order-preserving u64 bits),
-//               pass 1 — among the donors whose f64 distance equals it, atomicMin of the index;
+//               within a slot's threshold gets its f64 distance, compared with the f32 winner's
+//               own (computed by knn_ambig): pass 0 — at it, atomicMin of the index (exact ties:
+//               the lowest index, as the mirror's argmin); below it, atomicMin of the new f64
+//               minimum (order-preserving u64 bits); pass 1 — only over the receivers where pass 0
+//               found a strictly smaller f64 distance (rare): the lowest index at that minimum;
 //   knn_commit: the slot's donor ← that index.
-// Cost ≤ two f32 scans of the ambiguous receivers (f64 only for the few donors in a window);
+// Cost ≈ one f32 scan of the ambiguous receivers (f64 only for the donors in a window);
 // the result does not depend on atomic arrival order.
+
+__device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsigned long long mr,
+                                             const double* __restrict__ y, unsigned long long md, int F);
 
 __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long* __restrict__ best,
                                                         const unsigned* __restrict__ alt,
@@ -455,7 +460,12 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
                                                         const float* __restrict__ Mx, float* __restrict__ thr,
                                                         unsigned long long* __restrict__ dmin,
                                                         int* __restrict__ didx, int* __restrict__ rlist,
-                                                        int* __restrict__ counts) {
+                                                        int* __restrict__ counts,
+                                                        const double* __restrict__ R64,
+                                                        const unsigned long long* __restrict__ rmask,
+                                                        const double* __restrict__ D64,
+                                                        const unsigned long long* __restrict__ dmask,
+                                                        unsigned long long* __restrict__ dwin) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= nr) return;
   const float mn = Mx[0], Ff = (float)F;   // ‖m‖: norm over columns of the largest centred magnitude
@@ -480,8 +490,18 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
       }
     }
     thr[e] = t;
-    dmin[e] = ~0ull;
-    didx[e] = 0x7fffffff;
+    // the f32 winner's own f64 distance: pass 0 looks for donors strictly below it (rare) and, at it,
+    // for a lower index; only slots where something strictly below exists need pass 1
+    unsigned long long w64 = ~0ull;
+    int wi = 0x7fffffff;
+    if (t >= 0.f) {
+      wi = (int)(unsigned)(b & 0xFFFFFFFFull);
+      w64 = (unsigned long long)__double_as_longlong(
+          knn_dist64(R64 + (size_t)r * F, rmask[r], D64 + (size_t)wi * F, dmask[wi], F));
+    }
+    dwin[e] = w64;
+    dmin[e] = w64;
+    didx[e] = wi;
   }
   if (any) rlist[atomicAdd(&counts[0], 1)] = r;
 }
@@ -508,7 +528,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(
     const int* __restrict__ counts, const float* __restrict__ D, const unsigned long long* __restrict__ dmask,
     int nd, int F, int per_split, const int* __restrict__ slot_col, const float* __restrict__ thr,
     const double* __restrict__ R64, const double* __restrict__ D64, unsigned long long* __restrict__ dmin,
-    int* __restrict__ didx) {
+    int* __restrict__ didx, const unsigned long long* __restrict__ dwin, int* __restrict__ didx2) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
   const int nrl = counts[0];
   if ((int)blockIdx.x * 256 >= nrl) return;   // (grid sized for every receiver)
@@ -581,23 +601,52 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(
           if (d64 < 0.0) d64 = knn_dist64(x64, mr, D64 + (size_t)di * F, md, F);
           const size_t e = (size_t)r * kKnnSlots + k;
           const unsigned long long key = (unsigned long long)__double_as_longlong(d64);   // d64 ≥ 0
-          if constexpr (PASS == 0) atomicMin(&dmin[e], key);
-          else if (key == dmin[e]) atomicMin(&didx[e], di);
+          if constexpr (PASS == 0) {
+            // dmin starts at the f32 winner's f64 distance: below it → a new minimum (pass 1 finds
+            // its lowest index); at it → a lower index at the winner's distance
+            if (key < dwin[e]) atomicMin(&dmin[e], key);
+            else if (key == dwin[e]) atomicMin(&didx[e], di);
+          } else if (key == dmin[e]) {
+            atomicMin(&didx2[e], di);
+          }
         }
       }
     }
   }
 }
 
+__global__ __launch_bounds__(256) void knn_pass1_list_kernel(const int* __restrict__ rlist, const int* __restrict__ counts,
+                                                             const float* __restrict__ thr,
+                                                             const unsigned long long* __restrict__ dmin,
+                                                             const unsigned long long* __restrict__ dwin,
+                                                             float* __restrict__ thr2, int* __restrict__ didx2,
+                                                             int* __restrict__ rlist2, int* __restrict__ counts2) {
+  const int nrl = counts[0];
+  for (int w = blockIdx.x * 256 + threadIdx.x; w < nrl; w += gridDim.x * 256) {
+    const int r = rlist[w];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < kKnnSlots; ++k) {
+      const size_t e = (size_t)r * kKnnSlots + k;
+      const bool need = thr[e] >= 0.f && dmin[e] < dwin[e];
+      thr2[e] = need ? thr[e] : -1.f;
+      didx2[e] = 0x7fffffff;
+      any |= need;
+    }
+    if (any) rlist2[atomicAdd(&counts2[0], 1)] = r;
+  }
+}
+
 __global__ __launch_bounds__(256) void knn_commit_kernel(const int* __restrict__ rlist, const int* __restrict__ counts,
-                                                         const float* __restrict__ thr,
-                                                         const int* __restrict__ didx,
+                                                         const float* __restrict__ thr, const float* __restrict__ thr2,
+                                                         const int* __restrict__ didx, const int* __restrict__ didx2,
                                                          unsigned long long* __restrict__ best) {
   const int nrl = counts[0];
   for (int w = blockIdx.x * 256 + threadIdx.x; w < nrl * kKnnSlots; w += gridDim.x * 256) {
     const size_t e = (size_t)rlist[w / kKnnSlots] * kKnnSlots + w % kKnnSlots;
-    if (thr[e] >= 0.f && didx[e] != 0x7fffffff)
-      best[e] = (best[e] & 0xFFFFFFFF00000000ull) | (unsigned long long)(unsigned)didx[e];
+    if (thr[e] < 0.f) continue;
+    const int d = thr2[e] >= 0.f ? didx2[e] : didx[e];
+    if (d != 0x7fffffff) best[e] = (best[e] & 0xFFFFFFFF00000000ull) | (unsigned long long)(unsigned)d;
   }
 }
 
@@ -609,17 +658,25 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   HFENS_REQUIRE((work & 7) == 0, "knn_refine: work must be 8-byte aligned");
   if (nr == 0 || nd == 0) return;
   hipStream_t st = as_stream(stream);
-  // layout: dmin u64 [nr·8] | didx i32 [nr·8] | thr f32 [nr·8] | rlist i32 [nr] | counts i32 [4]
+  // layout: dmin u64 | dwin u64 [nr·8] | didx | didx2 i32 [nr·8] | thr | thr2 f32 [nr·8] | rlist | rlist2
+  // i32 [nr] | counts i32 [4] | counts2 i32 [4]
+  const size_t ns = (size_t)nr * kKnnSlots;
   unsigned long long* dmin = (unsigned long long*)work;
-  int* didx = (int*)(dmin + (size_t)nr * kKnnSlots);
-  float* thr = (float*)(didx + (size_t)nr * kKnnSlots);
-  int* rlist = (int*)(thr + (size_t)nr * kKnnSlots);
-  int* counts = rlist + nr;
-  HFENS_CHECK(hipMemsetAsync(counts, 0, 4 * sizeof(int), st));
+  unsigned long long* dwin = dmin + ns;
+  int* didx = (int*)(dwin + ns);
+  int* didx2 = didx + ns;
+  float* thr = (float*)(didx2 + ns);
+  float* thr2 = thr + ns;
+  int* rlist = (int*)(thr2 + ns);
+  int* rlist2 = rlist + nr;
+  int* counts = rlist2 + nr;
+  int* counts2 = counts + 4;
+  HFENS_CHECK(hipMemsetAsync(counts, 0, 8 * sizeof(int), st));
   const int rb = (nr + 255) / 256;
   hipLaunchKernelGGL(knn_ambig_kernel, dim3(rb), dim3(256), 0, st, (const unsigned long long*)best,
                      (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, dmin, didx, rlist,
-                     counts);
+                     counts, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
+                     (const unsigned long long*)dmask, dwin);
   launch_check();
   // donor splits as in knn_donors (≥ 2048 workgroups, ≤ 16k donors each): the ambiguous receivers
   // are often a large share at 10k rows (binary features tie exactly), and ⌈nr/256⌉ workgroups alone
@@ -640,11 +697,15 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
     hipLaunchKernelGGL((knn_cand_kernel<FM, 0>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                        (const unsigned long long*)rmask, rlist, counts, (const float*)D,
                        (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, (const double*)R64,
-                       (const double*)D64, dmin, didx);
+                       (const double*)D64, dmin, didx, (const unsigned long long*)dwin, didx2);
+    int g1 = rb < 1024 ? rb : 1024;
+    hipLaunchKernelGGL(knn_pass1_list_kernel, dim3(g1), dim3(256), 0, st, rlist, counts, thr, dmin,
+                       (const unsigned long long*)dwin, thr2, didx2, rlist2, counts2);
+    // pass 1 only over the receivers where a donor beat the f32 winner in f64 (usually none)
     hipLaunchKernelGGL((knn_cand_kernel<FM, 1>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
-                       (const unsigned long long*)rmask, rlist, counts, (const float*)D,
-                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, (const double*)R64,
-                       (const double*)D64, dmin, didx);
+                       (const unsigned long long*)rmask, rlist2, counts2, (const float*)D,
+                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr2, (const double*)R64,
+                       (const double*)D64, dmin, didx, (const unsigned long long*)dwin, didx2);
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
@@ -654,7 +715,7 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   else go(std::integral_constant<int, 64>{});
   int grid = (nr * kKnnSlots + 255) / 256;
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(knn_commit_kernel, dim3(grid), dim3(256), 0, st, rlist, counts, thr, didx,
+  hipLaunchKernelGGL(knn_commit_kernel, dim3(grid), dim3(256), 0, st, rlist, counts, thr, thr2, didx, didx2,
                      (unsigned long long*)best);
   launch_check();
 }

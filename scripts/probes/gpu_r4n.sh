@@ -20,4 +20,4 @@ R=$PWD
 cd /tmp && export TMPDIR=/tmp && cd $R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o hb --output-format csv -- python bench.py --steps 5 --warmup 2 > $D/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $D/prof.log; exit 1; }
 f=$(find $D/prof -name "*kernel_stats.csv" | head -1)
-cut -c1-120 $f | head -16
+cut -c1-120 $f > $D/kstats_short.txt; tail -n +1 $D/kstats_short.txt | sed -n 1,16p
