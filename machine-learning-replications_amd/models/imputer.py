@@ -19,6 +19,8 @@ from .base import Estimator, as_tensor
 SLOTS = 8
 # f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
 EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
+KNN_DEBUG = __import__("os").environ.get("HFENS_KNN_DEBUG", "0") == "1"
+LAST_REFINE: list = []
 
 
 def _masks_u64(miss: torch.Tensor) -> torch.Tensor:
@@ -191,9 +193,10 @@ class KNNImputer(Estimator):
             # f32 error bound of knn.hip knn_ambig)
             Mx = torch.linalg.vector_norm(torch.maximum(dmax, R32.abs().amax(0)).to(torch.float64)).reshape(1)
             Mx = Mx.to(torch.float32).contiguous()
-            # knn.hip knn_refine scratch: dmin, dwin u64 | didx, didx2 i32 | thr, thr2 f32 per slot;
-            # two receiver lists; counts
-            work = torch.empty(nr * SLOTS * 8 + 2 * nr + 8, dtype=torch.int32, device=dev)
+            # knn.hip knn_refine scratch: pair keys u64 [cap] | dmin, dwin u64 | didx, didx2 i32 | thr, thr2
+            # f32 per slot | pairs [2·cap] | two receiver lists | counts
+            cap = max(1 << 18, 16 * nr)
+            work = torch.empty(4 * cap + nr * SLOTS * 8 + 2 * nr + 12, dtype=torch.int32, device=dev)
         for s0 in range(0, nslot, SLOTS):
             slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
             blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)
@@ -204,7 +207,11 @@ class KNNImputer(Estimator):
                 # (knn.hip knn_refine) — the donors then equal the host mirror's f64 choice
                 E.knn_refine(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(), D32.shape[0], F,
                              slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
-                             Mx.data_ptr(), work.data_ptr(), ops.stream_ptr(dev))
+                             Mx.data_ptr(), work.data_ptr(), cap, ops.stream_ptr(dev))
+                if KNN_DEBUG:   # re-scanned receivers, window pairs, overflow, pass-1 receivers (synchronising)
+                    o = 4 * cap + 8 * nr * SLOTS + 2 * nr
+                    LAST_REFINE.append((nr, int(work[o]), int(work[o + 8]), int(work[o + 9]), int(work[o + 4]),
+                                        float(Mx[0])))
             if nslot != SLOTS:
                 best[:, s0:s0 + SLOTS] = blk
         hmark("imp_knn_launched")

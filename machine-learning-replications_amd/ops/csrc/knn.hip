@@ -441,14 +441,17 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 //               per-column largest centred magnitudes, for near-duplicate rows); compacts the
 //               ambiguous receivers, records each ambiguous slot's f32 threshold d1 + W;
 //   knn_cand  : the f32 direct-difference scan again, over the ambiguous receivers only (grid
-//               sized for every receiver, blocks past the device count exit at once): every donor
-//               within a slot's threshold gets its f64 distance, compared with the f32 winner's
-//               own (computed by knn_ambig): pass 0 — at it, atomicMin of the index (exact ties:
-//               the lowest index, as the mirror's argmin); below it, atomicMin of the new f64
-//               minimum (order-preserving u64 bits); pass 1 — only over the receivers where pass 0
-//               found a strictly smaller f64 distance (rare): the lowest index at that minimum;
+//               sized for every receiver, blocks past the device count exit at once), listing every
+//               (slot, donor) pair inside the slot's window;
+//   knn_eval  : the pairs in parallel (one thread each — a slot can have thousands of exact-tie
+//               donors, far too many for its scanning thread): the f64 distance, compared with the
+//               f32 winner's own (knn_ambig): at it, atomicMin of the index (exact ties: the lowest
+//               index, as the mirror's argmin); below it, atomicMin of the new f64 minimum
+//               (order-preserving u64 bits); then, for the slots where that happened (rare), the
+//               lowest index at the new minimum.  A list overflow falls back to evaluating in the
+//               scanning threads;
 //   knn_commit: the slot's donor ← that index.
-// Cost ≈ one f32 scan of the ambiguous receivers (f64 only for the donors in a window);
+// Cost ≈ one f32 scan of the ambiguous receivers plus one f64 distance per window pair;
 // the result does not depend on atomic arrival order.
 
 __device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsigned long long mr,
@@ -522,14 +525,19 @@ __device__ __forceinline__ double knn_dist64(const double* __restrict__ x, unsig
 }
 #pragma clang fp contract(on)
 
-template <int FMAX, int PASS>
+// MODE 0: list every (slot, donor) inside a window into pairs (cap entries; counts[1] = pairs,
+// counts[2] = overflow) for the parallel f64 evaluation below.  MODE 1 / 2: the serial fallback
+// used only after an overflow (counts[2] ≠ 0) — pass 0 / pass 1 evaluated in the scanning thread.
+template <int FMAX, int MODE>
 __global__ __launch_bounds__(256) void knn_cand_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, const int* __restrict__ rlist,
     const int* __restrict__ counts, const float* __restrict__ D, const unsigned long long* __restrict__ dmask,
     int nd, int F, int per_split, const int* __restrict__ slot_col, const float* __restrict__ thr,
     const double* __restrict__ R64, const double* __restrict__ D64, unsigned long long* __restrict__ dmin,
-    int* __restrict__ didx, const unsigned long long* __restrict__ dwin, int* __restrict__ didx2) {
+    int* __restrict__ didx, const unsigned long long* __restrict__ dwin, int* __restrict__ didx2,
+    int* __restrict__ pairs, long long cap, int* __restrict__ pcount) {
   constexpr int LD = (FMAX + 3) / 4 * 4;
+  if (MODE != 0 && pcount[1] == 0) return;   // (fallback only after an overflow)
   const int nrl = counts[0];
   if ((int)blockIdx.x * 256 >= nrl) return;   // (grid sized for every receiver)
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -594,23 +602,63 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(
       const float dist = fmaxf(s0 + s1, 0.f) * ((float)F / (float)present);
       if (!(dist <= tmax)) continue;
       const int di = d0 + t;
-      double d64 = -1.0;   // computed once for the donor, only if some slot's window holds it
+      double d64 = -1.0;
 #pragma unroll
       for (int k = 0; k < kKnnSlots; ++k) {
         if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist <= th[k]) {
-          if (d64 < 0.0) d64 = knn_dist64(x64, mr, D64 + (size_t)di * F, md, F);
           const size_t e = (size_t)r * kKnnSlots + k;
-          const unsigned long long key = (unsigned long long)__double_as_longlong(d64);   // d64 ≥ 0
-          if constexpr (PASS == 0) {
-            // dmin starts at the f32 winner's f64 distance: below it → a new minimum (pass 1 finds
-            // its lowest index); at it → a lower index at the winner's distance
-            if (key < dwin[e]) atomicMin(&dmin[e], key);
-            else if (key == dwin[e]) atomicMin(&didx[e], di);
-          } else if (key == dmin[e]) {
-            atomicMin(&didx2[e], di);
+          if constexpr (MODE == 0) {
+            const int p = atomicAdd(&pcount[0], 1);
+            if (p < cap) {
+              pairs[2 * (size_t)p] = (int)e;
+              pairs[2 * (size_t)p + 1] = di;
+            } else {
+              pcount[1] = 1;
+            }
+          } else {
+            if (d64 < 0.0) d64 = knn_dist64(x64, mr, D64 + (size_t)di * F, md, F);
+            const unsigned long long key = (unsigned long long)__double_as_longlong(d64);   // d64 ≥ 0
+            if constexpr (MODE == 1) {
+              if (key < dwin[e]) atomicMin(&dmin[e], key);
+              else if (key == dwin[e]) atomicMin(&didx[e], di);
+            } else if (key == dmin[e]) {
+              atomicMin(&didx2[e], di);
+            }
           }
         }
       }
+    }
+  }
+}
+
+// the listed (slot, donor) pairs in parallel, one per thread: STAGE 0 — the f64 distance (kept),
+// below the f32 winner's → atomicMin of the minimum, at it → of the index; STAGE 1 — at a smaller
+// minimum (slots flagged by knn_pass1_list), the lowest index there
+template <int STAGE>
+__global__ __launch_bounds__(256) void knn_eval_kernel(const int* __restrict__ pairs, const int* __restrict__ pcount,
+                                                       long long cap, const int* __restrict__ slot_col,
+                                                       const double* __restrict__ R64,
+                                                       const unsigned long long* __restrict__ rmask,
+                                                       const double* __restrict__ D64,
+                                                       const unsigned long long* __restrict__ dmask, int F,
+                                                       unsigned long long* __restrict__ keys,
+                                                       unsigned long long* __restrict__ dmin,
+                                                       const unsigned long long* __restrict__ dwin,
+                                                       int* __restrict__ didx, const float* __restrict__ thr2,
+                                                       int* __restrict__ didx2) {
+  const long long np = min((long long)pcount[0], cap);
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < np; p += (long long)gridDim.x * 256) {
+    const size_t e = (size_t)pairs[2 * p];
+    const int di = pairs[2 * p + 1];
+    if constexpr (STAGE == 0) {
+      const int r = (int)(e / kKnnSlots);
+      const double d64 = knn_dist64(R64 + (size_t)r * F, rmask[r], D64 + (size_t)di * F, dmask[di], F);
+      const unsigned long long key = (unsigned long long)__double_as_longlong(d64);
+      keys[p] = key;
+      if (key < dwin[e]) atomicMin(&dmin[e], key);
+      else if (key == dwin[e]) atomicMin(&didx[e], di);
+    } else {
+      if (thr2[e] >= 0.f && keys[p] == dmin[e]) atomicMin(&didx2[e], di);
     }
   }
 }
@@ -653,40 +701,44 @@ __global__ __launch_bounds__(256) void knn_commit_kernel(const int* __restrict__
 // work: 8-byte aligned scratch of knn_refine_work_words(nr) int32 words
 void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
                 uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t R64, uintptr_t D64, uintptr_t Mx,
-                uintptr_t work, uintptr_t stream) {
+                uintptr_t work, long long cap, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_refine: 1 <= F <= 64");
-  HFENS_REQUIRE((work & 7) == 0, "knn_refine: work must be 8-byte aligned");
+  HFENS_REQUIRE((work & 7) == 0 && cap >= 1, "knn_refine: work must be 8-byte aligned, cap >= 1");
   if (nr == 0 || nd == 0) return;
   hipStream_t st = as_stream(stream);
-  // layout: dmin u64 | dwin u64 [nr·8] | didx | didx2 i32 [nr·8] | thr | thr2 f32 [nr·8] | rlist | rlist2
-  // i32 [nr] | counts i32 [4] | counts2 i32 [4]
+  // work (8-byte aligned): keys u64 [cap] | dmin | dwin u64 [nr·8] | didx | didx2 i32 [nr·8] |
+  // thr | thr2 f32 [nr·8] | pairs i32 [2·cap] | rlist | rlist2 i32 [nr] | counts | counts2 | pcount i32 [4]
   const size_t ns = (size_t)nr * kKnnSlots;
-  unsigned long long* dmin = (unsigned long long*)work;
+  unsigned long long* keys = (unsigned long long*)work;
+  unsigned long long* dmin = keys + cap;
   unsigned long long* dwin = dmin + ns;
   int* didx = (int*)(dwin + ns);
   int* didx2 = didx + ns;
   float* thr = (float*)(didx2 + ns);
   float* thr2 = thr + ns;
-  int* rlist = (int*)(thr2 + ns);
+  int* pairs = (int*)(thr2 + ns);
+  int* rlist = pairs + 2 * cap;
   int* rlist2 = rlist + nr;
   int* counts = rlist2 + nr;
   int* counts2 = counts + 4;
-  HFENS_CHECK(hipMemsetAsync(counts, 0, 8 * sizeof(int), st));
+  int* pcount = counts2 + 4;
+  HFENS_CHECK(hipMemsetAsync(counts, 0, 12 * sizeof(int), st));
   const int rb = (nr + 255) / 256;
   hipLaunchKernelGGL(knn_ambig_kernel, dim3(rb), dim3(256), 0, st, (const unsigned long long*)best,
                      (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, dmin, didx, rlist,
                      counts, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
                      (const unsigned long long*)dmask, dwin);
   launch_check();
-  // donor splits as in knn_donors (≥ 2048 workgroups, ≤ 16k donors each): the ambiguous receivers
-  // are often a large share at 10k rows (binary features tie exactly), and ⌈nr/256⌉ workgroups alone
-  // would leave most CUs idle; blocks past the device receiver count exit at once
+  // donor splits as in knn_donors (≥ 2048 workgroups, ≤ 16k donors each); blocks past the device
+  // receiver count exit at once
   int splits = 2048 / rb;
   const int by_range = (nd + 16383) / 16384;
   if (splits < by_range) splits = by_range;
   const int max_splits = (nd + kKnnTile - 1) / kKnnTile;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
+  int eg = (int)((cap + 255) / 256);
+  if (eg > 2048) eg = 2048;
   auto go = [&](auto fm) {
     constexpr int FM = decltype(fm)::value;
     constexpr int LD = (FM + 3) / 4 * 4;
@@ -694,18 +746,27 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
     per = (per + kKnnTile - 1) / kKnnTile * kKnnTile;
     const int nsp = (nd + per - 1) / per;
     const size_t lds = (size_t)kKnnTile * LD * sizeof(float) + kKnnTile * sizeof(unsigned long long);
-    hipLaunchKernelGGL((knn_cand_kernel<FM, 0>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
-                       (const unsigned long long*)rmask, rlist, counts, (const float*)D,
-                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr, (const double*)R64,
-                       (const double*)D64, dmin, didx, (const unsigned long long*)dwin, didx2);
+    auto cand = [&](auto mode, const int* rl, const int* cn, const float* th) {
+      constexpr int MD = decltype(mode)::value;
+      hipLaunchKernelGGL((knn_cand_kernel<FM, MD>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
+                         (const unsigned long long*)rmask, rl, cn, (const float*)D, (const unsigned long long*)dmask,
+                         nd, F, per, (const int*)slot_col, th, (const double*)R64, (const double*)D64, dmin, didx,
+                         (const unsigned long long*)dwin, didx2, pairs, cap, pcount);
+    };
+    cand(std::integral_constant<int, 0>{}, rlist, counts, thr);          // list the window pairs
+    hipLaunchKernelGGL(knn_eval_kernel<0>, dim3(eg), dim3(256), 0, st, (const int*)pairs, (const int*)pcount, cap,
+                       (const int*)slot_col, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
+                       (const unsigned long long*)dmask, F, keys, dmin, (const unsigned long long*)dwin, didx,
+                       (const float*)thr2, didx2);
+    cand(std::integral_constant<int, 1>{}, rlist, counts, thr);          // (overflow only)
     int g1 = rb < 1024 ? rb : 1024;
     hipLaunchKernelGGL(knn_pass1_list_kernel, dim3(g1), dim3(256), 0, st, rlist, counts, thr, dmin,
                        (const unsigned long long*)dwin, thr2, didx2, rlist2, counts2);
-    // pass 1 only over the receivers where a donor beat the f32 winner in f64 (usually none)
-    hipLaunchKernelGGL((knn_cand_kernel<FM, 1>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
-                       (const unsigned long long*)rmask, rlist2, counts2, (const float*)D,
-                       (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col, thr2, (const double*)R64,
-                       (const double*)D64, dmin, didx, (const unsigned long long*)dwin, didx2);
+    hipLaunchKernelGGL(knn_eval_kernel<1>, dim3(eg), dim3(256), 0, st, (const int*)pairs, (const int*)pcount, cap,
+                       (const int*)slot_col, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
+                       (const unsigned long long*)dmask, F, keys, dmin, (const unsigned long long*)dwin, didx,
+                       (const float*)thr2, didx2);
+    cand(std::integral_constant<int, 2>{}, rlist2, counts2, thr2);       // (overflow only)
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
