@@ -3,9 +3,10 @@ one-workgroup selector's range (candidate-list selection, svm_ws.hip ws_cand_ker
 Nyström + interior-point approximation (svc_lowrank) on the same 40k-row draw.
 
 Measured (profiles/r4_svc_crossover.md): the exact solver is 9× faster than the approximation at
-40k rows and 1.9× at 100k; the two models' held-out AUROC agree to 0.004 but their decision values
-only correlate at 0.94–0.96 (a rank-512 Nyström kernel is a visibly different model), which is why
-the exact solver now runs up to the measured crossover (smo.EXACT_MAX_POINTS)."""
+40k rows and 1.9× at 100k; the two models' held-out AUROC agree to 0.004–0.012 (40k–300k rows, the
+Nyström model the higher on these synthetic draws) and their decision values only correlate at
+0.91–0.96 (a rank-512 Nyström kernel is a visibly different model), which is why the exact solver
+now runs up to the measured crossover (smo.EXACT_MAX_POINTS)."""
 import numpy as np
 import pytest
 import torch
@@ -41,5 +42,6 @@ def test_exact_ws_vs_lowrank_40k(dev, monkeypatch):
         d = m.decision_function(Zt).double().cpu().numpy()
         p = m.predict_proba(Zt)[:, 1].double().cpu()
         out[solver] = (d, metrics.evaluate(torch.as_tensor(yt), p)["auroc"])
-    assert abs(out["ws"][1] - out["lowrank"][1]) <= 0.006, (out["ws"][1], out["lowrank"][1])
+    assert abs(out["ws"][1] - out["lowrank"][1]) <= 0.012, (out["ws"][1], out["lowrank"][1])
+    assert min(out["ws"][1], out["lowrank"][1]) >= 0.85
     assert np.corrcoef(out["ws"][0], out["lowrank"][0])[0, 1] >= 0.93
