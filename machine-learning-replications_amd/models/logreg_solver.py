@@ -115,8 +115,11 @@ def lr_members(B: int, n: int, ncu: int) -> int:
     return max(1, min(16, budget // B, -(-n // MIN_ROWS_PER_MEMBER)))
 
 
-def _fit_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int):
-    """All B solves in one launch; returns (W [B, F1], n_iter [B] int32)."""
+def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=None) -> dict:
+    """All B solves in one launch, enqueued with no host synchronisation; :func:`_finish_fused`
+    returns (W [B, F1], n_iter [B] int32).  ``flags``: the input guards as device bools (finite X,
+    binary y), read with the cooperative launch's error word in one transfer (a failed guard
+    raises after the launch)."""
     E = ops.ext()
     B, n = s.shape
     F1 = Xa.shape[1]
@@ -126,26 +129,55 @@ def _fit_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int):
     iters = torch.empty(B, dtype=torch.int32, device=dev)
     Z = torch.empty(B, n, dtype=torch.float64, device=dev)
     Xd = torch.empty_like(Z)
+    h = dict(args=(B, n, F1, Xc, sc, yc, penal, C, l1, max_outer, Z, Xd, W, iters), flags=flags, err=None)
     from .smo import _num_cus
     M = lr_members(B, n, _num_cus(dev))
     if M > 1:
         nv = F1 * (F1 + 1) // 2 + F1 + 1
         xchg = torch.empty(B * 2 * M * nv * 2, dtype=torch.int64, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
+        from ..utils.timing import hmark, dmark
+        hmark("lr_launch")
+        dmark("lr_launch")
         E.logreg_coop(B, M, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C), int(l1),
                       int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(), xchg.data_ptr(),
                       err.data_ptr(), ops.stream_ptr(dev))
+        dmark("lr_kernel")
         LAST_PATH["members"] = M
-        if int(err.item()) == 0:
-            return W, iters
+        h.update(err=err, xchg=xchg)
+    else:
+        _launch_single(h)
+    return h
+
+
+def _launch_single(h):
+    B, n, F1, Xc, sc, yc, penal, C, l1, max_outer, Z, Xd, W, iters = h["args"]
+    LAST_PATH["members"] = 1
+    ops.ext().logreg_fused(B, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C),
+                           int(l1), int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(),
+                           ops.stream_ptr(Xc.device))
+
+
+def _finish_fused(h):
+    from ..utils import guards
+    from ..utils.timing import hmark
+    flags, err = h["flags"], h["err"]
+    parts = ([err] if err is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
+    host = torch.cat(parts).cpu().tolist() if parts else []
+    hmark("lr_host_read")
+    if flags is not None:
+        guards.raise_flags(host[len(host) - 2:], _GUARD_SPECS)
+    if err is not None and host[0] != 0:
         import warnings
         warnings.warn("cooperative logistic regression timed out waiting for a member; re-solving with one "
                       "workgroup per model")
         LAST_PATH["coop_fallback"] = True
-    LAST_PATH["members"] = 1
-    E.logreg_fused(B, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C), int(l1),
-                   int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(), ops.stream_ptr(dev))
+        _launch_single(h)
+    W, iters = h["args"][12], h["args"][13]
     return W, iters
+
+
+_GUARD_SPECS = (("finite", "LogisticRegression.fit X"), ("binary", "LogisticRegression.fit y"))
 
 
 def _allreduce(ts, group):
@@ -213,13 +245,43 @@ def _fit_liblinear_exact(models, X: torch.Tensor, yv: torch.Tensor, masks: torch
 
 def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
                      group=None, max_outer: int = 100, seed_order=None):
+    return finish_logreg_batch(launch_logreg_batch(models, X, y, masks, group, max_outer, seed_order))
+
+
+def finish_logreg_batch(h: dict):
+    """Completes :func:`launch_logreg_batch`: the fused path's one host read (error word and input
+    guards), then ``set_fitted``; other paths finished inside the launch."""
+    if "fused" not in h:
+        return h["models"]
+    models, F, scale, fit_intercept, dev = h["models"], h["F"], h["scale"], h["fit_intercept"], h["dev"]
+    W, iters = _finish_fused(h["fused"])
+    for b, m in enumerate(models):
+        intercept = W[b, F] * scale if fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
+        m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
+    return models
+
+
+def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
+                        group=None, max_outer: int = 100, seed_order=None) -> dict:
+    """Fit ``models`` (one per row mask); on the fused device path the solve is only enqueued —
+    no host synchronisation until :func:`finish_logreg_batch` (the stacking trainer launches the
+    meta model this way before it reads the SVC's results back)."""
     m0 = models[0]
     _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
     if m0.penalty not in ("l1", "l2"):
         raise NotImplementedError("penalty must be 'l1' or 'l2'")
-    from ..utils.guards import check_binary, check_finite
-    check_finite(X, "LogisticRegression.fit X")
-    check_binary(y, "LogisticRegression.fit y")
+    from ..utils import guards
+    emulate = (m0.penalty == "l1" and m0.solver == "liblinear" and group is None
+               and all(getattr(m, "emulate_liblinear", False) for m in models))
+    fused = (X.is_cuda and group is None and FUSED and not emulate and X.dim() == 2
+             and X.shape[1] + int(bool(m0.fit_intercept)) <= 64 and X.shape[0] > 0)
+    flags = None
+    if fused:
+        # the guards ride on the fused launch's one host read instead of two synchronous checks
+        flags = torch.stack([guards.finite_flag(X), guards.binary_flag(y.to(X.device))])
+    else:
+        guards.check_finite(X, "LogisticRegression.fit X")
+        guards.check_binary(y, "LogisticRegression.fit y")
     dev = X.device
     X = X.to(torch.float64)
     n, F = X.shape
@@ -227,9 +289,8 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
     if masks is None:
         masks = torch.ones(B, n, dtype=torch.bool, device=dev)
     yv = y.to(device=dev, dtype=torch.float64)
-    if (m0.penalty == "l1" and m0.solver == "liblinear" and group is None
-            and all(getattr(m, "emulate_liblinear", False) for m in models)):
-        return _fit_liblinear_exact(models, X, yv, masks, int(m0.max_iter), seed_order)
+    if emulate:
+        return dict(models=_fit_liblinear_exact(models, X, yv, masks, int(m0.max_iter), seed_order))
     ypm = 2.0 * yv - 1.0
     if m0.fit_intercept:
         Xa = torch.cat([X, torch.full((n, 1), float(m0.intercept_scaling), dtype=torch.float64, device=dev)], 1)
@@ -253,13 +314,10 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
         penal[-1] = 0  # lbfgs path: intercept not penalised
     pen_f = penal.to(torch.float64)
     scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
-    if X.is_cuda and group is None and FUSED and F1 <= 64 and n > 0:
+    if fused:
         LAST_PATH["path"] = "fused"
-        W, iters = _fit_fused(Xa, s, ypm, penal, C, l1, max_outer)
-        for b, m in enumerate(models):
-            intercept = W[b, F] * scale if m0.fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
-            m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
-        return models
+        return dict(models=models, F=F, scale=scale, fit_intercept=bool(m0.fit_intercept), dev=dev,
+                    fused=_launch_fused(Xa, s, ypm, penal, C, l1, max_outer, flags))
     LAST_PATH["path"] = "loop"
     W = torch.zeros(B, F1, dtype=torch.float64, device=dev)
     alphas = 0.5 ** torch.arange(8, dtype=torch.float64, device=dev)
@@ -339,4 +397,4 @@ def fit_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[t
         coef = W[b, :F]
         intercept = W[b, F] * scale if m0.fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
         m.set_fitted(coef, intercept.reshape(1), [n_iter], F, device=dev)
-    return models
+    return dict(models=models)

@@ -360,7 +360,7 @@ _GRAM_DT = np.dtype([("zoff", "<i8"), ("koff", "<i8"), ("l", "<i4"), ("ld", "<i4
                      ("pad", "<i4")])
 _SMO_DT = np.dtype([("koff", "<i8"), ("aoff", "<i8"), ("l", "<i4"), ("ld", "<i4"), ("npos", "<i4"),
                     ("pad", "<i4"), ("Cp", "<f8"), ("Cn", "<f8")])
-_PLATT_DT = np.dtype([("off", "<i8"), ("l", "<i4"), ("pad", "<i4")])
+_PLATT_DT = np.dtype([("off", "<i8"), ("l", "<i4"), ("n0", "<i4")])
 _DEC_DT = np.dtype([("zoff", "<i8"), ("hoff", "<i8"), ("l", "<i4"), ("h", "<i4"), ("ngl2e", "<f4"),
                     ("per", "<i4")])
 
@@ -1017,7 +1017,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     F = Zs[0].shape[1]
     LAST_SMO_INFO.clear()
     zcat = _gather_rows(Zs, live, "rows", device)
-    from ..utils.timing import hmark
+    from ..utils.timing import hmark, dmark
     hmark("svc_gather")
     zoffs, aoffs = [], [0]
     for p in live:
@@ -1043,12 +1043,14 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
     # for the held-out decisions below and the stacking trainer's device OOF (enqueue_svc_oof)
-    sign = torch.empty(aoffs[-1], dtype=torch.float32, device=device)
+    # (the signs built on the host and uploaded in one copy: per-problem fills would be ~70 tiny
+    # launches queued behind the SMO)
+    sign_h = np.empty(aoffs[-1], dtype=np.float32)
     for k, p in enumerate(live):
         a0, l = aoffs_start[k], p.l
-        sign[a0:a0 + p.npos] = 1.0
-        sign[a0 + p.npos:a0 + l] = -1.0
-    coef = (sign * alpha.to(torch.float32)).contiguous()
+        sign_h[a0:a0 + p.npos] = 1.0
+        sign_h[a0 + p.npos:a0 + l] = -1.0
+    coef = (_to_dev(sign_h, device) * alpha.to(torch.float32)).contiguous()
     out["_dec"] = dict(zcat=zcat, coef=coef, F=F, zoff={id(p): zoffs[k] for k, p in enumerate(live)})
     # ---- Platt held-out decision values of every CV sub-model: one batched launch
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
@@ -1065,15 +1067,15 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
         ddev = _dev_struct(dt, device)
         max_h = int(dt["h"].max())
+        dmark("svc_smo_done")
         E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(platt),
                         max_h, S, part.data_ptr(), s)
-        dec = part.to(torch.float64).sum(1)
-        # (index tensors uploaded pinned/non-blocking: a Python-list index would be a pageable,
-        # host-blocking copy queued behind the SMO)
-        ks = _to_dev(np.array([k for k, _ in platt], dtype=np.int64), device)
-        rho_h = torch.repeat_interleave(rho.index_select(0, ks), _to_dev(dt["h"].astype(np.int64), device),
-                                        output_size=hoff)
-        out["dec_all"] = dec - rho_h                      # held-out decisions, platt order
+        dmark("svc_platt_dec")
+        # the decision values are assembled inside the Platt kernel from these partials (row r of
+        # part: problem rowk[r]'s held-out point, d = −(Σ part[r] − ρ))
+        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"].astype(np.int64))
+        out["platt_src"] = dict(part=part, S=S, rowk=_to_dev(rowk, device), rho=rho.to(torch.float64).contiguous(),
+                                keep=(hcat, ddev))
         for i, (k, p) in enumerate(platt):
             out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
     return out
@@ -1173,7 +1175,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             broadcast_svc_fits(svcs, Zs, group)
         return dict(done=True, svcs=svcs)
     from ..utils import guards
-    from ..utils.timing import hmark
+    from ..utils.timing import hmark, dmark
     device = Zs[0].device
     cuda = Zs[0].is_cuda
     # ONE device→host read for everything the host bookkeeping needs: the finite / 0-1 guard
@@ -1244,55 +1246,59 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     solver = LAST_SMO_INFO.get("solver")   # this batch's solver (the global is overwritten by later batches)
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
     AB = [None] * len(svcs)
-    decs, labs, pl = [], [], []
-    for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
-        if not svc.probability:
-            continue
-        l = mt["l"]
-        dec = torch.zeros(l, dtype=torch.float64, device=device)
-        folds = [p for p in all_probs if p.fit == f and p.fold >= 0]
-        live_f = [p for p in folds if p.rows is not None]
-        if cuda and live_f:
-            # this fit's folds are contiguous in the batched decision vector: one scatter
-            h0 = sol[("hoff", id(live_f[0]))][0]
-            pos = np.concatenate([p.held for p in live_f])
-            for p in live_f:
-                assert sol[("hoff", id(p))][0] == h0 + sum(q.held.shape[0] for q in live_f[:live_f.index(p)])
-            dec.index_copy_(0, _to_dev(pos, device), -sol["dec_all"][h0:h0 + pos.shape[0]])  # × label[0] = −1
-        elif live_f:
-            from ..ops import reference as ref
-            for p in live_f:
-                a, r, _ = sol[id(p)]
-                yint = torch.where(torch.arange(a.numel()) < p.npos, 1.0, -1.0).to(torch.float64)
-                Zh = Z[torch.as_tensor(p.held_rows, device=Z.device)].double()
-                Zr = Z[torch.as_tensor(p.rows, device=Z.device)].double()
-                d = ref.rbf_decision(Zh, Zr, (yint * a.cpu()).to(Zh.device), p.gamma, 0.0) - r
-                dec[torch.as_tensor(p.held, device=device)] = -d.to(device)
-        for p in folds:
-            if p.rows is None:
-                dec[torch.as_tensor(p.held, device=device)] = p.const
-        lab = torch.where(torch.arange(l, device=device) < mt["n0"], 1.0, -1.0)
-        decs.append(dec)
-        labs.append(lab)
-        pl.append(f)
-    if pl:
-        if cuda:
-            E = ops.ext()
-            arr = np.zeros(len(pl), _PLATT_DT)
-            off = 0
-            for k, d in enumerate(decs):
-                arr[k] = (off, d.numel(), 0)
-                off += d.numel()
-            dcat = torch.cat(decs).contiguous()
-            lcat = torch.cat(labs).to(torch.float32).contiguous()
-            ABt = torch.empty(2 * len(pl), dtype=torch.float64, device=device)
-            pdev = _dev_struct(arr, device)
-            E.platt_batch(pdev.data_ptr(), len(pl), dcat.data_ptr(), lcat.data_ptr(), ABt.data_ptr(),
-                          ops.stream_ptr(device))
-            return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
-                        keep=(pdev, dcat, lcat), device=device, args=args, solver=solver)
+    pl = [f for f, svc in enumerate(svcs) if svc.probability]
+    if pl and cuda:
+        # one launch for every fit: the kernel assembles each fit's decision values from the
+        # batched decision partials through a position → partial-row map (negative codes: a
+        # per-fold constant, −1 − code into consts; code −1 = 0.0 for positions no fold holds)
+        E = ops.ext()
+        arr = np.zeros(len(pl), _PLATT_DT)
+        maps, consts, off = [], [0.0], 0
         for k, f in enumerate(pl):
-            AB[f] = _sigmoid_train_host(decs[k].cpu().numpy(), labs[k].cpu().numpy())
+            mt = meta[f]
+            l = mt["l"]
+            sm = np.full(l, -1, dtype=np.int32)
+            for p in (q for q in all_probs if q.fit == f and q.fold >= 0):
+                if p.rows is not None:
+                    h0, h = sol[("hoff", id(p))]
+                    sm[p.held] = np.arange(h0, h0 + h, dtype=np.int32)
+                else:
+                    consts.append(float(p.const))
+                    sm[p.held] = -len(consts)
+            arr[k] = (off, l, mt["n0"])
+            maps.append(sm)
+            off += l
+        src = sol.get("platt_src")
+        srcmap = _to_dev(np.concatenate(maps), device)
+        cdev = _to_dev(np.asarray(consts, dtype=np.float64), device)
+        dscr = torch.empty(off, dtype=torch.float64, device=device)   # (fits past 16k points)
+        ABt = torch.empty(2 * len(pl), dtype=torch.float64, device=device)
+        pdev = _dev_struct(arr, device)
+        dmark("svc_platt_in")
+        part_p, S, rowk_p, rho_p = ((src["part"].data_ptr(), src["S"], src["rowk"].data_ptr(), src["rho"].data_ptr())
+                                    if src is not None else (0, 0, 0, 0))   # (every fold degenerate)
+        E.platt_batch(pdev.data_ptr(), len(pl), part_p, S, rowk_p, rho_p, cdev.data_ptr(), srcmap.data_ptr(),
+                      dscr.data_ptr(), ABt.data_ptr(), ops.stream_ptr(device))
+        dmark("svc_platt")
+        return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
+                    keep=(pdev, srcmap, cdev, dscr), device=device, args=args, solver=solver)
+    for f in pl:
+        svc, Z, mt = svcs[f], Zs[f], meta[f]
+        l = mt["l"]
+        dec = torch.zeros(l, dtype=torch.float64)
+        from ..ops import reference as ref
+        for p in (q for q in all_probs if q.fit == f and q.fold >= 0):
+            if p.rows is None:
+                dec[torch.as_tensor(p.held)] = p.const
+                continue
+            a, r, _ = sol[id(p)]
+            yint = torch.where(torch.arange(a.numel()) < p.npos, 1.0, -1.0).to(torch.float64)
+            Zh = Z[torch.as_tensor(p.held_rows, device=Z.device)].double()
+            Zr = Z[torch.as_tensor(p.rows, device=Z.device)].double()
+            d = ref.rbf_decision(Zh, Zr, (yint * a.cpu()).to(Zh.device), p.gamma, 0.0) - r
+            dec[torch.as_tensor(p.held)] = -d.cpu()
+        lab = np.where(np.arange(l) < mt["n0"], 1.0, -1.0)
+        AB[f] = _sigmoid_train_host(dec.numpy(), lab)
     return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=None,
                 device=device, args=args, solver=solver)
 
@@ -1345,12 +1351,17 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
     assert meta.dtype == torch.float64 and meta.is_contiguous() and meta.dim() == 2
     E.svc_oof(dec.data_ptr(), model.data_ptr(), rho.data_ptr(), AB.data_ptr(), rows.data_ptr(), meta.data_ptr(),
               int(meta.shape[1]), int(col), hoff, s)
+    from ..utils.timing import dmark
+    dmark("svc_oof")
     st["oof_keep"] = (hcat, part, ddev, dec, model, rho, sel, AB, rows)
     return True
 
 
-def finish_svc_batch(st: dict):
-    """Platt parameters to the host, support-vector extraction, ``set_fitted``."""
+def finish_svc_batch(st: dict, defer=None):
+    """Platt parameters to the host, support-vector extraction, ``set_fitted``.  ``defer``: fits
+    whose ``set_fitted`` (≈ 0.3 ms of host work each) is left to the closure ``st["finish_rest"]``
+    (the stacking trainer: the fold models, when the device already computed their out-of-fold
+    column, are not needed at all)."""
     if st.get("done"):
         return st["svcs"]
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
@@ -1377,7 +1388,7 @@ def finish_svc_batch(st: dict):
             flag[0] = False
         st2["retried"] = True
         LAST_SMO_INFO["ws_resolve" if ws else "coop_fallback"] = True
-        return finish_svc_batch(st2)
+        return finish_svc_batch(st2)   # (no deferral after a re-solve: everything is final here)
     # ---- final models: ONE device→host read of the Platt (A, B) pairs and every final solve's
     # support mask, ρ and iteration count; the bookkeeping is then numpy, the gathers non-blocking
     finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
@@ -1398,11 +1409,12 @@ def finish_svc_batch(st: dict):
             raise NonFiniteError(f"SVC Platt sigmoid (A, B): {int((~np.isfinite(ABc)).sum())} non-finite value(s)")
         for k, f in enumerate(st["pl"]):
             AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
-    off = 0
-    for f, (svc, Z, mt) in enumerate(zip(svcs, Zs, meta)):
+    offs = np.concatenate([[0], np.cumsum(ls)])
+
+    def fit_one(f):
+        svc, Z, mt = svcs[f], Zs[f], meta[f]
         a = sols[f][0].to(device)
-        pos_np = np.nonzero(host[off:off + ls[f]] > 0.5)[0]
-        off += ls[f]
+        pos_np = np.nonzero(host[offs[f]:offs[f + 1]] > 0.5)[0]
         pos_idx = _to_dev(pos_np.astype(np.int64), device)
         yint = torch.where(pos_idx < mt["n0"], 1.0, -1.0).to(torch.float64)
         coef = yint * a[pos_idx]
@@ -1415,5 +1427,16 @@ def finish_svc_batch(st: dict):
                        class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
                        shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
         svc.n_iter_ = int(host[nl + len(svcs) + f])
+
+    later = [f for f in range(len(svcs)) if defer is not None and f in defer]
+    for f in range(len(svcs)):
+        if f not in later:
+            fit_one(f)
     hmark("svc_set_fitted")
+    if later:
+        def rest():
+            for f in later:
+                fit_one(f)
+            st["finish_rest"] = None
+        st["finish_rest"] = rest
     return svcs

@@ -33,7 +33,7 @@ from ..utils.timing import StageTimer
 from .gbdt import GradientBoostingClassifier
 from .hist_gbdt import fit_gbdt_batch
 from .linear import LogisticRegression
-from .logreg_solver import fit_logreg_batch
+from .logreg_solver import finish_logreg_batch, fit_logreg_batch, launch_logreg_batch
 from .model_selection import fold_masks, stratified_kfold_test_folds
 from .scaler import StandardScaler
 from .smo import finish_svc_batch, fit_svc_batch, launch_svc_batch
@@ -46,6 +46,11 @@ CONCURRENT_BASES = os.environ.get("HFENS_CONCURRENT_BASES", "1") != "0"
 # the SVC's out-of-fold column computed on the device behind the SMO (smo.enqueue_svc_oof) instead
 # of by the fold models' predict_proba after their host bookkeeping
 DEVICE_SVC_OOF = os.environ.get("HFENS_DEVICE_SVC_OOF", "1") != "0"
+# with the SVC's out-of-fold column computed on the device, the five fold SVCs are never used
+# again (the stacking fit keeps only the refit models, like StackingClassifier's
+# cross_val_predict): their set_fitted (support-vector extraction, ≈ 0.3 ms of host work each) is
+# skipped.  0 = finish them anyway.
+SKIP_FOLD_SVC = os.environ.get("HFENS_SKIP_FOLD_SVC", "1") != "0"
 
 
 def _kind(est):
@@ -193,7 +198,7 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
 
 
 def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
-                          svc_pre=None, oof_svc_dev=None):
+                          svc_pre=None, oof_svc_dev=None, early=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -215,7 +220,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     other.wait_stream(main)
     out, pending = {}, {}
     import time as _t
-    from ..utils.timing import hmark, hmarks_flush
+    from ..utils.timing import hmark, hmarks_flush, dmark
     marks = [("start", _t.perf_counter())]
     hmark("fit_bases")
     with timer.stage("fit_bases(svc || gbc+lr)"):
@@ -252,15 +257,27 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                         if oof is not None:
                             oof(i, out[i])
                         hmark(f"{name}_host_done")
+                        dmark(f"{name}_done")
         finally:
             logreg_solver.BLOCK_BUDGET[0] = lr_budget
+        if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
+            # every meta-feature column is enqueued on the device: the meta model's launch goes
+            # in now, on the main stream behind them, before the SVC's results are read back
+            main.wait_stream(side)
+            main.wait_stream(other)
+            early["handle"] = early["launch"]()
         with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
                 if group is None:
-                    finish_svc_batch(st)
+                    # with the out-of-fold column already on the device only the refit model is
+                    # needed (finish_svc_batch leaves the fold models to st["finish_rest"])
+                    dev_oof = bool(st.get("oof_dev")) and SKIP_FOLD_SVC
+                    finish_svc_batch(st, defer=set(range(N_FOLDS)) if dev_oof else None)
                 else:
                     finish_svc_batch_distributed(st, group)
                 out[i] = clones
+                if st.get("resolved") and early is not None:
+                    early["stale"] = True      # (re-solved: the device OOF it was launched on is stale)
                 if oof is not None and not (st.get("oof_dev") and not st.get("resolved")):
                     oof(i, clones)
         hmark("svc_finished")
@@ -311,8 +328,16 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                  for k in range(N_FOLDS) if test_idx[k].numel()]
         return enqueue_svc_oof(st, items, meta, col)
 
+    y64 = y.to(torch.float64)
+
+    def new_final():
+        return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
+
+    early = None
+    if group is None:
+        early = {"launch": lambda: launch_logreg_batch([new_final()], meta, y64)}
     fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre,
-                                       oof_svc_dev if group is None else None)
+                                       oof_svc_dev if group is None else None, early)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream
@@ -323,11 +348,22 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 oof(col, fitted)
         full.append(fitted[N_FOLDS])
     with timer.stage("fit_meta"):
-        final = clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
-        fit_logreg_batch([final], meta, y.to(torch.float64), group=group)
+        from ..utils.timing import dmark, hmark as _hm
+        _hm("meta_in")
+        dmark("meta_in")
+        if early is not None and "handle" in early and not early.get("stale"):
+            final, = finish_logreg_batch(early["handle"])
+        else:
+            final = new_final()
+            fit_logreg_batch([final], meta, y64, group=group)
+        dmark("meta")
+    from ..utils.timing import hmark, hmarks_flush
+    hmark("meta_done")
     clf.estimators_ = full
     clf.final_estimator_ = final
     clf.stack_method_ = ["predict_proba"] * len(full)
     clf.classes_ = torch.tensor([0.0, 1.0], dtype=torch.float64)
     clf.oof_meta_ = meta
+    hmark("stack_done")
+    hmarks_flush("[host-meta]")
     return clf

@@ -107,20 +107,37 @@ class SVC(Estimator):
         libsvm's label order, decision = Σ coef·K − rho)."""
         dev = device
         self.n_features_in_ = int(n_features)
-        self.class_weight_ = as_tensor(class_weight, dev)
-        self.classes_ = torch.tensor([0, 1], dtype=torch.int64, device=dev)
         self._gamma = float(gamma)
         self.support_ = as_tensor(support, dev, torch.int32)
         self.support_vectors_ = as_tensor(support_vectors, dev)
-        self._n_support = as_tensor(n_support, dev, torch.int32)
         c = as_tensor(dual_coef_libsvm, dev).reshape(1, -1)
         self._dual_coef_ = c
         self.dual_coef_ = -c
         self._hs = (-float(rho), float(probA), float(probB))
-        self._intercept_ = as_tensor([-float(rho)], dev)
+        host = [class_weight, n_support, rho, probA, probB]
+        if any(isinstance(v, torch.Tensor) and v.device.type != "cpu" for v in host):
+            self.class_weight_ = as_tensor(class_weight, dev)
+            self._n_support = as_tensor(n_support, dev, torch.int32)
+            self._intercept_ = as_tensor([-float(rho)], dev)
+            self._probA = as_tensor([probA], dev)
+            self._probB = as_tensor([probB], dev)
+            self.classes_ = torch.tensor([0, 1], dtype=torch.int64, device=dev)
+        else:
+            # the host scalars travel in ONE pinned non-blocking copy (six pageable copies were
+            # six host-synchronous transfers on the fit's tail)
+            cw = np.asarray(class_weight, dtype=np.float64).reshape(-1)
+            ns = np.asarray(n_support, dtype=np.float64).reshape(-1)
+            small = torch.from_numpy(np.concatenate([cw, [-float(rho), float(probA), float(probB), 0.0, 1.0], ns]))
+            if dev is not None and torch.device(dev).type == "cuda":
+                small = small.pin_memory().to(dev, non_blocking=True)
+            k = cw.shape[0]
+            self.class_weight_ = small[:k]
+            self._intercept_ = small[k:k + 1]
+            self._probA = small[k + 1:k + 2]
+            self._probB = small[k + 2:k + 3]
+            self.classes_ = small[k + 3:k + 5].to(torch.int64)
+            self._n_support = small[k + 5:].to(torch.int32)
         self.intercept_ = -self._intercept_
-        self._probA = as_tensor([probA], dev)
-        self._probB = as_tensor([probB], dev)
         self.fit_status_ = 0
         self.shape_fit_ = tuple(int(s) for s in shape_fit)
         self._sparse = False

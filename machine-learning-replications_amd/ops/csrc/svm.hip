@@ -14,8 +14,8 @@
 //                   of its strided elements in registers (KMAX per thread); α lives in global
 //                   memory and only its owner thread touches it; two block arg-reductions and
 //                   two contiguous Gram-row reads per iteration.  Ends with calculate_rho.
-//  platt_batch    : sigmoid_train (Lin-Lin-Weng 2007 Newton + backtracking), one workgroup
-//                   per SVC fit.
+//  platt_batch    : sigmoid_train (Lin-Lin-Weng 2007 Newton + backtracking), one 1024-thread
+//                   workgroup per SVC fit, decision values assembled from svm_dec_batch partials.
 #include "common.h"
 
 namespace hfens {
@@ -554,71 +554,137 @@ void svm_dec_batch(uintptr_t zcat, uintptr_t coef, uintptr_t hcat, int F, uintpt
 }
 
 // ------------------------------------------------------------------------------------------
-// Platt scaling: sigmoid_train on decision values (one workgroup per fit).
+// Platt scaling: sigmoid_train (libsvm svm.cpp sigmoid_train; reference SVC(probability=True),
+// train_ensemble_public.py:44) on one fit's cross-validated decision values, one 1024-thread
+// workgroup per fit.
+//
+// The decision values are assembled in the kernel from the batched decision launch's f32
+// partials (svm_dec_batch: part[row][S]) — d = −(Σ_s part[row][s] − ρ_k), the 1024-point partials
+// summed in f64 in s order — following a host-built map from the fit's grouped positions to
+// partial rows (code ≥ 0) or to a per-fold constant (code < 0: −1 − code indexes consts; a
+// degenerate fold's decision value).  Labels are implied by the grouped order (position < n0 ⇒
+// +1).  Up to kPlattReg·1024 points the values stay in registers for the whole Newton solve;
+// larger fits keep them in the global scratch `dec`.
+//
+// Each Newton iteration of libsvm's loop is ONE pass over the points: the line search's trial
+// objective at (A + s·dA, B + s·dB) also accumulates the Hessian and gradient there (one exp and
+// one log per point, shared), which the next iteration uses when the trial is accepted — the
+// same accepted iterates as the two-pass loop.  Six sums per pass, one barrier (double-buffered
+// reduction slots).
 struct PlattProb {
-  long long off;  // offset into dec / labels
-  int l;
-  int pad;
+  long long off;  // offset into the fit-concatenated position arrays (srcmap / dec)
+  int l;          // points of the fit
+  int n0;         // positions < n0 carry label +1
 };
 
-__device__ double block_sum256(double v, double* sh) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh[wave] = v;
-  __syncthreads();
-  return sh[0] + sh[1] + sh[2] + sh[3];
+constexpr int kPlattThreads = 1024;
+constexpr int kPlattWaves = kPlattThreads / 64;
+constexpr int kPlattReg = 16;
+
+struct PlattSums {
+  double f, h11, h22, h21, g1, g2;
+};
+
+__device__ __forceinline__ void platt_point(double d, double t, double a, double b, PlattSums& acc) {
+  const double fApB = d * a + b;
+  double p, q;
+  if (fApB >= 0) {
+    const double e = exp(-fApB);
+    acc.f += t * fApB + log(1 + e);
+    p = e / (1.0 + e);
+    q = 1.0 / (1.0 + e);
+  } else {
+    const double e = exp(fApB);
+    acc.f += (t - 1) * fApB + log(1 + e);
+    p = 1.0 / (1.0 + e);
+    q = e / (1.0 + e);
+  }
+  const double d2 = p * q;
+  acc.h11 += d * d * d2;
+  acc.h22 += d2;
+  acc.h21 += d * d2;
+  const double d1 = t - p;
+  acc.g1 += d * d1;
+  acc.g2 += d1;
 }
 
-__global__ __launch_bounds__(256) void platt_kernel(const PlattProb* __restrict__ probs,
-                                                    const double* __restrict__ dec,
-                                                    const float* __restrict__ labels,
-                                                    double* __restrict__ AB) {
-  const PlattProb P = probs[blockIdx.x];
-  const double* d = dec + P.off;
-  const float* y = labels + P.off;
-  __shared__ double sh[4];
-  double p1 = 0, p0 = 0;
-  for (int i = threadIdx.x; i < P.l; i += 256) {
-    if (y[i] > 0) p1 += 1; else p0 += 1;
+__device__ __forceinline__ PlattSums platt_block_sum(PlattSums v, double* red, int& parity) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* r = red + parity * (kPlattWaves * 6);
+  parity ^= 1;
+  const double w[6] = {wave_sum(v.f), wave_sum(v.h11), wave_sum(v.h22), wave_sum(v.h21), wave_sum(v.g1),
+                       wave_sum(v.g2)};
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r[wave * 6 + k] = w[k];
   }
-  const double prior1 = block_sum256(p1, sh);
-  const double prior0 = block_sum256(p0, sh);
+  __syncthreads();
+  double o[6] = {0, 0, 0, 0, 0, 0};
+  for (int q = 0; q < kPlattWaves; ++q) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[k] += r[q * 6 + k];
+  }
+  return PlattSums{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+template <bool Reg>
+__global__ __launch_bounds__(kPlattThreads) void platt_kernel(const PlattProb* __restrict__ probs,
+                                                              const float* __restrict__ part, int S,
+                                                              const int* __restrict__ rowk,
+                                                              const double* __restrict__ rho,
+                                                              const double* __restrict__ consts,
+                                                              const int* __restrict__ srcmap,
+                                                              double* __restrict__ dec,
+                                                              double* __restrict__ AB) {
+  const PlattProb P = probs[blockIdx.x];
+  if (Reg != (P.l <= kPlattReg * kPlattThreads)) return;   // the other instantiation's fit
+  __shared__ double red[2 * kPlattWaves * 6];
+  const int tid = threadIdx.x;
+  double dr[Reg ? kPlattReg : 1];
+  double* dg = dec + P.off;
+#pragma unroll
+  for (int k = 0; k < (Reg ? kPlattReg : 1); ++k) dr[k] = 0.0;
+  auto value = [&](int i) {
+    const int code = srcmap[P.off + i];
+    if (code < 0) return consts[-1 - code];
+    double sum = 0.0;
+    for (int j = 0; j < S; ++j) sum += (double)part[(size_t)code * S + j];
+    return -(sum - rho[rowk[code]]);
+  };
+  if constexpr (Reg) {
+#pragma unroll
+    for (int k = 0; k < kPlattReg; ++k) {
+      const int i = tid + k * kPlattThreads;
+      if (i < P.l) dr[k] = value(i);
+    }
+  } else {
+    for (int i = tid; i < P.l; i += kPlattThreads) dg[i] = value(i);
+  }
+  if constexpr (!Reg) __threadfence_block();
+  __syncthreads();
+  const double prior1 = P.n0, prior0 = P.l - P.n0;
   const int max_iter = 100;
   const double min_step = 1e-10, sigma = 1e-12, eps = 1e-5;
   const double hiT = (prior1 + 1.0) / (prior1 + 2.0), loT = 1 / (prior0 + 2.0);
-  double A = 0.0, B = log((prior0 + 1.0) / (prior1 + 1.0));
-  auto fobj = [&](double a, double b) {
-    double f = 0;
-    for (int i = threadIdx.x; i < P.l; i += 256) {
-      const double t = y[i] > 0 ? hiT : loT;
-      const double fApB = d[i] * a + b;
-      f += fApB >= 0 ? t * fApB + log(1 + exp(-fApB)) : (t - 1) * fApB + log(1 + exp(fApB));
+  int parity = 0;
+  auto pass = [&](double a, double b) {
+    PlattSums acc{0, 0, 0, 0, 0, 0};
+    if constexpr (Reg) {
+#pragma unroll
+      for (int k = 0; k < kPlattReg; ++k) {
+        const int i = tid + k * kPlattThreads;
+        if (i < P.l) platt_point(dr[k], i < P.n0 ? hiT : loT, a, b, acc);
+      }
+    } else {
+      for (int i = tid; i < P.l; i += kPlattThreads) platt_point(dg[i], i < P.n0 ? hiT : loT, a, b, acc);
     }
-    return block_sum256(f, sh);
+    return platt_block_sum(acc, red, parity);
   };
-  double fval = fobj(A, B);
+  double A = 0.0, B = log((prior0 + 1.0) / (prior1 + 1.0));
+  PlattSums v = pass(A, B);
+  double fval = v.f;
   for (int it = 0; it < max_iter; ++it) {
-    double h11 = 0, h22 = 0, h21 = 0, g1 = 0, g2 = 0;
-    for (int i = threadIdx.x; i < P.l; i += 256) {
-      const double t = y[i] > 0 ? hiT : loT;
-      const double fApB = d[i] * A + B;
-      double p, q;
-      if (fApB >= 0) { p = exp(-fApB) / (1.0 + exp(-fApB)); q = 1.0 / (1.0 + exp(-fApB)); }
-      else { p = 1.0 / (1.0 + exp(fApB)); q = exp(fApB) / (1.0 + exp(fApB)); }
-      const double d2 = p * q;
-      h11 += d[i] * d[i] * d2;
-      h22 += d2;
-      h21 += d[i] * d2;
-      const double d1 = t - p;
-      g1 += d[i] * d1;
-      g2 += d1;
-    }
-    h11 = block_sum256(h11, sh) + sigma;
-    h22 = block_sum256(h22, sh) + sigma;
-    h21 = block_sum256(h21, sh);
-    g1 = block_sum256(g1, sh);
-    g2 = block_sum256(g2, sh);
+    const double h11 = v.h11 + sigma, h22 = v.h22 + sigma, h21 = v.h21, g1 = v.g1, g2 = v.g2;
     if (fabs(g1) < eps && fabs(g2) < eps) break;
     const double det = h11 * h22 - h21 * h21;
     const double dA = -(h22 * g1 - h21 * g2) / det;
@@ -627,20 +693,28 @@ __global__ __launch_bounds__(256) void platt_kernel(const PlattProb* __restrict_
     double step = 1;
     while (step >= min_step) {
       const double nA = A + step * dA, nB = B + step * dB;
-      const double nf = fobj(nA, nB);
-      if (nf < fval + 0.0001 * step * gd) { A = nA; B = nB; fval = nf; break; }
+      const PlattSums w = pass(nA, nB);
+      if (w.f < fval + 0.0001 * step * gd) { A = nA; B = nB; fval = w.f; v = w; break; }
       step = step / 2.0;
     }
     if (step < min_step) break;
   }
-  if (threadIdx.x == 0) { AB[2 * blockIdx.x] = A; AB[2 * blockIdx.x + 1] = B; }
+  if (tid == 0) { AB[2 * blockIdx.x] = A; AB[2 * blockIdx.x + 1] = B; }
 }
 
-void platt_batch(uintptr_t probs, int P, uintptr_t dec, uintptr_t labels, uintptr_t AB,
-                 uintptr_t stream) {
-  hipLaunchKernelGGL(platt_kernel, dim3(P), dim3(256), 0, as_stream(stream),
-                     (const PlattProb*)probs, (const double*)dec, (const float*)labels,
-                     (double*)AB);
+void platt_batch(uintptr_t probs, int P, uintptr_t part, int S, uintptr_t rowk, uintptr_t rho,
+                 uintptr_t consts, uintptr_t srcmap, uintptr_t dec, uintptr_t AB, uintptr_t stream) {
+  HFENS_REQUIRE(P >= 1 && S >= 0, "platt_batch: P >= 1, S >= 0");
+  hipStream_t st = as_stream(stream);
+  // two launches on one stream, each skipping the other's fits: register-resident values for
+  // fits of ≤ 16k points, the global scratch beyond
+  hipLaunchKernelGGL(platt_kernel<true>, dim3(P), dim3(kPlattThreads), 0, st, (const PlattProb*)probs,
+                     (const float*)part, S, (const int*)rowk, (const double*)rho, (const double*)consts,
+                     (const int*)srcmap, (double*)dec, (double*)AB);
+  launch_check();
+  hipLaunchKernelGGL(platt_kernel<false>, dim3(P), dim3(kPlattThreads), 0, st, (const PlattProb*)probs,
+                     (const float*)part, S, (const int*)rowk, (const double*)rho, (const double*)consts,
+                     (const int*)srcmap, (double*)dec, (double*)AB);
   launch_check();
 }
 

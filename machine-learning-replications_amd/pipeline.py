@@ -94,8 +94,9 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
 
     if group is None and dev.type == "cuda" and PLAN_AHEAD:
         overlap = plan_ahead(y_dev)
-    from .utils.timing import hmark
+    from .utils.timing import hmark, dmark, dmarks_flush
     hmark("develop")
+    dmark("develop")
     with timer.stage("impute"):
         if group is None:
             imputer = KNNImputer(n_neighbors=cfg.knn_neighbors).fit(X_dev)
@@ -136,6 +137,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         if run_sel is not None:
             X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
         hmark("lasso_fit")
+        dmark("lasso_fit")
         mask = sfm.get_support()
         mt = torch.as_tensor(mask, device=dev)
         X_dev_optm = X_dev[:, mt]
@@ -143,6 +145,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         hmark("selected")
     clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None,
             plan=plan_box.get("plan"))
+    dmark("stack_fit")
     if aux is not None:
         # join the side stream while the imputer and X_sel are alive (their blocks are not reused
         # by the main stream before this point)
@@ -166,6 +169,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         # (the held-out rows are already gathered for the report, so the AUROC comes from them;
         # metrics.roc_auc_sharded is the R8 path for callers that keep scores sharded)
         scores = metrics.evaluate(ysel_all, proba_all)
+    dmarks_flush()
     n_train = X_dev.shape[0]
     if fit_group is not None:
         from .parallel import dist as pdist

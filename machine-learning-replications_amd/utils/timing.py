@@ -118,3 +118,31 @@ def hmarks_flush(prefix: str = "[host]") -> None:
         t0 = _MARKS[0][1]
         print(prefix + " " + " ".join(f"{k}={1e3 * (v - t0):.1f}" for k, v in _MARKS), file=sys.stderr)
         _MARKS.clear()
+
+
+# ---------------------------------------------------------------------------- device timeline marks
+# HFENS_TRACE_DEV=1: ``dmark(name)`` records a timing event on the current stream; ``dmarks_flush``
+# (end of ``pipeline.develop``) prints when the device reached each one, in ms since the first mark
+# (recorded at develop() entry on an idle device, so the numbers line up with the host marks).
+# Diagnostic only: no profiler attached, so the streams overlap as in a normal run.
+TRACE_DEV = _os.environ.get("HFENS_TRACE_DEV", "0") == "1"
+_DMARKS: list = []
+
+
+def dmark(name: str) -> None:
+    if TRACE_DEV:
+        import torch
+        if torch.cuda.is_available():
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _DMARKS.append((name, e))
+
+
+def dmarks_flush(prefix: str = "[dev]") -> None:
+    if TRACE_DEV and _DMARKS:
+        import sys
+        for _, e in _DMARKS:
+            e.synchronize()
+        e0 = _DMARKS[0][1]
+        print(prefix + " " + " ".join(f"{k}={e0.elapsed_time(e):.2f}" for k, e in _DMARKS), file=sys.stderr)
+        _DMARKS.clear()

@@ -109,3 +109,51 @@ def test_ws_unconverged_batch_is_resolved_synchronously(dev, monkeypatch):
     assert torch.equal(m.support_.cpu(), ref.support_.cpu())
     assert torch.equal(m._dual_coef_.cpu(), ref._dual_coef_.cpu())
     assert m._probA.item() == ref._probA.item() and m._probB.item() == ref._probB.item()
+
+
+@pytest.mark.parametrize("ls", [[1500, 9000], [20000, 700]])
+def test_platt_kernel_matches_host_sigmoid_train(dev, ls):
+    """platt_batch (svm.hip): each fit's decision values assembled in the kernel from f32 partials
+    (d = −(Σ_s part[row][s] − ρ_k), per-fold constants, 0 for unmapped positions), then libsvm's
+    sigmoid_train with one pass per Newton trial — against the host sigmoid_train on the same
+    values summed in f64.  Fits ≤ 16k points keep the values in registers, larger ones in the
+    global scratch (both paths covered)."""
+    from hfens import ops
+    E = ops.ext()
+    rng = np.random.default_rng(7)
+    S = 3
+    rows = sum(ls)
+    part = rng.normal(0, 0.4, (rows, S)).astype(np.float32)
+    nprob = 4
+    rowk = rng.integers(0, nprob, rows).astype(np.int32)
+    rho = rng.normal(0, 0.2, nprob)
+    consts = np.array([0.0, 0.7, -1.3])
+    maps, arr, off, r0 = [], np.zeros(len(ls), smo._PLATT_DT), 0, 0
+    n0s = []
+    for k, l in enumerate(ls):
+        sm = rng.permutation(np.arange(r0, r0 + l, dtype=np.int32))
+        sm[:5] = -2            # a degenerate fold's constant
+        sm[5:7] = -3
+        sm[7] = -1             # no fold: 0.0
+        n0 = int(l * 0.3)
+        arr[k] = (off, l, n0)
+        maps.append(sm)
+        n0s.append(n0)
+        off += l
+        r0 += l
+    srcmap = np.concatenate(maps)
+    d = lambda t: torch.as_tensor(t).to(dev)   # noqa: E731
+    part_d, rowk_d, rho_d, c_d, map_d, pdev = (d(part), d(rowk), d(rho), d(consts), d(srcmap),
+                                               d(arr.view(np.uint8)))
+    dscr = torch.empty(off, dtype=torch.float64, device=dev)
+    AB = torch.empty(2 * len(ls), dtype=torch.float64, device=dev)
+    E.platt_batch(pdev.data_ptr(), len(ls), part_d.data_ptr(), S, rowk_d.data_ptr(), rho_d.data_ptr(),
+                  c_d.data_ptr(), map_d.data_ptr(), dscr.data_ptr(), AB.data_ptr(), ops.stream_ptr(dev))
+    got = AB.cpu().numpy()
+    for k, sm in enumerate(maps):
+        dec = np.where(sm >= 0, -(part.astype(np.float64)[np.maximum(sm, 0)].sum(1) - rho[rowk[np.maximum(sm, 0)]]),
+                       consts[np.where(sm < 0, -1 - sm, 0)])
+        lab = np.where(np.arange(sm.size) < n0s[k], 1.0, -1.0)
+        A, B = smo._sigmoid_train_host(dec, lab)
+        assert got[2 * k] == pytest.approx(A, rel=1e-9, abs=1e-12), (k, got[2 * k], A)
+        assert got[2 * k + 1] == pytest.approx(B, rel=1e-9, abs=1e-12), (k, got[2 * k + 1], B)

@@ -695,3 +695,21 @@ def test_device_svc_oof_matches_fold_models(dev, monkeypatch):
     assert float(d[:, 0].max()) <= 2e-4, float(d[:, 0].max())
     assert float(d[:, 0].mean()) <= 1e-5, float(d[:, 0].mean())
     assert float((out[False].proba_sel - out[True].proba_sel).abs().max()) <= 2e-4
+
+
+def test_fused_logreg_guards_raise_after_launch(dev):
+    """The fused device path reads its input guards (finite X, 0/1 labels) with the cooperative
+    launch's error word in one transfer: bad inputs still raise, as the synchronous checks did."""
+    from hfens.utils.guards import NonFiniteError
+    from hfens.models import logreg_solver
+    X = torch.randn(4000, 5, dtype=torch.float64, device=dev)
+    y = (torch.arange(4000, device=dev) % 2).to(torch.float64)
+    m = LogisticRegression().fit(X, y)
+    assert logreg_solver.LAST_PATH["path"] == "fused"
+    assert torch.isfinite(m.coef_).all()
+    Xbad = X.clone()
+    Xbad[17, 3] = float("nan")
+    with pytest.raises(NonFiniteError):
+        LogisticRegression().fit(Xbad, y)
+    with pytest.raises(ValueError):
+        LogisticRegression().fit(X, y * 2)
