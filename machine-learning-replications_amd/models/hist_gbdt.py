@@ -356,6 +356,8 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     hmark("gbc_enqueued")
     check_finite(st.value, "GBDT leaf values")
     hmark("gbc_guarded")
+    if getattr(st, "persist_err", None) is not None and int(st.persist_err.item()) != 0:
+        raise RuntimeError("GBDT persistent stage loop: a grid-barrier wait passed its deadline")
     if getattr(st, "peer", None) is not None:
         st.peer.check()     # (after the guard's host read: no extra synchronisation point)
     _finish(models, st, sw, p1, group)
@@ -549,6 +551,16 @@ def _prune_graphs():
     while _GRAPH_KEEP and _GRAPH_KEEP[0][1].query():
         _GRAPH_KEEP.pop(0)
 PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage whose s_memtime stamps to keep
+# Persistent stage loop (the per-stage floor): ONE gbdt_stump_stage launch runs every
+# boosting stage with a per-model device barrier between stages instead of a launch per stage.
+# Measured (scripts/probes/gbdt_persist_probe.py, profiles/r4_gbdt_persist.md): 43.9 → 35.3 µs per
+# stage at 125k rows × 1 model (123 workgroups), no gain at ≥ 205 workgroups (125k × 5, 1M × 1:
+# the stage body, not the launch boundary, is the cost there).  "auto" = single process, no stamps,
+# ≥ PERSIST_MIN_ROWS rows (small fits run beside the SVC's spinning SMO members in the stacking
+# trainer and keep the launches) and ≤ PERSIST_MAX_WGS workgroups; "1" / "0" force it on / off.
+PERSIST = os.environ.get("HFENS_GBDT_PERSIST", "auto")
+PERSIST_MIN_ROWS = int(os.environ.get("HFENS_GBDT_PERSIST_MIN_ROWS", "65536"))
+PERSIST_MAX_WGS = int(os.environ.get("HFENS_GBDT_PERSIST_MAX_WGS", "128"))
 LAST_STAGE_PROF: dict = {}
 
 
@@ -615,7 +627,7 @@ def _run_stage(st: _State, group):
                            ptr(st.bagw), ptr(st.frank), partials.data_ptr(), plen, st.lr, st.qscale,
                            st.dscale, st.min_leaf_q,
                            st.min_split_q, ptr(prof) if (prof is not None and t == PROFILE_STAGE_T) else 0,
-                           ptr(t_dev), int(tick_in_reduce), s)
+                           ptr(t_dev), int(tick_in_reduce), 0, 0, 0, s)
         if t_dev is not None and not tick_in_reduce:
             E.gbdt_stage_tick(t_dev.data_ptr(), s)
         if group is not None and (t_dev is not None or t <= st.T):
@@ -633,6 +645,30 @@ def _run_stage(st: _State, group):
     t0 = time.perf_counter()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev0.record()
+    persist = (group is None and prof is None and not uses_partials and st.B * groups <= _num_cus(dev)
+               and (PERSIST == "1" or (PERSIST == "auto" and st.n >= PERSIST_MIN_ROWS
+                                       and st.B * groups <= PERSIST_MAX_WGS)))
+    GRAPH_INFO["persist"] = persist
+    if persist:
+        be = runtime.workspace(dev, "gbdt_persist_bar", st.B + 1, torch.int32)   # [B] counters, err
+        be.zero_()
+        E.gbdt_stump_stage(0, st.B, st.n, st.F, st.T, binsp.data_ptr(), ldb, bm.nbins.data_ptr(), hist_len,
+                           bm.lo_val.data_ptr(), bm.hi_val.data_ptr(), st.y.data_ptr(), st.w.data_ptr(),
+                           st.raw.data_ptr(), ptr(st.wt), ptr(st.seeds), st.row_off, st.subsample,
+                           comm.data_ptr(), st.feat.data_ptr(), st.blo.data_ptr(), st.thr.data_ptr(),
+                           st.value.data_ptr(), st.stats.data_ptr(), st.r2.data_ptr(), st.dev.data_ptr(),
+                           ptr(st.bagw), ptr(st.frank), partials.data_ptr(), plen, st.lr, st.qscale,
+                           st.dscale, st.min_leaf_q, st.min_split_q, 0, 0, 0, 1, be.data_ptr(),
+                           be.data_ptr() + 4 * st.B, s)
+        st.persist_err = be[st.B:st.B + 1]
+        GRAPH_INFO.update(units=0, stages_eager=0, host_s=time.perf_counter() - t0)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        GRAPH_INFO["loop_events"] = (ev0, ev1)
+        COLLECTIVES["per_stage"] = 0.0
+        COLLECTIVES["xgmi_per_stage"] = 0.0
+        st.reduced = True
+        return
     units = _graph_units(st, group, prof, peer)
     if units:
         # HIP graph of one 3-stage unit (stage kernel [+ partial reduce] + counter tick [+ the

@@ -925,7 +925,42 @@ struct StageJob {
   long long* partials;                // [B][G][3·hist_len + kSgExtra] per-workgroup slots, or nullptr
   long long* prof;                    // diagnostics: [B][G][6] s_memtime phase stamps, or nullptr
   const int* t_dev;                   // stage index read from device memory (graph replay), or nullptr: t
+  unsigned* bar;                      // persistent launch: [B] monotone per-model barrier counters (zeroed)
+  unsigned* err;                      // persistent launch: set when a barrier wait passed its deadline
 };
+
+// Barrier of the persistent stage loop (gbdt_stump_stage with persist = 1).  Models are independent
+// (stage t of model b reads only model b's stage t−1 slot), so each model's workgroups wait only for
+// each other: every workgroup adds one arrival to its model's monotone counter and waits until it
+// reaches k·G (barrier k, G workgroups per model);
+// agent-scope fences on both sides make the stage's int64 slot atomics and stores visible to every
+// XCD's next-stage reads.  Residency: the grid is at most one workgroup per CU (sg_plan) and no
+// workgroup waits on anything but this counter, so workgroups that are not yet resident (CUs held
+// by another stream's kernels) are dispatched as those finish.  A wait past the deadline (fixed
+// 100 MHz s_memrealtime clock) sets *err and every workgroup leaves the loop.
+__device__ __forceinline__ bool sg_grid_barrier(unsigned* bar, unsigned* err, unsigned target) {
+  __syncthreads();
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+          (long long)__builtin_amdgcn_s_memrealtime() - t0 > 200000000LL) {   // 2 s
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence();
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
 
 template <int NV, int NW = kSgWaves>
 __device__ __forceinline__ void sg_block_sum(long long (&v)[NV], long long* red, long long* out) {
@@ -1014,7 +1049,10 @@ __device__ __forceinline__ long long sg_comb(const int* T, int ind, int v) {
   return s + ((long long)r[kSgSlices - 1] << (7 * (kSgSlices - 1)));
 }
 
-template <bool MF, int NT>
+// Persist = false: one launch per stage t (J.t or *J.t_dev).  Persist = true: ONE launch runs every
+// stage t = 0 … T+1 of the boosting, separated by sg_grid_barrier — the same per-stage body, so the
+// same integers, splits and trees, without a launch boundary (and its host enqueue) per stage.
+template <bool MF, int NT, bool Persist = false>
 __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   constexpr int kT = NT, kW = NT / 64;       // threads, waves
   constexpr int RPT = kSgTile / kT;           // rows per thread in the apply
@@ -1046,12 +1084,11 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   __shared__ int s_ord[kStMaxF];   // split-scan order: features with > 4 bins first (spread over waves)
   int* Tsl = reinterpret_cast<int*>(qw + kSgRowPad + kSgArrSkew);   // MF: [n_mb·32 indicators][32 slice columns] int32
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = J.n, F = J.F, B = J.B, t = J.t_dev != nullptr ? *J.t_dev : J.t, T = J.T;
+  const int n = J.n, F = J.F, B = J.B, T = J.T;
+  const int t_first = Persist ? 0 : (J.t_dev != nullptr ? *J.t_dev : J.t);
+  const int t_last = Persist ? T + 1 : t_first;
   const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
   const size_t slot_sz = (size_t)B * slot_m;
-  long long* slot_prev = J.comm + (size_t)((t + 2) % 3) * slot_sz + (size_t)b * slot_m;
-  long long* slot_cur = J.comm + (size_t)(t % 3) * slot_sz + (size_t)b * slot_m;
-  long long* slot_next = J.comm + (size_t)((t + 1) % 3) * slot_sz;
   if (tid == 0) {
     int o = 0;
     n_bin = n_one = n_mid = n_wide = 0;
@@ -1086,11 +1123,18 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
     }
     pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0;
   }
-  // zero the slot that launch t+1 accumulates (nobody reads or writes it during launch t)
-  {
-    const size_t nwg = (size_t)gridDim.x * gridDim.y, wid = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    for (size_t k = wid * kT + tid; k < slot_sz; k += nwg * kT) slot_next[k] = 0;
+  for (int t = t_first;; ++t) {
+  if constexpr (Persist) {
+    if (t > t_first && !sg_grid_barrier(J.bar + b, J.err, (unsigned)(t - t_first) * gridDim.x)) return;
+    if (tid == 0) { pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0; }
   }
+  long long* slot_prev = J.comm + (size_t)((t + 2) % 3) * slot_sz + (size_t)b * slot_m;
+  long long* slot_cur = J.comm + (size_t)(t % 3) * slot_sz + (size_t)b * slot_m;
+  long long* slot_next = J.comm + (size_t)((t + 1) % 3) * slot_sz;
+  // zero this model's part of the slot that stage t+1 accumulates (nobody reads or writes it during
+  // stage t; per model, because in the persistent loop another model may still be in stage t−1,
+  // reading its own part of that slot)
+  for (size_t k = (size_t)blockIdx.x * kT + tid; k < slot_m; k += (size_t)gridDim.x * kT) slot_next[(size_t)b * slot_m + k] = 0;
   __syncthreads();
   const bool lead = blockIdx.x == 0;
   const double inv = 1.0 / J.qscale;
@@ -1112,7 +1156,7 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
       J.dev[pb] += E[4];
     }
   }
-  if (t > T) return;   // the closing launch only books the last slot
+  if (t > T) break;   // the closing launch only books the last slot
   // a sub-tile's row inputs (this thread's two rows: kSgTile = 2 × threads) are loaded one sub-tile
   // ahead — issued before the previous sub-tile's histogram, consumed by the next apply — so their
   // global latencies overlap the histogram instead of stalling the apply.  The first sub-tile's
@@ -1558,6 +1602,8 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
     else if (v != 0) atomicAdd((unsigned long long*)&slot_cur[k], (unsigned long long)v);
   }
   if (pst && tid == 0) pst[3] = (long long)__builtin_amdgcn_s_memtime() - t_0;
+  if (t >= t_last) break;
+  }   // stage loop
 }
 
 // Sum of the per-workgroup partial slots into the stage's comm slot: grid (slot chunks, G splits, B)
@@ -1621,7 +1667,8 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
                       uintptr_t blo, uintptr_t thr, uintptr_t value, uintptr_t stats, uintptr_t r2, uintptr_t dev,
                       uintptr_t bagw, uintptr_t frank, uintptr_t partials, long long partials_len, double lr,
                       double qscale, double dscale, double min_leaf_q, double min_split_q, uintptr_t prof,
-                      uintptr_t t_dev, int tick_in_reduce, uintptr_t stream) {
+                      uintptr_t t_dev, int tick_in_reduce, int persist, uintptr_t bar, uintptr_t err,
+                      uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= kStMaxF, "gbdt_stump_stage: 1 <= F <= 128");
   HFENS_REQUIRE(B >= 1 && B <= 65535 && n >= 1 && T >= 1 && t >= 0 && t <= T + 1, "gbdt_stump_stage: bad shape");
   const bool active = subsample < 1.0;
@@ -1639,7 +1686,8 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
              (long long*)comm, (int*)feat, (int*)blo, (double*)thr, (double*)value, (long long*)stats,
              (long long*)r2, (long long*)dev, (double*)bagw, (const int*)frank, row_off, lr, qscale, dscale,
              min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
-             hist_len, t, 0, ldb, (long long*)partials, (long long*)prof, (const int*)t_dev};
+             hist_len, t, 0, ldb, (long long*)partials, (long long*)prof, (const int*)t_dev, (unsigned*)bar,
+             (unsigned*)err};
   // t_dev (graph replay): the kernel takes the stage index from device memory; the host t still
   // selects the comm slot of the reduce launch, so a captured unit must start at t ≡ 0 (mod 3)
   HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");
@@ -1656,6 +1704,18 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
   const long long slot_m = 3LL * hist_len + kSgExtra;
   if (plan[2] == 0 || partials == 0) J.partials = nullptr;
   else HFENS_REQUIRE(partials_len >= plan[3], "gbdt_stump_stage: partials buffer too small (size it with gbdt_stage_plan)");
+  if (persist) {
+    // the whole boosting run in one launch (t = 0 … T+1); int64 slot atomics only (no partial
+    // reduce launch), no stamps, no device stage counter; at most one workgroup per CU
+    HFENS_REQUIRE(bar != 0 && err != 0 && t_dev == 0 && prof == 0 && t == 0,
+                  "gbdt_stump_stage: persist needs bar/err, t = 0, no t_dev/prof");
+    HFENS_REQUIRE((long long)groups * B <= ncu, "gbdt_stump_stage: persist grid exceeds one workgroup per CU");
+    J.partials = nullptr;
+    if (mf) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, kSgThreads, true>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+    else hipLaunchKernelGGL((gbdt_stump_stage_kernel<false, kSgThreads, true>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
+    launch_check();
+    return;
+  }
   if (mf && nt == 1024) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, 1024>), dim3(groups, B), dim3(1024), lds, as_stream(stream), J);
   else if (mf) hipLaunchKernelGGL((gbdt_stump_stage_kernel<true, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);
   else hipLaunchKernelGGL((gbdt_stump_stage_kernel<false, kSgThreads>), dim3(groups, B), dim3(kSgThreads), lds, as_stream(stream), J);

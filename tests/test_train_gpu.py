@@ -713,3 +713,34 @@ def test_fused_logreg_guards_raise_after_launch(dev):
         LogisticRegression().fit(Xbad, y)
     with pytest.raises(ValueError):
         LogisticRegression().fit(X, y * 2)
+
+
+@pytest.mark.parametrize("rows,subsample,mf", [(70000, 1.0, "1"), (130000, 0.7, "1"), (70000, 1.0, "0")])
+def test_gbdt_stage_persistent_bit_identical(dev, monkeypatch, rows, subsample, mf):
+    """The persistent stage loop (ONE gbdt_stump_stage launch for every boosting stage, a device
+    grid barrier between stages) gives the launch-per-stage loop's model bit for bit — trees,
+    thresholds, leaf values, impurities, train_score_ — with sklearn's tie ranks, bagging and both
+    histogram paths."""
+    from hfens.models import hist_gbdt
+    monkeypatch.setattr(hist_gbdt, "STUMP_PATH", "stage")
+    monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", False)
+    monkeypatch.setenv("HFENS_GBDT_MFMA", mf)
+    X, y = _data(rows, 24, 67)
+    g = torch.Generator().manual_seed(9)
+    X[:, 3] = torch.randint(0, 2, (rows,), generator=g).double()
+    X[:, 6] = torch.randint(0, 5, (rows,), generator=g).double()
+    masks = torch.ones(3, rows, dtype=torch.bool)
+    masks[1, ::5] = False
+    masks[2, 2::5] = False
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(hist_gbdt, "PERSIST", mode)
+        ms = [GradientBoostingClassifier(n_estimators=50, max_depth=1, subsample=subsample, random_state=s)
+              for s in (2020, 7, 8)]
+        fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        assert hist_gbdt.LAST_PATH["path"] == "stage"
+        assert hist_gbdt.GRAPH_INFO["persist"] == (mode == "1")
+        out[mode] = _gbdt_outputs(ms)
+    for a, b in zip(out["0"], out["1"]):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
