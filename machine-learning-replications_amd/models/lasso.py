@@ -160,7 +160,10 @@ class LassoCV(Estimator):
                                         cnt[k:].expand(A), grid[:, None])          # [A, 1, F]
                 ev = torch.cuda.Event()
                 ev.record(side)
+        from ..utils.timing import dmark
+        dmark("lasso_cv_in")
         coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+        dmark("lasso_cv_path")
         if overlap is not None:
             overlap()
         # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test

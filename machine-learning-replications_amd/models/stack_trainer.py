@@ -290,6 +290,8 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
                  plan=None):
     timer = timer or StageTimer(enabled=False)
+    from ..utils.timing import hmark as _hmk
+    _hmk("stack_in")
     dev = X.device
     n = X.shape[0]
     y_np = None
@@ -329,6 +331,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
         return enqueue_svc_oof(st, items, meta, col)
 
     y64 = y.to(torch.float64)
+    _hmk("stack_prep")
 
     def new_final():
         return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
