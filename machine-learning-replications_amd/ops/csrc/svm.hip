@@ -549,7 +549,7 @@ void svm_dec_batch(uintptr_t zcat, uintptr_t coef, uintptr_t hcat, int F, uintpt
     launch_check();                                                                              \
     return;                                                                                      \
   }
-  DEC_CASE(4) DEC_CASE(8) DEC_CASE(12) DEC_CASE(16) DEC_CASE(24) DEC_CASE(32)
+  DEC_CASE(4) DEC_CASE(8) DEC_CASE(9) DEC_CASE(12) DEC_CASE(16) DEC_CASE(20) DEC_CASE(24) DEC_CASE(32)
 #undef DEC_CASE
 }
 
