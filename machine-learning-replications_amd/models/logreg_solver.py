@@ -133,7 +133,7 @@ def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=N
     from .smo import _num_cus
     M = lr_members(B, n, _num_cus(dev))
     if M > 1:
-        nv = F1 * (F1 + 1) // 2 + F1 + 1
+        nv = max(F1 * (F1 + 1) // 2 + F1 + 1, 8)   # (logreg.hip logreg_nvmax: ≥ the 8 trial losses)
         xchg = torch.empty(B * 2 * M * nv * 2, dtype=torch.int64, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         from ..utils.timing import hmark, dmark

@@ -359,36 +359,67 @@ __global__ __launch_bounds__(kLrThreads) void logreg_fused_kernel(LrJob J) {
       __syncthreads();
     }
     if (sc[0] != 0.0) { nit = it + 1; break; }
-    // ---- C: losses at the 8 trial steps 2^-k, X̃d kept
-    double tk[kLrSteps];
-#pragma unroll
-    for (int k = 0; k < kLrSteps; ++k) tk[k] = 0.0;
-    for (int r = r0 + tid; r < r1; r += kLrThreads) {
-      const double* xr = J.X + (size_t)r * F1;
-      double xd = 0.0;
-      for (int f = 0; f < F1; ++f) xd = fma(xr[f], dd[f], xd);
-      Xd[r] = xd;
-      const double sw = s[r];
-      if (sw != 0.0) {
-        const double yp = J.ypm[r], z = Z[r];
-        double a = 1.0;
-#pragma unroll
-        for (int k = 0; k < kLrSteps; ++k) {
-          tk[k] += sw * lr_softplus(-yp * (z + a * xd));
-          a *= 0.5;
+    // ---- C: the loss at the full step 2^0 first (X̃d kept): a Newton step is almost always
+    // accepted at once, and the 7 shorter trials cost 7 of the pass's 8 softplus per row.  Only
+    // when the full step fails the Armijo test does a second pass evaluate steps 2^-1 … 2^-7 (from
+    // the stored X̃d).  Every trial loss is the sum the one-pass form computed — the same per-thread
+    // row order, the same per-step block reduction and member exchange order — so the chosen
+    // step, and the whole solve, are unchanged bit for bit.
+    const double F0 = data0 + sc[2], delta = sc[1];
+    auto reg_at = [&](double a) {
+      double reg = 0.0;
+      for (int f = 0; f < F1; ++f) {
+        if (!J.penal[f]) continue;
+        const double wc = Wl[f] + a * dd[f];
+        reg += J.l1 ? fabs(wc) : 0.5 * wc * wc;
+      }
+      return reg;
+    };
+    {
+      double t0[1] = {0.0};
+      for (int r = r0 + tid; r < r1; r += kLrThreads) {
+        const double* xr = J.X + (size_t)r * F1;
+        double xd = 0.0;
+        for (int f = 0; f < F1; ++f) xd = fma(xr[f], dd[f], xd);
+        Xd[r] = xd;
+        const double sw = s[r];
+        if (sw != 0.0) {
+          const double yp = J.ypm[r], z = Z[r];
+          t0[0] += sw * lr_softplus(-yp * (z + 1.0 * xd));
         }
       }
+      lr_block_sum<1>(t0, red, sc + 8);
+      if constexpr (Coop) {
+        if (!lr_exchange(sc + 8, 1, J, b, w, epoch, &xfail)) return;
+      }
     }
-    lr_block_sum<kLrSteps>(tk, red, sc + 8);
-    if constexpr (Coop) {
-      if (!lr_exchange(sc + 8, kLrSteps, J, b, w, epoch, &xfail)) return;
+    const bool full_ok = C * sc[8] + reg_at(1.0) <= F0 + 1e-2 * 1.0 * delta;
+    if (!full_ok) {
+      double tk[kLrSteps - 1];
+#pragma unroll
+      for (int k = 0; k < kLrSteps - 1; ++k) tk[k] = 0.0;
+      for (int r = r0 + tid; r < r1; r += kLrThreads) {
+        const double sw = s[r];
+        if (sw != 0.0) {
+          const double yp = J.ypm[r], z = Z[r], xd = Xd[r];
+          double a = 0.5;
+#pragma unroll
+          for (int k = 0; k < kLrSteps - 1; ++k) {
+            tk[k] += sw * lr_softplus(-yp * (z + a * xd));
+            a *= 0.5;
+          }
+        }
+      }
+      lr_block_sum<kLrSteps - 1>(tk, red, sc + 9);
+      if constexpr (Coop) {
+        if (!lr_exchange(sc + 9, kLrSteps - 1, J, b, w, epoch, &xfail)) return;
+      }
     }
     // Armijo: largest 2^-k with F(w + a d) ≤ F(w) + 0.01·a·Δ; none → the smallest step if it
     // still decreases F, else stop (every thread evaluates the same rule on LDS values)
-    const double F0 = data0 + sc[2], delta = sc[1];
-    int first = -1;
+    int first = full_ok ? 0 : -1;
     double FK7 = 0.0, a = 1.0;
-    for (int k = 0; k < kLrSteps; ++k) {
+    for (int k = 0; k < (full_ok ? 0 : kLrSteps); ++k) {
       double reg = 0.0;
       for (int f = 0; f < F1; ++f) {
         if (!J.penal[f]) continue;
@@ -451,8 +482,13 @@ void logreg_fused(int B, int n, int F1, uintptr_t X, uintptr_t s, uintptr_t ypm,
 }
 
 // exchange slots (u64 granules); models/logreg_solver.py sizes its buffer with the same formula
+static int logreg_nvmax(int F1) {   // values per member slot: H, g and the loss, or the trial losses
+  const int nv = F1 * (F1 + 1) / 2 + F1 + 1;
+  return nv > kLrSteps ? nv : kLrSteps;
+}
+
 static size_t logreg_coop_xchg_bytes(int B, int members, int F1) {
-  const int nvmax = F1 * (F1 + 1) / 2 + F1 + 1;
+  const int nvmax = logreg_nvmax(F1);
   return (size_t)B * 2 * members * nvmax * 2 * sizeof(unsigned long long);
 }
 
@@ -469,8 +505,7 @@ void logreg_coop(int B, int members, int n, int F1, uintptr_t X, uintptr_t s, ui
   HFENS_REQUIRE((long long)B * members <= ncu, "logreg_coop: B·members exceeds the CU count");
   int CR = 0;
   const size_t lds = logreg_lds_plan(F1, &CR);
-  const int npairs = F1 * (F1 + 1) / 2;
-  const int nvmax = npairs + F1 + 1;
+  const int nvmax = logreg_nvmax(F1);
   const int S = (n + members - 1) / members;
   hipStream_t st = as_stream(stream);
   // every polled granule starts at epoch 0 (epochs count from 1 within the launch)
