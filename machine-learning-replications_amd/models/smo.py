@@ -1041,6 +1041,24 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     for k, p in enumerate(live):
         a0 = aoffs_start[k]
         out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
+    # early read-back of what the final models' bookkeeping needs from the SMO alone (support masks,
+    # ρ, iterations, the error word), queued right behind the SMO: finish_svc_batch extracts the
+    # support vectors while the Platt and out-of-fold kernels still run, then reads only (A, B)
+    fin = sorted((p.fit, k) for k, p in enumerate(live) if p.fold < 0)
+    if fin and len({f for f, _ in fin}) == len(fin):
+        f64 = torch.float64
+        ks = [k for _, k in fin]
+        kidx = _to_dev(np.array(ks, dtype=np.int64), device)
+        parts = ([(alpha[aoffs_start[k]:aoffs_start[k] + live[k].l] > 0).to(f64) for k in ks]
+                 + [rho.index_select(0, kidx).to(f64).reshape(-1), iters.index_select(0, kidx).to(f64).reshape(-1)]
+                 + ([err.to(f64).reshape(-1).abs().max().reshape(1)] if err is not None else []))
+        early_dev = torch.cat(parts)
+        early_host = torch.empty(early_dev.shape, dtype=f64, pin_memory=True)
+        early_host.copy_(early_dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        out["_early"] = dict(host=early_host, ev=ev, ids=[id(live[k]) for k in ks], has_err=err is not None,
+                             keep=early_dev)
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
     # for the held-out decisions below and the stacking trainer's device OOF (enqueue_svc_oof)
     # (the signs built on the host and uploaded in one copy: per-problem fills would be ~70 tiny
@@ -1366,8 +1384,18 @@ def finish_svc_batch(st: dict, defer=None):
         return st["svcs"]
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
                                                    st["sol"], st["AB"], st["device"])
-    err = sol.get("smo_err")
-    if err is not None and float(err.max()) != 0.0:
+    early = sol.get("_early")
+    finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
+    if early is not None and early["ids"] != [id(p) for p in finals]:
+        early = None
+    if early is not None:
+        early["ev"].synchronize()
+        host_e = early["host"].numpy()
+        smo_failed = early["has_err"] and host_e[-1] != 0.0
+    else:
+        err = sol.get("smo_err")
+        smo_failed = err is not None and float(err.max()) != 0.0
+    if smo_failed:
         # cooperative SMO: a member exchange timed out (members not co-resident beside concurrent
         # work) → re-solve with the one-workgroup kernel; working-set SMO: a problem needed more
         # than WS_ROUNDS_AHEAD rounds → re-solve with host-checked rounds.  Under a process group
@@ -1391,27 +1419,25 @@ def finish_svc_batch(st: dict, defer=None):
         return finish_svc_batch(st2)   # (no deferral after a re-solve: everything is final here)
     # ---- final models: ONE device→host read of the Platt (A, B) pairs and every final solve's
     # support mask, ρ and iteration count; the bookkeeping is then numpy, the gathers non-blocking
-    finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
+    # ---- final models: the support masks, ρ and iteration counts of every final solve (the early
+    # read, or one read with the Platt pairs); the bookkeeping is then numpy, the gathers non-blocking
     sols = [sol[id(p)] for p in finals]
     ls = [int(a.numel()) for a, _, _ in sols]
-    host = torch.cat([torch.cat([(a > 0).to(torch.float64).reshape(-1) for a, _, _ in sols]),
-                      torch.stack([torch.as_tensor(r).to(device=device, dtype=torch.float64).reshape(()) for _, r, _ in sols]),
-                      torch.stack([torch.as_tensor(it).to(device=device, dtype=torch.float64).reshape(()) for _, _, it in sols])]
-                     + ([st["ABt"].to(device=device, dtype=torch.float64)] if st["ABt"] is not None else [])
-                     ).cpu().numpy()
     from ..utils.timing import hmark
+    if early is not None:
+        host = host_e
+    else:
+        host = torch.cat([torch.cat([(a > 0).to(torch.float64).reshape(-1) for a, _, _ in sols]),
+                          torch.stack([torch.as_tensor(r).to(device=device, dtype=torch.float64).reshape(()) for _, r, _ in sols]),
+                          torch.stack([torch.as_tensor(it).to(device=device, dtype=torch.float64).reshape(()) for _, _, it in sols])]
+                         + ([st["ABt"].to(device=device, dtype=torch.float64)] if st["ABt"] is not None else [])
+                         ).cpu().numpy()
     hmark("svc_host_read")
     nl = sum(ls)
-    if st["ABt"] is not None:
-        ABc = host[nl + 2 * len(svcs):]
-        if not np.isfinite(ABc).all():
-            from ..utils.guards import NonFiniteError
-            raise NonFiniteError(f"SVC Platt sigmoid (A, B): {int((~np.isfinite(ABc)).sum())} non-finite value(s)")
-        for k, f in enumerate(st["pl"]):
-            AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
     offs = np.concatenate([[0], np.cumsum(ls)])
 
-    def fit_one(f):
+    def prep_one(f):
+        """Everything of fit f's set_fitted but the Platt pair (device gathers enqueued)."""
         svc, Z, mt = svcs[f], Zs[f], meta[f]
         a = sols[f][0].to(device)
         pos_np = np.nonzero(host[offs[f]:offs[f + 1]] > 0.5)[0]
@@ -1420,18 +1446,38 @@ def finish_svc_batch(st: dict, defer=None):
         coef = yint * a[pos_idx]
         support = _to_dev(mt["grouped"][pos_np].astype(np.int64), device)
         n_sv0 = int((pos_np < mt["n0"]).sum())
+        return dict(support=support, support_vectors=Z[support].to(torch.float64),
+                    n_support=[n_sv0, int(pos_np.shape[0]) - n_sv0], dual_coef_libsvm=coef,
+                    rho=float(host[nl + f]), gamma=mt["gamma"],
+                    class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
+                    shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
+
+    def set_one(f, kw):
         A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
-        svc.set_fitted(support=support, support_vectors=Z[support].to(torch.float64),
-                       n_support=[n_sv0, int(pos_np.shape[0]) - n_sv0], dual_coef_libsvm=coef,
-                       rho=float(host[nl + f]), probA=A, probB=B, gamma=mt["gamma"],
-                       class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
-                       shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
-        svc.n_iter_ = int(host[nl + len(svcs) + f])
+        svcs[f].set_fitted(probA=A, probB=B, **kw)
+        svcs[f].n_iter_ = int(host[nl + len(svcs) + f])
+
+    def read_ab():
+        if st["ABt"] is None:
+            return
+        ABc = (st["ABt"].to(torch.float64).cpu().numpy() if early is not None
+               else host[nl + 2 * len(svcs):])
+        if not np.isfinite(ABc).all():
+            from ..utils.guards import NonFiniteError
+            raise NonFiniteError(f"SVC Platt sigmoid (A, B): {int((~np.isfinite(ABc)).sum())} non-finite value(s)")
+        for k, f in enumerate(st["pl"]):
+            AB[f] = (float(ABc[2 * k]), float(ABc[2 * k + 1]))
+
+    def fit_one(f):
+        set_one(f, prep_one(f))
 
     later = [f for f in range(len(svcs)) if defer is not None and f in defer]
-    for f in range(len(svcs)):
-        if f not in later:
-            fit_one(f)
+    now = [f for f in range(len(svcs)) if f not in later]
+    kws = {f: prep_one(f) for f in now}     # (with the early read: while the Platt kernels run)
+    read_ab()
+    hmark("svc_platt_read")
+    for f in now:
+        set_one(f, kws[f])
     hmark("svc_set_fitted")
     if later:
         def rest():
