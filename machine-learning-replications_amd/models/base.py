@@ -31,8 +31,13 @@ class Estimator:
         return {k: getattr(self, k) for k in self._param_names}
 
     def clone(self):
-        """Unfitted copy with the same hyper-parameters (sklearn ``clone``)."""
-        return type(self)(**copy.deepcopy(self.get_params()))
+        """Unfitted copy with the same hyper-parameters (sklearn ``clone``).  Immutable parameter
+        values (numbers, strings, None) are shared as they are; anything else is deep-copied (the
+        stacking trainer clones a dozen estimators per fit on the SVC's critical path)."""
+        params = self.get_params()
+        if all(v is None or isinstance(v, (bool, int, float, str)) for v in params.values()):
+            return type(self)(**params)
+        return type(self)(**copy.deepcopy(params))
 
     def _fitted_tensors(self):
         for k, v in vars(self).items():
