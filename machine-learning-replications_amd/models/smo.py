@@ -1045,7 +1045,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     # ρ, iterations, the error word), queued right behind the SMO: finish_svc_batch extracts the
     # support vectors while the Platt and out-of-fold kernels still run, then reads only (A, B)
     fin = sorted((p.fit, k) for k, p in enumerate(live) if p.fold < 0)
-    if fin and len({f for f, _ in fin}) == len(fin):
+    if EARLY_READ and fin and len({f for f, _ in fin}) == len(fin):
         f64 = torch.float64
         ks = [k for _, k in fin]
         kidx = _to_dev(np.array(ks, dtype=np.int64), device)
@@ -1144,6 +1144,10 @@ def fit_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter
 # range (F > 24) keep the one-workgroup selector's 32,768-point limit.  Host (CPU): the exact solver
 # stores every problem's Gram, so it stays below EXACT_HOST_MAX points and GRAM_BUDGET bytes.
 EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "150000"))
+# the final solves' support masks / ρ / iterations read back right behind the SMO (before the Platt
+# kernels), so finish_svc_batch's support extraction overlaps them (same-box A/B of the headline:
+# within its ±0.7 ms run-to-run spread, scripts/probes/gpu_r4an.sh, profiles/r4_runs/early_read_ab.log)
+EARLY_READ = os.environ.get("HFENS_SVC_EARLY_READ", "1") != "0"
 EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 
