@@ -41,6 +41,21 @@ class BinMapper:
     nb_host: Optional[np.ndarray] = None   # host copy of nbins
     edges: Optional[torch.Tensor] = None   # [F, max_nb] f32 upper edges, +inf padded
 
+    def select(self, cols) -> "BinMapper":
+        """The bin map of a column subset (every feature's bins depend on that column alone, so this
+        equals a fit on the selected columns: the stacking trainer bins all candidate columns under
+        the LassoCV path and keeps the selected ones)."""
+        idx = np.asarray(cols, dtype=np.int64)
+        it = torch.as_tensor(idx, device=self.nbins.device)
+        nb = np.asarray(self.nb_host if self.nb_host is not None else self.nbins.cpu().numpy())[idx].astype(np.int32)
+        edges = None
+        if self.edges is not None:
+            K = int(nb.max()) if nb.shape[0] else 1
+            edges = self.edges.index_select(0, it)[:, :K].contiguous()
+        return BinMapper(self.nbins.index_select(0, it).contiguous(), self.lo_val.index_select(0, it).contiguous(),
+                         self.hi_val.index_select(0, it).contiguous(), [self.uppers[int(i)] for i in idx],
+                         self.max_bins, nb_host=nb.copy(), edges=edges)
+
     @property
     def max_nb(self) -> int:
         return int(self.nb_host.max()) if self.nb_host is not None else int(self.nbins.max())
@@ -399,18 +414,15 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None, guard=None) -> Bi
         raise_flags(torch.stack(list(guard[0])).cpu().tolist(), guard[1])
     if group is not None and not LEGACY_DP_BINS:
         return _fit_bins_dp(X32, max_bins, group)
-    Xh = X32.cpu().numpy() if host else None
+    if host:
+        return fit_bins_host(X32.cpu().numpy(), max_bins, dev)
     nb = np.empty(F, dtype=np.int32)
     lo = np.zeros((F, 256), dtype=np.float64)
     hi = np.zeros((F, 256), dtype=np.float64)
     for f in range(F):
-        if host:
-            uu, cc = np.unique(Xh[:, f], return_counts=True)
-            u, c = torch.from_numpy(uu), torch.from_numpy(cc.astype(np.int64))
-        else:
-            u, c = _distinct(X32[:, f].contiguous(), group)
-            u = u.cpu()
-            c = c.cpu()
+        u, c = _distinct(X32[:, f].contiguous(), group)
+        u = u.cpu()
+        c = c.cpu()
         k = u.numel()
         if k <= max_bins:
             nb[f] = k
@@ -428,4 +440,36 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None, guard=None) -> Bi
             nb[f] = g
             lo[f, :g] = u[starts].double().numpy()
             hi[f, :g] = u[ends].double().numpy()
+    return _finalize(nb, lo, hi, max_bins, dev)
+
+
+def fit_bins_host(Xh32: np.ndarray, max_bins: int, dev) -> BinMapper:
+    """The host fit of :func:`fit_bins` from a float32 host array [n, F] (the caller already holds
+    the rows on the host, e.g. a pinned copy read under earlier device work): numpy distinct values
+    per column, the same bins as every other path."""
+    if not 2 <= max_bins <= 256:
+        raise ValueError("max_bins must be in [2, 256]")
+    n, F = Xh32.shape
+    nb = np.empty(F, dtype=np.int32)
+    lo = np.zeros((F, 256), dtype=np.float64)
+    hi = np.zeros((F, 256), dtype=np.float64)
+    for f in range(F):
+        u, c = np.unique(Xh32[:, f], return_counts=True)
+        k = u.shape[0]
+        if k <= max_bins:
+            nb[f] = k
+            lo[f, :k] = u.astype(np.float64)
+            hi[f, :k] = u.astype(np.float64)
+        else:
+            cum = np.cumsum(c.astype(np.int64)).astype(np.float64)
+            tot = float(cum[-1])
+            # group end = last distinct value whose cumulative count reaches the quantile
+            targets = np.arange(1, max_bins, dtype=np.float64) * (tot / max_bins)
+            ends = np.minimum(np.searchsorted(cum, targets), k - 1)
+            ends = np.unique(np.concatenate([ends, [k - 1]]))
+            starts = np.concatenate([[0], ends[:-1] + 1])
+            g = ends.shape[0]
+            nb[f] = g
+            lo[f, :g] = u[starts].astype(np.float64)
+            hi[f, :g] = u[ends].astype(np.float64)
     return _finalize(nb, lo, hi, max_bins, dev)

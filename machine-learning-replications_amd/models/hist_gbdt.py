@@ -20,6 +20,7 @@ Exactness notes (vs sklearn ``GradientBoostingClassifier``):
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 import time
@@ -261,12 +262,19 @@ def _check_same(models, attrs):
 
 
 def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
-                   group=None, binned: Optional[tuple] = None):
+                   group=None, binned: Optional[tuple] = None, deferred=None, finish=None,
+                   state_out: Optional[dict] = None):
     """Fit ``len(models)`` GBDTs on row subsets ``masks[b]`` (bool [B, n]) of one matrix.
 
     ``group``: torch.distributed process group when rows are sharded across ranks
     (histograms / node sums / deviance are all-reduced; results are bit-identical
     to the single-device fit).  ``binned``: optional precomputed ``(BinMapper, bins)``.
+    ``deferred`` (:class:`hfens.utils.guards.Deferred`, single process on the GPU): the input and
+    leaf-value guards are queued on it instead of read here — the fit is then enqueued with no host
+    synchronisation at all (the stacking trainer reads them once after the SVC).  ``finish``: the
+    model indices whose fitted state is built (default all; the stacking trainer keeps only the
+    refit).  ``state_out``: receives the device state (node tables, prior log-odds) for device
+    out-of-fold predictions.
     """
     m0 = models[0]
     _check_same(models, ("n_estimators", "learning_rate", "max_depth", "min_samples_leaf",
@@ -282,7 +290,12 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     from ..utils.timing import hmark
     hmark("gbc_start")
     guard = None
-    if binned is None and X.is_cuda:
+    dfr = deferred if (deferred is not None and X.is_cuda and group is None) else None
+    if dfr is not None:
+        from ..utils.guards import binary_flag, finite_flag
+        dfr.flag(finite_flag(X), "finite", "GradientBoostingClassifier.fit X")
+        dfr.flag(binary_flag(y), "binary", "GradientBoostingClassifier.fit y")
+    elif binned is None and X.is_cuda:
         # deferred: read with the bin fit's first transfer (one host sync instead of three)
         from ..utils.guards import binary_flag, finite_flag
         guard = ([finite_flag(X), binary_flag(y)],
@@ -346,21 +359,48 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
             st.row_off = pdist.row_offset(n, group, dev)[0]
     if D == 1 and SKLEARN_TIES and subsample == 1.0 and all(
             isinstance(m.random_state, (int, np.integer)) for m in models):
-        st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group,
-                                       nb_host=bm.nb_host if (all_rows and group is None) else None)
+        if X.is_cuda and group is None and DEVICE_RANKS and F <= 128:
+            st.frank = stump_ranks_device(models, bins, w, T)
+        else:
+            st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group,
+                                           nb_host=bm.nb_host if (all_rows and group is None) else None)
     hmark("gbc_ranks")
+    st.no_persist = dfr is not None     # (a persistent loop's barrier fallback needs a host read)
     if X.is_cuda:
         _run_device(st, group)
     else:
         _run_host(st, group)
     hmark("gbc_enqueued")
+    if dfr is not None:
+        from ..utils.guards import finite_flag
+        dfr.flag(finite_flag(st.value), "finite", "GBDT leaf values")
+        _finish(models, st, sw, p1, group, only=finish)
+        if state_out is not None:
+            state_out.update(st=st, raw0=raw0, T=T, NN=NN, lr=float(m0.learning_rate))
+        hmark("gbc_finished")
+        return models
     check_finite(st.value, "GBDT leaf values")
     hmark("gbc_guarded")
     if getattr(st, "persist_err", None) is not None and int(st.persist_err.item()) != 0:
-        raise RuntimeError("GBDT persistent stage loop: a grid-barrier wait passed its deadline")
+        # a grid-barrier wait of the persistent loop passed its deadline (sibling workgroups not
+        # dispatched in time: CUs held by another stream's or process's kernels) — the trees are
+        # partial.  Re-run the fit launch per stage (no co-residency needed): same trees, bit for bit.
+        if _PERSIST_OFF[0]:
+            raise RuntimeError("GBDT persistent stage loop: a grid-barrier wait passed its deadline")
+        import warnings
+        warnings.warn("GBDT persistent stage loop: a grid-barrier wait passed its deadline; "
+                      "re-running with one launch per stage", RuntimeWarning, stacklevel=2)
+        LAST_PATH["persist_fallback"] = LAST_PATH.get("persist_fallback", 0) + 1
+        _PERSIST_OFF[0] = True
+        try:
+            return fit_gbdt_batch(models, X, y, None if all_rows else masks, group=group, binned=binned)
+        finally:
+            _PERSIST_OFF[0] = False
     if getattr(st, "peer", None) is not None:
         st.peer.check()     # (after the guard's host read: no extra synchronisation point)
-    _finish(models, st, sw, p1, group)
+    _finish(models, st, sw, p1, group, only=finish)
+    if state_out is not None:
+        state_out.update(st=st, raw0=raw0, T=T, NN=NN, lr=float(m0.learning_rate))
     hmark("gbc_finished")
     return models
 
@@ -401,11 +441,40 @@ def sklearn_stump_ranks(models, bins: torch.Tensor, masks: torch.Tensor, T: int,
     for b, m in enumerate(models):
         # GradientBoostingClassifier._rng = RandomState(random_state); each tree's splitter draws
         # one randint(0, RAND_R_MAX) (checkpoint: MT position = n_estimators)
-        seeds = np.random.RandomState(int(m.random_state)).randint(0, RAND_R_MAX, size=T).astype(np.int64)
+        seeds = _tree_seeds(int(m.random_state), T)
         rk = np.empty((T, F), dtype=np.int32)
         _stump_ranks(T, F, seeds, np.ascontiguousarray(const[b]), rk)
         out[:, b, :] = rk
     return torch.from_numpy(out).to(bins.device)
+
+
+DEVICE_RANKS = os.environ.get("HFENS_GBDT_DEVICE_RANKS", "1") != "0"
+
+
+@functools.lru_cache(maxsize=64)
+def _tree_seeds(random_state: int, T: int) -> np.ndarray:
+    """The trees' rand_r states: GradientBoostingClassifier._rng = RandomState(random_state), one
+    randint(0, RAND_R_MAX) per tree (a pure function of its arguments, drawn once per process)."""
+    s = np.random.RandomState(int(random_state)).randint(0, RAND_R_MAX, size=T).astype(np.int64)
+    s.setflags(write=False)
+    return s
+
+
+def stump_ranks_device(models, bins: torch.Tensor, w: torch.Tensor, T: int) -> torch.Tensor:
+    """:func:`sklearn_stump_ranks` on the device (ops/csrc/stackdev.hip gbdt_ranks_dev): each model's
+    constant features from its rows' bins and every tree's visit order in one launch — no host read."""
+    from .. import ops
+    F, n = bins.shape
+    B = len(models)
+    seeds = np.stack([_tree_seeds(int(m.random_state), T) for m in models])
+    from .smo import _to_dev
+    sd = _to_dev(np.ascontiguousarray(seeds), bins.device)
+    out = torch.empty(T, B, F, dtype=torch.int32, device=bins.device)
+    bc = bins.contiguous()
+    wc = w.to(torch.float32).contiguous()
+    ops.ext().gbdt_ranks_dev(T, B, F, n, bc.data_ptr(), n, wc.data_ptr(), sd.data_ptr(), out.data_ptr(),
+                             ops.stream_ptr(bins.device))
+    return out
 
 
 def _stump_ranks(T, F, seeds, const, out):
@@ -561,6 +630,7 @@ PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage w
 PERSIST = os.environ.get("HFENS_GBDT_PERSIST", "auto")
 PERSIST_MIN_ROWS = int(os.environ.get("HFENS_GBDT_PERSIST_MIN_ROWS", "65536"))
 PERSIST_MAX_WGS = int(os.environ.get("HFENS_GBDT_PERSIST_MAX_WGS", "128"))
+_PERSIST_OFF = [False]     # set while a fit re-runs after a persistent-loop barrier timeout
 LAST_STAGE_PROF: dict = {}
 
 
@@ -646,6 +716,7 @@ def _run_stage(st: _State, group):
     ev0 = torch.cuda.Event(enable_timing=True)
     ev0.record()
     persist = (group is None and prof is None and not uses_partials and st.B * groups <= _num_cus(dev)
+               and not _PERSIST_OFF[0] and not getattr(st, "no_persist", False)
                and (PERSIST == "1" or (PERSIST == "auto" and st.n >= PERSIST_MIN_ROWS
                                        and st.B * groups <= PERSIST_MAX_WGS)))
     GRAPH_INFO["persist"] = persist
@@ -799,7 +870,7 @@ def _run_device(st: _State, group):
                     _reduce_delta(st.r2[t], snap, group)
 
 
-def _finish(models, st: _State, sw, p1, group):
+def _finish(models, st: _State, sw, p1, group, only=None):
     if group is not None and not st.reduced:
         from ..parallel import dist as pdist
         pdist.all_reduce_sum_(st.dev, group)
@@ -820,6 +891,8 @@ def _finish(models, st: _State, sw, p1, group):
         train_score = (st.dev.double() / st.dscale) / sw[None, :]
     heap_l = torch.arange(st.NN, device=st.feat.device) * 2 + 1
     for b, m in enumerate(models):
+        if only is not None and b not in only:
+            continue
         feat = st.feat[:, b]
         leaf = feat < 0
         left = torch.where(leaf, torch.full_like(heap_l, -1), heap_l[None].expand(st.T, -1))

@@ -102,6 +102,7 @@ FUSED = os.environ.get("HFENS_LOGREG_FUSED", "1") != "0"
 MEMBERS = int(os.environ.get("HFENS_LOGREG_MEMBERS", "0"))   # 0 = auto
 MIN_ROWS_PER_MEMBER = 512
 LAST_PATH = {"path": None}
+_WARNED_EMULATION = [False]
 # workgroups a cooperative LR launch may occupy (None = all CUs).  The stacking trainer lowers it
 # while a cooperative SMO holds most CUs on another stream: LR members spin on each other, so all of
 # them must fit on the CUs the SMO leaves free (stack_trainer._fit_bases_concurrent).
@@ -178,6 +179,20 @@ def _finish_fused(h):
 
 
 _GUARD_SPECS = (("finite", "LogisticRegression.fit X"), ("binary", "LogisticRegression.fit y"))
+
+
+def set_fitted_from(h: dict, only=None):
+    """``set_fitted`` of a fused launch's models from its device coefficients, without the host read
+    of :func:`finish_logreg_batch` (the caller has read the launch's error word and guards itself,
+    e.g. through :class:`hfens.utils.guards.Deferred`).  ``only``: model indices to finish."""
+    models, F, scale, fit_intercept, dev = h["models"], h["F"], h["scale"], h["fit_intercept"], h["dev"]
+    W, iters = h["fused"]["args"][12], h["fused"]["args"][13]
+    for b, m in enumerate(models):
+        if only is not None and b not in only:
+            continue
+        intercept = W[b, F] * scale if fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
+        m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
+    return models
 
 
 def _allreduce(ts, group):
@@ -271,8 +286,18 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
     if m0.penalty not in ("l1", "l2"):
         raise NotImplementedError("penalty must be 'l1' or 'l2'")
     from ..utils import guards
-    emulate = (m0.penalty == "l1" and m0.solver == "liblinear" and group is None
-               and all(getattr(m, "emulate_liblinear", False) for m in models))
+    want = (m0.penalty == "l1" and m0.solver == "liblinear"
+            and all(getattr(m, "emulate_liblinear", False) for m in models))
+    emulate = want and group is None
+    if want and group is not None and not _WARNED_EMULATION[0]:
+        # rows sharded over ranks (the data-parallel policy): liblinear's sequential host iterate
+        # would need every row on every rank, so the device solve runs — the exact optimum of the
+        # same objective, not the reference's default-tolerance iterate and seed draw (T:31/T:46)
+        import warnings
+        warnings.warn("liblinear emulation is single-process only: with rows sharded over ranks 'lg' is "
+                      "solved to its exact optimum instead of reproducing liblinear's seeded iterate",
+                      RuntimeWarning, stacklevel=2)
+        _WARNED_EMULATION[0] = True
     fused = (X.is_cuda and group is None and FUSED and not emulate and X.dim() == 2
              and X.shape[1] + int(bool(m0.fit_intercept)) <= 64 and X.shape[0] > 0)
     flags = None

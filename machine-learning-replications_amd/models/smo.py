@@ -1158,10 +1158,13 @@ def use_lowrank(sizes, F: int = 17, device_type: str = "cpu") -> bool:
     if SOLVER in ("exact", "ws"):
         return False
     m = max(sizes)
-    if device_type == "cuda":
-        return m > EXACT_MAX_POINTS or (F > WS_KC_MAX_F and m >= 32768)
     # problem sizes ≈ 0.8·l (Platt folds) and l (final) per fit
     gram = sum(4.0 * (5 * (0.8 * l) ** 2 + l * l) for l in sizes)
+    if device_type == "cuda":
+        # past the working-set kernel's feature budget the device solver is the stored-Gram one
+        # (_pick_solver): its Grams must fit the budget too
+        return (m > EXACT_MAX_POINTS or (F > WS_KC_MAX_F and m >= 32768)
+                or (F > WS_MAX_F and gram > GRAM_BUDGET))
     return m > EXACT_HOST_MAX or gram > GRAM_BUDGET
 
 

@@ -51,6 +51,11 @@ DEVICE_SVC_OOF = os.environ.get("HFENS_DEVICE_SVC_OOF", "1") != "0"
 # cross_val_predict): their set_fitted (support-vector extraction, ≈ 0.3 ms of host work each) is
 # skipped.  0 = finish them anyway.
 SKIP_FOLD_SVC = os.environ.get("HFENS_SKIP_FOLD_SVC", "1") != "0"
+# GBC and L1-LR fold batches enqueued with no host synchronisation (single process, GPU): their
+# input / leaf guards and the LR launch's error word are read once after the SVC (utils.guards.Deferred),
+# their out-of-fold columns come from the device node tables / coefficients (ops/csrc/stackdev.hip),
+# and only the refit models are finished.  0 = the synchronous per-batch fits of round 4.
+DEVICE_BASES = os.environ.get("HFENS_DEVICE_BASES", "1") != "0"
 
 
 def _kind(est):
@@ -198,7 +203,7 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
 
 
 def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
-                          svc_pre=None, oof_svc_dev=None, early=None):
+                          svc_pre=None, oof_svc_dev=None, early=None, dev_bases=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -253,9 +258,13 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
             with torch.cuda.stream(other):
                 for i, (name, est) in enumerate(clf.estimators):
                     if i not in svc_cols:
-                        out[i] = fit_base_batch(est, X, y, masks, group=group)
-                        if oof is not None:
-                            oof(i, out[i])
+                        r = dev_bases["fit"](i, est) if dev_bases is not None else None
+                        if r is not None:
+                            out[i] = r        # enqueued, out-of-fold column on the device
+                        else:
+                            out[i] = fit_base_batch(est, X, y, masks, group=group)
+                            if oof is not None:
+                                oof(i, out[i])
                         hmark(f"{name}_host_done")
                         dmark(f"{name}_done")
         finally:
@@ -283,8 +292,97 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         hmark("svc_finished")
         main.wait_stream(side)
         main.wait_stream(other)
+        if dev_bases is not None:
+            # the GBC / LR guards and error words: ONE read, long after their kernels finished
+            dev_bases["deferred"].resolve()
+            for f in dev_bases["post"]:
+                f()
+            hmark("bases_resolved")
     hmarks_flush()
     return [out[i] for i in range(len(kinds))]
+
+
+def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
+    """Host-synchronisation-free GBC / L1-LR fold batches for :func:`_fit_bases_concurrent`
+    (:data:`DEVICE_BASES`).  ``fit(col, est)`` enqueues one estimator's 6 fits and its out-of-fold
+    column (rows of fold k predicted by fold model k, written into ``meta[:, col]``), or returns None
+    for estimators it does not handle; ``deferred`` / ``post`` complete them after the SVC."""
+    from .. import ops
+    from ..utils.guards import Deferred
+    from .logreg_solver import launch_logreg_batch, set_fitted_from
+    dev = X.device
+    n, F = X.shape
+    rows_np = np.concatenate([np.nonzero(folds_np == k)[0] for k in range(N_FOLDS)]).astype(np.int64)
+    model_np = np.concatenate([np.full(int((folds_np == k).sum()), k, dtype=np.int32) for k in range(N_FOLDS)])
+    oof_rows, oof_model = _index_to(rows_np, dev), _index_to(model_np, dev).to(torch.int32)
+    m = int(rows_np.shape[0])
+    Xc = X.to(torch.float64).contiguous()
+    deferred, post, keep = Deferred(), [], []
+    nb = int(masks.shape[0])
+    E = ops.ext()
+
+    def gbc(col, est):
+        clones = [est.clone() for _ in range(nb)]
+        binned = None
+        ba, cols = (plan or {}).get("bins_all"), (plan or {}).get("cols")
+        if ba is not None and cols is not None and int(ba.max_bins) == int(clones[0].max_bins):
+            bm = ba.select(cols)     # binned under the LassoCV path (pipeline.develop), columns selected here
+            binned = (bm, bm.transform(Xc).contiguous())
+        so = {}
+        fit_gbdt_batch(clones, Xc, y, masks, binned=binned, deferred=deferred, finish={nb - 1}, state_out=so)
+        st, raw0 = so["st"], so["raw0"].contiguous()
+        E.oof_trees(Xc.data_ptr(), F, oof_rows.data_ptr(), oof_model.data_ptr(), m, so["T"], nb, so["NN"],
+                    st.feat.data_ptr(), st.thr.data_ptr(), st.value.data_ptr(), raw0.data_ptr(), so["lr"],
+                    meta.data_ptr(), int(meta.shape[1]), col, ops.stream_ptr(dev))
+        keep.append((st, raw0))
+        return clones
+
+    def lr(col, est):
+        clones = [est.clone() for _ in range(nb)]
+        # masks are [fold 0 … fold K−1, refit]; scikit-learn fits the refit first (seed draw order)
+        h = launch_logreg_batch(clones, Xc, y, masks, seed_order=[nb - 1] + list(range(nb - 1)))
+        if "fused" not in h:        # host emulation / loop path: fitted already
+            if oof is not None:
+                oof(col, clones)
+            return clones
+        fz = h["fused"]
+        W, F1 = fz["args"][12], int(fz["args"][2])
+
+        def column():
+            E.oof_linear(Xc.data_ptr(), F, oof_rows.data_ptr(), oof_model.data_ptr(), m, W.data_ptr(), F1,
+                         int(h["fit_intercept"]), float(h["scale"]), meta.data_ptr(), int(meta.shape[1]), col,
+                         ops.stream_ptr(dev))
+        column()
+        if fz["flags"] is not None:
+            deferred.flag(fz["flags"][0], "finite", "LogisticRegression.fit X")
+            deferred.flag(fz["flags"][1], "binary", "LogisticRegression.fit y")
+            fz["flags"] = None
+        if fz["err"] is not None:
+            def on_fail(_v):
+                # a cooperative member timed out: the one-workgroup re-solve, a fresh column, and the
+                # meta model launched on the stale one is refitted
+                import warnings
+                from . import logreg_solver
+                warnings.warn("cooperative logistic regression timed out waiting for a member; re-solving "
+                              "with one workgroup per model")
+                logreg_solver.LAST_PATH["coop_fallback"] = True
+                logreg_solver._launch_single(fz)
+                column()
+                if early is not None:
+                    early["stale"] = True
+            deferred.word(fz["err"], on_fail)
+        post.append(lambda: set_fitted_from(h, only={nb - 1}))
+        return clones
+
+    def fit(col, est):
+        kind = _kind(est)
+        if kind == "gbc":
+            return gbc(col, est)
+        if kind == "lr":
+            return lr(col, est)
+        return None
+
+    return dict(fit=fit, deferred=deferred, post=post, keep=keep)
 
 
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
@@ -296,7 +394,7 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     n = X.shape[0]
     y_np = None
     svc_pre = None
-    if plan is not None and group is None and int(plan["y_np"].shape[0]) == n:
+    if plan is not None and group is None and plan.get("y_np") is not None and int(plan["y_np"].shape[0]) == n:
         # folds, row sets and SVC problem expansions computed ahead from the same labels (plan_stacking)
         y_np, folds_np, svc_pre = plan["y_np"], plan["folds_np"], plan["svc_pre"]
     elif group is None:
@@ -339,8 +437,11 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     early = None
     if group is None:
         early = {"launch": lambda: launch_logreg_batch([new_final()], meta, y64)}
+    dev_bases = None
+    if group is None and X.is_cuda and DEVICE_BASES:
+        dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
     fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre,
-                                       oof_svc_dev if group is None else None, early)
+                                       oof_svc_dev if group is None else None, early, dev_bases)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream

@@ -927,6 +927,7 @@ struct StageJob {
   const int* t_dev;                   // stage index read from device memory (graph replay), or nullptr: t
   unsigned* bar;                      // persistent launch: [B] monotone per-model barrier counters (zeroed)
   unsigned* err;                      // persistent launch: set when a barrier wait passed its deadline
+  long long deadline;                 // persistent launch: barrier wait limit in 100 MHz ticks (< 0: fail at once)
 };
 
 // Barrier of the persistent stage loop (gbdt_stump_stage with persist = 1).  Models are independent
@@ -937,8 +938,10 @@ struct StageJob {
 // XCD's next-stage reads.  Residency: the grid is at most one workgroup per CU (sg_plan) and no
 // workgroup waits on anything but this counter, so workgroups that are not yet resident (CUs held
 // by another stream's kernels) are dispatched as those finish.  A wait past the deadline (fixed
-// 100 MHz s_memrealtime clock) sets *err and every workgroup leaves the loop.
-__device__ __forceinline__ bool sg_grid_barrier(unsigned* bar, unsigned* err, unsigned target) {
+// 100 MHz s_memrealtime clock, HFENS_GBDT_PERSIST_DEADLINE_MS, 2 s by default) sets *err and every
+// workgroup leaves the loop; the host then re-runs the fit launch per stage (models/hist_gbdt.py).
+// A negative deadline injects that failure at the first barrier (tests of the fallback).
+__device__ __forceinline__ bool sg_grid_barrier(unsigned* bar, unsigned* err, unsigned target, long long deadline) {
   __syncthreads();
   __shared__ int s_ok;
   if (threadIdx.x == 0) {
@@ -948,7 +951,7 @@ __device__ __forceinline__ bool sg_grid_barrier(unsigned* bar, unsigned* err, un
     int ok = 1;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-          (long long)__builtin_amdgcn_s_memrealtime() - t0 > 200000000LL) {   // 2 s
+          deadline < 0 || (long long)__builtin_amdgcn_s_memrealtime() - t0 > deadline) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -1125,7 +1128,7 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   }
   for (int t = t_first;; ++t) {
   if constexpr (Persist) {
-    if (t > t_first && !sg_grid_barrier(J.bar + b, J.err, (unsigned)(t - t_first) * gridDim.x)) return;
+    if (t > t_first && !sg_grid_barrier(J.bar + b, J.err, (unsigned)(t - t_first) * gridDim.x, J.deadline)) return;
     if (tid == 0) { pf_s = -3; pblo_s = 0; pv_s[0] = pv_s[1] = pv_s[2] = 0.0; }
   }
   long long* slot_prev = J.comm + (size_t)((t + 2) % 3) * slot_sz + (size_t)b * slot_m;
@@ -1687,7 +1690,8 @@ void gbdt_stump_stage(int t, int B, int n, int F, int T, uintptr_t bins, long lo
              (long long*)r2, (long long*)dev, (double*)bagw, (const int*)frank, row_off, lr, qscale, dscale,
              min_leaf_q, min_split_q, (unsigned)llround(subsample * 16777216.0), active ? 1 : 0, B, n, F, T,
              hist_len, t, 0, ldb, (long long*)partials, (long long*)prof, (const int*)t_dev, (unsigned*)bar,
-             (unsigned*)err};
+             (unsigned*)err, 200000000LL};
+  if (const char* dl = std::getenv("HFENS_GBDT_PERSIST_DEADLINE_MS")) J.deadline = std::atoll(dl) * 100000LL;
   // t_dev (graph replay): the kernel takes the stage index from device memory; the host t still
   // selects the comm slot of the reduce launch, so a captured unit must start at t ≡ 0 (mod 3)
   HFENS_REQUIRE(ldb >= n && ldb % kSgTile == 0 && (bins & 15) == 0, "gbdt_stump_stage: bins must be [F][ldb], ldb % 1024 == 0, 16-byte aligned");

@@ -35,6 +35,44 @@ DP_POLICY = os.environ.get("HFENS_DP_POLICY", "auto")
 TASK_MAX_ROWS = int(os.environ.get("HFENS_TASK_MAX_ROWS", str(1 << 18)))
 AUX_STREAM = os.environ.get("HFENS_AUX_STREAM", "1") != "0"   # held-out imputation on a side stream
 PLAN_AHEAD = os.environ.get("HFENS_PLAN_AHEAD", "1") != "0"   # stacking bookkeeping under the LassoCV path
+# the GBC's bin map of every candidate column fitted on the host under the LassoCV path (the selected
+# columns' bins are then a slice: binning.BinMapper.select), from one non-blocking copy of the imputed rows
+BIN_AHEAD = os.environ.get("HFENS_BIN_AHEAD", "1") != "0"
+
+
+def _bins_ahead(X_dev: torch.Tensor, clf):
+    """Enqueue the float32 copy of the imputed development rows to pinned host memory on a side
+    stream and return ``run()`` → the host bin fit of all columns (or None when the stack has no
+    gradient-boosting member).  ``run`` waits only for that copy."""
+    from .models.gbdt import GradientBoostingClassifier
+    mb = [int(e.max_bins) for _, e in clf.estimators if isinstance(e, GradientBoostingClassifier)]
+    if not mb or X_dev.shape[0] > (1 << 15):
+        return None
+    from . import runtime
+    dev = X_dev.device
+    side = runtime.stream(dev, "bins_ahead")
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        x32 = X_dev.to(torch.float32)
+        xh = torch.empty(x32.shape, dtype=torch.float32, pin_memory=True)
+        xh.copy_(x32, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    X_dev.record_stream(side)
+    box = {}
+
+    def run():
+        if "bm" not in box:
+            from .models.binning import fit_bins_host
+            ev.synchronize()
+            # (the bin tables' uploads go on the idle side stream: on the current stream they would
+            # queue behind the LassoCV path)
+            with torch.cuda.stream(side):
+                box["bm"] = fit_bins_host(xh.numpy(), mb[0], dev)
+            box["ev"] = torch.cuda.Event()
+            box["ev"].record(side)
+        return box["bm"], box["ev"]
+    return run
 
 
 def choose_policy(n_total: int) -> str:
@@ -119,6 +157,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         else:
             X_dev, X_sel = imputer.transform_many([X_dev, X_sel], streams=[None, aux])
         hmark("impute_enqueued")
+        bins_job = _bins_ahead(X_dev, clf) if (BIN_AHEAD and dev.type == "cuda" and group is None) else None
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
             y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
@@ -126,13 +165,24 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 overlap = plan_ahead(y_dev)
     fit_group = None if task else group
     with timer.stage("select"):
-        lasso_overlap = overlap
+        jobs = []
         if run_sel is not None:
-            def lasso_overlap():
+            def held_out():
                 run_sel()
                 hmark("heldout_impute_enqueued")
-                if overlap is not None:
-                    overlap()
+            jobs.append(held_out)
+        if overlap is not None:
+            jobs.append(overlap)
+        if bins_job is not None:
+            def bins():
+                plan_box["bins_all"] = bins_job()
+                hmark("bins_ahead")
+            jobs.append(bins)
+        lasso_overlap = None
+        if jobs:
+            def lasso_overlap():
+                for j in jobs:
+                    j()
         sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=lasso_overlap)
         if run_sel is not None:
             X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
@@ -143,8 +193,13 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         X_dev_optm = X_dev[:, mt]
         fn_new = [n for n, m in zip(names, mask) if m]
         hmark("selected")
+    plan = plan_box.get("plan")
+    if "bins_all" in plan_box:
+        bm_all, bm_ev = plan_box["bins_all"]
+        torch.cuda.current_stream(dev).wait_event(bm_ev)
+        plan = dict(plan or {}, bins_all=bm_all, cols=np.nonzero(mask)[0])
     clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None,
-            plan=plan_box.get("plan"))
+            plan=plan)
     dmark("stack_fit")
     if aux is not None:
         # join the side stream while the imputer and X_sel are alive (their blocks are not reused

@@ -48,3 +48,40 @@ def raise_flags(vals, specs) -> None:
             if kind == "finite":
                 raise NonFiniteError(f"{what}: non-finite value(s)")
             raise ValueError(f"{what}: labels must be 0/1")
+
+
+class Deferred:
+    """Device-side checks of a chain of fits read back in ONE transfer at its end (the stacking
+    trainer's base models: no host synchronisation between their launches and the meta model's).
+
+    ``flag(t, kind, what)``: a device bool (``finite_flag`` / ``binary_flag``) that raises like the
+    synchronous check if false; ``word(t, on_fail)``: a device integer whose non-zero value calls
+    ``on_fail(value)`` (solver fallbacks).  ``resolve()`` reads everything, runs the fallbacks, then
+    raises the first failed guard."""
+
+    def __init__(self):
+        self._flags, self._specs, self._words, self._hooks = [], [], [], []
+
+    def flag(self, t: torch.Tensor, kind: str, what: str) -> None:
+        self._flags.append(t.reshape(1).to(torch.int64))
+        self._specs.append((kind, what))
+
+    def word(self, t: torch.Tensor, on_fail) -> None:
+        self._words.append(t.reshape(-1)[:1].to(torch.int64))
+        self._hooks.append(on_fail)
+
+    def __len__(self) -> int:
+        return len(self._flags) + len(self._words)
+
+    def resolve(self) -> None:
+        if not len(self):
+            return
+        host = torch.cat(self._words + self._flags).cpu().tolist()
+        nw = len(self._words)
+        words, flags = host[:nw], host[nw:]
+        specs, hooks = self._specs, self._hooks
+        self._flags, self._specs, self._words, self._hooks = [], [], [], []
+        for v, h in zip(words, hooks):
+            if v != 0:
+                h(v)
+        raise_flags(flags, specs)

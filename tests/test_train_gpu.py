@@ -744,3 +744,86 @@ def test_gbdt_stage_persistent_bit_identical(dev, monkeypatch, rows, subsample, 
     for a, b in zip(out["0"], out["1"]):
         for u, v in zip(a, b):
             assert np.array_equal(u, v)
+
+
+def test_gbdt_persistent_barrier_timeout_falls_back(dev, monkeypatch):
+    """A persistent-loop grid-barrier wait past its deadline (here injected at the first barrier:
+    HFENS_GBDT_PERSIST_DEADLINE_MS < 0) no longer fails the fit: the boosting re-runs with one launch
+    per stage in the same process and gives the launch-per-stage model bit for bit."""
+    from hfens.models import hist_gbdt
+    monkeypatch.setattr(hist_gbdt, "STUMP_PATH", "stage")
+    monkeypatch.setattr(hist_gbdt, "FUSED_STUMPS", False)
+    rows = 130000
+    X, y = _data(rows, 24, 31)
+    masks = torch.ones(2, rows, dtype=torch.bool)
+    masks[1, ::3] = False
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(hist_gbdt, "PERSIST", mode)
+        if mode == "1":
+            monkeypatch.setenv("HFENS_GBDT_PERSIST_DEADLINE_MS", "-1")
+            hist_gbdt.LAST_PATH.pop("persist_fallback", None)
+        ms = [GradientBoostingClassifier(n_estimators=20, max_depth=1, random_state=s) for s in (3, 4)]
+        if mode == "1":
+            with pytest.warns(RuntimeWarning, match="deadline"):
+                fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+            assert hist_gbdt.LAST_PATH.get("persist_fallback") == 1
+            assert not hist_gbdt._PERSIST_OFF[0]
+        else:
+            fit_gbdt_batch(ms, X.to(dev), y.to(dev), masks.to(dev))
+        out[mode] = _gbdt_outputs(ms)
+    for a, b in zip(out["0"], out["1"]):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
+def test_stump_ranks_device_matches_host(dev):
+    """sklearn's root feature-visit order computed on the device (stackdev.hip gbdt_ranks_dev: each
+    model's constant features from its rows' bins, the rand_r Fisher-Yates per tree) equals the host
+    computation, including features constant on one model's rows only."""
+    from hfens.models import hist_gbdt
+    from hfens.models.binning import fit_bins
+    X, _ = _data(4000, 17, 12)
+    X[:, 4] = 1.0                                   # constant everywhere
+    X[:, 6] = 0.0
+    X[:5, 6] = 1.0                                  # constant on the rows of models that skip 0-4
+    masks = torch.ones(4, 4000, dtype=torch.bool)
+    masks[1, :5] = False
+    masks[2, ::3] = False
+    masks[3, 2000:] = False
+    Xd = X.to(dev)
+    bins = fit_bins(Xd, 256).transform(Xd).contiguous()
+    ms = [GradientBoostingClassifier(n_estimators=60, max_depth=1, random_state=s) for s in (2020, 7, 2020, 8)]
+    host = hist_gbdt.sklearn_stump_ranks(ms, bins, masks.to(dev), 60)
+    devr = hist_gbdt.stump_ranks_device(ms, bins, masks.to(dev).float(), 60)
+    assert torch.equal(host.cpu(), devr.cpu())
+
+
+def test_stacking_device_bases_match_synchronous(dev, monkeypatch):
+    """The host-synchronisation-free GBC / L1-LR fold batches (stack_trainer.DEVICE_BASES: deferred
+    guards, device stump ranks, bins from the all-column map fitted under the LassoCV path, device
+    out-of-fold columns) give the synchronous round-4 fit: the same refit trees and coefficients bit
+    for bit, out-of-fold columns to the f32 tree-walk rounding of the old path (its forest kernel
+    adds f32 leaf values; the device column is the f64 sum the reference's predict_proba forms)."""
+    from hfens import pipeline
+    from hfens.models import stack_trainer
+    Xd, yd, names = make_hf_cohort(3000, 40, seed=93, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(1000, 40, seed=94, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(stack_trainer, "DEVICE_BASES", flag)
+        monkeypatch.setattr(pipeline, "BIN_AHEAD", flag)
+        out[flag] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+    m0, m1 = out[False].model, out[True].model
+    assert np.array_equal(out[False].selected, out[True].selected)
+    g0, g1 = m0.estimators_[1], m1.estimators_[1]
+    for a in ("tree_feature_", "tree_threshold_", "tree_value_", "tree_impurity_", "train_score_"):
+        assert torch.equal(getattr(g0, a).cpu(), getattr(g1, a).cpu()), a
+    l0, l1 = m0.estimators_[2], m1.estimators_[2]
+    assert torch.equal(l0.coef_.cpu(), l1.coef_.cpu()) and torch.equal(l0.intercept_.cpu(), l1.intercept_.cpu())
+    d = (m0.oof_meta_ - m1.oof_meta_).abs()
+    assert float(d[:, 0].max()) == 0.0                    # the SVC column is untouched
+    assert float(d[:, 1].max()) <= 1e-6, float(d[:, 1].max())
+    assert float(d[:, 2].max()) <= 1e-12, float(d[:, 2].max())
+    assert float((out[False].proba_sel - out[True].proba_sel).abs().max()) <= 1e-5
