@@ -329,13 +329,20 @@ def _assemble(k_h, small_h, hi_h, lo_h, mn_h, max_bins: int, dev) -> BinMapper:
     return _finalize(nb, lo, hi, max_bins, dev)
 
 
-def _finalize(nb: np.ndarray, lo: np.ndarray, hi: np.ndarray, max_bins: int, dev) -> BinMapper:
-    """Edges of every feature at once (:func:`_edges_all`) and the device tables."""
+def _finalize(nb: np.ndarray, lo: np.ndarray, hi: np.ndarray, max_bins: int, dev,
+              non_blocking: bool = False) -> BinMapper:
+    """Edges of every feature at once (:func:`_edges_all`) and the device tables.  ``non_blocking``:
+    pinned copies that do not wait for the current stream's queued work."""
     E = _edges_all(lo, hi, nb)
-    edges = torch.from_numpy(E).to(dev)
+
+    def up(a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if non_blocking and torch.device(dev).type == "cuda":
+            return t.pin_memory().to(dev, non_blocking=True)
+        return t.to(dev)
+    edges = up(E)
     uppers = [edges[f, :int(nb[f])] for f in range(nb.shape[0])]
-    nbt = torch.from_numpy(nb.astype(np.int32))
-    return BinMapper(nbt.to(dev), torch.from_numpy(lo).to(dev), torch.from_numpy(hi).to(dev), uppers, max_bins,
+    return BinMapper(up(nb.astype(np.int32)), up(lo), up(hi), uppers, max_bins,
                      nb_host=nb.astype(np.int32).copy(), edges=edges)
 
 
@@ -443,7 +450,7 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None, guard=None) -> Bi
     return _finalize(nb, lo, hi, max_bins, dev)
 
 
-def fit_bins_host(Xh32: np.ndarray, max_bins: int, dev) -> BinMapper:
+def fit_bins_host(Xh32: np.ndarray, max_bins: int, dev, non_blocking: bool = False) -> BinMapper:
     """The host fit of :func:`fit_bins` from a float32 host array [n, F] (the caller already holds
     the rows on the host, e.g. a pinned copy read under earlier device work): numpy distinct values
     per column, the same bins as every other path."""
@@ -472,4 +479,4 @@ def fit_bins_host(Xh32: np.ndarray, max_bins: int, dev) -> BinMapper:
             nb[f] = g
             lo[f, :g] = u[starts].astype(np.float64)
             hi[f, :g] = u[ends].astype(np.float64)
-    return _finalize(nb, lo, hi, max_bins, dev)
+    return _finalize(nb, lo, hi, max_bins, dev, non_blocking)

@@ -106,7 +106,8 @@ class GradientBoostingClassifier(Estimator):
                    rng_state=None, device=None):
         self.n_features_in_ = int(n_features)
         self.n_features_ = int(n_features)
-        self.classes_ = torch.tensor([0, 1], dtype=torch.int64, device=device)
+        # (arange: a device fill, not a blocking host→device copy behind the stream's queued work)
+        self.classes_ = torch.arange(2, dtype=torch.int64, device=device)
         self.n_classes_ = 2
         self.max_features_ = int(n_features)
         self.tree_feature_ = as_tensor(feature, device, torch.int32)

@@ -374,9 +374,14 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
     if dfr is not None:
         from ..utils.guards import finite_flag
         dfr.flag(finite_flag(st.value), "finite", "GBDT leaf values")
-        _finish(models, st, sw, p1, group, only=finish)
-        if state_out is not None:
-            state_out.update(st=st, raw0=raw0, T=T, NN=NN, lr=float(m0.learning_rate))
+        # the fitted state (node tables → model attributes) is built by the caller after its
+        # deferred read: building it here could queue blocking host→device copies behind the
+        # stage loop on this stream, i.e. wait for it
+        fin = lambda: _finish(models, st, sw, p1, group, only=finish)   # noqa: E731
+        if state_out is None:
+            fin()
+        else:
+            state_out.update(st=st, raw0=raw0, T=T, NN=NN, lr=float(m0.learning_rate), finish=fin)
         hmark("gbc_finished")
         return models
     check_finite(st.value, "GBDT leaf values")
@@ -900,7 +905,7 @@ def _finish(models, st: _State, sw, p1, group, only=None):
         m.set_fitted(feature=torch.where(feat == -3, torch.full_like(feat, -2), feat),
                      threshold=st.thr[:, b], left=left, right=right, value=st.value[:, b],
                      impurity=imp[:, b], n_node_samples=torch.round(wsum[:, b]).to(torch.int64),
-                     weighted_n_node_samples=wsum[:, b], node_count=torch.full((st.T,), st.NN),
+                     weighted_n_node_samples=wsum[:, b], node_count=torch.full((st.T,), st.NN, device=st.feat.device),
                      class_prior=torch.stack([1 - p1[b], p1[b]]).double(), train_score=train_score[:, b],
                      n_features=st.F, rng_state=None, device=st.feat.device)
         m.tree_layout_ = "heap"

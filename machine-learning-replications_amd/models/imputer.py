@@ -160,17 +160,21 @@ class KNNImputer(Estimator):
         E = ops.ext()
         n, F = X.shape
         # the work lists from the rows' missing-column bitmasks, planned natively (host.hip
-        # knn_plan_host) into ONE pinned buffer → one H2D copy, sliced on the device
+        # knn_plan_host) into ONE pinned buffer → one H2D copy, sliced on the device.  A counting
+        # call sizes the buffer exactly (2·nr + nr·nslot + 3·nc: only the missing cells, not the
+        # worst case of every cell missing)
         dev = X.device
-        nslot_max = -(-F // SLOTS) * SLOTS
-        cap = 2 * n + n * nslot_max + 3 * n * F
-        hb = torch.empty(cap, dtype=torch.int64, pin_memory=True)
-        dims = np.zeros(3, dtype=np.int64)
+        dims = np.zeros(4, dtype=np.int64)
         bits = np.ascontiguousarray(bits, dtype=np.uint64)
-        E.knn_plan_host(bits.ctypes.data, n, F, SLOTS, hb.data_ptr(), cap, dims.ctypes.data)
-        nr, nc, nslot = (int(v) for v in dims)
-        if nr <= 0:
+        E.knn_plan_host(bits.ctypes.data, n, F, SLOTS, 0, 0, dims.ctypes.data)
+        nr, nc, nslot = (int(v) for v in dims[:3])
+        if nr == 0:
             return
+        cap = 2 * nr + nr * nslot + 3 * nc
+        hb = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+        E.knn_plan_host(bits.ctypes.data, n, F, SLOTS, hb.data_ptr(), cap, dims.ctypes.data)
+        if int(dims[3]) != 0 or int(dims[0]) != nr:
+            raise RuntimeError(f"knn_plan_host: work-list buffer of {cap} words rejected (dims {dims.tolist()})")
         center = self._col_mean
         from ..utils.timing import hmark
         hmark("imp_plan")

@@ -164,8 +164,6 @@ class LassoCV(Estimator):
         dmark("lasso_cv_in")
         coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
         dmark("lasso_cv_path")
-        if overlap is not None:
-            overlap()
         # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
         inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
         # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
@@ -178,12 +176,21 @@ class LassoCV(Estimator):
               + nt[:, None] * c * c - 2 * c * Ty[:, None] + Tyy[:, None])
         mse = se / nt[:, None]                                                          # [k, A]
         mean_mse = mse.mean(0)
-        best = int(torch.argmin(mean_mse))
+        best_dev = torch.argmin(mean_mse)
+        self.coef_dev_ = None
+        if refit_all is not None:
+            # the winner's coefficients stay on the device (no host read): a caller's overlap can
+            # queue work that depends on them (SelectFromModel's device column list → the stacking
+            # trainer's SVC batch) before this fit reads anything back
+            torch.cuda.current_stream(dev).wait_event(ev)
+            self.coef_dev_ = refit_all.index_select(0, best_dev.reshape(1))[0, 0]
+        if overlap is not None:
+            overlap()
+        best = int(best_dev)
         self.alpha_ = float(grid[best])
         self.alphas_ = grid
         self.mse_path_ = mse.t()
         if refit_all is not None:
-            torch.cuda.current_stream(dev).wait_event(ev)
             w = refit_all[best, 0]
         else:
             final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
@@ -204,8 +211,28 @@ class SelectFromModel(Estimator):
         self.threshold = threshold
         self.max_features = max_features
 
+    def _device_columns(self, coef_dev: torch.Tensor, F: int):
+        """The selected columns (ascending) from device coefficients, on the device: feature f is
+        kept iff its rank in ``argsort(−|coef|, kind='mergesort')`` (ties: lower index first) is
+        below max_features — the host rule of :meth:`fit` for threshold=-inf."""
+        k = min(int(self.max_features), F)
+        s = coef_dev.abs()
+        idx = torch.arange(F, device=s.device)
+        rank = ((s[None, :] > s[:, None]) | ((s[None, :] == s[:, None]) & (idx[None, :] < idx[:, None]))).sum(1)
+        key = torch.where(rank < k, idx, idx + F)
+        return torch.sort(key, stable=True).values[:k]
+
     def fit(self, X, y, group=None, overlap=None):
+        self.cols_dev_ = None
         if overlap is not None and isinstance(self.estimator, LassoCV):
+            user = overlap
+            if (self.max_features is not None and isinstance(self.threshold, float)
+                    and np.isneginf(self.threshold)):
+                def overlap():
+                    cd = getattr(self.estimator, "coef_dev_", None)
+                    if cd is not None:
+                        self.cols_dev_ = self._device_columns(cd, int(cd.shape[0]))
+                    user()
             self.estimator_ = self.estimator.fit(X, y, group=group, overlap=overlap)
         else:
             self.estimator_ = self.estimator.fit(X, y, group=group)

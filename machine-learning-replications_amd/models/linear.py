@@ -78,7 +78,8 @@ class LogisticRegression(Estimator):
 
     def set_fitted(self, coef, intercept, n_iter, n_features, device=None):
         self.n_features_in_ = int(n_features)
-        self.classes_ = torch.tensor([0, 1], dtype=torch.int64, device=device)
+        # (arange: a device fill, not a blocking host→device copy behind the stream's queued work)
+        self.classes_ = torch.arange(2, dtype=torch.int64, device=device)
         self.coef_ = as_tensor(coef, device).reshape(1, -1)
         self.intercept_ = as_tensor(intercept, device).reshape(1)
         self.n_iter_ = as_tensor(n_iter, device, torch.int32).reshape(1)

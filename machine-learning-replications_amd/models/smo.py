@@ -1,5 +1,8 @@
 """Batched C-SVC training with libsvm semantics.
 
+Licence: the host mirrors ``_smo_host`` / ``_sigmoid_train_host`` follow LIBSVM
+(BSD-3-Clause, Chang & Lin; THIRD_PARTY_NOTICES.md).
+
 ``fit_svc_batch`` trains any number of RBF ``SVC(probability=True)`` fits at once.
 Each fit expands into libsvm's problems:
 
@@ -848,6 +851,8 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
                 return torch.zeros(numel, dtype=dtype, device=device)
             pdev = _dev_struct(arr, device)
             host = None
+        if _GAMMA_CTX[0] is not None:
+            _GAMMA_CTX[0].patch(pdev, _WS_DT, "ngl2e", [live[j].fit for j in idx])
         states = buf("states", P * _WS_STATE_BYTES // 4, torch.int32)
         wsz = buf("wsz", P * Fp2 * Q, torch.float32)
         wsn = buf("wsn", P * Q, torch.float32)
@@ -1084,6 +1089,8 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
             hoff += h
         part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
         ddev = _dev_struct(dt, device)
+        if _GAMMA_CTX[0] is not None:
+            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt])
         max_h = int(dt["h"].max())
         dmark("svc_smo_done")
         E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(platt),
@@ -1168,8 +1175,51 @@ def use_lowrank(sizes, F: int = 17, device_type: str = "cpu") -> bool:
     return m > EXACT_HOST_MAX or gram > GRAM_BUDGET
 
 
+class _GammaDev:
+    """γ of every fit computed on the device (``svm_gamma``): the problem records built on the host
+    carry a placeholder that :meth:`patch` overwrites on the device, so no host read of the scaled
+    data's variance stands between the scaler and the SMO."""
+
+    def __init__(self, Zs, device):
+        from .. import ops
+        K, F = len(Zs), int(Zs[0].shape[1])
+        base = Zs[0]
+        lens = [int(Z.shape[0]) for Z in Zs]
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        contiguous = all(Z.is_contiguous() and Z.dtype == torch.float64 for Z in Zs) and all(
+            Zs[k].data_ptr() == base.data_ptr() + int(offs[k]) * F * 8 for k in range(K))
+        Zc = base if contiguous else torch.cat([Z.to(torch.float64) for Z in Zs]).contiguous()
+        self.offs = _to_dev(offs, device)
+        self.gam = torch.empty(K, dtype=torch.float64, device=device)
+        self.ngl = torch.empty(K, dtype=torch.float32, device=device)
+        ops.ext().svm_gamma(Zc.data_ptr(), self.offs.data_ptr(), K, F, self.gam.data_ptr(), self.ngl.data_ptr(),
+                            ops.stream_ptr(device))
+        self.keep = [Zc]
+
+    def patch(self, ddev: torch.Tensor, dtype: np.dtype, field: str, fits) -> None:
+        from .. import ops
+        fo = _to_dev(np.asarray(fits, dtype=np.int32), ddev.device)
+        ops.ext().svm_patch_f32(ddev.data_ptr(), int(dtype.itemsize), int(dtype.fields[field][1]), len(fits),
+                                fo.data_ptr(), self.ngl.data_ptr(), ops.stream_ptr(ddev.device))
+        self.keep.append(fo)
+
+    def resolve(self, all_probs, meta) -> None:
+        """The host's γ (models, host mirrors): one small read, after the SMO."""
+        g = self.gam.cpu().numpy()
+        if not np.isfinite(g).all():
+            from ..utils.guards import NonFiniteError
+            raise NonFiniteError("SVC.fit X: non-finite scaled value(s)")
+        for p in all_probs:
+            p.gamma = float(g[p.fit])
+        for f, mt in enumerate(meta):
+            mt["gamma"] = float(g[f])
+
+
+_GAMMA_CTX: list = [None]
+
+
 def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None,
-                     y_host=None, plan=None) -> dict:
+                     y_host=None, plan=None, gamma_dev: bool = False) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
@@ -1182,7 +1232,13 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
 
     ``y_host``: the fits' labels as host arrays (the caller already has them): the libsvm problem
     expansion then runs on the host while the device computes the guards and γ statistics, and
-    only those are read back."""
+    only those are read back.
+
+    ``gamma_dev`` (single process, GPU, a ``plan`` of 0/1 labels, gamma='scale', the working-set
+    solver): NO host read at all — γ is computed and patched into the problem records on the device
+    (:class:`_GammaDev`), the labels' 0/1 guard ran in the plan, and the scaled rows' finite guard is
+    the γ's own (read by :func:`finish_svc_batch`).  The stacking trainer uses it to enqueue the
+    whole batch before the selected columns reach the host (pipeline.develop)."""
     from .. import ops
     if use_lowrank([int(y.numel()) for y in ys], int(Zs[0].shape[1]), Zs[0].device.type):
         from .svc_lowrank import fit_svc_lowrank_batch
@@ -1209,16 +1265,22 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     sizes = [int(y.numel()) for y in ys]
     need_var = [svc.gamma == "scale" for svc in svcs]
     f64 = torch.float64
-    parts = []
-    if guards.ENABLED:
-        parts.append(torch.stack([torch.isfinite(Z).all() for Z in Zs]).to(f64))
-        parts.append(torch.stack([((y == 0) | (y == 1)).all() for y in ys]).to(f64))
-    if any(need_var):
-        parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
     pre = None
     if plan is not None and len(plan) == len(svcs) and all(int(p[0].shape[0]) == int(y.numel()) for p, y in zip(plan, ys)):
         pre = plan   # expanded ahead of time (plan_svc_problems), overlapped with earlier device work
         hmark("svc_expand_planned")
+    gdev = None
+    if (gamma_dev and cuda and group is None and pre is not None and all(need_var)
+            and _pick_solver(max(int(p.l) for _, pr, _ in pre for p in pr), int(Zs[0].shape[1])) == "ws"):
+        gdev = _GammaDev(Zs, device)
+    parts = []
+    if guards.ENABLED and gdev is None:
+        parts.append(torch.stack([torch.isfinite(Z).all() for Z in Zs]).to(f64))
+        parts.append(torch.stack([((y == 0) | (y == 1)).all() for y in ys]).to(f64))
+    if any(need_var) and gdev is None:
+        parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
+    if pre is not None:
+        pass
     elif y_host is not None and all(np.isin(np.unique(yh), (0.0, 1.0)).all() for yh in y_host):
         # host labels: expand the problems now (γ filled in below), overlapping the device work
         pre = []
@@ -1230,7 +1292,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         parts.append(torch.cat([y.reshape(-1).to(f64) for y in ys]))
     host = torch.cat(parts).cpu().numpy() if parts else np.zeros(0)
     o = 0
-    if guards.ENABLED:
+    if guards.ENABLED and gdev is None:
         for f in range(len(Zs)):
             if host[f] == 0.0:
                 guards.check_finite(Zs[f], f"SVC.fit X (fit {f})")
@@ -1238,7 +1300,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
                 guards.check_binary(ys[f], f"SVC.fit y (fit {f})")
         o = 2 * len(Zs)
     var = None
-    if any(need_var):
+    if any(need_var) and gdev is None:
         var = host[o:o + len(Zs)]
         o += len(Zs)
     y_all = host[o:]
@@ -1246,7 +1308,9 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     all_probs, meta = [], []
     off = 0
     for f, (svc, Z) in enumerate(zip(svcs, Zs)):
-        if svc.gamma == "scale":
+        if gdev is not None:
+            gamma = 0.0          # (placeholder: the device records are patched, the host reads γ at finish)
+        elif svc.gamma == "scale":
             v = float(var[f])
             gamma = 1.0 / (Z.shape[1] * v) if v != 0 else 1.0
         else:
@@ -1265,8 +1329,12 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     hmark("svc_expand")
     eps = float(svcs[0].tol)
     args = (svcs, Zs, ys, max_iter_cap, group)
-    sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
-           else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
+    _GAMMA_CTX[0] = gdev
+    try:
+        sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
+               else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
+    finally:
+        _GAMMA_CTX[0] = None
     hmark("svc_solve_enqueued")
     solver = LAST_SMO_INFO.get("solver")   # this batch's solver (the global is overwritten by later batches)
     # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
@@ -1306,7 +1374,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
                       dscr.data_ptr(), ABt.data_ptr(), ops.stream_ptr(device))
         dmark("svc_platt")
         return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
-                    keep=(pdev, srcmap, cdev, dscr), device=device, args=args, solver=solver)
+                    keep=(pdev, srcmap, cdev, dscr), device=device, args=args, solver=solver, gamma_dev=gdev)
     for f in pl:
         svc, Z, mt = svcs[f], Zs[f], meta[f]
         l = mt["l"]
@@ -1363,6 +1431,8 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
     hcat = torch.cat([Zt.to(torch.float32) for _, Zt, _ in items]).contiguous()
     part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
     ddev = _dev_struct(dt, device)
+    if st.get("gamma_dev") is not None:
+        st["gamma_dev"].patch(ddev, _DEC_DT, "ngl2e", [f for f, _, _ in items])
     E.svm_dec_batch(dec_state["zcat"].data_ptr(), dec_state["coef"].data_ptr(), hcat.data_ptr(), dec_state["F"],
                     ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(), s)
     dec = part.to(torch.float64).sum(1).contiguous()
@@ -1399,6 +1469,9 @@ def finish_svc_batch(st: dict, defer=None):
         early["ev"].synchronize()
         host_e = early["host"].numpy()
         smo_failed = early["has_err"] and host_e[-1] != 0.0
+    if st.get("gamma_dev") is not None:
+        st["gamma_dev"].resolve(all_probs, meta)     # (the host's γ; raises on non-finite scaled rows)
+        st["gamma_dev"] = None
     else:
         err = sol.get("smo_err")
         smo_failed = err is not None and float(err.max()) != 0.0

@@ -56,6 +56,8 @@ SKIP_FOLD_SVC = os.environ.get("HFENS_SKIP_FOLD_SVC", "1") != "0"
 # their out-of-fold columns come from the device node tables / coefficients (ops/csrc/stackdev.hip),
 # and only the refit models are finished.  0 = the synchronous per-batch fits of round 4.
 DEVICE_BASES = os.environ.get("HFENS_DEVICE_BASES", "1") != "0"
+# the meta model's launch enqueued before the SVC's results are read back (0: after them)
+EARLY_META = os.environ.get("HFENS_EARLY_META", "1") != "0"
 
 
 def _kind(est):
@@ -203,7 +205,7 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
 
 
 def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
-                          svc_pre=None, oof_svc_dev=None, early=None, dev_bases=None):
+                          svc_pre=None, oof_svc_dev=None, early=None, dev_bases=None, prelaunched=None):
     """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
     Returns the fitted clone lists in estimator order, or None when not applicable."""
     kinds = [_kind(e) for _, e in clf.estimators]
@@ -231,8 +233,10 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     with timer.stage("fit_bases(svc || gbc+lr)"):
         # every collective is issued from this thread in the same order on every rank:
         # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
+        if prelaunched is not None:
+            pending.update(prelaunched)     # (enqueued under the LassoCV path: prelaunch_svc)
         with torch.cuda.stream(side):
-            for i in svc_cols:
+            for i in ([] if prelaunched is not None else svc_cols):
                 clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
                 hmark("svc_inputs")
                 if group is None:
@@ -267,6 +271,12 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                                 oof(i, out[i])
                         hmark(f"{name}_host_done")
                         dmark(f"{name}_done")
+                if dev_bases is not None:
+                    # the refit models' fitted state from the device node tables / coefficients,
+                    # enqueued on this stream behind their solves while the SMO runs (no host read:
+                    # the guards are read after it)
+                    for f in dev_bases["post"]:
+                        f()
         finally:
             logreg_solver.BLOCK_BUDGET[0] = lr_budget
         if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
@@ -295,11 +305,61 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         if dev_bases is not None:
             # the GBC / LR guards and error words: ONE read, long after their kernels finished
             dev_bases["deferred"].resolve()
-            for f in dev_bases["post"]:
-                f()
             hmark("bases_resolved")
     hmarks_flush()
     return [out[i] for i in range(len(kinds))]
+
+
+PRELAUNCH_SVC = os.environ.get("HFENS_PRELAUNCH_SVC", "1") != "0"
+LAST_PRELAUNCH = {"used": False}
+
+
+def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Tensor, plan: dict):
+    """Enqueue the stacking fit's SVC batch (scaler fits, the 36 SMO problems, Platt, the device
+    out-of-fold column) BEFORE the selected columns are known on the host: ``cols_dev`` is
+    SelectFromModel's device column list, ``X_full`` the imputed development rows.  Everything else
+    is label-only (``plan``: plan_stacking), γ is computed on the device (smo.launch_svc_batch
+    gamma_dev), so nothing here reads the device — pipeline.develop calls it while the LassoCV path
+    runs, and the SMO starts as soon as the path and the column selection finish.  Returns the state
+    :func:`fit_stacking` continues from (it checks the host's selection against ``cols_dev``), or
+    None when the stack is not eligible."""
+    kinds = [_kind(e) for _, e in clf.estimators]
+    svc_cols = [i for i, k in enumerate(kinds) if k == "svc"]
+    if not (PRELAUNCH_SVC and X_full.is_cuda and CONCURRENT_BASES and DEVICE_SVC_OOF and svc_cols
+            and len(kinds) > len(svc_cols) and plan.get("svc_pre") and all(i in plan["svc_pre"] for i in svc_cols)):
+        return None
+    from .. import runtime
+    from .smo import launch_svc_batch, enqueue_svc_oof
+    dev = X_full.device
+    n = int(X_full.shape[0])
+    y_np, folds_np, rows_host = plan["y_np"], plan["folds_np"], plan["rows_host"]
+    if int(y_np.shape[0]) != n:
+        return None
+    main = torch.cuda.current_stream(dev)
+    side = runtime.stream(dev, "svc", priority=-1)
+    side.wait_stream(main)
+    masks = fold_masks(folds_np, N_FOLDS, device=dev)
+    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+    meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
+    pending = {}
+    with torch.cuda.stream(side):
+        X = X_full.index_select(1, cols_dev)
+        for i in svc_cols:
+            clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, None, rows_host)
+            st = launch_svc_batch(svcs, Zs, ys, y_host=[y_np[r] for r in rows_host], plan=plan["svc_pre"][i],
+                                  gamma_dev=True)
+            items = [(k, clones[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
+                     for k in range(N_FOLDS) if test_idx[k].numel()]
+            st["oof_dev"] = bool(st.get("gamma_dev") is not None) and enqueue_svc_oof(st, items, meta, i)
+            pending[i] = (clones, st)
+    for t in (X_full, cols_dev, y):
+        t.record_stream(side)
+    if not all(st["oof_dev"] for _, st in pending.values()):
+        # (not the device-γ working-set path: the batch above is still valid, finished as usual)
+        pass
+    from ..utils.timing import hmark
+    hmark("svc_prelaunched")
+    return dict(cols_dev=cols_dev, X=X, masks=masks, test_idx=test_idx, meta=meta, pending=pending)
 
 
 def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
@@ -335,6 +395,7 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
                     st.feat.data_ptr(), st.thr.data_ptr(), st.value.data_ptr(), raw0.data_ptr(), so["lr"],
                     meta.data_ptr(), int(meta.shape[1]), col, ops.stream_ptr(dev))
         keep.append((st, raw0))
+        post.append(so["finish"])
         return clones
 
     def lr(col, est):
@@ -368,6 +429,7 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
                 logreg_solver.LAST_PATH["coop_fallback"] = True
                 logreg_solver._launch_single(fz)
                 column()
+                set_fitted_from(h, only={nb - 1})     # (its intercept is a copy, not a view of W)
                 if early is not None:
                     early["stale"] = True
             deferred.word(fz["err"], on_fail)
@@ -403,14 +465,27 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
     else:
         from ..parallel import dist as pdist
         folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
-    masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
     rows_host = (plan["rows_host"] if svc_pre is not None
                  else [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)])
-    # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
-    # gathers / scatters then need no host synchronisation
-    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+    pre = plan.get("prelaunch") if (plan is not None and svc_pre is not None) else None
+    if pre is not None:
+        # the SVC batch was enqueued from the device column selection (prelaunch_svc): it is this
+        # fit's only if the host's selection agrees (it always should: same rule, same numbers)
+        cols = plan.get("cols")
+        if cols is None or not np.array_equal(pre["cols_dev"].cpu().numpy(), np.asarray(cols, dtype=np.int64)):
+            import warnings
+            warnings.warn("device column selection differs from the host's; relaunching the SVC batch")
+            pre = None
+    LAST_PRELAUNCH["used"] = pre is not None
+    if pre is not None:
+        masks, test_idx, meta = pre["masks"], pre["test_idx"], pre["meta"]
+    else:
+        masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
+        # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
+        # gathers / scatters then need no host synchronisation
+        test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+        meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
     full = []
-    meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
 
     def oof(col, fitted):
         from ..utils.timing import hmark
@@ -435,13 +510,14 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
         return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
 
     early = None
-    if group is None:
+    if group is None and EARLY_META:
         early = {"launch": lambda: launch_logreg_batch([new_final()], meta, y64)}
     dev_bases = None
     if group is None and X.is_cuda and DEVICE_BASES:
         dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
     fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre,
-                                       oof_svc_dev if group is None else None, early, dev_bases)
+                                       oof_svc_dev if group is None else None, early, dev_bases,
+                                       pre["pending"] if pre is not None else None)
     for col, (name, est) in enumerate(clf.estimators):
         if fitted_all is not None:
             fitted = fitted_all[col]        # OOF column already filled on the fitting stream

@@ -5,6 +5,8 @@
 //                bounded draws from sklearn/svm/src/newrand/newrand.h), so the 5 internal folds
 //                match the reference fit exactly.  Native because it is an l-step sequential
 //                Fisher-Yates loop executed for every SVC fit.
+// Licence: the libsvm RNG draws and the splitter's rand_r order follow scikit-learn / LIBSVM
+// (BSD-3-Clause; notices in THIRD_PARTY_NOTICES.md at the repository root).
 #include <cstdint>
 #include <random>
 
@@ -181,8 +183,9 @@ void stack_predict_host(int n, int F, uintptr_t X_, uintptr_t mean_, uintptr_t s
 // could launch).  bits [n] u64 (bit f = column f missing); out: int64 buffer of capacity `cap`
 // filled as [rows (nr) | bits of those rows (nr) | slot columns (nr × nslot, −1 padded) | flat slot
 // index of every missing cell (nc) | its row (nc) | its column (nc)], cells row-major with columns
-// ascending (the numpy order); dims[0..2] = nr, nc, nslot (nslot = max missing per row rounded up
-// to `slots`).  dims[0] = −1 when `cap` is too small (nothing written past it).
+// ascending (the numpy order); dims[0..3] = nr, nc, nslot (nslot = max missing per row rounded up
+// to `slots`), status (0 = written; −1 = `cap` below 2·nr + nr·nslot + 3·nc: nothing written — a
+// call with cap = 0 sizes the buffer).
 void knn_plan_host(uintptr_t bits_, long long n, int F, int slots, uintptr_t out_, long long cap, uintptr_t dims_) {
   const uint64_t* bits = reinterpret_cast<const uint64_t*>(bits_);
   long long* out = reinterpret_cast<long long*>(out_);
@@ -202,8 +205,9 @@ void knn_plan_host(uintptr_t bits_, long long n, int F, int slots, uintptr_t out
   dims[0] = nr;
   dims[1] = nc;
   dims[2] = nslot;
+  dims[3] = 0;
   if (2 * nr + nr * nslot + 3 * nc > cap) {
-    dims[0] = -1;
+    dims[3] = -1;
     return;
   }
   long long* rows = out;

@@ -21,6 +21,33 @@
 //   * tolerance eps · max(min(#pos, #neg), 1) / l on the accumulated violation.
 // Every floating-point expression keeps liblinear's evaluation order and no contraction into fma
 // (scikit-learn's wheel is built for the x86-64 baseline, which has none).
+//
+// This file re-expresses liblinear's solve_l1r_lr (the copy vendored by scikit-learn as
+// sklearn/svm/src/liblinear/linear.cpp) closely enough to reproduce its iterate bit for bit, so it
+// carries liblinear's licence:
+//
+//   Copyright (c) 2007-2023 The LIBLINEAR Project.
+//   All rights reserved.
+//
+//   Redistribution and use in source and binary forms, with or without modification, are permitted
+//   provided that the following conditions are met:
+//   1. Redistributions of source code must retain the above copyright notice, this list of
+//      conditions and the following disclaimer.
+//   2. Redistributions in binary form must reproduce the above copyright notice, this list of
+//      conditions and the following disclaimer in the documentation and/or other materials
+//      provided with the distribution.
+//   3. Neither name of copyright holders nor the names of its contributors may be used to endorse
+//      or promote products derived from this software without specific prior written permission.
+//
+//   THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND CONTRIBUTORS ``AS IS'' AND ANY EXPRESS
+//   OR IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE IMPLIED WARRANTIES OF MERCHANTABILITY
+//   AND FITNESS FOR A PARTICULAR PURPOSE ARE DISCLAIMED.  IN NO EVENT SHALL THE REGENTS OR
+//   CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL, EXEMPLARY, OR
+//   CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO, PROCUREMENT OF SUBSTITUTE GOODS OR
+//   SERVICES; LOSS OF USE, DATA, OR PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED AND ON ANY
+//   THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING NEGLIGENCE OR
+//   OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS SOFTWARE, EVEN IF ADVISED OF THE
+//   POSSIBILITY OF SUCH DAMAGE.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>

@@ -16,7 +16,7 @@
 
 namespace hfens {
 
-constexpr int kRkThreads = 256;
+constexpr int kRkThreads = 1024;
 constexpr int kRkMaxF = 128;
 
 __device__ __forceinline__ unsigned sk_rand_r_dev(unsigned* s) {
@@ -27,26 +27,45 @@ __device__ __forceinline__ unsigned sk_rand_r_dev(unsigned* s) {
   return *s % (2147483647u + 1u);
 }
 
-// grid B (one workgroup per model), block 256.  bins [F][ldb] u8, w [B][n] (> 0: the model's row),
+// grid B (one workgroup per model), block 1024.  bins [F][ldb] u8, w [B][n] (> 0: the model's row),
 // seeds [B][T] (the trees' rand_r states), ranks out [T][B][F] (visit position, F for constants).
+// Constant features: wave v scans features v, v + 16, … over all rows (4 rows per lane and load
+// when the rows are 4-aligned), min / max occupied bin by DPP-free xor shuffles, no barrier per
+// feature; then thread t walks tree t's Fisher-Yates draw.
 __global__ __launch_bounds__(kRkThreads) void gbdt_ranks_dev_kernel(int T, int B, int F, int n,
                                                                     const unsigned char* __restrict__ bins,
                                                                     long long ldb, const float* __restrict__ w,
                                                                     const long long* __restrict__ seeds,
                                                                     int* __restrict__ ranks) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int kW = kRkThreads / 64;
   __shared__ unsigned char cst[kRkMaxF];
-  __shared__ int red[2][kRkThreads / 64];
-  __shared__ unsigned char feats[kRkThreads * kRkMaxF];   // one Fisher-Yates array per thread
+  __shared__ unsigned char feats[kRkThreads / 4 * kRkMaxF];   // Fisher-Yates arrays (threads < T ≤ 256 used)
   const float* wb = w + (size_t)b * n;
-  for (int f = 0; f < F; ++f) {
+  const bool vec = (n % 4) == 0 && (ldb % 4) == 0 && ((uintptr_t)bins % 4) == 0 && ((uintptr_t)w % 16) == 0;
+  for (int f = wave; f < F; f += kW) {
     const unsigned char* bf = bins + (size_t)f * ldb;
     int mn = 256, mx = -1;
-    for (int r = tid; r < n; r += kRkThreads) {
-      if (wb[r] > 0.f) {
-        const int v = bf[r];
-        mn = min(mn, v);
-        mx = max(mx, v);
+    if (vec) {
+#pragma unroll 4
+      for (int r = 4 * lane; r < n; r += 256) {
+        const unsigned bv = *reinterpret_cast<const unsigned*>(bf + r);
+        const float4 wv = *reinterpret_cast<const float4*>(wb + r);
+        const float ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int v = (int)((bv >> (8 * q)) & 0xFFu);
+          mn = ww[q] > 0.f ? min(mn, v) : mn;
+          mx = ww[q] > 0.f ? max(mx, v) : mx;
+        }
+      }
+    } else {
+      for (int r = lane; r < n; r += 64) {
+        if (wb[r] > 0.f) {
+          const int v = bf[r];
+          mn = min(mn, v);
+          mx = max(mx, v);
+        }
       }
     }
 #pragma unroll
@@ -54,17 +73,12 @@ __global__ __launch_bounds__(kRkThreads) void gbdt_ranks_dev_kernel(int T, int B
       mn = min(mn, __shfl_xor(mn, o, kWave));
       mx = max(mx, __shfl_xor(mx, o, kWave));
     }
-    if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
-    __syncthreads();
-    if (tid == 0) {
-      int a = red[0][0], c = red[1][0];
-      for (int k = 1; k < kRkThreads / 64; ++k) { a = min(a, red[0][k]); c = max(c, red[1][k]); }
-      cst[f] = (unsigned char)(c <= a);   // one occupied bin (or no rows): constant, never visited
-    }
-    __syncthreads();
+    if (lane == 0) cst[f] = (unsigned char)(mx <= mn);   // one occupied bin (or no rows): constant
   }
+  __syncthreads();
+  if (tid >= kRkThreads / 4) return;
   unsigned char* fs = feats + (size_t)tid * kRkMaxF;
-  for (int t = tid; t < T; t += kRkThreads) {
+  for (int t = tid; t < T; t += kRkThreads / 4) {
     unsigned st = (unsigned)seeds[(size_t)b * T + t];
     int* rk = ranks + ((size_t)t * B + b) * F;
     for (int f = 0; f < F; ++f) { fs[f] = (unsigned char)f; rk[f] = F; }
@@ -167,6 +181,79 @@ void oof_linear(uintptr_t X, int F, uintptr_t rows, uintptr_t model, long long m
   hipLaunchKernelGGL(oof_linear_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, as_stream(stream),
                      (const double*)X, F, (const long long*)rows, (const int*)model, m, (const double*)W, F1,
                      has_icpt, icpt_scale, (double*)meta, ld, col);
+  launch_check();
+}
+
+// ---- SVC γ on the device (gamma='scale' = 1 / (F · Var(Z)), sklearn svm/_base.py) ---------------
+// One workgroup per fit over its scaled rows Z [l_f][F] (f64, rows offs[f] … offs[f+1] of one
+// concatenated matrix): two passes (mean, then Σ(z − mean)²) in a fixed order (deterministic).
+// gamma[f] f64 (NaN when Z has a non-finite value: raised by the host where it reads γ), and
+// ngl2e[f] = f32(−γ·log2 e), the field the SVC kernels' problem records carry.  With this the
+// stacking trainer enqueues the whole SVC batch (problem records patched on the device, below)
+// before the selected columns are even known on the host.
+constexpr int kGmThreads = 1024;
+
+__device__ __forceinline__ double block_sum_gm(double v, double* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int w = 0; w < kGmThreads / 64; ++w) r += sh[w];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kGmThreads) void svm_gamma_kernel(const double* __restrict__ Z, const long long* __restrict__ offs,
+                                                               int F, double* __restrict__ gamma,
+                                                               float* __restrict__ ngl2e) {
+  __shared__ double sh[kGmThreads / 64];
+  const int f = blockIdx.x;
+  const long long b = offs[f] * F, e = offs[f + 1] * F;
+  const double cnt = (double)(e - b);
+  double s = 0.0;
+  bool fin = true;
+  for (long long i = b + threadIdx.x; i < e; i += kGmThreads) {
+    const double z = Z[i];
+    fin = fin && isfinite(z);
+    s += z;
+  }
+  const double tot = block_sum_gm(s, sh);
+  const double bad = block_sum_gm(fin ? 0.0 : 1.0, sh);
+  const double mean = cnt > 0 ? tot / cnt : 0.0;
+  double q = 0.0;
+  for (long long i = b + threadIdx.x; i < e; i += kGmThreads) {
+    const double d = Z[i] - mean;
+    q += d * d;
+  }
+  const double var = cnt > 0 ? block_sum_gm(q, sh) / cnt : 0.0;
+  if (threadIdx.x == 0) {
+    double g = var != 0.0 ? 1.0 / ((double)F * var) : 1.0;
+    if (bad != 0.0 || !isfinite(var)) g = __longlong_as_double(0x7ff8000000000000LL);   // NaN
+    gamma[f] = g;
+    ngl2e[f] = (float)(-g * 1.4426950408889634);
+  }
+}
+
+void svm_gamma(uintptr_t Z, uintptr_t offs, int K, int F, uintptr_t gamma, uintptr_t ngl2e, uintptr_t stream) {
+  HFENS_REQUIRE(K >= 1 && F >= 1, "svm_gamma: K, F >= 1");
+  hipLaunchKernelGGL(svm_gamma_kernel, dim3(K), dim3(kGmThreads), 0, as_stream(stream), (const double*)Z,
+                     (const long long*)offs, F, (double*)gamma, (float*)ngl2e);
+  launch_check();
+}
+
+// record i of an array of `count` structs (stride bytes): its f32 field at byte `off` ← src[fit_of[i]]
+__global__ void svm_patch_f32_kernel(unsigned char* __restrict__ base, int stride, int off, int count,
+                                     const int* __restrict__ fit_of, const float* __restrict__ src) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) *reinterpret_cast<float*>(base + (size_t)i * stride + off) = src[fit_of[i]];
+}
+
+void svm_patch_f32(uintptr_t base, int stride, int off, int count, uintptr_t fit_of, uintptr_t src, uintptr_t stream) {
+  HFENS_REQUIRE(stride > 0 && off >= 0 && off + 4 <= stride && (off % 4) == 0 && count >= 0, "svm_patch_f32: bad layout");
+  if (count == 0) return;
+  hipLaunchKernelGGL(svm_patch_f32_kernel, dim3((count + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (unsigned char*)base, stride, off, count, (const int*)fit_of, (const float*)src);
   launch_check();
 }
 

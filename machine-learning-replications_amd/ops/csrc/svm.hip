@@ -16,6 +16,8 @@
 //                   two contiguous Gram-row reads per iteration.  Ends with calculate_rho.
 //  platt_batch    : sigmoid_train (Lin-Lin-Weng 2007 Newton + backtracking), one 1024-thread
 //                   workgroup per SVC fit, decision values assembled from svm_dec_batch partials.
+// Licence: the pair rule, clipping, sigmoid_train and coupling follow LIBSVM (BSD-3-Clause, Chang & Lin;
+// notice in THIRD_PARTY_NOTICES.md at the repository root).
 #include "common.h"
 
 namespace hfens {

@@ -37,7 +37,8 @@ AUX_STREAM = os.environ.get("HFENS_AUX_STREAM", "1") != "0"   # held-out imputat
 PLAN_AHEAD = os.environ.get("HFENS_PLAN_AHEAD", "1") != "0"   # stacking bookkeeping under the LassoCV path
 # the GBC's bin map of every candidate column fitted on the host under the LassoCV path (the selected
 # columns' bins are then a slice: binning.BinMapper.select), from one non-blocking copy of the imputed rows
-BIN_AHEAD = os.environ.get("HFENS_BIN_AHEAD", "1") != "0"
+# (default off: the GBC's host bin fit runs while the device solves the SVC, off the critical path)
+BIN_AHEAD = os.environ.get("HFENS_BIN_AHEAD", "0") == "1"
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
@@ -50,7 +51,10 @@ def _bins_ahead(X_dev: torch.Tensor, clf):
         return None
     from . import runtime
     dev = X_dev.device
-    side = runtime.stream(dev, "bins_ahead")
+    # (the held-out imputation's side stream, ahead of that imputation: a stream of its own would
+    # shift HIP's stream → hardware-queue round robin for every stream created after it — measured:
+    # an extra stream here put the stacking trainer's streams on shared queues and cost the SMO 5 ms)
+    side = runtime.stream(dev, "aux")
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
         x32 = X_dev.to(torch.float32)
@@ -65,10 +69,10 @@ def _bins_ahead(X_dev: torch.Tensor, clf):
         if "bm" not in box:
             from .models.binning import fit_bins_host
             ev.synchronize()
-            # (the bin tables' uploads go on the idle side stream: on the current stream they would
-            # queue behind the LassoCV path)
+            # (the bin tables' uploads are non-blocking copies on the side stream: on the current
+            # stream they would queue behind the LassoCV path)
             with torch.cuda.stream(side):
-                box["bm"] = fit_bins_host(xh.numpy(), mb[0], dev)
+                box["bm"] = fit_bins_host(xh.numpy(), mb[0], dev, non_blocking=True)
             box["ev"] = torch.cuda.Event()
             box["ev"].record(side)
         return box["bm"], box["ev"]
@@ -164,6 +168,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             if dev.type == "cuda" and PLAN_AHEAD:
                 overlap = plan_ahead(y_dev)
     fit_group = None if task else group
+    sel = build_selector(cfg)
     with timer.stage("select"):
         jobs = []
         if run_sel is not None:
@@ -178,12 +183,21 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 plan_box["bins_all"] = bins_job()
                 hmark("bins_ahead")
             jobs.append(bins)
+        if group is None and dev.type == "cuda" and overlap is not None:
+            def svc_early():
+                # the stacking fit's SVC batch, enqueued from the selector's DEVICE column list
+                # while the LassoCV path runs (stack_trainer.prelaunch_svc)
+                cols = getattr(sel, "cols_dev_", None)
+                if cols is not None and plan_box.get("plan") is not None:
+                    from .models.stack_trainer import prelaunch_svc
+                    plan_box["prelaunch"] = prelaunch_svc(clf, X_dev, cols, y_dev, plan_box["plan"])
+            jobs.append(svc_early)
         lasso_overlap = None
         if jobs:
             def lasso_overlap():
                 for j in jobs:
                     j()
-        sfm = build_selector(cfg).fit(X_dev, y_dev, group=fit_group, overlap=lasso_overlap)
+        sfm = sel.fit(X_dev, y_dev, group=fit_group, overlap=lasso_overlap)
         if run_sel is not None:
             X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
         hmark("lasso_fit")
@@ -194,6 +208,8 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         fn_new = [n for n, m in zip(names, mask) if m]
         hmark("selected")
     plan = plan_box.get("plan")
+    if plan_box.get("prelaunch") is not None:
+        plan = dict(plan, prelaunch=plan_box["prelaunch"], cols=np.nonzero(mask)[0])
     if "bins_all" in plan_box:
         bm_all, bm_ev = plan_box["bins_all"]
         torch.cuda.current_stream(dev).wait_event(bm_ev)

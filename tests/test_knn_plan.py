@@ -31,10 +31,15 @@ def test_knn_plan_host_matches_numpy(n, F, p):
     nslot_max = -(-F // 8) * 8
     cap = 2 * n + n * nslot_max + 3 * n * F
     out = np.zeros(cap, dtype=np.int64)
-    dims = np.zeros(3, dtype=np.int64)
+    dims = np.zeros(4, dtype=np.int64)
     ops.ext().knn_plan_host(bits.ctypes.data, n, F, 8, out.ctypes.data, cap, dims.ctypes.data)
+    assert int(dims[3]) == 0
     rows, ref = _numpy_plan(bits, F, 8)
-    nr, nc, nslot = (int(v) for v in dims)
+    nr, nc, nslot = (int(v) for v in dims[:3])
+    # a counting call (cap 0) gives the same sizes and writes nothing
+    d0 = np.zeros(4, dtype=np.int64)
+    ops.ext().knn_plan_host(bits.ctypes.data, n, F, 8, 0, 0, d0.ctypes.data)
+    assert d0[:3].tolist() == dims[:3].tolist() and (int(d0[3]) == -1 or nr == 0)
     assert nr == rows.shape[0]
     if nr == 0:
         return

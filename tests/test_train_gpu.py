@@ -813,7 +813,7 @@ def test_stacking_device_bases_match_synchronous(dev, monkeypatch):
     out = {}
     for flag in (False, True):
         monkeypatch.setattr(stack_trainer, "DEVICE_BASES", flag)
-        monkeypatch.setattr(pipeline, "BIN_AHEAD", flag)
+        monkeypatch.setattr(pipeline, "BIN_AHEAD", flag)   # (on: exercised here, off by default)
         out[flag] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
     m0, m1 = out[False].model, out[True].model
     assert np.array_equal(out[False].selected, out[True].selected)
@@ -827,3 +827,27 @@ def test_stacking_device_bases_match_synchronous(dev, monkeypatch):
     assert float(d[:, 1].max()) <= 1e-6, float(d[:, 1].max())
     assert float(d[:, 2].max()) <= 1e-12, float(d[:, 2].max())
     assert float((out[False].proba_sel - out[True].proba_sel).abs().max()) <= 1e-5
+
+
+def test_prelaunched_svc_batch_matches(dev, monkeypatch):
+    """The SVC batch enqueued under the LassoCV path from the selector's DEVICE column list
+    (stack_trainer.prelaunch_svc: device γ patched into the problem records, no host read before
+    the SMO) fits the same stack as the batch launched after the host knows the selection: the same
+    columns, γ to the last bits of a variance sum (device two-pass vs torch's), and the same model
+    up to the f32 pair sequence that a last-bit γ change may alter."""
+    from hfens import pipeline
+    from hfens.models import stack_trainer
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(stack_trainer, "PRELAUNCH_SVC", flag)
+        out[flag] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+        assert stack_trainer.LAST_PRELAUNCH["used"] == flag
+    assert np.array_equal(out[False].selected, out[True].selected)
+    s0, s1 = out[False].model.estimators_[0].steps[1][1], out[True].model.estimators_[0].steps[1][1]
+    assert abs(float(s0._gamma) - float(s1._gamma)) <= 1e-14 * float(s0._gamma)
+    d = float((out[False].proba_sel - out[True].proba_sel).abs().max())
+    assert d <= 2e-3, d
+    assert abs(out[False].scores["auroc"] - out[True].scores["auroc"]) <= 2e-3
