@@ -20,6 +20,9 @@ SLOTS = 8
 # f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
 EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
 KNN_DEBUG = __import__("os").environ.get("HFENS_KNN_DEBUG", "0") == "1"
+# the receivers, their slots and operands planned by device kernels (knn.hip knn_plan_dev) instead
+# of from a host read of the missing-value bitmasks: the donor search launches with no host round trip
+DEVICE_PLAN = __import__("os").environ.get("HFENS_KNN_DEVICE_PLAN", "1") != "0"
 LAST_REFINE: list = []
 
 
@@ -49,7 +52,15 @@ class KNNImputer(Estimator):
         fx = torch.where(self._mask_fit, torch.zeros_like(X), X)
         cnt = (~self._mask_fit).sum(0).clamp(min=1)
         self._col_mean = fx.sum(0) / cnt
+        self._keep_host = None
         return self
+
+    def _keep(self):
+        """Indices of the columns with a fit value (host array; one small read per fit, at the first
+        transform — the output width must be known on the host)."""
+        if self._keep_host is None:
+            self._keep_host = np.nonzero(self._valid.cpu().numpy())[0].astype(np.int64)
+        return self._keep_host
 
     def fit_transform(self, X):
         return self.fit(X).transform(X)
@@ -67,6 +78,8 @@ class KNNImputer(Estimator):
         returns the finished list (those matrices only ever waited for this transform's inputs)."""
         Xs = [as_tensor(X, device=self._fit_X.device).clone() for X in Xs]
         if Xs and Xs[0].is_cuda and self.n_neighbors == 1:
+            if DEVICE_PLAN and EXACT and Xs[0].shape[1] <= 64:
+                return self._impute_planned_many(Xs, streams, defer)
             return self._impute_device_many(Xs, streams, defer)
         if defer:
             done = self.transform_many(Xs)
@@ -98,6 +111,93 @@ class KNNImputer(Estimator):
     def _fit_prep64(self):
         self._fit_prep()
         return self._prep[3], self._prep[4]
+
+    def _impute_planned_many(self, Xs, streams, defer=False):
+        """:meth:`_impute_device_many` with the planning on the device (:meth:`_impute_planned`):
+        nothing is read back but the fit's valid-column list (once per fit)."""
+        from .smo import _to_dev
+        from ..utils.timing import hmark
+        dev = Xs[0].device
+        F = Xs[0].shape[1]
+        keep_h = self._keep()
+        keep = None if keep_h.shape[0] == F else _to_dev(keep_h, dev)
+        D32, dm = self._fit_prep()
+        D64, dmax = self._fit_prep64()
+        main = torch.cuda.current_stream(dev)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        out, jobs = [], []
+        for i, X in enumerate(Xs):
+            st = streams[i] if streams is not None and streams[i] is not None else None
+            if st is None:
+                self._impute_planned(X, D32, dm, D64, dmax)
+                out.append(X if keep is None else X.index_select(1, keep))
+                hmark("imp_main_enqueued")
+            else:
+                def job(i=i, X=X, st=st):
+                    st.wait_event(ready)
+                    for t in (X, D32, dm, D64, dmax, self._fit_X, self._col_mean) + ((keep,) if keep is not None else ()):
+                        t.record_stream(st)
+                    with torch.cuda.device(dev), torch.cuda.stream(st):
+                        self._impute_planned(X, D32, dm, D64, dmax)
+                        out[i] = X if keep is None else X.index_select(1, keep)
+                out.append(None)
+                jobs.append(job)
+        if not defer:
+            for job in jobs:
+                job()
+            return out
+        state = {"done": False}
+
+        def run():
+            if not state["done"]:
+                for job in jobs:
+                    job()
+                state["done"] = True
+            return out
+        return out, run
+
+    def _impute_planned(self, X, D32, dm, D64, dmax):
+        """One matrix, every step on the device: knn_plan_dev (receivers in row order, their slot
+        columns in groups of 8, centred f32 / raw f64 operands, the refine's error scale, counts),
+        the f32 donor search + f64 refine per slot group (kernels read the counts; groups past the
+        widest row exit at once), then knn_apply writes the donors' values in place."""
+        from .. import ops
+        E = ops.ext()
+        n, F = X.shape
+        if n == 0:
+            return
+        dev = X.device
+        s = ops.stream_ptr(dev)
+        G = -(-F // SLOTS)
+        Xc = X if X.is_contiguous() else X.contiguous()
+        i64, i32 = torch.int64, torch.int32
+        rows = torch.empty(n, dtype=i64, device=dev)
+        rbits = torch.empty(n, dtype=i64, device=dev)
+        slot = torch.empty(G, n, SLOTS, dtype=i32, device=dev)
+        R32 = torch.empty(n, F, dtype=torch.float32, device=dev)
+        R64 = torch.empty(n, F, dtype=torch.float64, device=dev)
+        small = torch.empty(F + 1 + 4 + (n + 255) // 256, dtype=i32, device=dev)   # colmax | Mx | cnt | block counts
+        colmax, Mx, cnt, bcnt = small[:F], small[F:F + 1], small[F + 1:F + 5], small[F + 5:]
+        E.knn_plan_dev(Xc.data_ptr(), n, F, self._col_mean.data_ptr(), dmax.data_ptr(), rows.data_ptr(),
+                       rbits.data_ptr(), slot.data_ptr(), G, R32.data_ptr(), R64.data_ptr(), colmax.data_ptr(),
+                       Mx.data_ptr(), cnt.data_ptr(), bcnt.data_ptr(), s)
+        best = torch.empty(G, n, SLOTS, dtype=i64, device=dev)
+        alt = torch.empty(n, SLOTS, dtype=i32, device=dev)
+        cap = max(1 << 18, 16 * n)
+        work = torch.empty(4 * cap + n * SLOTS * 8 + 2 * n + 12, dtype=i32, device=dev)
+        nd = D32.shape[0]
+        for g in range(G):
+            E.knn_donors(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
+                         slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), cnt.data_ptr(), g * SLOTS, s)
+            E.knn_refine(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
+                         slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
+                         Mx.data_ptr(), work.data_ptr(), cap, cnt.data_ptr(), g * SLOTS, s)
+        fx = self._fit_X if self._fit_X.is_contiguous() else self._fit_X.contiguous()
+        E.knn_apply(Xc.data_ptr(), n, F, rows.data_ptr(), slot.data_ptr(), best.data_ptr(), fx.data_ptr(),
+                    self._col_mean.data_ptr(), cnt.data_ptr(), s)
+        if Xc is not X:
+            X.copy_(Xc)
 
     def _impute_device_many(self, Xs, streams, defer=False):
         """The (row, column) work lists are built with numpy from the bitmasks and uploaded
@@ -205,13 +305,13 @@ class KNNImputer(Estimator):
             slot = slot_dev[:, s0:s0 + SLOTS].contiguous()
             blk = best[:, s0:s0 + SLOTS] if nslot == SLOTS else torch.empty(slot.shape, dtype=torch.int64, device=dev)
             E.knn_donors(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(),
-                         D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), ops.stream_ptr(dev))
+                         D32.shape[0], F, slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), 0, 0, ops.stream_ptr(dev))
             if EXACT:
                 # slots whose runner-up is within the f32 error of the best: re-decided in f64
                 # (knn.hip knn_refine) — the donors then equal the host mirror's f64 choice
                 E.knn_refine(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(), D32.shape[0], F,
                              slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
-                             Mx.data_ptr(), work.data_ptr(), cap, ops.stream_ptr(dev))
+                             Mx.data_ptr(), work.data_ptr(), cap, 0, 0, ops.stream_ptr(dev))
                 if KNN_DEBUG:   # re-scanned receivers, window pairs, overflow, pass-1 receivers (synchronising)
                     o = 4 * cap + 8 * nr * SLOTS + 2 * nr
                     LAST_REFINE.append((nr, int(work[o]), int(work[o + 8]), int(work[o + 9]), int(work[o + 4]),

@@ -280,11 +280,15 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
         finally:
             logreg_solver.BLOCK_BUDGET[0] = lr_budget
         if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
-            # every meta-feature column is enqueued on the device: the meta model's launch goes
-            # in now, on the main stream behind them, before the SVC's results are read back
-            main.wait_stream(side)
-            main.wait_stream(other)
-            early["handle"] = early["launch"]()
+            # every meta-feature column is enqueued on the device: the meta model's launch goes in
+            # now, before the SVC's results are read back — on the SVC stream, behind the SVC's own
+            # out-of-fold kernel.  (On the main stream its wait for the SVC would be the head of an
+            # otherwise idle hardware queue for the rest of the SMO: measured, such a pending
+            # cross-stream wait slowed the SMO's dispatches by 2-4 ms, profiles/r5_headline.md.)
+            side.wait_stream(main)
+            side.wait_stream(other)
+            with torch.cuda.stream(side):
+                early["handle"] = early["launch"]()
         with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
                 if group is None:
@@ -337,10 +341,10 @@ def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Te
         return None
     main = torch.cuda.current_stream(dev)
     side = runtime.stream(dev, "svc", priority=-1)
-    side.wait_stream(main)
     masks = fold_masks(folds_np, N_FOLDS, device=dev)
     test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
+    side.wait_stream(main)     # (after the tensors above: the SVC stream writes meta's column)
     pending = {}
     with torch.cuda.stream(side):
         X = X_full.index_select(1, cols_dev)

@@ -46,7 +46,12 @@ __global__ __launch_bounds__(256) void knn_donor_kernel(
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
     int per_split, const int* __restrict__ slot_col /*[nr][kKnnSlots] column or −1*/,
     unsigned long long* __restrict__ best /*[nr][kKnnSlots] packed (dist bits, idx)*/,
-    unsigned* __restrict__ alt /*[nr][kKnnSlots] f32 bits of the runner-up distance*/) {
+    unsigned* __restrict__ alt /*[nr][kKnnSlots] f32 bits of the runner-up distance*/,
+    const int* __restrict__ cnt /*device plan: [nr, nslot] or null*/, int s0) {
+  if (cnt != nullptr) {   // planned on the device (knn_plan_dev): receiver count and slot groups there
+    if (s0 >= cnt[1]) return;
+    nr = cnt[0];
+  }
   constexpr int LD = (FMAX + 3) / 4 * 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ds = sm;                                                        // [256][LD] donor tile
@@ -181,7 +186,11 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ D, const unsigned long long* __restrict__ dmask, int nd, int F,
     int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best,
-    unsigned* __restrict__ alt) {
+    unsigned* __restrict__ alt, const int* __restrict__ cnt, int s0) {
+  if (cnt != nullptr) {
+    if (s0 >= cnt[1]) return;
+    nr = cnt[0];
+  }
   constexpr int LD = (FMAX + 3) / 4 * 4;
   constexpr bool XS = knn_fast_xs<FMAX>();
   constexpr int TILE = knn_fast_tile<FMAX>();
@@ -375,8 +384,10 @@ __global__ __launch_bounds__(256) void knn_donor_fast_kernel(
   if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
 }
 
+// cnt (optional, device [nr, nslot] of knn_plan_dev): nr is then the capacity (grid, buffers) and the
+// kernels take the receiver count from the device; slot group s0 ≥ nslot exits at once.
 void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
-                uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t stream) {
+                uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t cnt, int s0, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_donors: 1 <= F <= 64 (64-bit missing masks)");
   if (nr == 0 || nd == 0) return;
   hipStream_t st = as_stream(stream);
@@ -410,17 +421,17 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
       hipLaunchKernelGGL(knn_donor_kernel<FM>, dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best, (unsigned*)alt);
+                         (unsigned long long*)best, (unsigned*)alt, (const int*)cnt, s0);
     else if (F == LD && !lds_tiles && (D & 15) == 0)
       hipLaunchKernelGGL((knn_donor_fast_kernel<FM, true>), dim3(rb, nsp), dim3(256), knn_fast_lds_sm<FM>(), st,
                          (const float*)R, (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best, (unsigned*)alt);
+                         (unsigned long long*)best, (unsigned*)alt, (const int*)cnt, s0);
     else
       hipLaunchKernelGGL((knn_donor_fast_kernel<FM, false>), dim3(rb, nsp), dim3(256), lds, st, (const float*)R,
                          (const unsigned long long*)rmask, nr, (const float*)D,
                          (const unsigned long long*)dmask, nd, F, per, (const int*)slot_col,
-                         (unsigned long long*)best, (unsigned*)alt);
+                         (unsigned long long*)best, (unsigned*)alt, (const int*)cnt, s0);
     launch_check();
   };
   if (F <= 16) go(std::integral_constant<int, 16>{});
@@ -468,7 +479,12 @@ __global__ __launch_bounds__(256) void knn_ambig_kernel(const unsigned long long
                                                         const unsigned long long* __restrict__ rmask,
                                                         const double* __restrict__ D64,
                                                         const unsigned long long* __restrict__ dmask,
-                                                        unsigned long long* __restrict__ dwin) {
+                                                        unsigned long long* __restrict__ dwin,
+                                                        const int* __restrict__ cnt, int s0) {
+  if (cnt != nullptr) {
+    if (s0 >= cnt[1]) return;
+    nr = cnt[0];
+  }
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= nr) return;
   const float mn = Mx[0], Ff = (float)F;   // ‖m‖: norm over columns of the largest centred magnitude
@@ -701,7 +717,7 @@ __global__ __launch_bounds__(256) void knn_commit_kernel(const int* __restrict__
 // work: 8-byte aligned scratch of knn_refine_work_words(nr) int32 words
 void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
                 uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t R64, uintptr_t D64, uintptr_t Mx,
-                uintptr_t work, long long cap, uintptr_t stream) {
+                uintptr_t work, long long cap, uintptr_t cnt, int s0, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_refine: 1 <= F <= 64");
   HFENS_REQUIRE((work & 7) == 0 && cap >= 1, "knn_refine: work must be 8-byte aligned, cap >= 1");
   if (nr == 0 || nd == 0) return;
@@ -727,7 +743,7 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   hipLaunchKernelGGL(knn_ambig_kernel, dim3(rb), dim3(256), 0, st, (const unsigned long long*)best,
                      (const unsigned*)alt, (const int*)slot_col, nr, F, (const float*)Mx, thr, dmin, didx, rlist,
                      counts, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
-                     (const unsigned long long*)dmask, dwin);
+                     (const unsigned long long*)dmask, dwin, (const int*)cnt, s0);
   launch_check();
   // donor splits as in knn_donors (≥ 2048 workgroups, ≤ 16k donors each); blocks past the device
   // receiver count exit at once
@@ -778,6 +794,170 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(knn_commit_kernel, dim3(grid), dim3(256), 0, st, rlist, counts, thr, thr2, didx, didx2,
                      (unsigned long long*)best);
+  launch_check();
+}
+
+// ---- device planning of an imputation (no host read of the missing-value pattern) ----------------
+// knn_plan_dev: rows of X [n][F] (f64, NaN = missing) with a missing feature, in row order (a
+// per-256-row-block count, one scan block, then the writes): rows [n] i64, rbits [n] u64,
+// slot [G][n][8] i32 (group g: the row's missing columns 8g … 8g+7 in column order, −1 padded),
+// R32 [n][F] f32 (x − centre, 0 where missing), R64 [n][F] f64 (x, 0 where missing),
+// colmax [F] f32 bits (max |R32| per column, atomicMax on the non-negative float bits),
+// cnt [4] i32 = {nr, nslot (max missing per row rounded up to 8), nc, 0}.  Work: bcnt [nb] i32.
+__global__ __launch_bounds__(256) void knn_plan_count_kernel(const double* __restrict__ X, long long n, int F,
+                                                             int* __restrict__ bcnt, int* __restrict__ cnt) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  int m = 0;
+  if (r < n)
+    for (int f = 0; f < F; ++f) m += isnan(X[r * F + f]) ? 1 : 0;
+  const unsigned long long b = __ballot(m > 0);
+  int mx = m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, kWave));
+  __shared__ int wc[4], wm[4], wn[4];
+  int nc = m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, kWave);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { wc[wave] = __popcll(b); wm[wave] = mx; wn[wave] = nc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+    atomicMax(&cnt[1], max(max(wm[0], wm[1]), max(wm[2], wm[3])));
+    atomicAdd(&cnt[2], wn[0] + wn[1] + wn[2] + wn[3]);
+  }
+}
+
+// one workgroup: exclusive scan of the block counts in place, nr, nslot rounded up to 8
+__global__ __launch_bounds__(1024) void knn_plan_scan_kernel(int* __restrict__ bcnt, int nb, int* __restrict__ cnt) {
+  __shared__ int part[1024];
+  const int per = (nb + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  int s = 0;
+  for (int i = 0; i < per; ++i) s += (b0 + i < nb) ? bcnt[b0 + i] : 0;
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = part[threadIdx.x] - s;   // exclusive
+  for (int i = 0; i < per; ++i) {
+    if (b0 + i < nb) {
+      const int c = bcnt[b0 + i];
+      bcnt[b0 + i] = run;
+      run += c;
+    }
+  }
+  if (threadIdx.x == 1023) {
+    cnt[0] = part[1023];
+    cnt[1] = (cnt[1] + kKnnSlots - 1) / kKnnSlots * kKnnSlots;
+  }
+}
+
+__global__ __launch_bounds__(256) void knn_plan_fill_kernel(const double* __restrict__ X, long long n, int F,
+                                                            const double* __restrict__ centre,
+                                                            const int* __restrict__ boff, int G,
+                                                            long long* __restrict__ rows,
+                                                            unsigned long long* __restrict__ rbits,
+                                                            int* __restrict__ slot, float* __restrict__ R32,
+                                                            double* __restrict__ R64, unsigned* __restrict__ colmax) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long bits = 0ull;
+  if (r < n)
+    for (int f = 0; f < F; ++f) bits |= (isnan(X[r * F + f]) ? 1ull : 0ull) << f;
+  const unsigned long long b = __ballot(bits != 0ull);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ int wc[4];
+  if (lane == 0) wc[wave] = __popcll(b);
+  __syncthreads();
+  if (bits == 0ull) return;
+  int k = boff[blockIdx.x] + __popcll(b & ((1ull << lane) - 1ull));
+  for (int w = 0; w < wave; ++w) k += wc[w];
+  rows[k] = r;
+  rbits[k] = bits;
+  int s = 0;
+  for (int f = 0; f < F; ++f) {
+    const double x = X[r * F + f];
+    const bool miss = (bits >> f) & 1ull;
+    const float z = miss ? 0.f : (float)(x - centre[f]);
+    R32[(size_t)k * F + f] = z;
+    R64[(size_t)k * F + f] = miss ? 0.0 : x;
+    if (!miss) atomicMax(&colmax[f], __float_as_uint(fabsf(z)));
+    if (miss) {
+      slot[((size_t)(s / kKnnSlots) * n + k) * kKnnSlots + s % kKnnSlots] = f;
+      ++s;
+    }
+  }
+  for (; s < G * kKnnSlots; ++s) slot[((size_t)(s / kKnnSlots) * n + k) * kKnnSlots + s % kKnnSlots] = -1;
+}
+
+// Mx[0] = ‖max(dmax, colmax)‖₂ (f64 sum of squares in column order, then f32): the refine's
+// error-window scale (knn_ambig)
+__global__ void knn_plan_mx_kernel(const float* __restrict__ dmax, const unsigned* __restrict__ colmax, int F,
+                                   float* __restrict__ Mx) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int f = 0; f < F; ++f) {
+    const double v = (double)fmaxf(dmax[f], __uint_as_float(colmax[f]));
+    s += v * v;
+  }
+  Mx[0] = (float)sqrt(s);
+}
+
+void knn_plan_dev(uintptr_t X, long long n, int F, uintptr_t centre, uintptr_t dmax, uintptr_t rows, uintptr_t rbits,
+                  uintptr_t slot, int G, uintptr_t R32, uintptr_t R64, uintptr_t colmax, uintptr_t Mx, uintptr_t cnt,
+                  uintptr_t bcnt, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64 && G * kKnnSlots >= F && n >= 1, "knn_plan_dev: 1 <= F <= 64, G·8 >= F");
+  hipStream_t st = as_stream(stream);
+  const long long nb = (n + 255) / 256;
+  HFENS_REQUIRE(nb <= (1LL << 30), "knn_plan_dev: too many rows");
+  HFENS_CHECK(hipMemsetAsync((void*)cnt, 0, 4 * sizeof(int), st));
+  HFENS_CHECK(hipMemsetAsync((void*)colmax, 0, (size_t)F * sizeof(unsigned), st));
+  hipLaunchKernelGGL(knn_plan_count_kernel, dim3((unsigned)nb), dim3(256), 0, st, (const double*)X, n, F,
+                     (int*)bcnt, (int*)cnt);
+  hipLaunchKernelGGL(knn_plan_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)bcnt, (int)nb, (int*)cnt);
+  hipLaunchKernelGGL(knn_plan_fill_kernel, dim3((unsigned)nb), dim3(256), 0, st, (const double*)X, n, F,
+                     (const double*)centre, (const int*)bcnt, G, (long long*)rows, (unsigned long long*)rbits,
+                     (int*)slot, (float*)R32, (double*)R64, (unsigned*)colmax);
+  hipLaunchKernelGGL(knn_plan_mx_kernel, dim3(1), dim3(64), 0, st, (const float*)dmax, (const unsigned*)colmax, F,
+                     (float*)Mx);
+  launch_check();
+}
+
+// X[rows[k], c] ← the donor's value (fitX [nd][F], NaN-free where the donor has c) or the column
+// mean when no donor has a defined distance; best [G][n][8] packed (d² bits, donor), all-ones = none
+__global__ __launch_bounds__(256) void knn_apply_kernel(double* __restrict__ X, long long n, int F,
+                                                        const long long* __restrict__ rows,
+                                                        const int* __restrict__ slot,
+                                                        const unsigned long long* __restrict__ best,
+                                                        const double* __restrict__ fitX,
+                                                        const double* __restrict__ colmean,
+                                                        const int* __restrict__ cnt) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= cnt[0]) return;
+  const long long r = rows[k];
+  const int G = cnt[1] / kKnnSlots;
+  for (int g = 0; g < G; ++g) {
+    for (int j = 0; j < kKnnSlots; ++j) {
+      const size_t e = ((size_t)g * n + k) * kKnnSlots + j;
+      const int c = slot[e];
+      if (c < 0) continue;
+      const unsigned long long b = best[e];
+      const long long d = b == ~0ull ? -1 : (long long)(b & 0xFFFFFFFFull);
+      X[r * F + c] = d >= 0 ? fitX[d * F + c] : colmean[c];
+    }
+  }
+}
+
+void knn_apply(uintptr_t X, long long n, int F, uintptr_t rows, uintptr_t slot, uintptr_t best, uintptr_t fitX,
+               uintptr_t colmean, uintptr_t cnt, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64 && n >= 1, "knn_apply: bad shape");
+  hipLaunchKernelGGL(knn_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), (double*)X,
+                     n, F, (const long long*)rows, (const int*)slot, (const unsigned long long*)best,
+                     (const double*)fitX, (const double*)colmean, (const int*)cnt);
   launch_check();
 }
 

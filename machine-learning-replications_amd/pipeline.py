@@ -39,6 +39,7 @@ PLAN_AHEAD = os.environ.get("HFENS_PLAN_AHEAD", "1") != "0"   # stacking bookkee
 # columns' bins are then a slice: binning.BinMapper.select), from one non-blocking copy of the imputed rows
 # (default off: the GBC's host bin fit runs while the device solves the SVC, off the critical path)
 BIN_AHEAD = os.environ.get("HFENS_BIN_AHEAD", "0") == "1"
+INIT_STREAMS = os.environ.get("HFENS_INIT_STREAMS", "1") != "0"   # runtime.init_fit_streams
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
@@ -110,6 +111,9 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                             dtype=torch.float64).to(dev)
     y_sel = torch.as_tensor(np.asarray(y_sel) if not isinstance(y_sel, torch.Tensor) else y_sel,
                             dtype=torch.float64).to(dev)
+    if dev.type == "cuda" and INIT_STREAMS:
+        from . import runtime
+        runtime.init_fit_streams(dev)
     task = False
     if group is not None:
         from .parallel import dist as pdist

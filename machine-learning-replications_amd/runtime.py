@@ -35,6 +35,23 @@ def stream(device, role: str, priority: int = 0) -> "torch.cuda.Stream":
     return s
 
 
+# The development fit's streams in ONE creation order.  HIP multiplexes streams onto a few hardware
+# queues per priority level as they are created (GPU_MAX_HW_QUEUES), so which streams share a
+# queue — i.e. which kernels serialise behind each other — depends on the order of first use.
+# Measured (profiles/r5_headline.md): enqueuing the SVC batch earlier changed that order and cost
+# the SMO 3-5 ms; creating every role here first keeps the measured-good assignment whatever the
+# code path.
+FIT_STREAMS = (("aux", 0), ("lasso_refit", 0), ("svc", -1), ("bases", 0), ("svc_ws_0", -1), ("svc_ws_1", -1))
+
+
+def init_fit_streams(device) -> None:
+    d = torch.device(device)
+    if d.type != "cuda" or (d, FIT_STREAMS[-1][0]) in _STREAMS:
+        return
+    for role, prio in FIT_STREAMS:
+        stream(d, role, priority=prio)
+
+
 def workspace(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
     """A ``numel``-element view of a process-lifetime buffer (grown, never shrunk).
 

@@ -333,6 +333,51 @@ def _stack_dp_lowrank(rank, world, group):
     return _stack_dp(rank, world, group, lowrank=True)
 
 
+def _svc_broadcast(rank, world, group):
+    """broadcast_svc_fits alone: every rank fits the same 6 SVCs, then each fit is replaced by its
+    owner's through the packed broadcast; returns every fit's state and the collective count."""
+    from hfens.models.smo import fit_svc_batch
+    from hfens.models.svc import SVC
+    from hfens.parallel import stack
+    X, y, _ = _data(300, 8, seed=21)
+    Z = (X - X.mean(0)) / X.std(0, unbiased=False)
+    Zs = [Z[30 * k:] for k in range(6)]
+    ys = [y[30 * k:] for k in range(6)]
+    svcs = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+    fit_svc_batch(svcs, Zs, ys)
+    # scramble the non-owned fits so that only the broadcast can restore them
+    for f, s in enumerate(svcs):
+        if f % world != rank:
+            s._dual_coef_ = s._dual_coef_ * 0.0 + 7.0
+            s._gamma = -1.0
+    stack.broadcast_svc_fits(svcs, Zs, group)
+    return ([(s.support_.clone(), s.support_vectors_.clone(), s._dual_coef_.clone(), float(s._intercept_[0]),
+              float(s._probA[0]), float(s._probB[0]), s._gamma, s.shape_fit_, s._n_support.clone())
+             for s in svcs], stack.COLLECTIVES["broadcast_svc_fits"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_broadcast_svc_fits_packed(world):
+    """the task-parallel SVC fits travel in TWO collectives for all six fits
+    (shape table + one packed f64 SUM), bit-exact: every rank ends with the owner's arrays."""
+    got, ncoll = _run("_svc_broadcast", world)
+    from hfens.models.smo import fit_svc_batch
+    from hfens.models.svc import SVC
+    X, y, _ = _data(300, 8, seed=21)
+    Z = (X - X.mean(0)) / X.std(0, unbiased=False)
+    Zs = [Z[30 * k:] for k in range(6)]
+    ys = [y[30 * k:] for k in range(6)]
+    ref = [SVC(class_weight="balanced", probability=True, random_state=2020) for _ in Zs]
+    fit_svc_batch(ref, Zs, ys)
+    assert ncoll == 2
+    for g, s in zip(got, ref):
+        sup, sv, coef, ic, pa, pb, gam, shp, ns = g
+        assert torch.equal(sup.to(torch.int32), s.support_) and torch.equal(sv, s.support_vectors_)
+        assert torch.equal(coef, s._dual_coef_) and ic == float(s._intercept_[0])
+        assert pa == float(s._probA[0]) and pb == float(s._probB[0]) and gam == s._gamma
+        assert tuple(shp) == tuple(s.shape_fit_) and torch.equal(ns.to(torch.int32), s._n_support.to(torch.int32))
+
+
 def _stack_single(lowrank=False):
     from hfens.models import smo
     from hfens.config import EnsembleConfig, build_estimators

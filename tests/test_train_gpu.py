@@ -517,6 +517,10 @@ def test_develop_plan_ahead_identical(dev, monkeypatch):
     Platt column maps: pipeline.PLAN_AHEAD) gives the same fit as computing it in line."""
     from hfens import pipeline
     from hfens.io.synth import make_hf_cohort
+    from hfens.models import stack_trainer
+    # (the SVC batch launched from the host selection in both: the prelaunched batch computes γ on
+    # the device, last-bit different — test_prelaunched_svc_batch_matches)
+    monkeypatch.setattr(stack_trainer, "PRELAUNCH_SVC", False)
     Xd, yd, names = make_hf_cohort(3000, 40, seed=77, nan_frac=0.02)
     Xs, ys, _ = make_hf_cohort(1000, 40, seed=78, nan_frac=0.02)
     args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
