@@ -710,7 +710,10 @@ def _run_stage(st: _State, group):
             # ONE exact int64 SUM per stage (SURVEY.md §5.8 R1/R2 merged)
             k = host_t % 3
             if peer is not None:
-                peer.allreduce_(comm[k * slot:(k + 1) * slot], k, t, t_dev, epoch_base=base, stream=s)
+                # peer slot = epoch mod 3 (epoch = base + t + 1): the rotation every user of the
+                # PeerComm follows, so consecutive epochs never share a slot across fits
+                peer.allreduce_(comm[k * slot:(k + 1) * slot], (base + host_t + 1) % 3, t, t_dev,
+                                epoch_base=base, stream=s)
                 n_xg[0] += 1
             else:
                 import torch.distributed as dist

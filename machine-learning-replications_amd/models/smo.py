@@ -686,12 +686,15 @@ def _ws_groups(live, device) -> List[List[int]]:
     return [sorted(g) for g in groups]
 
 
-def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None):
+def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None,
+              seed=None, q=None):
+    """``seed``: a feasible α (per point, this batch's layout) to start from instead of α = 0
+    (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`)."""
     P = len(live)
     n = aoffs[-1]
     ml = max(p.l for p in live)
     kc_all = ws_kc(F, ml)          # one solver kind for the whole batch (every group)
-    Q = ws_q(F, ml)
+    Q = ws_q(F, ml) if (q is None or kc_all) else int(q)
     Fp2 = 2 * _ws_ks(F)
     max_outer = (max(5_000, max(p.l for p in live) // 4) if max_iter_cap is None else int(max_iter_cap))
     max_inner = WS_MAX_INNER
@@ -742,7 +745,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         runs.append(_ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, st,
                               side, zn, alpha, G, keys, hist, n, Q, Fp2, kc_all, gi=gi if use_graph else None,
                               cap_stream=(side if side is not None else caller) if use_graph else None,
-                              frac=WS_INNER_FRAC_BIG if (gi == 0 and len(groups) > 1) else WS_INNER_FRAC))
+                              frac=WS_INNER_FRAC_BIG if (gi == 0 and len(groups) > 1) else WS_INNER_FRAC,
+                              seed=seed))
     from ..utils.timing import hmark
     hmark("ws_groups_ready")
     # HFENS_WS_EVENTS=1 (diagnostic): device events per group after every enqueued chunk, read by
@@ -820,7 +824,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
 
 
 def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_inner, s, side,
-              zn, alpha, G, keys, hist, n, Q, Fp2, kc=False, gi=None, cap_stream=None, frac=None):
+              zn, alpha, G, keys, hist, n, Q, Fp2, kc=False, gi=None, cap_stream=None, frac=None, seed=None):
     """State of the problems ``live[idx]``, whose rounds go on stream ``s`` (per-problem state is
     group-local; the per-point arrays are the shared ones, addressed by each problem's absolute
     offset).  Returns closures: ``steps(k)`` enqueues k rounds, ``sync_rounds(chunk)`` runs
@@ -873,6 +877,10 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
         gap = torch.empty(P, dtype=torch.float64, device=device)
         E.ws_init(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
                   states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
+        if seed is not None:
+            E.ws_seed(pdev.data_ptr(), P, max_l, zcat.data_ptr(), F, zn.data_ptr(), seed.data_ptr(),
+                      alpha.data_ptr(), G.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), s)
+            out["seed"] = seed
         out["idx_dev"] = _to_dev(out["idx"], device)
     done_view = states.view(P, _WS_STATE_BYTES // 4)[:, 0]
 
@@ -1014,6 +1022,57 @@ def _solve_distributed(solve_local, live, n_alpha, aoffs, device, group):
             flat[n_alpha + 2 * P:])
 
 
+# Cascade seed (the critical problem's pair count).  Every working-set problem of
+# ≥ CASCADE_MIN points is split into disjoint class-stratified parts of ≈ CASCADE_PART points, each
+# solved as an SVC with the SAME per-class C to the loose tolerance CASCADE_EPS (q = 512: half the
+# slots per pair); the concatenated part solutions satisfy the full problem's box and equality
+# constraints, so they are a feasible warm start, and the full problem is then solved from there to
+# libsvm's eps by the same rule — same dual, same KKT stopping test, a different pair path (α agrees
+# to O(eps), as with any working-set solve).  Host simulation of the bench's 10k refit problem
+# (scripts/probes/ws_cascade_sim.py, 8 parts, part eps 0.1): 778 part pairs + 4,954 seeded pairs
+# (22 rounds) vs 8,442 cold (37 rounds); decision values differ by 1.7e-3 from the cold solve, the
+# same as cold q = 512 vs q = 1024 (1.5e-3).
+CASCADE = os.environ.get("HFENS_SVM_CASCADE", "1") != "0"
+CASCADE_MIN = int(os.environ.get("HFENS_SVM_CASCADE_MIN", "4096"))
+CASCADE_PART = int(os.environ.get("HFENS_SVM_CASCADE_PART", "1250"))
+CASCADE_EPS = float(os.environ.get("HFENS_SVM_CASCADE_EPS", "0.1"))
+CASCADE_Q = int(os.environ.get("HFENS_SVM_CASCADE_Q", "512"))
+
+
+def cascade_parts(p: _Prob) -> List[np.ndarray]:
+    """Positions (in problem order: positives first) of p's parts, or [] when p is solved cold:
+    part k holds every P-th positive and every P-th negative from k on."""
+    if p.l < CASCADE_MIN or CASCADE_PART <= 0:
+        return []
+    P = max(2, int(round(p.l / CASCADE_PART)))
+    nneg = p.l - p.npos
+    if p.npos < P or nneg < P:
+        return []
+    return [np.concatenate([np.arange(k, p.npos, P), p.npos + np.arange(k, nneg, P)]) for k in range(P)]
+
+
+def _cascade_seed(E, live, Zs, aoffs, F, device, s, max_iter_cap=None):
+    """The feasible warm start of every problem (zeros for problems solved cold), or None."""
+    parts, where = [], []
+    for k, p in enumerate(live):
+        for pos in cascade_parts(p):
+            npos = int((pos < p.npos).sum())
+            parts.append(_Prob(p.fit, p.fold, p.rows[pos], npos, p.Cp, p.Cn, p.gamma))
+            where.append(aoffs[k] + pos)
+    if not parts:
+        return None
+    zpart = _gather_rows(Zs, parts, "rows", device)
+    po = [0]
+    for p in parts:
+        po.append(po[-1] + p.l)
+    a_parts, _, _, _ = _solve_ws(E, parts, zpart, po[:-1], po, F, device, CASCADE_EPS, max_iter_cap, s,
+                                 q=CASCADE_Q if ws_q(F) == 1024 else None)
+    seed = torch.zeros(aoffs[-1], dtype=torch.float64, device=device)
+    # (a part solve that did not reach CASCADE_EPS within its rounds is still feasible: it seeds)
+    seed.index_copy_(0, _to_dev(np.concatenate(where), device), a_parts)
+    return seed
+
+
 def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None):
     from .. import ops
     E = ops.ext()
@@ -1033,14 +1092,25 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
     if group is None:
-        alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s)
+        kw = {}
+        if solver == "ws" and CASCADE and not ws_kc(F, max_l):
+            seed = _cascade_seed(E, live, Zs, aoffs, F, device, s, max_iter_cap)
+            if seed is not None:
+                kw["seed"] = seed
+                hmark("svc_cascade_seeded")
+        alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, **kw)
     else:
         def solve_local(sub):
             zsub = _gather_rows(Zs, sub, "rows", device)
             so = [0]
             for p in sub:
                 so.append(so[-1] + p.l)
-            return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s)
+            kw = {}
+            if solver == "ws" and CASCADE and not ws_kc(F, max(p.l for p in sub)):
+                seed = _cascade_seed(E, sub, Zs, so, F, device, s, max_iter_cap)
+                if seed is not None:
+                    kw["seed"] = seed
+            return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s, **kw)
         alpha, rho, iters, err = _solve_distributed(solve_local, live, aoffs[-1], aoffs, device, group)
     out = {"smo_err": err}
     for k, p in enumerate(live):

@@ -1204,6 +1204,119 @@ __global__ __launch_bounds__(256) void ws_gupdate_kernel(const WsProb* __restric
   ws_publish_keys(P, b, row, valid, a, gnew, X);
 }
 
+// Warm start (cascade seed, models/smo.py _cascade_seed): α = aseed (a feasible point: the
+// concatenated solutions of disjoint sub-problems with the same C) and G_t = −1 + y_t Σ_c y_c α_c K_tc
+// over the nonzero α_c, then t's selection keys.  Every workgroup walks the problem's points in
+// chunks of kWsChunk, compacts the nonzero coefficients into LDS (ballot + per-wave prefix) and
+// runs ws_gupdate's MFMA + exp2 tile on them; each chunk's f32 partial joins an f64 accumulator
+// (≤ 256 terms per f32 sum, as in a gradient update round).  gkey must be zero on entry.
+template <int KS>
+__global__ __launch_bounds__(256) void ws_seed_kernel(const WsProb* __restrict__ probs,
+                                                      const float* __restrict__ zcat, int F,
+                                                      const float* __restrict__ zn_all,
+                                                      const double* __restrict__ aseed,
+                                                      double* __restrict__ alpha_all,
+                                                      double* __restrict__ G_all, WsAux X) {
+  const int b = blockIdx.y;
+  const WsProb P = probs[b];
+  const int row_blk = blockIdx.x * 256;
+  if (row_blk >= P.l) return;
+  __shared__ __attribute__((aligned(16))) float sv_l[2 * KS * kWsChunk];
+  __shared__ __attribute__((aligned(16))) float sn_l[kWsChunk];
+  __shared__ __attribute__((aligned(16))) float cf_l[kWsChunk];
+  __shared__ int wcnt[4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hi = lane >> 5;
+  const int r0 = row_blk + wave * 64;
+  const int row = r0 + lane;
+  const bool valid = row < P.l;
+  const bool live = r0 < P.l;   // wave-uniform
+  const double a = valid ? aseed[P.aoff + row] : 0.0;
+  const int ra = r0 + r32, rb = r0 + 32 + r32;
+  float za[KS], zb[KS];
+  const float* zA = zcat + (P.zoff + ra) * F;
+  const float* zBp = zcat + (P.zoff + rb) * F;
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    const int k = 2 * q + hi;
+    za[q] = (k < F && ra < P.l) ? zA[k] : 0.f;
+    zb[q] = (k < F && rb < P.l) ? zBp[k] : 0.f;
+  }
+  const float zsa = ra < P.l ? P.ngl2e * zn_all[P.aoff + ra] : 0.f;
+  const float zsb = rb < P.l ? P.ngl2e * zn_all[P.aoff + rb] : 0.f;
+  const float k2 = -2.f * P.ngl2e;
+  double da = 0.0, db = 0.0;
+  for (int c0 = 0; c0 < P.l; c0 += kWsChunk) {
+    const int c = c0 + tid;
+    const double ac = c < P.l ? aseed[P.aoff + c] : 0.0;
+    const bool nz = ac > 0.0;
+    const unsigned long long m = __ballot(nz);
+    __syncthreads();   // the previous chunk is consumed
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int base = 0, cnt = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int v = wcnt[w];
+      base += w < wave ? v : 0;
+      cnt += v;
+    }
+    if (cnt == 0) continue;   // block-uniform
+    const int ncp = (cnt + 31) & ~31;
+    if (nz) {
+      const int pos = base + __popcll(m & lanes_below());
+      const float* zc = zcat + (P.zoff + c) * F;
+#pragma unroll
+      for (int k = 0; k < 2 * KS; ++k) sv_l[k * kWsChunk + pos] = k < F ? zc[k] : 0.f;
+      sn_l[pos] = P.ngl2e * zn_all[P.aoff + c];
+      cf_l[pos] = (float)(c < P.npos ? ac : -ac);
+    }
+    for (int p = cnt + tid; p < ncp; p += 256) {
+#pragma unroll
+      for (int k = 0; k < 2 * KS; ++k) sv_l[k * kWsChunk + p] = 0.f;
+      sn_l[p] = 0.f;
+      cf_l[p] = 0.f;
+    }
+    __syncthreads();
+    if (!live) continue;
+    float pa = 0.f, pb = 0.f;
+    for (int t = 0; t < ncp; t += 32) {
+      f32x16 A = {0.f}, B = {0.f};
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        const float sv = sv_l[(2 * q + hi) * kWsChunk + t + r32];
+        A = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, za[q], A, 0, 0, 0);
+        B = __builtin_amdgcn_mfma_f32_32x32x2f32(sv, zb[q], B, 0, 0, 0);
+      }
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int cc = t + 8 * gq + 4 * hi;
+        const f32x4 snv = *reinterpret_cast<const f32x4*>(&sn_l[cc]);
+        const f32x4 cfv = *reinterpret_cast<const f32x4*>(&cf_l[cc]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pa = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, A[4 * gq + q], snv[q] + zsa), 0.f)), pa);
+          pb = fmaf(cfv[q], __builtin_amdgcn_exp2f(fminf(fmaf(k2, B[4 * gq + q], snv[q] + zsb), 0.f)), pb);
+        }
+      }
+    }
+    da += (double)pa;
+    db += (double)pb;
+  }
+  if (!live) return;
+  da += __shfl_xor(da, 32, kWave);
+  db += __shfl_xor(db, 32, kWave);
+  double g = -1.0;
+  if (valid) {
+    const double upd = lane < 32 ? da : db;
+    g = -1.0 + (row < P.npos ? upd : -upd);
+    alpha_all[P.aoff + row] = a;
+    G_all[P.aoff + row] = g;
+  }
+  ws_publish_keys(P, b, row, valid, a, g, X);
+}
+
 // libsvm calculate_rho over the final gradient.
 __global__ __launch_bounds__(kWsThreads) void ws_finalize_kernel(const WsProb* __restrict__ probs,
                                                                  const WsState* __restrict__ states,
@@ -1263,6 +1376,26 @@ void ws_init(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t
   hipLaunchKernelGGL(ws_init_kernel, dim3((max_l + 255) / 256, P), dim3(256), 0, as_stream(stream),
                      (const WsProb*)probs, (const float*)zcat, F, (float*)zn, (double*)alpha, (double*)G,
                      (WsState*)states, ws_aux(keys, n, gkey));
+  launch_check();
+}
+
+// After ws_init: α ← aseed (per point, the problems' layout) and G, keys from it (ws_seed_kernel).
+void ws_seed(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t zn, uintptr_t aseed,
+             uintptr_t alpha, uintptr_t G, uintptr_t keys, long long n, uintptr_t gkey, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 48, "ws_seed: 1 <= F <= 48");
+  if (P == 0 || max_l == 0) return;
+  hipStream_t st = as_stream(stream);
+  // ws_init folded the α = 0 maxima into gkey: the seeded point's replace them
+  HFENS_CHECK(hipMemsetAsync(reinterpret_cast<void*>(gkey), 0, sizeof(unsigned long long) * 2 * (size_t)P, st));
+  const dim3 grid((max_l + 255) / 256, P);
+  const WsAux X = ws_aux(keys, n, gkey);
+#define WS_SEED(K)                                                                                   \
+  case K:                                                                                           \
+    hipLaunchKernelGGL(ws_seed_kernel<K>, grid, dim3(256), 0, st, (const WsProb*)probs, (const float*)zcat, F, \
+                       (const float*)zn, (const double*)aseed, (double*)alpha, (double*)G, X);      \
+    break;
+  switch (ws_ks(F)) { WS_SEED(4) WS_SEED(9) WS_SEED(12) WS_SEED(24) }
+#undef WS_SEED
   launch_check();
 }
 

@@ -157,3 +157,76 @@ def test_platt_kernel_matches_host_sigmoid_train(dev, ls):
         A, B = smo._sigmoid_train_host(dec, lab)
         assert got[2 * k] == pytest.approx(A, rel=1e-9, abs=1e-12), (k, got[2 * k], A)
         assert got[2 * k + 1] == pytest.approx(B, rel=1e-9, abs=1e-12), (k, got[2 * k + 1], B)
+
+
+def test_ws_seed_gradient_matches_f64(dev):
+    """ws_seed (svm_ws.hip ws_seed_kernel): α ← a feasible seed, G = −1 + y ∘ K (y ∘ α) over the
+    nonzero α — against the same expression in f64 on the host (f32 kernel values: ≤ 1e-4)."""
+    from hfens import ops
+    E = ops.ext()
+    F = 17
+    ls, nposs = [3000, 1700], [1300, 900]
+    g = torch.Generator().manual_seed(5)
+    Zs = [torch.randn(l, F, generator=g, dtype=torch.float32) for l in ls]
+    gamma = 1.0 / F
+    arr = np.zeros(2, smo._WS_DT)
+    off = 0
+    seeds = []
+    for k, (l, npos) in enumerate(zip(ls, nposs)):
+        arr[k] = (off, off, l, npos, 0.9, 1.3, -gamma * 1.4426950408889634, 0)
+        a = torch.rand(l, generator=g, dtype=torch.float64) * 0.9
+        a[torch.rand(l, generator=g) < 0.5] = 0.0       # about half the points are not support vectors
+        a[npos:] = a[npos:].clamp(max=1.3)
+        seeds.append(a)
+        off += l
+    n = off
+    zcat = torch.cat(Zs).to(dev).contiguous()
+    aseed = torch.cat(seeds).to(dev)
+    pdev = smo._dev_struct(arr, dev)
+    zn = torch.empty(n, dtype=torch.float32, device=dev)
+    alpha = torch.empty(n, dtype=torch.float64, device=dev)
+    G = torch.empty(n, dtype=torch.float64, device=dev)
+    states = torch.zeros(2 * smo._WS_STATE_BYTES // 4, dtype=torch.int32, device=dev)
+    keys = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    hist = torch.zeros(1, dtype=torch.int32, device=dev)
+    gkey = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = ops.stream_ptr(dev)
+    E.ws_init(pdev.data_ptr(), 2, max(ls), zcat.data_ptr(), F, zn.data_ptr(), alpha.data_ptr(), G.data_ptr(),
+              states.data_ptr(), keys.data_ptr(), n, hist.data_ptr(), gkey.data_ptr(), s)
+    E.ws_seed(pdev.data_ptr(), 2, max(ls), zcat.data_ptr(), F, zn.data_ptr(), aseed.data_ptr(), alpha.data_ptr(),
+              G.data_ptr(), keys.data_ptr(), n, gkey.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(alpha.cpu(), aseed.cpu())
+    off = 0
+    for k, (l, npos) in enumerate(zip(ls, nposs)):
+        Z = Zs[k].double()
+        y = torch.ones(l, dtype=torch.float64)
+        y[npos:] = -1.0
+        K = torch.exp(-gamma * torch.cdist(Z, Z) ** 2)
+        ref = -1.0 + y * (K @ (y * seeds[k]))
+        got = G[off:off + l].cpu()
+        assert (got - ref).abs().max() <= 1e-4 * max(1.0, float(ref.abs().max())), (got - ref).abs().max()
+        off += l
+
+
+def test_ws_cascade_seed_matches_cold_solve(dev, monkeypatch):
+    """The cascade warm start (smo._cascade_seed: disjoint class-stratified parts with the same C,
+    solved loosely, then the full problem from their concatenated α) reaches the same stopping rule
+    and the same model to the solver's tolerance as the cold solve, in fewer pairs."""
+    X, y = _data(10000, 17, 77)
+    Z = ((X - X.mean(0)) / X.std(0, unbiased=False)).to(dev)
+    monkeypatch.setattr(smo, "SOLVER", "auto")
+    out = {}
+    for cascade in (False, True):
+        monkeypatch.setattr(smo, "CASCADE", cascade)
+        m = SVC(class_weight="balanced", random_state=2020).fit(Z, y.to(dev))
+        st = smo.LAST_WS_STATS
+        assert (st["gap"] < 1e-3).all(), st["gap"]
+        gamma = 1.0 / (17 * float(Z.var(unbiased=False)))
+        out[cascade] = dict(d=m.decision_function(Z).cpu().numpy(), pairs=int(st["inner"].max()),
+                            obj=_dual(Z.cpu().numpy(), None, m._dual_coef_[0].cpu().numpy(),
+                                      m.support_.cpu().numpy(), gamma))
+    dd = np.abs(out[True]["d"] - out[False]["d"])
+    assert np.median(dd) < 1e-3 and dd.max() < 1e-2, (np.median(dd), dd.max())
+    assert abs(out[True]["obj"] - out[False]["obj"]) <= 1e-3 * abs(out[False]["obj"])
+    assert out[True]["pairs"] < 0.8 * out[False]["pairs"], (out[True]["pairs"], out[False]["pairs"])
