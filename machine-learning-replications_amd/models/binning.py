@@ -422,7 +422,7 @@ def fit_bins(X: torch.Tensor, max_bins: int = 256, group=None, guard=None) -> Bi
     if group is not None and not LEGACY_DP_BINS:
         return _fit_bins_dp(X32, max_bins, group)
     if host:
-        return fit_bins_host(X32.cpu().numpy(), max_bins, dev)
+        return fit_bins_host(X32.cpu().numpy(), max_bins, dev, non_blocking=X32.is_cuda)
     nb = np.empty(F, dtype=np.int32)
     lo = np.zeros((F, 256), dtype=np.float64)
     hi = np.zeros((F, 256), dtype=np.float64)

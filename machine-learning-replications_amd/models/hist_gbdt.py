@@ -615,10 +615,95 @@ def _graph_units(st, group, prof, peer=None) -> int:
         import torch.distributed as dist
         if peer is None and dist.get_backend(group) != "nccl":
             return 0     # gloo collectives cannot be captured; peer kernels and RCCL can
+        if not validate_stage_graph(group, st.raw.device, peer):
+            return 0     # the group's replayed collectives disagreed with eager ones: eager loop
     elif STAGE_GRAPH != "1":
         return 0     # single process: the eager loop is GPU-bound already (measured), keep it
     # units of 3 stages t ≡ 0, 1, 2 (mod 3) while every stage of the unit still all-reduces (t ≤ T)
     return (st.T + 1) // 3
+
+
+# First-use validation of the stage graph under a process group: a 3-stage unit of
+# just the per-stage reduction (device stage counter tick + the peer kernel or the captured RCCL
+# all-reduce, the slots rotating as in the fit) is captured once and replayed twice on
+# rank-specific int64 payloads; the results must equal eager all-reduces of the same payloads bit
+# for bit on every rank.  All ranks agree (MIN) and keep the graph or run the stage loop eagerly
+# together; the outcome is logged and kept in GRAPH_PROBES.  HFENS_GBDT_GRAPH_PROBE_CORRUPT=<rank>
+# perturbs that rank's replayed result (tests of the fallback).
+GRAPH_PROBES: dict = {}
+
+
+def validate_stage_graph(group, dev, peer) -> bool:
+    import logging
+    import torch.distributed as dist
+    from .. import ops, runtime
+    key = (id(group), id(peer) if peer is not None else 0)
+    if key in GRAPH_PROBES:
+        return GRAPH_PROBES[key]["ok"]
+    W, me = dist.get_world_size(group), dist.get_rank(group)
+    E = ops.ext()
+    m, reps = 3 * 1024 + 5, 2
+    lib_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+    buf = torch.zeros(3 * m, dtype=torch.int64, device=dev)
+    tdev = torch.zeros(1, dtype=torch.int32, device=dev)
+    base = peer.epoch if peer is not None else 0
+
+    def payload(rank, r):
+        g = np.random.default_rng(0xB0057 + 104729 * rank + r)
+        return torch.from_numpy(g.integers(-(1 << 40), 1 << 40, 3 * m, dtype=np.int64))
+    ok, detail = True, ""
+    try:
+        cap = runtime.stream(dev, "gbdt_graph")
+        cur = torch.cuda.current_stream(dev)
+        cap.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cap):
+            s = ops.stream_ptr(dev)
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                for k in range(3):
+                    E.gbdt_stage_tick(tdev.data_ptr(), s)
+                    if peer is not None:
+                        peer.allreduce_(buf[k * m:(k + 1) * m], (base + k + 1) % 3, k, tdev, epoch_base=base, stream=s)
+                    else:
+                        dist.all_reduce(buf[k * m:(k + 1) * m], op=dist.ReduceOp.SUM, group=group)
+            finally:
+                g.capture_end()
+        got = []
+        for r in range(reps):
+            buf.copy_(payload(me, r).to(dev))
+            g.replay()
+            torch.cuda.synchronize(dev)
+            got.append(buf.cpu())
+        if peer is not None:
+            peer.advance(3 * reps)
+            peer.check()
+        corrupt = os.environ.get("HFENS_GBDT_GRAPH_PROBE_CORRUPT", "")
+        if corrupt != "" and int(corrupt) == me:
+            got[-1][m + 7] += 1
+        for r in range(reps):
+            ref = payload(me, r).to(lib_dev)
+            dist.all_reduce(ref, op=dist.ReduceOp.SUM, group=group)
+            if not torch.equal(got[r], ref.cpu()):
+                ok, detail = False, f"rank {me}: replay {r}: {int((got[r] != ref.cpu()).sum())} of {3 * m} differ"
+                break
+        del g
+    except RuntimeError as e:
+        ok, detail = False, f"rank {me}: {e}"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=lib_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    notes = [None] * W
+    dist.all_gather_object(notes, detail, group=group)
+    joint = bool(int(flag.item()))
+    GRAPH_PROBES[key] = dict(ok=joint, world=W, peer=peer is not None, mismatches=[d for d in notes if d])
+    log = logging.getLogger("hfens.gbdt")
+    if joint:
+        log.info("GBDT stage graph validated against eager reductions (world %d, %s)", W,
+                 "peer kernel" if peer is not None else "RCCL")
+    else:
+        log.warning("GBDT stage graph disagrees with eager reductions: %s — eager stage loop",
+                    "; ".join(GRAPH_PROBES[key]["mismatches"]))
+    return joint
 
 
 def _prune_graphs():
@@ -688,6 +773,8 @@ def _run_stage(st: _State, group):
     if group is not None and dev.type == "cuda":
         from ..parallel import xgmi
         peer = xgmi.peer_comm(group, dev, slot)
+    # (before the epoch base is read: a first-use graph validation takes epochs of its own)
+    units = _graph_units(st, group, prof, peer)
     base = peer.epoch if peer is not None else 0
 
     def stage(t, host_t, t_dev=None):
@@ -748,7 +835,6 @@ def _run_stage(st: _State, group):
         COLLECTIVES["xgmi_per_stage"] = 0.0
         st.reduced = True
         return
-    units = _graph_units(st, group, prof, peer)
     if units:
         # HIP graph of one 3-stage unit (stage kernel [+ partial reduce] + counter tick [+ the
         # stage's all-reduce], × 3 — the comm slots rotate with period 3), captured once per fit

@@ -301,9 +301,12 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
     fused = (X.is_cuda and group is None and FUSED and not emulate and X.dim() == 2
              and X.shape[1] + int(bool(m0.fit_intercept)) <= 64 and X.shape[0] > 0)
     flags = None
+    from ..utils.timing import hmark
+    hmark("lr_in")
     if fused:
         # the guards ride on the fused launch's one host read instead of two synchronous checks
         flags = torch.stack([guards.finite_flag(X), guards.binary_flag(y.to(X.device))])
+        hmark("lr_flags")
     else:
         guards.check_finite(X, "LogisticRegression.fit X")
         guards.check_binary(y, "LogisticRegression.fit y")
@@ -322,6 +325,7 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
     else:
         Xa = X
     F1 = Xa.shape[1]
+    hmark("lr_xa")
     # per-model sample weights: class weights computed on that model's training rows
     mk = masks.to(torch.float64)
     if m0.class_weight == "balanced":
@@ -336,11 +340,12 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
     l1 = m0.penalty == "l1"
     penal = torch.ones(F1, dtype=torch.uint8, device=dev)
     if not l1 and m0.fit_intercept:
-        penal[-1] = 0  # lbfgs path: intercept not penalised
+        penal[-1:].zero_()  # lbfgs path: intercept not penalised (a fill: no host→device copy)
     pen_f = penal.to(torch.float64)
     scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
     if fused:
         LAST_PATH["path"] = "fused"
+        hmark("lr_prep")
         return dict(models=models, F=F, scale=scale, fit_intercept=bool(m0.fit_intercept), dev=dev,
                     fused=_launch_fused(Xa, s, ypm, penal, C, l1, max_outer, flags))
     LAST_PATH["path"] = "loop"

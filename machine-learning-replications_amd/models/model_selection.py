@@ -42,7 +42,13 @@ def kfold_test_folds(n: int, n_splits: int) -> np.ndarray:
 def fold_masks(test_folds, n_splits: int, device=None, with_full: bool = True) -> torch.Tensor:
     """Training masks ``[n_splits (+1), n]``: fold k trains on rows not in test fold k;
     the optional last row is the full refit."""
-    tf = torch.as_tensor(np.asarray(test_folds), device=device)
+    tf = torch.from_numpy(np.ascontiguousarray(test_folds))
+    if device is not None and torch.device(device).type == "cuda":
+        # pinned, non-blocking: a pageable upload would hold the host until the stream's queued work
+        # (e.g. the LassoCV path under which the stacking trainer is prelaunched) has finished
+        tf = tf.pin_memory().to(device, non_blocking=True)
+    elif device is not None:
+        tf = tf.to(device)
     m = torch.stack([tf != k for k in range(n_splits)])
     if with_full:
         m = torch.cat([m, torch.ones(1, tf.numel(), dtype=torch.bool, device=device)])

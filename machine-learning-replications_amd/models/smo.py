@@ -687,7 +687,7 @@ def _ws_groups(live, device) -> List[List[int]]:
 
 
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None,
-              seed=None, q=None):
+              seed=None, q=None, groups=None):
     """``seed``: a feasible α (per point, this batch's layout) to start from instead of α = 0
     (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`)."""
     P = len(live)
@@ -704,7 +704,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     sync = _WS_SYNC[0] or big
     if big and steps_per_check is None:
         steps_per_check = WS_BIG_CHUNK
-    groups = _ws_groups(live, device) if not sync else [list(range(P))]
+    groups = (_ws_groups(live, device) if groups is None else [list(range(P))]) if not sync else [list(range(P))]
     cuda = torch.device(device).type == "cuda"
     caller = torch.cuda.current_stream(device) if cuda else None
     # HIP graphs of the rounds (K-cached, rounds enqueued ahead): ~290 rounds × 2 launches × 3 groups
@@ -1034,42 +1034,72 @@ def _solve_distributed(solve_local, live, n_alpha, aoffs, device, group):
 # same as cold q = 512 vs q = 1024 (1.5e-3).
 CASCADE = os.environ.get("HFENS_SVM_CASCADE", "1") != "0"
 CASCADE_MIN = int(os.environ.get("HFENS_SVM_CASCADE_MIN", "4096"))
-CASCADE_PART = int(os.environ.get("HFENS_SVM_CASCADE_PART", "1250"))
+CASCADE_PART = int(os.environ.get("HFENS_SVM_CASCADE_PART", "1600"))
 CASCADE_EPS = float(os.environ.get("HFENS_SVM_CASCADE_EPS", "0.1"))
 CASCADE_Q = int(os.environ.get("HFENS_SVM_CASCADE_Q", "512"))
+# working-set rounds the parts get (a fixed budget: every round is enqueued ahead without a host
+# check, so rounds past the parts' convergence are launches the full solve waits on; a part stopped
+# by the budget is still feasible and still seeds)
+CASCADE_ROUNDS = int(os.environ.get("HFENS_SVM_CASCADE_ROUNDS", "8"))
+LAST_CASCADE: dict = {}
+
+
+def cascade_split(l: int, npos: int) -> int:
+    """Number of cascade parts of a problem of l points (npos positive); 0 = solved cold."""
+    if l < CASCADE_MIN or CASCADE_PART <= 0:
+        return 0
+    P = max(2, int(round(l / CASCADE_PART)))
+    return P if (npos >= P and l - npos >= P) else 0
 
 
 def cascade_parts(p: _Prob) -> List[np.ndarray]:
     """Positions (in problem order: positives first) of p's parts, or [] when p is solved cold:
-    part k holds every P-th positive and every P-th negative from k on."""
-    if p.l < CASCADE_MIN or CASCADE_PART <= 0:
-        return []
-    P = max(2, int(round(p.l / CASCADE_PART)))
+    part j holds every P-th positive and every P-th negative from j on (the host mirror of
+    stackdev.hip cascade_where_kernel)."""
+    P = cascade_split(p.l, p.npos)
     nneg = p.l - p.npos
-    if p.npos < P or nneg < P:
-        return []
-    return [np.concatenate([np.arange(k, p.npos, P), p.npos + np.arange(k, nneg, P)]) for k in range(P)]
+    return [np.concatenate([np.arange(j, p.npos, P), p.npos + np.arange(j, nneg, P)]) for j in range(P)]
 
 
-def _cascade_seed(E, live, Zs, aoffs, F, device, s, max_iter_cap=None):
-    """The feasible warm start of every problem (zeros for problems solved cold), or None."""
-    parts, where = [], []
+class _Part:
+    """A cascade part's solver record (its rows are gathered on the device, never listed on the host)."""
+    __slots__ = ("fit", "fold", "l", "npos", "Cp", "Cn", "gamma")
+
+    def __init__(self, fit, fold, l, npos, Cp, Cn, gamma):
+        self.fit, self.fold, self.l, self.npos, self.Cp, self.Cn, self.gamma = fit, fold, l, npos, Cp, Cn, gamma
+
+
+def _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap=None):
+    """The feasible warm start of every problem (zeros for problems solved cold), or None.  The
+    parts' point lists are built on the device (cascade_where) and their features gathered from the
+    parents' rows in ``zcat`` — the host only counts."""
+    parts, tab = [], []
+    start = 0
     for k, p in enumerate(live):
-        for pos in cascade_parts(p):
-            npos = int((pos < p.npos).sum())
-            parts.append(_Prob(p.fit, p.fold, p.rows[pos], npos, p.Cp, p.Cn, p.gamma))
-            where.append(aoffs[k] + pos)
+        P = cascade_split(p.l, p.npos)
+        nneg = p.l - p.npos
+        for j in range(P):
+            cp, cn = (p.npos - j + P - 1) // P, (nneg - j + P - 1) // P
+            parts.append(_Part(p.fit, p.fold, cp + cn, cp, p.Cp, p.Cn, p.gamma))
+            tab.append((start, cp + cn, aoffs[k], P, j, p.npos, cp))
+            start += cp + cn
     if not parts:
         return None
-    zpart = _gather_rows(Zs, parts, "rows", device)
-    po = [0]
-    for p in parts:
-        po.append(po[-1] + p.l)
-    a_parts, _, _, _ = _solve_ws(E, parts, zpart, po[:-1], po, F, device, CASCADE_EPS, max_iter_cap, s,
-                                 q=CASCADE_Q if ws_q(F) == 1024 else None)
+    tab_np = np.asarray(tab, dtype=np.int64)
+    where = torch.empty(start, dtype=torch.int64, device=device)
+    E.cascade_where(_to_dev(tab_np.reshape(-1), device).data_ptr(), len(parts), int(tab_np[:, 1].max()),
+                    where.data_ptr(), s)
+    zpart = zcat.index_select(0, where)
+    po = np.concatenate([[0], np.cumsum(tab_np[:, 1])]).tolist()
+    a_parts, _, _, _ = _solve_ws(E, parts, zpart, po[:-1], po, F, device, CASCADE_EPS, CASCADE_ROUNDS, s,
+                                 q=CASCADE_Q if ws_q(F) == 1024 else None, groups=1)
+    from ..utils.timing import dmark
+    dmark("svc_parts_done")
+    LAST_CASCADE.clear()
+    LAST_CASCADE.update(parts=len(parts), stats=LAST_WS_STATS._f)   # read lazily (device stats)
     seed = torch.zeros(aoffs[-1], dtype=torch.float64, device=device)
-    # (a part solve that did not reach CASCADE_EPS within its rounds is still feasible: it seeds)
-    seed.index_copy_(0, _to_dev(np.concatenate(where), device), a_parts)
+    # (a part solve stopped by its round budget is still feasible: it seeds)
+    seed.index_copy_(0, where, a_parts)
     return seed
 
 
@@ -1094,7 +1124,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     if group is None:
         kw = {}
         if solver == "ws" and CASCADE and not ws_kc(F, max_l):
-            seed = _cascade_seed(E, live, Zs, aoffs, F, device, s, max_iter_cap)
+            seed = _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap)
             if seed is not None:
                 kw["seed"] = seed
                 hmark("svc_cascade_seeded")
@@ -1107,7 +1137,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                 so.append(so[-1] + p.l)
             kw = {}
             if solver == "ws" and CASCADE and not ws_kc(F, max(p.l for p in sub)):
-                seed = _cascade_seed(E, sub, Zs, so, F, device, s, max_iter_cap)
+                seed = _cascade_seed(E, sub, zsub, so, F, device, s, max_iter_cap)
                 if seed is not None:
                     kw["seed"] = seed
             return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s, **kw)

@@ -271,12 +271,17 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                                 oof(i, out[i])
                         hmark(f"{name}_host_done")
                         dmark(f"{name}_done")
+                # every meta-feature column of these bases is enqueued on this stream by now: the
+                # meta model waits for this point, not for the bookkeeping enqueued after it
+                cols_ev = torch.cuda.Event()
+                cols_ev.record(other)
                 if dev_bases is not None:
                     # the refit models' fitted state from the device node tables / coefficients,
                     # enqueued on this stream behind their solves while the SMO runs (no host read:
                     # the guards are read after it)
                     for f in dev_bases["post"]:
                         f()
+                    hmark("bases_post")
         finally:
             logreg_solver.BLOCK_BUDGET[0] = lr_budget
         if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
@@ -285,8 +290,9 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
             # out-of-fold kernel.  (On the main stream its wait for the SVC would be the head of an
             # otherwise idle hardware queue for the rest of the SMO: measured, such a pending
             # cross-stream wait slowed the SMO's dispatches by 2-4 ms, profiles/r5_headline.md.)
+            hmark("early_in")
             side.wait_stream(main)
-            side.wait_stream(other)
+            side.wait_event(cols_ev)
             with torch.cuda.stream(side):
                 early["handle"] = early["launch"]()
         with torch.cuda.stream(side):

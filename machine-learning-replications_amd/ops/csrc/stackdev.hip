@@ -257,4 +257,25 @@ void svm_patch_f32(uintptr_t base, int stride, int off, int count, uintptr_t fit
   launch_check();
 }
 
+// Cascade parts of the working-set SMO (models/smo.py _cascade_seed): part q of a parent problem
+// (points [0, npos) positive, then negative) holds the parent's positives j, j+P, … then its
+// negatives npos+j, npos+j+P, …; where[start_q + t] = the parent's absolute point index of the
+// part's t-th point.  tab: [Q][7] int64 {start, len, aoff, P, j, npos, cp}; grid (x: points, y: parts).
+__global__ void cascade_where_kernel(const long long* __restrict__ tab, long long* __restrict__ where) {
+  const long long* r = tab + 7 * (size_t)blockIdx.y;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= r[1]) return;
+  const long long P = r[3], j = r[4], npos = r[5], cp = r[6];
+  const long long pos = t < cp ? j + t * P : npos + j + (t - cp) * P;
+  where[r[0] + t] = r[2] + pos;
+}
+
+void cascade_where(uintptr_t tab, int Q, long long max_len, uintptr_t where, uintptr_t stream) {
+  HFENS_REQUIRE(Q >= 0 && max_len >= 0 && Q <= 65535, "cascade_where: 0 <= parts <= 65535");
+  if (Q == 0 || max_len == 0) return;
+  hipLaunchKernelGGL(cascade_where_kernel, dim3((unsigned)((max_len + 255) / 256), Q), dim3(256), 0, as_stream(stream),
+                     (const long long*)tab, (long long*)where);
+  launch_check();
+}
+
 }  // namespace hfens

@@ -22,9 +22,19 @@ peer; ``1`` requires it; ``0`` never uses it.  Only uncached (fine-grained) buff
 the driver cannot share one, the group keeps RCCL (no coarse-grained fallback, whose L2 lines an
 acquire would not invalidate).  A peer wait that times out sets an error flag that
 :meth:`PeerComm.check` all-reduces over the group, so every rank raises together.
+
+Self-validation: the first time a group's peer buffers exist, :func:`validate`
+runs probe reductions through the peer kernel — an int64 sum spanning several chunks and f64
+sum / max / min — and compares them bit for bit with the collective library's answer (int64:
+``all_reduce``; f64: ``all_gather`` then the same rank-order fold).  Every rank then keeps the peer
+path or drops to RCCL TOGETHER (one MIN agreement), and the outcome is logged and kept in
+:data:`PROBES`.  ``HFENS_XGMI_PROBE_CORRUPT=<rank>`` perturbs that rank's peer result (tests of the
+mismatch path).  Every user of a PeerComm takes slot = epoch mod 3, so consecutive reductions
+never share a slot whichever caller issued them.
 """
 from __future__ import annotations
 
+import logging
 import os
 import socket
 from typing import Dict, Optional
@@ -154,6 +164,80 @@ class PeerComm:
 
 _CACHE: Dict[tuple, PeerComm] = {}
 _OK: Dict[int, bool] = {}
+PROBES: Dict[int, dict] = {}     # id(group) → outcome of the first-use validation
+PROBE = os.environ.get("HFENS_XGMI_PROBE", "1") != "0"
+_LOG = logging.getLogger("hfens.xgmi")
+
+
+def _probe_payloads(rank: int, n: int):
+    rng = np.random.default_rng(0x5EED + 7919 * rank)
+    ints = rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64)
+    # no zeros (−0.0 + 0.0 and 0.0 + −0.0 differ in sign): magnitudes over 12 decades
+    f = rng.standard_normal(n) * np.exp(rng.uniform(-14.0, 14.0, n))
+    f[f == 0.0] = 1.0
+    return ints, f
+
+
+def validate(pc: "PeerComm") -> bool:
+    """Collective: probe the peer kernel against the collective library, bit for bit; returns the
+    group's joint verdict (True on every rank or False on every rank)."""
+    import torch.distributed as dist
+    W, me, group = pc.W, pc.me, pc.group
+    n = int(min(pc.cap, 2 * CHUNK + 37))
+    gloo = dist.get_backend(group) == "gloo"
+    lib_dev = torch.device("cpu") if gloo else pc.device
+    mine_i, mine_f = _probe_payloads(me, n)
+    corrupt = os.environ.get("HFENS_XGMI_PROBE_CORRUPT", "")
+    detail = ""
+    ok = True
+    try:
+        ti = torch.from_numpy(mine_i.copy()).to(pc.device)
+        pc.allreduce_(ti, (pc.epoch + 1) % 3, 0, epoch_base=pc.epoch)
+        pc.epoch += 1
+        tf = {op: pc.reduce_f64_(torch.from_numpy(mine_f.copy()).to(pc.device), op) for op in ("sum", "max", "min")}
+        torch.cuda.synchronize(pc.device)
+        got_i = ti.cpu()
+        got_f = {op: t.cpu() for op, t in tf.items()}
+        if corrupt != "" and int(corrupt) == me:
+            got_i[n // 2] += 1
+        # the library's answers
+        ref_i = torch.from_numpy(mine_i.copy()).to(lib_dev)
+        dist.all_reduce(ref_i, op=dist.ReduceOp.SUM, group=group)
+        allf = [torch.empty(n, dtype=torch.float64, device=lib_dev) for _ in range(W)]
+        dist.all_gather(allf, torch.from_numpy(mine_f.copy()).to(lib_dev), group=group)
+        allf = [t.cpu() for t in allf]
+        ref_f = {"sum": allf[0].clone(), "max": allf[0].clone(), "min": allf[0].clone()}
+        for r in range(1, W):
+            ref_f["sum"] = ref_f["sum"] + allf[r]
+            ref_f["max"] = torch.maximum(ref_f["max"], allf[r])
+            ref_f["min"] = torch.minimum(ref_f["min"], allf[r])
+        bad = []
+        if not torch.equal(got_i, ref_i.cpu()):
+            bad.append(f"int64 sum ({int((got_i != ref_i.cpu()).sum())} of {n} differ)")
+        for op in ("sum", "max", "min"):
+            if not torch.equal(got_f[op].view(torch.int64), ref_f[op].view(torch.int64)):
+                bad.append(f"f64 {op} ({int((got_f[op] != ref_f[op]).sum())} of {n} differ)")
+        if bad:
+            ok, detail = False, f"rank {me}: " + ", ".join(bad)
+        try:
+            pc.check()   # a peer wait that timed out on any rank
+        except RuntimeError as e:
+            ok, detail = False, f"rank {me}: {e}"
+    except RuntimeError as e:
+        ok, detail = False, f"rank {me}: {e}"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=lib_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    joint = bool(int(flag.item()))
+    notes = [None] * W
+    dist.all_gather_object(notes, detail, group=group)
+    rec = dict(ok=joint, world=W, elements=n, mismatches=[d for d in notes if d])
+    PROBES[id(group)] = rec
+    if joint:
+        _LOG.info("xGMI peer path validated against the collective library (world %d, %d elements)", W, n)
+    else:
+        _LOG.warning("xGMI peer path disagrees with the collective library: %s — every rank uses RCCL",
+                     "; ".join(rec["mismatches"]))
+    return joint
 
 
 def _same_host(group) -> bool:
@@ -194,6 +278,13 @@ def peer_comm(group, device, cap: int, tag: str = "") -> Optional[PeerComm]:
             _CACHE.pop(key, None)
             return None
         pc.epoch = epoch
+        if PROBE and gid not in PROBES and not validate(pc):
+            pc.close()
+            _OK[gid] = False
+            if MODE == "1":
+                raise RuntimeError("HFENS_XGMI=1 but the peer path failed its validation: "
+                                   + "; ".join(PROBES[gid]["mismatches"]))
+            return None
         _CACHE[key] = pc
     return pc
 
@@ -220,3 +311,4 @@ def release_all():
         pc.close()
     _CACHE.clear()
     _OK.clear()
+    PROBES.clear()

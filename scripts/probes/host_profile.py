@@ -21,14 +21,15 @@ def step():
     return develop(Xd, yd, Xs, ys, names, device=dev, timer=StageTimer(enabled=False))
 
 
-for _ in range(2):
+for _ in range(4):
     step()
 torch.cuda.synchronize()
 pr = cProfile.Profile()
 pr.enable()
-step()
+for _ in range(3):
+    step()
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(25)
-st.sort_stats("cumulative").print_stats(40)
+st.sort_stats("tottime").print_stats(45)
+st.sort_stats("cumulative").print_stats(70)

@@ -23,6 +23,10 @@ for rep in range(4):
 torch.cuda.synchronize()
 print(tm.table())
 st = smo.LAST_WS_STATS
+if smo.LAST_CASCADE.get("stats"):
+    cs = smo.LAST_CASCADE["stats"]()
+    print("cascade parts", smo.LAST_CASCADE["parts"], "outer max", int(cs["outer"].max()), "mean",
+          float(cs["outer"].mean()), "inner max", int(cs["inner"].max()), "gap max", float(cs["gap"].max()))
 print("q", st.get("q"), "outer", st["outer"].tolist())
 print("inner", st["inner"].tolist())
 clk = 2.4e3  # cycles per µs (s_memtime ≈ shader clock)

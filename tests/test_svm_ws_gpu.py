@@ -230,3 +230,25 @@ def test_ws_cascade_seed_matches_cold_solve(dev, monkeypatch):
     assert np.median(dd) < 1e-3 and dd.max() < 1e-2, (np.median(dd), dd.max())
     assert abs(out[True]["obj"] - out[False]["obj"]) <= 1e-3 * abs(out[False]["obj"])
     assert out[True]["pairs"] < 0.8 * out[False]["pairs"], (out[True]["pairs"], out[False]["pairs"])
+
+
+def test_cascade_where_matches_host_parts(dev):
+    """stackdev.hip cascade_where (the parts' point lists, built on the device) equals the host
+    mirror smo.cascade_parts for parents of assorted sizes and class balances."""
+    from hfens import ops
+    parents = [(10000, 2300), (8000, 1841), (6400, 1500), (4096, 7), (5000, 4990)]
+    tab, ref, aoff, start = [], [], 0, 0
+    for l, npos in parents:
+        p = smo._Prob(0, -1, np.arange(l), npos, 1.0, 1.0, 0.1)
+        P = smo.cascade_split(l, npos)
+        for j, pos in enumerate(smo.cascade_parts(p)):
+            cp = int((pos < npos).sum())
+            tab.append((start, pos.shape[0], aoff, P, j, npos, cp))
+            ref.append(aoff + pos)
+            start += pos.shape[0]
+        aoff += l
+    tab = np.asarray(tab, dtype=np.int64)
+    where = torch.empty(start, dtype=torch.int64, device=dev)
+    ops.ext().cascade_where(torch.from_numpy(tab.reshape(-1)).to(dev).data_ptr(), tab.shape[0], int(tab[:, 1].max()),
+                            where.data_ptr(), ops.stream_ptr(dev))
+    assert np.array_equal(where.cpu().numpy(), np.concatenate(ref))

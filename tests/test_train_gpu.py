@@ -232,11 +232,12 @@ def test_gbdt_stage_sklearn_ties_match_host(dev, rows):
         assert torch.allclose(a.train_score_, b.train_score_.cpu(), rtol=1e-12)
 
 
-def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0, fail_open_rank=-1):
+def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0, fail_open_rank=-1, env=None):
     import os
     # ranks sharing ONE card: one hardware queue each, so 4 processes' queues are all resident
     # (a spinning peer kernel must not keep another rank's queue from being scheduled)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HFENS_XGMI=xgmi, GPU_MAX_HW_QUEUES="1")
+    os.environ.update(env or {})
     import torch.distributed as dist
     from hfens.models import hist_gbdt
     from hfens.parallel import dist as pdist
@@ -257,15 +258,17 @@ def _dp_stage_worker(rank, world, port, q, xgmi="0", T=30, subsample=1.0, fail_o
             fit_gbdt_batch(ms, shard_rows(X, rank, world).to(dev), shard_rows(y, rank, world).to(dev),
                            group=dist.group.WORLD)
         if rank == 0:
+            from hfens.parallel import xgmi as _xg
             q.put((hist_gbdt.LAST_PATH["path"], hist_gbdt.COLLECTIVES["per_stage"],
                    hist_gbdt.COLLECTIVES.get("xgmi_per_stage", 0.0), hist_gbdt.GRAPH_INFO.get("units", 0),
                    [(m.tree_feature_.cpu().numpy(), m.tree_threshold_.cpu().numpy(), m.tree_value_.cpu().numpy(),
-                     m.tree_impurity_.cpu().numpy(), m.train_score_.cpu().numpy()) for m in ms]))
+                     m.tree_impurity_.cpu().numpy(), m.train_score_.cpu().numpy()) for m in ms],
+                   list(_xg.PROBES.values()), list(hist_gbdt.GRAPH_PROBES.values())))
     finally:
         pdist.shutdown()
 
 
-def _run_dp_stage(world, xgmi, T=30, subsample=1.0, fail_open_rank=-1):
+def _run_dp_stage(world, xgmi, T=30, subsample=1.0, fail_open_rank=-1, env=None, probes=False):
     import socket
     import torch.multiprocessing as mp
     sk = socket.socket()
@@ -274,7 +277,7 @@ def _run_dp_stage(world, xgmi, T=30, subsample=1.0, fail_open_rank=-1):
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_stage_worker, args=(r, world, port, q, xgmi, T, subsample, fail_open_rank))
+    procs = [ctx.Process(target=_dp_stage_worker, args=(r, world, port, q, xgmi, T, subsample, fail_open_rank, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -282,7 +285,7 @@ def _run_dp_stage(world, xgmi, T=30, subsample=1.0, fail_open_rank=-1):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return out
+    return out if probes else out[:5]
 
 
 def _check_dp_stage_equal(dev, got, T=30, subsample=1.0):
@@ -316,6 +319,40 @@ def test_gbdt_stage_xgmi_bit_identical(dev, world, subsample):
     assert path == "stage" and per_stage == 0.0 and xg == 1.0
     assert units == 31 // 3          # the stage loop ran as replayed HIP graphs
     _check_dp_stage_equal(dev, got, subsample=subsample)
+
+
+def test_xgmi_first_use_probe_validates(dev):
+    """the first use of the peer buffers runs probe reductions (int64 sum over several
+    chunks, f64 sum / max / min in rank order) through the peer kernel and through the collective
+    library, bit for bit, and the first stage-graph use replays captured reductions against eager
+    ones — both pass on every rank, so the fit keeps the peer kernel inside the replayed graph."""
+    path, per_stage, xg, units, got, pr, gpr = _run_dp_stage(2, "try", probes=True)
+    assert pr and all(p["ok"] and not p["mismatches"] for p in pr), pr
+    assert gpr and all(p["ok"] and p["peer"] for p in gpr), gpr
+    assert per_stage == 0.0 and xg == 1.0 and units == 31 // 3
+    _check_dp_stage_equal(dev, got)
+
+
+def test_xgmi_probe_mismatch_falls_back_together(dev):
+    """One rank's probe result disagrees with the library's (HFENS_XGMI_PROBE_CORRUPT): every rank
+    drops the peer path together, the mismatch is recorded with the rank that saw it, and the fit
+    runs on the collective library — one all-reduce per stage, the single-process model bit for bit."""
+    path, per_stage, xg, units, got, pr, gpr = _run_dp_stage(3, "try", env={"HFENS_XGMI_PROBE_CORRUPT": "1"},
+                                                             probes=True)
+    assert len(pr) == 1 and not pr[0]["ok"] and any(m.startswith("rank 1:") for m in pr[0]["mismatches"]), pr
+    assert path == "stage" and per_stage == 1.0 and xg == 0.0
+    _check_dp_stage_equal(dev, got)
+
+
+def test_stage_graph_probe_mismatch_runs_eagerly(dev):
+    """The stage-graph probe disagrees on one rank (HFENS_GBDT_GRAPH_PROBE_CORRUPT): every rank runs
+    the stage loop eagerly (no replayed units) on the still-valid peer kernel, bit for bit."""
+    path, per_stage, xg, units, got, pr, gpr = _run_dp_stage(2, "1", env={"HFENS_GBDT_GRAPH_PROBE_CORRUPT": "1"},
+                                                             probes=True)
+    assert pr and pr[0]["ok"]
+    assert gpr and not gpr[0]["ok"] and gpr[0]["mismatches"], gpr
+    assert units == 0 and per_stage == 0.0 and xg == 1.0
+    _check_dp_stage_equal(dev, got)
 
 
 def test_gbdt_stage_xgmi_mapping_failure_falls_back(dev):
