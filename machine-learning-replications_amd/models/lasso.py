@@ -64,6 +64,16 @@ def _cd_path_host(G, q, yy, n, alphas, max_iter, tol):
 
 
 SPECULATIVE_REFIT = os.environ.get("HFENS_LASSO_SPEC_REFIT", "1") != "0"
+# Speculative selection (device path): the CV paths run on a stream of their own, and beside them one
+# cold-start solve on all rows at the grid's SMALLEST alpha — the refit the CV choice makes whenever
+# the least-regularised model wins (on the Table S1-shaped cohorts it does: best = last of 100 alphas
+# on three draws).  Its coefficients (``coef_spec_dev_``, event ``spec_ev_``) are ready long before the
+# CV paths end, so a caller's overlap can start work on the selection they imply (the stacking
+# trainer's SVC batch) while the paths still run; the caller checks the speculation against the real
+# selection afterwards and redoes the work on a miss.  The CV-side results are computed after the
+# overlap, so nothing the overlap enqueues waits behind the paths.
+SPECULATE = os.environ.get("HFENS_LASSO_SPECULATE", "1") != "0"
+SPEC_ALPHA_INDEX = -1     # the grid point speculated on (tests move it to force a miss)
 
 
 class LassoCV(Estimator):
@@ -144,6 +154,19 @@ class LassoCV(Estimator):
         grid = grid.to(dev)
         A = int(grid.numel())
         refit_all = None
+        self.coef_spec_dev_ = self.spec_ev_ = None
+        spec = dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and SPECULATE and group is None
+        if spec:
+            from .. import runtime
+            main = torch.cuda.current_stream(dev)
+            sst = runtime.stream(dev, "lasso_spec", priority=-1)
+            sst.wait_stream(main)
+            with torch.cuda.stream(sst):
+                # (the same kernel on the same inputs as refit_all's last problem: bit-identical)
+                a = SPEC_ALPHA_INDEX % A
+                self.coef_spec_dev_ = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[a:a + 1][None])[0, 0]
+                self.spec_ev_ = torch.cuda.Event()
+                self.spec_ev_.record(sst)
         if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT:
             # the refit at the CV-chosen alpha is a cold-start solve on all rows (sklearn's
             # Lasso(alpha=best).fit); which alpha wins is known only after the CV paths, so solve the
@@ -162,8 +185,26 @@ class LassoCV(Estimator):
                 ev.record(side)
         from ..utils.timing import dmark
         dmark("lasso_cv_in")
-        coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
-        dmark("lasso_cv_path")
+        if spec:
+            # the CV paths on a stream of their own: work the overlap enqueues on the caller's stream
+            # does not queue behind them (joined before the MSE below, after the overlap)
+            pst = runtime.stream(dev, "lasso_path")
+            pst.wait_stream(main)
+            with torch.cuda.stream(pst):
+                coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+                dmark("lasso_cv_path")
+                path_ev = torch.cuda.Event()
+                path_ev.record(pst)
+            for t in (G, q, yy, cnt, grid):
+                t.record_stream(pst)
+            coefs.record_stream(main)
+            if overlap is not None:
+                overlap()
+                overlap = None
+            main.wait_event(path_ev)
+        else:
+            coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+            dmark("lasso_cv_path")
         # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
         inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
         # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
@@ -229,7 +270,15 @@ class SelectFromModel(Estimator):
             if (self.max_features is not None and isinstance(self.threshold, float)
                     and np.isneginf(self.threshold)):
                 def overlap():
-                    cd = getattr(self.estimator, "coef_dev_", None)
+                    est = self.estimator
+                    cd = getattr(est, "coef_spec_dev_", None)
+                    self.cols_speculative_ = cd is not None
+                    if cd is not None:
+                        # speculative: the selection of the smallest-alpha refit (LassoCV.SPECULATE),
+                        # checked against the real selection by whoever uses it
+                        torch.cuda.current_stream(cd.device).wait_event(est.spec_ev_)
+                    else:
+                        cd = getattr(est, "coef_dev_", None)
                     if cd is not None:
                         self.cols_dev_ = self._device_columns(cd, int(cd.shape[0]))
                     user()

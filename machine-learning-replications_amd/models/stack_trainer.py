@@ -482,9 +482,15 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
         # the SVC batch was enqueued from the device column selection (prelaunch_svc): it is this
         # fit's only if the host's selection agrees (it always should: same rule, same numbers)
         cols = plan.get("cols")
+        LAST_PRELAUNCH["speculative"] = bool(pre.get("speculative"))
         if cols is None or not np.array_equal(pre["cols_dev"].cpu().numpy(), np.asarray(cols, dtype=np.int64)):
-            import warnings
-            warnings.warn("device column selection differs from the host's; relaunching the SVC batch")
+            if pre.get("speculative"):
+                # the CV chose another alpha than the speculated one, with another selection: the
+                # batch enqueued on the speculated columns is discarded and the SVC fit redone
+                LAST_PRELAUNCH["spec_miss"] = LAST_PRELAUNCH.get("spec_miss", 0) + 1
+            else:
+                import warnings
+                warnings.warn("device column selection differs from the host's; relaunching the SVC batch")
             pre = None
     LAST_PRELAUNCH["used"] = pre is not None
     if pre is not None:

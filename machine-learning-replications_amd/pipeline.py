@@ -173,13 +173,22 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 overlap = plan_ahead(y_dev)
     fit_group = None if task else group
     sel = build_selector(cfg)
+    if overlap is not None and group is None:
+        # the label-only stacking plan now, on the host, while the device imputes (LassoCV's
+        # prelude reads wait for the imputation anyway): it is ready before the LassoCV path is
+        # launched, so the SVC batch can be enqueued first thing under the path
+        overlap()
+        hmark("plan_ready")
+        overlap, planned = None, True
+    else:
+        planned = False
     with timer.stage("select"):
         jobs = []
+        held_out = None
         if run_sel is not None:
             def held_out():
                 run_sel()
                 hmark("heldout_impute_enqueued")
-            jobs.append(held_out)
         if overlap is not None:
             jobs.append(overlap)
         if bins_job is not None:
@@ -187,15 +196,20 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 plan_box["bins_all"] = bins_job()
                 hmark("bins_ahead")
             jobs.append(bins)
-        if group is None and dev.type == "cuda" and overlap is not None:
+        if group is None and dev.type == "cuda" and (overlap is not None or planned):
             def svc_early():
                 # the stacking fit's SVC batch, enqueued from the selector's DEVICE column list
-                # while the LassoCV path runs (stack_trainer.prelaunch_svc)
+                # (speculative: lasso.SPECULATE) while the LassoCV path runs (stack_trainer.prelaunch_svc)
                 cols = getattr(sel, "cols_dev_", None)
                 if cols is not None and plan_box.get("plan") is not None:
                     from .models.stack_trainer import prelaunch_svc
-                    plan_box["prelaunch"] = prelaunch_svc(clf, X_dev, cols, y_dev, plan_box["plan"])
+                    pre = prelaunch_svc(clf, X_dev, cols, y_dev, plan_box["plan"])
+                    if pre is not None:
+                        pre["speculative"] = bool(getattr(sel, "cols_speculative_", False))
+                    plan_box["prelaunch"] = pre
             jobs.append(svc_early)
+        if held_out is not None:
+            jobs.append(held_out)     # (after the SVC batch: the held-out rows are needed last)
         lasso_overlap = None
         if jobs:
             def lasso_overlap():
@@ -221,6 +235,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
     clf.fit(X_dev_optm, y_dev, timer=timer, group=fit_group, svc_group=group if task else None,
             plan=plan)
     dmark("stack_fit")
+    hmark("stack_fit")
     if aux is not None:
         # join the side stream while the imputer and X_sel are alive (their blocks are not reused
         # by the main stream before this point)
@@ -244,6 +259,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         # (the held-out rows are already gathered for the report, so the AUROC comes from them;
         # metrics.roc_auc_sharded is the R8 path for callers that keep scores sharded)
         scores = metrics.evaluate(ysel_all, proba_all)
+    hmark("develop_end")
     dmarks_flush()
     n_train = X_dev.shape[0]
     if fit_group is not None:

@@ -16,6 +16,8 @@ run base
 run graph HFENS_SVM_WS_GRAPH=all
 run graph_r6 HFENS_SVM_WS_GRAPH=all HFENS_SVM_CASCADE_ROUNDS=6
 run graph_p1250 HFENS_SVM_WS_GRAPH=all HFENS_SVM_CASCADE_PART=1250
+run graph_q512 HFENS_SVM_WS_GRAPH=all HFENS_SVM_WS_Q=512
+run graph_q512_f3 HFENS_SVM_WS_GRAPH=all HFENS_SVM_WS_Q=512 HFENS_SVM_WS_FRAC=0.3
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]);print('bench', d['ms_per_step'], d['diag']['step_ms_min_med_max'], d['auroc'])"
 HFENS_SVM_WS_GRAPH=all timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_graph.json 2> $O/bench_graph.err || { echo "bench failed"; tail -5 $O/bench_graph.err; exit 1; }

@@ -892,3 +892,37 @@ def test_prelaunched_svc_batch_matches(dev, monkeypatch):
     d = float((out[False].proba_sel - out[True].proba_sel).abs().max())
     assert d <= 2e-3, d
     assert abs(out[False].scores["auroc"] - out[True].scores["auroc"]) <= 2e-3
+
+
+def test_lasso_speculation_hit_and_miss(dev, monkeypatch):
+    """The speculative selection (lasso.SPECULATE: the smallest-alpha refit's columns, the SVC batch
+    enqueued on them while the CV paths run).  Hit: the selection, α and model equal the
+    non-speculative prelaunch (same device-γ batch on the same columns).  Forced miss (speculating on
+    the LARGEST alpha): the batch is discarded and redone on the real selection, quietly, giving the
+    non-prelaunched fit."""
+    from hfens import pipeline
+    from hfens.models import lasso, stack_trainer
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+
+    def run(spec, idx=-1, pre=True):
+        monkeypatch.setattr(lasso, "SPECULATE", spec)
+        monkeypatch.setattr(lasso, "SPEC_ALPHA_INDEX", idx)
+        monkeypatch.setattr(stack_trainer, "PRELAUNCH_SVC", pre)
+        stack_trainer.LAST_PRELAUNCH.clear()
+        r = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+        return r, dict(stack_trainer.LAST_PRELAUNCH)
+    base, lp0 = run(False)
+    hit, lp1 = run(True)
+    assert lp0["used"] and lp1["used"] and lp1["speculative"] and not lp1.get("spec_miss")
+    assert np.array_equal(base.selected, hit.selected)
+    assert torch.equal(base.proba_sel, hit.proba_sel)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")        # a speculation miss is not a warning
+        miss, lp2 = run(True, idx=0)
+    assert lp2.get("spec_miss") == 1 and not lp2["used"]
+    nopre, _ = run(False, pre=False)
+    assert np.array_equal(miss.selected, nopre.selected)
+    assert torch.equal(miss.proba_sel, nopre.proba_sel)
