@@ -643,6 +643,8 @@ def validate_stage_graph(group, dev, peer) -> bool:
     W, me = dist.get_world_size(group), dist.get_rank(group)
     E = ops.ext()
     m, reps = 3 * 1024 + 5, 2
+    if peer is not None:
+        m = min(m, int(peer.cap))     # (one stage slot of the group's peer buffers)
     lib_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
     buf = torch.zeros(3 * m, dtype=torch.int64, device=dev)
     tdev = torch.zeros(1, dtype=torch.int32, device=dev)

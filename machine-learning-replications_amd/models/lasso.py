@@ -165,6 +165,8 @@ class LassoCV(Estimator):
                 # (the same kernel on the same inputs as refit_all's last problem: bit-identical)
                 a = SPEC_ALPHA_INDEX % A
                 self.coef_spec_dev_ = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[a:a + 1][None])[0, 0]
+                from ..utils.timing import dmark
+                dmark("lasso_spec")
                 self.spec_ev_ = torch.cuda.Event()
                 self.spec_ev_.record(sst)
         if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT:

@@ -1294,6 +1294,11 @@ class _GammaDev:
         self.ngl = torch.empty(K, dtype=torch.float32, device=device)
         ops.ext().svm_gamma(Zc.data_ptr(), self.offs.data_ptr(), K, F, self.gam.data_ptr(), self.ngl.data_ptr(),
                             ops.stream_ptr(device))
+        # read back right behind its kernel (pinned + event): resolve() waits for γ, not for the SMO
+        self.host = torch.empty(K, dtype=torch.float64, pin_memory=True)
+        self.host.copy_(self.gam, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
         self.keep = [Zc]
 
     def patch(self, ddev: torch.Tensor, dtype: np.dtype, field: str, fits) -> None:
@@ -1304,8 +1309,9 @@ class _GammaDev:
         self.keep.append(fo)
 
     def resolve(self, all_probs, meta) -> None:
-        """The host's γ (models, host mirrors): one small read, after the SMO."""
-        g = self.gam.cpu().numpy()
+        """The host's γ (models, host mirrors): one small read, queued when γ was computed."""
+        self.ev.synchronize()
+        g = self.host.numpy().copy()
         if not np.isfinite(g).all():
             from ..utils.guards import NonFiniteError
             raise NonFiniteError("SVC.fit X: non-finite scaled value(s)")
@@ -1473,7 +1479,14 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         E.platt_batch(pdev.data_ptr(), len(pl), part_p, S, rowk_p, rho_p, cdev.data_ptr(), srcmap.data_ptr(),
                       dscr.data_ptr(), ABt.data_ptr(), ops.stream_ptr(device))
         dmark("svc_platt")
+        # the pairs' read-back queued right behind the Platt kernel (pinned, with an event): the host
+        # waits for the Platt fits only, not for whatever is enqueued on this stream after them
+        ab_host = torch.empty(ABt.shape, dtype=torch.float64, pin_memory=True)
+        ab_host.copy_(ABt, non_blocking=True)
+        ab_ev = torch.cuda.Event()
+        ab_ev.record()
         return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
+                    ab_host=(ab_host, ab_ev),
                     keep=(pdev, srcmap, cdev, dscr), device=device, args=args, solver=solver, gamma_dev=gdev)
     for f in pl:
         svc, Z, mt = svcs[f], Zs[f], meta[f]
@@ -1640,8 +1653,13 @@ def finish_svc_batch(st: dict, defer=None):
     def read_ab():
         if st["ABt"] is None:
             return
-        ABc = (st["ABt"].to(torch.float64).cpu().numpy() if early is not None
-               else host[nl + 2 * len(svcs):])
+        if early is not None and st.get("ab_host") is not None:
+            st["ab_host"][1].synchronize()
+            ABc = st["ab_host"][0].numpy()
+        elif early is not None:
+            ABc = st["ABt"].to(torch.float64).cpu().numpy()
+        else:
+            ABc = host[nl + 2 * len(svcs):]
         if not np.isfinite(ABc).all():
             from ..utils.guards import NonFiniteError
             raise NonFiniteError(f"SVC Platt sigmoid (A, B): {int((~np.isfinite(ABc)).sum())} non-finite value(s)")

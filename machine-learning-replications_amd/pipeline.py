@@ -35,6 +35,7 @@ DP_POLICY = os.environ.get("HFENS_DP_POLICY", "auto")
 TASK_MAX_ROWS = int(os.environ.get("HFENS_TASK_MAX_ROWS", str(1 << 18)))
 AUX_STREAM = os.environ.get("HFENS_AUX_STREAM", "1") != "0"   # held-out imputation on a side stream
 PLAN_AHEAD = os.environ.get("HFENS_PLAN_AHEAD", "1") != "0"   # stacking bookkeeping under the LassoCV path
+PLAN_THREAD = os.environ.get("HFENS_PLAN_THREAD", "1") != "0"  # … computed on a host thread of its own
 # the GBC's bin map of every candidate column fitted on the host under the LassoCV path (the selected
 # columns' bins are then a slice: binning.BinMapper.select), from one non-blocking copy of the imputed rows
 # (default off: the GBC's host bin fit runs while the device solves the SVC, off the critical path)
@@ -132,10 +133,33 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         y_ev = torch.cuda.Event()
         y_ev.record()
 
+        box = {}
+
+        def work():
+            try:
+                from .models.stack_trainer import plan_stacking
+                y_ev.synchronize()
+                box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
+            except BaseException as e:   # re-raised by run() on the calling thread
+                box["err"] = e
+
+        if PLAN_THREAD:
+            # on a host thread of its own: it runs while this thread waits on the device (the
+            # imputation, LassoCV's prelude reads), not after
+            import threading
+            th = threading.Thread(target=work, name="hfens-plan", daemon=True)
+            th.start()
+        else:
+            th = None
+
         def run():
-            from .models.stack_trainer import plan_stacking
-            y_ev.synchronize()
-            plan_box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
+            if th is not None:
+                th.join()
+            else:
+                work()
+            if "err" in box:
+                raise box["err"]
+            plan_box["plan"] = box["plan"]
         return run
 
     if group is None and dev.type == "cuda" and PLAN_AHEAD:
@@ -173,15 +197,17 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 overlap = plan_ahead(y_dev)
     fit_group = None if task else group
     sel = build_selector(cfg)
-    if overlap is not None and group is None:
+    planned = False
+    if overlap is not None and group is None and not PLAN_THREAD:
         # the label-only stacking plan now, on the host, while the device imputes (LassoCV's
         # prelude reads wait for the imputation anyway): it is ready before the LassoCV path is
         # launched, so the SVC batch can be enqueued first thing under the path
         overlap()
         hmark("plan_ready")
         overlap, planned = None, True
-    else:
-        planned = False
+    elif overlap is not None and group is None:
+        # (PLAN_THREAD: joined as the first job under the LassoCV path)
+        planned = True
     with timer.stage("select"):
         jobs = []
         held_out = None
