@@ -1092,12 +1092,16 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   const int t_last = Persist ? T + 1 : t_first;
   const size_t slot_m = 3 * (size_t)J.hist_len + kSgExtra;
   const size_t slot_sz = (size_t)B * slot_m;
+  // the features' bin counts: one load per thread, in parallel (a serial loop of dependent global
+  // loads in thread 0 cost several µs per launch)
+  if (tid < F) s_nb[tid] = J.nbins[tid];
+  __syncthreads();
   if (tid == 0) {
     int o = 0;
     n_bin = n_one = n_mid = n_wide = 0;
     for (int f = 0; f < F; ++f) {
-      const int nb = J.nbins[f];
-      s_nb[f] = nb; s_off[f] = o; o += nb;
+      const int nb = s_nb[f];
+      s_off[f] = o; o += nb;
       if (nb == 2) l_bin[n_bin++] = f;
       else if (nb <= 1) l_one[n_one++] = f;
       else if (nb <= 8) l_mid[n_mid++] = f;
@@ -1322,9 +1326,15 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
       for (int k = tid; k < n_mb * 32 * 32; k += kT) Tsl[k] = 0;
   }
   if (w0r < w1r) load_bins(w0r, pf);   // (its weights / raw / labels were issued before the split)
+  // MF: the matrix-core slice sums stay in registers across the tile's sub-tiles (exact int32: at
+  // most 127 per row per slice) and are folded into the LDS table once, after the last sub-tile
+  sg_v16i acc_all[MF ? 4 : 1];
+#pragma unroll
+  for (int mb = 0; mb < (MF ? 4 : 1); ++mb) acc_all[mb] = sg_v16i{};
   for (int r0 = w0r; r0 < w1r; r0 += kSgTile) {
     const int m = min(kSgTile, w1r - r0);
     __syncthreads();   // the previous sub-tile's histogram passes are done with the row cache
+    const long long t_ap = pst ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
       const int k = tid + u * kT;
@@ -1377,9 +1387,10 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
     }
     if (!has_cur) continue;
     for (int k = m + tid; k < kSgTile; k += kT) { qg[sg_ri(k)] = 0; qh[sg_ri(k)] = 0; qw[sg_ri(k)] = 0; }
+    if (pst && tid == 0) pst[1] += (long long)__builtin_amdgcn_s_memtime() - t_ap;   // wave 0's apply, summed
     __syncthreads();
-    if (pst && tid == 0 && r0 == w0r) pst[1] = (long long)__builtin_amdgcn_s_memtime() - t_0;
     if constexpr (MF) {
+      const long long t_a = pst ? (long long)__builtin_amdgcn_s_memtime() : 0;
       // (a) binary / ≤ 8-bin features on the matrix cores: wave w takes rows [128w, 128w + 128) of
       // the sub-tile in 4 K-steps of 32; lane (c = lane & 31, h = lane >> 5) holds, for the 16 rows
       // 16h … 16h + 15 of the step, slice c % 7 of value c / 7 (B, c < 21) and the indicator bytes
@@ -1389,9 +1400,7 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
       const int vsel = c / kSgSlices, ks = c - kSgSlices * vsel;
       const long long* qv = vsel == 0 ? qg : (vsel == 1 ? qh : qw);
       const int nmb = n_mb;
-      sg_v16i acc[4];
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) acc[mb] = sg_v16i{};
+      sg_v16i (&acc)[4] = acc_all;
       // A bytes of every M-block, one K-step ahead (the global loads overlap the B build and MFMAs)
       const unsigned char* arow[4];
 #pragma unroll
@@ -1444,36 +1453,41 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
           araw[mb] = anext[mb];
         }
       }
-      // fold this wave's 32×32 slice sums into the workgroup table (D: col = lane & 31,
-      // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+      const long long t_b = pst ? (long long)__builtin_amdgcn_s_memtime() : 0;
+      if (pst && tid == 0) pst[4] += t_b - t_a;   // (diagnostics: wave 0's MFMA part, summed over sub-tiles)
+      // (b) wider features: LDS int64 atomics (integer sums: any order is exact).  Every wave takes
+      // its own RPW-row slice of the sub-tile for ALL wide features (lane ℓ: RPW/64 consecutive
+      // rows), so all waves share the work whatever the number of wide features
+      {
+        constexpr int RL = RPW / 64;            // rows per lane (2 at 512 threads)
+        static_assert(RL == 1 || RL == 2 || RL == 4, "the wide-feature pass reads 1, 2 or 4 bin bytes per lane");
+        const int kb = RPW * wave + RL * lane;   // first row of this lane in the sub-tile
+        long long wq2[RL], gq2[RL], hq2[RL];
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        if (mb >= nmb) continue;
+        for (int j = 0; j < RL; ++j) {
+          const int ri = sg_ri(kb + j);
+          wq2[j] = qw[ri]; gq2[j] = qg[ri]; hq2[j] = qh[ri];
+        }
+        const unsigned char* bt = J.bins + r0 + kb;
+        for (int fi = 0; fi < n_wide; ++fi) {
+          const int f = l_wide[fi], off = s_off[f];
+          const unsigned char* bf_ = bt + (size_t)f * J.ldb;
+          unsigned v2;
+          if constexpr (RL == 4) v2 = *reinterpret_cast<const unsigned*>(bf_);
+          else if constexpr (RL == 2) v2 = *reinterpret_cast<const unsigned short*>(bf_);
+          else v2 = *bf_;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const int v = acc[mb][r];
-          if (v != 0) atomicAdd(&Tsl[(mb * 32 + row) * 32 + c], v);
+          for (int j = 0; j < RL; ++j) {
+            if (wq2[j] == 0) continue;
+            const unsigned bb = (v2 >> (8 * j)) & 0xFFu;
+            long long* cell = hl + ((size_t)off + bb) * 3;
+            atomicAdd((unsigned long long*)&cell[0], (unsigned long long)gq2[j]);
+            atomicAdd((unsigned long long*)&cell[1], (unsigned long long)hq2[j]);
+            atomicAdd((unsigned long long*)&cell[2], (unsigned long long)wq2[j]);
+          }
         }
       }
-      // (b) wider features: LDS int64 atomics, lane ℓ owns rows 16ℓ … 16ℓ+15, features split over waves
-      const unsigned char* bt = J.bins + r0 + 16 * lane;
-      for (int fi = wave; fi < n_wide; fi += kW) {
-        const int f = l_wide[fi], off = s_off[f];
-        const uint4 v4 = *reinterpret_cast<const uint4*>(bt + (size_t)f * J.ldb);
-        const unsigned wd[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int ri = 17 * lane + j;   // sg_ri(16·lane + j)
-          const long long wq = qw[ri];
-          if (wq == 0) continue;
-          const unsigned bb = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-          long long* cell = hl + ((size_t)off + bb) * 3;
-          atomicAdd((unsigned long long*)&cell[0], (unsigned long long)qg[ri]);
-          atomicAdd((unsigned long long*)&cell[1], (unsigned long long)qh[ri]);
-          atomicAdd((unsigned long long*)&cell[2], (unsigned long long)wq);
-        }
-      }
+      if (pst && tid == 0) pst[5] += (long long)__builtin_amdgcn_s_memtime() - t_b;   // wave 0's wide part
     } else {
       // stage-t histogram of the sub-tile.  Every wave covers ALL 1024 rows (lane ℓ owns rows
       // 16ℓ … 16ℓ+15, their quantised g/h/w in registers) and takes features f ≡ wave (mod 8): one
@@ -1564,6 +1578,19 @@ __global__ __launch_bounds__(NT) void gbdt_stump_stage_kernel(StageJob J) {
   }
   if constexpr (MF) {
     if (has_cur) {
+      // fold each wave's 32×32 slice sums into the workgroup table (D: col = lane & 31,
+      // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) — once per stage
+      const int c = lane & 31, hh = lane >> 5;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        if (mb >= n_mb) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int v = acc_all[mb][r];
+          if (v != 0) atomicAdd(&Tsl[(mb * 32 + row) * 32 + c], v);
+        }
+      }
       // slice sums → int64 bins: bin c ≥ 1 of an MFMA feature is its indicator row, bin 0 the node
       // total (all-ones row) minus the others; constant features get the total
       __syncthreads();
