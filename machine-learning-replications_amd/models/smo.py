@@ -1037,6 +1037,8 @@ CASCADE_MIN = int(os.environ.get("HFENS_SVM_CASCADE_MIN", "4096"))
 CASCADE_PART = int(os.environ.get("HFENS_SVM_CASCADE_PART", "1600"))
 CASCADE_EPS = float(os.environ.get("HFENS_SVM_CASCADE_EPS", "0.1"))
 CASCADE_Q = int(os.environ.get("HFENS_SVM_CASCADE_Q", "512"))
+# also seed the K-cached solver (problems past 16k points: candidate-list rounds of q = 256)
+CASCADE_KC = os.environ.get("HFENS_SVM_CASCADE_KC", "1") != "0"
 # working-set rounds the parts get (a fixed budget: every round is enqueued ahead without a host
 # check, so rounds past the parts' convergence are launches the full solve waits on; a part stopped
 # by the budget is still feasible and still seeds)
@@ -1123,7 +1125,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     solve = _solve_ws if solver == "ws" else _solve_exact
     if group is None:
         kw = {}
-        if solver == "ws" and CASCADE and not ws_kc(F, max_l):
+        if solver == "ws" and CASCADE and (CASCADE_KC or not ws_kc(F, max_l)):
             seed = _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap)
             if seed is not None:
                 kw["seed"] = seed
@@ -1136,7 +1138,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
             for p in sub:
                 so.append(so[-1] + p.l)
             kw = {}
-            if solver == "ws" and CASCADE and not ws_kc(F, max(p.l for p in sub)):
+            if solver == "ws" and CASCADE and (CASCADE_KC or not ws_kc(F, max(p.l for p in sub))):
                 seed = _cascade_seed(E, sub, zsub, so, F, device, s, max_iter_cap)
                 if seed is not None:
                     kw["seed"] = seed

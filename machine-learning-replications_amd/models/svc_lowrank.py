@@ -351,7 +351,8 @@ def ipm_svc_dual(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: 
     # on the GPU the r × r factor / solves are the native single-workgroup kernels (ops/csrc/
     # linalg.hip: equilibration and jitter retries on the device, no library workspace, no host
     # read of `info`); the host path keeps torch.linalg
-    native = Phi.is_cuda and ops.has_ext()
+    # (the native factor holds r ≤ 1024; larger landmark sets take the library factor on the device)
+    native = Phi.is_cuda and ops.has_ext() and r <= 1024
     if native:
         E = ops.ext()
         Lc = torch.empty(r, r, dtype=dt, device=Phi.device)

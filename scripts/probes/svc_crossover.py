@@ -27,8 +27,15 @@ for rows in [int(a) for a in sys.argv[1:]] or [40000]:
     Zt = torch.as_tensor((Xt - mu) / sd, device=dev)
     yd = torch.as_tensor(y, device=dev)
     dec = {}
-    for solver in ("ws", "lowrank"):
-        smo.SOLVER = solver
+    from hfens.models import svc_lowrank
+    solvers = os.environ.get("SOLVERS", "ws,lowrank").split(",")
+    for solver in solvers:
+        # ws = exact working set (cascade-seeded), ws_cold = exact without the seed,
+        # lowrankN = Nyström + IPM with N landmarks (lowrank = the default count)
+        smo.SOLVER = "ws" if solver.startswith("ws") else "lowrank"
+        smo.CASCADE = solver != "ws_cold"
+        if solver.startswith("lowrank") and solver != "lowrank":
+            svc_lowrank.N_LANDMARKS = int(solver[7:])
         for rep in range(2):   # second fit timed (first: allocations, code objects)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -40,11 +47,13 @@ for rows in [int(a) for a in sys.argv[1:]] or [40000]:
         dec[solver] = d
         out = dict(rows=rows, solver=solver, fit_s=round(dt, 3),
                    auroc=round(float(metrics.evaluate(torch.as_tensor(yt), torch.as_tensor(p))["auroc"]), 5))
-        if solver == "ws":
+        if solver.startswith("ws"):
             st = smo.LAST_WS_STATS
             out.update(rounds_max=int(st["outer"].max()), pairs_max=int(st["inner"].max()),
                        gap_max=float(st["gap"].max()))
         print(json.dumps(out), flush=True)
-    c = np.corrcoef(dec["ws"], dec["lowrank"])[0, 1]
-    print(json.dumps(dict(rows=rows, decision_corr=round(float(c), 6),
-                          max_abs_diff=round(float(np.abs(dec["ws"] - dec["lowrank"]).max()), 5))), flush=True)
+    ref = solvers[0]
+    for other in solvers[1:]:
+        c = np.corrcoef(dec[ref], dec[other])[0, 1]
+        print(json.dumps(dict(rows=rows, ref=ref, other=other, decision_corr=round(float(c), 6),
+                              max_abs_diff=round(float(np.abs(dec[ref] - dec[other]).max()), 5))), flush=True)

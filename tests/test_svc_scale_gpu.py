@@ -45,3 +45,29 @@ def test_exact_ws_vs_lowrank_40k(dev, monkeypatch):
     assert abs(out["ws"][1] - out["lowrank"][1]) <= 0.012, (out["ws"][1], out["lowrank"][1])
     assert min(out["ws"][1], out["lowrank"][1]) >= 0.85
     assert np.corrcoef(out["ws"][0], out["lowrank"][0])[0, 1] >= 0.93
+
+
+def test_nystrom_pinned_where_it_runs_200k(dev, monkeypatch):
+    """the Nyström substitute pinned at a size where the default actually takes it
+    (200k points > smo.EXACT_MAX_POINTS), against the exact working-set solve of the same fit.
+    Bounds from the round-5 record (profiles/r5_nystrom.md, 512 landmarks): decision correlation
+    0.923, |ΔAUROC| 0.010 at 200k (0.915 / 0.012 at 300k)."""
+    X, y = _draw(200000, 200)
+    Xt, yt = _draw(20000, 201)
+    mu, sd = X.mean(0), X.std(0)
+    sd = np.where(sd > 0, sd, 1.0)
+    Z = torch.as_tensor((X - mu) / sd, device=dev)
+    Zt = torch.as_tensor((Xt - mu) / sd, device=dev)
+    yd = torch.as_tensor(y, device=dev)
+    assert 200000 > smo.EXACT_MAX_POINTS and smo.use_lowrank([200000], 17, "cuda")
+    out = {}
+    for solver in ("ws", "lowrank"):
+        monkeypatch.setattr(smo, "SOLVER", solver)
+        m = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, yd)
+        if solver == "ws":
+            assert (smo.LAST_WS_STATS["gap"] < 1e-3 + 1e-5).all()
+        d = m.decision_function(Zt).double().cpu().numpy()
+        p = m.predict_proba(Zt)[:, 1].double().cpu()
+        out[solver] = (d, metrics.evaluate(torch.as_tensor(yt), p)["auroc"])
+    assert abs(out["ws"][1] - out["lowrank"][1]) <= 0.015, (out["ws"][1], out["lowrank"][1])
+    assert np.corrcoef(out["ws"][0], out["lowrank"][0])[0, 1] >= 0.90
