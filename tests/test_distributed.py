@@ -559,3 +559,43 @@ def test_seed_layout_cost_model():
     assert ensemble.my_seeds(4, 8, 5, 4) == [1, 3] and ensemble.my_seeds(3, 8, 5, 4) == [0, 2, 4]
     with pytest.raises(ValueError):
         ensemble.seed_layout(8, 5, 1000, "3")
+
+
+def _ipm_batched(rank, world, group):
+    """Three row-sharded interior-point problems (different sizes): solved one after another
+    (ipm_svc_dual, a collective per reduction of each) and in lock-step (_drive, one collective per
+    reduction step for all of them)."""
+    from hfens.models import svc_lowrank as sl
+    g = torch.Generator().manual_seed(5)
+    probs = []
+    for l in (900, 700, 500):
+        Phi = torch.randn(l, 24, generator=g, dtype=torch.float64) / 4
+        y = torch.where(torch.rand(l, generator=g) < 0.3, 1.0, -1.0).to(torch.float64)
+        c = torch.where(y > 0, 1.7, 0.6).to(torch.float64)
+        lo, hi = rank * l // world, (rank + 1) * l // world
+        probs.append((Phi[lo:hi].contiguous(), y[lo:hi].contiguous(), c[lo:hi].contiguous()))
+    sl._Red.STATS.update(rccl=0, peer=0)
+    single = [sl.ipm_svc_dual(P, y, c, group=group) for P, y, c in probs]
+    n_single = sl._Red.STATS["rccl"]
+    sl._Red.STATS.update(rccl=0, peer=0)
+    batched = sl._drive([sl._ipm_gen(P, y, c) for P, y, c in probs], sl._Red(group))
+    n_batch = sl._Red.STATS["rccl"]
+    da = max(float((a1 - a2).abs().max()) for (a1, _, _), (a2, _, _) in zip(single, batched))
+    drho = max(abs(r1 - r2) for (_, r1, _), (_, r2, _) in zip(single, batched))
+    t = torch.tensor([da, drho], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    iters = [it for _, _, it in single]
+    assert iters == [it for _, _, it in batched]
+    return float(t[0]), float(t[1]), n_single, n_batch, iters
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_batched_ipm_one_collective_per_step(world):
+    """the row-sharded interior points of one SVC fit run in lock-step from one host
+    thread (svc_lowrank._drive) — the same iterates as solving them one after another (≤ 1e-8; the
+    reductions are the same sums, merged into one buffer), with the collectives per iteration
+    counted per FIT (≤ 17 + the 3 setup reductions), not per problem."""
+    da, drho, n_single, n_batch, iters = _run("_ipm_batched", world)
+    assert da <= 1e-8 and drho <= 1e-8, (da, drho)
+    assert n_batch <= 17 * max(iters) + 3, (n_batch, iters)
+    assert n_single >= 2 * n_batch, (n_single, n_batch)
