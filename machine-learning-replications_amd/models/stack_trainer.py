@@ -339,11 +339,16 @@ def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Te
             and len(kinds) > len(svc_cols) and plan.get("svc_pre") and all(i in plan["svc_pre"] for i in svc_cols)):
         return None
     from .. import runtime
-    from .smo import launch_svc_batch, enqueue_svc_oof
+    from .smo import launch_svc_batch, enqueue_svc_oof, use_lowrank
     dev = X_full.device
     n = int(X_full.shape[0])
     y_np, folds_np, rows_host = plan["y_np"], plan["folds_np"], plan["rows_host"]
     if int(y_np.shape[0]) != n:
+        return None
+    if use_lowrank([len(r) for r in rows_host], int(cols_dev.shape[0]), "cuda"):
+        # the Nyström interior point is driven from the host (a synchronisation per iteration):
+        # launched here it would hold this thread for the whole solve instead of running beside
+        # the GBC / LR fits, as it does from the stacking trainer's streams
         return None
     main = torch.cuda.current_stream(dev)
     side = runtime.stream(dev, "svc", priority=-1)
