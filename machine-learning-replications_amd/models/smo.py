@@ -170,11 +170,13 @@ def plan_svc_problems(svc, y_fits) -> Optional[list]:
     pre = []
     for f, yh in enumerate(y_fits):
         y_np = np.asarray(yh, dtype=np.float64).reshape(-1)
-        if not np.isin(np.unique(y_np), (0.0, 1.0)).all():
+        if not ((y_np == 0.0) | (y_np == 1.0)).all():
             return None
         probs, mt = _expand(f, y_np, None, _class_weights_host(svc, y_np), svc)
         final = probs[-1]
-        if final.l <= _MAP_MAX:
+        # (the column maps serve the stored-Gram exact solver only; the working-set solver, which
+        # takes every batch from WS_MIN_POINTS points on, never reads them)
+        if final.l <= _MAP_MAX and (SOLVER == "exact" or (SOLVER == "auto" and final.l < WS_MIN_POINTS)):
             inv = np.full(int(final.rows.max()) + 1, -1, dtype=np.int64)
             inv[final.rows] = np.arange(final.l)
             for p in probs[:-1]:
@@ -647,6 +649,9 @@ WS_INNER_FRAC_BIG = float(os.environ.get("HFENS_SVM_WS_FRAC_BIG", str(WS_INNER_F
 # in its next working set)
 WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
+# … for a cascade-seeded batch (the bench's seeded problems need ≤ 24 rounds; every round past a
+# problem's convergence is three no-op launches its group's stream still runs before the finish)
+WS_SEEDED_AHEAD = int(os.environ.get("HFENS_SVM_WS_SEEDED_AHEAD", "48"))
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
 # HIP-graph replay of the rounds: "1" K-cached rounds only, "all" the q = 1024 rounds too, "0" off
@@ -769,7 +774,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         # a batch still unconverged after them reports err and is re-solved synchronously by
         # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
         # group's stream starts within one chunk of host launch time.
-        left = min(WS_KC_ROUNDS_AHEAD if kc_all else WS_ROUNDS_AHEAD, max_outer)
+        ahead = WS_KC_ROUNDS_AHEAD if kc_all else (WS_SEEDED_AHEAD if seed is not None else WS_ROUNDS_AHEAD)
+        left = min(ahead, max_outer)
         chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
         while left > 0:
             k = min(chunk, left)
@@ -1389,7 +1395,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         parts.append(torch.stack([Z.to(f64).var(unbiased=False) for Z in Zs]))
     if pre is not None:
         pass
-    elif y_host is not None and all(np.isin(np.unique(yh), (0.0, 1.0)).all() for yh in y_host):
+    elif y_host is not None and all(((yh == 0.0) | (yh == 1.0)).all() for yh in y_host):
         # host labels: expand the problems now (γ filled in below), overlapping the device work
         pre = []
         for f, (svc, yh) in enumerate(zip(svcs, y_host)):

@@ -101,6 +101,7 @@ def test_ws_unconverged_batch_is_resolved_synchronously(dev, monkeypatch):
     ref = SVC(class_weight="balanced", probability=True, random_state=2020).fit(Z, y.to(dev))
     assert "ws_resolve" not in smo.LAST_SMO_INFO
     monkeypatch.setattr(smo, "WS_ROUNDS_AHEAD", 2)
+    monkeypatch.setattr(smo, "WS_SEEDED_AHEAD", 2)
     monkeypatch.setattr(smo, "WS_KC_ROUNDS_AHEAD", 2)
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
