@@ -276,12 +276,57 @@ def finish_logreg_batch(h: dict):
     return models
 
 
+def logreg_label_prep(models, y: torch.Tensor, n: int, device) -> dict:
+    """The label-only inputs of a single-process fused :func:`launch_logreg_batch` (the labels'
+    guard, ±1 labels, sample weights, penalty mask, intercept column), enqueued on the CURRENT
+    stream — so a caller can compute them while the features are still being produced on another
+    stream (the stacking trainer's meta model, behind the out-of-fold columns)."""
+    from ..utils import guards
+    m0 = models[0]
+    B = len(models)
+    yv = y.to(device=device, dtype=torch.float64)
+    masks = torch.ones(B, n, dtype=torch.bool, device=device)
+    mk = masks.to(torch.float64)
+    if m0.class_weight == "balanced":
+        cnt1 = (mk * yv[None]).sum(1)
+        cnt = torch.stack([mk.sum(1) - cnt1, cnt1], 1)
+        cw = cnt.sum(1, keepdim=True) / (2.0 * cnt)
+        sw = mk * torch.where(yv[None] > 0.5, cw[:, 1:2], cw[:, 0:1])
+    else:
+        sw = mk
+    F1_extra = int(bool(m0.fit_intercept))
+    ones = (torch.full((n, 1), float(m0.intercept_scaling), dtype=torch.float64, device=device)
+            if m0.fit_intercept else None)
+    return dict(n=n, yflag=guards.binary_flag(yv), masks=masks, yv=yv, ypm=2.0 * yv - 1.0, s=sw, ones=ones,
+                extra=F1_extra)
+
+
 def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
-                        group=None, max_outer: int = 100, seed_order=None) -> dict:
+                        group=None, max_outer: int = 100, seed_order=None, prep: Optional[dict] = None) -> dict:
     """Fit ``models`` (one per row mask); on the fused device path the solve is only enqueued —
     no host synchronisation until :func:`finish_logreg_batch` (the stacking trainer launches the
-    meta model this way before it reads the SVC's results back)."""
+    meta model this way before it reads the SVC's results back).  ``prep``: the label-only inputs
+    from :func:`logreg_label_prep` (no masks; single process)."""
     m0 = models[0]
+    if prep is not None and masks is None and group is None and X.is_cuda and FUSED and X.dim() == 2 \
+            and int(X.shape[0]) == prep["n"] and X.shape[1] + prep["extra"] <= 64 and m0.penalty in ("l1", "l2") \
+            and not (m0.penalty == "l1" and m0.solver == "liblinear"
+                     and all(getattr(mm, "emulate_liblinear", False) for mm in models)):
+        # only the feature-dependent work remains: the finite guard and the intercept column
+        from ..utils import guards
+        _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
+        X = X.to(torch.float64)
+        flags = torch.stack([guards.finite_flag(X), prep["yflag"]])
+        Xa = torch.cat([X, prep["ones"]], 1) if prep["ones"] is not None else X
+        F1 = Xa.shape[1]
+        l1 = m0.penalty == "l1"
+        penal = torch.ones(F1, dtype=torch.uint8, device=X.device)
+        if not l1 and m0.fit_intercept:
+            penal[-1:].zero_()
+        scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
+        LAST_PATH["path"] = "fused"
+        return dict(models=models, F=int(X.shape[1]), scale=scale, fit_intercept=bool(m0.fit_intercept), dev=X.device,
+                    fused=_launch_fused(Xa, prep["s"], prep["ypm"], penal, float(m0.C), l1, max_outer, flags))
     _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
     if m0.penalty not in ("l1", "l2"):
         raise NotImplementedError("penalty must be 'l1' or 'l2'")

@@ -295,7 +295,12 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
             side.wait_event(cols_ev)
             with torch.cuda.stream(side):
                 early["handle"] = early["launch"]()
-        with torch.cuda.stream(side):
+        # (the refit SVC's bookkeeping stays on the SVC stream: on the caller's stream its wait
+        # for the SMO, pending at the head of an idle queue, slowed the SMO itself — 22.7 vs 19.3
+        # ms / fit; on a new stream the stream → hardware-queue mapping moved and the GBC / LR
+        # stream shared a queue with an SMO group — 20.4 ms)
+        fin = side
+        with torch.cuda.stream(fin):
             for i, (clones, st) in pending.items():
                 if group is None:
                     # with the out-of-fold column already on the device only the refit model is
@@ -532,7 +537,12 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
 
     early = None
     if group is None and EARLY_META:
-        early = {"launch": lambda: launch_logreg_batch([new_final()], meta, y64)}
+        fm = [new_final()]
+        # the meta model's label-only inputs now, on this (otherwise idle) stream: behind the
+        # out-of-fold columns only the features' guard and the intercept column remain
+        from .logreg_solver import logreg_label_prep
+        lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
+        early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
     dev_bases = None
     if group is None and X.is_cuda and DEVICE_BASES:
         dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
