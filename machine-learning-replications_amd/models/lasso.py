@@ -201,6 +201,8 @@ class LassoCV(Estimator):
                 t.record_stream(pst)
             coefs.record_stream(main)
             if overlap is not None:
+                from ..utils.timing import hmark
+                hmark("lasso_launched")
                 overlap()
                 overlap = None
             main.wait_event(path_ev)
@@ -283,6 +285,8 @@ class SelectFromModel(Estimator):
                         cd = getattr(est, "coef_dev_", None)
                     if cd is not None:
                         self.cols_dev_ = self._device_columns(cd, int(cd.shape[0]))
+                    from ..utils.timing import hmark
+                    hmark("cols_dev")
                     user()
             self.estimator_ = self.estimator.fit(X, y, group=group, overlap=overlap)
         else:

@@ -148,6 +148,16 @@ def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=N
         h.update(err=err, xchg=xchg)
     else:
         _launch_single(h)
+    # the error word and guards' read-back queued right behind the solve (pinned + event):
+    # _finish_fused then waits for this solve only
+    parts = ([h["err"]] if h["err"] is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
+    if parts:
+        dv = torch.cat(parts)
+        host = torch.empty(dv.shape, dtype=dv.dtype, pin_memory=True)
+        host.copy_(dv, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        h["staged"] = (host, ev, dv)
     return h
 
 
@@ -164,7 +174,12 @@ def _finish_fused(h):
     from ..utils.timing import hmark
     flags, err = h["flags"], h["err"]
     parts = ([err] if err is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
-    host = torch.cat(parts).cpu().tolist() if parts else []
+    st = h.get("staged")
+    if st is not None and st[2].numel() == sum(int(p.numel()) for p in parts):
+        st[1].synchronize()
+        host = st[0].tolist()
+    else:
+        host = torch.cat(parts).cpu().tolist() if parts else []
     hmark("lr_host_read")
     if flags is not None:
         guards.raise_flags(host[len(host) - 2:], _GUARD_SPECS)

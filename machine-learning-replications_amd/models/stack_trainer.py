@@ -281,6 +281,7 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
                     # the guards are read after it)
                     for f in dev_bases["post"]:
                         f()
+                    dev_bases["deferred"].stage()   # (their guards' read-back, queued right here)
                     hmark("bases_post")
         finally:
             logreg_solver.BLOCK_BUDGET[0] = lr_budget
@@ -362,10 +363,13 @@ def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Te
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
     side.wait_stream(main)     # (after the tensors above: the SVC stream writes meta's column)
     pending = {}
+    from ..utils.timing import hmark
+    hmark("pre_masks")
     with torch.cuda.stream(side):
         X = X_full.index_select(1, cols_dev)
         for i in svc_cols:
             clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, None, rows_host)
+            hmark("pre_svc_inputs")
             st = launch_svc_batch(svcs, Zs, ys, y_host=[y_np[r] for r in rows_host], plan=plan["svc_pre"][i],
                                   gamma_dev=True)
             items = [(k, clones[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])

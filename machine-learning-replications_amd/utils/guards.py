@@ -61,6 +61,20 @@ class Deferred:
 
     def __init__(self):
         self._flags, self._specs, self._words, self._hooks = [], [], [], []
+        self._staged = None
+
+    def stage(self) -> None:
+        """Queue the read-back now, on the current stream, behind the kernels that produce the
+        values (pinned copy + event): :meth:`resolve` then waits for those kernels only, not for
+        whatever a later join queues in front of a plain read."""
+        if not len(self) or not self._flags + self._words or not (self._words + self._flags)[0].is_cuda:
+            return
+        dev = torch.cat(self._words + self._flags)
+        host = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+        host.copy_(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._staged = (host, ev, len(self._words), len(self._flags), dev)
 
     def flag(self, t: torch.Tensor, kind: str, what: str) -> None:
         self._flags.append(t.reshape(1).to(torch.int64))
@@ -76,7 +90,13 @@ class Deferred:
     def resolve(self) -> None:
         if not len(self):
             return
-        host = torch.cat(self._words + self._flags).cpu().tolist()
+        st = self._staged
+        self._staged = None
+        if st is not None and st[2] == len(self._words) and st[3] == len(self._flags):
+            st[1].synchronize()
+            host = st[0].tolist()
+        else:
+            host = torch.cat(self._words + self._flags).cpu().tolist()
         nw = len(self._words)
         words, flags = host[:nw], host[nw:]
         specs, hooks = self._specs, self._hooks
