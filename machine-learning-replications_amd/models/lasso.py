@@ -115,14 +115,23 @@ class LassoCV(Estimator):
     def fit(self, X, y, group=None, overlap=None):
         """``overlap``: optional host callable run while the device solves the CV path (between its
         launch and the first read of its result) — host work hidden under the path's GPU time."""
-        from ..utils.guards import check_finite
-        X = check_finite(as_tensor(X), "LassoCV.fit X")
-        y = check_finite(as_tensor(y, device=X.device), "LassoCV.fit y")
-        n, F = X.shape
+        from ..utils.guards import check_finite, finite_flag, raise_flags
+        X = as_tensor(X)
+        y = as_tensor(y, device=X.device)
         dev = X.device
+        one_read = dev.type == "cuda" and group is None and self.alphas is None
+        if one_read:
+            # the input guards ride on the alpha grid's read below (ONE host read in the prelude)
+            flags = [finite_flag(X), finite_flag(y)]
+        else:
+            check_finite(X, "LassoCV.fit X")
+            check_finite(y, "LassoCV.fit y")
+        n, F = X.shape
         k = 5 if self.cv is None else int(self.cv)
         if group is None:
-            tf = torch.as_tensor(kfold_test_folds(n, k), device=dev)
+            tfh = torch.from_numpy(kfold_test_folds(n, k))
+            # (pinned, non-blocking: a pageable upload waits for the stream's queued work)
+            tf = tfh.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else tfh.to(dev)
         else:
             from ..parallel import dist as pdist
             tf = pdist.sharded_kfold_test_folds(n, k, group, dev)
@@ -144,14 +153,20 @@ class LassoCV(Estimator):
         yy = Syy - cnt * my * my
         # alpha grid on all rows (problem k = full data)
         if self.alphas is None:
-            amax = float(q[k].abs().max()) / float(cnt[k])
+            if one_read:
+                hv = torch.stack([q[k].abs().max(), cnt[k], flags[0].to(torch.float64),
+                                  flags[1].to(torch.float64)]).cpu().tolist()
+                raise_flags([hv[2] != 0.0, hv[3] != 0.0], [("finite", "LassoCV.fit X"), ("finite", "LassoCV.fit y")])
+                amax = hv[0] / hv[1]
+            else:
+                amax = float(q[k].abs().max()) / float(cnt[k])
             if amax <= np.finfo(np.float64).resolution:
                 grid = torch.full((self.n_alphas,), np.finfo(np.float64).resolution, dtype=torch.float64)
             else:
                 grid = torch.as_tensor(np.geomspace(amax, amax * self.eps, num=self.n_alphas))
         else:
             grid = torch.as_tensor(np.sort(np.asarray(self.alphas, dtype=np.float64))[::-1].copy())
-        grid = grid.to(dev)
+        grid = grid.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else grid.to(dev)
         A = int(grid.numel())
         refit_all = None
         self.coef_spec_dev_ = self.spec_ev_ = None
