@@ -11,12 +11,21 @@ over the k nearest) runs on the host path.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 from .base import Estimator, as_tensor
 
 SLOTS = 8
+# the donor search's filter on the bf16 matrix cores (knn.hip knn_donor_mfma_kernel; the exact
+# direct-difference pass decides every slot as before, so the slots are the same bits): HFENS_KNN_MFMA
+# "auto" (default) takes it when rows × donors ≥ MFMA_MIN_PAIRS — measured 377–388 vs 305–347 G pairs/s
+# of the packed-FMA filter at 100k–300k rows, but slower on a 10k-row cohort, whose search is a few
+# hundred µs of launch-sized work (profiles/r5_knn_mfma.md); "1" always, "0" never
+MFMA_FILTER = os.environ.get("HFENS_KNN_MFMA", "auto")
+MFMA_MIN_PAIRS = 1 << 31
 # f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
 EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
 KNN_DEBUG = __import__("os").environ.get("HFENS_KNN_DEBUG", "0") == "1"
@@ -187,9 +196,22 @@ class KNNImputer(Estimator):
         cap = max(1 << 18, 16 * n)
         work = torch.empty(4 * cap + n * SLOTS * 8 + 2 * n + 12, dtype=i32, device=dev)
         nd = D32.shape[0]
+        mf = None
+        use_mf = MFMA_FILTER == "1" or (MFMA_FILTER == "auto" and n * nd >= MFMA_MIN_PAIRS)
+        if use_mf and F <= 48 and nd > 0:
+            # the donors' bf16 operand items of the matrix-core filter, built once for every slot group
+            wd = np.zeros(1, dtype=np.int64)
+            E.knn_mfma_item_words(F, wd.ctypes.data)
+            mf = (torch.empty(nd * int(wd[0]), dtype=torch.int32, device=dev), torch.empty(nd, dtype=torch.float32, device=dev))
+            E.knn_mfma_prep(D32.data_ptr(), dm.data_ptr(), nd, F, mf[0].data_ptr(), mf[1].data_ptr(), s)
         for g in range(G):
-            E.knn_donors(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
-                         slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), cnt.data_ptr(), g * SLOTS, s)
+            if mf is not None:
+                E.knn_donors_mfma(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
+                                  slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), cnt.data_ptr(), g * SLOTS,
+                                  mf[0].data_ptr(), mf[1].data_ptr(), s)
+            else:
+                E.knn_donors(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
+                             slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), cnt.data_ptr(), g * SLOTS, s)
             E.knn_refine(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
                          slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
                          Mx.data_ptr(), work.data_ptr(), cap, cnt.data_ptr(), g * SLOTS, s)

@@ -442,6 +442,336 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 }
 
 
+// ---- the donor filter on the bf16 matrix cores (SURVEY K1's Gram form) ----------
+// The packed-FMA fast pass above costs ~2 VALU instructions per feature and pair.  Here the whole
+// masked filter distance of 32 donors × 32 receivers is one GEMM on v_mfma_f32_32x32x16_bf16.
+// With x̃, ỹ the rows zero-filled at missing cells, the squared distance over the features present
+// in BOTH rows is
+//     ‖x̃‖² + ‖ỹ‖² − 2 x̃·ỹ − Σ_f [d misses f] x̃_f² − Σ_f [r misses f] ỹ_f²,
+// and all three sums are inner products along K: items (ỹ hi, −2x̃ hi), (ỹ hi, −2x̃ lo),
+// (ỹ lo, −2x̃ hi), ([d misses f], −x̃² hi), ([d misses f], −x̃² lo), (ỹ² hi, −[r misses f]),
+// (ỹ² lo, −[r misses f]) — 7F items, each f32 value cut into two bf16 pieces (hi = truncation,
+// lo = truncation of the rest; the indicators are exact).  The dropped lo×lo pieces and the f32
+// accumulation stay below 2⁻¹³·(‖x̃‖² + ‖ỹ‖²); a donor whose estimate minus 2⁻¹¹·(‖x̃‖² + ‖ỹ‖²),
+// scaled by F/common and rounded down, reaches the lane's worst slot cannot improve any slot and is
+// skipped, so the VALU epilogue is a dozen instructions per pair; every other donor runs
+// knn_donor_kernel's exact masked direct-difference pass, which alone decides the slots.  The exact
+// pass sees every donor the packed-FMA kernel's exact pass would (the skip is sound), so the per-slot
+// best and runner-up are the same bits (tests/test_prep_gpu.py::test_knn_mfma_filter_same_slots).
+// Lane ℓ and ℓ + 32 share a receiver (column ℓ mod 32 of the tile) and take alternating donor quads
+// of each 32-donor tile, each with its own slots — merged like donor splits (knn_merge_slots:
+// order-independent).  8 waves share each staged donor tile (256 receivers per workgroup), the
+// receivers' rows live in LDS (registers go to the 18 operand blocks), and the next tile's loads
+// are issued before this tile's product.
+template <int FM>
+struct KnnMf {
+  static constexpr int NB = (7 * FM + 15) / 16;    // MFMA k-blocks of the items
+  static constexpr int LP = NB * 16;
+  static constexpr int LPS = LP + 8;               // LDS row stride (u16): rows 16 B apart in the banks
+  static constexpr int TILE = 32;
+  static constexpr int WAVES = 8;
+  static constexpr int A4 = TILE * LP / 8;         // uint4 of a tile's items
+  static constexpr int Y4 = TILE * FM / 4;         // float4 of a tile's rows
+};
+typedef __bf16 knn_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int knn_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned knn_bf_hi(float v) { return __float_as_uint(v) >> 16; }
+__device__ __forceinline__ unsigned knn_bf_lo(float v) {
+  const float r = v - __uint_as_float(__float_as_uint(v) & 0xFFFF0000u);
+  return __float_as_uint(r) >> 16;
+}
+
+// donor side: items [nd][LP] (bf16 bits, kinds: 0/1 ỹ hi, 2 ỹ lo, 3/4 [d misses f], 5 ỹ² hi, 6 ỹ² lo),
+// rows [nd][FM] zero-filled
+// f32 (FM-strided: float4 staging), ‖ỹ‖² [nd]
+template <int FM>
+__global__ __launch_bounds__(256) void knn_mfma_prep_kernel(const float* __restrict__ D,
+                                                            const unsigned long long* __restrict__ dmask,
+                                                            int nd, int F, unsigned short* __restrict__ items,
+                                                            float* __restrict__ rowsFM, float* __restrict__ ny) {
+  using K = KnnMf<FM>;
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= nd) return;
+  const unsigned long long md = dmask[d];
+  unsigned short* it = items + (size_t)d * K::LP;
+  float nsum = 0.f;
+  for (int f = 0; f < FM; ++f) {
+    const float y = (f < F && !((md >> f) & 1ull)) ? D[(size_t)d * F + f] : 0.f;
+    rowsFM[(size_t)d * FM + f] = y;
+    nsum = fmaf(y, y, nsum);
+  }
+  for (int q = 0; q < K::LP; ++q) {
+    const int kind = q / FM, f = q - kind * FM;
+    const bool miss = f >= F || ((md >> f) & 1ull);
+    const float y = miss ? 0.f : D[(size_t)d * F + f];
+    unsigned w = 0u;
+    if (kind <= 1) w = knn_bf_hi(y);
+    else if (kind == 2) w = knn_bf_lo(y);
+    else if (kind <= 4) w = (f < F && miss) ? 0x3F80u : 0u;
+    else if (kind == 5) w = knn_bf_hi(y * y);
+    else if (kind == 6) w = knn_bf_lo(y * y);
+    it[q] = (unsigned short)w;
+  }
+  ny[d] = nsum;
+}
+
+template <int FM>
+__global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
+    const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
+    const float* __restrict__ rowsFM, const unsigned long long* __restrict__ dmask, int nd, int F,
+    int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best,
+    unsigned* __restrict__ alt, const int* __restrict__ cnt, int s0,
+    const unsigned short* __restrict__ items, const float* __restrict__ ny_all) {
+  using K = KnnMf<FM>;
+  if (cnt != nullptr) {
+    if (s0 >= cnt[1]) return;
+    nr = cnt[0];
+  }
+  constexpr int LD = FM;   // (FM is a multiple of 8)
+  constexpr int NT = 64 * K::WAVES;
+  __shared__ __attribute__((aligned(16))) unsigned short tA[K::TILE * K::LPS];
+  __shared__ __attribute__((aligned(16))) float tY[K::TILE * LD];
+  __shared__ unsigned long long tM[K::TILE];
+  __shared__ float tN[K::TILE];
+  __shared__ float s_scale[65];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
+  const int r = blockIdx.x * (32 * K::WAVES) + wave * 32 + r32;
+  const bool active = r < nr;
+  const int d_begin = blockIdx.y * per_split;
+  const int d_end = min(nd, d_begin + per_split);
+  const unsigned long long mr = active ? rmask[r] : 0ull;
+  // the receivers' zero-filled rows stay in LDS (the operand build and the exact pass read them)
+  __shared__ __attribute__((aligned(16))) float xs[32 * K::WAVES][LD + 4];
+  float* xrow = xs[wave * 32 + r32];
+  float nx = 0.f;
+  for (int f = hh; f < LD; f += 2) {
+    const float v = (active && f < F && !((mr >> f) & 1ull)) ? R[(size_t)r * F + f] : 0.f;
+    xrow[f] = v;
+  }
+  __syncthreads();
+#pragma unroll 8
+  for (int f = 0; f < LD; ++f) nx = fmaf(xrow[f], xrow[f], nx);
+  // receiver operands: item q = 16m + 8hh + e of the lane's half (kinds: 0 −2x̃ hi, 1 −2x̃ lo, 2 −2x̃ hi,
+  // 3 −x̃² hi, 4 −x̃² lo, 5/6 −[r misses f])
+  knn_bf16x8 bq[K::NB];
+#pragma unroll
+  for (int m = 0; m < K::NB; ++m) {
+    unsigned w[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      unsigned v2[2];
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        const int q = 16 * m + 8 * hh + 2 * e2 + dd;
+        const int kind = q / FM, f = q - kind * FM;
+        const float xv = kind < 7 ? xrow[f] : 0.f;
+        const float v = kind <= 2 ? -2.f * xv : -(xv * xv);
+        const bool rm = f < F && ((mr >> f) & 1ull);
+        unsigned ww = 0u;
+        if (kind == 0 || kind == 2 || kind == 3) ww = knn_bf_hi(v);
+        else if (kind == 1 || kind == 4) ww = knn_bf_lo(v);
+        else if (kind <= 6) ww = rm ? 0xBF80u : 0u;
+        v2[dd] = ww;
+      }
+      w[e2] = v2[0] | (v2[1] << 16);
+    }
+    bq[m] = __builtin_bit_cast(knn_bf16x8, (knn_u32x4){w[0], w[1], w[2], w[3]});
+  }
+  int col[kKnnSlots];
+  float bd[kKnnSlots], b2[kKnnSlots];
+  int bi[kKnnSlots];
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k) {
+    col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
+    bd[k] = INFINITY;
+    b2[k] = INFINITY;
+    bi[k] = -1;
+    any |= col[k] >= 0;
+  }
+  unsigned long long need = 0ull;
+#pragma unroll
+  for (int k = 0; k < kKnnSlots; ++k)
+    if (col[k] >= 0) need |= 1ull << col[k];
+  float bmax = INFINITY;
+  if (tid <= 64) s_scale[tid] = tid > 0 ? (float)F / (float)tid : 0.f;
+  const bool wave_any = __ballot(any) != 0ull;
+  // prefetch of a tile into registers (issued one tile ahead)
+  constexpr int PA = (K::A4 + NT - 1) / NT, PY = (K::Y4 + NT - 1) / NT;
+  knn_u32x4 pa[PA];
+  float4 py[PY];
+  unsigned long long pm = ~0ull;
+  float pn = 0.f;
+  auto fetch = [&](int d0) {
+    const int nt = min(K::TILE, d_end - d0);
+    const knn_u32x4* srcA = reinterpret_cast<const knn_u32x4*>(items + (size_t)d0 * K::LP);
+    const float4* srcY = reinterpret_cast<const float4*>(rowsFM + (size_t)d0 * LD);
+#pragma unroll
+    for (int u = 0; u < PA; ++u) {
+      const int e = tid + u * NT;
+      pa[u] = (e < nt * K::LP / 8) ? srcA[e] : (knn_u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < PY; ++u) {
+      const int e = tid + u * NT;
+      py[u] = (e < nt * LD / 4) ? srcY[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < K::TILE) {
+      pm = tid < nt ? dmask[d0 + tid] : ~0ull;
+      pn = tid < nt ? ny_all[d0 + tid] : 0.f;
+    }
+  };
+  if (d_begin < d_end) fetch(d_begin);
+  for (int d0 = d_begin; d0 < d_end; d0 += K::TILE) {
+    const int nt = min(K::TILE, d_end - d0);
+    __syncthreads();   // the previous tile is consumed
+#pragma unroll
+    for (int u = 0; u < PA; ++u) {
+      const int e = tid + u * NT;
+      if (e < K::A4) reinterpret_cast<knn_u32x4*>(tA)[(e / (K::LP / 8)) * (K::LPS / 8) + e % (K::LP / 8)] = pa[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PY; ++u) {
+      const int e = tid + u * NT;
+      if (e < K::Y4) reinterpret_cast<float4*>(tY)[e] = py[u];
+    }
+    if (tid < K::TILE) { tM[tid] = pm; tN[tid] = pn; }
+    __syncthreads();
+    if (d0 + K::TILE < d_end) fetch(d0 + K::TILE);   // the next tile's loads fly under this one
+    if (!wave_any) continue;
+    f32x16 acc = {0.f};
+#pragma unroll
+    for (int m = 0; m < K::NB; ++m) {
+      const knn_u32x4 raw = *reinterpret_cast<const knn_u32x4*>(&tA[r32 * K::LPS + 16 * m + 8 * hh]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(knn_bf16x8, raw), bq[m], acc, 0, 0, 0);
+    }
+    if (!any) continue;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;   // donor of accumulator j (increasing in j)
+      if (row >= nt) continue;
+      const unsigned long long md = tM[row];
+      if ((need & ~md) == 0ull) continue;
+      const int present = F - __builtin_popcountll(mr | md);
+      if (present <= 0) continue;
+      const float* yrow = tY + row * LD;
+      const float ynorm = tN[row];
+      const float est = (nx + ynorm) + acc[j];
+      const float bound = 4.8828125e-04f * (nx + ynorm);   // 2^-11 (‖x̃‖² + ‖ỹ‖²)
+      const float scale = s_scale[present];
+      const float lb = fmaxf(est - bound, 0.f) * scale * 0.99999905f;
+      if (!(lb < bmax)) continue;
+      // ---- exact pass (knn_donor_kernel's masked direct differences, same order and roundings)
+      const float4* xd4 = reinterpret_cast<const float4*>(yrow);
+      const float4* xr4 = reinterpret_cast<const float4*>(xrow);
+      const unsigned long long both = ~(mr | md);
+      const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int q = 0; q < LD / 4; ++q) {
+        const float4 v = xd4[q];
+        const float4 u = xr4[q];
+        const unsigned bqm = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+        const float a = (bqm & 1u) ? u.x - v.x : 0.f;
+        const float b = (bqm & 2u) ? u.y - v.y : 0.f;
+        const float c = (bqm & 4u) ? u.z - v.z : 0.f;
+        const float d = (bqm & 8u) ? u.w - v.w : 0.f;
+        sa = fmaf(a, a, sa);
+        sb = fmaf(b, b, sb);
+        sa = fmaf(c, c, sa);
+        sb = fmaf(d, d, sb);
+      }
+      const float dist = fmaxf(sa + sb, 0.f) * scale;
+      if (!(dist < bmax)) continue;
+      const int di = d0 + row;
+      float mx = 0.f;
+#pragma unroll
+      for (int k = 0; k < kKnnSlots; ++k) {
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < b2[k]) {
+          const bool nb = dist < bd[k];
+          b2[k] = nb ? bd[k] : dist;
+          bi[k] = nb ? di : bi[k];
+          bd[k] = nb ? dist : bd[k];
+        }
+        if (col[k] >= 0) mx = fmaxf(mx, b2[k]);
+      }
+      bmax = mx;
+    }
+  }
+  if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
+}
+
+// 32-bit words per donor of the prep buffer (bf16 items, then the FM-strided zero-filled f32 row) → *out
+static int knn_mf_fm(int F) { return F <= 16 ? 16 : F <= 24 ? 24 : F <= 32 ? 32 : F <= 40 ? 40 : 48; }
+void knn_mfma_item_words(int F, uintptr_t out) {
+  const int FM = knn_mf_fm(F);
+  *reinterpret_cast<long long*>(out) = (long long)(((7 * FM + 15) / 16) * 16 / 2 + FM);
+}
+
+void knn_mfma_prep(uintptr_t D, uintptr_t dmask, int nd, int F, uintptr_t items, uintptr_t ny, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 48, "knn_mfma_prep: 1 <= F <= 48");
+  if (nd == 0) return;
+  auto go = [&](auto fm) {
+    constexpr int FM = decltype(fm)::value;
+    using K = KnnMf<FM>;
+    unsigned short* it = (unsigned short*)items;
+    float* rows = reinterpret_cast<float*>(it + (size_t)nd * K::LP);
+    hipLaunchKernelGGL(knn_mfma_prep_kernel<FM>, dim3((nd + 255) / 256), dim3(256), 0, as_stream(stream),
+                       (const float*)D, (const unsigned long long*)dmask, nd, F, it, rows, (float*)ny);
+  };
+  const int FM = knn_mf_fm(F);
+  if (FM == 16) go(std::integral_constant<int, 16>{});
+  else if (FM == 24) go(std::integral_constant<int, 24>{});
+  else if (FM == 32) go(std::integral_constant<int, 32>{});
+  else if (FM == 40) go(std::integral_constant<int, 40>{});
+  else go(std::integral_constant<int, 48>{});
+  launch_check();
+}
+
+// knn_donors with the matrix-core filter; `items` / `ny` from knn_mfma_prep of the same donors
+void knn_donors_mfma(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
+                     uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t cnt, int s0, uintptr_t items,
+                     uintptr_t ny, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 48, "knn_donors_mfma: 1 <= F <= 48");
+  (void)D;
+  if (nr == 0 || nd == 0) return;
+  hipStream_t st = as_stream(stream);
+  HFENS_CHECK(hipMemsetAsync((void*)best, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned long long), st));
+  HFENS_CHECK(hipMemsetAsync((void*)alt, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned), st));
+  const int rb = (nr + 255) / 256;
+  // ≈ kWgs workgroups (two 8-wave workgroups fill a CU at this kernel's occupancy), ≥ kMinPer donors each
+  // (scan: profiles/r5_runs/knn_mfma_grid.log)
+  static const int kWgs = getenv("HFENS_KNN_MFMA_WGS") ? atoi(getenv("HFENS_KNN_MFMA_WGS")) : 512;
+  static const int kMinPer = getenv("HFENS_KNN_MFMA_MINPER") ? atoi(getenv("HFENS_KNN_MFMA_MINPER")) : 256;
+  int splits = kWgs / rb;
+  const int by_range = (nd + 16383) / 16384;
+  if (splits < by_range) splits = by_range;
+  const int max_splits = (nd + kMinPer - 1) / kMinPer;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int per = (nd + splits - 1) / splits;
+  per = (per + 31) / 32 * 32;
+  const int nsp = (nd + per - 1) / per;
+  auto go = [&](auto fm) {
+    constexpr int FM = decltype(fm)::value;
+    using K = KnnMf<FM>;
+    const unsigned short* it = (const unsigned short*)items;
+    const float* rows = reinterpret_cast<const float*>(it + (size_t)nd * K::LP);
+    hipLaunchKernelGGL(knn_donor_mfma_kernel<FM>, dim3(rb, nsp), dim3(512), 0, st, (const float*)R,
+                       (const unsigned long long*)rmask, nr, rows, (const unsigned long long*)dmask, nd, F, per,
+                       (const int*)slot_col, (unsigned long long*)best, (unsigned*)alt, (const int*)cnt, s0, it,
+                       (const float*)ny);
+  };
+  const int FM = knn_mf_fm(F);
+  if (FM == 16) go(std::integral_constant<int, 16>{});
+  else if (FM == 24) go(std::integral_constant<int, 24>{});
+  else if (FM == 32) go(std::integral_constant<int, 32>{});
+  else if (FM == 40) go(std::integral_constant<int, 40>{});
+  else go(std::integral_constant<int, 48>{});
+  launch_check();
+}
+
 // ---- f64-exact donors: the f32 search above picks the same donor as the f64
 // direct-difference mirror (models/imputer.py _impute_host: Σ over common features in feature
 // order of fl((x−y)·(x−y)) in f64, × F / |common|, lowest index on ties) except where another

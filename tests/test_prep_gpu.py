@@ -85,3 +85,67 @@ def test_knn_fast_pass_same_donors(dev, monkeypatch, n, F, nan):
         imp = KNNImputer(n_neighbors=1).fit(Xt)
         out[k] = imp.transform(Xt).cpu()
     assert torch.equal(out["direct"], out["fast"])
+
+
+@pytest.mark.parametrize("n,F,nan", [(3000, 40, 0.02), (2500, 17, 0.1), (2000, 24, 0.3), (1500, 48, 0.05),
+                                     (60000, 40, 0.02)])
+def test_knn_mfma_filter_same_slots(dev, n, F, nan):
+    """the donor search with its filter on the bf16 matrix cores
+    (knn.hip knn_donor_mfma_kernel) gives the SAME per-slot best (f32 distance bits, donor) and the
+    same runner-up distances as the packed-FMA kernel — the exact pass decides both, the matrix-core
+    bound only skips donors that cannot matter — duplicated rows (exact ties) included."""
+    from hfens import ops
+    X, _, _ = make_hf_cohort(n, F, seed=7 * n + F, nan_frac=nan)
+    X = np.concatenate([X, X[: n // 10]], axis=0)
+    X[::11, 2] = np.nan
+    mu = np.nanmean(X, 0)
+    miss = np.isnan(X)
+    Xc = np.where(miss, 0.0, X - mu).astype(np.float32)
+    bits = (miss.astype(np.uint64) << np.arange(F, dtype=np.uint64)).sum(1).astype(np.uint64).view(np.int64)
+    rows = np.nonzero(miss.any(1))[0]
+    slot = np.full((rows.shape[0], 8), -1, dtype=np.int32)
+    for i, r in enumerate(rows):
+        c = np.nonzero(miss[r])[0][:8]
+        slot[i, :c.shape[0]] = c
+    E = ops.ext()
+    s = ops.stream_ptr(dev)
+    R = torch.as_tensor(Xc[rows], device=dev).contiguous()
+    rm = torch.as_tensor(bits[rows], device=dev)
+    D = torch.as_tensor(Xc, device=dev).contiguous()
+    dm = torch.as_tensor(bits, device=dev)
+    sl = torch.as_tensor(slot, device=dev)
+    nr, nd = R.shape[0], D.shape[0]
+    out = {}
+    for kind in ("fast", "mfma"):
+        best = torch.empty(nr, 8, dtype=torch.int64, device=dev)
+        alt = torch.empty(nr, 8, dtype=torch.int32, device=dev)
+        if kind == "fast":
+            E.knn_donors(R.data_ptr(), rm.data_ptr(), nr, D.data_ptr(), dm.data_ptr(), nd, F, sl.data_ptr(),
+                         best.data_ptr(), alt.data_ptr(), 0, 0, s)
+        else:
+            wd = np.zeros(1, dtype=np.int64)
+            E.knn_mfma_item_words(F, wd.ctypes.data)
+            items = torch.empty(nd * int(wd[0]), dtype=torch.int32, device=dev)
+            ny = torch.empty(nd, dtype=torch.float32, device=dev)
+            E.knn_mfma_prep(D.data_ptr(), dm.data_ptr(), nd, F, items.data_ptr(), ny.data_ptr(), s)
+            E.knn_donors_mfma(R.data_ptr(), rm.data_ptr(), nr, D.data_ptr(), dm.data_ptr(), nd, F, sl.data_ptr(),
+                              best.data_ptr(), alt.data_ptr(), 0, 0, items.data_ptr(), ny.data_ptr(), s)
+        torch.cuda.synchronize()
+        out[kind] = (best.cpu(), alt.cpu())
+    assert torch.equal(out["fast"][0], out["mfma"][0])
+    assert torch.equal(out["fast"][1], out["mfma"][1])
+
+
+def test_knn_imputer_mfma_same_output(dev, monkeypatch):
+    """The imputer's output with the matrix-core donor filter forced on equals the packed-FMA path's
+    bit for bit (the exact passes decide the donors; f64 refine and apply are shared)."""
+    from hfens.models import imputer as imp_mod
+    from hfens.models.imputer import KNNImputer
+    X, _, _ = make_hf_cohort(20000, 40, seed=5, nan_frac=0.03)
+    Xt = torch.as_tensor(X, device=dev)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(imp_mod, "MFMA_FILTER", mode)
+        out[mode] = KNNImputer(n_neighbors=1).fit(Xt).transform(Xt).cpu()
+    assert not torch.isnan(out["1"]).any()
+    assert torch.equal(out["0"], out["1"])
