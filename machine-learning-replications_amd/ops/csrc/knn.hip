@@ -543,7 +543,11 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
   const unsigned long long mr = active ? rmask[r] : 0ull;
   // the receivers' zero-filled rows stay in LDS (the operand build and the exact pass read them)
   __shared__ __attribute__((aligned(16))) float xs[32 * K::WAVES][LD + 4];
+  __shared__ unsigned long long smr[32 * K::WAVES];
+  __shared__ unsigned short clist[K::WAVES][1024];   // a wave's (lane, accumulator) candidates
+  __shared__ float dbuf[K::WAVES][1024];             // their exact distances
   float* xrow = xs[wave * 32 + r32];
+  if (hh == 0) smr[wave * 32 + r32] = mr;
   float nx = 0.f;
   for (int f = hh; f < LD; f += 2) {
     const float v = (active && f < F && !((mr >> f) & 1ull)) ? R[(size_t)r * F + f] : 0.f;
@@ -646,26 +650,59 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
       const knn_u32x4 raw = *reinterpret_cast<const knn_u32x4*>(&tA[r32 * K::LPS + 16 * m + 8 * hh]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(knn_bf16x8, raw), bq[m], acc, 0, 0, 0);
     }
-    if (!any) continue;
+    // (a) the bound: which of the lane's 16 donors can still improve a slot (bmax of the tile start:
+    //     a stale bmax only lets more donors through, and those change nothing below)
+    unsigned cand = 0u;
+    if (any) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;   // donor of accumulator j (increasing in j)
-      if (row >= nt) continue;
+      for (int j = 0; j < 16; ++j) {
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;   // donor of accumulator j (increasing in j)
+        if (row >= nt) continue;
+        const unsigned long long md = tM[row];
+        if ((need & ~md) == 0ull) continue;
+        const int present = F - __builtin_popcountll(mr | md);
+        if (present <= 0) continue;
+        const float ynorm = tN[row];
+        const float est = (nx + ynorm) + acc[j];
+        const float bound = 4.8828125e-04f * (nx + ynorm);   // 2^-11 (‖x̃‖² + ‖ỹ‖²)
+        const float lb = fmaxf(est - bound, 0.f) * s_scale[present] * 0.99999905f;
+        if (lb < bmax) cand |= 1u << j;
+      }
+    }
+    // (b) the exact passes of the whole wave's candidates, compacted over its 64 lanes (one lane per
+    //     candidate instead of every lane waiting on the few whose donor passed)
+    const int mine = __builtin_popcount(cand);
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (total == 0) continue;
+    {
+      int pos = incl - mine;
+      unsigned c2 = cand;
+      while (c2) {
+        const int j = __builtin_ctz(c2);
+        c2 &= c2 - 1u;
+        clist[wave][pos++] = (unsigned short)((lane << 4) | j);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int c = lane; c < total; c += 64) {
+      const int code = clist[wave][c];
+      const int owner = code >> 4, j = code & 15;
+      const int row = (j & 3) + 8 * (j >> 2) + 4 * (owner >> 5);
       const unsigned long long md = tM[row];
-      if ((need & ~md) == 0ull) continue;
-      const int present = F - __builtin_popcountll(mr | md);
-      if (present <= 0) continue;
-      const float* yrow = tY + row * LD;
-      const float ynorm = tN[row];
-      const float est = (nx + ynorm) + acc[j];
-      const float bound = 4.8828125e-04f * (nx + ynorm);   // 2^-11 (‖x̃‖² + ‖ỹ‖²)
-      const float scale = s_scale[present];
-      const float lb = fmaxf(est - bound, 0.f) * scale * 0.99999905f;
-      if (!(lb < bmax)) continue;
-      // ---- exact pass (knn_donor_kernel's masked direct differences, same order and roundings)
-      const float4* xd4 = reinterpret_cast<const float4*>(yrow);
-      const float4* xr4 = reinterpret_cast<const float4*>(xrow);
-      const unsigned long long both = ~(mr | md);
+      const unsigned long long mro = smr[wave * 32 + (owner & 31)];
+      const int present = F - __builtin_popcountll(mro | md);
+      // knn_donor_kernel's masked direct differences, same order and roundings
+      const float4* xd4 = reinterpret_cast<const float4*>(tY + row * LD);
+      const float4* xr4 = reinterpret_cast<const float4*>(xs[wave * 32 + (owner & 31)]);
+      const unsigned long long both = ~(mro | md);
       const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
       float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -675,15 +712,26 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
         const unsigned bqm = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
         const float a = (bqm & 1u) ? u.x - v.x : 0.f;
         const float b = (bqm & 2u) ? u.y - v.y : 0.f;
-        const float c = (bqm & 4u) ? u.z - v.z : 0.f;
+        const float cc = (bqm & 4u) ? u.z - v.z : 0.f;
         const float d = (bqm & 8u) ? u.w - v.w : 0.f;
         sa = fmaf(a, a, sa);
         sb = fmaf(b, b, sb);
-        sa = fmaf(c, c, sa);
+        sa = fmaf(cc, cc, sa);
         sb = fmaf(d, d, sb);
       }
-      const float dist = fmaxf(sa + sb, 0.f) * scale;
+      dbuf[wave][code] = fmaxf(sa + sb, 0.f) * s_scale[present];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (c) each lane folds its own candidates into its slots in donor order
+    while (cand) {
+      const int j = __builtin_ctz(cand);
+      cand &= cand - 1u;
+      const float dist = dbuf[wave][(lane << 4) | j];
       if (!(dist < bmax)) continue;
+      const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;
+      const unsigned long long md = tM[row];
       const int di = d0 + row;
       float mx = 0.f;
 #pragma unroll
