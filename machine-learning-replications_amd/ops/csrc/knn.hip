@@ -533,7 +533,7 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
   __shared__ __attribute__((aligned(16))) unsigned short tA[K::TILE * K::LPS];
   __shared__ __attribute__((aligned(16))) float tY[K::TILE * LD];
   __shared__ unsigned long long tM[K::TILE];
-  __shared__ float tN[K::TILE];
+  __shared__ knn_u32x4 tR[K::TILE];   // a donor's mask and ‖ỹ‖² in one 16-byte read
   __shared__ float s_scale[65];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
   const int r = blockIdx.x * (32 * K::WAVES) + wave * 32 + r32;
@@ -600,6 +600,7 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     if (col[k] >= 0) need |= 1ull << col[k];
   float bmax = INFINITY;
   if (tid <= 64) s_scale[tid] = tid > 0 ? (float)F / (float)tid : 0.f;
+  const float fF = (float)F * 0.99999905f;
   const bool wave_any = __ballot(any) != 0ull;
   // prefetch of a tile into registers (issued one tile ahead)
   constexpr int PA = (K::A4 + NT - 1) / NT, PY = (K::Y4 + NT - 1) / NT;
@@ -640,7 +641,10 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
       const int e = tid + u * NT;
       if (e < K::Y4) reinterpret_cast<float4*>(tY)[e] = py[u];
     }
-    if (tid < K::TILE) { tM[tid] = pm; tN[tid] = pn; }
+    if (tid < K::TILE) {
+      tM[tid] = pm;
+      tR[tid] = (knn_u32x4){(unsigned)pm, (unsigned)(pm >> 32), __float_as_uint(pn), 0u};
+    }
     __syncthreads();
     if (d0 + K::TILE < d_end) fetch(d0 + K::TILE);   // the next tile's loads fly under this one
     if (!wave_any) continue;
@@ -654,19 +658,18 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     //     a stale bmax only lets more donors through, and those change nothing below)
     unsigned cand = 0u;
     if (any) {
+      // branch-free: lb·(1 + ε) < bmax ⇔ max(est − bound, 0)·F·c < bmax·common (no division, one
+      // LDS read of the row's mask and norm); rows ≥ nt carry an all-ones mask (no common feature)
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;   // donor of accumulator j (increasing in j)
-        if (row >= nt) continue;
-        const unsigned long long md = tM[row];
-        if ((need & ~md) == 0ull) continue;
+        const knn_u32x4 rw = *reinterpret_cast<const knn_u32x4*>(&tR[row]);
+        const unsigned long long md = (unsigned long long)rw.x | ((unsigned long long)rw.y << 32);
+        const float ynorm = __uint_as_float(rw.z);
         const int present = F - __builtin_popcountll(mr | md);
-        if (present <= 0) continue;
-        const float ynorm = tN[row];
-        const float est = (nx + ynorm) + acc[j];
-        const float bound = 4.8828125e-04f * (nx + ynorm);   // 2^-11 (‖x̃‖² + ‖ỹ‖²)
-        const float lb = fmaxf(est - bound, 0.f) * s_scale[present] * 0.99999905f;
-        if (lb < bmax) cand |= 1u << j;
+        const float lhs = fmaxf((nx + ynorm) + acc[j] - 4.8828125e-04f * (nx + ynorm), 0.f) * fF;
+        const bool ok = ((need & ~md) != 0ull) & (present > 0) & (lhs < bmax * (float)present);
+        cand |= (unsigned)ok << j;
       }
     }
     // (b) the exact passes of the whole wave's candidates, compacted over its 64 lanes (one lane per
