@@ -534,6 +534,7 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
   __shared__ __attribute__((aligned(16))) float tY[K::TILE * LD];
   __shared__ unsigned long long tM[K::TILE];
   __shared__ knn_u32x4 tR[K::TILE];   // a donor's mask and ‖ỹ‖² in one 16-byte read
+  __shared__ __attribute__((aligned(16))) float tNy[K::TILE];
   __shared__ float s_scale[65];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
   const int r = blockIdx.x * (32 * K::WAVES) + wave * 32 + r32;
@@ -644,6 +645,7 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     if (tid < K::TILE) {
       tM[tid] = pm;
       tR[tid] = (knn_u32x4){(unsigned)pm, (unsigned)(pm >> 32), __float_as_uint(pn), 0u};
+      tNy[tid] = pn;
     }
     __syncthreads();
     if (d0 + K::TILE < d_end) fetch(d0 + K::TILE);   // the next tile's loads fly under this one
@@ -658,22 +660,40 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     //     a stale bmax only lets more donors through, and those change nothing below)
     unsigned cand = 0u;
     if (any) {
-      // branch-free: lb·(1 + ε) < bmax ⇔ max(est − bound, 0)·F·c < bmax·common (no division, one
-      // LDS read of the row's mask and norm); rows ≥ nt carry an all-ones mask (no common feature)
+      // first a cheap test without the F/common scale (≥ 1): max(est − bound, 0) ≥ bmax already
+      // skips, and it holds for almost every pair once the slots have filled
+      const float bq1 = bmax * 1.0000038f;                   // (1 + 2^-18): covers the roundings
+      const float nxk = nx * 0.99951171875f;                  // (1 − 2^-11) ‖x̃‖²
+      unsigned pre = 0u;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;   // donor of accumulator j (increasing in j)
+      for (int g = 0; g < 4; ++g) {   // accumulators 4g..4g+3 are donors 8g + 4hh + 0..3
+        const float4 ny4 = *reinterpret_cast<const float4*>(&tNy[8 * g + 4 * hh]);
+        pre |= (unsigned)(fmaf(ny4.x, 0.99951171875f, nxk) + acc[4 * g] < bq1) << (4 * g);
+        pre |= (unsigned)(fmaf(ny4.y, 0.99951171875f, nxk) + acc[4 * g + 1] < bq1) << (4 * g + 1);
+        pre |= (unsigned)(fmaf(ny4.z, 0.99951171875f, nxk) + acc[4 * g + 2] < bq1) << (4 * g + 2);
+        pre |= (unsigned)(fmaf(ny4.w, 0.99951171875f, nxk) + acc[4 * g + 3] < bq1) << (4 * g + 3);
+      }
+      // then the full test: lb·(1 + ε) < bmax ⇔ max(est − bound, 0)·F·c < bmax·common (no
+      // division); rows ≥ nt carry an all-ones mask (no common feature)
+      while (pre) {
+        const int j = __builtin_ctz(pre);
+        pre &= pre - 1u;
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;
         const knn_u32x4 rw = *reinterpret_cast<const knn_u32x4*>(&tR[row]);
         const unsigned long long md = (unsigned long long)rw.x | ((unsigned long long)rw.y << 32);
         const float ynorm = __uint_as_float(rw.z);
         const int present = F - __builtin_popcountll(mr | md);
-        const float lhs = fmaxf((nx + ynorm) + acc[j] - 4.8828125e-04f * (nx + ynorm), 0.f) * fF;
+        float aj = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) aj = jj == j ? acc[jj] : aj;
+        const float lhs = fmaxf((nx + ynorm) + aj - 4.8828125e-04f * (nx + ynorm), 0.f) * fF;
         const bool ok = ((need & ~md) != 0ull) & (present > 0) & (lhs < bmax * (float)present);
         cand |= (unsigned)ok << j;
       }
     }
     // (b) the exact passes of the whole wave's candidates, compacted over its 64 lanes (one lane per
     //     candidate instead of every lane waiting on the few whose donor passed)
+    if (__ballot(cand != 0u) == 0ull) continue;
     const int mine = __builtin_popcount(cand);
     int incl = mine;
 #pragma unroll
