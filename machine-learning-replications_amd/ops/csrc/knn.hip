@@ -454,8 +454,9 @@ void knn_donors(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
 // lo = truncation of the rest; the indicators are exact).  The dropped lo×lo pieces and the f32
 // accumulation stay below 2⁻¹³·(‖x̃‖² + ‖ỹ‖²); a donor whose estimate minus 2⁻¹¹·(‖x̃‖² + ‖ỹ‖²),
 // scaled by F/common and rounded down, reaches the lane's worst slot cannot improve any slot and is
-// skipped, so the VALU epilogue is a dozen instructions per pair; every other donor runs
-// knn_donor_kernel's exact masked direct-difference pass, which alone decides the slots.  The exact
+// skipped (a scale-free test first: five VALU instructions per pair); every other donor is queued
+// per lane and runs knn_donor_kernel's exact masked direct-difference pass in batches compacted over
+// the wave's 64 lanes, and that pass alone decides the slots.  The exact
 // pass sees every donor the packed-FMA kernel's exact pass would (the skip is sound), so the per-slot
 // best and runner-up are the same bits (tests/test_prep_gpu.py::test_knn_mfma_filter_same_slots).
 // Lane ℓ and ℓ + 32 share a receiver (column ℓ mod 32 of the tile) and take alternating donor quads
@@ -469,7 +470,7 @@ struct KnnMf {
   static constexpr int LP = NB * 16;
   static constexpr int LPS = LP + 8;               // LDS row stride (u16): rows 16 B apart in the banks
   static constexpr int TILE = 32;
-  static constexpr int WAVES = 8;
+  static constexpr int WAVES = FM >= 48 ? 4 : 8;   // (LDS: 160 KB per workgroup)
   static constexpr int A4 = TILE * LP / 8;         // uint4 of a tile's items
   static constexpr int Y4 = TILE * FM / 4;         // float4 of a tile's rows
 };
@@ -545,8 +546,10 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
   // the receivers' zero-filled rows stay in LDS (the operand build and the exact pass read them)
   __shared__ __attribute__((aligned(16))) float xs[32 * K::WAVES][LD + 4];
   __shared__ unsigned long long smr[32 * K::WAVES];
-  __shared__ unsigned short clist[K::WAVES][1024];   // a wave's (lane, accumulator) candidates
-  __shared__ float dbuf[K::WAVES][1024];             // their exact distances
+  constexpr int kQc = 16;   // ≥ 16: a tile adds at most 16 candidates per lane after a flush
+  __shared__ unsigned short clist[K::WAVES][64 * kQc];   // a wave's queued (lane, entry) candidates
+  __shared__ int q_idx[K::WAVES][64][kQc];               // each lane's queued donors
+  __shared__ float q_dist[K::WAVES][64][kQc];            // their exact distances
   float* xrow = xs[wave * 32 + r32];
   if (hh == 0) smr[wave * 32 + r32] = mr;
   float nx = 0.f;
@@ -628,6 +631,78 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
       pn = tid < nt ? ny_all[d0 + tid] : 0.f;
     }
   };
+  // candidate queue of each lane (donor indices, increasing) and the batched exact pass: the wave's
+  // queued candidates are compacted over its 64 lanes (one lane per candidate, donor rows from global
+  // memory), then every lane folds its own in donor order — a wave pays the exact pass's latency
+  // once per kQc-entry batch instead of once per tile that holds any candidate
+  int qlen = 0;
+  auto flush = [&]() {
+    const int mine = qlen;
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (total == 0) return;
+    for (int e = 0, pos = incl - mine; e < mine; ++e, ++pos) clist[wave][pos] = (unsigned short)((lane << 5) | e);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int c = lane; c < total; c += 64) {
+      const int code = clist[wave][c];
+      const int owner = code >> 5, e = code & 31;
+      const int di = q_idx[wave][owner][e];
+      const unsigned long long md = dmask[di];
+      const unsigned long long mro = smr[wave * 32 + (owner & 31)];
+      const int present = F - __builtin_popcountll(mro | md);
+      // knn_donor_kernel's masked direct differences, same order and roundings
+      const float4* xd4 = reinterpret_cast<const float4*>(rowsFM + (size_t)di * LD);
+      const float4* xr4 = reinterpret_cast<const float4*>(xs[wave * 32 + (owner & 31)]);
+      const unsigned long long both = ~(mro | md);
+      const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int q = 0; q < LD / 4; ++q) {
+        const float4 v = xd4[q];
+        const float4 u = xr4[q];
+        const unsigned bqm = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
+        const float a = (bqm & 1u) ? u.x - v.x : 0.f;
+        const float b = (bqm & 2u) ? u.y - v.y : 0.f;
+        const float cc = (bqm & 4u) ? u.z - v.z : 0.f;
+        const float d = (bqm & 8u) ? u.w - v.w : 0.f;
+        sa = fmaf(a, a, sa);
+        sb = fmaf(b, b, sb);
+        sa = fmaf(cc, cc, sa);
+        sb = fmaf(d, d, sb);
+      }
+      q_dist[wave][owner][e] = fmaxf(sa + sb, 0.f) * s_scale[present];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int e = 0; e < mine; ++e) {
+      const float dist = q_dist[wave][lane][e];
+      if (!(dist < bmax)) continue;
+      const int di = q_idx[wave][lane][e];
+      const unsigned long long md = dmask[di];
+      float mx = 0.f;
+#pragma unroll
+      for (int k = 0; k < kKnnSlots; ++k) {
+        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < b2[k]) {
+          const bool nb = dist < bd[k];
+          b2[k] = nb ? bd[k] : dist;
+          bi[k] = nb ? di : bi[k];
+          bd[k] = nb ? dist : bd[k];
+        }
+        if (col[k] >= 0) mx = fmaxf(mx, b2[k]);
+      }
+      bmax = mx;
+    }
+    qlen = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
   if (d_begin < d_end) fetch(d_begin);
   for (int d0 = d_begin; d0 < d_end; d0 += K::TILE) {
     const int nt = min(K::TILE, d_end - d0);
@@ -691,85 +766,16 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
         cand |= (unsigned)ok << j;
       }
     }
-    // (b) the exact passes of the whole wave's candidates, compacted over its 64 lanes (one lane per
-    //     candidate instead of every lane waiting on the few whose donor passed)
+    // (b) queue the lane's candidates (donor order); the exact passes run batched over the wave
     if (__ballot(cand != 0u) == 0ull) continue;
-    const int mine = __builtin_popcount(cand);
-    int incl = mine;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
-    }
-    const int total = __shfl(incl, 63, 64);
-    if (total == 0) continue;
-    {
-      int pos = incl - mine;
-      unsigned c2 = cand;
-      while (c2) {
-        const int j = __builtin_ctz(c2);
-        c2 &= c2 - 1u;
-        clist[wave][pos++] = (unsigned short)((lane << 4) | j);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int c = lane; c < total; c += 64) {
-      const int code = clist[wave][c];
-      const int owner = code >> 4, j = code & 15;
-      const int row = (j & 3) + 8 * (j >> 2) + 4 * (owner >> 5);
-      const unsigned long long md = tM[row];
-      const unsigned long long mro = smr[wave * 32 + (owner & 31)];
-      const int present = F - __builtin_popcountll(mro | md);
-      // knn_donor_kernel's masked direct differences, same order and roundings
-      const float4* xd4 = reinterpret_cast<const float4*>(tY + row * LD);
-      const float4* xr4 = reinterpret_cast<const float4*>(xs[wave * 32 + (owner & 31)]);
-      const unsigned long long both = ~(mro | md);
-      const unsigned blo = (unsigned)both, bhi = (unsigned)(both >> 32);
-      float sa = 0.f, sb = 0.f;
-#pragma unroll
-      for (int q = 0; q < LD / 4; ++q) {
-        const float4 v = xd4[q];
-        const float4 u = xr4[q];
-        const unsigned bqm = ((4 * q < 32 ? blo >> (4 * q) : bhi >> (4 * q - 32))) & 0xFu;
-        const float a = (bqm & 1u) ? u.x - v.x : 0.f;
-        const float b = (bqm & 2u) ? u.y - v.y : 0.f;
-        const float cc = (bqm & 4u) ? u.z - v.z : 0.f;
-        const float d = (bqm & 8u) ? u.w - v.w : 0.f;
-        sa = fmaf(a, a, sa);
-        sb = fmaf(b, b, sb);
-        sa = fmaf(cc, cc, sa);
-        sb = fmaf(d, d, sb);
-      }
-      dbuf[wave][code] = fmaxf(sa + sb, 0.f) * s_scale[present];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (c) each lane folds its own candidates into its slots in donor order
+    if (__ballot(qlen + __builtin_popcount(cand) > kQc) != 0ull) flush();
     while (cand) {
       const int j = __builtin_ctz(cand);
       cand &= cand - 1u;
-      const float dist = dbuf[wave][(lane << 4) | j];
-      if (!(dist < bmax)) continue;
-      const int row = (j & 3) + 8 * (j >> 2) + 4 * hh;
-      const unsigned long long md = tM[row];
-      const int di = d0 + row;
-      float mx = 0.f;
-#pragma unroll
-      for (int k = 0; k < kKnnSlots; ++k) {
-        if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist < b2[k]) {
-          const bool nb = dist < bd[k];
-          b2[k] = nb ? bd[k] : dist;
-          bi[k] = nb ? di : bi[k];
-          bd[k] = nb ? dist : bd[k];
-        }
-        if (col[k] >= 0) mx = fmaxf(mx, b2[k]);
-      }
-      bmax = mx;
+      q_idx[wave][lane][qlen++] = d0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
     }
   }
+  flush();
   if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
 }
 
@@ -810,7 +816,8 @@ void knn_donors_mfma(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_
   hipStream_t st = as_stream(stream);
   HFENS_CHECK(hipMemsetAsync((void*)best, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned long long), st));
   HFENS_CHECK(hipMemsetAsync((void*)alt, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned), st));
-  const int rb = (nr + 255) / 256;
+  const int rpb = knn_mf_fm(F) >= 48 ? 128 : 256;   // receivers per workgroup (32 per wave)
+  const int rb = (nr + rpb - 1) / rpb;
   // ≈ kWgs workgroups (two 8-wave workgroups fill a CU at this kernel's occupancy), ≥ kMinPer donors each
   // (scan: profiles/r5_runs/knn_mfma_grid.log)
   static const int kWgs = getenv("HFENS_KNN_MFMA_WGS") ? atoi(getenv("HFENS_KNN_MFMA_WGS")) : 512;
@@ -829,7 +836,8 @@ void knn_donors_mfma(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_
     using K = KnnMf<FM>;
     const unsigned short* it = (const unsigned short*)items;
     const float* rows = reinterpret_cast<const float*>(it + (size_t)nd * K::LP);
-    hipLaunchKernelGGL(knn_donor_mfma_kernel<FM>, dim3(rb, nsp), dim3(512), 0, st, (const float*)R,
+    static_assert(32 * K::WAVES == (FM >= 48 ? 128 : 256), "receivers per workgroup");
+    hipLaunchKernelGGL(knn_donor_mfma_kernel<FM>, dim3(rb, nsp), dim3(64 * K::WAVES), 0, st, (const float*)R,
                        (const unsigned long long*)rmask, nr, rows, (const unsigned long long*)dmask, nd, F, per,
                        (const int*)slot_col, (unsigned long long*)best, (unsigned*)alt, (const int*)cnt, s0, it,
                        (const float*)ny);
