@@ -104,8 +104,11 @@ NATIVE_SYRK = os.environ.get("HFENS_WSYRK", "0") == "1"
 # Measured at 1M × 512 (profiles/r4_svc_crossover.md): 80 iterations at 15.8 ms against the f64
 # path's 36 at 13.6 ms — late in the solve D⁻¹ spans many decades and the ~1e-7 error in S costs
 # more Newton steps than the cheaper product saves (the Gram is not the per-iteration bottleneck)
-# — so "f64", the library block-upper f64 path, is the default and "f32" is opt-in.
-GRAM = os.environ.get("HFENS_IPM_GRAM", "f64")
+# — so "f32" is opt-in.  "f64x" (default): lowrank.hip wsyrk_f64x — every product and sum f64, Φ
+# read from its exact f32 copy, d ⊙ Φ formed while staging (no scaled copy), 64 × 64 upper tiles
+# only: 4.5 ms per 1M × 428 product against 6.0 ms for "f64", the library block-upper path plus
+# its scaled copy (scripts/probes/ipm_pass_cost.py; max relative difference 2e-15).
+GRAM = os.environ.get("HFENS_IPM_GRAM", "f64x")
 SYRK_BLOCK = int(os.environ.get("HFENS_SYRK_BLOCK", "128"))   # library path: block-upper product (0: full)
 DEBUG = os.environ.get("HFENS_IPM_DEBUG", "0") == "1"   # per-iteration state (synchronising)
 CHECK = os.environ.get("HFENS_IPM_DEBUG", "0") == "2"   # name the first non-finite quantity
@@ -145,6 +148,14 @@ def _weighted_gram(Phi: torch.Tensor, d: torch.Tensor, P32: torch.Tensor = None)
         S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
         ops.ext().wsyrk_f32(P32.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
                             ops.stream_ptr(Phi.device))
+        return S
+    if GRAM == "f64x" and P32 is not None and _native(Phi) and r <= 2048 and r % 4 == 0 and P32.data_ptr() % 16 == 0:
+        from .. import runtime
+        plen = _part_len("wsyrk_part_len", l, r)
+        part = runtime.workspace(Phi.device, _ws_name("wsyrk_part"), plen, torch.float64)
+        S = torch.empty(r, r, dtype=torch.float64, device=Phi.device)
+        ops.ext().wsyrk_f64x(P32.data_ptr(), d.contiguous().data_ptr(), l, r, part.data_ptr(), plen, S.data_ptr(),
+                             ops.stream_ptr(Phi.device))
         return S
     if NATIVE_SYRK and _native(Phi) and r <= 2048:
         from .. import runtime

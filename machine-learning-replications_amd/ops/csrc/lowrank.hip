@@ -274,6 +274,124 @@ __global__ __launch_bounds__(kSyThreads) void wsyrk_f32_kernel(const float* __re
       }
 }
 
+// ---- wsyrk_f64x: the f64 product read from the exact f32 copy of Φ -------------
+// 64 × 64 output tiles (upper triangle only: 28 tiles for r = 428, padding (448/428)² instead of
+// the 128-tile kernels' 40 blocks of 64²), 4 waves of 32 × 32 (2 × 2 f64 MFMA 16x16x4 blocks; the
+// wave below the diagonal of a diagonal tile skips, the reduction reads only j ≥ i there), 32-row
+// slabs staged through LDS with the next slab's loads in flight under this slab's MFMAs.  Φ is read as
+// f32 (exact; half the bytes) and widened while staging; d ⊙ Φ is formed in f64; every product and
+// sum is f64 — only the summation order differs from the library path.  Row groups (split-K) are
+// XCD-aware as in wsyrk_f64_kernel; partial tiles are summed in group order (deterministic).
+constexpr int kXT = 64;
+constexpr int kXKC = 32;
+constexpr int kXLd = kXT + 2;   // padded LDS row (f64)
+
+__global__ __launch_bounds__(kSyThreads, 2) void wsyrk_f64x_kernel(const float* __restrict__ Phi,
+                                                                    const double* __restrict__ d, long long n, int r,
+                                                                    int nt, int T, int G, long long rows_per_group,
+                                                                    double* __restrict__ part) {
+  __shared__ double As[kXKC][kXLd];
+  __shared__ double Bs[kXKC][kXLd];
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int gi = xcd + 8 * (q / T), tile = q % T;
+  if (gi >= G) return;
+  int t = tile, I = 0;
+  while (t >= nt - I) { t -= nt - I; ++I; }
+  const int J = I + t;
+  const int c0a = I * kXT, c0b = J * kXT;
+  const long long r0 = (long long)gi * rows_per_group, r1 = min(n, r0 + rows_per_group);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  const bool active = c0a + wr < r && c0b + wc < r && !(I == J && wr > wc);   // wave-uniform
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // staging: 32 rows × 64 columns per operand = 512 float4, 2 per thread per operand
+  f32x4 va[2], vb[2];
+  double vd[2];
+  long long lrow0 = r0;
+  auto load = [&](long long row0) {
+    lrow0 = row0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * kSyThreads;
+      const int rr = e >> 4, c4 = (e & 15) * 4;
+      const long long row = min(row0 + rr, r1 - 1);
+      const float* pr = Phi + row * r;
+      va[u] = *reinterpret_cast<const f32x4*>(pr + min(c0a + c4, r - 4));
+      vb[u] = *reinterpret_cast<const f32x4*>(pr + min(c0b + c4, r - 4));
+      vd[u] = d[row];
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * kSyThreads;
+      const int rr = e >> 4, c4 = (e & 15) * 4;
+      const bool ok = lrow0 + rr < r1;
+      const bool oka = ok && c0a + c4 < r, okb = ok && c0b + c4 < r;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        As[rr][c4 + k] = oka ? (double)va[u][k] : 0.0;
+        Bs[rr][c4 + k] = okb ? vd[u] * (double)vb[u][k] : 0.0;
+      }
+    }
+  };
+  if (r0 < r1) load(r0);
+  for (long long row0 = r0; row0 < r1; row0 += kXKC) {
+    __syncthreads();   // the previous slab's operand reads are done
+    store();
+    __syncthreads();
+    if (row0 + kXKC < r1) load(row0 + kXKC);   // the next slab's loads fly under this slab's MFMAs
+    if (active) {
+#pragma unroll
+      for (int ks = 0; ks < kXKC / 4; ++ks) {
+        const int kr = 4 * ks + (lane >> 4);
+        double a[2], b[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          a[p] = As[kr][wr + 16 * p + (lane & 15)];
+          b[p] = Bs[kr][wc + 16 * p + (lane & 15)];
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) acc[p][qq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[qq], acc[p][qq], 0, 0, 0);
+      }
+    }
+  }
+  double* out = part + ((size_t)gi * T + tile) * kXT * kXT;
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int row = wr + 16 * p + (lane >> 4) + 4 * reg;
+        const int col = wc + 16 * qq + (lane & 15);
+        out[row * kXT + col] = active ? acc[p][qq][reg] : 0.0;
+      }
+}
+
+__global__ __launch_bounds__(256) void wsyrk_x_reduce_kernel(const double* __restrict__ part, int G, int T, int nt,
+                                                             int r, double* __restrict__ S) {
+  int t = blockIdx.x, I = 0;
+  while (t >= nt - I) { t -= nt - I; ++I; }
+  const int J = I + t;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < kXT * kXT; e += gridDim.y * 256) {
+    const int row = e / kXT, col = e % kXT;
+    const int i = I * kXT + row, j = J * kXT + col;
+    if (i >= r || j >= r) continue;
+    if (I == J && j < i) continue;
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += part[((size_t)g * T + blockIdx.x) * kXT * kXT + e];
+    S[(size_t)i * r + j] = s;
+    S[(size_t)j * r + i] = s;
+  }
+}
+
 // row groups of the split-K (the partial buffer is sized from wsyrk_part_len below)
 static int wsyrk_groups(long long n, int T) {
   int dev = 0, ncu = 256;
@@ -289,7 +407,12 @@ static int wsyrk_groups(long long n, int T) {
 // workspaces from these, never from a copy of the rules
 void wsyrk_part_len(long long n, int r, uintptr_t out) {
   const int nt = (r + kSyT - 1) / kSyT, T = nt * (nt + 1) / 2;
-  *reinterpret_cast<long long*>(out) = (long long)wsyrk_groups(n, T) * T * kSyT * kSyT;
+  long long len = (long long)wsyrk_groups(n, T) * T * kSyT * kSyT;
+  // the 64-tile kernel's partials (wsyrk_f64x): ≤ its workgroup budget + one group of tiles
+  const int ntx = (r + 63) / 64, Tx = ntx * (ntx + 1) / 2;
+  const int wgs = getenv("HFENS_WSYRKX_WGS") ? atoi(getenv("HFENS_WSYRKX_WGS")) : 2048;
+  const long long lx = (long long)((wgs + Tx - 1) / Tx) * Tx * 64 * 64;
+  *reinterpret_cast<long long*>(out) = len > lx ? len : lx;
 }
 
 // launch shape of the skinny passes: rows in flight per thread / wave, and the grid (sweep knobs
@@ -385,6 +508,31 @@ void wsyrk_f32(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, l
                      (const double*)d, n, r, nt, T, G, per, (double*)part);
   launch_check();
   hipLaunchKernelGGL(wsyrk_reduce_kernel, dim3(T, 16), dim3(256), 0, st, (const double*)part, G, T, nt, r,
+                     (double*)S);
+  launch_check();
+}
+
+// S = Φᵀ diag(d) Φ in f64 from the exact f32 copy of Φ (wsyrk_f64x_kernel); the same partial layout,
+// row groups and reduction as wsyrk_f64 (part_len from wsyrk_part_len).
+void wsyrk_f64x(uintptr_t Phi, uintptr_t d, long long n, int r, uintptr_t part, long long part_len, uintptr_t S,
+                uintptr_t stream) {
+  HFENS_REQUIRE(n >= 1 && r >= 4 && r <= 2048 && r % 4 == 0, "wsyrk_f64x: n >= 1, 4 <= r <= 2048, r % 4 == 0");
+  HFENS_REQUIRE((Phi & 15) == 0, "wsyrk_f64x: Φ must be 16-byte aligned");
+  const int nt = (r + kXT - 1) / kXT, T = nt * (nt + 1) / 2;
+  static const int kWgs = getenv("HFENS_WSYRKX_WGS") ? atoi(getenv("HFENS_WSYRKX_WGS")) : 2048;
+  long long G = (kWgs + T - 1) / T;
+  const long long max_g = (n + 4 * kXKC - 1) / (4 * kXKC);
+  if (G > max_g) G = max_g;
+  if (G < 1) G = 1;
+  HFENS_REQUIRE(part_len >= G * T * kXT * kXT, "wsyrk_f64x: partial buffer too small");
+  long long per = (n + G - 1) / G;
+  per = (per + kXKC - 1) / kXKC * kXKC;
+  hipStream_t st = as_stream(stream);
+  const long long blocks = 8LL * ((G + 7) / 8) * T;
+  hipLaunchKernelGGL(wsyrk_f64x_kernel, dim3((unsigned)blocks), dim3(kSyThreads), 0, st, (const float*)Phi,
+                     (const double*)d, n, r, nt, T, (int)G, per, (double*)part);
+  launch_check();
+  hipLaunchKernelGGL(wsyrk_x_reduce_kernel, dim3(T, 4), dim3(256), 0, st, (const double*)part, (int)G, T, nt, r,
                      (double*)S);
   launch_check();
 }

@@ -196,9 +196,31 @@ def test_wsyrk_f32_matches_f64(dev, monkeypatch, n, r):
     assert torch.equal(S, _weighted_gram(Phi, d, P32))      # deterministic
 
 
+@pytest.mark.parametrize("n,r", [(37, 16), (20011, 428), (70000, 512), (5000, 132), (3000, 2048)])
+def test_wsyrk_f64x_matches_f64(dev, monkeypatch, n, r):
+    """The native f64 weighted SYRK from the exact f32 copy of Φ (lowrank.hip wsyrk_f64x: 64 × 64
+    upper tiles, f64 MFMA, split-K summed in group order) against torch's f64 product: every entry
+    within 1e-13 of the magnitude of its terms (f64 sums in another order), symmetric, deterministic."""
+    from hfens.models import svc_lowrank
+    from hfens.models.svc_lowrank import _weighted_gram
+    monkeypatch.setattr(svc_lowrank, "GRAM", "f64x")
+    g = torch.Generator(device=dev).manual_seed(7 * n + r)
+    P32 = torch.randn(n, r, generator=g, device=dev, dtype=torch.float32)
+    Phi = P32.double()
+    d = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 10 ** torch.randint(-6, 6, (n,), generator=g, device=dev)
+    S = _weighted_gram(Phi, d, P32)
+    want = Phi.T @ (d[:, None] * Phi)
+    mag = Phi.abs().T @ (d[:, None] * Phi.abs())
+    assert torch.equal(S, S.T)
+    err = float(((S - want).abs() / mag).max())
+    assert err < 1e-13, err
+    assert torch.equal(S, _weighted_gram(Phi, d, P32))      # deterministic
+
+
 def test_ipm_f32_gram_matches_f64_path(dev, monkeypatch):
-    """The interior point with the f32-MFMA Gram in its Newton systems (the default) converges to the
-    f64 path's optimum: same stopping test (f64 residuals), dual coefficients and ρ within 1e-6."""
+    """The interior point with the f32-MFMA Gram in its Newton systems (opt-in) converges to the
+    f64 path's optimum: same stopping test (f64 residuals), dual coefficients and ρ within 1e-6; the
+    default native f64 Gram (wsyrk_f64x) follows the library f64 path to rounding."""
     from hfens.io.synth import make_hf_cohort
     from hfens.models import svc_lowrank
     X, y, _ = make_hf_cohort(30000, 17, seed=5, nan_frac=0.0)
@@ -211,11 +233,16 @@ def test_ipm_f32_gram_matches_f64_path(dev, monkeypatch):
     yv = torch.as_tensor(np.where(y > 0.5, -1.0, 1.0), device=dev)
     c = torch.where(yv > 0, 0.62, 2.5).to(torch.float64)
     out = {}
-    for mode in ("f64", "f32"):
+    for mode in ("f64", "f32", "f64x"):
         monkeypatch.setattr(svc_lowrank, "GRAM", mode)
         a, rho, it = svc_lowrank.ipm_svc_dual(Phi, yv, c)
         out[mode] = (a, rho, it)
     a64, rho64, it64 = out["f64"]
+    ax, rhox, itx = out["f64x"]
+    assert abs(itx - it64) <= 1, (itx, it64)
+    w64, wx = Phi.T @ (yv * a64), Phi.T @ (yv * ax)
+    assert float((wx - w64).abs().max() / w64.abs().max()) <= 1e-6
+    assert abs(rhox - rho64) <= 1e-7, (rhox, rho64)
     a32, rho32, it32 = out["f32"]
     assert it32 <= it64 + 5, (it32, it64)
     # Q = diag(y) Φ Φᵀ diag(y) has rank ≤ 256 < l: the dual optimum α is not unique, the model is —
