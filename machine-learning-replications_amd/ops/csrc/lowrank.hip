@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kSyThreads) void wsyrk_f32_kernel(const float* __re
 // XCD-aware as in wsyrk_f64_kernel; partial tiles are summed in group order (deterministic).
 constexpr int kXT = 64;
 constexpr int kXKC = 32;
-constexpr int kXLd = kXT + 2;   // padded LDS row (f64)
+constexpr int kXLd = kXT + 16;  // padded LDS row (f64): rows 32 banks apart, each half-wave read conflict-free
 
 __global__ __launch_bounds__(kSyThreads, 2) void wsyrk_f64x_kernel(const float* __restrict__ Phi,
                                                                     const double* __restrict__ d, long long n, int r,

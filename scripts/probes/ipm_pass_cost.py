@@ -35,6 +35,7 @@ for k in (1, 2):
     print(f"phi_gemv_f32 k={k}: {ms:.3f} ms  {(l * r * 4 + l * k * 8) / ms / 1e9:.2f} TB/s", flush=True)
     ms = t(lambda: sl._phit(Phi, V, P32))
     print(f"phit_f32 k={k}: {ms:.3f} ms  {(l * r * 4 + l * k * 8) / ms / 1e9:.2f} TB/s", flush=True)
+sl.GRAM = "f64"
 for bs in (128, 96, 64, 32):
     sl.SYRK_BLOCK = bs
     ms = t(lambda: sl._weighted_gram(Phi, d, P32), 5)
