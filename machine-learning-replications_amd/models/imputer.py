@@ -215,7 +215,8 @@ class KNNImputer(Estimator):
                              slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), cnt.data_ptr(), g * SLOTS, s)
             E.knn_refine(R32.data_ptr(), rbits.data_ptr(), n, D32.data_ptr(), dm.data_ptr(), nd, F,
                          slot[g].data_ptr(), best[g].data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
-                         Mx.data_ptr(), work.data_ptr(), cap, cnt.data_ptr(), g * SLOTS, s)
+                         Mx.data_ptr(), work.data_ptr(), cap, cnt.data_ptr(), g * SLOTS,
+                         mf[0].data_ptr() if mf is not None else 0, mf[1].data_ptr() if mf is not None else 0, s)
         fx = self._fit_X if self._fit_X.is_contiguous() else self._fit_X.contiguous()
         E.knn_apply(Xc.data_ptr(), n, F, rows.data_ptr(), slot.data_ptr(), best.data_ptr(), fx.data_ptr(),
                     self._col_mean.data_ptr(), cnt.data_ptr(), s)
@@ -334,7 +335,7 @@ class KNNImputer(Estimator):
                 # (knn.hip knn_refine) — the donors then equal the host mirror's f64 choice
                 E.knn_refine(R32.data_ptr(), rm.data_ptr(), nr, D32.data_ptr(), dm.data_ptr(), D32.shape[0], F,
                              slot.data_ptr(), blk.data_ptr(), alt.data_ptr(), R64.data_ptr(), D64.data_ptr(),
-                             Mx.data_ptr(), work.data_ptr(), cap, 0, 0, ops.stream_ptr(dev))
+                             Mx.data_ptr(), work.data_ptr(), cap, 0, 0, 0, 0, ops.stream_ptr(dev))
                 if KNN_DEBUG:   # re-scanned receivers, window pairs, overflow, pass-1 receivers (synchronising)
                     o = 4 * cap + 8 * nr * SLOTS + 2 * nr
                     LAST_REFINE.append((nr, int(work[o]), int(work[o + 8]), int(work[o + 9]), int(work[o + 4]),

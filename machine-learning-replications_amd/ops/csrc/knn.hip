@@ -517,15 +517,24 @@ __global__ __launch_bounds__(256) void knn_mfma_prep_kernel(const float* __restr
   ny[d] = nsum;
 }
 
-template <int FM>
+// MODE 1 (knn_refine's window listing, the role of knn_cand_kernel<·, 0>): the receivers are
+// rlist[0 … counts[0]), each slot k has a fixed window thr[k] (≥ 0: listed), and every (slot, donor)
+// with exact f32 distance ≤ thr[k] is appended to pairs (pcount[0]; overflow → pcount[1]) — the same
+// pairs knn_cand_kernel lists (the matrix-core bound only skips donors above every window)
+template <int FM, int MODE = 0>
 __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     const float* __restrict__ R, const unsigned long long* __restrict__ rmask, int nr,
     const float* __restrict__ rowsFM, const unsigned long long* __restrict__ dmask, int nd, int F,
     int per_split, const int* __restrict__ slot_col, unsigned long long* __restrict__ best,
     unsigned* __restrict__ alt, const int* __restrict__ cnt, int s0,
-    const unsigned short* __restrict__ items, const float* __restrict__ ny_all) {
+    const unsigned short* __restrict__ items, const float* __restrict__ ny_all,
+    const int* __restrict__ rlist = nullptr, const float* __restrict__ thr = nullptr,
+    int* __restrict__ pairs = nullptr, long long cap = 0, int* __restrict__ pcount = nullptr) {
   using K = KnnMf<FM>;
-  if (cnt != nullptr) {
+  if constexpr (MODE == 1) {
+    nr = cnt[0];
+    if ((int)blockIdx.x * (32 * K::WAVES) >= nr) return;
+  } else if (cnt != nullptr) {
     if (s0 >= cnt[1]) return;
     nr = cnt[0];
   }
@@ -538,8 +547,9 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
   __shared__ __attribute__((aligned(16))) float tNy[K::TILE];
   __shared__ float s_scale[65];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
-  const int r = blockIdx.x * (32 * K::WAVES) + wave * 32 + r32;
-  const bool active = r < nr;
+  const int li = blockIdx.x * (32 * K::WAVES) + wave * 32 + r32;
+  const bool active = li < nr;
+  const int r = MODE == 1 ? (active ? rlist[li] : 0) : li;
   const int d_begin = blockIdx.y * per_split;
   const int d_end = min(nd, d_begin + per_split);
   const unsigned long long mr = active ? rmask[r] : 0ull;
@@ -587,22 +597,32 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     bq[m] = __builtin_bit_cast(knn_bf16x8, (knn_u32x4){w[0], w[1], w[2], w[3]});
   }
   int col[kKnnSlots];
-  float bd[kKnnSlots], b2[kKnnSlots];
+  float bd[kKnnSlots], b2[kKnnSlots];   // MODE 1: b2 holds the slot's window
   int bi[kKnnSlots];
   bool any = false;
+  float tmax = -1.f;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k) {
-    col[k] = active ? slot_col[(size_t)r * kKnnSlots + k] : -1;
+    const size_t e = (size_t)r * kKnnSlots + k;
     bd[k] = INFINITY;
     b2[k] = INFINITY;
     bi[k] = -1;
+    if constexpr (MODE == 1) {
+      const float t = active ? thr[e] : -1.f;
+      col[k] = t >= 0.f ? slot_col[e] : -1;
+      b2[k] = t;
+      if (col[k] >= 0) tmax = fmaxf(tmax, t);
+    } else {
+      col[k] = active ? slot_col[e] : -1;
+    }
     any |= col[k] >= 0;
   }
   unsigned long long need = 0ull;
 #pragma unroll
   for (int k = 0; k < kKnnSlots; ++k)
     if (col[k] >= 0) need |= 1ull << col[k];
-  float bmax = INFINITY;
+  // MODE 1: the windows are fixed; ×(1 + 2⁻²⁰) so the strict tests below keep a pair at the window
+  float bmax = MODE == 1 ? (tmax >= 0.f ? tmax * 1.00000095f : -1.f) : INFINITY;
   if (tid <= 64) s_scale[tid] = tid > 0 ? (float)F / (float)tid : 0.f;
   const float fF = (float)F * 0.99999905f;
   const bool wave_any = __ballot(any) != 0ull;
@@ -684,6 +704,23 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int e = 0; e < mine; ++e) {
       const float dist = q_dist[wave][lane][e];
+      if constexpr (MODE == 1) {
+        const int di = q_idx[wave][lane][e];
+        const unsigned long long md = dmask[di];
+#pragma unroll
+        for (int k = 0; k < kKnnSlots; ++k) {
+          if (col[k] >= 0 && !((md >> col[k]) & 1ull) && dist <= b2[k]) {
+            const int p = atomicAdd(&pcount[0], 1);
+            if (p < cap) {
+              pairs[2 * (size_t)p] = (int)((size_t)r * kKnnSlots + k);
+              pairs[2 * (size_t)p + 1] = di;
+            } else {
+              pcount[1] = 1;
+            }
+          }
+        }
+        continue;
+      }
       if (!(dist < bmax)) continue;
       const int di = q_idx[wave][lane][e];
       const unsigned long long md = dmask[di];
@@ -776,7 +813,8 @@ __global__ __launch_bounds__(512) void knn_donor_mfma_kernel(
     }
   }
   flush();
-  if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
+  if constexpr (MODE == 0)
+    if (active) knn_merge_slots(best, alt, r, bd, b2, bi);
 }
 
 // 32-bit words per donor of the prep buffer (bf16 items, then the FM-strided zero-filled f32 row) → *out
@@ -1124,9 +1162,35 @@ __global__ __launch_bounds__(256) void knn_commit_kernel(const int* __restrict__
 }
 
 // work: 8-byte aligned scratch of knn_refine_work_words(nr) int32 words
+// items / ny: knn_mfma_prep of the donors (0: none) — the window listing then runs on the matrix-core
+// filter (knn_donor_mfma_kernel<·, 1>) instead of knn_cand_kernel's packed-FMA scan
+static int knn_mf_fm(int F);
+template <int FM>
+static void knn_cand_mfma(const float* R, const unsigned long long* rmask, int nr, const unsigned long long* dmask,
+                          int nd, int F, const int* slot_col, const int* rlist, const int* counts, const float* thr,
+                          int* pairs, long long cap, int* pcount, const unsigned short* items, const float* ny,
+                          hipStream_t st) {
+  using K = KnnMf<FM>;
+  const int rpb = 32 * K::WAVES;
+  const int rb = (nr + rpb - 1) / rpb;
+  int splits = (nd + 16383) / 16384;
+  if (splits < 64) splits = 64;
+  const int max_splits = (nd + 255) / 256;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int per = (nd + splits - 1) / splits;
+  per = (per + 31) / 32 * 32;
+  const int nsp = (nd + per - 1) / per;
+  const float* rows = reinterpret_cast<const float*>(items + (size_t)nd * K::LP);
+  hipLaunchKernelGGL((knn_donor_mfma_kernel<FM, 1>), dim3(rb, nsp), dim3(64 * K::WAVES), 0, st, R, rmask, nr, rows,
+                     dmask, nd, F, per, slot_col, (unsigned long long*)nullptr, (unsigned*)nullptr, counts, 0, items,
+                     ny, rlist, thr, pairs, cap, pcount);
+}
+
 void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dmask, int nd, int F,
                 uintptr_t slot_col, uintptr_t best, uintptr_t alt, uintptr_t R64, uintptr_t D64, uintptr_t Mx,
-                uintptr_t work, long long cap, uintptr_t cnt, int s0, uintptr_t stream) {
+                uintptr_t work, long long cap, uintptr_t cnt, int s0, uintptr_t items, uintptr_t ny,
+                uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "knn_refine: 1 <= F <= 64");
   HFENS_REQUIRE((work & 7) == 0 && cap >= 1, "knn_refine: work must be 8-byte aligned, cap >= 1");
   if (nr == 0 || nd == 0) return;
@@ -1178,7 +1242,23 @@ void knn_refine(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_t dma
                          nd, F, per, (const int*)slot_col, th, (const double*)R64, (const double*)D64, dmin, didx,
                          (const unsigned long long*)dwin, didx2, pairs, cap, pcount);
     };
-    cand(std::integral_constant<int, 0>{}, rlist, counts, thr);          // list the window pairs
+    if (items != 0 && F <= 48) {                                          // list the window pairs
+      const int fm = knn_mf_fm(F);
+      auto mf = [&](auto k) {
+        knn_cand_mfma<decltype(k)::value>((const float*)R, (const unsigned long long*)rmask, nr,
+                                          (const unsigned long long*)dmask, nd, F, (const int*)slot_col, rlist,
+                                          counts, thr, pairs, cap, pcount, (const unsigned short*)items,
+                                          (const float*)ny, st);
+      };
+      if (fm == 16) mf(std::integral_constant<int, 16>{});
+      else if (fm == 24) mf(std::integral_constant<int, 24>{});
+      else if (fm == 32) mf(std::integral_constant<int, 32>{});
+      else if (fm == 40) mf(std::integral_constant<int, 40>{});
+      else mf(std::integral_constant<int, 48>{});
+      launch_check();
+    } else {
+      cand(std::integral_constant<int, 0>{}, rlist, counts, thr);
+    }
     hipLaunchKernelGGL(knn_eval_kernel<0>, dim3(eg), dim3(256), 0, st, (const int*)pairs, (const int*)pcount, cap,
                        (const int*)slot_col, (const double*)R64, (const unsigned long long*)rmask, (const double*)D64,
                        (const unsigned long long*)dmask, F, keys, dmin, (const unsigned long long*)dwin, didx,

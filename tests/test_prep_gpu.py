@@ -11,8 +11,13 @@ from hfens import ops
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("mfma", ["auto", "1"])
 @pytest.mark.parametrize("n,F,nan", [(3000, 40, 0.02), (700, 64, 0.05), (500, 17, 0.3), (6000, 40, 0.05)])
-def test_knn_imputer_device_matches_host(dev, n, F, nan):
+def test_knn_imputer_device_matches_host(dev, monkeypatch, n, F, nan, mfma):
+    """The device imputation equals the host f64 mirror bit for bit — with the packed-FMA search
+    and with the matrix-core filter forced (its donor search AND its f64-refine window listing)."""
+    from hfens.models import imputer as imp_mod
+    monkeypatch.setattr(imp_mod, "MFMA_FILTER", mfma)
     X, _, _ = make_hf_cohort(n, F, seed=n + F, nan_frac=nan)
     X = np.concatenate([X, X[: n // 20] + 1e-9 * (n % 7)], axis=0)   # near-duplicate donors: f32 near-ties
     Xt = torch.as_tensor(X)
@@ -142,6 +147,7 @@ def test_knn_imputer_mfma_same_output(dev, monkeypatch):
     from hfens.models import imputer as imp_mod
     from hfens.models.imputer import KNNImputer
     X, _, _ = make_hf_cohort(20000, 40, seed=5, nan_frac=0.03)
+    X = np.concatenate([X, X[:1500] + 1e-9], axis=0)   # near-duplicate donors: the f64 refine's windows
     Xt = torch.as_tensor(X, device=dev)
     out = {}
     for mode in ("0", "1"):
