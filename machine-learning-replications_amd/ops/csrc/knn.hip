@@ -860,8 +860,13 @@ void knn_donors_mfma(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_
   // (scan: profiles/r5_runs/knn_mfma_grid.log)
   static const int kWgs = getenv("HFENS_KNN_MFMA_WGS") ? atoi(getenv("HFENS_KNN_MFMA_WGS")) : 512;
   static const int kMinPer = getenv("HFENS_KNN_MFMA_MINPER") ? atoi(getenv("HFENS_KNN_MFMA_MINPER")) : 256;
+  // no cap on a split's donor range: each split restarts the slots' filling phase (every donor a
+  // candidate until the slots hold two), which at 1M rows cost more than the grid's width gained
+  // (1M-row imputation 0.81 s at ≤ 16,384 donors per split, 0.71 at 32,768, 0.58 unsplit:
+  // profiles/r5_runs/knn_split_range.log)
+  static const int kRange = getenv("HFENS_KNN_MFMA_RANGE") ? atoi(getenv("HFENS_KNN_MFMA_RANGE")) : (1 << 30);
   int splits = kWgs / rb;
-  const int by_range = (nd + 16383) / 16384;
+  const int by_range = (nd + kRange - 1) / kRange;
   if (splits < by_range) splits = by_range;
   const int max_splits = (nd + kMinPer - 1) / kMinPer;
   if (splits > max_splits) splits = max_splits;
