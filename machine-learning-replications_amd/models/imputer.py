@@ -21,12 +21,11 @@ from .base import Estimator, as_tensor
 SLOTS = 8
 # the donor search's filter on the bf16 matrix cores (knn.hip knn_donor_mfma_kernel; the exact
 # direct-difference pass decides every slot as before, so the slots are the same bits): HFENS_KNN_MFMA
-# "auto" (default) takes it from MFMA_MIN_PAIRS rows × donors — 621 / 760 / 811 vs 260 / 309 / 347
-# G pairs/s of the packed-FMA filter at 50k / 100k / 300k rows, but 0.48 vs 0.42 ms on a 10k-row
-# cohort, where the per-workgroup operand build and the slot-filling phase dominate
-# (profiles/r5_knn_mfma.md); "1" always, "0" never
+# "auto" (default) takes it from MFMA_MIN_PAIRS rows × donors — 0.35 / 0.40 / 0.70 / 6.3 / 43.6 ms
+# against 0.41 / 0.42 / 1.22 / 18.0 / 142.6 ms for the packed-FMA filter at 8k / 10k / 20k / 100k /
+# 300k rows (profiles/r5_knn_mfma.md); "1" always, "0" never
 MFMA_FILTER = os.environ.get("HFENS_KNN_MFMA", "auto")
-MFMA_MIN_PAIRS = 1 << 28
+MFMA_MIN_PAIRS = 1 << 24
 # f64-exact donors on the device (knn.hip knn_refine): the f32 search's near-ties re-decided in f64
 EXACT = __import__("os").environ.get("HFENS_KNN_EXACT", "1") != "0"
 KNN_DEBUG = __import__("os").environ.get("HFENS_KNN_DEBUG", "0") == "1"

@@ -856,9 +856,9 @@ void knn_donors_mfma(uintptr_t R, uintptr_t rmask, int nr, uintptr_t D, uintptr_
   HFENS_CHECK(hipMemsetAsync((void*)alt, 0xFF, (size_t)nr * kKnnSlots * sizeof(unsigned), st));
   const int rpb = knn_mf_fm(F) >= 48 ? 128 : 256;   // receivers per workgroup (32 per wave)
   const int rb = (nr + rpb - 1) / rpb;
-  // ≈ kWgs workgroups (two 8-wave workgroups fill a CU at this kernel's occupancy), ≥ kMinPer donors each
-  // (scan: profiles/r5_runs/knn_mfma_grid.log)
-  static const int kWgs = getenv("HFENS_KNN_MFMA_WGS") ? atoi(getenv("HFENS_KNN_MFMA_WGS")) : 512;
+  // ≈ kWgs workgroups, ≥ kMinPer donors each: fewer, longer splits (each restarts the slots' filling
+  // phase) beat a fuller grid down to 8k rows (scans: profiles/r5_runs/knn_mfma_grid.log, knn_mfma_small.log)
+  static const int kWgs = getenv("HFENS_KNN_MFMA_WGS") ? atoi(getenv("HFENS_KNN_MFMA_WGS")) : 256;
   static const int kMinPer = getenv("HFENS_KNN_MFMA_MINPER") ? atoi(getenv("HFENS_KNN_MFMA_MINPER")) : 256;
   // no cap on a split's donor range: each split restarts the slots' filling phase (every donor a
   // candidate until the slots hold two), which at 1M rows cost more than the grid's width gained
