@@ -1216,11 +1216,20 @@ __global__ __launch_bounds__(256) void ws_seed_kernel(const WsProb* __restrict__
                                                       const float* __restrict__ zn_all,
                                                       const double* __restrict__ aseed,
                                                       double* __restrict__ alpha_all,
-                                                      double* __restrict__ G_all, WsAux X) {
+                                                      double* __restrict__ G_all, WsAux X,
+                                                      double* __restrict__ part, int max_l, int cols_per_split) {
   const int b = blockIdx.y;
   const WsProb P = probs[b];
   const int row_blk = blockIdx.x * 256;
   if (row_blk >= P.l) return;
+  // split-K over the columns (gridDim.z > 1): this workgroup's column range, partial sums to part
+  const int c_begin = blockIdx.z * cols_per_split;
+  const int c_end = min(P.l, c_begin + cols_per_split);
+  if (gridDim.z > 1 && c_begin >= P.l) {
+    const int row = row_blk + threadIdx.x;
+    if (row < P.l) part[((size_t)blockIdx.z * gridDim.y + b) * max_l + row] = 0.0;
+    return;
+  }
   __shared__ __attribute__((aligned(16))) float sv_l[2 * KS * kWsChunk];
   __shared__ __attribute__((aligned(16))) float sn_l[kWsChunk];
   __shared__ __attribute__((aligned(16))) float cf_l[kWsChunk];
@@ -1247,9 +1256,9 @@ __global__ __launch_bounds__(256) void ws_seed_kernel(const WsProb* __restrict__
   const float zsb = rb < P.l ? P.ngl2e * zn_all[P.aoff + rb] : 0.f;
   const float k2 = -2.f * P.ngl2e;
   double da = 0.0, db = 0.0;
-  for (int c0 = 0; c0 < P.l; c0 += kWsChunk) {
+  for (int c0 = c_begin; c0 < c_end; c0 += kWsChunk) {
     const int c = c0 + tid;
-    const double ac = c < P.l ? aseed[P.aoff + c] : 0.0;
+    const double ac = c < c_end ? aseed[P.aoff + c] : 0.0;
     const bool nz = ac > 0.0;
     const unsigned long long m = __ballot(nz);
     __syncthreads();   // the previous chunk is consumed
@@ -1307,9 +1316,35 @@ __global__ __launch_bounds__(256) void ws_seed_kernel(const WsProb* __restrict__
   if (!live) return;
   da += __shfl_xor(da, 32, kWave);
   db += __shfl_xor(db, 32, kWave);
+  if (gridDim.z > 1) {
+    if (valid) part[((size_t)blockIdx.z * gridDim.y + b) * max_l + row] = lane < 32 ? da : db;
+    return;
+  }
   double g = -1.0;
   if (valid) {
     const double upd = lane < 32 ? da : db;
+    g = -1.0 + (row < P.npos ? upd : -upd);
+    alpha_all[P.aoff + row] = a;
+    G_all[P.aoff + row] = g;
+  }
+  ws_publish_keys(P, b, row, valid, a, g, X);
+}
+
+// the split-K seed's partial sums in split order (deterministic), then α, G and the keys
+__global__ __launch_bounds__(256) void ws_seed_fin_kernel(const WsProb* __restrict__ probs,
+                                                          const double* __restrict__ aseed,
+                                                          double* __restrict__ alpha_all, double* __restrict__ G_all,
+                                                          WsAux X, const double* __restrict__ part, int max_l, int S) {
+  const int b = blockIdx.y;
+  const WsProb P = probs[b];
+  if ((int)blockIdx.x * 256 >= P.l) return;
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = row < P.l;
+  double g = -1.0, a = 0.0;
+  if (valid) {
+    double upd = 0.0;
+    for (int s = 0; s < S; ++s) upd += part[((size_t)s * gridDim.y + b) * max_l + row];
+    a = aseed[P.aoff + row];
     g = -1.0 + (row < P.npos ? upd : -upd);
     alpha_all[P.aoff + row] = a;
     G_all[P.aoff + row] = g;
@@ -1387,16 +1422,34 @@ void ws_seed(uintptr_t probs, int P, int max_l, uintptr_t zcat, int F, uintptr_t
   hipStream_t st = as_stream(stream);
   // ws_init folded the α = 0 maxima into gkey: the seeded point's replace them
   HFENS_CHECK(hipMemsetAsync(reinterpret_cast<void*>(gkey), 0, sizeof(unsigned long long) * 2 * (size_t)P, st));
-  const dim3 grid((max_l + 255) / 256, P);
+  const int rb = (max_l + 255) / 256;
   const WsAux X = ws_aux(keys, n, gkey);
+  // split-K over the columns when the row blocks alone leave the chip idle (the stacking fit's
+  // 10k-point final problem: 40 workgroups; its seed sat on the critical path for ≈ 0.3 ms):
+  // ≈ 2048 workgroups, whole 256-column chunks per split, partials summed in split order
+  const int nchunk = (max_l + kWsChunk - 1) / kWsChunk;
+  int S = (2048 + rb * P - 1) / (rb * P);
+  if (S > nchunk) S = nchunk;
+  if (S < 1) S = 1;
+  const int cps = (nchunk + S - 1) / S * kWsChunk;
+  S = (max_l + cps - 1) / cps;
+  double* part = nullptr;
+  if (S > 1) HFENS_CHECK(hipMallocAsync(reinterpret_cast<void**>(&part), sizeof(double) * (size_t)S * P * max_l, st));
+  const dim3 grid(rb, P, S);
 #define WS_SEED(K)                                                                                   \
   case K:                                                                                           \
     hipLaunchKernelGGL(ws_seed_kernel<K>, grid, dim3(256), 0, st, (const WsProb*)probs, (const float*)zcat, F, \
-                       (const float*)zn, (const double*)aseed, (double*)alpha, (double*)G, X);      \
+                       (const float*)zn, (const double*)aseed, (double*)alpha, (double*)G, X, part, max_l, cps); \
     break;
   switch (ws_ks(F)) { WS_SEED(4) WS_SEED(9) WS_SEED(12) WS_SEED(24) }
 #undef WS_SEED
   launch_check();
+  if (S > 1) {
+    hipLaunchKernelGGL(ws_seed_fin_kernel, dim3(rb, P), dim3(256), 0, st, (const WsProb*)probs, (const double*)aseed,
+                       (double*)alpha, (double*)G, X, (const double*)part, max_l, S);
+    launch_check();
+    HFENS_CHECK(hipFreeAsync(part, st));
+  }
 }
 
 // n_iter outer iterations (select+solve, then the gradient update) enqueued back to back; finished
