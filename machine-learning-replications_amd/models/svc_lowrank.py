@@ -437,11 +437,25 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
         chpt = torch.empty(32 * r, dtype=dt, device=Phi.device)            # chol_spd_mw transposed panel
     yk = {1: y[:, None], 2: torch.stack([y, y], 1)}
     it = 0
+    # the elementwise row passes as single native kernels (lowrank.hip ipm_resid / ipm_pred / ipm_corr /
+    # ipm_minv_pre / ipm_minv_post / ipm_update: the same IEEE operations in the same order as the
+    # torch expressions beside them, contraction off — bit-identical iterates, ~60 fewer launches and
+    # row passes per iteration)
+    fz = native and l > 0 and not _FUSED_OFF
+    sp = ops.stream_ptr(Phi.device) if fz else 0
     for it in range(1, max_iter + 1):
-        s = c - a
-        w = (yield ("sum", _phit(Phi, (y * a)[:, None], P32)[:, 0]))   # Φᵀ Y α
-        g = y * _phi_mv(Phi, w[:, None], P32)[:, 0] - 1.0   # Qα − 1
-        rd = g + _bc(b, y) * y - nu + mu
+        if fz:
+            w = (yield ("sum", _phit(Phi, (y * a)[:, None], P32)[:, 0]))   # Φᵀ Y α
+            Pw = _phi_mv(Phi, w[:, None], P32)
+            s, rd = torch.empty_like(a), torch.empty_like(a)
+            bc = b.reshape(1).contiguous()
+            E.ipm_resid(c.data_ptr(), a.data_ptr(), y.data_ptr(), Pw.data_ptr(), int(Pw.stride(0)), bc.data_ptr(),
+                        nu.data_ptr(), mu.data_ptr(), l, s.data_ptr(), rd.data_ptr(), sp)
+        else:
+            s = c - a
+            w = (yield ("sum", _phit(Phi, (y * a)[:, None], P32)[:, 0]))   # Φᵀ Y α
+            g = y * _phi_mv(Phi, w[:, None], P32)[:, 0] - 1.0   # Qα − 1
+            rd = g + _bc(b, y) * y - nu + mu
         sums = (yield ("sum", torch.stack([torch.dot(y, a), torch.dot(a, nu) + torch.dot(s, mu)])))
         re = sums[0]
         gap = sums[1] / (2 * lg)
@@ -467,8 +481,14 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
         if float(chk[0]) < tol and float(chk[1]) < RD_LOOSE and float(chk[2]) < 1e-8 * csum:
             LAST_INFO["loose_rd_stops"] = LAST_INFO.get("loose_rd_stops", 0) + 1
             break
-        D = nu / a + mu / s
-        Dinv = 1.0 / D
+        if fz:
+            Dinv, rnu_p, rmu_p = (torch.empty_like(a) for _ in range(3))
+            Dinv2, H2 = torch.empty(l, 2, dtype=dt, device=Phi.device), torch.empty(l, 2, dtype=dt, device=Phi.device)
+            E.ipm_pred(a.data_ptr(), s.data_ptr(), nu.data_ptr(), mu.data_ptr(), rd.data_ptr(), y.data_ptr(), l,
+                       Dinv.data_ptr(), Dinv2.data_ptr(), rnu_p.data_ptr(), rmu_p.data_ptr(), H2.data_ptr(), sp)
+        else:
+            D = nu / a + mu / s
+            Dinv = 1.0 / D
         # S = I + Vᵀ D⁻¹ V  (V = YΦ, so Vᵀ D⁻¹ V = Φᵀ D⁻¹ Φ).  Free points drive D → 0, so S spans
         # many decades: equilibrate symmetrically before the Cholesky (exact); a relative jitter on
         # the unit diagonal is added only if it still fails.
@@ -476,6 +496,7 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
         S_prev, Dinv_prev = S, Dinv
         if DEBUG:
             dS = torch.diagonal(S)
+            D = nu / a + mu / s
             print(f"[ipm] it {it} gap {float(chk[0]):.3e} rd {float(chk[1]):.3e} D [{float(D.min()):.3e}, "
                   f"{float(D.max()):.3e}] a_min {float(a.min()):.3e} s_min {float(s.min()):.3e} "
                   f"diagS [{float(dS.min()):.3e}, {float(dS.max()):.3e}] finite {bool(torch.isfinite(S).all())}",
@@ -498,10 +519,20 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
 
         # same-shape operands in Minv (no [l, k] × [l, 1] broadcasting: torch's broadcast kernels ran
         # ~10× below the vectorised same-shape ones on these 10⁶-row vectors)
-        Dk = {1: Dinv[:, None], 2: torch.stack([Dinv, Dinv], 1)}
+        Dk = {1: Dinv[:, None], 2: Dinv2 if fz else torch.stack([Dinv, Dinv], 1)}
 
         def Minv(u):  # (D + V Vᵀ)⁻¹ u for u [l, k], V = YΦ
             kk = u.shape[1]
+            if fz:
+                uc = u.contiguous()
+                du, V = torch.empty_like(uc), torch.empty_like(uc)
+                E.ipm_minv_pre(Dinv.data_ptr(), y.data_ptr(), uc.data_ptr(), kk, l, du.data_ptr(), V.data_ptr(), sp)
+                rhs = (yield ("sum", _phit(Phi, V, P32))).contiguous()
+                E.chol_solve(Lc.data_ptr(), scv.data_ptr(), r, rhs.shape[1], rhs.data_ptr(), sp)
+                P = _phi_mv(Phi, rhs, P32).contiguous()
+                out = torch.empty_like(uc)
+                E.ipm_minv_post(Dinv.data_ptr(), y.data_ptr(), du.data_ptr(), P.data_ptr(), kk, l, out.data_ptr(), sp)
+                return out
             Dinv_k = Dk[kk] if kk in Dk else Dinv[:, None]
             y_k = yk[kk] if kk in yk else y[:, None]
             du = Dinv_k * u
@@ -553,9 +584,13 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
                                          torch.minimum(_max_step(nu, dnu), _max_step(mu, dmu)))))
 
         # predictor (affine scaling): its right-hand side and y share one pass over Φ
-        rnu, rmu = a * nu, s * mu
-        h = -rd - rnu / a + rmu / s
-        M2 = yield from Minv(torch.stack([h, y], 1))
+        if fz:
+            rnu, rmu = rnu_p, rmu_p
+            M2 = yield from Minv(H2)
+        else:
+            rnu, rmu = a * nu, s * mu
+            h = -rd - rnu / a + rmu / s
+            M2 = yield from Minv(torch.stack([h, y], 1))
         Mh, My = M2[:, 0], M2[:, 1]
         yd2 = (yield ("sum", torch.stack([torch.dot(y, My), torch.dot(y, Mh)])))
         yMy = yd2[0]
@@ -567,8 +602,14 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
         # corrector (centring + second-order terms)
         tau = sigma * gap
         tauv = _bc(tau, a)
-        rnu, rmu = a * nu + da * dnu - tauv, s * mu - da * dmu - tauv
-        h = -rd - rnu / a + rmu / s
+        if fz:
+            rnu, rmu, h = (torch.empty_like(a) for _ in range(3))
+            tc = tau.reshape(1).contiguous()
+            E.ipm_corr(a.data_ptr(), s.data_ptr(), nu.data_ptr(), mu.data_ptr(), da.data_ptr(), dnu.data_ptr(),
+                       dmu.data_ptr(), rd.data_ptr(), tc.data_ptr(), l, rnu.data_ptr(), rmu.data_ptr(), h.data_ptr(), sp)
+        else:
+            rnu, rmu = a * nu + da * dnu - tauv, s * mu - da * dmu - tauv
+            h = -rd - rnu / a + rmu / s
         Mc = (yield from Minv(h[:, None]))[:, 0]
         if CHECK:
             for nm, v in (("S", S), ("L", Lc if native else S), ("info", info if native else S), ("h_pred", M2[:, 0]),
@@ -634,11 +675,19 @@ def _ipm_gen(Phi: torch.Tensor, y: torch.Tensor, c: torch.Tensor, max_iter: int 
         t = 0.995 * alpha
         if DEBUG:
             print(f"[ipm]   step ta {float(ta):.3e} t {float(t):.3e} sigma {float(sigma):.3e}", flush=True)
-        tv = _bc(t, a)
-        a = a + tv * da
-        b = b + t * db
-        nu = nu + tv * dnu
-        mu = mu + tv * dmu
+        if fz:
+            a2, nu2, mu2 = (torch.empty_like(a) for _ in range(3))
+            tcv = t.reshape(1).contiguous()
+            E.ipm_update(a.data_ptr(), nu.data_ptr(), mu.data_ptr(), da.contiguous().data_ptr(), dnu.contiguous().data_ptr(),
+                         dmu.contiguous().data_ptr(), tcv.data_ptr(), l, a2.data_ptr(), nu2.data_ptr(), mu2.data_ptr(), sp)
+            a, nu, mu = a2, nu2, mu2
+            b = b + t * db
+        else:
+            tv = _bc(t, a)
+            a = a + tv * da
+            b = b + t * db
+            nu = nu + tv * dnu
+            mu = mu + tv * dmu
     # snap points the interior point left within 1e-9·C of a bound (their multiplier carries the
     # gap); ρ = −b: stationarity gives y_i G_i = −b on every free point, which is libsvm's ρ
     a = torch.where(a < 1e-9 * c, torch.zeros_like(a), torch.where(a > c * (1 - 1e-9), c, a))

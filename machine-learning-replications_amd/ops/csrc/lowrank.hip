@@ -940,6 +940,104 @@ __global__ __launch_bounds__(256) void ipm_dirs_kernel(const double* __restrict_
   }
 }
 
+// iteration prologue: s = c − α and the dual residual rd = ((y·(Φw) − 1) + b·y − ν) + μ
+// (P: the column Φw, stride sp; b a device scalar)
+__global__ __launch_bounds__(256) void ipm_resid_kernel(const double* __restrict__ c, const double* __restrict__ a,
+                                                        const double* __restrict__ y, const double* __restrict__ P, int sp,
+                                                        const double* __restrict__ bp, const double* __restrict__ nu,
+                                                        const double* __restrict__ mu, long long n, double* __restrict__ s,
+                                                        double* __restrict__ rd) {
+#pragma clang fp contract(off)
+  const double b = *bp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    s[i] = c[i] - a[i];
+    const double g = y[i] * P[i * sp] - 1.0;
+    rd[i] = ((g + b * y[i]) - nu[i]) + mu[i];
+  }
+}
+
+// predictor set-up: D⁻¹ = 1 / (ν/α + μ/s) (and its two-column copy), rν = α·ν, rμ = s·μ and the
+// right-hand sides [h, y] with h = ((−rd) − rν/α) + rμ/s
+__global__ __launch_bounds__(256) void ipm_pred_kernel(const double* __restrict__ a, const double* __restrict__ s,
+                                                       const double* __restrict__ nu, const double* __restrict__ mu,
+                                                       const double* __restrict__ rd, const double* __restrict__ y,
+                                                       long long n, double* __restrict__ Dinv, double* __restrict__ Dinv2,
+                                                       double* __restrict__ rnu, double* __restrict__ rmu,
+                                                       double* __restrict__ H2) {
+#pragma clang fp contract(off)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double D = nu[i] / a[i] + mu[i] / s[i];
+    const double di = 1.0 / D;
+    Dinv[i] = di;
+    Dinv2[2 * i] = di;
+    Dinv2[2 * i + 1] = di;
+    const double rn = a[i] * nu[i], rm = s[i] * mu[i];
+    rnu[i] = rn;
+    rmu[i] = rm;
+    H2[2 * i] = (-rd[i] - rn / a[i]) + rm / s[i];
+    H2[2 * i + 1] = y[i];
+  }
+}
+
+// corrector right-hand side: rν = (α·ν + Δα·Δν) − τ, rμ = (s·μ − Δα·Δμ) − τ, h = ((−rd) − rν/α) + rμ/s
+__global__ __launch_bounds__(256) void ipm_corr_kernel(const double* __restrict__ a, const double* __restrict__ s,
+                                                       const double* __restrict__ nu, const double* __restrict__ mu,
+                                                       const double* __restrict__ da, const double* __restrict__ dnu,
+                                                       const double* __restrict__ dmu, const double* __restrict__ rd,
+                                                       const double* __restrict__ taup, long long n,
+                                                       double* __restrict__ rnu, double* __restrict__ rmu,
+                                                       double* __restrict__ h) {
+#pragma clang fp contract(off)
+  const double tau = *taup;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double rn = (a[i] * nu[i] + da[i] * dnu[i]) - tau;
+    const double rm = (s[i] * mu[i] - da[i] * dmu[i]) - tau;
+    rnu[i] = rn;
+    rmu[i] = rm;
+    h[i] = (-rd[i] - rn / a[i]) + rm / s[i];
+  }
+}
+
+// the Woodbury solve's row passes around Φᵀ / Φ: du = D⁻¹ ∘ U, V = y ∘ du (k columns, row-major),
+// and afterwards out = du − D⁻¹ ∘ (y ∘ P)
+__global__ __launch_bounds__(256) void ipm_minv_pre_kernel(const double* __restrict__ Dinv, const double* __restrict__ y,
+                                                           const double* __restrict__ U, int k, long long n,
+                                                           double* __restrict__ du, double* __restrict__ V) {
+#pragma clang fp contract(off)
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n * k; e += (long long)gridDim.x * 256) {
+    const long long i = e / k;
+    const double d = Dinv[i] * U[e];
+    du[e] = d;
+    V[e] = y[i] * d;
+  }
+}
+
+__global__ __launch_bounds__(256) void ipm_minv_post_kernel(const double* __restrict__ Dinv, const double* __restrict__ y,
+                                                            const double* __restrict__ du, const double* __restrict__ P,
+                                                            int k, long long n, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n * k; e += (long long)gridDim.x * 256) {
+    const long long i = e / k;
+    out[e] = du[e] - Dinv[i] * (y[i] * P[e]);
+  }
+}
+
+// the step: α + t·Δα, ν + t·Δν, μ + t·Δμ (t a device scalar)
+__global__ __launch_bounds__(256) void ipm_update_kernel(const double* __restrict__ a, const double* __restrict__ nu,
+                                                         const double* __restrict__ mu, const double* __restrict__ da,
+                                                         const double* __restrict__ dnu, const double* __restrict__ dmu,
+                                                         const double* __restrict__ tp, long long n,
+                                                         double* __restrict__ a2, double* __restrict__ nu2,
+                                                         double* __restrict__ mu2) {
+#pragma clang fp contract(off)
+  const double t = *tp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    a2[i] = a[i] + t * da[i];
+    nu2[i] = nu[i] + t * dnu[i];
+    mu2[i] = mu[i] + t * dmu[i];
+  }
+}
+
 // Gondzio corrector target: the trial point's complementarity products pushed into [0.1τ, 10τ]
 __global__ __launch_bounds__(256) void ipm_gondzio_rhs_kernel(const double* __restrict__ a, const double* __restrict__ s,
                                                               const double* __restrict__ nu, const double* __restrict__ mu,
@@ -1004,6 +1102,64 @@ static unsigned ipm_blocks(long long n) {
   long long b = (n + 255) / 256;
   if (b > 8LL * ncu) b = 8LL * ncu;
   return (unsigned)(b < 1 ? 1 : b);
+}
+
+static int ipm_grid(long long n) {
+  long long g = (n + 255) / 256;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+}
+
+void ipm_resid(uintptr_t c, uintptr_t a, uintptr_t y, uintptr_t P, int sp, uintptr_t b, uintptr_t nu, uintptr_t mu,
+               long long n, uintptr_t s, uintptr_t rd, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_resid_kernel, dim3(ipm_grid(n)), dim3(256), 0, as_stream(stream), (const double*)c,
+                     (const double*)a, (const double*)y, (const double*)P, sp, (const double*)b, (const double*)nu,
+                     (const double*)mu, n, (double*)s, (double*)rd);
+  launch_check();
+}
+
+void ipm_pred(uintptr_t a, uintptr_t s, uintptr_t nu, uintptr_t mu, uintptr_t rd, uintptr_t y, long long n,
+              uintptr_t Dinv, uintptr_t Dinv2, uintptr_t rnu, uintptr_t rmu, uintptr_t H2, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_pred_kernel, dim3(ipm_grid(n)), dim3(256), 0, as_stream(stream), (const double*)a,
+                     (const double*)s, (const double*)nu, (const double*)mu, (const double*)rd, (const double*)y, n,
+                     (double*)Dinv, (double*)Dinv2, (double*)rnu, (double*)rmu, (double*)H2);
+  launch_check();
+}
+
+void ipm_corr(uintptr_t a, uintptr_t s, uintptr_t nu, uintptr_t mu, uintptr_t da, uintptr_t dnu, uintptr_t dmu,
+              uintptr_t rd, uintptr_t tau, long long n, uintptr_t rnu, uintptr_t rmu, uintptr_t h, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_corr_kernel, dim3(ipm_grid(n)), dim3(256), 0, as_stream(stream), (const double*)a,
+                     (const double*)s, (const double*)nu, (const double*)mu, (const double*)da, (const double*)dnu,
+                     (const double*)dmu, (const double*)rd, (const double*)tau, n, (double*)rnu, (double*)rmu,
+                     (double*)h);
+  launch_check();
+}
+
+void ipm_minv_pre(uintptr_t Dinv, uintptr_t y, uintptr_t U, int k, long long n, uintptr_t du, uintptr_t V,
+                  uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_minv_pre_kernel, dim3(ipm_grid(n * k)), dim3(256), 0, as_stream(stream), (const double*)Dinv,
+                     (const double*)y, (const double*)U, k, n, (double*)du, (double*)V);
+  launch_check();
+}
+
+void ipm_minv_post(uintptr_t Dinv, uintptr_t y, uintptr_t du, uintptr_t P, int k, long long n, uintptr_t out,
+                   uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_minv_post_kernel, dim3(ipm_grid(n * k)), dim3(256), 0, as_stream(stream), (const double*)Dinv,
+                     (const double*)y, (const double*)du, (const double*)P, k, n, (double*)out);
+  launch_check();
+}
+
+void ipm_update(uintptr_t a, uintptr_t nu, uintptr_t mu, uintptr_t da, uintptr_t dnu, uintptr_t dmu, uintptr_t t,
+                long long n, uintptr_t a2, uintptr_t nu2, uintptr_t mu2, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ipm_update_kernel, dim3(ipm_grid(n)), dim3(256), 0, as_stream(stream), (const double*)a,
+                     (const double*)nu, (const double*)mu, (const double*)da, (const double*)dnu, (const double*)dmu,
+                     (const double*)t, n, (double*)a2, (double*)nu2, (double*)mu2);
+  launch_check();
 }
 
 void ipm_dirs(uintptr_t Mh, int smh, uintptr_t My, int smy, uintptr_t db, uintptr_t rnu, uintptr_t rmu, uintptr_t nu,
