@@ -654,7 +654,15 @@ def validate_stage_graph(group, dev, peer) -> bool:
         g = np.random.default_rng(0xB0057 + 104729 * rank + r)
         return torch.from_numpy(g.integers(-(1 << 40), 1 << 40, 3 * m, dtype=np.int64))
     ok, detail = True, ""
+    fail_local = os.environ.get("HFENS_GBDT_GRAPH_PROBE_RAISE", "")
+    g = None
+    # Every rank issues the same collective sequence whatever fails locally: (1) the
+    # capture is local; (2) one MIN agreement on it — only a group whose every rank captured
+    # replays (a replayed RCCL all-reduce needs every rank's replay); (3) the eager references and
+    # the final agreement run on every rank.
     try:
+        if fail_local != "" and int(fail_local) == me:
+            raise RuntimeError("HFENS_GBDT_GRAPH_PROBE_RAISE")
         cap = runtime.stream(dev, "gbdt_graph")
         cur = torch.cuda.current_stream(dev)
         cap.wait_stream(cur)
@@ -671,27 +679,36 @@ def validate_stage_graph(group, dev, peer) -> bool:
                         dist.all_reduce(buf[k * m:(k + 1) * m], op=dist.ReduceOp.SUM, group=group)
             finally:
                 g.capture_end()
+    except RuntimeError as e:
+        ok, detail, g = False, f"rank {me}: capture: {e}", None
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=lib_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    captured = bool(int(flag.item()))
+    if captured:
         got = []
-        for r in range(reps):
-            buf.copy_(payload(me, r).to(dev))
-            g.replay()
-            torch.cuda.synchronize(dev)
-            got.append(buf.cpu())
+        try:
+            for r in range(reps):
+                buf.copy_(payload(me, r).to(dev))
+                g.replay()
+                torch.cuda.synchronize(dev)
+                got.append(buf.cpu())
+            corrupt = os.environ.get("HFENS_GBDT_GRAPH_PROBE_CORRUPT", "")
+            if corrupt != "" and int(corrupt) == me:
+                got[-1][m + 7] += 1
+        except RuntimeError as e:
+            ok, detail = False, f"rank {me}: replay: {e}"
         if peer is not None:
             peer.advance(3 * reps)
-            peer.check()
-        corrupt = os.environ.get("HFENS_GBDT_GRAPH_PROBE_CORRUPT", "")
-        if corrupt != "" and int(corrupt) == me:
-            got[-1][m + 7] += 1
+            try:
+                peer.check()      # (collective: every rank calls it; it raises after its all-reduce)
+            except RuntimeError as e:
+                ok, detail = False, f"rank {me}: {e}"
         for r in range(reps):
             ref = payload(me, r).to(lib_dev)
             dist.all_reduce(ref, op=dist.ReduceOp.SUM, group=group)
-            if not torch.equal(got[r], ref.cpu()):
+            if ok and not torch.equal(got[r], ref.cpu()):
                 ok, detail = False, f"rank {me}: replay {r}: {int((got[r] != ref.cpu()).sum())} of {3 * m} differ"
-                break
-        del g
-    except RuntimeError as e:
-        ok, detail = False, f"rank {me}: {e}"
+    del g
     flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=lib_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
     notes = [None] * W

@@ -170,7 +170,9 @@ class LassoCV(Estimator):
         A = int(grid.numel())
         refit_all = None
         self.coef_spec_dev_ = self.spec_ev_ = None
-        spec = dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and SPECULATE and group is None
+        # (only a caller with an overlap can use the speculation: SelectFromModel's)
+        spec = (dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and SPECULATE and group is None
+                and overlap is not None)
         if spec:
             from .. import runtime
             main = torch.cuda.current_stream(dev)
@@ -184,6 +186,8 @@ class LassoCV(Estimator):
                 dmark("lasso_spec")
                 self.spec_ev_ = torch.cuda.Event()
                 self.spec_ev_.record(sst)
+            for t in (G, q, yy, cnt, grid):
+                t.record_stream(sst)     # (the solve may still read them after fit returns)
         if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT:
             # the refit at the CV-chosen alpha is a cold-start solve on all rows (sklearn's
             # Lasso(alpha=best).fit); which alpha wins is known only after the CV paths, so solve the

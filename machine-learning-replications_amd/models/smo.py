@@ -1003,29 +1003,32 @@ def assign_problems(sizes, world: int) -> List[int]:
 
 def _solve_distributed(solve_local, live, n_alpha, aoffs, device, group):
     """Task-parallel SMO (SURVEY.md §2.4 ensemble parallel, call site R9): rank r solves the
-    problems ``assign_problems`` gives it; one SUM all-reduce of a zero-filled
-    [α | ρ | iters | err] vector (every entry has exactly one non-zero contributor, so the sum is
-    exact) gives every rank every solution."""
+    problems ``assign_problems`` gives it; one SUM all-reduce of a zero-filled int64
+    [α bits | ρ bits | iters | err count] vector gives every rank every solution.  Every α / ρ / iters
+    entry has exactly one non-zero contributor and travels as its f64 BIT PATTERN (an f64
+    sum would turn an owner's −0.0 into +0.0; an integer x + 0 = x for every pattern), so every rank
+    holds the owner's bits; the last entry counts the ranks whose solve reported an error."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     owner = assign_problems([p.l for p in live], world)
     mine = [k for k in range(len(live)) if owner[k] == rank]
     P = len(live)
-    flat = torch.zeros(n_alpha + 2 * P + 1, dtype=torch.float64, device=device)
+    flat = torch.zeros(n_alpha + 2 * P + 1, dtype=torch.int64, device=device)
     if mine:
         sub = [live[k] for k in mine]
         a_s, r_s, it_s, err_s = solve_local(sub)
         so = np.concatenate([[0], np.cumsum([p.l for p in sub])]).astype(np.int64)
         for i, k in enumerate(mine):
-            flat[aoffs[k]:aoffs[k] + live[k].l] = a_s[so[i]:so[i + 1]].to(torch.float64)
+            flat[aoffs[k]:aoffs[k] + live[k].l] = a_s[so[i]:so[i + 1]].to(torch.float64).view(torch.int64)
         idx = _to_dev(np.asarray(mine, dtype=np.int64), device)
-        flat[n_alpha:n_alpha + P].index_copy_(0, idx, r_s.to(torch.float64).reshape(-1))
-        flat[n_alpha + P:n_alpha + 2 * P].index_copy_(0, idx, it_s.to(torch.float64).reshape(-1))
+        flat[n_alpha:n_alpha + P].index_copy_(0, idx, r_s.to(torch.float64).reshape(-1).contiguous().view(torch.int64))
+        flat[n_alpha + P:n_alpha + 2 * P].index_copy_(0, idx, it_s.to(torch.int64).reshape(-1))
         if err_s is not None:
-            flat[n_alpha + 2 * P:] += err_s.to(torch.float64)
+            flat[n_alpha + 2 * P:] += (err_s.to(torch.float64).reshape(-1) != 0).any().to(torch.int64)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-    return (flat[:n_alpha], flat[n_alpha:n_alpha + P], flat[n_alpha + P:n_alpha + 2 * P].round().to(torch.int32),
-            flat[n_alpha + 2 * P:])
+    bits = flat[:n_alpha + P].view(torch.float64)
+    return (bits[:n_alpha], bits[n_alpha:], flat[n_alpha + P:n_alpha + 2 * P].to(torch.int32),
+            flat[n_alpha + 2 * P:].to(torch.float64))
 
 
 # Cascade seed (VERDICT r4 #2: the critical problem's pair count).  Every working-set problem of
@@ -1590,12 +1593,12 @@ def finish_svc_batch(st: dict, defer=None):
         early["ev"].synchronize()
         host_e = early["host"].numpy()
         smo_failed = early["has_err"] and host_e[-1] != 0.0
-    if st.get("gamma_dev") is not None:
-        st["gamma_dev"].resolve(all_probs, meta)     # (the host's γ; raises on non-finite scaled rows)
-        st["gamma_dev"] = None
     else:
         err = sol.get("smo_err")
         smo_failed = err is not None and float(err.max()) != 0.0
+    if st.get("gamma_dev") is not None:
+        st["gamma_dev"].resolve(all_probs, meta)     # (the host's γ; raises on non-finite scaled rows)
+        st["gamma_dev"] = None
     if smo_failed:
         # cooperative SMO: a member exchange timed out (members not co-resident beside concurrent
         # work) → re-solve with the one-workgroup kernel; working-set SMO: a problem needed more

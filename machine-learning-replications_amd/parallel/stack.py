@@ -65,8 +65,10 @@ def broadcast_svc_fits(svcs, Zs, group):
     """Every rank receives fit ``f`` from its owner, rank ``f mod world``, in TWO collectives for
     all fits (the per-fit object broadcast + 9 tensor broadcasts were ≈ 60 RCCL
     calls per stacking fit): a SUM of an int64 shape table, then a SUM of ONE packed f64 buffer in
-    which each fit's slice is written by its owner alone — x + 0 = x exactly, so every rank ends with
-    the owner's bits (integers below 2^53 travel exactly in f64)."""
+    which each fit's slice is written by its owner alone.  The buffer is summed as its int64 bit
+    patterns (in f64, an owner's −0.0 plus the others' +0.0 would arrive as +0.0); an
+    integer x + 0 = x for every pattern, so every rank ends with the owner's bits (integers below
+    2^53 travel exactly in f64)."""
     world, rank = pdist.dist.get_world_size(group), pdist.dist.get_rank(group)
     dev = pdist._default_device(group)
     K = len(svcs)
@@ -93,7 +95,7 @@ def broadcast_svc_fits(svcs, Zs, group):
                  svc._probB.reshape(-1), svc.class_weight_.reshape(-1),
                  torch.tensor([svc._gamma, float(svc.shape_fit_[0]), float(svc.shape_fit_[1])], dtype=f64)]
         buf[offs[f]:offs[f + 1]] = torch.cat([t.to(device=dev, dtype=f64) for t in parts])
-    pdist.dist.all_reduce(buf, op=pdist.dist.ReduceOp.SUM, group=group)
+    pdist.dist.all_reduce(buf.view(torch.int64), op=pdist.dist.ReduceOp.SUM, group=group)
     COLLECTIVES["broadcast_svc_fits"] = 2
     for f, svc in enumerate(svcs):
         if f in mine:

@@ -188,9 +188,16 @@ def validate(pc: "PeerComm") -> bool:
     lib_dev = torch.device("cpu") if gloo else pc.device
     mine_i, mine_f = _probe_payloads(me, n)
     corrupt = os.environ.get("HFENS_XGMI_PROBE_CORRUPT", "")
+    fail_local = os.environ.get("HFENS_XGMI_PROBE_RAISE", "")
     detail = ""
     ok = True
+    # (1) local phase: the peer kernels (which synchronise only through their own flags) and the
+    # local reads; a failure here — an exception or a timed-out peer wait — is this rank's alone.
+    # No collective-library call may sit inside it: a rank that jumped out of it early would issue
+    # a different collective sequence from the others.
     try:
+        if fail_local != "" and int(fail_local) == me:
+            raise RuntimeError("HFENS_XGMI_PROBE_RAISE")
         ti = torch.from_numpy(mine_i.copy()).to(pc.device)
         pc.allreduce_(ti, (pc.epoch + 1) % 3, 0, epoch_base=pc.epoch)
         pc.epoch += 1
@@ -198,13 +205,21 @@ def validate(pc: "PeerComm") -> bool:
         torch.cuda.synchronize(pc.device)
         got_i = ti.cpu()
         got_f = {op: t.cpu() for op, t in tf.items()}
+        timed_out = int(pc.err.item()) != 0
+        pc.err.zero_()
+        if timed_out:
+            raise RuntimeError("peer wait timed out")
         if corrupt != "" and int(corrupt) == me:
             got_i[n // 2] += 1
-        # the library's answers
-        ref_i = torch.from_numpy(mine_i.copy()).to(lib_dev)
-        dist.all_reduce(ref_i, op=dist.ReduceOp.SUM, group=group)
-        allf = [torch.empty(n, dtype=torch.float64, device=lib_dev) for _ in range(W)]
-        dist.all_gather(allf, torch.from_numpy(mine_f.copy()).to(lib_dev), group=group)
+    except RuntimeError as e:
+        ok, detail = False, f"rank {me}: {e}"
+    # (2) every rank issues the same collectives from here on, whatever happened locally: the
+    # library's answers, then one MIN agreement on the verdict
+    ref_i = torch.from_numpy(mine_i.copy()).to(lib_dev)
+    dist.all_reduce(ref_i, op=dist.ReduceOp.SUM, group=group)
+    allf = [torch.empty(n, dtype=torch.float64, device=lib_dev) for _ in range(W)]
+    dist.all_gather(allf, torch.from_numpy(mine_f.copy()).to(lib_dev), group=group)
+    if ok:
         allf = [t.cpu() for t in allf]
         ref_f = {"sum": allf[0].clone(), "max": allf[0].clone(), "min": allf[0].clone()}
         for r in range(1, W):
@@ -219,12 +234,6 @@ def validate(pc: "PeerComm") -> bool:
                 bad.append(f"f64 {op} ({int((got_f[op] != ref_f[op]).sum())} of {n} differ)")
         if bad:
             ok, detail = False, f"rank {me}: " + ", ".join(bad)
-        try:
-            pc.check()   # a peer wait that timed out on any rank
-        except RuntimeError as e:
-            ok, detail = False, f"rank {me}: {e}"
-    except RuntimeError as e:
-        ok, detail = False, f"rank {me}: {e}"
     flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=lib_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
     joint = bool(int(flag.item()))

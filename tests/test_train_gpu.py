@@ -344,6 +344,30 @@ def test_xgmi_probe_mismatch_falls_back_together(dev):
     _check_dp_stage_equal(dev, got)
 
 
+def test_xgmi_probe_local_raise_falls_back_together(dev):
+    """one rank RAISES inside the peer-probe's local phase (HFENS_XGMI_PROBE_RAISE) and
+    so never runs its peer kernels: the others' peer waits time out, every rank still issues the
+    same collective sequence (no hang), all drop the peer path together and the fit runs on the
+    collective library, bit for bit."""
+    path, per_stage, xg, units, got, pr, gpr = _run_dp_stage(
+        2, "try", env={"HFENS_XGMI_PROBE_RAISE": "1", "HFENS_XGMI_TIMEOUT": "2"}, probes=True)
+    assert len(pr) == 1 and not pr[0]["ok"] and any(m.startswith("rank 1:") for m in pr[0]["mismatches"]), pr
+    assert path == "stage" and per_stage == 1.0 and xg == 0.0
+    _check_dp_stage_equal(dev, got)
+
+
+def test_stage_graph_probe_local_raise_runs_eagerly(dev):
+    """one rank's stage-graph capture raises (HFENS_GBDT_GRAPH_PROBE_RAISE): nobody
+    replays (the capture agreement comes first), every rank runs the stage loop eagerly on the
+    still-valid peer kernel, bit for bit."""
+    path, per_stage, xg, units, got, pr, gpr = _run_dp_stage(2, "1", env={"HFENS_GBDT_GRAPH_PROBE_RAISE": "0"},
+                                                             probes=True)
+    assert pr and pr[0]["ok"]
+    assert gpr and not gpr[0]["ok"] and any(m.startswith("rank 0:") for m in gpr[0]["mismatches"]), gpr
+    assert units == 0 and per_stage == 0.0 and xg == 1.0
+    _check_dp_stage_equal(dev, got)
+
+
 def test_stage_graph_probe_mismatch_runs_eagerly(dev):
     """The stage-graph probe disagrees on one rank (HFENS_GBDT_GRAPH_PROBE_CORRUPT): every rank runs
     the stage loop eagerly (no replayed units) on the still-valid peer kernel, bit for bit."""
