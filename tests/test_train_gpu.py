@@ -950,3 +950,22 @@ def test_lasso_speculation_hit_and_miss(dev, monkeypatch):
     nopre, _ = run(False, pre=False)
     assert np.array_equal(miss.selected, nopre.selected)
     assert torch.equal(miss.proba_sel, nopre.proba_sel)
+
+
+def test_prelaunched_svc_without_early_read(dev, monkeypatch):
+    """the prelaunched (device-γ) SVC batch finished WITHOUT the early read-back
+    (HFENS_SVC_EARLY_READ=0) reads the SMO error word itself and resolves γ — no UnboundLocalError —
+    and fits the same stack as with the early read (the same solve; only the read-back differs)."""
+    from hfens import pipeline
+    from hfens.models import smo, stack_trainer
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for early in (True, False):
+        monkeypatch.setattr(smo, "EARLY_READ", early)
+        stack_trainer.LAST_PRELAUNCH.clear()
+        out[early] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+        assert stack_trainer.LAST_PRELAUNCH["used"]
+    assert np.array_equal(out[True].selected, out[False].selected)
+    assert torch.equal(out[True].proba_sel, out[False].proba_sel)
