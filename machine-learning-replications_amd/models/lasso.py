@@ -74,6 +74,12 @@ SPECULATIVE_REFIT = os.environ.get("HFENS_LASSO_SPEC_REFIT", "1") != "0"
 # overlap, so nothing the overlap enqueues waits behind the paths.
 SPECULATE = os.environ.get("HFENS_LASSO_SPECULATE", "1") != "0"
 SPEC_ALPHA_INDEX = -1     # the grid point speculated on (tests move it to force a miss)
+EARLY_SPEC = os.environ.get("HFENS_LASSO_EARLY_SPEC", "1") != "0"
+# with the early speculation, the every-alpha refit beside the CV paths is not solved (the hit's refit
+# is the speculative one; a miss solves its one refit after the paths): its 100 one-wave solves ran
+# beside the prelaunched stack and held CUs the GBDT stage kernel and the SMO needed
+# (profiles/r6_runs/r6d: 25.2 vs 19.2 ms / fit with the bases behind the paths)
+EARLY_REFIT_ALL = os.environ.get("HFENS_LASSO_EARLY_REFIT_ALL", "0") == "1"
 
 
 class LassoCV(Estimator):
@@ -112,9 +118,11 @@ class LassoCV(Estimator):
                                              float(self.tol))) for p in range(P)]
         return torch.stack(out).to(Gs.device)
 
-    def fit(self, X, y, group=None, overlap=None):
+    def fit(self, X, y, group=None, overlap=None, early_overlap=None):
         """``overlap``: optional host callable run while the device solves the CV path (between its
-        launch and the first read of its result) — host work hidden under the path's GPU time."""
+        launch and the first read of its result) — host work hidden under the path's GPU time.
+        ``early_overlap``: run right after the speculative refit is enqueued, before the alpha grid's
+        host read (only when the speculation runs early, :data:`EARLY_SPEC`)."""
         from ..utils.guards import check_finite, finite_flag, raise_flags
         X = as_tensor(X)
         y = as_tensor(y, device=X.device)
@@ -151,6 +159,34 @@ class LassoCV(Estimator):
         G = Sxx - cnt[:, None, None] * mx[:, :, None] * mx[:, None, :]
         q = Sxy - cnt[:, None] * mx * my[:, None]
         yy = Syy - cnt * my * my
+        from ..utils.timing import dmark, hmark
+        main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        self.coef_spec_dev_ = self.spec_ev_ = None
+        # (only a caller with an overlap can use the speculation: SelectFromModel's)
+        spec = (dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and SPECULATE and group is None
+                and overlap is not None)
+        # EARLY_SPEC: the speculative refit goes in BEFORE the alpha grid's host read (which waits for
+        # the imputation): np.geomspace's end points are exactly amax and amax·eps (numpy assigns them),
+        # and amax = max|q| / n is one IEEE division, so the device computes the speculated grid
+        # point bit for bit.  The caller's early overlap (the stacking fit enqueued on the speculative
+        # selection) then runs while the device still imputes, instead of after the read.
+        early = (spec and EARLY_SPEC and self.alphas is None and one_read
+                 and SPEC_ALPHA_INDEX % self.n_alphas in (0, self.n_alphas - 1))
+        if early:
+            res = float(np.finfo(np.float64).resolution)
+            amax_d = q[k].abs().max() / cnt[k]
+            a_d = amax_d if SPEC_ALPHA_INDEX % self.n_alphas == 0 else amax_d * self.eps
+            a_d = torch.where(amax_d <= res, torch.full_like(a_d, res), a_d)
+            # (on the caller's stream: its consumers — the speculative selection and the stacking
+            # batches enqueued on it — wait for it anyway; the CV paths below start behind it)
+            self.coef_spec_dev_ = self._solve(G[k:], q[k:], yy[k:], cnt[k:], a_d.reshape(1, 1))[0, 0]
+            dmark("lasso_spec")
+            self.spec_ev_ = torch.cuda.Event()
+            self.spec_ev_.record(main)
+            self.spec_alpha_dev_ = a_d
+            if early_overlap is not None:
+                hmark("lasso_spec_launched")
+                early_overlap()
         # alpha grid on all rows (problem k = full data)
         if self.alphas is None:
             if one_read:
@@ -169,26 +205,33 @@ class LassoCV(Estimator):
         grid = grid.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else grid.to(dev)
         A = int(grid.numel())
         refit_all = None
-        self.coef_spec_dev_ = self.spec_ev_ = None
-        # (only a caller with an overlap can use the speculation: SelectFromModel's)
-        spec = (dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and SPECULATE and group is None
-                and overlap is not None)
-        if spec:
+        if spec and not early:
             from .. import runtime
-            main = torch.cuda.current_stream(dev)
             sst = runtime.stream(dev, "lasso_spec", priority=-1)
             sst.wait_stream(main)
             with torch.cuda.stream(sst):
                 # (the same kernel on the same inputs as refit_all's last problem: bit-identical)
                 a = SPEC_ALPHA_INDEX % A
                 self.coef_spec_dev_ = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[a:a + 1][None])[0, 0]
-                from ..utils.timing import dmark
                 dmark("lasso_spec")
                 self.spec_ev_ = torch.cuda.Event()
                 self.spec_ev_.record(sst)
             for t in (G, q, yy, cnt, grid):
                 t.record_stream(sst)     # (the solve may still read them after fit returns)
-        if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT:
+        if early:
+            # the CV paths, then every alpha's cold-start refit (below), on ONE side stream: neither
+            # is on the critical path any more (the stacking fit already runs on the speculative
+            # selection), and no further stream changes the measured stream → hardware-queue layout
+            from .. import runtime
+            pst = runtime.stream(dev, "lasso_refit")
+            pst.wait_stream(main)
+            with torch.cuda.stream(pst):
+                coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
+                dmark("lasso_cv_path")
+                path_ev = torch.cuda.Event()
+                path_ev.record(pst)
+            coefs.record_stream(main)
+        if dev.type == "cuda" and F <= 64 and SPECULATIVE_REFIT and not (early and not EARLY_REFIT_ALL):
             # the refit at the CV-chosen alpha is a cold-start solve on all rows (sklearn's
             # Lasso(alpha=best).fit); which alpha wins is known only after the CV paths, so solve the
             # cold start for EVERY alpha on a side stream while the CV paths run (one wave each, the
@@ -196,7 +239,6 @@ class LassoCV(Estimator):
             # inputs as the one-problem refit, bit-identical, and no second dependent launch on the
             # critical path
             from .. import runtime
-            main = torch.cuda.current_stream(dev)
             side = runtime.stream(dev, "lasso_refit")
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -204,9 +246,16 @@ class LassoCV(Estimator):
                                         cnt[k:].expand(A), grid[:, None])          # [A, 1, F]
                 ev = torch.cuda.Event()
                 ev.record(side)
-        from ..utils.timing import dmark
         dmark("lasso_cv_in")
-        if spec:
+        if early:
+            for t in (G, q, yy, cnt, grid):
+                t.record_stream(pst)
+            if overlap is not None:
+                hmark("lasso_launched")
+                overlap()
+                overlap = None
+            main.wait_event(path_ev)
+        elif spec:
             # the CV paths on a stream of their own: work the overlap enqueues on the caller's stream
             # does not queue behind them (joined before the MSE below, after the overlap)
             pst = runtime.stream(dev, "lasso_path")
@@ -220,7 +269,6 @@ class LassoCV(Estimator):
                 t.record_stream(pst)
             coefs.record_stream(main)
             if overlap is not None:
-                from ..utils.timing import hmark
                 hmark("lasso_launched")
                 overlap()
                 overlap = None
@@ -256,6 +304,11 @@ class LassoCV(Estimator):
         self.mse_path_ = mse.t()
         if refit_all is not None:
             w = refit_all[best, 0]
+        elif (early and best == SPEC_ALPHA_INDEX % A
+              and float(self.spec_alpha_dev_) == float(grid[best])):
+            # the speculation hit: its refit IS the refit at the chosen alpha (same kernel, same
+            # inputs, the same alpha bits)
+            w = self.coef_spec_dev_
         else:
             final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
             w = final[0, 0]
@@ -286,13 +339,25 @@ class SelectFromModel(Estimator):
         key = torch.where(rank < k, idx, idx + F)
         return torch.sort(key, stable=True).values[:k]
 
-    def fit(self, X, y, group=None, overlap=None):
+    def fit(self, X, y, group=None, overlap=None, early_overlap=None):
+        """``overlap`` / ``early_overlap``: host callables run under the LassoCV path (see
+        :meth:`LassoCV.fit`).  With threshold=-inf and max_features, ``cols_dev_`` (the selected
+        columns on the device, from the speculative refit when there is one) is set before either
+        runs; ``early_overlap`` runs as soon as the speculative selection is enqueued (before the
+        LassoCV's host read) or, without an early speculation, right before ``overlap``."""
         self.cols_dev_ = None
-        if overlap is not None and isinstance(self.estimator, LassoCV):
-            user = overlap
-            if (self.max_features is not None and isinstance(self.threshold, float)
-                    and np.isneginf(self.threshold)):
-                def overlap():
+        self.cols_host_ = None
+        if (overlap is not None or early_overlap is not None) and isinstance(self.estimator, LassoCV):
+            user_late, user_early = overlap, early_overlap
+            done = [False]
+            dev_rule = (self.max_features is not None and isinstance(self.threshold, float)
+                        and np.isneginf(self.threshold))
+
+            def early():
+                if done[0]:
+                    return
+                done[0] = True
+                if dev_rule:
                     est = self.estimator
                     cd = getattr(est, "coef_spec_dev_", None)
                     self.cols_speculative_ = cd is not None
@@ -304,14 +369,28 @@ class SelectFromModel(Estimator):
                         cd = getattr(est, "coef_dev_", None)
                     if cd is not None:
                         self.cols_dev_ = self._device_columns(cd, int(cd.shape[0]))
+                        # the host copy for the caller's check, read right behind the columns
+                        # (pinned + event: the check waits for them, not for later work)
+                        h = torch.empty(self.cols_dev_.shape, dtype=self.cols_dev_.dtype, pin_memory=True)
+                        h.copy_(self.cols_dev_, non_blocking=True)
+                        hev = torch.cuda.Event()
+                        hev.record()
+                        self.cols_host_ = (h, hev)
                     from ..utils.timing import hmark
                     hmark("cols_dev")
-                    user()
-            self.estimator_ = self.estimator.fit(X, y, group=group, overlap=overlap)
+                if user_early is not None:
+                    user_early()
+
+            def late():
+                early()
+                if user_late is not None:
+                    user_late()
+            self.estimator_ = self.estimator.fit(X, y, group=group, overlap=late, early_overlap=early)
         else:
             self.estimator_ = self.estimator.fit(X, y, group=group)
-            if overlap is not None:
-                overlap()
+            for f in (early_overlap, overlap):
+                if f is not None:
+                    f()
         scores = self.estimator_.coef_.abs().cpu().numpy()
         F = scores.size
         mask = np.ones(F, dtype=bool)

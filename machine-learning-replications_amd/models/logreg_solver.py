@@ -105,7 +105,7 @@ LAST_PATH = {"path": None}
 _WARNED_EMULATION = [False]
 # workgroups a cooperative LR launch may occupy (None = all CUs).  The stacking trainer lowers it
 # while a cooperative SMO holds most CUs on another stream: LR members spin on each other, so all of
-# them must fit on the CUs the SMO leaves free (stack_trainer._fit_bases_concurrent).
+# them must fit on the CUs the SMO leaves free (stack_trainer._launch_bases).
 BLOCK_BUDGET = [None]
 
 

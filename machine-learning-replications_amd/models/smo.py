@@ -1351,8 +1351,8 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     expansion then runs on the host while the device computes the guards and γ statistics, and
     only those are read back.
 
-    ``gamma_dev`` (single process, GPU, a ``plan`` of 0/1 labels, gamma='scale', the working-set
-    solver): NO host read at all — γ is computed and patched into the problem records on the device
+    ``gamma_dev`` (GPU, a ``plan`` of 0/1 labels, gamma='scale', the working-set solver): NO host
+    read at all — γ is computed and patched into the problem records on the device
     (:class:`_GammaDev`), the labels' 0/1 guard ran in the plan, and the scaled rows' finite guard is
     the γ's own (read by :func:`finish_svc_batch`).  The stacking trainer uses it to enqueue the
     whole batch before the selected columns reach the host (pipeline.develop)."""
@@ -1387,7 +1387,9 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         pre = plan   # expanded ahead of time (plan_svc_problems), overlapped with earlier device work
         hmark("svc_expand_planned")
     gdev = None
-    if (gamma_dev and cuda and group is None and pre is not None and all(need_var)
+    # (with ``group``, the task-parallel policy: every rank holds the same Zs, so every rank's γ
+    # kernel computes the same bits)
+    if (gamma_dev and cuda and pre is not None and all(need_var)
             and _pick_solver(max(int(p.l) for _, pr, _ in pre for p in pr), int(Zs[0].shape[1])) == "ws"):
         gdev = _GammaDev(Zs, device)
     parts = []

@@ -204,17 +204,20 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
     return dict(y_np=y_np, folds_np=folds_np, rows_host=rows_host, svc_pre=svc_pre)
 
 
-def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=None, rows_host=None, y_np=None,
-                          svc_pre=None, oof_svc_dev=None, early=None, dev_bases=None, prelaunched=None):
-    """SVC batch on a side stream ∥ the other base models on a second stream (one host thread).
-    Returns the fitted clone lists in estimator order, or None when not applicable."""
+def _launch_svc(stc) -> bool:
+    """SVC batch on a side stream ∥ the other base models on a second stream (:func:`_launch_bases`),
+    from one host thread: everything ENQUEUED, nothing read back (:func:`_finish_concurrent`
+    completes it).  Returns False when not applicable (the caller then fits sequentially)."""
+    clf, X, y, masks, group = stc["clf"], stc["X"], stc["y"], stc["masks"], stc["group"]
+    svc_group, rows_host, y_np, svc_pre = stc["svc_group"], stc["rows_host"], stc["y_np"], stc["svc_pre"]
+    oof, early, dev_bases = stc["oof"], stc["early"], stc["dev_bases"]
     kinds = [_kind(e) for _, e in clf.estimators]
     svc_cols = [i for i, k in enumerate(kinds) if k in ("svc", "svc_raw")]
     if not (X.is_cuda and CONCURRENT_BASES and svc_cols and len(kinds) > len(svc_cols)):
-        return None
+        return False
     dev = X.device
     if group is not None:
-        from ..parallel.stack import finish_svc_batch_distributed, launch_svc_batch_distributed
+        from ..parallel.stack import launch_svc_batch_distributed
     # two pool streams (the legacy default stream would implicitly serialise with them); the SVC
     # stream at high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues and
     # two same-priority pool streams were measured landing on ONE queue (serialised)
@@ -224,84 +227,110 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
     main = torch.cuda.current_stream(dev)
     side, other = runtime.stream(dev, "svc", priority=-1), runtime.stream(dev, "bases")
     side.wait_stream(main)
-    other.wait_stream(main)
+    if stc.get("x_event") is not None:
+        # (the prelaunch: X is produced on the SVC stream from the speculative selection)
+        side.wait_event(stc["x_event"])
     out, pending = {}, {}
-    import time as _t
-    from ..utils.timing import hmark, hmarks_flush, dmark
-    marks = [("start", _t.perf_counter())]
+    from ..utils.timing import hmark, dmark
     hmark("fit_bases")
-    with timer.stage("fit_bases(svc || gbc+lr)"):
-        # every collective is issued from this thread in the same order on every rank:
-        # SVC all-gathers → GBC/LR all-reduces → SVC broadcasts
-        if prelaunched is not None:
-            pending.update(prelaunched)     # (enqueued under the LassoCV path: prelaunch_svc)
+    # every collective is issued from this thread in the same order on every rank:
+    # SVC all-gathers / the task-parallel SMO all-reduce → GBC/LR all-reduces → SVC broadcasts
+    with torch.cuda.stream(side):
+        for i in svc_cols:
+            clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
+            hmark("svc_inputs")
+            if group is None:
+                yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
+                # device γ (no host read before the SMO) whenever the batch is eligible
+                st = launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh, plan=(svc_pre or {}).get(i),
+                                      gamma_dev=GAMMA_DEV)
+                if stc["oof_svc_dev"] is not None:
+                    # the OOF column straight from the device solution, behind the SMO on this
+                    # stream: no wait for the fitted models' host bookkeeping
+                    st["oof_dev"] = stc["oof_svc_dev"](i, clones, st)
+                pending[i] = (clones, st)
+            else:
+                pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
+            hmark("svc_launched")
+    stc.update(pending=pending, out=out, side=side, other=other, main=main, svc_cols=svc_cols, bases_done=False)
+    return True
+
+
+def _launch_bases(stc):
+    """The GBC / L1-LR fold batches on the "bases" stream (device out-of-fold columns), then the
+    meta model's early launch behind every out-of-fold column."""
+    clf, X, y, masks, group = stc["clf"], stc["X"], stc["y"], stc["masks"], stc["group"]
+    oof, early, dev_bases = stc["oof"], stc["early"], stc["dev_bases"]
+    side, other, main, svc_cols, out, pending = (stc["side"], stc["other"], stc["main"], stc["svc_cols"],
+                                                 stc["out"], stc["pending"])
+    from ..utils.timing import hmark, dmark
+    other.wait_stream(main)
+    if stc.get("x_event") is not None:
+        other.wait_event(stc["x_event"])
+        X.record_stream(other)
+    # cooperative LR members must all fit on the CUs a cooperative SMO leaves free
+    from . import logreg_solver, smo as _smo
+    lr_budget = logreg_solver.BLOCK_BUDGET[0]
+    if _smo.LAST_SMO_INFO.get("solver") in ("coop", "coop-otf"):
+        logreg_solver.BLOCK_BUDGET[0] = max(1, _smo.COOP_RESERVE_CUS // 2)
+    elif _smo.LAST_SMO_INFO.get("solver") == "ws" and X.is_cuda:
+        # the working-set solver holds one CU per problem (its gradient updates come and go)
+        logreg_solver.BLOCK_BUDGET[0] = max(1, _smo._num_cus(X.device) - int(_smo.LAST_SMO_INFO["problems"]) - 8)
+    try:
+        with torch.cuda.stream(other):
+            for i, (name, est) in enumerate(clf.estimators):
+                if i not in svc_cols:
+                    r = dev_bases["fit"](i, est) if dev_bases is not None else None
+                    if r is not None:
+                        out[i] = r        # enqueued, out-of-fold column on the device
+                    else:
+                        out[i] = fit_base_batch(est, X, y, masks, group=group)
+                        if oof is not None:
+                            oof(i, out[i])
+                    hmark(f"{name}_host_done")
+                    dmark(f"{name}_done")
+            # every meta-feature column of these bases is enqueued on this stream by now: the
+            # meta model waits for this point, not for the bookkeeping enqueued after it
+            cols_ev = torch.cuda.Event()
+            cols_ev.record(other)
+            if dev_bases is not None:
+                # the refit models' fitted state from the device node tables / coefficients,
+                # enqueued on this stream behind their solves while the SMO runs (no host read:
+                # the guards are read after it)
+                for f in dev_bases["post"]:
+                    f()
+                dev_bases["deferred"].stage()   # (their guards' read-back, queued right here)
+                hmark("bases_post")
+    finally:
+        logreg_solver.BLOCK_BUDGET[0] = lr_budget
+    if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
+        # every meta-feature column is enqueued on the device: the meta model's launch goes in
+        # now, before the SVC's results are read back — on the SVC stream, behind the SVC's own
+        # out-of-fold kernel.  (On the main stream its wait for the SVC would be the head of an
+        # otherwise idle hardware queue for the rest of the SMO: measured, such a pending
+        # cross-stream wait slowed the SMO's dispatches by 2-4 ms, profiles/r5_headline.md.)
+        hmark("early_in")
+        side.wait_stream(main)
+        side.wait_event(cols_ev)
         with torch.cuda.stream(side):
-            for i in ([] if prelaunched is not None else svc_cols):
-                clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
-                hmark("svc_inputs")
-                if group is None:
-                    yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
-                    pending[i] = (clones, launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh,
-                                                           plan=(svc_pre or {}).get(i)))
-                    if oof_svc_dev is not None and svc_group is None:
-                        # the OOF column straight from the device solution, behind the SMO on this
-                        # stream: no wait for the fitted models' host bookkeeping
-                        pending[i][1]["oof_dev"] = oof_svc_dev(i, clones, pending[i][1])
-                else:
-                    pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
-                hmark("svc_launched")
-        # cooperative LR members must all fit on the CUs a cooperative SMO leaves free
-        from . import logreg_solver, smo as _smo
-        lr_budget = logreg_solver.BLOCK_BUDGET[0]
-        if _smo.LAST_SMO_INFO.get("solver") in ("coop", "coop-otf"):
-            logreg_solver.BLOCK_BUDGET[0] = max(1, _smo.COOP_RESERVE_CUS // 2)
-        elif _smo.LAST_SMO_INFO.get("solver") == "ws" and X.is_cuda:
-            # the working-set solver holds one CU per problem (its gradient updates come and go)
-            logreg_solver.BLOCK_BUDGET[0] = max(1, _smo._num_cus(X.device) - int(_smo.LAST_SMO_INFO["problems"]) - 8)
-        try:
-            with torch.cuda.stream(other):
-                for i, (name, est) in enumerate(clf.estimators):
-                    if i not in svc_cols:
-                        r = dev_bases["fit"](i, est) if dev_bases is not None else None
-                        if r is not None:
-                            out[i] = r        # enqueued, out-of-fold column on the device
-                        else:
-                            out[i] = fit_base_batch(est, X, y, masks, group=group)
-                            if oof is not None:
-                                oof(i, out[i])
-                        hmark(f"{name}_host_done")
-                        dmark(f"{name}_done")
-                # every meta-feature column of these bases is enqueued on this stream by now: the
-                # meta model waits for this point, not for the bookkeeping enqueued after it
-                cols_ev = torch.cuda.Event()
-                cols_ev.record(other)
-                if dev_bases is not None:
-                    # the refit models' fitted state from the device node tables / coefficients,
-                    # enqueued on this stream behind their solves while the SMO runs (no host read:
-                    # the guards are read after it)
-                    for f in dev_bases["post"]:
-                        f()
-                    dev_bases["deferred"].stage()   # (their guards' read-back, queued right here)
-                    hmark("bases_post")
-        finally:
-            logreg_solver.BLOCK_BUDGET[0] = lr_budget
-        if early is not None and pending and all(st.get("oof_dev") for _, st in pending.values()):
-            # every meta-feature column is enqueued on the device: the meta model's launch goes in
-            # now, before the SVC's results are read back — on the SVC stream, behind the SVC's own
-            # out-of-fold kernel.  (On the main stream its wait for the SVC would be the head of an
-            # otherwise idle hardware queue for the rest of the SMO: measured, such a pending
-            # cross-stream wait slowed the SMO's dispatches by 2-4 ms, profiles/r5_headline.md.)
-            hmark("early_in")
-            side.wait_stream(main)
-            side.wait_event(cols_ev)
-            with torch.cuda.stream(side):
-                early["handle"] = early["launch"]()
+            early["handle"] = early["launch"]()
+    stc["bases_done"] = True
+
+
+def _finish_concurrent(stc):
+    """Read back and complete what :func:`_launch_concurrent` enqueued; returns the fitted clone
+    lists in estimator order."""
+    from ..utils.timing import hmark, hmarks_flush
+    group, pending, out, early, oof = stc["group"], stc["pending"], stc["out"], stc["early"], stc["oof"]
+    side, other, main, dev_bases = stc["side"], stc["other"], stc["main"], stc["dev_bases"]
+    if group is not None:
+        from ..parallel.stack import finish_svc_batch_distributed
+    with stc["timer"].stage("fit_bases(svc || gbc+lr)"):
         # (the refit SVC's bookkeeping stays on the SVC stream: on the caller's stream its wait
         # for the SMO, pending at the head of an idle queue, slowed the SMO itself — 22.7 vs 19.3
         # ms / fit; on a new stream the stream → hardware-queue mapping moved and the GBC / LR
         # stream shared a queue with an SMO group — 20.4 ms)
-        fin = side
-        with torch.cuda.stream(fin):
+        with torch.cuda.stream(side):
             for i, (clones, st) in pending.items():
                 if group is None:
                     # with the out-of-fold column already on the device only the refit model is
@@ -323,32 +352,43 @@ def _fit_bases_concurrent(clf, X, y, masks, group, timer, oof=None, svc_group=No
             dev_bases["deferred"].resolve()
             hmark("bases_resolved")
     hmarks_flush()
-    return [out[i] for i in range(len(kinds))]
+    return [out[i] for i in range(len(stc["clf"].estimators))]
 
 
 PRELAUNCH_SVC = os.environ.get("HFENS_PRELAUNCH_SVC", "1") != "0"
+# the prelaunch enqueues the WHOLE stacking fit (GBC / L1-LR fold batches and the meta model too, not
+# only the SVC batch) on the speculative selection: the bases' chain (≈ 7 ms from the selection) ran
+# after lasso_fit before and ended beside the SMO (profiles/r6_runs/r6a: lg_done 18.1 vs svc_oof 18.5 ms).
+# The bases go in right behind the SVC batch (prelaunch_bases from the early overlap; after the CV
+# paths with pipeline.BASES_AFTER_CV — measured slower, profiles/r6_runs/r6e)
+PRELAUNCH_BASES = os.environ.get("HFENS_PRELAUNCH_BASES", "1") != "0"
+# device γ for the stacking fit's SVC batch whenever eligible (working-set solver, planned labels,
+# gamma='scale'): no host read of the scaled rows' variance before the SMO, prelaunched or not
+GAMMA_DEV = os.environ.get("HFENS_SVC_GAMMA_DEV", "1") != "0"
 LAST_PRELAUNCH = {"used": False}
 
 
-def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Tensor, plan: dict):
-    """Enqueue the stacking fit's SVC batch (scaler fits, the 36 SMO problems, Platt, the device
-    out-of-fold column) BEFORE the selected columns are known on the host: ``cols_dev`` is
-    SelectFromModel's device column list, ``X_full`` the imputed development rows.  Everything else
-    is label-only (``plan``: plan_stacking), γ is computed on the device (smo.launch_svc_batch
-    gamma_dev), so nothing here reads the device — pipeline.develop calls it while the LassoCV path
-    runs, and the SMO starts as soon as the path and the column selection finish.  Returns the state
-    :func:`fit_stacking` continues from (it checks the host's selection against ``cols_dev``), or
-    None when the stack is not eligible."""
+def prelaunch_stack(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Tensor, plan: dict,
+                    svc_group=None):
+    """Enqueue the stacking fit (scaler fits, the 36 SMO problems, Platt, the device out-of-fold
+    columns, the GBC / L1-LR fold batches and the meta model) BEFORE the selected columns are known
+    on the host: ``cols_dev`` is SelectFromModel's device column list, ``X_full`` the imputed
+    development rows.  Everything else is label-only (``plan``: plan_stacking), γ is computed on the
+    device (smo.launch_svc_batch gamma_dev), so nothing here waits for the selection — pipeline.develop
+    calls it under the LassoCV path and the fit starts as soon as the (speculative) selection exists.
+    ``svc_group``: the task-parallel policy (every rank holds every row; only the SMO problems are
+    spread over the ranks).  Returns the state :func:`fit_stacking` finishes (after checking the host's
+    selection against ``cols_dev``), or None when the stack is not eligible."""
     kinds = [_kind(e) for _, e in clf.estimators]
     svc_cols = [i for i, k in enumerate(kinds) if k == "svc"]
     if not (PRELAUNCH_SVC and X_full.is_cuda and CONCURRENT_BASES and DEVICE_SVC_OOF and svc_cols
             and len(kinds) > len(svc_cols) and plan.get("svc_pre") and all(i in plan["svc_pre"] for i in svc_cols)):
         return None
     from .. import runtime
-    from .smo import launch_svc_batch, enqueue_svc_oof, use_lowrank
+    from .smo import use_lowrank
     dev = X_full.device
     n = int(X_full.shape[0])
-    y_np, folds_np, rows_host = plan["y_np"], plan["folds_np"], plan["rows_host"]
+    y_np, rows_host = plan["y_np"], plan["rows_host"]
     if int(y_np.shape[0]) != n:
         return None
     if use_lowrank([len(r) for r in rows_host], int(cols_dev.shape[0]), "cuda"):
@@ -356,34 +396,144 @@ def prelaunch_svc(clf, X_full: torch.Tensor, cols_dev: torch.Tensor, y: torch.Te
         # launched here it would hold this thread for the whole solve instead of running beside
         # the GBC / LR fits, as it does from the stacking trainer's streams
         return None
-    main = torch.cuda.current_stream(dev)
-    side = runtime.stream(dev, "svc", priority=-1)
-    masks = fold_masks(folds_np, N_FOLDS, device=dev)
-    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
-    meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
-    side.wait_stream(main)     # (after the tensors above: the SVC stream writes meta's column)
-    pending = {}
     from ..utils.timing import hmark
     hmark("pre_masks")
+    main = torch.cuda.current_stream(dev)
+    side = runtime.stream(dev, "svc", priority=-1)
+    side.wait_stream(main)
     with torch.cuda.stream(side):
         X = X_full.index_select(1, cols_dev)
-        for i in svc_cols:
-            clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, None, rows_host)
-            hmark("pre_svc_inputs")
-            st = launch_svc_batch(svcs, Zs, ys, y_host=[y_np[r] for r in rows_host], plan=plan["svc_pre"][i],
-                                  gamma_dev=True)
-            items = [(k, clones[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
-                     for k in range(N_FOLDS) if test_idx[k].numel()]
-            st["oof_dev"] = bool(st.get("gamma_dev") is not None) and enqueue_svc_oof(st, items, meta, i)
-            pending[i] = (clones, st)
+        x_ev = torch.cuda.Event()
+        x_ev.record(side)
     for t in (X_full, cols_dev, y):
         t.record_stream(side)
-    if not all(st["oof_dev"] for _, st in pending.values()):
-        # (not the device-γ working-set path: the batch above is still valid, finished as usual)
-        pass
-    from ..utils.timing import hmark
+    stc = launch_stacking(clf, X, y, group=None, svc_group=svc_group, plan=plan, x_event=x_ev, bases=False)
     hmark("svc_prelaunched")
-    return dict(cols_dev=cols_dev, X=X, masks=masks, test_idx=test_idx, meta=meta, pending=pending)
+    return dict(cols_dev=cols_dev, X=X, state=stc)
+
+
+def prelaunch_bases(pre) -> None:
+    """The GBC / L1-LR batches and the meta model of a :func:`prelaunch_stack` state, enqueued (the
+    pipeline calls it under the LassoCV path right after the CV paths are launched: the SVC batch
+    first, the LassoCV's own paths second, the bases last — each waits on the host before it)."""
+    stc = pre["state"] if pre is not None else None
+    if stc is not None and PRELAUNCH_BASES and stc["concurrent"] and not stc["bases_done"]:
+        _launch_bases(stc)
+
+
+def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
+                    plan=None, x_event=None, bases: bool = True) -> dict:
+    """The enqueue half of :func:`fit_stacking`: folds, masks, the SVC batch, the GBC / LR batches
+    (``bases``; otherwise they are fitted in :func:`finish_stacking`) and the meta model's launch,
+    with no host read on the single-process GPU path.  ``x_event``: X is produced on the SVC stream
+    (the prelaunch); the streams wait for it."""
+    timer = timer or StageTimer(enabled=False)
+    from ..utils.timing import hmark as _hmk
+    _hmk("stack_in")
+    dev = X.device
+    n = X.shape[0]
+    y_np = None
+    svc_pre = None
+    if plan is not None and group is None and plan.get("y_np") is not None and int(plan["y_np"].shape[0]) == n:
+        # folds, row sets and SVC problem expansions computed ahead from the same labels (plan_stacking)
+        y_np, folds_np, svc_pre = plan["y_np"], plan["folds_np"], plan["svc_pre"]
+    elif group is None:
+        y_np = y.cpu().numpy().astype(np.float64)
+        folds_np = stratified_kfold_test_folds(y_np, N_FOLDS)
+    else:
+        from ..parallel import dist as pdist
+        folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
+    rows_host = (plan["rows_host"] if svc_pre is not None
+                 else [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)])
+    masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
+    # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
+    # gathers / scatters then need no host synchronisation
+    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+    meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
+    stc = dict(clf=clf, X=X, y=y, masks=masks, test_idx=test_idx, meta=meta, group=group, svc_group=svc_group,
+               rows_host=rows_host, y_np=y_np, svc_pre=svc_pre, folds_np=folds_np, timer=timer, plan=plan,
+               x_event=x_event, concurrent=False)
+
+    def oof(col, fitted):
+        from ..utils.timing import hmark
+        hmark(f"oof{col}")
+        for k in range(N_FOLDS):
+            if test_idx[k].numel():
+                p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
+                meta[:, col].index_copy_(0, test_idx[k], p1)
+
+    def oof_svc_dev(col, fitted, st):
+        if not (DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])):
+            return False
+        from .smo import enqueue_svc_oof
+        items = [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
+                 for k in range(N_FOLDS) if test_idx[k].numel()]
+        return enqueue_svc_oof(st, items, meta, col)
+
+    y64 = y.to(torch.float64)
+    stc.update(oof=oof, oof_svc_dev=oof_svc_dev if group is None else None, y64=y64)
+    _hmk("stack_prep")
+
+    def new_final():
+        return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
+    stc["new_final"] = new_final
+    early = None
+    if group is None and EARLY_META:
+        fm = [new_final()]
+        # the meta model's label-only inputs now, on this (otherwise idle) stream: behind the
+        # out-of-fold columns only the features' guard and the intercept column remain
+        from .logreg_solver import logreg_label_prep
+        lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
+        early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
+    dev_bases = None
+    if group is None and X.is_cuda and DEVICE_BASES:
+        dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
+    stc.update(early=early, dev_bases=dev_bases)
+    stc["concurrent"] = _launch_svc(stc)
+    if stc["concurrent"] and bases:
+        _launch_bases(stc)
+    return stc
+
+
+def finish_stacking(stc):
+    """Complete :func:`launch_stacking`: read the SVC / base models back, fit (or collect) the meta
+    model and set the StackingClassifier's fitted attributes."""
+    clf, timer, group, svc_group = stc["clf"], stc["timer"], stc["group"], stc["svc_group"]
+    X, y, masks, meta, y64, early = stc["X"], stc["y"], stc["masks"], stc["meta"], stc["y64"], stc["early"]
+    if stc["concurrent"] and not stc["bases_done"]:
+        _launch_bases(stc)        # (prelaunched without the bases: PRELAUNCH_BASES=0)
+    fitted_all = _finish_concurrent(stc) if stc["concurrent"] else None
+    full = []
+    for col, (name, est) in enumerate(clf.estimators):
+        if fitted_all is not None:
+            fitted = fitted_all[col]        # OOF column already filled on the fitting stream
+        else:
+            with timer.stage(f"fit_{name}"):
+                fitted = fit_base_batch(est, X, y, masks, group=group, svc_group=svc_group,
+                                        rows_host=stc["rows_host"])
+            with timer.stage(f"oof_{name}"):
+                stc["oof"](col, fitted)
+        full.append(fitted[N_FOLDS])
+    with timer.stage("fit_meta"):
+        from ..utils.timing import dmark, hmark as _hm
+        _hm("meta_in")
+        dmark("meta_in")
+        if early is not None and "handle" in early and not early.get("stale"):
+            final, = finish_logreg_batch(early["handle"])
+        else:
+            final = stc["new_final"]()
+            fit_logreg_batch([final], meta, y64, group=group)
+        dmark("meta")
+    from ..utils.timing import hmark, hmarks_flush
+    hmark("meta_done")
+    clf.estimators_ = full
+    clf.final_estimator_ = final
+    clf.stack_method_ = ["predict_proba"] * len(full)
+    clf.classes_ = torch.tensor([0.0, 1.0], dtype=torch.float64)
+    clf.oof_meta_ = meta
+    hmark("stack_done")
+    hmarks_flush("[host-meta]")
+    return clf
 
 
 def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
@@ -473,112 +623,31 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
 
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
                  plan=None):
-    timer = timer or StageTimer(enabled=False)
-    from ..utils.timing import hmark as _hmk
-    _hmk("stack_in")
-    dev = X.device
-    n = X.shape[0]
-    y_np = None
-    svc_pre = None
-    if plan is not None and group is None and plan.get("y_np") is not None and int(plan["y_np"].shape[0]) == n:
-        # folds, row sets and SVC problem expansions computed ahead from the same labels (plan_stacking)
-        y_np, folds_np, svc_pre = plan["y_np"], plan["folds_np"], plan["svc_pre"]
-    elif group is None:
-        y_np = y.cpu().numpy().astype(np.float64)
-        folds_np = stratified_kfold_test_folds(y_np, N_FOLDS)
-    else:
-        from ..parallel import dist as pdist
-        folds_np = pdist.sharded_stratified_folds(y, N_FOLDS, group).cpu().numpy()
-    rows_host = (plan["rows_host"] if svc_pre is not None
-                 else [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)])
-    pre = plan.get("prelaunch") if (plan is not None and svc_pre is not None) else None
+    pre = plan.get("prelaunch") if (plan is not None and group is None) else None
     if pre is not None:
-        # the SVC batch was enqueued from the device column selection (prelaunch_svc): it is this
-        # fit's only if the host's selection agrees (it always should: same rule, same numbers)
+        # the stack was enqueued from the device column selection (prelaunch_stack): it is this
+        # fit's only if the host's selection agrees (a speculation on the smallest alpha can miss)
         cols = plan.get("cols")
         LAST_PRELAUNCH["speculative"] = bool(pre.get("speculative"))
-        if cols is None or not np.array_equal(pre["cols_dev"].cpu().numpy(), np.asarray(cols, dtype=np.int64)):
+        ch = pre.get("cols_host")
+        if ch is not None:
+            ch[1].synchronize()
+            cdev = ch[0].numpy()
+        else:
+            cdev = pre["cols_dev"].cpu().numpy()
+        if cols is None or not np.array_equal(cdev, np.asarray(cols, dtype=np.int64)):
             if pre.get("speculative"):
                 # the CV chose another alpha than the speculated one, with another selection: the
-                # batch enqueued on the speculated columns is discarded and the SVC fit redone
+                # stack enqueued on the speculated columns is discarded and the fit redone
                 LAST_PRELAUNCH["spec_miss"] = LAST_PRELAUNCH.get("spec_miss", 0) + 1
             else:
                 import warnings
-                warnings.warn("device column selection differs from the host's; relaunching the SVC batch")
+                warnings.warn("device column selection differs from the host's; relaunching the stacking fit")
             pre = None
     LAST_PRELAUNCH["used"] = pre is not None
     if pre is not None:
-        masks, test_idx, meta = pre["masks"], pre["test_idx"], pre["meta"]
+        stc = pre["state"]
+        stc["timer"] = timer or stc["timer"]
     else:
-        masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
-        # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
-        # gathers / scatters then need no host synchronisation
-        test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
-        meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
-    full = []
-
-    def oof(col, fitted):
-        from ..utils.timing import hmark
-        hmark(f"oof{col}")
-        for k in range(N_FOLDS):
-            if test_idx[k].numel():
-                p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
-                meta[:, col].index_copy_(0, test_idx[k], p1)
-
-    def oof_svc_dev(col, fitted, st):
-        if not (DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])):
-            return False
-        from .smo import enqueue_svc_oof
-        items = [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
-                 for k in range(N_FOLDS) if test_idx[k].numel()]
-        return enqueue_svc_oof(st, items, meta, col)
-
-    y64 = y.to(torch.float64)
-    _hmk("stack_prep")
-
-    def new_final():
-        return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
-
-    early = None
-    if group is None and EARLY_META:
-        fm = [new_final()]
-        # the meta model's label-only inputs now, on this (otherwise idle) stream: behind the
-        # out-of-fold columns only the features' guard and the intercept column remain
-        from .logreg_solver import logreg_label_prep
-        lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
-        early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
-    dev_bases = None
-    if group is None and X.is_cuda and DEVICE_BASES:
-        dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
-    fitted_all = _fit_bases_concurrent(clf, X, y, masks, group, timer, oof, svc_group, rows_host, y_np, svc_pre,
-                                       oof_svc_dev if group is None else None, early, dev_bases,
-                                       pre["pending"] if pre is not None else None)
-    for col, (name, est) in enumerate(clf.estimators):
-        if fitted_all is not None:
-            fitted = fitted_all[col]        # OOF column already filled on the fitting stream
-        else:
-            with timer.stage(f"fit_{name}"):
-                fitted = fit_base_batch(est, X, y, masks, group=group, svc_group=svc_group, rows_host=rows_host)
-            with timer.stage(f"oof_{name}"):
-                oof(col, fitted)
-        full.append(fitted[N_FOLDS])
-    with timer.stage("fit_meta"):
-        from ..utils.timing import dmark, hmark as _hm
-        _hm("meta_in")
-        dmark("meta_in")
-        if early is not None and "handle" in early and not early.get("stale"):
-            final, = finish_logreg_batch(early["handle"])
-        else:
-            final = new_final()
-            fit_logreg_batch([final], meta, y64, group=group)
-        dmark("meta")
-    from ..utils.timing import hmark, hmarks_flush
-    hmark("meta_done")
-    clf.estimators_ = full
-    clf.final_estimator_ = final
-    clf.stack_method_ = ["predict_proba"] * len(full)
-    clf.classes_ = torch.tensor([0.0, 1.0], dtype=torch.float64)
-    clf.oof_meta_ = meta
-    hmark("stack_done")
-    hmarks_flush("[host-meta]")
-    return clf
+        stc = launch_stacking(clf, X, y, timer, group, svc_group, plan)
+    return finish_stacking(stc)

@@ -44,6 +44,11 @@ PLAN_THREAD = os.environ.get("HFENS_PLAN_THREAD", "0") == "1"
 # (default off: the GBC's host bin fit runs while the device solves the SVC, off the critical path)
 BIN_AHEAD = os.environ.get("HFENS_BIN_AHEAD", "0") == "1"
 INIT_STREAMS = os.environ.get("HFENS_INIT_STREAMS", "1") != "0"   # runtime.init_fit_streams
+# the prelaunched stack's GBC / LR batches enqueued after the LassoCV's CV paths (1) or right behind
+# the SVC batch, before the grid read (0, default).  Measured on one box (profiles/r6_runs/r6e): with
+# the CV paths launched first, the paths, the SMO and the GBC stage loop ran side by side and the SMO
+# took 15.5 instead of 11 ms (24.9 / 26.9 vs 19.0 / 18.6 ms / fit)
+BASES_AFTER_CV = os.environ.get("HFENS_BASES_AFTER_CV", "0") == "1"
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
@@ -165,8 +170,15 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             plan_box["plan"] = box["plan"]
         return run
 
+    y_full = None
     if group is None and dev.type == "cuda" and PLAN_AHEAD:
         overlap = plan_ahead(y_dev)
+    elif task:
+        # the labels are gathered first (they do not wait for the imputation), so the plan below
+        # is computed on the host while the device imputes, as in one process
+        y_full = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
+        if dev.type == "cuda" and PLAN_AHEAD:
+            overlap = plan_ahead(y_full)
     from .utils.timing import hmark, dmark, dmarks_flush
     hmark("develop")
     dmark("develop")
@@ -195,56 +207,76 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         bins_job = _bins_ahead(X_dev, clf) if (BIN_AHEAD and dev.type == "cuda" and group is None) else None
         if task:
             X_dev = pdist.all_gather_rows(X_dev, group)
-            y_dev = pdist.all_gather_rows(y_dev[:, None], group)[:, 0]
-            if dev.type == "cuda" and PLAN_AHEAD:
-                overlap = plan_ahead(y_dev)
+            y_dev = y_full
     fit_group = None if task else group
     sel = build_selector(cfg)
     planned = False
-    if overlap is not None and group is None and not PLAN_THREAD:
+    # (task policy: every rank holds every row, so the single-process critical path applies — the
+    # plan, the speculative LassoCV refit and the stacking prelaunch; only the SMO problems are
+    # spread over the ranks, by the one all-reduce inside the prelaunched SVC batch)
+    local = group is None or task
+    if overlap is not None and local and not PLAN_THREAD:
         # the label-only stacking plan now, on the host, while the device imputes (LassoCV's
         # prelude reads wait for the imputation anyway): it is ready before the LassoCV path is
-        # launched, so the SVC batch can be enqueued first thing under the path
+        # launched, so the stacking fit can be enqueued first thing under the path
         overlap()
         hmark("plan_ready")
         overlap, planned = None, True
-    elif overlap is not None and group is None:
+    elif overlap is not None and local:
         # (PLAN_THREAD: joined as the first job under the LassoCV path)
         planned = True
     with timer.stage("select"):
-        jobs = []
+        jobs, early_jobs = [], []
         held_out = None
         if run_sel is not None:
             def held_out():
                 run_sel()
                 hmark("heldout_impute_enqueued")
         if overlap is not None:
-            jobs.append(overlap)
+            early_jobs.append(overlap)
         if bins_job is not None:
             def bins():
                 plan_box["bins_all"] = bins_job()
                 hmark("bins_ahead")
             jobs.append(bins)
-        if group is None and dev.type == "cuda" and (overlap is not None or planned):
-            def svc_early():
-                # the stacking fit's SVC batch, enqueued from the selector's DEVICE column list
-                # (speculative: lasso.SPECULATE) while the LassoCV path runs (stack_trainer.prelaunch_svc)
+        if local and dev.type == "cuda" and (overlap is not None or planned):
+            def stack_early():
+                # the stacking fit (SVC batch, GBC / L1-LR batches, meta model) enqueued from the
+                # selector's DEVICE column list — speculative (lasso.SPECULATE: the smallest-alpha
+                # refit's selection, enqueued before the LassoCV's grid read, lasso.EARLY_SPEC) —
+                # while the device still imputes / runs the LassoCV path (stack_trainer.prelaunch_stack)
                 cols = getattr(sel, "cols_dev_", None)
                 if cols is not None and plan_box.get("plan") is not None:
-                    from .models.stack_trainer import prelaunch_svc
-                    pre = prelaunch_svc(clf, X_dev, cols, y_dev, plan_box["plan"])
+                    from .models.stack_trainer import prelaunch_stack
+                    pre = prelaunch_stack(clf, X_dev, cols, y_dev, plan_box["plan"],
+                                          svc_group=group if task else None)
                     if pre is not None:
                         pre["speculative"] = bool(getattr(sel, "cols_speculative_", False))
+                        pre["cols_host"] = getattr(sel, "cols_host_", None)
                     plan_box["prelaunch"] = pre
-            jobs.append(svc_early)
+            early_jobs.append(stack_early)
+            def stack_bases():
+                # the GBC / L1-LR batches and the meta model of the prelaunched stack, behind the
+                # LassoCV's CV paths (which the speculation's check waits for)
+                from .models.stack_trainer import prelaunch_bases
+                prelaunch_bases(plan_box.get("prelaunch"))
+                hmark("bases_prelaunched")
+            if BASES_AFTER_CV:
+                jobs.insert(0, stack_bases)
+            else:
+                early_jobs.append(stack_bases)
         if held_out is not None:
-            jobs.append(held_out)     # (after the SVC batch: the held-out rows are needed last)
-        lasso_overlap = None
-        if jobs:
-            def lasso_overlap():
-                for j in jobs:
+            jobs.append(held_out)     # (after the stacking fit: the held-out rows are needed last)
+
+        def run_all(js):
+            if not js:
+                return None
+
+            def f():
+                for j in js:
                     j()
-        sfm = sel.fit(X_dev, y_dev, group=fit_group, overlap=lasso_overlap)
+            return f
+        sfm = sel.fit(X_dev, y_dev, group=fit_group, overlap=run_all(jobs), early_overlap=run_all(early_jobs))
         if run_sel is not None:
             X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
         hmark("lasso_fit")

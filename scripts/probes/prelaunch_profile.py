@@ -1,5 +1,5 @@
 """cProfile of the host work between the LassoCV path launch and the SVC batch's first rounds:
-stack_trainer.prelaunch_svc (the SVC batch enqueued on the speculative selection), 3 fits."""
+stack_trainer.prelaunch_stack (the stacking fit enqueued on the speculative selection), 3 fits."""
 import cProfile
 import os
 import pstats
@@ -17,7 +17,7 @@ dev = torch.device("cuda")
 Xd, yd, names = make_hf_cohort(10000, 40, seed=2020, nan_frac=0.02)
 Xs, ys, _ = make_hf_cohort(10000, 40, seed=2021, nan_frac=0.02)
 Xd, yd, Xs, ys = (torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys))
-orig = stack_trainer.prelaunch_svc
+orig = stack_trainer.prelaunch_stack
 pr = cProfile.Profile()
 on = [False]
 
@@ -32,7 +32,7 @@ def wrapped(*a, **k):
         pr.disable()
 
 
-stack_trainer.prelaunch_svc = wrapped
+stack_trainer.prelaunch_stack = wrapped
 for i in range(7):
     on[0] = i >= 4
     develop(Xd, yd, Xs, ys, names, device=dev, timer=StageTimer(enabled=False), evaluate=False)

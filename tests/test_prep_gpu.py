@@ -73,6 +73,39 @@ def test_lasso_speculative_refit_bit_identical(dev, monkeypatch):
     assert out[False][2] == out[True][2]
 
 
+@pytest.mark.parametrize("idx", [-1, 0])
+def test_lasso_early_speculation_bit_identical(dev, monkeypatch, idx):
+    """The early speculation (lasso.EARLY_SPEC: the speculated grid point computed on the device,
+    its refit enqueued before the grid's host read, no every-alpha refit) gives exactly the
+    non-speculative fit — α, coefficients, intercept, selection — when it hits (idx −1, the
+    smallest alpha: the cohort's winner) and when it misses (idx 0: the one refit after the paths);
+    its device alpha equals the host grid's end point bit for bit, and the early overlap runs
+    before the late one."""
+    from hfens.models import lasso
+    X, y, _ = make_hf_cohort(5000, 40, seed=9, nan_frac=0.0)
+    Xt, yt = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    out = {}
+    for spec in (False, True):
+        monkeypatch.setattr(lasso, "SPECULATE", spec)
+        monkeypatch.setattr(lasso, "SPEC_ALPHA_INDEX", idx)
+        order = []
+        s = lasso.SelectFromModel(LassoCV(cv=10), threshold=-np.inf, max_features=17)
+        s.fit(Xt, yt, overlap=lambda: order.append("late"), early_overlap=lambda: order.append("early"))
+        m = s.estimator_
+        assert order == ["early", "late"]
+        out[spec] = (m.alpha_, m.coef_.cpu(), float(m.intercept_), s.get_support().copy(),
+                     s.cols_dev_.cpu().numpy())
+        if spec:
+            assert float(m.spec_alpha_dev_) == float(m.alphas_[idx])
+            assert bool(s.cols_speculative_)
+    assert out[False][0] == out[True][0]
+    assert torch.equal(out[False][1], out[True][1])
+    assert out[False][2] == out[True][2]
+    assert np.array_equal(out[False][3], out[True][3])
+    assert np.array_equal(out[False][4], np.nonzero(out[False][3])[0])
+    assert np.array_equal(out[True][4], np.nonzero(out[True][3])[0]) == (idx == -1)
+
+
 @pytest.mark.parametrize("n,F,nan", [(20000, 40, 0.02), (6000, 17, 0.1), (3000, 64, 0.3), (4000, 33, 0.0)])
 def test_knn_fast_pass_same_donors(dev, monkeypatch, n, F, nan):
     """the packed-FMA fast pass with its exact lower-bound skip

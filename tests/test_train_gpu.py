@@ -896,7 +896,7 @@ def test_stacking_device_bases_match_synchronous(dev, monkeypatch):
 
 def test_prelaunched_svc_batch_matches(dev, monkeypatch):
     """The SVC batch enqueued under the LassoCV path from the selector's DEVICE column list
-    (stack_trainer.prelaunch_svc: device γ patched into the problem records, no host read before
+    (stack_trainer.prelaunch_stack: device γ patched into the problem records, no host read before
     the SMO) fits the same stack as the batch launched after the host knows the selection: the same
     columns, γ to the last bits of a variance sum (device two-pass vs torch's), and the same model
     up to the f32 pair sequence that a last-bit γ change may alter."""
@@ -969,3 +969,79 @@ def test_prelaunched_svc_without_early_read(dev, monkeypatch):
         assert stack_trainer.LAST_PRELAUNCH["used"]
     assert np.array_equal(out[True].selected, out[False].selected)
     assert torch.equal(out[True].proba_sel, out[False].proba_sel)
+
+
+def _task_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HFENS_DIST_REQUIRE_DEVICE="1")
+    import torch.distributed as dist
+    from hfens import pipeline
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import stack_trainer
+    from hfens.parallel import dist as pdist
+    from hfens.parallel.dist import all_gather_rows, shard_rows
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pdist.require_device_tensors()
+    try:
+        dev = torch.device("cuda:0")
+        pipeline.DP_POLICY = "task"
+        Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+        Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+        a = [torch.as_tensor(shard_rows(v, rank, world), device=dev) for v in (Xd, yd, Xs, ys)]
+        r = pipeline.develop(a[0], a[1], a[2], a[3], names, device=dev, group=dist.group.WORLD)
+        p = all_gather_rows(r.proba_sel.double()[:, None], dist.group.WORLD)[:, 0]
+        if rank == 0:
+            q.put((r.selected.copy(), p.cpu().numpy(), dict(stack_trainer.LAST_PRELAUNCH),
+                   r.model.oof_meta_.cpu().numpy(), _stack_params(r.model)))
+    finally:
+        pdist.shutdown()
+
+
+def _stack_params(m):
+    """The fitted refit models' parameters (host arrays) of a stacking fit."""
+    svc = m.estimators_[0].steps[1][1]
+    return [svc._dual_coef_.cpu().numpy(), svc._intercept_.cpu().numpy(), svc.support_.cpu().numpy(),
+            np.array([svc._probA.item(), svc._probB.item()]), m.estimators_[1].tree_value_.cpu().numpy(),
+            m.estimators_[1].tree_feature_.cpu().numpy(), m.estimators_[2].coef_.cpu().numpy(),
+            m.final_estimator_.coef_.cpu().numpy(), m.final_estimator_.intercept_.cpu().numpy()]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_develop_task_policy_prelaunched_matches_single(dev, world):
+    """the task policy (every rank holds every row, the SMO problems spread over the
+    ranks) runs the single-process critical path — the speculative selection, the stacking fit
+    prelaunched under the LassoCV path (device γ, device out-of-fold columns, the meta model) with
+    the task-parallel SMO's one all-reduce inside it.  2 and 3 processes on one card (gloo, device
+    tensors only): the stack's out-of-fold matrix and the held-out probabilities equal the single
+    process's bit for bit (the solutions travel as their f64 bit patterns), and so do the refit
+    models' parameters; the held-out rows are scored per shard (other batch shapes of the f32
+    inference kernels), so within 1e-5."""
+    import socket
+    import torch.multiprocessing as mp
+    from hfens import pipeline
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import stack_trainer
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_task_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    sel, p, lp, oof, params = q.get(timeout=150)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert lp["used"] and lp["speculative"] and not lp.get("spec_miss")
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    a = [torch.as_tensor(v, device=dev) for v in (Xd, yd, Xs, ys)]
+    r = pipeline.develop(a[0], a[1], a[2], a[3], names, device=dev)
+    assert stack_trainer.LAST_PRELAUNCH["used"]
+    assert np.array_equal(sel, r.selected)
+    assert np.array_equal(oof, r.model.oof_meta_.cpu().numpy())
+    for a, b in zip(params, _stack_params(r.model)):
+        assert np.array_equal(a, b)
+    assert float(np.abs(p - r.proba_sel.double().cpu().numpy()).max()) <= 1e-5
