@@ -18,6 +18,37 @@ import torch
 
 def stratified_kfold_test_folds(y, n_splits: int = 5) -> np.ndarray:
     y = np.asarray(y.cpu() if isinstance(y, torch.Tensor) else y).ravel()
+    if y.size:
+        tf = _stratified_binary(y, n_splits)
+        if tf is not None:
+            return tf
+    return _stratified_generic(y, n_splits)
+
+
+def _stratified_binary(y: np.ndarray, n_splits: int):
+    """Two-class labels (the stacking fit's): the same assignment as :func:`_stratified_generic`
+    in a few vector ops — class 0 is the first label seen, the sorted encoded labels are class 0's
+    count then class 1's, so fold i's share of class 0 is the count of positions ≡ i (mod k)
+    below that count.  None when the labels are not two-valued."""
+    enc = y != y[0]
+    j = int(enc.argmax())
+    if not enc[j] or not ((y == y[0]) | (y == y[j])).all():
+        return None
+    n = y.size
+    c0 = n - int(np.count_nonzero(enc))
+    counts = np.array([c0, n - c0])
+    if np.all(n_splits > counts):
+        raise ValueError(f"n_splits={n_splits} cannot be greater than the number of members in each class")
+    i = np.arange(n_splits)
+    tot = (n - i + n_splits - 1) // n_splits                   # positions ≡ i (mod k) in [0, n)
+    a0 = np.where(c0 > i, (c0 - i + n_splits - 1) // n_splits, 0)
+    test_folds = np.empty(n, dtype=np.int64)
+    test_folds[~enc] = np.repeat(i, a0)
+    test_folds[enc] = np.repeat(i, tot - a0)
+    return test_folds
+
+
+def _stratified_generic(y: np.ndarray, n_splits: int) -> np.ndarray:
     _, y_idx, y_inv = np.unique(y, return_index=True, return_inverse=True)
     _, class_perm = np.unique(y_idx, return_inverse=True)
     y_enc = class_perm[y_inv]

@@ -128,8 +128,46 @@ class _Prob:
 
 
 def _expand(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
-    """libsvm problem list of one SVC fit — pure host index bookkeeping on the labels (numpy),
-    so preparing the 36 problems costs no device round trips."""
+    """libsvm problem list of one SVC fit — pure host index bookkeeping on the labels, so preparing
+    the 36 problems costs no device round trips (native: ops/csrc/host.hip svc_expand_host, one call;
+    :func:`_expand_py` is the numpy original, equal array for array — tests/test_smo_host.py)."""
+    from .. import ops
+    if NATIVE_EXPAND and ops.has_ext():
+        return _expand_native(fit_id, y_np, gamma, cw, svc)
+    return _expand_py(fit_id, y_np, gamma, cw, svc)
+
+
+NATIVE_EXPAND = os.environ.get("HFENS_NATIVE_EXPAND", "1") != "0"
+
+
+def _expand_native(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
+    from .. import ops
+    y = np.ascontiguousarray(y_np, dtype=np.float64)
+    l = int(y.shape[0])
+    seed = sklearn_libsvm_seed(svc.random_state) & 0xFFFFFFFF if svc.probability else -1
+    out = np.empty((7 if svc.probability else 1) * l, dtype=np.int64)
+    meta = np.empty(21, dtype=np.int64)
+    ops.ext().svc_expand_host(y.ctypes.data, l, seed, out.ctypes.data, meta.ctypes.data)
+    grouped = out[:l]
+    n0 = int(meta[0])
+    C0, C1 = float(svc.C * cw[0]), float(svc.C * cw[1])
+    probs = []
+    if svc.probability:
+        perm, gp, rows_all = out[l:2 * l], out[2 * l:3 * l], out[3 * l:]
+        for k in range(5):
+            b, e = k * l // 5, (k + 1) * l // 5
+            n1, nn0, off, ln = (int(v) for v in meta[1 + 4 * k:5 + 4 * k])
+            held = perm[b:e]
+            if n1 == 0 or nn0 == 0:
+                probs.append(_Prob(fit_id, k, None, 0, 0.0, 0.0, gamma, held, gp[b:e],
+                                   const=1.0 if n1 == 0 else -1.0))
+                continue
+            probs.append(_Prob(fit_id, k, rows_all[off:off + ln], n1, C1, C0, gamma, held, gp[b:e]))
+    probs.append(_Prob(fit_id, -1, grouped, n0, C0, C1, gamma))
+    return probs, dict(grouped=grouped, n0=n0, l=l, gamma=gamma, C0=C0, C1=C1)
+
+
+def _expand_py(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
     yb = y_np > 0.5
     idx0 = np.nonzero(~yb)[0]
     idx1 = np.nonzero(yb)[0]
@@ -654,7 +692,11 @@ WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds 
 WS_SEEDED_AHEAD = int(os.environ.get("HFENS_SVM_WS_SEEDED_AHEAD", "48"))
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
-# HIP-graph replay of the rounds: "1" K-cached rounds only, "all" the q = 1024 rounds too, "0" off
+# HIP-graph replay of the rounds: "1" K-cached rounds only, "all" the q = 1024 rounds too, "0" off.
+# ("all" re-measured in round 6, when the prelaunched stack's host enqueue — 38 ws_steps calls,
+# ≈ 450 kernel launches, 1.7 ms of host time per fit — sat on the critical path: no gain, 19.2 /
+# 20.4 vs 19.3 / 18.9 ms, profiles/r6_runs/r6g; ROCm's graph launch costs about as much host time
+# per node as a direct launch)
 WS_GRAPH = os.environ.get("HFENS_SVM_WS_GRAPH", "1")
 WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # rounds per captured graph
 _WS_GRAPHS: dict = {}
@@ -838,9 +880,17 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
     P = len(idx)
     frac = WS_INNER_FRAC if frac is None else frac
     arr = np.zeros(P, _WS_DT)
-    for k, j in enumerate(idx):
-        p = live[j]
-        arr[k] = (zoffs[j], aoffs[j], p.l, p.npos, p.Cp, p.Cn, -p.gamma * 1.4426950408889634, 0)
+    # (column-wise: a per-record tuple assignment costs ~1.5 µs each, ≈ 0.3 ms for the cascade's
+    # ~200 parts on the host critical path)
+    ii = np.asarray(idx, dtype=np.int64)
+    ps = [live[j] for j in idx]
+    arr["zoff"] = np.asarray(zoffs, dtype=np.int64)[ii]
+    arr["aoff"] = np.asarray(aoffs, dtype=np.int64)[ii]
+    arr["l"] = [p.l for p in ps]
+    arr["npos"] = [p.npos for p in ps]
+    arr["Cp"] = [p.Cp for p in ps]
+    arr["Cn"] = [p.Cn for p in ps]
+    arr["ngl2e"] = [-p.gamma * 1.4426950408889634 for p in ps]
     max_l = int(arr["l"].max())
     ctx = (lambda: torch.cuda.stream(side)) if side is not None else contextlib.nullcontext
     out = dict(side=side, idx=np.asarray(idx, dtype=np.int64), err=None)

@@ -477,6 +477,9 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
     def new_final():
         return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
     stc["new_final"] = new_final
+    stc.update(early=None, dev_bases=None)
+    # the SVC batch first (the fit's critical path); the other bases' device state after it
+    stc["concurrent"] = _launch_svc(stc)
     early = None
     if group is None and EARLY_META:
         fm = [new_final()]
@@ -489,7 +492,6 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
     if group is None and X.is_cuda and DEVICE_BASES:
         dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
     stc.update(early=early, dev_bases=dev_bases)
-    stc["concurrent"] = _launch_svc(stc)
     if stc["concurrent"] and bases:
         _launch_bases(stc)
     return stc

@@ -7,8 +7,10 @@
 //                Fisher-Yates loop executed for every SVC fit.
 // Licence: the libsvm RNG draws and the splitter's rand_r order follow scikit-learn / LIBSVM
 // (BSD-3-Clause; notices in THIRD_PARTY_NOTICES.md at the repository root).
+#include <algorithm>
 #include <cstdint>
 #include <random>
+#include <vector>
 
 namespace hfens {
 
@@ -235,6 +237,69 @@ void knn_plan_host(uintptr_t bits_, long long n, int F, int slots, uintptr_t out
     }
     for (; s < nslot; ++s) slot[k * nslot + s] = -1;
     ++k;
+  }
+}
+
+
+// svc_expand_host: the label-only libsvm problem expansion of one probability SVC fit
+// (models/smo.py _expand): class-grouped positions (class 0 first), the Platt-CV permutation
+// (libsvm_perm above), and for each of the 5 internal folds the training rows in permutation order,
+// class 1 first — every array the 36-problem batch is built from, in ONE host call instead of ~20
+// numpy calls per fold (the stacking plan sits on the headline's host critical path).
+//   y[n] (0/1) → out (int64): grouped[n] | perm[n] | gp[n] = grouped[perm] | rows of folds 0..4
+//   (concatenated, ≤ 4n) ; meta (int64): n0, then per fold (n1, nn0, rows offset, rows length).
+//   seed < 0: no Platt folds (only grouped).
+void svc_expand_host(uintptr_t y_ptr, long long n, long long seed, uintptr_t out_ptr, uintptr_t meta_ptr) {
+  const double* y = reinterpret_cast<const double*>(y_ptr);
+  int64_t* out = reinterpret_cast<int64_t*>(out_ptr);
+  int64_t* meta = reinterpret_cast<int64_t*>(meta_ptr);
+  int64_t* grouped = out;
+  int64_t n0 = 0;
+  for (long long i = 0; i < n; ++i)
+    if (!(y[i] > 0.5)) grouped[n0++] = i;
+  int64_t w = n0;
+  for (long long i = 0; i < n; ++i)
+    if (y[i] > 0.5) grouped[w++] = i;
+  meta[0] = n0;
+  if (seed < 0) return;
+  const long long l = n;
+  int64_t* perm = out + l;
+  int64_t* gp = out + 2 * l;
+  int64_t* rows = out + 3 * l;
+  libsvm_perm(static_cast<int>(l), seed, reinterpret_cast<uintptr_t>(perm));
+  for (long long i = 0; i < l; ++i) gp[i] = grouped[perm[i]];
+  // class-1 / class-0 permutation positions and their rows (each in position order), then every
+  // fold's training rows are two contiguous copies per class around the fold's position range
+  std::vector<int64_t> i1, i0, g1, g0;
+  i1.reserve(l - n0);
+  i0.reserve(n0);
+  for (long long p = 0; p < l; ++p) (perm[p] >= n0 ? i1 : i0).push_back(p);
+  g1.resize(i1.size());
+  g0.resize(i0.size());
+  for (size_t j = 0; j < i1.size(); ++j) g1[j] = gp[i1[j]];
+  for (size_t j = 0; j < i0.size(); ++j) g0[j] = gp[i0[j]];
+  int64_t off = 0;
+  for (int k = 0; k < 5; ++k) {
+    const long long b = k * l / 5, e = (k + 1) * l / 5;
+    const int64_t lo1 = std::lower_bound(i1.begin(), i1.end(), (int64_t)b) - i1.begin();
+    const int64_t hi1 = std::lower_bound(i1.begin(), i1.end(), (int64_t)e) - i1.begin();
+    const int64_t lo0 = std::lower_bound(i0.begin(), i0.end(), (int64_t)b) - i0.begin();
+    const int64_t hi0 = std::lower_bound(i0.begin(), i0.end(), (int64_t)e) - i0.begin();
+    const int64_t n1 = lo1 + (int64_t)i1.size() - hi1, nn0 = lo0 + (int64_t)i0.size() - hi0;
+    meta[1 + 4 * k] = n1;
+    meta[2 + 4 * k] = nn0;
+    meta[3 + 4 * k] = off;
+    if (n1 == 0 || nn0 == 0) {
+      meta[4 + 4 * k] = 0;
+      continue;
+    }
+    int64_t* r = rows + off;
+    r = std::copy(g1.begin(), g1.begin() + lo1, r);
+    r = std::copy(g1.begin() + hi1, g1.end(), r);
+    r = std::copy(g0.begin(), g0.begin() + lo0, r);
+    r = std::copy(g0.begin() + hi0, g0.end(), r);
+    meta[4 + 4 * k] = n1 + nn0;
+    off += n1 + nn0;
   }
 }
 

@@ -21,3 +21,47 @@ def test_cascade_parts_partition_the_problem(l, npos):
         cp = int((pos < npos).sum())
         assert np.all(pos[:cp] < npos) and np.all(pos[cp:] >= npos)
         assert abs(cp - npos / P) <= 1 and abs((pos.shape[0] - cp) - (l - npos) / P) <= 1
+
+
+@pytest.mark.parametrize("n,p1,seed", [(10000, 0.2, 2020), (713, 0.198, 7), (37, 0.05, 3), (12, 0.1, 1), (9, 0.0, 5)])
+def test_native_expand_matches_numpy(n, p1, seed):
+    """ops/csrc/host.hip svc_expand_host (one native call per fit, the stacking plan's hot loop)
+    equals the numpy expansion array for array: grouped positions, Platt folds' training rows in
+    permutation order (class 1 first), held-out positions and rows, class counts, constant folds."""
+    from hfens import ops
+    from hfens.models import smo
+    from hfens.models.svc import SVC
+    if not ops.has_ext():
+        pytest.skip("extension not built")
+    rng = np.random.default_rng(seed)
+    y = (rng.random(n) < p1).astype(np.float64)
+    for prob in (True, False):
+        svc = SVC(class_weight="balanced", probability=prob, random_state=seed)
+        cw = np.array([0.7, 2.1])
+        a, ma = smo._expand_native(0, y, 0.25, cw, svc)
+        b, mb = smo._expand_py(0, y, 0.25, cw, svc)
+        assert len(a) == len(b)
+        assert ma["n0"] == mb["n0"] and ma["l"] == mb["l"] and np.array_equal(ma["grouped"], mb["grouped"])
+        for p, q in zip(a, b):
+            assert (p.fold, p.npos, p.Cp, p.Cn, p.const) == (q.fold, q.npos, q.Cp, q.Cn, q.const)
+            for f in ("rows", "held", "held_rows"):
+                u, v = getattr(p, f), getattr(q, f)
+                assert (u is None) == (v is None)
+                if u is not None:
+                    assert np.array_equal(u, v), f
+
+
+@pytest.mark.parametrize("n,p1,seed", [(10000, 0.2, 1), (713, 0.198, 2), (23, 0.5, 3), (11, 0.3, 4)])
+def test_stratified_binary_fast_path_matches_generic(n, p1, seed):
+    """model_selection._stratified_binary (the stacking plan's folds in a few vector ops) gives
+    StratifiedKFold's assignment exactly as the generic np.unique path does, whichever class
+    appears first."""
+    from hfens.models import model_selection as ms
+    rng = np.random.default_rng(seed)
+    for first in (0.0, 1.0):
+        y = (rng.random(n) < p1).astype(np.float64)
+        y[0] = first
+        if len(np.unique(y)) < 2:
+            continue
+        assert np.array_equal(ms._stratified_binary(y, 5), ms._stratified_generic(y, 5))
+    assert ms._stratified_binary(np.array([0.0, 1.0, 2.0, 1.0, 0.0, 2.0]), 2) is None
