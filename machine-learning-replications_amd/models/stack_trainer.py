@@ -365,6 +365,10 @@ PRELAUNCH_BASES = os.environ.get("HFENS_PRELAUNCH_BASES", "1") != "0"
 # device γ for the stacking fit's SVC batch whenever eligible (working-set solver, planned labels,
 # gamma='scale'): no host read of the scaled rows' variance before the SMO, prelaunched or not
 GAMMA_DEV = os.environ.get("HFENS_SVC_GAMMA_DEV", "1") != "0"
+# the GBC / LR / meta device state (index uploads, label prep) built before the SVC batch is enqueued
+# ("before") or after it on the bases stream ("after"); built after it on the caller's stream it made
+# the GBC's host bin fit wait for the whole SMO (profiles/r6_runs/r6h: gbc_binned 16.7 ms)
+BASES_SETUP = os.environ.get("HFENS_BASES_SETUP", "before")
 LAST_PRELAUNCH = {"used": False}
 
 
@@ -478,20 +482,32 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
         return clf.final_estimator.clone() if clf.final_estimator is not None else LogisticRegression()
     stc["new_final"] = new_final
     stc.update(early=None, dev_bases=None)
-    # the SVC batch first (the fit's critical path); the other bases' device state after it
-    stc["concurrent"] = _launch_svc(stc)
-    early = None
-    if group is None and EARLY_META:
-        fm = [new_final()]
-        # the meta model's label-only inputs now, on this (otherwise idle) stream: behind the
-        # out-of-fold columns only the features' guard and the intercept column remain
-        from .logreg_solver import logreg_label_prep
-        lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
-        early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
-    dev_bases = None
-    if group is None and X.is_cuda and DEVICE_BASES:
-        dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
-    stc.update(early=early, dev_bases=dev_bases)
+
+    def bases_state():
+        early = None
+        if group is None and EARLY_META:
+            fm = [new_final()]
+            # the meta model's label-only inputs now, on this (otherwise idle) stream: behind the
+            # out-of-fold columns only the features' guard and the intercept column remain
+            from .logreg_solver import logreg_label_prep
+            lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
+            early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
+        dev_bases = None
+        if group is None and X.is_cuda and DEVICE_BASES:
+            dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)
+        stc.update(early=early, dev_bases=dev_bases)
+    if BASES_SETUP == "before" or not X.is_cuda:
+        bases_state()
+        stc["concurrent"] = _launch_svc(stc)
+    else:
+        # the SVC batch first (the fit's critical path); the other bases' device state after it, on
+        # the bases stream
+        stc["concurrent"] = _launch_svc(stc)
+        from .. import runtime
+        other = runtime.stream(dev, "bases")
+        other.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(other):
+            bases_state()
     if stc["concurrent"] and bases:
         _launch_bases(stc)
     return stc
