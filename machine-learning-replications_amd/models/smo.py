@@ -1039,13 +1039,22 @@ PROFILE_WS = os.environ.get("HFENS_PROFILE_WS", "0") == "1"       # phase counte
 
 
 def assign_problems(sizes, world: int) -> List[int]:
-    """Owner rank of every SMO problem: longest-processing-time-first (largest problem onto the
-    least-loaded rank; cost ∝ points, since pairs grow ~linearly with l and the cooperative
-    solver's per-pair time is ~flat).  Deterministic, identical on every rank."""
+    """Owner rank of every SMO problem, identical on every rank.  On a GPU the problems of one rank
+    run side by side (one CU each), so a rank's time is its LARGEST problem's (the sequential pair
+    loop), not the sum: the largest problem — the fit's critical path — gets rank 0 to itself
+    (nothing else competes for its rank's CUs, HBM or host launches), and the others are spread
+    longest-first onto the least-loaded of ranks 1 … W−1 (cost ∝ points).  One rank: all on 0."""
     load = [0] * world
     owner = [0] * len(sizes)
-    for k in sorted(range(len(sizes)), key=lambda k: (-sizes[k], k)):
-        r = min(range(world), key=lambda r: (load[r], r))
+    order = sorted(range(len(sizes)), key=lambda k: (-sizes[k], k))
+    if world >= 2 and len(sizes) >= 2:
+        owner[order[0]] = 0
+        load[0] = sizes[order[0]]
+        order, ranks = order[1:], range(1, world)
+    else:
+        ranks = range(world)
+    for k in order:
+        r = min(ranks, key=lambda r: (load[r], r))
         owner[k] = r
         load[r] += sizes[k]
     return owner

@@ -278,17 +278,23 @@ def _launch_bases(stc):
         logreg_solver.BLOCK_BUDGET[0] = max(1, _smo._num_cus(X.device) - int(_smo.LAST_SMO_INFO["problems"]) - 8)
     try:
         with torch.cuda.stream(other):
-            for i, (name, est) in enumerate(clf.estimators):
-                if i not in svc_cols:
-                    r = dev_bases["fit"](i, est) if dev_bases is not None else None
-                    if r is not None:
-                        out[i] = r        # enqueued, out-of-fold column on the device
-                    else:
-                        out[i] = fit_base_batch(est, X, y, masks, group=group)
-                        if oof is not None:
-                            oof(i, out[i])
-                    hmark(f"{name}_host_done")
-                    dmark(f"{name}_done")
+            # the L1-LR batch (one ≈ 2 ms cooperative launch) before the GBC's 100-stage loop: the
+            # meta model waits for both, and the LR behind the GBC ended last (r6i: lg_done 17.9 vs
+            # the SVC's out-of-fold column at 17.5 ms)
+            order = [i for i in range(len(clf.estimators)) if i not in svc_cols]
+            if LR_FIRST:
+                order.sort(key=lambda i: 0 if _kind(clf.estimators[i][1]) == "lr" else 1)
+            for i in order:
+                name, est = clf.estimators[i]
+                r = dev_bases["fit"](i, est) if dev_bases is not None else None
+                if r is not None:
+                    out[i] = r        # enqueued, out-of-fold column on the device
+                else:
+                    out[i] = fit_base_batch(est, X, y, masks, group=group)
+                    if oof is not None:
+                        oof(i, out[i])
+                hmark(f"{name}_host_done")
+                dmark(f"{name}_done")
             # every meta-feature column of these bases is enqueued on this stream by now: the
             # meta model waits for this point, not for the bookkeeping enqueued after it
             cols_ev = torch.cuda.Event()
@@ -366,9 +372,12 @@ PRELAUNCH_BASES = os.environ.get("HFENS_PRELAUNCH_BASES", "1") != "0"
 # gamma='scale'): no host read of the scaled rows' variance before the SMO, prelaunched or not
 GAMMA_DEV = os.environ.get("HFENS_SVC_GAMMA_DEV", "1") != "0"
 # the GBC / LR / meta device state (index uploads, label prep) built before the SVC batch is enqueued
-# ("before") or after it on the bases stream ("after"); built after it on the caller's stream it made
-# the GBC's host bin fit wait for the whole SMO (profiles/r6_runs/r6h: gbc_binned 16.7 ms)
-BASES_SETUP = os.environ.get("HFENS_BASES_SETUP", "before")
+# ("before") or after it on the bases stream ("after", default: the SVC batch's host enqueue starts
+# ≈ 0.4 ms earlier; same fit time on one box, 18.99 / 18.19 vs 19.03 / 18.23 ms, profiles/r6_runs/r6i);
+# built after it on the CALLER's stream it made the GBC's host bin fit wait for the whole SMO
+# (profiles/r6_runs/r6h: gbc_binned 16.7 ms)
+BASES_SETUP = os.environ.get("HFENS_BASES_SETUP", "after")
+LR_FIRST = os.environ.get("HFENS_LR_FIRST", "1") != "0"
 LAST_PRELAUNCH = {"used": False}
 
 

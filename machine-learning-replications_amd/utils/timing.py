@@ -112,9 +112,17 @@ def hmark(name: str) -> None:
         _MARKS.append((name, time.perf_counter()))
 
 
+def _rank_prefix(prefix: str) -> str:
+    """"[host]" → "[host r1]" on rank 1 of a multi-process run (torchrun: the ranks share stderr)."""
+    if int(_os.environ.get("WORLD_SIZE", "1")) > 1:
+        return prefix[:-1] + f" r{_os.environ.get('RANK', '0')}]"
+    return prefix
+
+
 def hmarks_flush(prefix: str = "[host]") -> None:
     if TRACE_HOST and _MARKS:
         import sys
+        prefix = _rank_prefix(prefix)
         t0 = _MARKS[0][1]
         print(prefix + " " + " ".join(f"{k}={1e3 * (v - t0):.1f}" for k, v in _MARKS), file=sys.stderr)
         _MARKS.clear()
@@ -141,6 +149,7 @@ def dmark(name: str) -> None:
 def dmarks_flush(prefix: str = "[dev]") -> None:
     if TRACE_DEV and _DMARKS:
         import sys
+        prefix = _rank_prefix(prefix)
         for _, e in _DMARKS:
             e.synchronize()
         e0 = _DMARKS[0][1]

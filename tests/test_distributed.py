@@ -243,11 +243,17 @@ def test_lasso_dp(world):
 
 
 def test_assign_problems_lpt():
+    """The largest SMO problem (the critical path) owns rank 0 alone; the rest are spread
+    longest-first over ranks 1 … W−1; one rank keeps everything."""
     from hfens.models.smo import assign_problems
-    own = assign_problems([10, 8, 8, 8, 8, 8, 6, 6], 4)
-    assert own[0] == 0 and sorted(set(own)) == [0, 1, 2, 3]
-    loads = [sum(s for s, o in zip([10, 8, 8, 8, 8, 8, 6, 6], own) if o == r) for r in range(4)]
-    assert max(loads) - min(loads) <= 4
+    sizes = [10, 8, 8, 8, 8, 8, 6, 6]
+    own = assign_problems(sizes, 4)
+    assert own[0] == 0 and own.count(0) == 1 and sorted(set(own)) == [0, 1, 2, 3]
+    loads = [sum(s for s, o in zip(sizes, own) if o == r) for r in range(1, 4)]
+    assert max(loads) - min(loads) <= 6
+    assert assign_problems(sizes, 1) == [0] * len(sizes)
+    assert assign_problems(sizes, 2) == [0] + [1] * 7
+    assert assign_problems([5], 3) == [0]
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
