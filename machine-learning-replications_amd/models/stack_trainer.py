@@ -282,7 +282,12 @@ def _launch_bases(stc):
             # meta model waits for both, and the LR behind the GBC ended last (r6i: lg_done 17.9 vs
             # the SVC's out-of-fold column at 17.5 ms)
             order = [i for i in range(len(clf.estimators)) if i not in svc_cols]
-            if LR_FIRST:
+            if LR_FIRST and dev_bases is not None:
+                for i in order:
+                    if _kind(clf.estimators[i][1]) == "gbc":
+                        dev_bases["prebin"](clf.estimators[i][1])
+                        hmark("gbc_prebinned")
+                        break
                 order.sort(key=lambda i: 0 if _kind(clf.estimators[i][1]) == "lr" else 1)
             for i in order:
                 name, est = clf.estimators[i]
@@ -582,11 +587,21 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
     nb = int(masks.shape[0])
     E = ops.ext()
 
+    box = {}
+
+    def prebin(est):
+        """The GBC's bin map (its host fit reads X back: done before anything else is queued on
+        the bases stream, so that read does not wait for another base's solve)."""
+        from .binning import fit_bins
+        # (the inputs' guards are queued by the fit itself, on the deferred read)
+        bm = fit_bins(Xc, int(est.max_bins))
+        box["binned"] = (bm, bm.transform(Xc).contiguous())
+
     def gbc(col, est):
         clones = [est.clone() for _ in range(nb)]
-        binned = None
+        binned = box.pop("binned", None)
         ba, cols = (plan or {}).get("bins_all"), (plan or {}).get("cols")
-        if ba is not None and cols is not None and int(ba.max_bins) == int(clones[0].max_bins):
+        if binned is None and ba is not None and cols is not None and int(ba.max_bins) == int(clones[0].max_bins):
             bm = ba.select(cols)     # binned under the LassoCV path (pipeline.develop), columns selected here
             binned = (bm, bm.transform(Xc).contiguous())
         so = {}
@@ -645,7 +660,7 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
             return lr(col, est)
         return None
 
-    return dict(fit=fit, deferred=deferred, post=post, keep=keep)
+    return dict(fit=fit, deferred=deferred, post=post, keep=keep, prebin=prebin)
 
 
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
