@@ -365,7 +365,10 @@ def fit_gbdt_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[tor
             st.frank = sklearn_stump_ranks(models, bins, masks.to(dev), T, group,
                                            nb_host=bm.nb_host if (all_rows and group is None) else None)
     hmark("gbc_ranks")
-    st.no_persist = dfr is not None     # (a persistent loop's barrier fallback needs a host read)
+    # (a persistent loop's barrier fallback needs a host read: under a deferred read only when the
+    # caller handles it, PERSIST_STACK — the stacking trainer registers the loop's error word)
+    st.no_persist = dfr is not None and not (PERSIST_STACK and state_out is not None)
+    st.force_persist = dfr is not None and PERSIST_STACK and state_out is not None
     if X.is_cuda:
         _run_device(st, group)
     else:
@@ -739,6 +742,10 @@ PROFILE_STAGE_T = int(os.environ.get("HFENS_GBDT_STAGE_PROF", "-1"))   # stage w
 PERSIST = os.environ.get("HFENS_GBDT_PERSIST", "auto")
 PERSIST_MIN_ROWS = int(os.environ.get("HFENS_GBDT_PERSIST_MIN_ROWS", "65536"))
 PERSIST_MAX_WGS = int(os.environ.get("HFENS_GBDT_PERSIST_MAX_WGS", "128"))
+# the stacking trainer's deferred (no host read) GBC batch as ONE persistent launch too, whatever its
+# size (the headline's 10k rows × 6 models: 60 workgroups, 100 stage launches otherwise); its barrier
+# deadline word is read with the batch's deferred guards and a miss re-runs the fit per stage
+PERSIST_STACK = os.environ.get("HFENS_GBDT_PERSIST_STACK", "0") == "1"
 _PERSIST_OFF = [False]     # set while a fit re-runs after a persistent-loop barrier timeout
 LAST_STAGE_PROF: dict = {}
 
@@ -831,8 +838,9 @@ def _run_stage(st: _State, group):
     ev0.record()
     persist = (group is None and prof is None and not uses_partials and st.B * groups <= _num_cus(dev)
                and not _PERSIST_OFF[0] and not getattr(st, "no_persist", False)
-               and (PERSIST == "1" or (PERSIST == "auto" and st.n >= PERSIST_MIN_ROWS
-                                       and st.B * groups <= PERSIST_MAX_WGS)))
+               and (PERSIST == "1" or (PERSIST == "auto" and getattr(st, "force_persist", False)
+                                       and st.B * groups <= PERSIST_MAX_WGS)
+                    or (PERSIST == "auto" and st.n >= PERSIST_MIN_ROWS and st.B * groups <= PERSIST_MAX_WGS)))
     GRAPH_INFO["persist"] = persist
     if persist:
         be = runtime.workspace(dev, "gbdt_persist_bar", st.B + 1, torch.int32)   # [B] counters, err

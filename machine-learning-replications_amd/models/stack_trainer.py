@@ -607,11 +607,35 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
         so = {}
         fit_gbdt_batch(clones, Xc, y, masks, binned=binned, deferred=deferred, finish={nb - 1}, state_out=so)
         st, raw0 = so["st"], so["raw0"].contiguous()
-        E.oof_trees(Xc.data_ptr(), F, oof_rows.data_ptr(), oof_model.data_ptr(), m, so["T"], nb, so["NN"],
-                    st.feat.data_ptr(), st.thr.data_ptr(), st.value.data_ptr(), raw0.data_ptr(), so["lr"],
-                    meta.data_ptr(), int(meta.shape[1]), col, ops.stream_ptr(dev))
+
+        def column(so_, st_, raw0_):
+            E.oof_trees(Xc.data_ptr(), F, oof_rows.data_ptr(), oof_model.data_ptr(), m, so_["T"], nb, so_["NN"],
+                        st_.feat.data_ptr(), st_.thr.data_ptr(), st_.value.data_ptr(), raw0_.data_ptr(), so_["lr"],
+                        meta.data_ptr(), int(meta.shape[1]), col, ops.stream_ptr(dev))
+        column(so, st, raw0)
         keep.append((st, raw0))
         post.append(so["finish"])
+        if getattr(st, "persist_err", None) is not None:
+            def on_fail(_v):
+                # a barrier wait of the persistent stage loop passed its deadline: the trees are
+                # partial — re-run the batch with one launch per stage (same trees, bit for bit), its
+                # out-of-fold column, and the meta model launched on the stale one is refitted
+                import warnings
+                from . import hist_gbdt
+                warnings.warn("GBDT persistent stage loop: a barrier wait passed its deadline; re-running "
+                              "the stacking GBC batch with one launch per stage", RuntimeWarning)
+                hist_gbdt.LAST_PATH["persist_fallback"] = hist_gbdt.LAST_PATH.get("persist_fallback", 0) + 1
+                hist_gbdt._PERSIST_OFF[0] = True
+                try:
+                    so2 = {}
+                    fit_gbdt_batch(clones, Xc, y, masks, binned=binned, finish={nb - 1}, state_out=so2)
+                finally:
+                    hist_gbdt._PERSIST_OFF[0] = False
+                column(so2, so2["st"], so2["raw0"].contiguous())
+                keep.append((so2["st"], so2["raw0"]))
+                if early is not None:
+                    early["stale"] = True
+            deferred.word(st.persist_err, on_fail)
         return clones
 
     def lr(col, est):

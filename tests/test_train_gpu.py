@@ -1045,3 +1045,33 @@ def test_develop_task_policy_prelaunched_matches_single(dev, world):
     for a, b in zip(params, _stack_params(r.model)):
         assert np.array_equal(a, b)
     assert float(np.abs(p - r.proba_sel.double().cpu().numpy()).max()) <= 1e-5
+
+
+def test_stacking_persistent_gbc_and_fallback(dev, monkeypatch):
+    """HFENS_GBDT_PERSIST_STACK: the stacking fit's deferred GBC batch as ONE persistent launch gives
+    the launch-per-stage stack bit for bit; a forced barrier-deadline miss is caught
+    by the deferred read, re-runs the batch per stage and refits the meta model — the same stack
+    (deadline −1: the failure injected at the first barrier)."""
+    from hfens import pipeline
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import hist_gbdt
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for tag, persist, deadline in (("launch", False, None), ("persist", True, None), ("miss", True, "-1")):
+        monkeypatch.setattr(hist_gbdt, "PERSIST_STACK", persist)
+        if deadline is not None:
+            monkeypatch.setenv("HFENS_GBDT_PERSIST_DEADLINE_MS", deadline)
+        hist_gbdt.LAST_PATH.pop("persist_fallback", None)
+        import warnings
+        with warnings.catch_warnings(record=True):
+            warnings.simplefilter("always")
+            out[tag] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+        out[tag + "_persist"] = hist_gbdt.GRAPH_INFO.get("persist")
+        out[tag + "_fb"] = hist_gbdt.LAST_PATH.get("persist_fallback", 0)
+    assert out["persist_persist"] and not out["launch_persist"] and out["persist_fb"] == 0
+    assert out["miss_fb"] >= 1
+    for tag in ("persist", "miss"):
+        assert torch.equal(out["launch"].model.oof_meta_, out[tag].model.oof_meta_)
+        assert torch.equal(out["launch"].proba_sel, out[tag].proba_sel)
