@@ -745,7 +745,9 @@ PERSIST_MAX_WGS = int(os.environ.get("HFENS_GBDT_PERSIST_MAX_WGS", "128"))
 # the stacking trainer's deferred (no host read) GBC batch as ONE persistent launch too, whatever its
 # size (the headline's 10k rows × 6 models: 60 workgroups, 100 stage launches otherwise); its barrier
 # deadline word is read with the batch's deferred guards and a miss re-runs the fit per stage
-PERSIST_STACK = os.environ.get("HFENS_GBDT_PERSIST_STACK", "0") == "1"
+# (measured on one box, profiles/r6_runs/r6m: 18.40 / 18.11 vs 19.20 / 19.21 ms / fit; gbc_done 15.0 vs
+# 18.8 ms in the device timeline)
+PERSIST_STACK = os.environ.get("HFENS_GBDT_PERSIST_STACK", "1") == "1"
 _PERSIST_OFF = [False]     # set while a fit re-runs after a persistent-loop barrier timeout
 LAST_STAGE_PROF: dict = {}
 
