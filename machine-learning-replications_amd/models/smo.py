@@ -831,6 +831,9 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         r["finish"]()
         if evs is not None:
             _mark(gi, r)
+        # the run's closures refer back to its dict (finish sets out["err"]): drop them, so the runs
+        # kept by the lazy statistics below are freed by reference counting, not by a full GC
+        r["finish"] = r["steps"] = r["sync_rounds"] = None
     if evs is not None:
         LAST_WS_EVENTS.clear()
         LAST_WS_EVENTS.update(evs, chunk=chunk if not sync else None)
@@ -1750,9 +1753,13 @@ def finish_svc_batch(st: dict, defer=None):
         set_one(f, kws[f])
     hmark("svc_set_fitted")
     if later:
+        pending = list(later)
+
         def rest():
-            for f in later:
-                fit_one(f)
-            st["finish_rest"] = None
+            # (no reference to st: a closure stored in st that refers back to it made a reference
+            # cycle that kept the batch's device buffers — ≈ 77 MB per headline fit with the working-
+            # set runs below — alive until a full GC, profiles/r6_runs/r6p)
+            while pending:
+                fit_one(pending.pop(0))
         st["finish_rest"] = rest
     return svcs

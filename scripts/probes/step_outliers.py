@@ -28,7 +28,21 @@ Xd, yd, names = make_hf_cohort(10000, 40, seed=2020, nan_frac=0.02)
 Xs, ys, _ = make_hf_cohort(10000, 40, seed=2021, nan_frac=0.02)
 Xd, yd, Xs, ys = (torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys))
 gcn = [0]
-gc.callbacks.append(lambda phase, info: gcn.__setitem__(0, gcn[0] + (phase == "start")))
+gcinfo = {"gen": -1, "ms": 0.0, "t": 0.0}
+
+
+def _gc_cb(phase, info):
+    if phase == "start":
+        gcn[0] += 1
+        gcinfo["gen"] = max(gcinfo["gen"], info["generation"])
+        gcinfo["t"] = time.perf_counter()
+    else:
+        gcinfo["ms"] += 1e3 * (time.perf_counter() - gcinfo["t"])
+
+
+gc.callbacks.append(_gc_cb)
+if os.environ.get("GC_OFF", "0") == "1":
+    gc.disable()
 
 
 def fit():
@@ -46,7 +60,8 @@ for k in range(steps):
     for d in (smo.LAST_SMO_INFO, logreg_solver.LAST_PATH, hist_gbdt.LAST_PATH, stack_trainer.LAST_PRELAUNCH):
         for key in ("ws_resolve", "coop_fallback", "persist_fallback", "spec_miss"):
             d.pop(key, None)
-    g0, r0 = gcn[0], torch.cuda.memory_reserved(dev)
+    g0, r0, a0 = gcn[0], torch.cuda.memory_reserved(dev), torch.cuda.memory_allocated(dev)
+    gcinfo.update(gen=-1, ms=0.0)
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     if SYNC:
         torch.cuda.synchronize()
@@ -60,7 +75,9 @@ for k in range(steps):
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     recs.append(dict(step=k, ms=round(dt, 3), cpu_ms=round(1e3 * (time.process_time() - c0), 2),
                      nivcsw=ru1.ru_nivcsw - ru0.ru_nivcsw, nvcsw=ru1.ru_nvcsw - ru0.ru_nvcsw,
-                     gc=gcn[0] - g0, reserved_growth=torch.cuda.memory_reserved(dev) - r0,
+                     gc=gcn[0] - g0, gc_gen=gcinfo["gen"], gc_ms=round(gcinfo["ms"], 3),
+                     reserved_growth=torch.cuda.memory_reserved(dev) - r0,
+                     allocated_growth=torch.cuda.memory_allocated(dev) - a0,
                      spec_miss=stack_trainer.LAST_PRELAUNCH.get("spec_miss", 0),
                      ws_resolve=bool(smo.LAST_SMO_INFO.get("ws_resolve")),
                      coop_fallback=bool(smo.LAST_SMO_INFO.get("coop_fallback")) or bool(logreg_solver.LAST_PATH.get("coop_fallback")),
@@ -69,4 +86,6 @@ for k in range(steps):
 ms = sorted(r["ms"] for r in recs)
 med = ms[len(ms) // 2]
 print(json.dumps(dict(summary=True, steps=steps, min=ms[0], median=med, max=ms[-1], ratio=round(ms[-1] / med, 3),
+                      reserved_total_growth=sum(r["reserved_growth"] for r in recs),
+                      allocated_total_growth=sum(r["allocated_growth"] for r in recs),
                       over_1_25=[r for r in recs if r["ms"] > 1.25 * med])), flush=True)
