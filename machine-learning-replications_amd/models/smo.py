@@ -734,7 +734,7 @@ def _ws_groups(live, device) -> List[List[int]]:
 
 
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None,
-              seed=None, q=None, groups=None):
+              seed=None, q=None, groups=None, deps_out=None):
     """``seed``: a feasible α (per point, this batch's layout) to start from instead of α = 0
     (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`)."""
     P = len(live)
@@ -837,10 +837,18 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     if evs is not None:
         LAST_WS_EVENTS.clear()
         LAST_WS_EVENTS.update(evs, chunk=chunk if not sync else None)
+    # split join (deps_out given, no graphs): the caller's stream does NOT wait for every group —
+    # the consumers wait for the groups of the problems they read (deps_out["wait"]); everything
+    # that needs the whole batch (ρ / iterations of every problem, the error word) is assembled on
+    # the first group's stream after it has waited for the others (deps_out["join"]).  The stacking
+    # fit's Platt / out-of-fold / meta chain reads only the Platt-CV and fold problems, so it no
+    # longer waits for the refit's final problem — the longest one (profiles/r6_headline.md).
+    split = deps_out is not None and not use_graph and len(runs) > 1 and cuda
     for r in runs:
         if r["side"] is not None:
-            caller.wait_stream(r["side"])
-            for t in (alpha, G, zn, keys, r["rho"], r["iters"], r["idx_dev"]):
+            if not split:
+                caller.wait_stream(r["side"])
+            for t in (alpha, G, zn, keys, zcat, r["rho"], r["iters"], r["idx_dev"]) + ((seed,) if seed is not None else ()):
                 t.record_stream(r["side"])
     if use_graph:
         # the solution leaves the workspace: the next fit's rounds may overwrite it while this
@@ -848,6 +856,47 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         alpha = alpha.clone()
     if len(runs) == 1:
         rho, iters, err = runs[0]["rho"], runs[0]["iters"], runs[0]["err"]
+    elif split:
+        ev_of = []
+        for r in runs:
+            ev = torch.cuda.Event()
+            ev.record(r["side"] if r["side"] is not None else caller)
+            ev_of.append(ev)
+        J = runs[0]["side"] if runs[0]["side"] is not None else caller
+        for gi, ev in enumerate(ev_of):
+            if runs[gi]["side"] is not J:
+                J.wait_event(ev)
+        with torch.cuda.stream(J):
+            rho = torch.empty(P, dtype=torch.float64, device=device)
+            iters = torch.empty(P, dtype=torch.int32, device=device)
+            for r in runs:
+                rho.index_copy_(0, r["idx_dev"], r["rho"])
+                iters.index_copy_(0, r["idx_dev"], r["iters"])
+            err = torch.stack([r["err"] for r in runs]).amax().reshape(1)
+            join_ev = torch.cuda.Event()
+            join_ev.record(J)
+        for t in (rho, iters, err):
+            t.record_stream(caller)
+        run_of = np.empty(P, dtype=np.int64)
+        for gi, r in enumerate(runs):
+            run_of[r["idx"]] = gi
+
+        def wait(stream, problems):
+            """Make ``stream`` wait for the groups holding ``problems`` (indices into live)."""
+            for gi in sorted({int(run_of[k]) for k in problems}):
+                stream.wait_event(ev_of[gi])
+
+        def rho_for(stream, problems):
+            """ρ of every problem [P] on ``stream``, valid for the groups holding ``problems``."""
+            gis = sorted({int(run_of[k]) for k in problems})
+            with torch.cuda.stream(stream):
+                rr = torch.zeros(P, dtype=torch.float64, device=device)
+                for gi in gis:
+                    stream.wait_event(ev_of[gi])
+                    runs[gi]["rho"].record_stream(stream)
+                    rr.index_copy_(0, runs[gi]["idx_dev"], runs[gi]["rho"])
+            return rr
+        deps_out.update(wait=wait, rho_for=rho_for, join=J, join_ev=join_ev)
     else:
         rho = torch.empty(P, dtype=torch.float64, device=device)
         iters = torch.empty(P, dtype=torch.int32, device=device)
@@ -856,7 +905,9 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             iters.index_copy_(0, r["idx_dev"], r["iters"])
         err = None if sync else torch.stack([r["err"] for r in runs]).amax().reshape(1)
 
-    def stats():   # read back only when someone looks (tests, bench diagnostics): no sync here
+    def stats():   # read back only when someone looks (tests, bench diagnostics)
+        if cuda:
+            torch.cuda.synchronize(device)   # (the groups' streams need not be joined to the caller's)
         order = np.concatenate([r["idx"] for r in runs])
         inv = np.empty_like(order)
         inv[order] = np.arange(order.shape[0])
@@ -1194,6 +1245,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     max_l = max(p.l for p in live)
     solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
+    deps: dict = {}
     if group is None:
         kw = {}
         if solver == "ws" and CASCADE and (CASCADE_KC or not ws_kc(F, max_l)):
@@ -1201,6 +1253,8 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
             if seed is not None:
                 kw["seed"] = seed
                 hmark("svc_cascade_seeded")
+        if solver == "ws" and SPLIT_JOIN:
+            kw["deps_out"] = deps
         alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, **kw)
     else:
         def solve_local(sub):
@@ -1216,6 +1270,9 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
             return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s, **kw)
         alpha, rho, iters, err = _solve_distributed(solve_local, live, aoffs[-1], aoffs, device, group)
     out = {"smo_err": err}
+    J = deps.get("join")
+    if J is not None:
+        out["_deps"] = deps     # (consumers wait for the groups they read; finish joins them all)
     for k, p in enumerate(live):
         a0 = aoffs_start[k]
         out[id(p)] = (alpha[a0:a0 + p.l], rho[k], iters[k])
@@ -1226,15 +1283,17 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     if EARLY_READ and fin and len({f for f, _ in fin}) == len(fin):
         f64 = torch.float64
         ks = [k for _, k in fin]
-        kidx = _to_dev(np.array(ks, dtype=np.int64), device)
-        parts = ([(alpha[aoffs_start[k]:aoffs_start[k] + live[k].l] > 0).to(f64) for k in ks]
-                 + [rho.index_select(0, kidx).to(f64).reshape(-1), iters.index_select(0, kidx).to(f64).reshape(-1)]
-                 + ([err.to(f64).reshape(-1).abs().max().reshape(1)] if err is not None else []))
-        early_dev = torch.cat(parts)
-        early_host = torch.empty(early_dev.shape, dtype=f64, pin_memory=True)
-        early_host.copy_(early_dev, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        # (split join: on the joining stream, behind every group)
+        with (torch.cuda.stream(J) if J is not None else contextlib.nullcontext()):
+            kidx = _to_dev(np.array(ks, dtype=np.int64), device)
+            parts = ([(alpha[aoffs_start[k]:aoffs_start[k] + live[k].l] > 0).to(f64) for k in ks]
+                     + [rho.index_select(0, kidx).to(f64).reshape(-1), iters.index_select(0, kidx).to(f64).reshape(-1)]
+                     + ([err.to(f64).reshape(-1).abs().max().reshape(1)] if err is not None else []))
+            early_dev = torch.cat(parts)
+            early_host = torch.empty(early_dev.shape, dtype=f64, pin_memory=True)
+            early_host.copy_(early_dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         out["_early"] = dict(host=early_host, ev=ev, ids=[id(live[k]) for k in ks], has_err=err is not None,
                              keep=early_dev)
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
@@ -1246,10 +1305,18 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         a0, l = aoffs_start[k], p.l
         sign_h[a0:a0 + p.npos] = 1.0
         sign_h[a0 + p.npos:a0 + l] = -1.0
-    coef = (_to_dev(sign_h, device) * alpha.to(torch.float32)).contiguous()
-    out["_dec"] = dict(zcat=zcat, coef=coef, F=F, zoff={id(p): zoffs[k] for k, p in enumerate(live)})
-    # ---- Platt held-out decision values of every CV sub-model: one batched launch
+    sign_d = _to_dev(sign_h, device)
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
+    rho_pl = rho
+    if J is not None:
+        # the Platt decisions read only the Platt-CV problems: wait for their groups alone
+        cur = torch.cuda.current_stream(device)
+        deps["wait"](cur, [k for k, _ in platt])
+        rho_pl = deps["rho_for"](cur, [k for k, _ in platt])
+    coef = (sign_d * alpha.to(torch.float32)).contiguous()
+    out["_dec"] = dict(zcat=zcat, coef=coef, F=F, zoff={id(p): zoffs[k] for k, p in enumerate(live)},
+                       sign=sign_d, alpha=alpha, kof={id(p): k for k, p in enumerate(live)})
+    # ---- Platt held-out decision values of every CV sub-model: one batched launch
     if platt:
         hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
         per = 1024
@@ -1272,7 +1339,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         # the decision values are assembled inside the Platt kernel from these partials (row r of
         # part: problem rowk[r]'s held-out point, d = −(Σ part[r] − ρ))
         rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"].astype(np.int64))
-        out["platt_src"] = dict(part=part, S=S, rowk=_to_dev(rowk, device), rho=rho.to(torch.float64).contiguous(),
+        out["platt_src"] = dict(part=part, S=S, rowk=_to_dev(rowk, device), rho=rho_pl.to(torch.float64).contiguous(),
                                 keep=(hcat, ddev))
         for i, (k, p) in enumerate(platt):
             out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
@@ -1328,6 +1395,10 @@ EXACT_MAX_POINTS = int(os.environ.get("HFENS_SVM_EXACT_MAX", "150000"))
 # kernels), so finish_svc_batch's support extraction overlaps them (same-box A/B of the headline:
 # within its ±0.7 ms run-to-run spread, scripts/probes/gpu_r4an.sh, profiles/r4_runs/early_read_ab.log)
 EARLY_READ = os.environ.get("HFENS_SVC_EARLY_READ", "1") != "0"
+# split join of the working-set groups (_solve_ws deps_out): the Platt decisions and the stacking
+# fit's out-of-fold column wait only for the groups of the problems they read, not for the refit's
+# final problem (the longest, whose model is only needed at the end)
+SPLIT_JOIN = os.environ.get("HFENS_SVM_SPLIT_JOIN", "1") != "0"
 EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 
@@ -1621,13 +1692,25 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
     ddev = _dev_struct(dt, device)
     if st.get("gamma_dev") is not None:
         st["gamma_dev"].patch(ddev, _DEC_DT, "ngl2e", [f for f, _, _ in items])
-    E.svm_dec_batch(dec_state["zcat"].data_ptr(), dec_state["coef"].data_ptr(), hcat.data_ptr(), dec_state["F"],
+    deps = sol.get("_deps")
+    coef, rho_src = dec_state["coef"], None
+    if deps is not None:
+        # split join: wait for the groups of these final problems only, then y·α and ρ from them
+        cur = torch.cuda.current_stream(device)
+        ks = [dec_state["kof"][id(p)] for p in finals]
+        deps["wait"](cur, ks)
+        coef = (dec_state["sign"] * dec_state["alpha"].to(torch.float32)).contiguous()
+        rho_src = deps["rho_for"](cur, ks)
+    E.svm_dec_batch(dec_state["zcat"].data_ptr(), coef.data_ptr(), hcat.data_ptr(), dec_state["F"],
                     ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(), s)
     dec = part.to(torch.float64).sum(1).contiguous()
     model = torch.repeat_interleave(torch.arange(len(items), dtype=torch.int32),
                                     torch.as_tensor(hs, dtype=torch.int64))
     model = _to_dev(model.numpy(), device)
-    rho = torch.stack([st["sol"][id(p)][1].reshape(()).to(torch.float64) for p in finals]).contiguous()
+    if rho_src is not None:
+        rho = rho_src.index_select(0, _to_dev(np.asarray(ks, dtype=np.int64), device)).contiguous()
+    else:
+        rho = torch.stack([st["sol"][id(p)][1].reshape(()).to(torch.float64) for p in finals]).contiguous()
     sel = _to_dev(np.array([pl.index(f) for f, _, _ in items], dtype=np.int64), device)
     AB = st["ABt"].view(-1, 2).index_select(0, sel).reshape(-1).contiguous()
     rows = torch.cat([r.to(torch.int64) for _, _, r in items]).contiguous()
@@ -1636,7 +1719,7 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
               int(meta.shape[1]), int(col), hoff, s)
     from ..utils.timing import dmark
     dmark("svc_oof")
-    st["oof_keep"] = (hcat, part, ddev, dec, model, rho, sel, AB, rows)
+    st["oof_keep"] = (hcat, part, ddev, dec, model, rho, sel, AB, rows, coef)
     return True
 
 
@@ -1649,6 +1732,9 @@ def finish_svc_batch(st: dict, defer=None):
         return st["svcs"]
     svcs, Zs, meta, all_probs, sol, AB, device = (st["svcs"], st["Zs"], st["meta"], st["all_probs"],
                                                    st["sol"], st["AB"], st["device"])
+    if sol.get("_deps") is not None:
+        # (split join) everything from here on sees the whole batch: the refit's final problem too
+        torch.cuda.current_stream(device).wait_event(sol["_deps"]["join_ev"])
     early = sol.get("_early")
     finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
     if early is not None and early["ids"] != [id(p) for p in finals]:
