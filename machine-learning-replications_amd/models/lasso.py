@@ -118,11 +118,13 @@ class LassoCV(Estimator):
                                              float(self.tol))) for p in range(P)]
         return torch.stack(out).to(Gs.device)
 
-    def fit(self, X, y, group=None, overlap=None, early_overlap=None):
+    def fit(self, X, y, group=None, overlap=None, early_overlap=None, tail_out=None):
         """``overlap``: optional host callable run while the device solves the CV path (between its
         launch and the first read of its result) — host work hidden under the path's GPU time.
         ``early_overlap``: run right after the speculative refit is enqueued, before the alpha grid's
-        host read (only when the speculation runs early, :data:`EARLY_SPEC`)."""
+        host read (only when the speculation runs early, :data:`EARLY_SPEC`).  ``tail_out`` (a list,
+        early speculation only): the fit returns once the CV paths are enqueued and appends the
+        closure that completes it (waits for the paths, picks α, refits) — the caller runs it later."""
         from ..utils.guards import check_finite, finite_flag, raise_flags
         X = as_tensor(X)
         y = as_tensor(y, device=X.device)
@@ -247,6 +249,7 @@ class LassoCV(Estimator):
                 ev = torch.cuda.Event()
                 ev.record(side)
         dmark("lasso_cv_in")
+        join_ev = None
         if early:
             for t in (G, q, yy, cnt, grid):
                 t.record_stream(pst)
@@ -254,7 +257,7 @@ class LassoCV(Estimator):
                 hmark("lasso_launched")
                 overlap()
                 overlap = None
-            main.wait_event(path_ev)
+            join_ev = path_ev      # (joined in tail(): the MSE below waits for the paths)
         elif spec:
             # the CV paths on a stream of their own: work the overlap enqueues on the caller's stream
             # does not queue behind them (joined before the MSE below, after the overlap)
@@ -276,46 +279,58 @@ class LassoCV(Estimator):
         else:
             coefs = self._solve(G[:k], q[:k], yy[:k], cnt[:k], grid[None].expand(k, -1))   # [k, A, F]
             dmark("lasso_cv_path")
-        # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
-        inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
-        # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
-        # already globally reduced, so no per-row pass and no [k, A, n] intermediate.
-        Txx, Tx, Txy = Sxx[k] - Sxx[:k], sx[k] - sx[:k], Sxy[k] - Sxy[:k]
-        Ty, Tyy, nt = sy[k] - sy[:k], Syy[k] - Syy[:k], cnt[k] - cnt[:k]
-        c = inter
-        se = (torch.einsum("paf,pfg,pag->pa", coefs, Txx, coefs)
-              + 2 * c * torch.einsum("pf,paf->pa", Tx, coefs) - 2 * torch.einsum("pf,paf->pa", Txy, coefs)
-              + nt[:, None] * c * c - 2 * c * Ty[:, None] + Tyy[:, None])
-        mse = se / nt[:, None]                                                          # [k, A]
-        mean_mse = mse.mean(0)
-        best_dev = torch.argmin(mean_mse)
-        self.coef_dev_ = None
-        if refit_all is not None:
-            # the winner's coefficients stay on the device (no host read): a caller's overlap can
-            # queue work that depends on them (SelectFromModel's device column list → the stacking
-            # trainer's SVC batch) before this fit reads anything back
-            torch.cuda.current_stream(dev).wait_event(ev)
-            self.coef_dev_ = refit_all.index_select(0, best_dev.reshape(1))[0, 0]
-        if overlap is not None:
-            overlap()
-        best = int(best_dev)
-        self.alpha_ = float(grid[best])
-        self.alphas_ = grid
-        self.mse_path_ = mse.t()
-        if refit_all is not None:
-            w = refit_all[best, 0]
-        elif (early and best == SPEC_ALPHA_INDEX % A
-              and float(self.spec_alpha_dev_) == float(grid[best])):
-            # the speculation hit: its refit IS the refit at the chosen alpha (same kernel, same
-            # inputs, the same alpha bits)
-            w = self.coef_spec_dev_
-        else:
-            final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
-            w = final[0, 0]
-        self.coef_ = w
-        self.intercept_ = my[k] - mx[k] @ w
-        self.n_features_in_ = F
-        return self
+        def tail():
+            """The CV paths' winner, its refit and the fitted attributes (the host reads)."""
+            nonlocal overlap
+            if join_ev is not None:
+                main.wait_event(join_ev)
+            # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
+            inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
+            # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
+            # already globally reduced, so no per-row pass and no [k, A, n] intermediate.
+            Txx, Tx, Txy = Sxx[k] - Sxx[:k], sx[k] - sx[:k], Sxy[k] - Sxy[:k]
+            Ty, Tyy, nt = sy[k] - sy[:k], Syy[k] - Syy[:k], cnt[k] - cnt[:k]
+            c = inter
+            se = (torch.einsum("paf,pfg,pag->pa", coefs, Txx, coefs)
+                  + 2 * c * torch.einsum("pf,paf->pa", Tx, coefs) - 2 * torch.einsum("pf,paf->pa", Txy, coefs)
+                  + nt[:, None] * c * c - 2 * c * Ty[:, None] + Tyy[:, None])
+            mse = se / nt[:, None]                                                          # [k, A]
+            mean_mse = mse.mean(0)
+            best_dev = torch.argmin(mean_mse)
+            self.coef_dev_ = None
+            if refit_all is not None:
+                # the winner's coefficients stay on the device (no host read): a caller's overlap can
+                # queue work that depends on them (SelectFromModel's device column list → the stacking
+                # trainer's SVC batch) before this fit reads anything back
+                torch.cuda.current_stream(dev).wait_event(ev)
+                self.coef_dev_ = refit_all.index_select(0, best_dev.reshape(1))[0, 0]
+            if overlap is not None:
+                overlap()
+            best = int(best_dev)
+            self.alpha_ = float(grid[best])
+            self.alphas_ = grid
+            self.mse_path_ = mse.t()
+            if refit_all is not None:
+                w = refit_all[best, 0]
+            elif (early and best == SPEC_ALPHA_INDEX % A
+                  and float(self.spec_alpha_dev_) == float(grid[best])):
+                # the speculation hit: its refit IS the refit at the chosen alpha (same kernel, same
+                # inputs, the same alpha bits)
+                w = self.coef_spec_dev_
+            else:
+                final = self._solve(G[k:], q[k:], yy[k:], cnt[k:], grid[best:best + 1][None])
+                w = final[0, 0]
+            self.coef_ = w
+            self.intercept_ = my[k] - mx[k] @ w
+            self.n_features_in_ = F
+            return self
+
+        if tail_out is not None and early:
+            # the caller completes the fit later (pipeline.develop: after finishing the stacking fit
+            # enqueued on the speculative selection, so the host waits for both at once)
+            tail_out.append(tail)
+            return self
+        return tail()
 
 
 class SelectFromModel(Estimator):
@@ -339,12 +354,14 @@ class SelectFromModel(Estimator):
         key = torch.where(rank < k, idx, idx + F)
         return torch.sort(key, stable=True).values[:k]
 
-    def fit(self, X, y, group=None, overlap=None, early_overlap=None):
+    def fit(self, X, y, group=None, overlap=None, early_overlap=None, tail_out=None):
         """``overlap`` / ``early_overlap``: host callables run under the LassoCV path (see
         :meth:`LassoCV.fit`).  With threshold=-inf and max_features, ``cols_dev_`` (the selected
         columns on the device, from the speculative refit when there is one) is set before either
         runs; ``early_overlap`` runs as soon as the speculative selection is enqueued (before the
-        LassoCV's host read) or, without an early speculation, right before ``overlap``."""
+        LassoCV's host read) or, without an early speculation, right before ``overlap``.
+        ``tail_out``: see :meth:`LassoCV.fit` — the selection is then completed by the appended
+        closure."""
         self.cols_dev_ = None
         self.cols_host_ = None
         if (overlap is not None or early_overlap is not None) and isinstance(self.estimator, LassoCV):
@@ -385,12 +402,23 @@ class SelectFromModel(Estimator):
                 early()
                 if user_late is not None:
                     user_late()
-            self.estimator_ = self.estimator.fit(X, y, group=group, overlap=late, early_overlap=early)
+            inner = [] if tail_out is not None else None
+            self.estimator_ = self.estimator.fit(X, y, group=group, overlap=late, early_overlap=early,
+                                                 tail_out=inner)
+            if inner:
+                def tail():
+                    inner[0]()
+                    self._select()
+                tail_out.append(tail)
+                return self
         else:
             self.estimator_ = self.estimator.fit(X, y, group=group)
             for f in (early_overlap, overlap):
                 if f is not None:
                     f()
+        return self._select()
+
+    def _select(self):
         scores = self.estimator_.coef_.abs().cpu().numpy()
         F = scores.size
         mask = np.ones(F, dtype=bool)

@@ -1398,7 +1398,9 @@ EARLY_READ = os.environ.get("HFENS_SVC_EARLY_READ", "1") != "0"
 # split join of the working-set groups (_solve_ws deps_out): the Platt decisions and the stacking
 # fit's out-of-fold column wait only for the groups of the problems they read, not for the refit's
 # final problem (the longest, whose model is only needed at the end)
-SPLIT_JOIN = os.environ.get("HFENS_SVM_SPLIT_JOIN", "1") != "0"
+# (measured, profiles/r6_runs/r6r: no gain on the headline — the Platt-CV groups end within
+# ≈ 0.1 ms of the refit's 10k problem — so it is off by default: 18.07 / 17.79 vs 17.92 / 18.11 ms)
+SPLIT_JOIN = os.environ.get("HFENS_SVM_SPLIT_JOIN", "0") == "1"
 EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 

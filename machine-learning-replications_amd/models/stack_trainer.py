@@ -687,6 +687,16 @@ def _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof):
     return dict(fit=fit, deferred=deferred, post=post, keep=keep, prebin=prebin)
 
 
+def finish_prelaunched(pre: dict, timer: StageTimer = None) -> None:
+    """Finish a :func:`prelaunch_stack` state before its selection is confirmed (pipeline.develop,
+    while the LassoCV paths still run); :func:`fit_stacking` then only checks the selection — and
+    refits from scratch on a miss."""
+    stc = pre["state"]
+    stc["timer"] = timer or stc["timer"]
+    finish_stacking(stc)
+    pre["finished"] = True
+
+
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
                  plan=None):
     pre = plan.get("prelaunch") if (plan is not None and group is None) else None
@@ -711,6 +721,8 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
                 warnings.warn("device column selection differs from the host's; relaunching the stacking fit")
             pre = None
     LAST_PRELAUNCH["used"] = pre is not None
+    if pre is not None and pre.get("finished"):
+        return clf          # (finish_prelaunched already completed it)
     if pre is not None:
         stc = pre["state"]
         stc["timer"] = timer or stc["timer"]

@@ -49,6 +49,9 @@ INIT_STREAMS = os.environ.get("HFENS_INIT_STREAMS", "1") != "0"   # runtime.init
 # the CV paths launched first, the paths, the SMO and the GBC stage loop ran side by side and the SMO
 # took 15.5 instead of 11 ms (24.9 / 26.9 vs 19.0 / 18.6 ms / fit)
 BASES_AFTER_CV = os.environ.get("HFENS_BASES_AFTER_CV", "0") == "1"
+# the prelaunched stack finished (its host reads) before the LassoCV's own tail (its host reads of the
+# CV paths' winner), not after it
+FINISH_BEFORE_LASSO = os.environ.get("HFENS_FINISH_BEFORE_LASSO", "1") != "0"
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
@@ -276,7 +279,21 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
                 for j in js:
                     j()
             return f
-        sfm = sel.fit(X_dev, y_dev, group=fit_group, overlap=run_all(jobs), early_overlap=run_all(early_jobs))
+        tails = [] if (local and dev.type == "cuda" and planned and FINISH_BEFORE_LASSO) else None
+        sfm = sel.fit(X_dev, y_dev, group=fit_group, overlap=run_all(jobs), early_overlap=run_all(early_jobs),
+                      tail_out=tails)
+        if tails:
+            # the LassoCV fit returned with its CV paths still running: finish the stacking fit
+            # enqueued on the speculative selection first (its host reads wait for the SMO), then
+            # the LassoCV (its reads wait for the paths) — the host waits for both at once instead
+            # of one after the other; fit_stacking checks the selection and redoes the stack on a miss
+            pre = plan_box.get("prelaunch")
+            if pre is not None:
+                from .models.stack_trainer import finish_prelaunched
+                finish_prelaunched(pre, timer)
+                hmark("stack_spec_finished")
+            for t in tails:
+                t()
         if run_sel is not None:
             X_sel = run_sel()[1]      # (already run inside the LassoCV path; a no-op then)
         hmark("lasso_fit")
