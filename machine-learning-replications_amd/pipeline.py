@@ -50,8 +50,10 @@ INIT_STREAMS = os.environ.get("HFENS_INIT_STREAMS", "1") != "0"   # runtime.init
 # took 15.5 instead of 11 ms (24.9 / 26.9 vs 19.0 / 18.6 ms / fit)
 BASES_AFTER_CV = os.environ.get("HFENS_BASES_AFTER_CV", "0") == "1"
 # the prelaunched stack finished (its host reads) before the LassoCV's own tail (its host reads of the
-# CV paths' winner), not after it
-FINISH_BEFORE_LASSO = os.environ.get("HFENS_FINISH_BEFORE_LASSO", "1") != "0"
+# CV paths' winner) instead of after it.  Measured slower (profiles/r6_runs/r6s: 18.9 / 18.7 vs
+# 18.3 / 17.9 ms): the paths end ≈ 3 ms before the SMO, and their short tail then waited behind the
+# stack's reads; off by default
+FINISH_BEFORE_LASSO = os.environ.get("HFENS_FINISH_BEFORE_LASSO", "0") == "1"
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
