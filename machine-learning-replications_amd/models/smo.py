@@ -148,6 +148,11 @@ def _expand_native(fit_id, y_np: np.ndarray, gamma: float, cw: np.ndarray, svc):
     out = np.empty((7 if svc.probability else 1) * l, dtype=np.int64)
     meta = np.empty(21, dtype=np.int64)
     ops.ext().svc_expand_host(y.ctypes.data, l, seed, out.ctypes.data, meta.ctypes.data)
+    return _wrap_expansion(fit_id, l, out, meta, gamma, cw, svc)
+
+
+def _wrap_expansion(fit_id, l: int, out: np.ndarray, meta: np.ndarray, gamma, cw, svc):
+    """The problem list of one fit from the native expansion's arrays (svc_expand_host layout)."""
     grouped = out[:l]
     n0 = int(meta[0])
     C0, C1 = float(svc.C * cw[0]), float(svc.C * cw[1])

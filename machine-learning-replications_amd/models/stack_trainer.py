@@ -204,6 +204,58 @@ def plan_stacking(clf, y_np: np.ndarray) -> dict:
     return dict(y_np=y_np, folds_np=folds_np, rows_host=rows_host, svc_pre=svc_pre)
 
 
+NATIVE_PLAN = os.environ.get("HFENS_NATIVE_PLAN", "1") != "0"
+
+
+def plan_stacking_start(clf, y_np: np.ndarray):
+    """Start :func:`plan_stacking`'s label work on a helper thread in ONE native call with the GIL
+    released (ops/csrc/host.hip stack_plan_host: folds + every fit's libsvm expansion), so it runs
+    while the calling thread launches the imputation and the LassoCV prelude.  Returns ``join()`` →
+    the plan (equal to plan_stacking's, array for array: tests/test_smo_host.py), or None when not
+    eligible (no extension, labels not 0/1 of both classes, not one probability SVC pipeline)."""
+    from .. import ops
+    from . import smo
+    y_np = np.ascontiguousarray(np.asarray(y_np, dtype=np.float64).reshape(-1))
+    n = int(y_np.shape[0])
+    svc_cols = [i for i, (_, e) in enumerate(clf.estimators) if _kind(e) == "svc"]
+    if not (NATIVE_PLAN and ops.has_ext() and len(svc_cols) == 1 and n >= N_FOLDS):
+        return None
+    svc = clf.estimators[svc_cols[0]][1].steps[-1][1]
+    if not svc.probability or not ((y_np == 0.0) | (y_np == 1.0)).all():
+        return None
+    c1 = int(np.count_nonzero(y_np))
+    if min(c1, n - c1) < N_FOLDS:
+        return None
+    if smo.SOLVER == "exact" or (smo.SOLVER == "auto" and n < smo.WS_MIN_POINTS):
+        return None      # (the stored-Gram solver's Platt column maps: plan_stacking)
+    seed = smo.sklearn_libsvm_seed(svc.random_state) & 0xFFFFFFFF
+    nf1 = N_FOLDS + 1
+    folds = np.empty(n, dtype=np.int64)
+    rows = np.empty(nf1 * n, dtype=np.int64)
+    lens = np.empty(nf1, dtype=np.int64)
+    out = np.empty(nf1 * 7 * n, dtype=np.int64)
+    meta = np.empty(nf1 * 21, dtype=np.int64)
+    import threading
+    E = ops.ext()
+    th = threading.Thread(target=E.stack_plan_host, name="hfens-plan-native", daemon=True,
+                          args=(y_np.ctypes.data, n, N_FOLDS, seed, folds.ctypes.data, rows.ctypes.data,
+                                lens.ctypes.data, out.ctypes.data, meta.ctypes.data))
+    th.start()
+
+    def join():
+        th.join()
+        rows_host = [rows[f * n:f * n + int(lens[f])] for f in range(nf1)]
+        pre = []
+        for f in range(nf1):
+            l = int(lens[f])
+            yf = y_np[rows_host[f]]
+            probs, mt = smo._wrap_expansion(f, l, out[f * 7 * n:(f + 1) * 7 * n], meta[f * 21:(f + 1) * 21], None,
+                                            smo._class_weights_host(svc, yf), svc)
+            pre.append((yf, probs, mt))
+        return dict(y_np=y_np, folds_np=folds, rows_host=rows_host, svc_pre={svc_cols[0]: pre})
+    return join
+
+
 def _launch_svc(stc) -> bool:
     """SVC batch on a side stream ∥ the other base models on a second stream (:func:`_launch_bases`),
     from one host thread: everything ENQUEUED, nothing read back (:func:`_finish_concurrent`

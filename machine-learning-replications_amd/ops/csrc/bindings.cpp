@@ -16,6 +16,9 @@ long long stack_infer_lds(int F, int mp, int nodes_total);
 // liblinear_host.hip
 int liblinear_l1r_lr(uintptr_t X, uintptr_t y, uintptr_t sw, int l, int n, double bias, double C0, double C1,
                      double eps, int max_newton_iter, long long seed, uintptr_t w);
+// host.hip
+void stack_plan_host(uintptr_t y_ptr, long long n, int n_folds, long long seed, uintptr_t folds_ptr,
+                     uintptr_t rows_ptr, uintptr_t lens_ptr, uintptr_t out_ptr, uintptr_t meta_ptr);
 #define HFENS_DECLS
 #include "decls.inc"
 #undef HFENS_DECLS
@@ -31,6 +34,8 @@ PYBIND11_MODULE(_hfens_hip, m) {
   m.def("stack_infer_lds", &hfens::stack_infer_lds);
   // (host-only and sequential: release the GIL so the stacking fit's six solves run in parallel threads)
   m.def("liblinear_l1r_lr", &hfens::liblinear_l1r_lr, py::call_guard<py::gil_scoped_release>());
+  // (the label-only stacking plan on a helper thread while the main thread launches device work)
+  m.def("stack_plan_host", &hfens::stack_plan_host, py::call_guard<py::gil_scoped_release>());
 #define HFENS_DEFS
 #include "decls.inc"
 #undef HFENS_DEFS

@@ -303,4 +303,55 @@ void svc_expand_host(uintptr_t y_ptr, long long n, long long seed, uintptr_t out
   }
 }
 
+// stack_plan_host: the label-only stacking plan of pipeline.develop in ONE native call, so it can run
+// on a helper thread with the GIL released while the main thread launches the imputation and the
+// LassoCV prelude: StratifiedKFold(n_folds) test folds of two-class labels (sklearn's assignment:
+// the class seen first is class 0, each class's members dealt to folds in row order by the counts of
+// the sorted encoded labels), then every fit's (the n_folds fold fits and the refit) libsvm problem
+// expansion (svc_expand_host).
+//   y[n] ∈ {0, 1} (checked by the caller) → folds[n]; per fit f: out[f·7n …] and meta[f·21 …] as
+//   svc_expand_host writes them for that fit's labels (fit f < n_folds: rows with fold ≠ f; the
+//   refit: all rows, in row order).  rows_out[(n_folds + 1)·n]: every fit's row list; lens[n_folds+1].
+void stack_plan_host(uintptr_t y_ptr, long long n, int n_folds, long long seed, uintptr_t folds_ptr,
+                     uintptr_t rows_ptr, uintptr_t lens_ptr, uintptr_t out_ptr, uintptr_t meta_ptr) {
+  const double* y = reinterpret_cast<const double*>(y_ptr);
+  int64_t* folds = reinterpret_cast<int64_t*>(folds_ptr);
+  int64_t* rows = reinterpret_cast<int64_t*>(rows_ptr);
+  int64_t* lens = reinterpret_cast<int64_t*>(lens_ptr);
+  const double first = y[0];
+  int64_t c0 = 0;
+  for (long long i = 0; i < n; ++i) c0 += (y[i] == first);
+  const int64_t k = n_folds;
+  std::vector<int64_t> next0(k), next1(k);
+  // fold i takes the positions ≡ i (mod k) of the sorted encoded labels: class 0 holds [0, c0)
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t tot = (n - i + k - 1) / k;
+    const int64_t a0 = c0 > i ? (c0 - i + k - 1) / k : 0;
+    next0[i] = a0;
+    next1[i] = tot - a0;
+  }
+  int64_t f0 = 0, f1 = 0;
+  for (long long i = 0; i < n; ++i) {
+    if (y[i] == first) {
+      while (f0 < k && next0[f0] == 0) ++f0;
+      folds[i] = f0;
+      --next0[f0];
+    } else {
+      while (f1 < k && next1[f1] == 0) ++f1;
+      folds[i] = f1;
+      --next1[f1];
+    }
+  }
+  std::vector<double> yf(n);
+  for (int64_t f = 0; f <= k; ++f) {
+    int64_t* r = rows + f * n;
+    int64_t m = 0;
+    for (long long i = 0; i < n; ++i)
+      if (f == k || folds[i] != f) { r[m] = i; yf[m] = y[i]; ++m; }
+    lens[f] = m;
+    svc_expand_host(reinterpret_cast<uintptr_t>(yf.data()), m, seed,
+                    out_ptr + sizeof(int64_t) * (size_t)(f * 7 * n), meta_ptr + sizeof(int64_t) * (size_t)(f * 21));
+  }
+}
+
 }  // namespace hfens

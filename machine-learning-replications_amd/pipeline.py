@@ -147,10 +147,20 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         y_ev.record()
 
         box = {}
+        native = None
+        if not PLAN_THREAD:
+            # the label work natively on a helper thread (GIL released) while this thread launches
+            # the imputation and the LassoCV prelude; the labels' copy is done at once (idle device)
+            from .models.stack_trainer import plan_stacking_start
+            y_ev.synchronize()
+            native = plan_stacking_start(clf, y_pin.numpy().copy())
 
         def work():
             try:
                 from .models.stack_trainer import plan_stacking
+                if native is not None:
+                    box["plan"] = native()
+                    return
                 y_ev.synchronize()
                 box["plan"] = plan_stacking(clf, y_pin.numpy().copy())
             except BaseException as e:   # re-raised by run() on the calling thread

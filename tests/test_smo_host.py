@@ -65,3 +65,40 @@ def test_stratified_binary_fast_path_matches_generic(n, p1, seed):
             continue
         assert np.array_equal(ms._stratified_binary(y, 5), ms._stratified_generic(y, 5))
     assert ms._stratified_binary(np.array([0.0, 1.0, 2.0, 1.0, 0.0, 2.0]), 2) is None
+
+
+@pytest.mark.parametrize("n,p1,seed", [(10000, 0.2, 2020), (5003, 0.198, 7), (4300, 0.3, 3), (713, 0.2, 4)])
+def test_native_stacking_plan_matches_python(n, p1, seed):
+    """stack_trainer.plan_stacking_start (ONE GIL-free native call on a helper thread: StratifiedKFold
+    test folds of two-class labels + every fit's libsvm expansion) gives plan_stacking's plan array for
+    array, whichever class is seen first (below the working-set solver's size the stored-Gram solver's
+    column maps keep the Python plan: None)."""
+    from hfens import ops
+    from hfens.config import EnsembleConfig, build_estimators
+    from hfens.models import stack_trainer
+    if not ops.has_ext():
+        pytest.skip("extension not built")
+    clf = build_estimators(EnsembleConfig())
+    rng = np.random.default_rng(seed)
+    for first in (0.0, 1.0):
+        y = (rng.random(n) < p1).astype(np.float64)
+        y[0] = first
+        join = stack_trainer.plan_stacking_start(clf, y)
+        from hfens.models import smo
+        if n < smo.WS_MIN_POINTS:
+            assert join is None
+            continue
+        assert join is not None
+        a, b = join(), stack_trainer.plan_stacking(clf, y)
+        assert np.array_equal(a["folds_np"], b["folds_np"])
+        assert all(np.array_equal(u, v) for u, v in zip(a["rows_host"], b["rows_host"]))
+        assert a["svc_pre"].keys() == b["svc_pre"].keys()
+        for k in a["svc_pre"]:
+            for (ya, pa, ma), (yb, pb, mb) in zip(a["svc_pre"][k], b["svc_pre"][k]):
+                assert np.array_equal(ya, yb) and ma["n0"] == mb["n0"] and np.array_equal(ma["grouped"], mb["grouped"])
+                assert (ma["C0"], ma["C1"]) == (mb["C0"], mb["C1"])
+                for p, q in zip(pa, pb):
+                    assert (p.fit, p.fold, p.npos, p.Cp, p.Cn, p.const) == (q.fit, q.fold, q.npos, q.Cp, q.Cn, q.const)
+                    for f in ("rows", "held", "held_rows"):
+                        u, v = getattr(p, f), getattr(q, f)
+                        assert (u is None) == (v is None) and (u is None or np.array_equal(u, v))
