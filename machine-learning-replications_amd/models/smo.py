@@ -1235,7 +1235,7 @@ def _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap=None):
     return seed
 
 
-def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None):
+def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None, oof_items=None):
     from .. import ops
     E = ops.ext()
     s = ops.stream_ptr(device)
@@ -1324,29 +1324,47 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     coef = (sign_d * alpha.to(torch.float32)).contiguous()
     out["_dec"] = dict(zcat=zcat, coef=coef, F=F, zoff={id(p): zoffs[k] for k, p in enumerate(live)},
                        sign=sign_d, alpha=alpha, kof={id(p): k for k, p in enumerate(live)})
-    # ---- Platt held-out decision values of every CV sub-model: one batched launch
+    # ---- Platt held-out decision values of every CV sub-model: one batched launch — with the
+    # stacking fit's out-of-fold rows (``oof_items``: [(fit f, fold-f-scaled rows)], decided by fit f's
+    # final problem) in the SAME launch, so enqueue_svc_oof needs no decision launch of its own
     if platt:
+        oof = []
+        if oof_items and J is None:
+            finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
+            oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
+            if len(oof) != len(oof_items):
+                oof = []
         hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
+        if oof:
+            hcat = torch.cat([hcat] + [Zt.to(torch.float32) for _, Zt in oof]).contiguous()
         per = 1024
         S = (max_l + per - 1) // per
-        dt = np.zeros(len(platt), _DEC_DT)
+        dt = np.zeros(len(platt) + len(oof), _DEC_DT)
         hoff = 0
         for i, (k, p) in enumerate(platt):
             h = int(p.held_rows.shape[0])
             dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
             hoff += h
+        hoff_platt = hoff
+        for i, (k, Zt) in enumerate(oof):
+            h = int(Zt.shape[0])
+            dt[len(platt) + i] = (zoffs[k], hoff, live[k].l, h, -live[k].gamma * 1.4426950408889634, per)
+            hoff += h
         part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
         ddev = _dev_struct(dt, device)
         if _GAMMA_CTX[0] is not None:
-            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt])
+            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt] + [live[k].fit for k, _ in oof])
         max_h = int(dt["h"].max())
         dmark("svc_smo_done")
-        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(platt),
+        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(dt),
                         max_h, S, part.data_ptr(), s)
+        if oof:
+            out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in oof_items], part=part, hoff0=hoff_platt,
+                                  hoff=hoff - hoff_platt)
         dmark("svc_platt_dec")
         # the decision values are assembled inside the Platt kernel from these partials (row r of
         # part: problem rowk[r]'s held-out point, d = −(Σ part[r] − ρ))
-        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"].astype(np.int64))
+        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"][:len(platt)].astype(np.int64))
         out["platt_src"] = dict(part=part, S=S, rowk=_to_dev(rowk, device), rho=rho_pl.to(torch.float64).contiguous(),
                                 keep=(hcat, ddev))
         for i, (k, p) in enumerate(platt):
@@ -1479,7 +1497,7 @@ _GAMMA_CTX: list = [None]
 
 
 def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_iter_cap=None, group=None,
-                     y_host=None, plan=None, gamma_dev: bool = False) -> dict:
+                     y_host=None, plan=None, gamma_dev: bool = False, oof_items=None) -> dict:
     """Everything up to the Platt sigmoid fits, enqueued on the current stream with no host
     synchronisation after the SMO launch (so the caller can overlap other work); complete
     with :func:`finish_svc_batch`.  ``group``: every rank holds the same (full) ``Zs``; the SMO
@@ -1593,7 +1611,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     args = (svcs, Zs, ys, max_iter_cap, group)
     _GAMMA_CTX[0] = gdev
     try:
-        sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group) if cuda
+        sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group, oof_items=oof_items) if cuda
                else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
     finally:
         _GAMMA_CTX[0] = None
@@ -1697,6 +1715,11 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
         dt[i] = (dec_state["zoff"][id(p)], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
         hoff += h
         hs.append(h)
+    pre = sol.get("oof_pre")
+    if pre is not None and pre["ids"] == [(f, id(Zt)) for f, Zt, _ in items] and pre["hoff"] == hoff:
+        # the decisions came with the Platt launch (launch_svc_batch oof_items): only the sigmoid
+        dec = pre["part"][pre["hoff0"]:pre["hoff0"] + hoff].to(torch.float64).sum(1).contiguous()
+        return _svc_oof_tail(st, items, finals, dec, hs, meta, col, device, None, (pre,))
     hcat = torch.cat([Zt.to(torch.float32) for _, Zt, _ in items]).contiguous()
     part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
     ddev = _dev_struct(dt, device)
@@ -1714,12 +1737,23 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
     E.svm_dec_batch(dec_state["zcat"].data_ptr(), coef.data_ptr(), hcat.data_ptr(), dec_state["F"],
                     ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(), s)
     dec = part.to(torch.float64).sum(1).contiguous()
+    return _svc_oof_tail(st, items, finals, dec, hs, meta, col, device,
+                         rho_src.index_select(0, _to_dev(np.asarray(ks, dtype=np.int64), device)).contiguous()
+                         if rho_src is not None else None, (hcat, part, ddev, coef))
+
+
+def _svc_oof_tail(st, items, finals, dec, hs, meta, col, device, rho, keep) -> bool:
+    """The out-of-fold probabilities from the decision values ``dec`` (rows of ``items`` in order):
+    Platt sigmoid + coupling with each final model's ρ and (A, B), scattered into ``meta[:, col]``."""
+    from .. import ops
+    E = ops.ext()
+    s = ops.stream_ptr(device)
+    pl = st["pl"]
+    hoff = int(dec.shape[0])
     model = torch.repeat_interleave(torch.arange(len(items), dtype=torch.int32),
                                     torch.as_tensor(hs, dtype=torch.int64))
     model = _to_dev(model.numpy(), device)
-    if rho_src is not None:
-        rho = rho_src.index_select(0, _to_dev(np.asarray(ks, dtype=np.int64), device)).contiguous()
-    else:
+    if rho is None:
         rho = torch.stack([st["sol"][id(p)][1].reshape(()).to(torch.float64) for p in finals]).contiguous()
     sel = _to_dev(np.array([pl.index(f) for f, _, _ in items], dtype=np.int64), device)
     AB = st["ABt"].view(-1, 2).index_select(0, sel).reshape(-1).contiguous()
@@ -1729,7 +1763,7 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
               int(meta.shape[1]), int(col), hoff, s)
     from ..utils.timing import dmark
     dmark("svc_oof")
-    st["oof_keep"] = (hcat, part, ddev, dec, model, rho, sel, AB, rows, coef)
+    st["oof_keep"] = keep + (dec, model, rho, sel, AB, rows)
     return True
 
 

@@ -293,13 +293,17 @@ def _launch_svc(stc) -> bool:
             hmark("svc_inputs")
             if group is None:
                 yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
+                # the out-of-fold rows, scaled by their fold's scaler, go into the SVC batch's Platt
+                # decision launch (one launch for both)
+                items = stc["oof_items"](clones) if stc["oof_svc_dev"] is not None else None
                 # device γ (no host read before the SMO) whenever the batch is eligible
                 st = launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh, plan=(svc_pre or {}).get(i),
-                                      gamma_dev=GAMMA_DEV)
+                                      gamma_dev=GAMMA_DEV,
+                                      oof_items=[(k, Zt) for k, Zt, _ in items] if (items and MERGED_OOF_DEC) else None)
                 if stc["oof_svc_dev"] is not None:
                     # the OOF column straight from the device solution, behind the SMO on this
                     # stream: no wait for the fitted models' host bookkeeping
-                    st["oof_dev"] = stc["oof_svc_dev"](i, clones, st)
+                    st["oof_dev"] = stc["oof_svc_dev"](i, clones, st, items)
                 pending[i] = (clones, st)
             else:
                 pending[i] = (clones, launch_svc_batch_distributed(svcs, Zs, ys, group))
@@ -435,6 +439,9 @@ GAMMA_DEV = os.environ.get("HFENS_SVC_GAMMA_DEV", "1") != "0"
 # (profiles/r6_runs/r6h: gbc_binned 16.7 ms)
 BASES_SETUP = os.environ.get("HFENS_BASES_SETUP", "after")
 LR_FIRST = os.environ.get("HFENS_LR_FIRST", "1") != "0"
+# the SVC's out-of-fold decisions computed in the batch's Platt decision launch (one launch, the same
+# partials bit for bit: extra all-zero split columns add exact zeros)
+MERGED_OOF_DEC = os.environ.get("HFENS_MERGED_OOF_DEC", "1") != "0"
 LAST_PRELAUNCH = {"used": False}
 
 
@@ -532,16 +539,21 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
-    def oof_svc_dev(col, fitted, st):
+    def oof_items(fitted):
         if not (DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])):
+            return None
+        return [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
+                for k in range(N_FOLDS) if test_idx[k].numel()]
+
+    def oof_svc_dev(col, fitted, st, items=None):
+        items = items if items is not None else oof_items(fitted)
+        if items is None:
             return False
         from .smo import enqueue_svc_oof
-        items = [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
-                 for k in range(N_FOLDS) if test_idx[k].numel()]
         return enqueue_svc_oof(st, items, meta, col)
 
     y64 = y.to(torch.float64)
-    stc.update(oof=oof, oof_svc_dev=oof_svc_dev if group is None else None, y64=y64)
+    stc.update(oof=oof, oof_svc_dev=oof_svc_dev if group is None else None, oof_items=oof_items, y64=y64)
     _hmk("stack_prep")
 
     def new_final():

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r6y
 mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests/test_svm_ws_gpu.py tests/test_train_gpu.py tests/test_bench_parity_gpu.py tests/test_svc_scale_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "prelaunch or speculat or device_bases or task_policy or bench_shape or plan_ahead" > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -60 $O/pytest.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_svm_ws_gpu.py tests/test_train_gpu.py tests/test_bench_parity_gpu.py tests/test_svc_scale_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "prelaunch or speculat or device_bases or device_svc_oof or merged_oof or task_policy or bench_shape or plan_ahead" > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -60 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for t in a b; do HFENS_NATIVE_PLAN=1 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/b_$t.json 2> $O/b_$t.err || { echo "bench failed"; tail -20 $O/b_$t.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/b_$t.json').read().strip().splitlines()[-1]);print('bench', d['ms_per_step'], d['diag']['step_ms_min_med_max'], d['auroc'], d['diag']['svm'])"; done
@@ -12,3 +12,5 @@ grep "^\[dev\]" $O/tl.err | tail -2 | head -1 | cut -c1-900
 for t in c d; do HFENS_NATIVE_PLAN=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/b_$t.json 2> $O/b_$t.err || { echo "bench failed"; tail -20 $O/b_$t.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/b_$t.json').read().strip().splitlines()[-1]);print('bench noplan', d['ms_per_step'], d['diag']['step_ms_min_med_max'])"; done
 grep "^\[host\]" $O/tl.err | tail -2 | head -1 | tr ' ' '\n' | grep -v ws_chunk | tr '\n' ' ' | cut -c1-900; echo
+for t in e f; do HFENS_MERGED_OOF_DEC=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/b_$t.json 2> $O/b_$t.err || { echo "bench failed"; tail -20 $O/b_$t.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/b_$t.json').read().strip().splitlines()[-1]);print('bench nomerge', d['ms_per_step'], d['diag']['step_ms_min_med_max'])"; done

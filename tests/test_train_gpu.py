@@ -1110,3 +1110,21 @@ def test_headline_fit_leaves_no_device_memory_in_reference_cycles(dev):
             gc.enable()
     assert not leaked, f"{len(leaked)} CUDA tensors in reference cycles"
     assert a1 - a0 <= (1 << 20), a1 - a0
+
+
+def test_merged_oof_decisions_bit_identical(dev, monkeypatch):
+    """stack_trainer.MERGED_OOF_DEC: the SVC's out-of-fold decisions computed inside the batch's
+    Platt decision launch give the separate launch's out-of-fold column bit for bit (same partials;
+    the longer launch only adds all-zero split columns)."""
+    from hfens import pipeline
+    from hfens.io.synth import make_hf_cohort
+    from hfens.models import smo, stack_trainer
+    Xd, yd, names = make_hf_cohort(6000, 40, seed=95, nan_frac=0.02)
+    Xs, ys, _ = make_hf_cohort(2000, 40, seed=96, nan_frac=0.02)
+    args = [torch.as_tensor(a, device=dev) for a in (Xd, yd, Xs, ys)]
+    out = {}
+    for merged in (False, True):
+        monkeypatch.setattr(stack_trainer, "MERGED_OOF_DEC", merged)
+        out[merged] = pipeline.develop(args[0], args[1], args[2], args[3], names, device=dev)
+    assert torch.equal(out[False].model.oof_meta_, out[True].model.oof_meta_)
+    assert torch.equal(out[False].proba_sel, out[True].proba_sel)
