@@ -284,6 +284,7 @@ class LassoCV(Estimator):
             nonlocal overlap
             if join_ev is not None:
                 main.wait_event(join_ev)
+            hmark("lasso_tail")
             # test MSE per fold and alpha: residual = X_test·w + (ȳ_tr − x̄_tr·w) − y_test
             inter = my[:k, None] - torch.einsum("pf,paf->pa", mx[:k], coefs)               # [k, A]
             # Σ_test (x·w + c − y)² from the test-fold moments (all rows minus fold-train rows);
@@ -307,6 +308,7 @@ class LassoCV(Estimator):
             if overlap is not None:
                 overlap()
             best = int(best_dev)
+            hmark("lasso_best_read")
             self.alpha_ = float(grid[best])
             self.alphas_ = grid
             self.mse_path_ = mse.t()
