@@ -1235,7 +1235,8 @@ def _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap=None):
     return seed
 
 
-def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None, oof_items=None):
+def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=None, oof_items=None,
+                  platt_prep=None):
     from .. import ops
     E = ops.ext()
     s = ops.stream_ptr(device)
@@ -1253,6 +1254,53 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     max_l = max(p.l for p in live)
     solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
+    # ---- label-only tables of the post-SMO launches, uploaded BEFORE the rounds (each in-stream
+    # upload queued behind the SMO cost ≈ 30 µs on the critical path): the signs of y·α, the Platt
+    # decision table (+ the stacking fit's out-of-fold rows, ``oof_items``), the Platt kernel's maps
+    platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
+    sign_h = np.empty(aoffs[-1], dtype=np.float32)
+    for k, p in enumerate(live):
+        a0, l = aoffs_start[k], p.l
+        sign_h[a0:a0 + p.npos] = 1.0
+        sign_h[a0 + p.npos:a0 + l] = -1.0
+    sign_d = _to_dev(sign_h, device)
+    pre_dec = None
+    out = {}
+    if platt:
+        oof = []
+        if oof_items and not (SPLIT_JOIN and group is None):
+            finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
+            oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
+            if len(oof) != len(oof_items):
+                oof = []
+        hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
+        if oof:
+            hcat = torch.cat([hcat] + [Zt.to(torch.float32) for _, Zt in oof]).contiguous()
+        per = 1024
+        S = (max_l + per - 1) // per
+        dt = np.zeros(len(platt) + len(oof), _DEC_DT)
+        hoff = 0
+        for i, (k, p) in enumerate(platt):
+            h = int(p.held_rows.shape[0])
+            dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
+            hoff += h
+        hoff_platt = hoff
+        for i, (k, Zt) in enumerate(oof):
+            h = int(Zt.shape[0])
+            dt[len(platt) + i] = (zoffs[k], hoff, live[k].l, h, -live[k].gamma * 1.4426950408889634, per)
+            hoff += h
+        part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
+        ddev = _dev_struct(dt, device)
+        if _GAMMA_CTX[0] is not None:
+            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt] + [live[k].fit for k, _ in oof])
+        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"][:len(platt)].astype(np.int64))
+        rowk_d = _to_dev(rowk, device)
+        for i, (k, p) in enumerate(platt):
+            out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
+        if platt_prep is not None:
+            out["platt_prep"] = platt_prep({id(p): out[("hoff", id(p))] for _, p in platt})
+        pre_dec = dict(oof=oof, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
+                       rowk=rowk_d)
     deps: dict = {}
     if group is None:
         kw = {}
@@ -1277,7 +1325,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                     kw["seed"] = seed
             return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s, **kw)
         alpha, rho, iters, err = _solve_distributed(solve_local, live, aoffs[-1], aoffs, device, group)
-    out = {"smo_err": err}
+    out["smo_err"] = err
     J = deps.get("join")
     if J is not None:
         out["_deps"] = deps     # (consumers wait for the groups they read; finish joins them all)
@@ -1306,15 +1354,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                              keep=early_dev)
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
     # for the held-out decisions below and the stacking trainer's device OOF (enqueue_svc_oof)
-    # (the signs built on the host and uploaded in one copy: per-problem fills would be ~70 tiny
-    # launches queued behind the SMO)
-    sign_h = np.empty(aoffs[-1], dtype=np.float32)
-    for k, p in enumerate(live):
-        a0, l = aoffs_start[k], p.l
-        sign_h[a0:a0 + p.npos] = 1.0
-        sign_h[a0 + p.npos:a0 + l] = -1.0
-    sign_d = _to_dev(sign_h, device)
-    platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
+    # (the signs built on the host and uploaded in one copy, before the rounds)
     rho_pl = rho
     if J is not None:
         # the Platt decisions read only the Platt-CV problems: wait for their groups alone
@@ -1327,48 +1367,19 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     # ---- Platt held-out decision values of every CV sub-model: one batched launch — with the
     # stacking fit's out-of-fold rows (``oof_items``: [(fit f, fold-f-scaled rows)], decided by fit f's
     # final problem) in the SAME launch, so enqueue_svc_oof needs no decision launch of its own
-    if platt:
-        oof = []
-        if oof_items and J is None:
-            finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
-            oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
-            if len(oof) != len(oof_items):
-                oof = []
-        hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
-        if oof:
-            hcat = torch.cat([hcat] + [Zt.to(torch.float32) for _, Zt in oof]).contiguous()
-        per = 1024
-        S = (max_l + per - 1) // per
-        dt = np.zeros(len(platt) + len(oof), _DEC_DT)
-        hoff = 0
-        for i, (k, p) in enumerate(platt):
-            h = int(p.held_rows.shape[0])
-            dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
-            hoff += h
-        hoff_platt = hoff
-        for i, (k, Zt) in enumerate(oof):
-            h = int(Zt.shape[0])
-            dt[len(platt) + i] = (zoffs[k], hoff, live[k].l, h, -live[k].gamma * 1.4426950408889634, per)
-            hoff += h
-        part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
-        ddev = _dev_struct(dt, device)
-        if _GAMMA_CTX[0] is not None:
-            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt] + [live[k].fit for k, _ in oof])
-        max_h = int(dt["h"].max())
+    if pre_dec is not None:
+        pdd = pre_dec
         dmark("svc_smo_done")
-        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), hcat.data_ptr(), F, ddev.data_ptr(), len(dt),
-                        max_h, S, part.data_ptr(), s)
-        if oof:
-            out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in oof_items], part=part, hoff0=hoff_platt,
-                                  hoff=hoff - hoff_platt)
+        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), pdd["hcat"].data_ptr(), F, pdd["ddev"].data_ptr(),
+                        len(pdd["dt"]), int(pdd["dt"]["h"].max()), pdd["S"], pdd["part"].data_ptr(), s)
+        if pdd["oof"]:
+            out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in oof_items], part=pdd["part"], hoff0=pdd["hoff_platt"],
+                                  hoff=pdd["hoff"] - pdd["hoff_platt"])
         dmark("svc_platt_dec")
         # the decision values are assembled inside the Platt kernel from these partials (row r of
         # part: problem rowk[r]'s held-out point, d = −(Σ part[r] − ρ))
-        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"][:len(platt)].astype(np.int64))
-        out["platt_src"] = dict(part=part, S=S, rowk=_to_dev(rowk, device), rho=rho_pl.to(torch.float64).contiguous(),
-                                keep=(hcat, ddev))
-        for i, (k, p) in enumerate(platt):
-            out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
+        out["platt_src"] = dict(part=pdd["part"], S=pdd["S"], rowk=pdd["rowk"],
+                                rho=rho_pl.to(torch.float64).contiguous(), keep=(pdd["hcat"], pdd["ddev"]))
     return out
 
 
@@ -1609,22 +1620,11 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
     hmark("svc_expand")
     eps = float(svcs[0].tol)
     args = (svcs, Zs, ys, max_iter_cap, group)
-    _GAMMA_CTX[0] = gdev
-    try:
-        sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group, oof_items=oof_items) if cuda
-               else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
-    finally:
-        _GAMMA_CTX[0] = None
-    hmark("svc_solve_enqueued")
-    solver = LAST_SMO_INFO.get("solver")   # this batch's solver (the global is overwritten by later batches)
-    # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
-    AB = [None] * len(svcs)
     pl = [f for f, svc in enumerate(svcs) if svc.probability]
-    if pl and cuda:
-        # one launch for every fit: the kernel assembles each fit's decision values from the
-        # batched decision partials through a position → partial-row map (negative codes: a
-        # per-fold constant, −1 − code into consts; code −1 = 0.0 for positions no fold holds)
-        E = ops.ext()
+
+    def platt_prep(hoff_of):
+        """The Platt kernel's label-only tables (grouped-position → decision-partial row maps,
+        per-fold constants, the fit records), uploaded before the SMO rounds."""
         arr = np.zeros(len(pl), _PLATT_DT)
         maps, consts, off = [], [0.0], 0
         for k, f in enumerate(pl):
@@ -1633,7 +1633,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             sm = np.full(l, -1, dtype=np.int32)
             for p in (q for q in all_probs if q.fit == f and q.fold >= 0):
                 if p.rows is not None:
-                    h0, h = sol[("hoff", id(p))]
+                    h0, h = hoff_of[id(p)]
                     sm[p.held] = np.arange(h0, h0 + h, dtype=np.int32)
                 else:
                     consts.append(float(p.const))
@@ -1641,12 +1641,32 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
             arr[k] = (off, l, mt["n0"])
             maps.append(sm)
             off += l
+        return dict(srcmap=_to_dev(np.concatenate(maps), device),
+                    cdev=_to_dev(np.asarray(consts, dtype=np.float64), device), off=off,
+                    pdev=_dev_struct(arr, device))
+    _GAMMA_CTX[0] = gdev
+    try:
+        sol = (_solve_device(all_probs, Zs, device, eps, max_iter_cap, group, oof_items=oof_items,
+                             platt_prep=platt_prep if pl else None) if cuda
+               else _solve_host(all_probs, Zs, eps, max_iter_cap, group))
+    finally:
+        _GAMMA_CTX[0] = None
+    hmark("svc_solve_enqueued")
+    solver = LAST_SMO_INFO.get("solver")   # this batch's solver (the global is overwritten by later batches)
+    # ---- Platt: held-out decision values per fit (grouped-position order), then sigmoid fits
+    AB = [None] * len(svcs)
+    if pl and cuda:
+        # one launch for every fit: the kernel assembles each fit's decision values from the
+        # batched decision partials through a position → partial-row map (negative codes: a
+        # per-fold constant, −1 − code into consts; code −1 = 0.0 for positions no fold holds)
+        E = ops.ext()
+        pp = sol.get("platt_prep")
+        if pp is None:      # (every Platt fold degenerate: nothing was prepared ahead)
+            pp = platt_prep({id(p): sol[("hoff", id(p))] for p in all_probs if ("hoff", id(p)) in sol})
         src = sol.get("platt_src")
-        srcmap = _to_dev(np.concatenate(maps), device)
-        cdev = _to_dev(np.asarray(consts, dtype=np.float64), device)
+        srcmap, cdev, pdev, off = pp["srcmap"], pp["cdev"], pp["pdev"], pp["off"]
         dscr = torch.empty(off, dtype=torch.float64, device=device)   # (fits past 16k points)
         ABt = torch.empty(2 * len(pl), dtype=torch.float64, device=device)
-        pdev = _dev_struct(arr, device)
         dmark("svc_platt_in")
         part_p, S, rowk_p, rho_p = ((src["part"].data_ptr(), src["S"], src["rowk"].data_ptr(), src["rho"].data_ptr())
                                     if src is not None else (0, 0, 0, 0))   # (every fold degenerate)
