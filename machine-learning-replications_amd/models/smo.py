@@ -1254,53 +1254,59 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     max_l = max(p.l for p in live)
     solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
-    # ---- label-only tables of the post-SMO launches, uploaded BEFORE the rounds (each in-stream
-    # upload queued behind the SMO cost ≈ 30 µs on the critical path): the signs of y·α, the Platt
-    # decision table (+ the stacking fit's out-of-fold rows, ``oof_items``), the Platt kernel's maps
+    # ---- label-only tables of the post-SMO launches, uploaded BEFORE the main rounds — after the
+    # cascade parts are enqueued, while the device solves them (each in-stream upload queued behind
+    # the SMO cost ≈ 30 µs on the critical path; ahead of the parts they delayed the parts' enqueue):
+    # the signs of y·α, the Platt decision table (+ the stacking fit's out-of-fold rows,
+    # ``oof_items``), the Platt kernel's maps
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
-    sign_h = np.empty(aoffs[-1], dtype=np.float32)
-    for k, p in enumerate(live):
-        a0, l = aoffs_start[k], p.l
-        sign_h[a0:a0 + p.npos] = 1.0
-        sign_h[a0 + p.npos:a0 + l] = -1.0
-    sign_d = _to_dev(sign_h, device)
-    pre_dec = None
     out = {}
-    if platt:
-        oof = []
-        if oof_items and not (SPLIT_JOIN and group is None):
-            finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
-            oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
-            if len(oof) != len(oof_items):
-                oof = []
-        hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
-        if oof:
-            hcat = torch.cat([hcat] + [Zt.to(torch.float32) for _, Zt in oof]).contiguous()
-        per = 1024
-        S = (max_l + per - 1) // per
-        dt = np.zeros(len(platt) + len(oof), _DEC_DT)
-        hoff = 0
-        for i, (k, p) in enumerate(platt):
-            h = int(p.held_rows.shape[0])
-            dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
-            hoff += h
-        hoff_platt = hoff
-        for i, (k, Zt) in enumerate(oof):
-            h = int(Zt.shape[0])
-            dt[len(platt) + i] = (zoffs[k], hoff, live[k].l, h, -live[k].gamma * 1.4426950408889634, per)
-            hoff += h
-        part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
-        ddev = _dev_struct(dt, device)
-        if _GAMMA_CTX[0] is not None:
-            _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt] + [live[k].fit for k, _ in oof])
-        rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"][:len(platt)].astype(np.int64))
-        rowk_d = _to_dev(rowk, device)
-        for i, (k, p) in enumerate(platt):
-            out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
-        if platt_prep is not None:
-            out["platt_prep"] = platt_prep({id(p): out[("hoff", id(p))] for _, p in platt})
-        pre_dec = dict(oof=oof, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
-                       rowk=rowk_d)
+    tabs = {}
+
+    def prep_tables():
+        sign_h = np.empty(aoffs[-1], dtype=np.float32)
+        for k, p in enumerate(live):
+            a0, l = aoffs_start[k], p.l
+            sign_h[a0:a0 + p.npos] = 1.0
+            sign_h[a0 + p.npos:a0 + l] = -1.0
+        sign_d = _to_dev(sign_h, device)
+        pre_dec = None
+        if platt:
+            oof = []
+            if oof_items and not (SPLIT_JOIN and group is None):
+                finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
+                oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
+                if len(oof) != len(oof_items):
+                    oof = []
+            hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
+            if oof:
+                hcat = torch.cat([hcat] + [Zt.to(torch.float32) for _, Zt in oof]).contiguous()
+            per = 1024
+            S = (max_l + per - 1) // per
+            dt = np.zeros(len(platt) + len(oof), _DEC_DT)
+            hoff = 0
+            for i, (k, p) in enumerate(platt):
+                h = int(p.held_rows.shape[0])
+                dt[i] = (zoffs[k], hoff, p.l, h, -p.gamma * 1.4426950408889634, per)
+                hoff += h
+            hoff_platt = hoff
+            for i, (k, Zt) in enumerate(oof):
+                h = int(Zt.shape[0])
+                dt[len(platt) + i] = (zoffs[k], hoff, live[k].l, h, -live[k].gamma * 1.4426950408889634, per)
+                hoff += h
+            part = torch.zeros(hoff, S, dtype=torch.float32, device=device)
+            ddev = _dev_struct(dt, device)
+            if _GAMMA_CTX[0] is not None:
+                _GAMMA_CTX[0].patch(ddev, _DEC_DT, "ngl2e", [p.fit for _, p in platt] + [live[k].fit for k, _ in oof])
+            rowk = np.repeat(np.array([k for k, _ in platt], dtype=np.int32), dt["h"][:len(platt)].astype(np.int64))
+            rowk_d = _to_dev(rowk, device)
+            for i, (k, p) in enumerate(platt):
+                out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
+            if platt_prep is not None:
+                out["platt_prep"] = platt_prep({id(p): out[("hoff", id(p))] for _, p in platt})
+            pre_dec = dict(oof=oof, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
+                           rowk=rowk_d)
+        tabs.update(sign_d=sign_d, pre_dec=pre_dec)
     deps: dict = {}
     if group is None:
         kw = {}
@@ -1311,6 +1317,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                 hmark("svc_cascade_seeded")
         if solver == "ws" and SPLIT_JOIN:
             kw["deps_out"] = deps
+        prep_tables()
         alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, **kw)
     else:
         def solve_local(sub):
@@ -1324,6 +1331,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                 if seed is not None:
                     kw["seed"] = seed
             return solve(E, sub, zsub, so[:-1], so, F, device, eps, max_iter_cap, s, **kw)
+        prep_tables()
         alpha, rho, iters, err = _solve_distributed(solve_local, live, aoffs[-1], aoffs, device, group)
     out["smo_err"] = err
     J = deps.get("join")
@@ -1355,6 +1363,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
     # for the held-out decisions below and the stacking trainer's device OOF (enqueue_svc_oof)
     # (the signs built on the host and uploaded in one copy, before the rounds)
+    sign_d, pre_dec = tabs["sign_d"], tabs["pre_dec"]
     rho_pl = rho
     if J is not None:
         # the Platt decisions read only the Platt-CV problems: wait for their groups alone
