@@ -187,6 +187,19 @@ def main():
     pdist.shutdown()
 
 
+def _ws_critical(st):
+    """The working-set solve of the problem with the most pairs (the fit's critical path): rounds,
+    pairs and its in-kernel s_memtime phase totals (shader-clock kilocycles; the per-pair figure is
+    the inner loop's)."""
+    k = int(st["inner"].argmax())
+    pairs = max(int(st["inner"][k]), 1)
+    return {"rounds": int(st["outer"][k]), "pairs": pairs,
+            "kcyc_select": round(float(st["cyc_select"][k]) / 1e3, 1),
+            "kcyc_build": round(float(st["cyc_build"][k]) / 1e3, 1),
+            "kcyc_inner": round(float(st["cyc_inner"][k]) / 1e3, 1),
+            "cyc_per_pair": round(float(st["cyc_inner"][k]) / pairs)}
+
+
 def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
     """Facts that explain a training-bench run (VERDICT r1 'next round' #1): device, which
     solver / kernel paths ran, and how host-bound the timed steps were."""
@@ -197,10 +210,12 @@ def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
              "host_cpu_fraction": round(cpu / max(elapsed, 1e-12), 3),
              "stage_host_seconds": host_med,
              "step_ms_min_med_max": [round(1e3 * x, 2) for x in _step_stats(step_ends, t0)],
+             "step_ms": [round(1e3 * (b - a), 2) for a, b in zip([t0] + list(step_ends[:-1]), step_ends)],
              "svm": dict(smo.LAST_SMO_INFO, **({"lowrank": {k: v for k, v in svc_lowrank.LAST_INFO.items()}}
                                               if smo.LAST_SMO_INFO.get("solver") == "nystrom-ipm" else {}),
                          **({"ws_rounds_max": int(smo.LAST_WS_STATS["outer"].max()),
-                             "ws_pairs_max": int(smo.LAST_WS_STATS["inner"].max())}
+                             "ws_pairs_max": int(smo.LAST_WS_STATS["inner"].max()),
+                             "ws_critical": _ws_critical(smo.LAST_WS_STATS)}
                             if smo.LAST_SMO_INFO.get("solver") == "ws" else {})),
              "gbdt_path": hist_gbdt.LAST_PATH.get("path"),
              "logreg_path": logreg_solver.LAST_PATH.get("path"),

@@ -707,6 +707,7 @@ WS_GRAPH_CHUNK = int(os.environ.get("HFENS_SVM_WS_GRAPH_CHUNK", "32"))   # round
 _WS_GRAPHS: dict = {}
 WS_BIG_CHUNK = int(os.environ.get("HFENS_SVM_WS_BIG_CHUNK", "64"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
+WS_G0_FIRST = os.environ.get("HFENS_SVM_WS_G0_FIRST", "1") == "1"
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
@@ -739,9 +740,11 @@ def _ws_groups(live, device) -> List[List[int]]:
 
 
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None,
-              seed=None, q=None, groups=None, deps_out=None):
+              seed=None, q=None, groups=None, deps_out=None, after_first=None):
     """``seed``: a feasible α (per point, this batch's layout) to start from instead of α = 0
-    (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`)."""
+    (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`); ``after_first``:
+    host work (no device dependency on the rounds) run once every group's first rounds are
+    enqueued."""
     P = len(live)
     n = aoffs[-1]
     ml = max(p.l for p in live)
@@ -784,6 +787,13 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
         hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
     runs = []
+    ahead = WS_KC_ROUNDS_AHEAD if kc_all else (WS_SEEDED_AHEAD if seed is not None else WS_ROUNDS_AHEAD)
+    left = min(ahead, max_outer)
+    chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
+    done = [0] * len(groups)
+    # the first group (the largest problems: the batch's critical path) gets its first rounds
+    # enqueued as soon as its own state is, before the other groups' states are built
+    g0_first = WS_G0_FIRST and not sync and not use_graph and len(groups) > 1
     for gi, idx in enumerate(groups):
         # the last (smallest) group on the caller's stream, the others on process-lifetime side streams
         side = None
@@ -799,6 +809,9 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
                               cap_stream=(side if side is not None else caller) if use_graph else None,
                               frac=WS_INNER_FRAC_BIG if (gi == 0 and len(groups) > 1) else WS_INNER_FRAC,
                               seed=seed))
+        if g0_first and gi == 0:
+            done[0] = min(chunk, left)
+            runs[0]["steps"](done[0])
     from ..utils.timing import hmark
     hmark("ws_groups_ready")
     # HFENS_WS_EVENTS=1 (diagnostic): device events per group after every enqueued chunk, read by
@@ -814,6 +827,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
             e.record(r["side"] if r["side"] is not None else caller)
             evs["rounds"][gi].append(e)
     if sync:
+        if after_first is not None:
+            after_first()
         runs[0]["sync_rounds"](steps_per_check)
     else:
         # no host synchronisation: WS_ROUNDS_AHEAD rounds are enqueued at once (finished problems
@@ -821,17 +836,20 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         # a batch still unconverged after them reports err and is re-solved synchronously by
         # finish_svc_batch.  The groups' rounds are enqueued interleaved in chunks, so every
         # group's stream starts within one chunk of host launch time.
-        ahead = WS_KC_ROUNDS_AHEAD if kc_all else (WS_SEEDED_AHEAD if seed is not None else WS_ROUNDS_AHEAD)
-        left = min(ahead, max_outer)
-        chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
-        while left > 0:
-            k = min(chunk, left)
+        while any(d < left for d in done):
             for gi, r in enumerate(runs):
-                r["steps"](k)
-                if evs is not None:
-                    _mark(gi, r)
-            left -= k
+                k = min(chunk, left - done[gi])
+                if k > 0:
+                    r["steps"](k)
+                    done[gi] += k
+                    if evs is not None:
+                        _mark(gi, r)
+            if after_first is not None:
+                after_first()
+                after_first = None
             hmark("ws_chunk")
+        if after_first is not None:
+            after_first()
     for gi, r in enumerate(runs):
         r["finish"]()
         if evs is not None:
@@ -1254,9 +1272,10 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     max_l = max(p.l for p in live)
     solver = _pick_solver(max_l, F)
     solve = _solve_ws if solver == "ws" else _solve_exact
-    # ---- label-only tables of the post-SMO launches, uploaded BEFORE the main rounds — after the
-    # cascade parts are enqueued, while the device solves them (each in-stream upload queued behind
-    # the SMO cost ≈ 30 µs on the critical path; ahead of the parts they delayed the parts' enqueue):
+    # ---- label-only tables of the post-SMO launches, uploaded while the main rounds run — once
+    # every group's first rounds are enqueued (TABLES_AFTER_FIRST; each in-stream upload queued
+    # behind the whole SMO cost ≈ 30 µs on the critical path; ahead of the parts they delayed the
+    # parts' enqueue, ahead of the main rounds the critical group's first round):
     # the signs of y·α, the Platt decision table (+ the stacking fit's out-of-fold rows,
     # ``oof_items``), the Platt kernel's maps
     platt = [(k, p) for k, p in enumerate(live) if p.fold >= 0]
@@ -1307,6 +1326,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
             pre_dec = dict(oof=oof, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
                            rowk=rowk_d)
         tabs.update(sign_d=sign_d, pre_dec=pre_dec)
+        hmark("svc_tables")
     deps: dict = {}
     if group is None:
         kw = {}
@@ -1317,7 +1337,11 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                 hmark("svc_cascade_seeded")
         if solver == "ws" and SPLIT_JOIN:
             kw["deps_out"] = deps
-        prep_tables()
+        if solver == "ws" and TABLES_AFTER_FIRST:
+            # (built while the device runs the first rounds, off the critical group's enqueue)
+            kw["after_first"] = prep_tables
+        else:
+            prep_tables()
         alpha, rho, iters, err = solve(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, **kw)
     else:
         def solve_local(sub):
@@ -1447,6 +1471,9 @@ EARLY_READ = os.environ.get("HFENS_SVC_EARLY_READ", "1") != "0"
 # (measured, profiles/r6_runs/r6r: no gain on the headline — the Platt-CV groups end within
 # ≈ 0.1 ms of the refit's 10k problem — so it is off by default: 18.07 / 17.79 vs 17.92 / 18.11 ms)
 SPLIT_JOIN = os.environ.get("HFENS_SVM_SPLIT_JOIN", "0") == "1"
+# the post-SMO label-only tables built once every working-set group's first rounds are enqueued
+# ("0": before the main rounds, behind the cascade parts)
+TABLES_AFTER_FIRST = os.environ.get("HFENS_SVC_TABLES_AFTER_FIRST", "1") == "1"
 EXACT_HOST_MAX = int(os.environ.get("HFENS_SVM_EXACT_HOST_MAX", "32768"))
 GRAM_BUDGET = float(os.environ.get("HFENS_SVM_GRAM_BUDGET", str(96 << 30)))
 
