@@ -742,7 +742,9 @@ def _ws_groups(live, device) -> List[List[int]]:
 def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, steps_per_check=None,
               seed=None, q=None, groups=None, deps_out=None, after_first=None):
     """``seed``: a feasible α (per point, this batch's layout) to start from instead of α = 0
-    (:func:`_cascade_seed`); ``q``: the working-set size (default :func:`ws_q`); ``after_first``:
+    (:func:`_cascade_seed`) — every value AT a bound or at least f32 resolution inside it (the
+    selection keys read f64 α, the inner solve f32 α: a value within an f32 ulp of a bound is free
+    to one and bound to the other, profiles/r6_nystrom_seed.md); ``q``: the working-set size (default :func:`ws_q`); ``after_first``:
     host work (no device dependency on the rounds) run once every group's first rounds are
     enqueued."""
     P = len(live)
