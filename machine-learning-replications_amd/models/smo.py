@@ -245,9 +245,36 @@ def _to_dev(a: np.ndarray, device) -> torch.Tensor:
 
 
 def _gather_rows(Zs, probs, attr, device) -> torch.Tensor:
-    """Concatenate Zs[p.fit][getattr(p, attr)] over ``probs`` with one gather per fit."""
-    parts = []
+    """Concatenate Zs[p.fit][getattr(p, attr)] over ``probs`` with one gather per fit — or ONE
+    gather when every Zs[f] is a row block of one matrix (the stacking trainer's batched scaler
+    output: one upload and two launches instead of six of each)."""
     fits = sorted({p.fit for p in probs})
+    base = Zs[0]._base
+    if (base is not None and base.dim() == 2 and base.is_contiguous() and base.storage_offset() == 0
+            and all(Z._base is base and Z.is_contiguous() for Z in Zs)):
+        F = base.shape[1]
+        order, idx, offs = [], [], []
+        for f in fits:
+            sub = [p for p in probs if p.fit == f]
+            off = Zs[f].storage_offset() // F
+            for p in sub:
+                idx.append(getattr(p, attr))
+                offs.append(off)
+            order += sub
+        if [id(p) for p in order] != [id(p) for p in probs]:
+            raise AssertionError("problems must be grouped by fit")
+        # the global row indices written straight into pinned memory (one pass, no staging copy)
+        total = sum(int(a.shape[0]) for a in idx)
+        cuda = torch.device(device).type == "cuda"
+        h = torch.empty(total, dtype=torch.int64, pin_memory=cuda)
+        cat = h.numpy()
+        pos = 0
+        for a, off in zip(idx, offs):
+            np.add(a, off, out=cat[pos:pos + a.shape[0]], casting="unsafe")
+            pos += a.shape[0]
+        ii = h.to(device, non_blocking=True) if cuda else h
+        return base.index_select(0, ii).to(torch.float32)
+    parts = []
     order = []
     for f in fits:
         idx = [getattr(p, attr) for p in probs if p.fit == f]
@@ -749,11 +776,11 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     enqueued."""
     P = len(live)
     n = aoffs[-1]
-    ml = max(p.l for p in live)
+    ml = _max_l(live)
     kc_all = ws_kc(F, ml)          # one solver kind for the whole batch (every group)
     Q = ws_q(F, ml) if (q is None or kc_all) else int(q)
     Fp2 = 2 * _ws_ks(F)
-    max_outer = (max(5_000, max(p.l for p in live) // 4) if max_iter_cap is None else int(max_iter_cap))
+    max_outer = (max(5_000, ml // 4) if max_iter_cap is None else int(max_iter_cap))
     max_inner = WS_MAX_INNER
     # large problems (candidate-list selection, hundreds to thousands of rounds): host-checked rounds
     # in chunks of WS_BIG_CHUNK from the start, one group (the rounds-ahead guess would be far off)
@@ -945,7 +972,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         return out
     LAST_WS_STATS.set_thunk(stats)
     LAST_SMO_INFO.clear()
-    LAST_SMO_INFO.update(problems=P, max_l=int(max(p.l for p in live)), solver="ws", q=Q, ws_groups=len(runs),
+    LAST_SMO_INFO.update(problems=P, max_l=int(ml), solver="ws", q=Q, ws_groups=len(runs),
                          ws_kc=kc_all)
     return alpha, rho, iters, err
 
@@ -962,14 +989,21 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
     # (column-wise: a per-record tuple assignment costs ~1.5 µs each, ≈ 0.3 ms for the cascade's
     # ~200 parts on the host critical path)
     ii = np.asarray(idx, dtype=np.int64)
-    ps = [live[j] for j in idx]
     arr["zoff"] = np.asarray(zoffs, dtype=np.int64)[ii]
     arr["aoff"] = np.asarray(aoffs, dtype=np.int64)[ii]
-    arr["l"] = [p.l for p in ps]
-    arr["npos"] = [p.npos for p in ps]
-    arr["Cp"] = [p.Cp for p in ps]
-    arr["Cn"] = [p.Cn for p in ps]
-    arr["ngl2e"] = [-p.gamma * 1.4426950408889634 for p in ps]
+    if isinstance(live, _PartSet):
+        arr["l"], arr["npos"] = live.l[ii], live.npos[ii]
+        arr["Cp"], arr["Cn"] = live.Cp[ii], live.Cn[ii]
+        arr["ngl2e"] = -live.gamma[ii] * 1.4426950408889634
+        fits = live.fit[ii]
+    else:
+        ps = [live[j] for j in idx]
+        arr["l"] = [p.l for p in ps]
+        arr["npos"] = [p.npos for p in ps]
+        arr["Cp"] = [p.Cp for p in ps]
+        arr["Cn"] = [p.Cn for p in ps]
+        arr["ngl2e"] = [-p.gamma * 1.4426950408889634 for p in ps]
+        fits = [p.fit for p in ps]
     max_l = int(arr["l"].max())
     ctx = (lambda: torch.cuda.stream(side)) if side is not None else contextlib.nullcontext
     out = dict(side=side, idx=np.asarray(idx, dtype=np.int64), err=None)
@@ -991,7 +1025,7 @@ def _ws_group(E, live, idx, zcat, zoffs, aoffs, F, device, eps, max_outer, max_i
             pdev = _dev_struct(arr, device)
             host = None
         if _GAMMA_CTX[0] is not None:
-            _GAMMA_CTX[0].patch(pdev, _WS_DT, "ngl2e", [live[j].fit for j in idx])
+            _GAMMA_CTX[0].patch(pdev, _WS_DT, "ngl2e", fits)
         states = buf("states", P * _WS_STATE_BYTES // 4, torch.int32)
         wsz = buf("wsz", P * Fp2 * Q, torch.float32)
         wsn = buf("wsn", P * Q, torch.float32)
@@ -1221,24 +1255,71 @@ class _Part:
         self.fit, self.fold, self.l, self.npos, self.Cp, self.Cn, self.gamma = fit, fold, l, npos, Cp, Cn, gamma
 
 
+class _PartSet:
+    """The cascade's parts as arrays (one entry per part): built with a few numpy operations instead
+    of ≈ 200 Python records per fit on the host path to the parts' launch.  Indexing yields a
+    :class:`_Part`; :func:`_ws_group` and :func:`_solve_ws` read the arrays directly."""
+
+    def __init__(self, fit, fold, l, npos, Cp, Cn, gamma):
+        self.fit, self.fold, self.l, self.npos, self.Cp, self.Cn, self.gamma = fit, fold, l, npos, Cp, Cn, gamma
+        self.max_l = int(l.max()) if l.shape[0] else 0
+
+    def __len__(self):
+        return int(self.l.shape[0])
+
+    def __getitem__(self, k):
+        return _Part(int(self.fit[k]), int(self.fold[k]), int(self.l[k]), int(self.npos[k]), float(self.Cp[k]),
+                     float(self.Cn[k]), float(self.gamma[k]))
+
+    def __iter__(self):
+        return (self[k] for k in range(len(self)))
+
+
+def _max_l(live) -> int:
+    return live.max_l if isinstance(live, _PartSet) else max(p.l for p in live)
+
+
+def _cascade_tables(live, aoffs):
+    """(parts table [n_parts, 7] int64: start, length, parent offset, P, j, parent npos, part npos;
+    the parts as a :class:`_PartSet`), or None when no problem is split.  :func:`cascade_split`,
+    vectorised: P = max(2, round(l / CASCADE_PART)) parts (round half to even, as Python's round)
+    when l ≥ CASCADE_MIN and both classes have ≥ P points, else 0 (solved cold)."""
+    K = len(live)
+    l = np.fromiter((p.l for p in live), np.int64, K)
+    npos = np.fromiter((p.npos for p in live), np.int64, K)
+    if CASCADE_PART > 0:
+        P = np.maximum(2, np.rint(l / CASCADE_PART).astype(np.int64))
+        P = np.where((l >= CASCADE_MIN) & (npos >= P) & (l - npos >= P), P, 0)
+    else:
+        P = np.zeros(K, np.int64)
+    if not P.any():
+        return None
+    # part j of problem k takes ⌈(npos − j) / P⌉ positives and ⌈(nneg − j) / P⌉ negatives
+    kk = np.repeat(np.arange(K), P)
+    j = np.arange(kk.shape[0]) - np.repeat(np.cumsum(P) - P, P)
+    Pk, nk = P[kk], npos[kk]
+    cp = (nk - j + Pk - 1) // Pk
+    cn = (l[kk] - nk - j + Pk - 1) // Pk
+    ln = cp + cn
+    start = np.cumsum(ln) - ln
+    tab_np = np.stack([start, ln, np.asarray(aoffs[:K], dtype=np.int64)[kk], Pk, j, nk, cp], axis=1)
+    f64 = np.float64
+    parts = _PartSet(np.fromiter((p.fit for p in live), np.int64, K)[kk],
+                     np.fromiter((p.fold for p in live), np.int64, K)[kk], ln, cp,
+                     np.fromiter((p.Cp for p in live), f64, K)[kk], np.fromiter((p.Cn for p in live), f64, K)[kk],
+                     np.fromiter((p.gamma for p in live), f64, K)[kk])
+    return tab_np, parts
+
+
 def _cascade_seed(E, live, zcat, aoffs, F, device, s, max_iter_cap=None):
     """The feasible warm start of every problem (zeros for problems solved cold), or None.  The
     parts' point lists are built on the device (cascade_where) and their features gathered from the
     parents' rows in ``zcat`` — the host only counts."""
-    parts, tab = [], []
-    start = 0
-    for k, p in enumerate(live):
-        P = cascade_split(p.l, p.npos)
-        nneg = p.l - p.npos
-        for j in range(P):
-            cp, cn = (p.npos - j + P - 1) // P, (nneg - j + P - 1) // P
-            parts.append(_Part(p.fit, p.fold, cp + cn, cp, p.Cp, p.Cn, p.gamma))
-            tab.append((start, cp + cn, aoffs[k], P, j, p.npos, cp))
-            start += cp + cn
-    if not parts:
+    ct = _cascade_tables(live, aoffs)
+    if ct is None:
         return None
-    tab_np = np.asarray(tab, dtype=np.int64)
-    where = torch.empty(start, dtype=torch.int64, device=device)
+    tab_np, parts = ct
+    where = torch.empty(int(tab_np[:, 1].sum()), dtype=torch.int64, device=device)
     E.cascade_where(_to_dev(tab_np.reshape(-1), device).data_ptr(), len(parts), int(tab_np[:, 1].max()),
                     where.data_ptr(), s)
     zpart = zcat.index_select(0, where)

@@ -235,25 +235,76 @@ def plan_stacking_start(clf, y_np: np.ndarray):
     lens = np.empty(nf1, dtype=np.int64)
     out = np.empty(nf1 * 7 * n, dtype=np.int64)
     meta = np.empty(nf1 * 21, dtype=np.int64)
-    import threading
     E = ops.ext()
-    th = threading.Thread(target=E.stack_plan_host, name="hfens-plan-native", daemon=True,
-                          args=(y_np.ctypes.data, n, N_FOLDS, seed, folds.ctypes.data, rows.ctypes.data,
-                                lens.ctypes.data, out.ctypes.data, meta.ctypes.data))
-    th.start()
+    done = _plan_worker().submit(E.stack_plan_host, y_np.ctypes.data, n, N_FOLDS, seed, folds.ctypes.data,
+                                 rows.ctypes.data, lens.ctypes.data, out.ctypes.data, meta.ctypes.data)
+    balanced = svc.class_weight == "balanced"
 
     def join():
-        th.join()
+        done.wait()
+        if done.error is not None:
+            raise done.error
         rows_host = [rows[f * n:f * n + int(lens[f])] for f in range(nf1)]
         pre = []
         for f in range(nf1):
             l = int(lens[f])
             yf = y_np[rows_host[f]]
-            probs, mt = smo._wrap_expansion(f, l, out[f * 7 * n:(f + 1) * 7 * n], meta[f * 21:(f + 1) * 21], None,
-                                            smo._class_weights_host(svc, yf), svc)
+            mf = meta[f * 21:(f + 1) * 21]
+            # 'balanced': l / (2·[#class 0, #class 1]) from the expansion's class-0 count (= the
+            # bincount of _class_weights_host, the same f64 expression)
+            cw = (l / (2 * np.array([mf[0], l - mf[0]], dtype=np.float64)) if balanced
+                  else smo._class_weights_host(svc, yf))
+            probs, mt = smo._wrap_expansion(f, l, out[f * 7 * n:(f + 1) * 7 * n], mf, None, cw, svc)
             pre.append((yf, probs, mt))
         return dict(y_np=y_np, folds_np=folds, rows_host=rows_host, svc_pre={svc_cols[0]: pre})
     return join
+
+
+class _Done:
+    """Completion of one :class:`_PlanWorker` job."""
+
+    def __init__(self):
+        import threading
+        self._ev = threading.Event()
+        self.error = None
+
+    def wait(self):
+        self._ev.wait()
+
+
+class _PlanWorker:
+    """One long-lived daemon thread running native host jobs (GIL released inside them) — a thread
+    start per fit cost ≈ 0.1 ms of the launching thread's time (scripts/probes/preparts_profile.py)."""
+
+    def __init__(self):
+        import queue
+        import threading
+        self._q = queue.SimpleQueue()
+        self._th = threading.Thread(target=self._run, name="hfens-plan-native", daemon=True)
+        self._th.start()
+
+    def _run(self):
+        while True:
+            fn, args, done = self._q.get()
+            try:
+                fn(*args)
+            except BaseException as e:   # re-raised by the joining thread
+                done.error = e
+            done._ev.set()
+
+    def submit(self, fn, *args) -> _Done:
+        done = _Done()
+        self._q.put((fn, args, done))
+        return done
+
+
+_PLAN_WORKER: list = []
+
+
+def _plan_worker() -> _PlanWorker:
+    if not _PLAN_WORKER:
+        _PLAN_WORKER.append(_PlanWorker())
+    return _PLAN_WORKER[0]
 
 
 def _launch_svc(stc) -> bool:

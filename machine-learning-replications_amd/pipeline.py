@@ -54,6 +54,11 @@ BASES_AFTER_CV = os.environ.get("HFENS_BASES_AFTER_CV", "0") == "1"
 # 18.3 / 17.9 ms): the paths end ≈ 3 ms before the SMO, and their short tail then waited behind the
 # stack's reads; off by default
 FINISH_BEFORE_LASSO = os.environ.get("HFENS_FINISH_BEFORE_LASSO", "0") == "1"
+# the native stacking plan (stack_trainer.plan_stacking_start, a helper thread with the GIL released)
+# joined as the first job under the LassoCV's early speculation instead of right after the imputation
+# is enqueued: the thread then has the LassoCV prelude's host time to finish in, and the join no
+# longer waits for it on the host path to the SVC's cascade parts
+PLAN_JOIN_LATE = os.environ.get("HFENS_PLAN_JOIN_LATE", "1") == "1"
 
 
 def _bins_ahead(X_dev: torch.Tensor, clf):
@@ -183,6 +188,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
             if "err" in box:
                 raise box["err"]
             plan_box["plan"] = box["plan"]
+        run.native = native is not None
         return run
 
     y_full = None
@@ -230,7 +236,7 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
     # plan, the speculative LassoCV refit and the stacking prelaunch; only the SMO problems are
     # spread over the ranks, by the one all-reduce inside the prelaunched SVC batch)
     local = group is None or task
-    if overlap is not None and local and not PLAN_THREAD:
+    if overlap is not None and local and not PLAN_THREAD and not (PLAN_JOIN_LATE and getattr(overlap, "native", False)):
         # the label-only stacking plan now, on the host, while the device imputes (LassoCV's
         # prelude reads wait for the imputation anyway): it is ready before the LassoCV path is
         # launched, so the stacking fit can be enqueued first thing under the path
@@ -238,7 +244,8 @@ def develop(X_dev, y_dev, X_sel, y_sel, names, device="cpu", cfg: Optional[Ensem
         hmark("plan_ready")
         overlap, planned = None, True
     elif overlap is not None and local:
-        # (PLAN_THREAD: joined as the first job under the LassoCV path)
+        # (PLAN_THREAD / a native plan with PLAN_JOIN_LATE: joined as the first job under the
+        # LassoCV path)
         planned = True
     with timer.stage("select"):
         jobs, early_jobs = [], []

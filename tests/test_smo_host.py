@@ -23,6 +23,53 @@ def test_cascade_parts_partition_the_problem(l, npos):
         assert abs(cp - npos / P) <= 1 and abs((pos.shape[0] - cp) - (l - npos) / P) <= 1
 
 
+def test_gather_rows_single_gather_matches_per_fit():
+    """smo._gather_rows: when every fit's matrix is a row block of one matrix (the batched scaler's
+    output) the one-gather path returns exactly the per-fit gathers' concatenation."""
+    import torch
+    from hfens.models import smo
+
+    class P:
+        def __init__(self, fit, rows):
+            self.fit, self.rows = fit, rows
+    rng = np.random.default_rng(0)
+    Z = torch.randn(150, 4, dtype=torch.float64)
+    blocks = [Z[0:50], Z[50:100], Z[100:150]]
+    probs = [P(f, rng.integers(0, 50, size=int(rng.integers(5, 30))).astype(np.int64)) for f in (0, 0, 1, 2, 2, 2)]
+    one = smo._gather_rows(blocks, probs, "rows", "cpu")
+    per_fit = smo._gather_rows([b.clone() for b in blocks], probs, "rows", "cpu")
+    assert one.dtype == torch.float32 and torch.equal(one, per_fit)
+
+
+def test_cascade_tables_match_the_per_problem_split():
+    """smo._cascade_tables (vectorised) equals the per-problem loop over cascade_split: the parts
+    table rows (start, length, parent offset, P, j, parent npos, part npos) and every part's record."""
+    from hfens.models import smo
+    rng = np.random.default_rng(5)
+    sizes = [10000, 8000, 8000, 6400, 6400, 4096, 4095, 4500, 5000, 3000, 12345, 5201]
+    live, aoffs = [], [0]
+    for k, l in enumerate(sizes):
+        npos = int(rng.integers(1, l)) if k != 7 else 2       # (k = 7: too few positives to split)
+        live.append(smo._Prob(k % 6, k % 5 - 1, np.arange(l), npos, 1.0 + 0.1 * k, 0.7 + 0.05 * k, 0.05 + 0.01 * k))
+        aoffs.append(aoffs[-1] + l)
+    tab, start = [], 0
+    ref = []
+    for k, p in enumerate(live):
+        P = smo.cascade_split(p.l, p.npos)
+        for j in range(P):
+            cp, cn = (p.npos - j + P - 1) // P, (p.l - p.npos - j + P - 1) // P
+            tab.append((start, cp + cn, aoffs[k], P, j, p.npos, cp))
+            ref.append((p.fit, p.fold, cp + cn, cp, p.Cp, p.Cn, p.gamma))
+            start += cp + cn
+    got_tab, parts = smo._cascade_tables(live, aoffs)
+    assert got_tab.dtype == np.int64 and np.array_equal(got_tab, np.asarray(tab, dtype=np.int64))
+    assert len(parts) == len(ref) and parts.max_l == max(r[2] for r in ref)
+    for k, r in enumerate(ref):
+        q = parts[k]
+        assert (q.fit, q.fold, q.l, q.npos, q.Cp, q.Cn, q.gamma) == r
+    assert smo._cascade_tables([live[7]], [0, live[7].l]) is None
+
+
 @pytest.mark.parametrize("n,p1,seed", [(10000, 0.2, 2020), (713, 0.198, 7), (37, 0.05, 3), (12, 0.1, 1), (9, 0.0, 5)])
 def test_native_expand_matches_numpy(n, p1, seed):
     """ops/csrc/host.hip svc_expand_host (one native call per fit, the stacking plan's hot loop)
