@@ -1922,8 +1922,11 @@ def finish_svc_batch(st: dict, defer=None):
     finals = [[q for q in all_probs if q.fit == f and q.fold < 0][0] for f in range(len(svcs))]
     if early is not None and early["ids"] != [id(p) for p in finals]:
         early = None
+    from ..utils.timing import hmark
     if early is not None:
+        hmark("svc_early_wait")
         early["ev"].synchronize()
+        hmark("svc_early_synced")
         host_e = early["host"].numpy()
         smo_failed = early["has_err"] and host_e[-1] != 0.0
     else:

@@ -647,6 +647,8 @@ def finish_stacking(stc):
     model and set the StackingClassifier's fitted attributes."""
     clf, timer, group, svc_group = stc["clf"], stc["timer"], stc["group"], stc["svc_group"]
     X, y, masks, meta, y64, early = stc["X"], stc["y"], stc["masks"], stc["meta"], stc["y64"], stc["early"]
+    from ..utils.timing import hmark as _hmf
+    _hmf("finish_in")
     if stc["concurrent"] and not stc["bases_done"]:
         _launch_bases(stc)        # (prelaunched without the bases: PRELAUNCH_BASES=0)
     fitted_all = _finish_concurrent(stc) if stc["concurrent"] else None
@@ -826,6 +828,8 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
             cdev = ch[0].numpy()
         else:
             cdev = pre["cols_dev"].cpu().numpy()
+        from ..utils.timing import hmark
+        hmark("stack_checked")
         if cols is None or not np.array_equal(cdev, np.asarray(cols, dtype=np.int64)):
             if pre.get("speculative"):
                 # the CV chose another alpha than the speculated one, with another selection: the
