@@ -23,5 +23,13 @@ Phi = Phi.to(torch.float32).to(torch.float64)
 yv = torch.as_tensor(np.where(y > 0.5, -1.0, 1.0), device=dev)
 c = torch.where(yv > 0, 0.62, 2.5).to(torch.float64)
 print("rank", Phi.shape, flush=True)
-a, rho, it = svc_lowrank.ipm_svc_dual(Phi, yv, c)
-print(f"iterations {it} rho {rho:.6f} nsv {int((a > 0).sum())} bound {int((a >= c * (1 - 1e-9)).sum())}", flush=True)
+import time  # noqa: E402
+for rep in range(int(os.environ.get("REPS", "1"))):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    a, rho, it = svc_lowrank.ipm_svc_dual(Phi, yv, c)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+w = Phi.t() @ (yv * a)
+print(f"iterations {it} solve_s {dt:.3f} rho {rho:.9f} |w| {float(w.norm()):.9f} nsv {int((a > 0).sum())} "
+      f"bound {int((a >= c * (1 - 1e-9)).sum())} correctors {svc_lowrank.N_CORRECTORS}", flush=True)
