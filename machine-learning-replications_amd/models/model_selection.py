@@ -80,7 +80,8 @@ def fold_masks(test_folds, n_splits: int, device=None, with_full: bool = True) -
         tf = tf.pin_memory().to(device, non_blocking=True)
     elif device is not None:
         tf = tf.to(device)
-    m = torch.stack([tf != k for k in range(n_splits)])
-    if with_full:
-        m = torch.cat([m, torch.ones(1, tf.numel(), dtype=torch.bool, device=device)])
-    return m
+    # one comparison against [0, …, K−1] (and K, which no fold id equals: the all-true refit row).
+    # (no element assignment on the device tensor: a host scalar written into it was a blocking
+    # copy that waited for the stream's queued work — ≈ 0.6 ms of the prelaunch's host time)
+    ks = torch.arange(n_splits + int(with_full), device=tf.device, dtype=tf.dtype)
+    return tf[None, :] != ks[:, None]

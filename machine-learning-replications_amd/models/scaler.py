@@ -45,6 +45,14 @@ class StandardScaler(Estimator):
         self.scale_ = torch.where(scale == 0.0, torch.ones_like(scale), scale)
         return self
 
+    def _set_parts(self, mean, var, scale, n):
+        """:meth:`_set` with the scale already formed (the stacking trainer forms every fold's scale
+        in one batched sqrt / where — the same elementwise expressions)."""
+        self.n_features_in_ = int(mean.numel())
+        self.n_samples_seen_ = int(n)
+        self.mean_, self.var_, self.scale_ = mean, var, scale
+        return self
+
     def transform(self, X):
         X = as_tensor(X, device=self.mean_.device)
         if self.with_mean:

@@ -1375,10 +1375,12 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         pre_dec = None
         if platt:
             oof = []
-            if oof_items and not (SPLIT_JOIN and group is None):
+            # (``oof_items`` may be a callable: the caller's out-of-fold rows formed only now)
+            oi = oof_items() if callable(oof_items) else oof_items
+            if oi and not (SPLIT_JOIN and group is None):
                 finals = {p.fit: k for k, p in enumerate(live) if p.fold < 0}
-                oof = [(finals[f], Zt) for f, Zt in oof_items if f in finals]
-                if len(oof) != len(oof_items):
+                oof = [(finals[f], Zt) for f, Zt in oi if f in finals]
+                if len(oof) != len(oi):
                     oof = []
             hcat = _gather_rows(Zs, [p for _, p in platt], "held_rows", device)
             if oof:
@@ -1406,7 +1408,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                 out[("hoff", id(p))] = (int(dt[i]["hoff"]), int(dt[i]["h"]))
             if platt_prep is not None:
                 out["platt_prep"] = platt_prep({id(p): out[("hoff", id(p))] for _, p in platt})
-            pre_dec = dict(oof=oof, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
+            pre_dec = dict(oof=oof, oi=oi, hcat=hcat, S=S, dt=dt, hoff=hoff, hoff_platt=hoff_platt, part=part, ddev=ddev,
                            rowk=rowk_d)
         tabs.update(sign_d=sign_d, pre_dec=pre_dec)
         hmark("svc_tables")
@@ -1489,7 +1491,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), pdd["hcat"].data_ptr(), F, pdd["ddev"].data_ptr(),
                         len(pdd["dt"]), int(pdd["dt"]["h"].max()), pdd["S"], pdd["part"].data_ptr(), s)
         if pdd["oof"]:
-            out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in oof_items], part=pdd["part"], hoff0=pdd["hoff_platt"],
+            out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in pdd["oi"]], part=pdd["part"], hoff0=pdd["hoff_platt"],
                                   hoff=pdd["hoff"] - pdd["hoff_platt"])
         dmark("svc_platt_dec")
         # the decision values are assembled inside the Platt kernel from these partials (row r of

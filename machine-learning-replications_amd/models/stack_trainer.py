@@ -131,8 +131,12 @@ def _svc_inputs(est, X, y, masks, group=None, rows_host=None):
         if ops.has_ext():
             mean, var, Z, offs, idx = scaler_batch_device(X, rows_host)
             ycat = y.index_select(0, idx)
+            # every clone's scaler attributes from ONE sqrt / where over [K, F] (StandardScaler._set's
+            # expressions, elementwise: the same bits as K separate calls)
+            sd = torch.sqrt(var)
+            scale = torch.where(sd == 0.0, torch.ones_like(sd), sd)
             for k, c in enumerate(clones):
-                c.steps[0][1]._set(mean[k], var[k], int(offs[k + 1] - offs[k]))
+                c.steps[0][1]._set_parts(mean[k], var[k], scale[k], int(offs[k + 1] - offs[k]))
                 Zs.append(Z[offs[k]:offs[k + 1]])
                 ys.append(ycat[offs[k]:offs[k + 1]])
             return clones, [c.steps[-1][1] for c in clones], Zs, ys
@@ -343,14 +347,24 @@ def _launch_svc(stc) -> bool:
             clones, svcs, Zs, ys = _svc_inputs(clf.estimators[i][1], X, y, masks, group, rows_host)
             hmark("svc_inputs")
             if group is None:
-                yh = [y_np[r] for r in rows_host] if (y_np is not None and rows_host is not None) else None
+                plan_i = (svc_pre or {}).get(i)
+                yh = ([y_np[r] for r in rows_host] if (plan_i is None and y_np is not None and rows_host is not None)
+                      else None)
                 # the out-of-fold rows, scaled by their fold's scaler, go into the SVC batch's Platt
-                # decision launch (one launch for both)
-                items = stc["oof_items"](clones) if stc["oof_svc_dev"] is not None else None
+                # decision launch (one launch for both) — built when the batch asks for them (its
+                # post-SMO tables, after the cascade parts and the first rounds are enqueued)
+                memo = {}
+
+                def items_of(clones=clones, memo=memo):
+                    if "v" not in memo:
+                        memo["v"] = stc["oof_items"](clones)
+                    return memo["v"]
+                merged = (stc["oof_svc_dev"] is not None and MERGED_OOF_DEC and stc["oof_items_ok"](clones))
                 # device γ (no host read before the SMO) whenever the batch is eligible
-                st = launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh, plan=(svc_pre or {}).get(i),
+                st = launch_svc_batch(svcs, Zs, ys, group=svc_group, y_host=yh, plan=plan_i,
                                       gamma_dev=GAMMA_DEV,
-                                      oof_items=[(k, Zt) for k, Zt, _ in items] if (items and MERGED_OOF_DEC) else None)
+                                      oof_items=(lambda: [(k, Zt) for k, Zt, _ in items_of()]) if merged else None)
+                items = items_of() if stc["oof_svc_dev"] is not None else None
                 if stc["oof_svc_dev"] is not None:
                     # the OOF column straight from the device solution, behind the SMO on this
                     # stream: no wait for the fitted models' host bookkeeping
@@ -574,9 +588,15 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
     rows_host = (plan["rows_host"] if svc_pre is not None
                  else [np.nonzero(folds_np != k)[0] for k in range(N_FOLDS)] + [np.arange(n)])
     masks = fold_masks(folds_np, N_FOLDS, device=dev)        # [6, n]
-    # OOF rows per fold as device index tensors (uploaded once, non-blocking): the meta-feature
-    # gathers / scatters then need no host synchronisation
-    test_idx = [_index_to(np.nonzero(folds_np == k)[0], dev) for k in range(N_FOLDS)]
+    # OOF rows per fold as device index tensors (ONE upload, non-blocking, split into per-fold views:
+    # a stable argsort lists each fold's rows in ascending order, as np.nonzero does): the
+    # meta-feature gathers / scatters then need no host synchronisation
+    f8 = np.asarray(folds_np).astype(np.int8)      # (fold ids < 128: numpy's stable sort is a radix sort)
+    order = np.argsort(f8, kind="stable")
+    cnt = np.bincount(f8, minlength=N_FOLDS)
+    order_d = _index_to(order, dev)
+    starts = np.concatenate([[0], np.cumsum(cnt)])
+    test_idx = [order_d[int(starts[k]):int(starts[k + 1])] for k in range(N_FOLDS)]
     meta = torch.zeros(n, len(clf.estimators), dtype=torch.float64, device=dev)
     stc = dict(clf=clf, X=X, y=y, masks=masks, test_idx=test_idx, meta=meta, group=group, svc_group=svc_group,
                rows_host=rows_host, y_np=y_np, svc_pre=svc_pre, folds_np=folds_np, timer=timer, plan=plan,
@@ -590,8 +610,11 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
                 p1 = fitted[k].predict_proba(X.index_select(0, test_idx[k]))[:, 1].to(torch.float64)
                 meta[:, col].index_copy_(0, test_idx[k], p1)
 
+    def oof_items_ok(fitted):
+        return DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])
+
     def oof_items(fitted):
-        if not (DEVICE_SVC_OOF and all(hasattr(c, "steps") for c in fitted[:N_FOLDS])):
+        if not oof_items_ok(fitted):
             return None
         return [(k, fitted[k].steps[0][1].transform(X.index_select(0, test_idx[k])), test_idx[k])
                 for k in range(N_FOLDS) if test_idx[k].numel()]
@@ -604,7 +627,8 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
         return enqueue_svc_oof(st, items, meta, col)
 
     y64 = y.to(torch.float64)
-    stc.update(oof=oof, oof_svc_dev=oof_svc_dev if group is None else None, oof_items=oof_items, y64=y64)
+    stc.update(oof=oof, oof_svc_dev=oof_svc_dev if group is None else None, oof_items=oof_items,
+               oof_items_ok=oof_items_ok, y64=y64)
     _hmk("stack_prep")
 
     def new_final():
