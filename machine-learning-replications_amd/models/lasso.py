@@ -389,12 +389,15 @@ class SelectFromModel(Estimator):
                     if cd is not None:
                         self.cols_dev_ = self._device_columns(cd, int(cd.shape[0]))
                         # the host copy for the caller's check, read right behind the columns
-                        # (pinned + event: the check waits for them, not for later work)
-                        h = torch.empty(self.cols_dev_.shape, dtype=self.cols_dev_.dtype, pin_memory=True)
-                        h.copy_(self.cols_dev_, non_blocking=True)
-                        hev = torch.cuda.Event()
-                        hev.record()
-                        self.cols_host_ = (h, hev)
+                        # (pinned + event), on a pool stream
+                        from .. import runtime
+                        main = torch.cuda.current_stream(cd.device)
+                        cs = runtime.stream(cd.device, "lasso_refit")
+                        cs.wait_stream(main)
+                        from ..utils.hostread import stage
+                        with torch.cuda.stream(cs):
+                            self.cols_host_ = stage(self.cols_dev_, cs)   # (polled: utils.hostread)
+                        self.cols_dev_.record_stream(cs)
                     from ..utils.timing import hmark
                     hmark("cols_dev")
                 if user_early is not None:

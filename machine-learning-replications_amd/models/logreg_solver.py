@@ -153,10 +153,8 @@ def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=N
     parts = ([h["err"]] if h["err"] is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
     if parts:
         dv = torch.cat(parts)
-        host = torch.empty(dv.shape, dtype=dv.dtype, pin_memory=True)
-        host.copy_(dv, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        from ..utils.hostread import stage
+        host, ev = stage(dv)
         h["staged"] = (host, ev, dv)
     return h
 
@@ -176,8 +174,8 @@ def _finish_fused(h):
     parts = ([err] if err is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
     st = h.get("staged")
     if st is not None and st[2].numel() == sum(int(p.numel()) for p in parts):
-        st[1].synchronize()
-        host = st[0].tolist()
+        from ..utils.hostread import landed
+        host = landed(st[0], st[1]).tolist()
     else:
         host = torch.cat(parts).cpu().tolist() if parts else []
     hmark("lr_host_read")

@@ -29,6 +29,8 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from ..utils.hostread import landed   # early read-backs polled on their data
+
 TAU = 1e-12
 INT_MAX = np.iinfo(np.int32).max
 
@@ -1464,6 +1466,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                      + ([err.to(f64).reshape(-1).abs().max().reshape(1)] if err is not None else []))
             early_dev = torch.cat(parts)
             early_host = torch.empty(early_dev.shape, dtype=f64, pin_memory=True)
+            early_host.fill_(float("nan"))     # (finite once landed: polled by finish_svc_batch)
             early_host.copy_(early_dev, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -1600,6 +1603,7 @@ class _GammaDev:
                             ops.stream_ptr(device))
         # read back right behind its kernel (pinned + event): resolve() waits for γ, not for the SMO
         self.host = torch.empty(K, dtype=torch.float64, pin_memory=True)
+        self.host.fill_(float("nan"))     # (polled by resolve: see landed)
         self.host.copy_(self.gam, non_blocking=True)
         self.ev = torch.cuda.Event()
         self.ev.record()
@@ -1614,8 +1618,9 @@ class _GammaDev:
 
     def resolve(self, all_probs, meta) -> None:
         """The host's γ (models, host mirrors): one small read, queued when γ was computed."""
-        self.ev.synchronize()
-        g = self.host.numpy().copy()
+        # (γ is finite unless the scaled rows are not: a non-finite γ waits out landed's budget,
+        # then the event, then raises below)
+        g = landed(self.host, self.ev).copy()
         if not np.isfinite(g).all():
             from ..utils.guards import NonFiniteError
             raise NonFiniteError("SVC.fit X: non-finite scaled value(s)")
@@ -1797,6 +1802,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         # the pairs' read-back queued right behind the Platt kernel (pinned, with an event): the host
         # waits for the Platt fits only, not for whatever is enqueued on this stream after them
         ab_host = torch.empty(ABt.shape, dtype=torch.float64, pin_memory=True)
+        ab_host.fill_(float("nan"))
         ab_host.copy_(ABt, non_blocking=True)
         ab_ev = torch.cuda.Event()
         ab_ev.record()
@@ -1927,9 +1933,8 @@ def finish_svc_batch(st: dict, defer=None):
     from ..utils.timing import hmark
     if early is not None:
         hmark("svc_early_wait")
-        early["ev"].synchronize()
+        host_e = landed(early["host"], early["ev"])
         hmark("svc_early_synced")
-        host_e = early["host"].numpy()
         smo_failed = early["has_err"] and host_e[-1] != 0.0
     else:
         err = sol.get("smo_err")
@@ -2003,8 +2008,7 @@ def finish_svc_batch(st: dict, defer=None):
         if st["ABt"] is None:
             return
         if early is not None and st.get("ab_host") is not None:
-            st["ab_host"][1].synchronize()
-            ABc = st["ab_host"][0].numpy()
+            ABc = landed(*st["ab_host"])
         elif early is not None:
             ABc = st["ABt"].to(torch.float64).cpu().numpy()
         else:

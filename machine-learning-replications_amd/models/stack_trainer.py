@@ -841,6 +841,8 @@ def finish_prelaunched(pre: dict, timer: StageTimer = None) -> None:
 def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None, group=None, svc_group=None,
                  plan=None):
     pre = plan.get("prelaunch") if (plan is not None and group is None) else None
+    from ..utils.timing import hmark
+    hmark("stack_check_in")
     if pre is not None:
         # the stack was enqueued from the device column selection (prelaunch_stack): it is this
         # fit's only if the host's selection agrees (a speculation on the smallest alpha can miss)
@@ -848,11 +850,11 @@ def fit_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = None
         LAST_PRELAUNCH["speculative"] = bool(pre.get("speculative"))
         ch = pre.get("cols_host")
         if ch is not None:
-            ch[1].synchronize()
-            cdev = ch[0].numpy()
+            from ..utils.hostread import landed
+            cdev = landed(ch[0], ch[1]).copy()
+            hmark("cols_synced")
         else:
             cdev = pre["cols_dev"].cpu().numpy()
-        from ..utils.timing import hmark
         hmark("stack_checked")
         if cols is None or not np.array_equal(cdev, np.asarray(cols, dtype=np.int64)):
             if pre.get("speculative"):

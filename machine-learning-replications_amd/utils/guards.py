@@ -70,10 +70,8 @@ class Deferred:
         if not len(self) or not self._flags + self._words or not (self._words + self._flags)[0].is_cuda:
             return
         dev = torch.cat(self._words + self._flags)
-        host = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
-        host.copy_(dev, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        from .hostread import stage
+        host, ev = stage(dev)
         self._staged = (host, ev, len(self._words), len(self._flags), dev)
 
     def flag(self, t: torch.Tensor, kind: str, what: str) -> None:
@@ -93,8 +91,8 @@ class Deferred:
         st = self._staged
         self._staged = None
         if st is not None and st[2] == len(self._words) and st[3] == len(self._flags):
-            st[1].synchronize()
-            host = st[0].tolist()
+            from .hostread import landed
+            host = landed(st[0], st[1]).tolist()
         else:
             host = torch.cat(self._words + self._flags).cpu().tolist()
         nw = len(self._words)
