@@ -19,6 +19,10 @@ for line in open(path):
 dev, host = dev[skip:], host[skip:]
 keys = ["lasso_spec", "svc_parts_done", "svc_smo_done", "svc_platt", "svc_oof", "lr_kernel", "gbc_done", "lasso_cv_path", "meta", "stack_fit"]
 print(f"fits {len(dev)} dev medians: " + " ".join(f"{k}={median(d[k] for d in dev if k in d):.2f}" for k in keys if any(k in d for d in dev)))
+if all("svc_platt_dec" in d and "svc_smo_done" in d for d in dev):
+    print(f"tail medians: dec {median(d['svc_platt_dec'] - d['svc_smo_done'] for d in dev):.3f} "
+          f"platt {median(d['svc_platt'] - d['svc_platt_in'] for d in dev):.3f} "
+          f"smo→stack_fit {median(d['stack_fit'] - d['svc_smo_done'] for d in dev):.3f}")
 hk = ["develop", "lasso_spec_launched", "svc_cascade_seeded", "ws_groups_ready", "svc_solve_enqueued", "lasso_best_read", "svc_host_read"]
 print("host medians (ms after develop): " + " ".join(
     f"{k}={median(h[k] - h['develop'] for h in host if k in h and 'develop' in h):.2f}" for k in hk[1:] if any(k in h for h in host)))
