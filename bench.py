@@ -203,7 +203,10 @@ def _ws_critical(st):
             "kcyc_select": round(float(st["cyc_select"][k]) / 1e3, 1),
             "kcyc_build": round(float(st["cyc_build"][k]) / 1e3, 1),
             "kcyc_inner": round(float(st["cyc_inner"][k]) / 1e3, 1),
-            "cyc_per_pair": round(float(st["cyc_inner"][k]) / pairs)}
+            "cyc_per_pair": round(float(st["cyc_inner"][k]) / pairs),
+            # shader clock of the inner phase: s_memtime cycles per 100 MHz s_memrealtime tick
+            "inner_clock_ghz": (round(float(st["cyc_inner"][k]) / float(st["cyc_p2"][k]) * 0.1, 3)
+                                if float(st["cyc_p2"][k]) > 0 else None)}
 
 
 def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):

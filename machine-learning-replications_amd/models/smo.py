@@ -721,9 +721,13 @@ WS_INNER_FRAC_BIG = float(os.environ.get("HFENS_SVM_WS_FRAC_BIG", str(WS_INNER_F
 # in its next working set)
 WS_MAX_INNER = int(os.environ.get("HFENS_SVM_WS_INNER", "4096"))
 WS_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_AHEAD", "64"))      # rounds enqueued without a host check
-# … for a cascade-seeded batch (the bench's seeded problems need ≤ 24 rounds; every round past a
-# problem's convergence is three no-op launches its group's stream still runs before the finish)
-WS_SEEDED_AHEAD = int(os.environ.get("HFENS_SVM_WS_SEEDED_AHEAD", "48"))
+# … for a cascade-seeded batch, per 10k points of its largest problem (scaled up above 10k): the
+# bench's seeded problems need ≤ 24 rounds, and every round past a problem's convergence is three
+# no-op launches its group's stream still runs before the finish — measured (profiles/r6_runs/r6av,
+# traced medians on one box): SMO done 15.2–15.4 ms at 48 rounds ahead, 14.8 at 32, 14.7 at 28.  A
+# batch that needs more rounds reports err and is re-solved with host-checked rounds (correct,
+# slower: tests/test_svm_ws_gpu.py)
+WS_SEEDED_AHEAD = int(os.environ.get("HFENS_SVM_WS_SEEDED_AHEAD", "32"))
 # the K-cached solver's rounds are ~4× as many (q = 256): on the bench's 10k-point problem ≈ 190
 WS_KC_ROUNDS_AHEAD = int(os.environ.get("HFENS_SVM_WS_KC_AHEAD", "288"))
 # HIP-graph replay of the rounds: "1" K-cached rounds only, "all" the q = 1024 rounds too, "0" off.
@@ -818,7 +822,8 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
         keys = torch.zeros(2 * n, dtype=torch.int32, device=device)
         hist = torch.zeros(1, dtype=torch.int32, device=device)   # (unused slot kept in the ABI)
     runs = []
-    ahead = WS_KC_ROUNDS_AHEAD if kc_all else (WS_SEEDED_AHEAD if seed is not None else WS_ROUNDS_AHEAD)
+    ahead = (WS_KC_ROUNDS_AHEAD if kc_all else
+             (-(-WS_SEEDED_AHEAD * max(ml, 10000) // 10000) if seed is not None else WS_ROUNDS_AHEAD))
     left = min(ahead, max_outer)
     chunk = WS_GRAPH_CHUNK if use_graph else _WS_ENQ_CHUNK
     done = [0] * len(groups)

@@ -553,6 +553,7 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
   }
   __syncthreads();
   const long long c2 = __builtin_amdgcn_s_memtime();
+  const long long r2 = __builtin_amdgcn_s_memrealtime();   // (100 MHz: the inner phase's clock, diagnostics)
   bool valid[SL], pos[SL];
   int tt[SL];
   // yg = y·G (the solver's natural variable: keys −yG / yG, gd = GmaxB + yG, and the update
@@ -807,9 +808,11 @@ __global__ __launch_bounds__(TH) void ws_solve_kernel(
     wdc[(size_t)b * Q + p] = 0.f;
   }
   const long long c3 = __builtin_amdgcn_s_memtime();
+  const long long r3 = __builtin_amdgcn_s_memrealtime();
   if (tid == 0) {
     S->cyc_build += c2 - c1;
     S->cyc_inner += c3 - c2;
+    S->cyc_p2 += r3 - r2;   // (the selector's third sub-phase slot is unused: real-time ticks of the inner phase)
     // no pair moved: the f32 selection keys hid an f64 violation below eps-resolution — done
     if (it == 0 || nc == 0) S->done = 1;
     S->nc = nc;
