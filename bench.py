@@ -201,6 +201,8 @@ def _ws_critical(st):
     pairs = max(int(st["inner"][k]), 1)
     return {"rounds": int(st["outer"][k]), "pairs": pairs,
             "kcyc_select": round(float(st["cyc_select"][k]) / 1e3, 1),
+            "kcyc_select_keys": round(float(st["cyc_p0"][k]) / 1e3, 1),      # key loads, counts, gap test
+            "kcyc_select_pick": round(float(st["cyc_p1"][k]) / 1e3, 1),      # radix histograms + compaction
             "kcyc_build": round(float(st["cyc_build"][k]) / 1e3, 1),
             "kcyc_inner": round(float(st["cyc_inner"][k]) / 1e3, 1),
             "cyc_per_pair": round(float(st["cyc_inner"][k]) / pairs),

@@ -741,6 +741,9 @@ _WS_GRAPHS: dict = {}
 WS_BIG_CHUNK = int(os.environ.get("HFENS_SVM_WS_BIG_CHUNK", "64"))
 WS_THREADS = int(os.environ.get("HFENS_SVM_WS_THREADS", "256"))      # inner-solver workgroup (256 or 512)
 WS_G0_FIRST = os.environ.get("HFENS_SVM_WS_G0_FIRST", "1") == "1"
+# the last (smallest-problem) group on a side stream of its own (runtime FIT_STREAMS svc_ws_2, normal
+# priority) instead of the caller's high-priority stream
+WS_LAST_SIDE = os.environ.get("HFENS_SVM_WS_LAST_SIDE", "0") == "1"
 _WS_SYNC = [False]   # set while re-solving a batch that did not converge within WS_ROUNDS_AHEAD
 
 
@@ -833,7 +836,7 @@ def _solve_ws(E, live, zcat, zoffs, aoffs, F, device, eps, max_iter_cap, s, step
     for gi, idx in enumerate(groups):
         # the last (smallest) group on the caller's stream, the others on process-lifetime side streams
         side = None
-        if gi == len(groups) - 1:
+        if gi == len(groups) - 1 and not (WS_LAST_SIDE and cuda and gi > 0):
             st = s
         else:
             from .. import runtime

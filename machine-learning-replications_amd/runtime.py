@@ -18,6 +18,8 @@ from typing import Dict, Tuple
 
 import threading
 
+import os
+
 import torch
 
 _STREAMS: Dict[Tuple[torch.device, str], torch.cuda.Stream] = {}
@@ -41,7 +43,15 @@ def stream(device, role: str, priority: int = 0) -> "torch.cuda.Stream":
 # Measured (profiles/r5_headline.md): enqueuing the SVC batch earlier changed that order and cost
 # the SMO 3-5 ms; creating every role here first keeps the measured-good assignment whatever the
 # code path.
-FIT_STREAMS = (("aux", 0), ("lasso_refit", 0), ("svc", -1), ("bases", 0), ("svc_ws_0", -1), ("svc_ws_1", -1))
+# (svc_ws_1, the 8k-point problems' working-set group, at normal priority: the critical group's
+# launches then dispatch ahead of its — measured 16.4 / 16.7 vs 17.1 / 17.0 ms per fit on one box,
+# profiles/r6_runs/r6az; svc_ws_2: the smallest group's own stream when smo.WS_LAST_SIDE)
+FIT_STREAMS = (("aux", 0), ("lasso_refit", 0), ("svc", -1), ("bases", 0), ("svc_ws_0", -1),
+               ("svc_ws_1", int(os.environ.get("HFENS_WS1_PRIORITY", "0"))))
+if os.environ.get("HFENS_SVM_WS_LAST_SIDE", "0") == "1":
+    # (measured slower at either priority: the extra stream shared a hardware queue with the GBC /
+    # LassoCV streams, or slowed the SMO — profiles/r6_runs/r6ba, r6bb)
+    FIT_STREAMS += (("svc_ws_2", int(os.environ.get("HFENS_WS2_PRIORITY", "0"))),)
 
 
 def init_fit_streams(device) -> None:
