@@ -46,9 +46,10 @@ def stream(device, role: str, priority: int = 0) -> "torch.cuda.Stream":
 # (svc_ws_1, the 8k-point problems' working-set group, at normal priority: the critical group's
 # launches then dispatch ahead of its — measured 16.4 / 16.7 vs 17.1 / 17.0 ms per fit on one box,
 # profiles/r6_runs/r6az; svc_ws_2: the smallest group's own stream when smo.WS_LAST_SIDE)
-FIT_STREAMS = (("aux", 0), ("lasso_refit", 0), ("svc", -1), ("bases", 0), ("svc_ws_0", -1),
+FIT_STREAMS = (("aux", 0), ("lasso_refit", 0), ("svc", int(os.environ.get("HFENS_SVC_PRIORITY", "-1"))), ("bases", 0),
+               ("svc_ws_0", -1),
                ("svc_ws_1", int(os.environ.get("HFENS_WS1_PRIORITY", "0"))))
-if os.environ.get("HFENS_SVM_WS_LAST_SIDE", "0") == "1":
+if os.environ.get("HFENS_SVM_WS_LAST_SIDE", "0") == "1" and os.environ.get("HFENS_SVM_WS_GROUPS", "3") != "2":
     # (measured slower at either priority: the extra stream shared a hardware queue with the GBC /
     # LassoCV streams, or slowed the SMO — profiles/r6_runs/r6ba, r6bb)
     FIT_STREAMS += (("svc_ws_2", int(os.environ.get("HFENS_WS2_PRIORITY", "0"))),)
