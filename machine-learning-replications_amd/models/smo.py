@@ -1499,8 +1499,10 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
     if pre_dec is not None:
         pdd = pre_dec
         dmark("svc_smo_done")
-        E.svm_dec_batch(zcat.data_ptr(), coef.data_ptr(), pdd["hcat"].data_ptr(), F, pdd["ddev"].data_ptr(),
-                        len(pdd["dt"]), int(pdd["dt"]["h"].max()), pdd["S"], pdd["part"].data_ptr(), s)
+        zsv, csv, cnt = _sv_compact(E, zcat, coef, F, pdd["ddev"], len(pdd["dt"]), device, s)
+        E.svm_dec_batch(zsv.data_ptr(), csv.data_ptr(), pdd["hcat"].data_ptr(), F, pdd["ddev"].data_ptr(),
+                        len(pdd["dt"]), int(pdd["dt"]["h"].max()), pdd["S"], pdd["part"].data_ptr(),
+                        cnt.data_ptr() if cnt is not None else 0, s)
         if pdd["oof"]:
             out["oof_pre"] = dict(ids=[(f, id(Zt)) for f, Zt in pdd["oi"]], part=pdd["part"], hoff0=pdd["hoff_platt"],
                                   hoff=pdd["hoff"] - pdd["hoff_platt"])
@@ -1508,7 +1510,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
         # the decision values are assembled inside the Platt kernel from these partials (row r of
         # part: problem rowk[r]'s held-out point, d = −(Σ part[r] − ρ))
         out["platt_src"] = dict(part=pdd["part"], S=pdd["S"], rowk=pdd["rowk"],
-                                rho=rho_pl.to(torch.float64).contiguous(), keep=(pdd["hcat"], pdd["ddev"]))
+                                rho=rho_pl.to(torch.float64).contiguous(), keep=(pdd["hcat"], pdd["ddev"], zsv, csv, cnt))
     return out
 
 
@@ -1889,12 +1891,33 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
         deps["wait"](cur, ks)
         coef = (dec_state["sign"] * dec_state["alpha"].to(torch.float32)).contiguous()
         rho_src = deps["rho_for"](cur, ks)
-    E.svm_dec_batch(dec_state["zcat"].data_ptr(), coef.data_ptr(), hcat.data_ptr(), dec_state["F"],
-                    ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(), s)
+    zsv, csv, cnt = _sv_compact(E, dec_state["zcat"], coef, dec_state["F"], ddev, len(items), device, s)
+    E.svm_dec_batch(zsv.data_ptr(), csv.data_ptr(), hcat.data_ptr(), dec_state["F"],
+                    ddev.data_ptr(), len(items), int(max(hs)), S, part.data_ptr(),
+                    cnt.data_ptr() if cnt is not None else 0, s)
     dec = part.to(torch.float64).sum(1).contiguous()
     return _svc_oof_tail(st, items, finals, dec, hs, meta, col, device,
                          rho_src.index_select(0, _to_dev(np.asarray(ks, dtype=np.int64), device)).contiguous()
-                         if rho_src is not None else None, (hcat, part, ddev, coef))
+                         if rho_src is not None else None, (hcat, part, ddev, coef, zsv, csv, cnt))
+
+
+# the decision launches read only each problem's support vectors (svm_sv_compact: ≈ 45 % of the
+# points on the bench's problems; the skipped terms are exact zeros, the f32 partials group
+# differently)
+DEC_COMPACT = os.environ.get("HFENS_SVC_DEC_COMPACT", "1") != "0"
+
+
+def _sv_compact(E, zcat, coef, F, ddev, P, device, s):
+    """(rows, coefficients, per-problem counts) for a decision launch: the support vectors of every
+    decision problem compacted in place of its points (same offsets), or the inputs unchanged."""
+    if not DEC_COMPACT:
+        return zcat, coef, None
+    zc = torch.empty_like(zcat)
+    cc = torch.empty_like(coef)
+    cnt = torch.empty(P, dtype=torch.int32, device=device)
+    E.svm_sv_compact(zcat.data_ptr(), coef.data_ptr(), F, ddev.data_ptr(), P, zc.data_ptr(), cc.data_ptr(),
+                     cnt.data_ptr(), s)
+    return zc, cc, cnt
 
 
 def _svc_oof_tail(st, items, finals, dec, hs, meta, col, device, rho, keep) -> bool:

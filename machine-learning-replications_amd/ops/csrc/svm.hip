@@ -470,18 +470,72 @@ struct DecProb {
   int per;          // SVs per split (multiple of 32)
 };
 
+// Support-vector compaction ahead of the decisions: problem p's rows with a non-zero coefficient
+// (y·α ≠ 0; ≈ 45 % of the points on the bench's problems), in their original order, copied to the
+// same offsets of zc / cc, their count to counts[p].  One 1024-thread workgroup per problem: a
+// ballot + wave-prefix compaction per 1024-point chunk.  The decision terms of the skipped points
+// are exact zeros, so only the grouping of the f32 partial sums changes.
+__global__ __launch_bounds__(1024) void svm_sv_compact_kernel(const float* __restrict__ zcat,
+                                                             const float* __restrict__ coef, int F,
+                                                             const DecProb* __restrict__ probs,
+                                                             float* __restrict__ zc, float* __restrict__ cc,
+                                                             int* __restrict__ counts) {
+  const DecProb P = probs[blockIdx.x];
+  __shared__ int wtot[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int base = 0;
+  for (int c0 = 0; c0 < P.l; c0 += 1024) {
+    const int t = c0 + threadIdx.x;
+    const float cf = t < P.l ? coef[P.zoff + t] : 0.f;
+    const bool sv = cf != 0.f;
+    const unsigned long long bal = __ballot(sv);
+    if (lane == 0) wtot[wave] = __popcll(bal);
+    __syncthreads();
+    int wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const int v = wtot[w];
+      wb += w < wave ? v : 0;
+      tot += v;
+    }
+    if (sv) {
+      const long long pos = P.zoff + base + wb + __popcll(bal & ((1ull << lane) - 1ull));
+      const float* src = zcat + (P.zoff + t) * F;
+      float* dst = zc + pos * F;
+      for (int k = 0; k < F; ++k) dst[k] = src[k];
+      cc[pos] = cf;
+    }
+    base += tot;
+    __syncthreads();   // wtot is rewritten by the next chunk
+  }
+  if (threadIdx.x == 0) counts[blockIdx.x] = base;
+}
+
+void svm_sv_compact(uintptr_t zcat, uintptr_t coef, int F, uintptr_t probs, int P, uintptr_t zc, uintptr_t cc,
+                    uintptr_t counts, uintptr_t stream) {
+  HFENS_REQUIRE(F >= 1 && F <= 64 && P >= 0, "svm_sv_compact: 1 <= F <= 64");
+  if (P == 0) return;
+  hipLaunchKernelGGL(svm_sv_compact_kernel, dim3(P), dim3(1024), 0, as_stream(stream), (const float*)zcat,
+                     (const float*)coef, F, (const DecProb*)probs, (float*)zc, (float*)cc, (int*)counts);
+  launch_check();
+}
+
 template <int KS>
 __global__ __launch_bounds__(256) void svm_dec_batch_kernel(const float* __restrict__ zcat,
                                                             const float* __restrict__ coef,
                                                             const float* __restrict__ hcat, int F,
                                                             const DecProb* __restrict__ probs,
-                                                            int S, float* __restrict__ part) {
+                                                            int S, float* __restrict__ part,
+                                                            const int* __restrict__ counts) {
   const DecProb P = probs[blockIdx.z];
   const int row0 = blockIdx.x * 128;
   const int s = blockIdx.y;
   const int t_begin = s * P.per;
-  if (row0 >= P.h || t_begin >= P.l) return;
-  const int t_end = min(P.l, t_begin + P.per);
+  // (counts: the compacted support vectors of each problem, svm_sv_compact; splits past them write
+  // nothing — the caller's partials are zero-filled)
+  const int L = counts != nullptr ? min(counts[blockIdx.z], P.l) : P.l;
+  if (row0 >= P.h || t_begin >= L) return;
+  const int t_end = min(L, t_begin + P.per);
   constexpr int CH = 256;
   __shared__ __attribute__((aligned(16))) float sv_l[2 * KS][CH];
   __shared__ __attribute__((aligned(16))) float sn_l[CH];
@@ -538,7 +592,7 @@ __global__ __launch_bounds__(256) void svm_dec_batch_kernel(const float* __restr
 }
 
 void svm_dec_batch(uintptr_t zcat, uintptr_t coef, uintptr_t hcat, int F, uintptr_t probs, int P,
-                   int max_h, int S, uintptr_t part, uintptr_t stream) {
+                   int max_h, int S, uintptr_t part, uintptr_t counts, uintptr_t stream) {
   HFENS_REQUIRE(F >= 1 && F <= 64, "svm_dec_batch: 1 <= F <= 64");
   dim3 grid((max_h + 127) / 128, S, P);
   const int ks = (F + 1) / 2;
@@ -547,7 +601,7 @@ void svm_dec_batch(uintptr_t zcat, uintptr_t coef, uintptr_t hcat, int F, uintpt
   if (ks <= KS_) {                                                                               \
     hipLaunchKernelGGL(svm_dec_batch_kernel<KS_>, grid, dim3(256), 0, st, (const float*)zcat,    \
                        (const float*)coef, (const float*)hcat, F, (const DecProb*)probs, S,      \
-                       (float*)part);                                                            \
+                       (float*)part, (const int*)counts);                                        \
     launch_check();                                                                              \
     return;                                                                                      \
   }
