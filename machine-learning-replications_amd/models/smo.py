@@ -1806,8 +1806,12 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         dmark("svc_platt_in")
         part_p, S, rowk_p, rho_p = ((src["part"].data_ptr(), src["S"], src["rowk"].data_ptr(), src["rho"].data_ptr())
                                     if src is not None else (0, 0, 0, 0))   # (every fold degenerate)
+        # (PLATT_COOP: every fit's points over 8 workgroups meeting at a counter per Newton pass)
+        cbar = torch.zeros(len(pl), dtype=torch.int32, device=device) if PLATT_COOP else None
+        cpart = torch.empty(len(pl) * 2 * 8 * 6, dtype=torch.float64, device=device) if PLATT_COOP else None
         E.platt_batch(pdev.data_ptr(), len(pl), part_p, S, rowk_p, rho_p, cdev.data_ptr(), srcmap.data_ptr(),
-                      dscr.data_ptr(), ABt.data_ptr(), ops.stream_ptr(device))
+                      dscr.data_ptr(), ABt.data_ptr(), cbar.data_ptr() if PLATT_COOP else 0,
+                      cpart.data_ptr() if PLATT_COOP else 0, ops.stream_ptr(device))
         dmark("svc_platt")
         # the pairs' read-back queued right behind the Platt kernel (pinned, with an event): the host
         # waits for the Platt fits only, not for whatever is enqueued on this stream after them
@@ -1818,7 +1822,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         ab_ev.record()
         return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
                     ab_host=(ab_host, ab_ev),
-                    keep=(pdev, srcmap, cdev, dscr), device=device, args=args, solver=solver, gamma_dev=gdev)
+                    keep=(pdev, srcmap, cdev, dscr, cbar, cpart), device=device, args=args, solver=solver, gamma_dev=gdev)
     for f in pl:
         svc, Z, mt = svcs[f], Zs[f], meta[f]
         l = mt["l"]
@@ -1905,6 +1909,8 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
 # points on the bench's problems; the skipped terms are exact zeros, the f32 partials group
 # differently)
 DEC_COMPACT = os.environ.get("HFENS_SVC_DEC_COMPACT", "1") != "0"
+# the Platt sigmoid fits with each fit's points over 8 workgroups (svm.hip platt_coop_kernel)
+PLATT_COOP = os.environ.get("HFENS_PLATT_COOP", "1") != "0"
 
 
 def _sv_compact(E, zcat, coef, F, ddev, P, device, s):

@@ -758,15 +758,136 @@ __global__ __launch_bounds__(kPlattThreads) void platt_kernel(const PlattProb* _
   if (tid == 0) { AB[2 * blockIdx.x] = A; AB[2 * blockIdx.x + 1] = B; }
 }
 
+// The same Newton loop with each fit's points split over NWG workgroups (the single-workgroup kernel
+// runs six fits on six CUs, its passes bound by one CU's f64 exp / log throughput).  Per pass every
+// workgroup reduces its own points, publishes the six sums in a parity slot and meets the fit's other
+// workgroups at a counter (vector atomics, agent scope); every workgroup then adds the NWG partials in
+// workgroup order — the same sums, hence the same iterates, in every workgroup; workgroup 0 writes
+// (A, B).  A counter wait past kPlattCoopDeadline (10 ms: workgroups not co-resident) turns that
+// workgroup into a solo one that sums all the fit's points itself from then on — slower, same result
+// up to the summation order, never stuck.
+constexpr int kPlattCoopWgs = 8;
+constexpr long long kPlattCoopDeadline = 1000000;   // 100 MHz real-time ticks
+
+template <int NWG>
+__global__ __launch_bounds__(kPlattThreads) void platt_coop_kernel(const PlattProb* __restrict__ probs,
+                                                                   const float* __restrict__ part, int S,
+                                                                   const int* __restrict__ rowk,
+                                                                   const double* __restrict__ rho,
+                                                                   const double* __restrict__ consts,
+                                                                   const int* __restrict__ srcmap,
+                                                                   double* __restrict__ AB, int* __restrict__ bar,
+                                                                   double* __restrict__ cpart) {
+  constexpr int R = (kPlattReg + NWG - 1) / NWG;   // register slots per thread for this workgroup's chunk
+  const int g = blockIdx.x, fit = blockIdx.y;
+  const PlattProb P = probs[fit];
+  if (P.l > R * kPlattThreads * NWG || P.l > kPlattReg * kPlattThreads) return;   // (the scratch kernel's fits)
+  __shared__ double red[2 * kPlattWaves * 6];
+  __shared__ int s_solo;
+  const int tid = threadIdx.x;
+  const int chunk = (P.l + NWG - 1) / NWG;
+  const int lo = g * chunk, hi = min(P.l, lo + chunk);
+  auto value = [&](int i) {
+    const int code = srcmap[P.off + i];
+    if (code < 0) return consts[-1 - code];
+    double sum = 0.0;
+    for (int j = 0; j < S; ++j) sum += (double)part[(size_t)code * S + j];
+    return -(sum - rho[rowk[code]]);
+  };
+  double dr[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = lo + tid + k * kPlattThreads;
+    dr[k] = i < hi ? value(i) : 0.0;
+  }
+  if (tid == 0) s_solo = 0;
+  __syncthreads();
+  const double prior1 = P.n0, prior0 = P.l - P.n0;
+  const int max_iter = 100;
+  const double min_step = 1e-10, sigma = 1e-12, eps = 1e-5;
+  const double hiT = (prior1 + 1.0) / (prior1 + 2.0), loT = 1 / (prior0 + 2.0);
+  int parity = 0, npass = 0;
+  bool solo = false;
+  auto pass = [&](double a, double b) {
+    PlattSums acc{0, 0, 0, 0, 0, 0};
+    if (!solo) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int i = lo + tid + k * kPlattThreads;
+        if (i < hi) platt_point(dr[k], i < P.n0 ? hiT : loT, a, b, acc);
+      }
+      const PlattSums loc = platt_block_sum(acc, red, parity);
+      double* slot = cpart + ((size_t)(fit * 2 + (npass & 1)) * NWG) * 6;
+      if (tid == 0) {
+        const double v[6] = {loc.f, loc.h11, loc.h22, loc.h21, loc.g1, loc.g2};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) __hip_atomic_store(slot + g * 6 + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        __hip_atomic_fetch_add(bar + fit, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const int target = (npass + 1) * NWG;
+        const long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(bar + fit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kPlattCoopDeadline) { s_solo = 1; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();
+      }
+      __syncthreads();
+      ++npass;
+      if (!s_solo) {
+        double o[6] = {0, 0, 0, 0, 0, 0};
+        for (int q = 0; q < NWG; ++q) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) o[k] += __hip_atomic_load(slot + q * 6 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return PlattSums{o[0], o[1], o[2], o[3], o[4], o[5]};
+      }
+      solo = true;
+      acc = PlattSums{0, 0, 0, 0, 0, 0};
+    }
+    // solo: every point of the fit, values re-assembled from the partials
+    for (int i = tid; i < P.l; i += kPlattThreads) platt_point(value(i), i < P.n0 ? hiT : loT, a, b, acc);
+    return platt_block_sum(acc, red, parity);
+  };
+  double A = 0.0, B = log((prior0 + 1.0) / (prior1 + 1.0));
+  PlattSums v = pass(A, B);
+  double fval = v.f;
+  for (int it = 0; it < max_iter; ++it) {
+    const double h11 = v.h11 + sigma, h22 = v.h22 + sigma, h21 = v.h21, g1 = v.g1, g2 = v.g2;
+    if (fabs(g1) < eps && fabs(g2) < eps) break;
+    const double det = h11 * h22 - h21 * h21;
+    const double dA = -(h22 * g1 - h21 * g2) / det;
+    const double dB = -(-h21 * g1 + h11 * g2) / det;
+    const double gd = g1 * dA + g2 * dB;
+    double step = 1;
+    while (step >= min_step) {
+      const double nA = A + step * dA, nB = B + step * dB;
+      const PlattSums w = pass(nA, nB);
+      if (w.f < fval + 0.0001 * step * gd) { A = nA; B = nB; fval = w.f; v = w; break; }
+      step = step / 2.0;
+    }
+    if (step < min_step) break;
+  }
+  if (tid == 0 && g == 0) { AB[2 * fit] = A; AB[2 * fit + 1] = B; }
+}
+
 void platt_batch(uintptr_t probs, int P, uintptr_t part, int S, uintptr_t rowk, uintptr_t rho,
-                 uintptr_t consts, uintptr_t srcmap, uintptr_t dec, uintptr_t AB, uintptr_t stream) {
+                 uintptr_t consts, uintptr_t srcmap, uintptr_t dec, uintptr_t AB, uintptr_t coop_bar,
+                 uintptr_t coop_part, uintptr_t stream) {
   HFENS_REQUIRE(P >= 1 && S >= 0, "platt_batch: P >= 1, S >= 0");
   hipStream_t st = as_stream(stream);
   // two launches on one stream, each skipping the other's fits: register-resident values for
-  // fits of ≤ 16k points, the global scratch beyond
-  hipLaunchKernelGGL(platt_kernel<true>, dim3(P), dim3(kPlattThreads), 0, st, (const PlattProb*)probs,
-                     (const float*)part, S, (const int*)rowk, (const double*)rho, (const double*)consts,
-                     (const int*)srcmap, (double*)dec, (double*)AB);
+  // fits of ≤ 16k points (split over kPlattCoopWgs workgroups each when coop_bar is given: a zeroed
+  // int[P] counter array and a double[P][2][kPlattCoopWgs][6] partial buffer), the global scratch beyond
+  if (coop_bar != 0) {
+    hipLaunchKernelGGL(platt_coop_kernel<kPlattCoopWgs>, dim3(kPlattCoopWgs, P), dim3(kPlattThreads), 0, st,
+                       (const PlattProb*)probs, (const float*)part, S, (const int*)rowk, (const double*)rho,
+                       (const double*)consts, (const int*)srcmap, (double*)AB, (int*)coop_bar, (double*)coop_part);
+  } else {
+    hipLaunchKernelGGL(platt_kernel<true>, dim3(P), dim3(kPlattThreads), 0, st, (const PlattProb*)probs,
+                       (const float*)part, S, (const int*)rowk, (const double*)rho, (const double*)consts,
+                       (const int*)srcmap, (double*)dec, (double*)AB);
+  }
   launch_check();
   hipLaunchKernelGGL(platt_kernel<false>, dim3(P), dim3(kPlattThreads), 0, st, (const PlattProb*)probs,
                      (const float*)part, S, (const int*)rowk, (const double*)rho, (const double*)consts,

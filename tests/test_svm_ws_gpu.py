@@ -112,13 +112,15 @@ def test_ws_unconverged_batch_is_resolved_synchronously(dev, monkeypatch):
     assert m._probA.item() == ref._probA.item() and m._probB.item() == ref._probB.item()
 
 
+@pytest.mark.parametrize("coop", [False, True])
 @pytest.mark.parametrize("ls", [[1500, 9000], [20000, 700]])
-def test_platt_kernel_matches_host_sigmoid_train(dev, ls):
+def test_platt_kernel_matches_host_sigmoid_train(dev, ls, coop):
     """platt_batch (svm.hip): each fit's decision values assembled in the kernel from f32 partials
     (d = −(Σ_s part[row][s] − ρ_k), per-fold constants, 0 for unmapped positions), then libsvm's
     sigmoid_train with one pass per Newton trial — against the host sigmoid_train on the same
     values summed in f64.  Fits ≤ 16k points keep the values in registers, larger ones in the
-    global scratch (both paths covered)."""
+    global scratch (both paths covered); ``coop``: the ≤ 16k fits split over 8 workgroups per fit
+    (platt_coop_kernel)."""
     from hfens import ops
     E = ops.ext()
     rng = np.random.default_rng(7)
@@ -148,8 +150,11 @@ def test_platt_kernel_matches_host_sigmoid_train(dev, ls):
                                                d(arr.view(np.uint8)))
     dscr = torch.empty(off, dtype=torch.float64, device=dev)
     AB = torch.empty(2 * len(ls), dtype=torch.float64, device=dev)
+    cbar = torch.zeros(len(ls), dtype=torch.int32, device=dev)
+    cpart = torch.empty(len(ls) * 2 * 8 * 6, dtype=torch.float64, device=dev)
     E.platt_batch(pdev.data_ptr(), len(ls), part_d.data_ptr(), S, rowk_d.data_ptr(), rho_d.data_ptr(),
-                  c_d.data_ptr(), map_d.data_ptr(), dscr.data_ptr(), AB.data_ptr(), ops.stream_ptr(dev))
+                  c_d.data_ptr(), map_d.data_ptr(), dscr.data_ptr(), AB.data_ptr(),
+                  cbar.data_ptr() if coop else 0, cpart.data_ptr() if coop else 0, ops.stream_ptr(dev))
     got = AB.cpu().numpy()
     for k, sm in enumerate(maps):
         dec = np.where(sm >= 0, -(part.astype(np.float64)[np.maximum(sm, 0)].sum(1) - rho[rowk[np.maximum(sm, 0)]]),
