@@ -162,9 +162,12 @@ def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=N
 def _launch_single(h):
     B, n, F1, Xc, sc, yc, penal, C, l1, max_outer, Z, Xd, W, iters = h["args"]
     LAST_PATH["members"] = 1
+    from ..utils.timing import dmark
+    dmark("lr_launch")
     ops.ext().logreg_fused(B, n, F1, Xc.data_ptr(), sc.data_ptr(), yc.data_ptr(), penal.data_ptr(), float(C),
                            int(l1), int(max_outer), Z.data_ptr(), Xd.data_ptr(), W.data_ptr(), iters.data_ptr(),
                            ops.stream_ptr(Xc.device))
+    dmark("lr_kernel")
 
 
 def _finish_fused(h):
@@ -186,6 +189,7 @@ def _finish_fused(h):
         warnings.warn("cooperative logistic regression timed out waiting for a member; re-solving with one "
                       "workgroup per model")
         LAST_PATH["coop_fallback"] = True
+        h["refit"] = True        # (models set at launch hold the failed solve's intercept copies)
         _launch_single(h)
     W, iters = h["args"][12], h["args"][13]
     return W, iters
@@ -281,12 +285,20 @@ def finish_logreg_batch(h: dict):
     guards), then ``set_fitted``; other paths finished inside the launch."""
     if "fused" not in h:
         return h["models"]
+    _finish_fused(h["fused"])
+    if not h.get("preset") or h["fused"].get("refit"):
+        _set_models(h)
+    return h["models"]
+
+
+def _set_models(h: dict) -> None:
+    """``set_fitted`` of a fused launch's models from its device solution (stream-ordered behind
+    the solve: valid to call before the solve has run)."""
     models, F, scale, fit_intercept, dev = h["models"], h["F"], h["scale"], h["fit_intercept"], h["dev"]
-    W, iters = _finish_fused(h["fused"])
+    W, iters = h["fused"]["args"][12], h["fused"]["args"][13]
     for b, m in enumerate(models):
         intercept = W[b, F] * scale if fit_intercept else torch.zeros((), dtype=torch.float64, device=dev)
         m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
-    return models
 
 
 def logreg_label_prep(models, y: torch.Tensor, n: int, device) -> dict:
@@ -315,11 +327,14 @@ def logreg_label_prep(models, y: torch.Tensor, n: int, device) -> dict:
 
 
 def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optional[torch.Tensor] = None,
-                        group=None, max_outer: int = 100, seed_order=None, prep: Optional[dict] = None) -> dict:
+                        group=None, max_outer: int = 100, seed_order=None, prep: Optional[dict] = None,
+                        preset: bool = False) -> dict:
     """Fit ``models`` (one per row mask); on the fused device path the solve is only enqueued —
     no host synchronisation until :func:`finish_logreg_batch` (the stacking trainer launches the
     meta model this way before it reads the SVC's results back).  ``prep``: the label-only inputs
-    from :func:`logreg_label_prep` (no masks; single process)."""
+    from :func:`logreg_label_prep` (no masks; single process).  ``preset`` (with ``prep``): the
+    models' ``set_fitted`` runs here, behind the enqueued solve, so :func:`finish_logreg_batch`
+    is left with the error word / guards read only (the stacking fit's last host step)."""
     m0 = models[0]
     if prep is not None and masks is None and group is None and X.is_cuda and FUSED and X.dim() == 2 \
             and int(X.shape[0]) == prep["n"] and X.shape[1] + prep["extra"] <= 64 and m0.penalty in ("l1", "l2") \
@@ -338,8 +353,12 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
             penal[-1:].zero_()
         scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
         LAST_PATH["path"] = "fused"
-        return dict(models=models, F=int(X.shape[1]), scale=scale, fit_intercept=bool(m0.fit_intercept), dev=X.device,
-                    fused=_launch_fused(Xa, prep["s"], prep["ypm"], penal, float(m0.C), l1, max_outer, flags))
+        h = dict(models=models, F=int(X.shape[1]), scale=scale, fit_intercept=bool(m0.fit_intercept), dev=X.device,
+                 fused=_launch_fused(Xa, prep["s"], prep["ypm"], penal, float(m0.C), l1, max_outer, flags))
+        if preset:
+            _set_models(h)
+            h["preset"] = True
+        return h
     _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
     if m0.penalty not in ("l1", "l2"):
         raise NotImplementedError("penalty must be 'l1' or 'l2'")

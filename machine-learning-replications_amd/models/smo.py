@@ -29,7 +29,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from ..utils.hostread import landed   # early read-backs polled on their data
+from ..utils.hostread import landed, stage   # early read-backs polled on their data
 
 TAU = 1e-12
 INT_MAX = np.iinfo(np.int32).max
@@ -1473,11 +1473,7 @@ def _solve_device(probs: List[_Prob], Zs, device, eps, max_iter_cap=None, group=
                      + [rho.index_select(0, kidx).to(f64).reshape(-1), iters.index_select(0, kidx).to(f64).reshape(-1)]
                      + ([err.to(f64).reshape(-1).abs().max().reshape(1)] if err is not None else []))
             early_dev = torch.cat(parts)
-            early_host = torch.empty(early_dev.shape, dtype=f64, pin_memory=True)
-            early_host.fill_(float("nan"))     # (finite once landed: polled by finish_svc_batch)
-            early_host.copy_(early_dev, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+            early_host, ev = stage(early_dev)     # (finite once landed: polled by finish_svc_batch)
         out["_early"] = dict(host=early_host, ev=ev, ids=[id(live[k]) for k in ks], has_err=err is not None,
                              keep=early_dev)
     # y·α of every problem in f32 (the decision kernels' coefficients), kept with the problems' rows
@@ -1612,11 +1608,7 @@ class _GammaDev:
         ops.ext().svm_gamma(Zc.data_ptr(), self.offs.data_ptr(), K, F, self.gam.data_ptr(), self.ngl.data_ptr(),
                             ops.stream_ptr(device))
         # read back right behind its kernel (pinned + event): resolve() waits for γ, not for the SMO
-        self.host = torch.empty(K, dtype=torch.float64, pin_memory=True)
-        self.host.fill_(float("nan"))     # (polled by resolve: see landed)
-        self.host.copy_(self.gam, non_blocking=True)
-        self.ev = torch.cuda.Event()
-        self.ev.record()
+        self.host, self.ev = stage(self.gam)     # (polled by resolve: see landed)
         self.keep = [Zc]
 
     def patch(self, ddev: torch.Tensor, dtype: np.dtype, field: str, fits) -> None:
@@ -1815,11 +1807,7 @@ def launch_svc_batch(svcs, Zs: List[torch.Tensor], ys: List[torch.Tensor], max_i
         dmark("svc_platt")
         # the pairs' read-back queued right behind the Platt kernel (pinned, with an event): the host
         # waits for the Platt fits only, not for whatever is enqueued on this stream after them
-        ab_host = torch.empty(ABt.shape, dtype=torch.float64, pin_memory=True)
-        ab_host.fill_(float("nan"))
-        ab_host.copy_(ABt, non_blocking=True)
-        ab_ev = torch.cuda.Event()
-        ab_ev.record()
+        ab_host, ab_ev = stage(ABt)
         return dict(svcs=svcs, Zs=Zs, meta=meta, all_probs=all_probs, sol=sol, pl=pl, AB=AB, ABt=ABt,
                     ab_host=(ab_host, ab_ev),
                     keep=(pdev, srcmap, cdev, dscr, cbar, cpart), device=device, args=args, solver=solver, gamma_dev=gdev)
@@ -1911,6 +1899,9 @@ def enqueue_svc_oof(st: dict, items, meta: torch.Tensor, col: int) -> bool:
 DEC_COMPACT = os.environ.get("HFENS_SVC_DEC_COMPACT", "1") != "0"
 # the Platt sigmoid fits with each fit's points over 8 workgroups (svm.hip platt_coop_kernel)
 PLATT_COOP = os.environ.get("HFENS_PLATT_COOP", "1") != "0"
+# finish_svc_batch: the final models' set_fitted before the Platt pairs are read back (their
+# bookkeeping overlaps the decision / Platt kernels; SVC.set_platt installs the pair after)
+SET_BEFORE_PLATT = os.environ.get("HFENS_SVC_SET_BEFORE_PLATT", "1") != "0"
 
 
 def _sv_compact(E, zcat, coef, F, ddev, P, device, s):
@@ -2036,8 +2027,8 @@ def finish_svc_batch(st: dict, defer=None):
                     class_weight=torch.tensor([mt["C0"] / svc.C, mt["C1"] / svc.C]),
                     shape_fit=tuple(Z.shape), n_features=Z.shape[1], device=device)
 
-    def set_one(f, kw):
-        A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
+    def set_one(f, kw, platt=True):
+        A, B = AB[f] if platt and AB[f] is not None else (0.0, 0.0)
         svcs[f].set_fitted(probA=A, probB=B, **kw)
         svcs[f].n_iter_ = int(host[nl + len(svcs) + f])
 
@@ -2062,10 +2053,23 @@ def finish_svc_batch(st: dict, defer=None):
     later = [f for f in range(len(svcs)) if defer is not None and f in defer]
     now = [f for f in range(len(svcs)) if f not in later]
     kws = {f: prep_one(f) for f in now}     # (with the early read: while the Platt kernels run)
+    pre = SET_BEFORE_PLATT and early is not None and st.get("ab_host") is not None and st["ABt"] is not None
+    if pre:
+        # set_fitted too while the Platt kernels run; the pair (device: the kernel's own output)
+        # goes in after its read-back
+        for f in now:
+            set_one(f, kws[f], platt=False)
     read_ab()
     hmark("svc_platt_read")
-    for f in now:
-        set_one(f, kws[f])
+    if pre:
+        slot = {f: k for k, f in enumerate(st["pl"])}
+        for f in now:
+            A, B = AB[f] if AB[f] is not None else (0.0, 0.0)
+            k = slot.get(f)
+            svcs[f].set_platt(A, B, st["ABt"][2 * k:2 * k + 2] if k is not None else None)
+    else:
+        for f in now:
+            set_one(f, kws[f])
     hmark("svc_set_fitted")
     if later:
         pending = list(later)

@@ -58,6 +58,11 @@ SKIP_FOLD_SVC = os.environ.get("HFENS_SKIP_FOLD_SVC", "1") != "0"
 DEVICE_BASES = os.environ.get("HFENS_DEVICE_BASES", "1") != "0"
 # the meta model's launch enqueued before the SVC's results are read back (0: after them)
 EARLY_META = os.environ.get("HFENS_EARLY_META", "1") != "0"
+# ... with its set_fitted done at that launch (the fit's tail then only reads its error word / guards)
+META_PRESET = os.environ.get("HFENS_META_PRESET", "1") != "0"
+# the GBC / L1-LR guards resolved BEFORE the SVC's read-back when their staged copy has already
+# landed (they finish milliseconds before the SMO): off the tail's host path
+BASES_EARLY_RESOLVE = os.environ.get("HFENS_BASES_EARLY_RESOLVE", "1") != "0"
 
 
 def _kind(est):
@@ -458,6 +463,14 @@ def _finish_concurrent(stc):
     if group is not None:
         from ..parallel.stack import finish_svc_batch_distributed
     with stc["timer"].stage("fit_bases(svc || gbc+lr)"):
+        resolved = False
+        if dev_bases is not None and BASES_EARLY_RESOLVE and dev_bases["deferred"].ready():
+            # (their kernels have finished: the read is a look at host memory.  A fallback hook
+            # re-solves on the caller's stream, after the bases' own)
+            main.wait_stream(other)
+            dev_bases["deferred"].resolve()
+            resolved = True
+            hmark("bases_resolved_early")
         # (the refit SVC's bookkeeping stays on the SVC stream: on the caller's stream its wait
         # for the SMO, pending at the head of an idle queue, slowed the SMO itself — 22.7 vs 19.3
         # ms / fit; on a new stream the stream → hardware-queue mapping moved and the GBC / LR
@@ -479,7 +492,7 @@ def _finish_concurrent(stc):
         hmark("svc_finished")
         main.wait_stream(side)
         main.wait_stream(other)
-        if dev_bases is not None:
+        if dev_bases is not None and not resolved:
             # the GBC / LR guards and error words: ONE read, long after their kernels finished
             dev_bases["deferred"].resolve()
             hmark("bases_resolved")
@@ -644,7 +657,7 @@ def launch_stacking(clf, X: torch.Tensor, y: torch.Tensor, timer: StageTimer = N
             # out-of-fold columns only the features' guard and the intercept column remain
             from .logreg_solver import logreg_label_prep
             lprep = logreg_label_prep(fm, y64, n, dev) if X.is_cuda else None
-            early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep)}
+            early = {"launch": lambda: launch_logreg_batch(fm, meta, y64, prep=lprep, preset=META_PRESET)}
         dev_bases = None
         if group is None and X.is_cuda and DEVICE_BASES:
             dev_bases = _device_bases(clf, X, y, masks, folds_np, meta, plan, early, oof)

@@ -143,3 +143,19 @@ class SVC(Estimator):
         self._sparse = False
         self._packed = None
         return self
+
+    def set_platt(self, probA: float, probB: float, dev_pair=None):
+        """Install the Platt pair after a :meth:`set_fitted` that ran before the pair was read back
+        (the stacking fit's tail: the model's bookkeeping overlaps the Platt kernels).  ``dev_pair``:
+        the pair's float64 device copy [A, B] (the Platt kernel's output), used without a copy."""
+        self._hs = (self._hs[0], float(probA), float(probB))
+        if dev_pair is not None:
+            self._probA = dev_pair[0:1]
+            self._probB = dev_pair[1:2]
+        elif float(probA) != 0.0 or float(probB) != 0.0:
+            pair = torch.tensor([float(probA), float(probB)], dtype=torch.float64)
+            dev = self._intercept_.device
+            if dev.type == "cuda":
+                pair = pair.pin_memory().to(dev, non_blocking=True)
+            self._probA, self._probB = pair[0:1], pair[1:2]
+        return self

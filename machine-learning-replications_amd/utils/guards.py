@@ -85,6 +85,16 @@ class Deferred:
     def __len__(self) -> int:
         return len(self._flags) + len(self._words)
 
+    def ready(self) -> bool:
+        """True when :meth:`resolve` would not wait: nothing to read, or the staged copy has landed."""
+        if not len(self):
+            return True
+        st = self._staged
+        if st is None or st[2] != len(self._words) or st[3] != len(self._flags):
+            return False
+        from .hostread import _pending
+        return not _pending(st[0].numpy())
+
     def resolve(self) -> None:
         if not len(self):
             return

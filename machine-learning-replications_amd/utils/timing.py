@@ -124,7 +124,7 @@ def hmarks_flush(prefix: str = "[host]") -> None:
         import sys
         prefix = _rank_prefix(prefix)
         t0 = _MARKS[0][1]
-        print(prefix + " " + " ".join(f"{k}={1e3 * (v - t0):.1f}" for k, v in _MARKS), file=sys.stderr)
+        print(prefix + " " + " ".join(f"{k}={1e3 * (v - t0):.2f}" for k, v in _MARKS), file=sys.stderr)
         _MARKS.clear()
 
 

@@ -4,5 +4,5 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 O=gpurun_out/r6bj
 mkdir -p $O
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 3 > $O/bench.json 2> $O/prof.err || { echo "prof failed"; tail -20 $O/prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 3 > $O/bench.json 2> $O/prof.err || { echo "prof failed"; tail -20 $O/prof.err; exit 1; }
 ls $O/prof

@@ -23,6 +23,11 @@ if all("svc_platt_dec" in d and "svc_smo_done" in d for d in dev):
     print(f"tail medians: dec {median(d['svc_platt_dec'] - d['svc_smo_done'] for d in dev):.3f} "
           f"platt {median(d['svc_platt'] - d['svc_platt_in'] for d in dev):.3f} "
           f"smo→stack_fit {median(d['stack_fit'] - d['svc_smo_done'] for d in dev):.3f}")
+if all(k in d for d in dev for k in ("svc_oof", "lr_launch", "lr_kernel", "meta", "stack_fit")):
+    print(f"meta medians: oof→lr_kernel {median(d['lr_kernel'] - d['svc_oof'] for d in dev):.3f} "
+          f"lr_launch→lr_kernel {median(d['lr_kernel'] - d['lr_launch'] for d in dev):.3f} "
+          f"lr_kernel→meta {median(d['meta'] - d['lr_kernel'] for d in dev):.3f} "
+          f"meta→stack_fit {median(d['stack_fit'] - d['meta'] for d in dev):.3f}")
 hk = ["develop", "lasso_spec_launched", "svc_cascade_seeded", "ws_groups_ready", "svc_solve_enqueued", "lasso_best_read", "svc_host_read"]
 print("host medians (ms after develop): " + " ".join(
     f"{k}={median(h[k] - h['develop'] for h in host if k in h and 'develop' in h):.2f}" for k in hk[1:] if any(k in h for h in host)))

@@ -86,6 +86,30 @@ def test_logreg_fused_matches_device_loop(dev, monkeypatch, pen):
         assert torch.allclose(a.intercept_, b.intercept_, atol=1e-7)
 
 
+@pytest.mark.parametrize("refit", [False, True])
+def test_logreg_preset_matches_finish(dev, refit):
+    """launch_logreg_batch(prep=..., preset=True) (the stacking fit's meta model: set_fitted at
+    launch, behind the enqueued solve) leaves the same fitted models as set_fitted at finish; after a
+    cooperative-exchange fallback (simulated: ``refit``) the models are set again from the re-solve."""
+    from hfens.models import logreg_solver
+    X, y = _data(4000, 3, 29)
+    Xd, yd = X.to(dev).to(torch.float64), y.to(dev).to(torch.float64)
+    out = []
+    for preset in (False, True):
+        ms = [LogisticRegression()]
+        prep = logreg_solver.logreg_label_prep(ms, yd, Xd.shape[0], Xd.device)
+        h = logreg_solver.launch_logreg_batch(ms, Xd, yd, prep=prep, preset=preset)
+        assert h.get("preset", False) == preset
+        if refit and preset:
+            ms[0].intercept_.fill_(123.0)      # (what a stale launch-time copy would leave)
+            h["fused"]["refit"] = True
+        logreg_solver.finish_logreg_batch(h)
+        out.append(ms[0])
+    assert torch.equal(out[0].coef_, out[1].coef_)
+    assert torch.equal(out[0].intercept_, out[1].intercept_)
+    assert torch.equal(out[0].n_iter_, out[1].n_iter_)
+
+
 @pytest.mark.parametrize("pen,n,members", [("l1", 8000, 5), ("l2", 10007, 16), ("l1", 300, 3), ("l2", 2000, 1)])
 def test_logreg_coop_matches_single_workgroup(dev, monkeypatch, pen, n, members):
     """logreg_coop (members exchange ordered partial sums of H, g and the line-search losses) takes
