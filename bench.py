@@ -138,6 +138,7 @@ def main():
     # the timed region nothing); the per-stage table below is the median over the timed steps
     timers = [StageTimer(enabled=True, events=True) for _ in range(a.steps)]
     threads0 = _thread_cpu()
+    sampler = _SyscallSampler() if os.environ.get("HFENS_THREAD_SAMPLE") == "1" else None
     cpu0 = time.process_time()
     t0 = time.perf_counter()
     step_ends = []
@@ -148,6 +149,8 @@ def main():
     elapsed = time.perf_counter() - t0
     cpu = time.process_time() - cpu0
     threads1 = _thread_cpu()
+    if sampler is not None:
+        print("[thread-sample] " + sampler.stop(), file=sys.stderr)
     if group is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
@@ -241,6 +244,50 @@ def run_facts(dev, steps, elapsed, cpu, host_med, step_ends, t0):
     return facts
 
 
+class _SyscallSampler:
+    """HFENS_THREAD_SAMPLE=1: samples /proc/self/task/*/syscall every ≈ 0.5 ms over the timed steps
+    and reports, per thread, how often it was in user space ("running") or in which system call
+    (x86-64 numbers: 16 ioctl, 7 poll, 202 futex, 23 select, 35 nanosleep) — what the busy
+    runtime thread of the headline's host profile is doing."""
+
+    def __init__(self):
+        import threading
+        self._stop = threading.Event()
+        self.counts = {}
+        self._me = None
+        self._th = threading.Thread(target=self._run, name="hfens-sampler", daemon=True)
+        self._th.start()
+
+    def _run(self):
+        self._me = str(threading_native_id())
+        while not self._stop.is_set():
+            for tid in os.listdir("/proc/self/task"):
+                if tid == self._me:
+                    continue
+                try:
+                    with open(f"/proc/self/task/{tid}/syscall") as f:
+                        w = f.read().split()
+                except OSError:
+                    continue
+                key = w[0] if w else "?"
+                d = self.counts.setdefault(tid, {})
+                d[key] = d.get(key, 0) + 1
+            time.sleep(0.0005)
+
+    def stop(self) -> str:
+        self._stop.set()
+        self._th.join()
+        tot = {t: sum(d.values()) for t, d in self.counts.items()}
+        busy = sorted(self.counts, key=lambda t: -(tot[t] - self.counts[t].get("202", 0)))[:4]
+        return " | ".join(f"tid {t}: " + ", ".join(f"{k}={v}" for k, v in sorted(self.counts[t].items(), key=lambda x: -x[1])[:4])
+                          for t in busy)
+
+
+def threading_native_id():
+    import threading
+    return threading.get_native_id()
+
+
 def _thread_cpu():
     """{(tid, name): CPU seconds} of this process's threads (Linux /proc), {} elsewhere."""
     out = {}
@@ -254,6 +301,7 @@ def _thread_cpu():
                 with open(f"/proc/self/task/{tid}/comm") as f:
                     name = f.read().strip()
                 out[(tid, name)] = (int(fields[11]) + int(fields[12])) / tick
+                out[(tid, name + ":sys")] = int(fields[12]) / tick
             except OSError:
                 continue
     except OSError:
@@ -263,12 +311,15 @@ def _thread_cpu():
 
 def _thread_delta(a, b, top=5):
     """CPU seconds per thread name over the timed steps, the busiest few (explains host load)."""
+    import threading
     main = str(os.getpid())
+    py = {str(t.native_id): t.name for t in threading.enumerate() if t.native_id is not None}
     agg = {}
     for k, v in b.items():
         d = v - a.get(k, 0.0)
         if d > 0:
-            agg[f"{k[1]}{'(main)' if k[0] == main else ''}#{k[0]}"] = d
+            tag = "(main)" if k[0] == main else (f"({py[k[0]]})" if k[0] in py else "(native)")
+            agg[f"{k[1]}{tag}#{k[0]}"] = d
     return {k: round(v, 3) for k, v in sorted(agg.items(), key=lambda x: -x[1])[:top]}
 
 
