@@ -136,7 +136,10 @@ def main():
     barrier()
     # every timed step carries an event-based stage timer (no host synchronisation: it costs
     # the timed region nothing); the per-stage table below is the median over the timed steps
-    timers = [StageTimer(enabled=True, events=True) for _ in range(a.steps)]
+    # (HFENS_BENCH_STAGE_EVENTS=0: no timing events in the timed steps — the per-stage table is then
+    # empty; an A/B of the events' own cost, profiles/r6_runs/r6bt)
+    stage_events = os.environ.get("HFENS_BENCH_STAGE_EVENTS", "1") != "0"
+    timers = [StageTimer(enabled=stage_events, events=True) for _ in range(a.steps)]
     threads0 = _thread_cpu()
     sampler = _SyscallSampler() if os.environ.get("HFENS_THREAD_SAMPLE") == "1" else None
     cpu0 = time.process_time()

@@ -119,8 +119,8 @@ def lr_members(B: int, n: int, ncu: int) -> int:
 def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=None) -> dict:
     """All B solves in one launch, enqueued with no host synchronisation; :func:`_finish_fused`
     returns (W [B, F1], n_iter [B] int32).  ``flags``: the input guards as device bools (finite X,
-    binary y), read with the cooperative launch's error word in one transfer (a failed guard
-    raises after the launch)."""
+    binary y) — or a callable producing them, called right after the launch — read with the
+    cooperative launch's error word in one transfer (a failed guard raises after the launch)."""
     E = ops.ext()
     B, n = s.shape
     F1 = Xa.shape[1]
@@ -148,6 +148,9 @@ def _launch_fused(Xa, s, ypm, penal, C: float, l1: bool, max_outer: int, flags=N
         h.update(err=err, xchg=xchg)
     else:
         _launch_single(h)
+    if callable(flags):
+        # (the guards computed behind the solve: nothing but the read-back consumes them)
+        flags = h["flags"] = flags()
     # the error word and guards' read-back queued right behind the solve (pinned + event):
     # _finish_fused then waits for this solve only
     parts = ([h["err"]] if h["err"] is not None else []) + ([flags.to(torch.int32)] if flags is not None else [])
@@ -301,6 +304,21 @@ def _set_models(h: dict) -> None:
         m.set_fitted(W[b, :F], intercept.reshape(1), iters[b:b + 1], F, device=dev)
 
 
+_PENAL: dict = {}
+
+
+def _penal_mask(F1: int, l1: bool, fit_intercept: bool, device) -> torch.Tensor:
+    """The penalty mask (1 = penalised; the lbfgs-path intercept is not), one per shape and device:
+    the kernels only read it, so a fit's critical path carries no fills for it."""
+    key = (F1, l1, fit_intercept, str(device))
+    t = _PENAL.get(key)
+    if t is None:
+        # (a blocking host → device copy, once: complete before any stream can read it)
+        t = torch.tensor([1] * (F1 - 1) + [0 if (not l1 and fit_intercept) else 1], dtype=torch.uint8).to(device)
+        _PENAL[key] = t
+    return t
+
+
 def logreg_label_prep(models, y: torch.Tensor, n: int, device) -> dict:
     """The label-only inputs of a single-process fused :func:`launch_logreg_batch` (the labels'
     guard, ±1 labels, sample weights, penalty mask, intercept column), enqueued on the CURRENT
@@ -344,13 +362,11 @@ def launch_logreg_batch(models, X: torch.Tensor, y: torch.Tensor, masks: Optiona
         from ..utils import guards
         _check_same(models, ("penalty", "C", "fit_intercept", "intercept_scaling", "class_weight", "solver"))
         X = X.to(torch.float64)
-        flags = torch.stack([guards.finite_flag(X), prep["yflag"]])
+        flags = lambda: torch.stack([guards.finite_flag(X), prep["yflag"]])   # noqa: E731 (after the launch)
         Xa = torch.cat([X, prep["ones"]], 1) if prep["ones"] is not None else X
         F1 = Xa.shape[1]
         l1 = m0.penalty == "l1"
-        penal = torch.ones(F1, dtype=torch.uint8, device=X.device)
-        if not l1 and m0.fit_intercept:
-            penal[-1:].zero_()
+        penal = _penal_mask(F1, l1, bool(m0.fit_intercept), X.device)
         scale = float(m0.intercept_scaling) if (m0.fit_intercept and l1) else 1.0
         LAST_PATH["path"] = "fused"
         h = dict(models=models, F=int(X.shape[1]), scale=scale, fit_intercept=bool(m0.fit_intercept), dev=X.device,
