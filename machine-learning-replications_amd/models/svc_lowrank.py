@@ -56,8 +56,22 @@ RD_LOOSE = 1e-5
 N_CORRECTORS = int(os.environ.get("HFENS_IPM_CORRECTORS", "2"))
 
 
+# the RBF matrices of the Nyström map from ops/csrc/nystrom.hip (one pass writing K once, distances
+# summed from the differences) instead of the library's GEMM form (seven HBM passes over l × m)
+NATIVE_RBF = os.environ.get("HFENS_NATIVE_RBF", "1") != "0"
+
+
 def _rbf(A: torch.Tensor, B: torch.Tensor, gamma: float) -> torch.Tensor:
-    """exp(−γ‖a − b‖²) for all row pairs, f64 (GEMM form, clamped at 0)."""
+    """exp(−γ‖a − b‖²) for all row pairs, f64 (native: the differences' squares; otherwise the GEMM
+    form, clamped at 0)."""
+    if (NATIVE_RBF and A.is_cuda and A.dtype == torch.float64 and B.dtype == torch.float64
+            and A.dim() == 2 and B.dim() == 2 and A.shape[1] == B.shape[1] and 1 <= A.shape[1] <= 32
+            and B.shape[0] >= 1 and ops.has_ext()):
+        Ac, Bc = A.contiguous(), B.contiguous()
+        out = torch.empty(Ac.shape[0], Bc.shape[0], dtype=torch.float64, device=A.device)
+        ops.ext().rbf_f64(Ac.data_ptr(), int(Ac.shape[0]), Bc.data_ptr(), int(Bc.shape[0]), int(Ac.shape[1]),
+                          float(gamma), out.data_ptr(), ops.stream_ptr(A.device))
+        return out
     d2 = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
     return torch.exp(-gamma * d2.clamp_(min=0.0))
 
