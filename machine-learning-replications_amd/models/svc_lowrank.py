@@ -54,6 +54,11 @@ IPM_MAX_ITER = 80
 IPM_TOL = 1e-8
 RD_LOOSE = 1e-5
 N_CORRECTORS = int(os.environ.get("HFENS_IPM_CORRECTORS", "2"))
+# priority of the interior-point solves' streams (created after the fit's stream set,
+# runtime.FIT_STREAMS: the priority picks the hardware-queue set they are spread over).  At normal
+# priority, behind round 6's stream set, config 3 took 17.41–17.50 s per fit with unchanged solve
+# times; at -1 15.67 s (profiles/r6_runs/r6bx, r6by, r6bz)
+IPM_STREAM_PRIORITY = int(os.environ.get("HFENS_IPM_STREAM_PRIORITY", "-1"))
 
 
 # the RBF matrices of the Nyström map from ops/csrc/nystrom.hip (one pass writing K once, distances
@@ -870,7 +875,7 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
             def worker(t):
                 _TL.tag = f"#s{slot}t{t}"
                 with torch.cuda.device(dev):
-                    st = runtime.stream(dev, f"ipm{slot}_{t}")
+                    st = runtime.stream(dev, f"ipm{slot}_{t}", priority=IPM_STREAM_PRIORITY)
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
                         return [(j, solve_cv(p, sgs[t])) for j, p in enumerate(cv) if j % nthr == t]
@@ -880,7 +885,7 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
                 # own thread and stream beside them, submitted first
                 _TL.tag = f"#s{slot}final"
                 with torch.cuda.device(dev):
-                    st = runtime.stream(dev, f"ipm_final{slot}")
+                    st = runtime.stream(dev, f"ipm_final{slot}", priority=IPM_STREAM_PRIORITY)
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
                         rho_f, it_f, beta_f = solve_final(sgs[nthr])
@@ -959,7 +964,7 @@ def fit_svc_lowrank_batch(svcs, Zs, ys, n_landmarks: int = None, group=None):
             slot = slots.get()
             try:
                 with torch.cuda.device(dev):
-                    fs = runtime.stream(dev, f"ipm_fit{slot}")
+                    fs = runtime.stream(dev, f"ipm_fit{slot}", priority=IPM_STREAM_PRIORITY)
                     fs.wait_stream(caller)
                     with torch.cuda.stream(fs):
                         fit_one(f, svcs[f], Zs[f], ys[f], slot)
