@@ -135,7 +135,7 @@ F32_PHI = os.environ.get("HFENS_IPM_F32PHI", "1") != "0"
 IPM_A0 = float(os.environ.get("HFENS_IPM_A0", "0.5"))     # starting α = A0·c
 BATCH_IPM = os.environ.get("HFENS_IPM_BATCH", "1") != "0"      # one-thread group path: lock-step solves
 IPM_THREADS = int(os.environ.get("HFENS_IPM_THREADS", "5"))   # concurrent Platt-CV solves per fit (+ the final): 5 measured 16.6 vs 17.2 s at 3 (config 3)
-FIT_THREADS = int(os.environ.get("HFENS_IPM_FITS", "1"))      # fits solved at a time (2: no gain measured, GPU saturated)
+FIT_THREADS = int(os.environ.get("HFENS_IPM_FITS", "3"))      # fits solved at a time: config 3 14.69 s at 3 vs 15.70 at 1, 14.89 at 2, 14.62 at 6 (profiles/r6_runs/r6cc, r6cd; round 4 saw no gain at 2 under the old stream layout)
 IPM_NU0 = float(os.environ.get("HFENS_IPM_NU0", "1.0"))   # starting bound multipliers ν = μ
 CHOL_MW = os.environ.get("HFENS_CHOL_MW", "1") != "0"      # multi-workgroup r × r Cholesky (r ≤ 512)
 
